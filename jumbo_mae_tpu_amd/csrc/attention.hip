@@ -1,0 +1,454 @@
+// Fused short-sequence multi-head attention, forward + backward, for gfx950 MFMA.
+//
+// Shapes of this workload: encoder S=52 (3 CLS + 49 kept patches), hd=64;
+// MAE decoder S=199, hd=32; finetune S=199, hd=64.  The whole sequence of one (batch, head)
+// fits in LDS, so one 256-thread workgroup (4 waves) owns one (b, h): no online softmax, no
+// S x S matrix in HBM, one pass over q/k/v.
+//
+// MFMA: v_mfma_f32_16x16x32_bf16 (fp32 accumulate).  Orientation ("key on the lane"):
+//   forward   S^T = K Q^T  -> the C tile holds one query per lane column and 4 keys per lane
+//             group, so the softmax column reduction is in-register + 2 cross-lane shuffles and
+//             P^T is *already* the B operand of O^T = V^T P^T (k-permuted; V^T is read with the
+//             same permutation) -- no LDS round trip for P.
+//   backward  S = Q K^T and dP = dO V^T with the key on the lane; their C tiles are directly the
+//             B operands of dV^T += dO^T P and dK^T += Q^T dS.  dS crosses LDS once (per 64-query
+//             chunk) for dQ^T = K^T dS^T.  Each wave keeps dK^T/dV^T of its key tiles in
+//             registers across the whole query sweep: no atomics, deterministic.
+//
+// Sequence is padded to SP (multiple of 32) inside LDS; padded keys get P = 0, padded queries
+// get lse = +inf (P = 0) and zero dO, so they contribute nothing.
+//
+// Memory layout: qkv [B, S, 3, H, hd] (output of the fused QKV GEMM, read in place),
+// o / do [B, S, H, hd], lse [B, H, S] (natural log), dqkv [B, S, 3, H, hd].
+#include "common.h"
+
+namespace {
+
+constexpr float LOG2E = 1.4426950408889634f;
+constexpr float LN2 = 0.6931471805599453f;
+
+JM_DEVICE bf16x8_t pack8(const float* f) {
+  s16x8_t s;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) s[j] = (short)f2bf(f[j]);
+  return __builtin_bit_cast(bf16x8_t, s);
+}
+
+JM_DEVICE bf16x8_t cat44(s16x4_t lo, s16x4_t hi) {
+  s16x8_t s;
+  s[0] = lo[0]; s[1] = lo[1]; s[2] = lo[2]; s[3] = lo[3];
+  s[4] = hi[0]; s[5] = hi[1]; s[6] = hi[2]; s[7] = hi[3];
+  return __builtin_bit_cast(bf16x8_t, s);
+}
+
+JM_DEVICE bf16x8_t ld8(const uint16_t* p) { return *reinterpret_cast<const bf16x8_t*>(p); }
+JM_DEVICE s16x4_t ld4(const uint16_t* p) { return *reinterpret_cast<const s16x4_t*>(p); }
+
+// ds_read_b64_tr_b16 (gfx950): per 16-lane group, lane 4q+p supplies the address of row q,
+// columns 4p..4p+3 of a 4 x 16 block of 16-bit elements; lane i receives column i of the 4 rows.
+// Lets row-major LDS images serve as transposed MFMA operands (no second, transposed copy).
+JM_DEVICE s16x4_t tr4(const uint16_t* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4_t*)(p));
+}
+
+JM_DEVICE f32x4_t mfma(bf16x8_t a, bf16x8_t b, f32x4_t c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+// --------------------------------------------------------------------------------- forward
+template <int HD, int SP, bool TR>
+__global__ __launch_bounds__(256) void attn_fwd_kernel(const uint16_t* __restrict__ qkv, uint16_t* __restrict__ o,
+                                                       float* __restrict__ lse, int S, int H, float scale) {
+  constexpr int KS = HD + 8;  // K row stride (elements), 16-B aligned, breaks bank aliasing
+  constexpr int VS = SP + 8;  // V^T row stride
+  constexpr int NT = SP / 16;
+  constexpr int KK = HD / 32;
+  constexpr int DT = HD / 16;
+  extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
+  uint16_t* Ks = smem;
+  uint16_t* Vt = smem + SP * KS;  // TR: row-major V [SP][KS]; else V^T [HD][VS]
+
+  const int bh = blockIdx.x;
+  const int b = bh / H, h = bh - (bh / H) * H;
+  const long ts = 3L * H * HD;  // token stride in qkv
+  const uint16_t* base = qkv + (long)b * S * ts;
+  const uint16_t* Qg = base + h * HD;
+  const uint16_t* Kg = base + (H + h) * HD;
+  const uint16_t* Vg = base + (2 * H + h) * HD;
+
+  constexpr int CPR = HD / 8;
+  for (int i = threadIdx.x; i < SP * CPR; i += 256) {
+    const int r = i / CPR, c = (i % CPR) * 8;
+    uint4 kv = make_uint4(0, 0, 0, 0), vv = make_uint4(0, 0, 0, 0);
+    if (r < S) {
+      kv = *reinterpret_cast<const uint4*>(Kg + r * ts + c);
+      vv = *reinterpret_cast<const uint4*>(Vg + r * ts + c);
+    }
+    *reinterpret_cast<uint4*>(Ks + r * KS + c) = kv;
+    if (TR) {
+      *reinterpret_cast<uint4*>(Vt + r * KS + c) = vv;
+    } else {
+      const uint16_t* vh = reinterpret_cast<const uint16_t*>(&vv);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) Vt[(c + j) * VS + r] = vh[j];
+    }
+  }
+  __syncthreads();
+
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int l16 = lane & 15, g = lane >> 4;
+  const float sl2 = scale * LOG2E;
+
+  for (int qt = wave; qt < NT; qt += 4) {
+    const int q = qt * 16 + l16;
+    bf16x8_t qf[KK];
+#pragma unroll
+    for (int kk = 0; kk < KK; ++kk) {
+      if (q < S) {
+        qf[kk] = ld8(Qg + (long)q * ts + 32 * kk + 8 * g);
+      } else {
+        s16x8_t z = {0, 0, 0, 0, 0, 0, 0, 0};
+        qf[kk] = __builtin_bit_cast(bf16x8_t, z);
+      }
+    }
+    f32x4_t sc[NT];
+#pragma unroll
+    for (int kt = 0; kt < NT; ++kt) {
+      f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kk = 0; kk < KK; ++kk) acc = mfma(ld8(Ks + (kt * 16 + l16) * KS + 32 * kk + 8 * g), qf[kk], acc);
+      sc[kt] = acc;
+    }
+    // sc[kt][i] = S^T[key = kt*16 + 4g + i][query = qt*16 + l16]
+    float m = -INFINITY;
+#pragma unroll
+    for (int kt = 0; kt < NT; ++kt) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int key = kt * 16 + 4 * g + i;
+        const float v = key < S ? sc[kt][i] * sl2 : -INFINITY;
+        sc[kt][i] = v;
+        m = fmaxf(m, v);
+      }
+    }
+    m = fmaxf(m, __shfl_xor(m, 16, WAVE));
+    m = fmaxf(m, __shfl_xor(m, 32, WAVE));
+    float l = 0.f;
+#pragma unroll
+    for (int kt = 0; kt < NT; ++kt) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float p = exp2f(sc[kt][i] - m);
+        sc[kt][i] = p;
+        l += p;
+      }
+    }
+    l += __shfl_xor(l, 16, WAVE);
+    l += __shfl_xor(l, 32, WAVE);
+
+    f32x4_t oacc[DT];
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) oacc[dt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < NT / 2; ++s) {
+      float pf[8] = {sc[2 * s][0], sc[2 * s][1], sc[2 * s][2], sc[2 * s][3],
+                     sc[2 * s + 1][0], sc[2 * s + 1][1], sc[2 * s + 1][2], sc[2 * s + 1][3]};
+      const bf16x8_t pb = pack8(pf);
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt) {
+        bf16x8_t va;
+        if (TR) {
+          const uint16_t* vr = Vt + (32 * s + 4 * g + (l16 >> 2)) * KS + dt * 16 + 4 * (l16 & 3);
+          va = cat44(tr4(vr), tr4(vr + 16 * KS));
+        } else {
+          const uint16_t* vr = Vt + (dt * 16 + l16) * VS + 32 * s + 4 * g;
+          va = cat44(ld4(vr), ld4(vr + 16));
+        }
+        oacc[dt] = mfma(va, pb, oacc[dt]);
+      }
+    }
+    // oacc[dt][i] = O^T[d = dt*16 + 4g + i][query]
+    if (q < S) {
+      const float inv = 1.f / l;
+      uint16_t* orow = o + ((long)b * S + q) * H * HD + h * HD;
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt) {
+        float v[4] = {oacc[dt][0] * inv, oacc[dt][1] * inv, oacc[dt][2] * inv, oacc[dt][3] * inv};
+        store4(orow + dt * 16 + 4 * g, v);
+      }
+      if (g == 0) lse[((long)b * H + h) * S + q] = (m + log2f(l)) * LN2;
+    }
+  }
+}
+
+// -------------------------------------------------------------------------------- backward
+template <int HD, int SP, bool TR>
+__global__ __launch_bounds__(256) void attn_bwd_kernel(const uint16_t* __restrict__ qkv,
+                                                       const uint16_t* __restrict__ o,
+                                                       const uint16_t* __restrict__ dO,
+                                                       const float* __restrict__ lse,
+                                                       uint16_t* __restrict__ dqkv, int S, int H, float scale) {
+  constexpr int RS = HD + 8;  // row-major image stride
+  constexpr int TS = SP + 8;  // transposed image stride
+  constexpr int NT = SP / 16;
+  constexpr int KK = HD / 32;
+  constexpr int DT = HD / 16;
+  constexpr int QC = 64;  // query rows per dS chunk
+  constexpr int NKW = (NT + 3) / 4;  // key tiles per wave
+  extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
+  uint16_t* Qs = smem;
+  uint16_t* Ks = Qs + SP * RS;
+  uint16_t* Vs = Ks + SP * RS;
+  uint16_t* dOs = Vs + SP * RS;
+  // TR: transposed operands come from the row-major images through ds_read_b64_tr_b16
+  uint16_t* Qt = dOs + SP * RS;
+  uint16_t* dOt = Qt + (TR ? 0 : HD * TS);
+  uint16_t* Kt = dOt + (TR ? 0 : HD * TS);
+  uint16_t* dSs = Kt + (TR ? 0 : HD * TS);
+  float* lse_s = reinterpret_cast<float*>(dSs + QC * TS);
+  float* delta_s = lse_s + SP;
+
+  const int bh = blockIdx.x;
+  const int b = bh / H, h = bh - (bh / H) * H;
+  const long ts = 3L * H * HD;
+  const long os = (long)H * HD;
+  const uint16_t* base = qkv + (long)b * S * ts;
+  const uint16_t* Qg = base + h * HD;
+  const uint16_t* Kg = base + (H + h) * HD;
+  const uint16_t* Vg = base + (2 * H + h) * HD;
+  const uint16_t* Og = o + (long)b * S * os + h * HD;
+  const uint16_t* dOg = dO + (long)b * S * os + h * HD;
+  uint16_t* dQg = dqkv + (long)b * S * ts + h * HD;
+  uint16_t* dKg = dqkv + (long)b * S * ts + (H + h) * HD;
+  uint16_t* dVg = dqkv + (long)b * S * ts + (2 * H + h) * HD;
+
+  for (int i = threadIdx.x; i < SP; i += 256) {
+    delta_s[i] = 0.f;
+    lse_s[i] = i < S ? lse[((long)b * H + h) * S + i] * LOG2E : INFINITY;
+  }
+  __syncthreads();
+  constexpr int CPR = HD / 8;
+  for (int i = threadIdx.x; i < SP * CPR; i += 256) {
+    const int r = i / CPR, c = (i % CPR) * 8;
+    uint4 qv = make_uint4(0, 0, 0, 0), kv = qv, vv = qv, dv = qv;
+    float dsum = 0.f;
+    if (r < S) {
+      qv = *reinterpret_cast<const uint4*>(Qg + r * ts + c);
+      kv = *reinterpret_cast<const uint4*>(Kg + r * ts + c);
+      vv = *reinterpret_cast<const uint4*>(Vg + r * ts + c);
+      dv = *reinterpret_cast<const uint4*>(dOg + r * os + c);
+      float of[8], df[8];
+      load8(Og + r * os + c, of);
+      load8(dOg + r * os + c, df);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) dsum += of[j] * df[j];
+    }
+    *reinterpret_cast<uint4*>(Qs + r * RS + c) = qv;
+    *reinterpret_cast<uint4*>(Ks + r * RS + c) = kv;
+    *reinterpret_cast<uint4*>(Vs + r * RS + c) = vv;
+    *reinterpret_cast<uint4*>(dOs + r * RS + c) = dv;
+    if (!TR) {
+      const uint16_t* qh = reinterpret_cast<const uint16_t*>(&qv);
+      const uint16_t* kh = reinterpret_cast<const uint16_t*>(&kv);
+      const uint16_t* dh = reinterpret_cast<const uint16_t*>(&dv);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        Qt[(c + j) * TS + r] = qh[j];
+        Kt[(c + j) * TS + r] = kh[j];
+        dOt[(c + j) * TS + r] = dh[j];
+      }
+    }
+    if (r < S) atomicAdd(&delta_s[r], dsum);
+  }
+  __syncthreads();
+
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int l16 = lane & 15, g = lane >> 4;
+  const float sl2 = scale * LOG2E;
+
+  f32x4_t dvacc[NKW][DT], dkacc[NKW][DT];
+#pragma unroll
+  for (int w = 0; w < NKW; ++w)
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) {
+      dvacc[w][dt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+      dkacc[w][dt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    }
+
+  for (int qc = 0; qc * QC < SP; ++qc) {
+#pragma unroll
+    for (int w = 0; w < NKW; ++w) {
+      const int kt = wave + 4 * w;
+      if (kt < NT) {
+        bf16x8_t kf[KK], vf[KK];
+#pragma unroll
+        for (int kk = 0; kk < KK; ++kk) {
+          kf[kk] = ld8(Ks + (kt * 16 + l16) * RS + 32 * kk + 8 * g);
+          vf[kk] = ld8(Vs + (kt * 16 + l16) * RS + 32 * kk + 8 * g);
+        }
+        const int key = kt * 16 + l16;
+#pragma unroll
+        for (int r = 0; r < QC / 32; ++r) {
+          const int qbase = qc * QC + 32 * r;
+          if (qbase < SP) {
+            float pf[8], df[8];
+#pragma unroll
+            for (int half = 0; half < 2; ++half) {
+              const int q0 = qbase + 16 * half;
+              f32x4_t s = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+              for (int kk = 0; kk < KK; ++kk) {
+                s = mfma(ld8(Qs + (q0 + l16) * RS + 32 * kk + 8 * g), kf[kk], s);
+                dp = mfma(ld8(dOs + (q0 + l16) * RS + 32 * kk + 8 * g), vf[kk], dp);
+              }
+              // s[i] = S[q = q0 + 4g + i][key]
+#pragma unroll
+              for (int i = 0; i < 4; ++i) {
+                const int q = q0 + 4 * g + i;
+                const float p = key < S ? exp2f(s[i] * sl2 - lse_s[q]) : 0.f;
+                const float ds = p * (dp[i] - delta_s[q]);
+                pf[4 * half + i] = p;
+                df[4 * half + i] = ds;
+                dSs[(q - qc * QC) * TS + key] = f2bf(ds);
+              }
+            }
+            const bf16x8_t pb = pack8(pf);
+            const bf16x8_t dsb = pack8(df);
+#pragma unroll
+            for (int dt = 0; dt < DT; ++dt) {
+              bf16x8_t a_do, a_q;
+              if (TR) {
+                const int off = (qbase + 4 * g + (l16 >> 2)) * RS + dt * 16 + 4 * (l16 & 3);
+                a_do = cat44(tr4(dOs + off), tr4(dOs + off + 16 * RS));
+                a_q = cat44(tr4(Qs + off), tr4(Qs + off + 16 * RS));
+              } else {
+                const int d = dt * 16 + l16;
+                const uint16_t* dor = dOt + d * TS + qbase + 4 * g;
+                const uint16_t* qr = Qt + d * TS + qbase + 4 * g;
+                a_do = cat44(ld4(dor), ld4(dor + 16));
+                a_q = cat44(ld4(qr), ld4(qr + 16));
+              }
+              dvacc[w][dt] = mfma(a_do, pb, dvacc[w][dt]);
+              dkacc[w][dt] = mfma(a_q, dsb, dkacc[w][dt]);
+            }
+          }
+        }
+      }
+    }
+    __syncthreads();
+    // dQ^T[d][q] = sum_key K^T[d][key] dS^T[key][q] for the query tile of this wave
+    {
+      const int qt = qc * (QC / 16) + wave;
+      if (qt < NT) {
+        f32x4_t dq[DT];
+#pragma unroll
+        for (int dt = 0; dt < DT; ++dt) dq[dt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < SP / 32; ++s) {
+          const bf16x8_t bop = ld8(dSs + (wave * 16 + l16) * TS + 32 * s + 8 * g);
+#pragma unroll
+          for (int dt = 0; dt < DT; ++dt) {
+            bf16x8_t ka;
+            if (TR) {
+              const uint16_t* kr = Ks + (32 * s + 8 * g + (l16 >> 2)) * RS + dt * 16 + 4 * (l16 & 3);
+              ka = cat44(tr4(kr), tr4(kr + 4 * RS));
+            } else {
+              ka = ld8(Kt + (dt * 16 + l16) * TS + 32 * s + 8 * g);
+            }
+            dq[dt] = mfma(ka, bop, dq[dt]);
+          }
+        }
+        const int q = qt * 16 + l16;
+        if (q < S) {
+#pragma unroll
+          for (int dt = 0; dt < DT; ++dt) {
+            float v[4] = {dq[dt][0] * scale, dq[dt][1] * scale, dq[dt][2] * scale, dq[dt][3] * scale};
+            store4(dQg + (long)q * ts + dt * 16 + 4 * g, v);
+          }
+        }
+      }
+    }
+    __syncthreads();
+  }
+  // write dK, dV of this wave's key tiles: acc[dt][i] = X^T[d = dt*16+4g+i][key = kt*16+l16]
+#pragma unroll
+  for (int w = 0; w < NKW; ++w) {
+    const int kt = wave + 4 * w;
+    const int key = kt * 16 + l16;
+    if (kt < NT && key < S) {
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt) {
+        float kv[4] = {dkacc[w][dt][0] * scale, dkacc[w][dt][1] * scale, dkacc[w][dt][2] * scale,
+                       dkacc[w][dt][3] * scale};
+        float vv[4] = {dvacc[w][dt][0], dvacc[w][dt][1], dvacc[w][dt][2], dvacc[w][dt][3]};
+        store4(dKg + (long)key * ts + dt * 16 + 4 * g, kv);
+        store4(dVg + (long)key * ts + dt * 16 + 4 * g, vv);
+      }
+    }
+  }
+}
+
+template <int HD, int SP, bool TR>
+size_t fwd_smem() { return (size_t)(SP * (HD + 8) + (TR ? SP * (HD + 8) : HD * (SP + 8))) * 2; }
+template <int HD, int SP, bool TR>
+size_t bwd_smem() {
+  return (size_t)(4 * SP * (HD + 8) + (TR ? 0 : 3 * HD * (SP + 8)) + 64 * (SP + 8)) * 2 + 2 * SP * sizeof(float);
+}
+
+int g_use_tr = 1;  // runtime switch (tests run both variants)
+
+template <int HD, int SP, bool TR>
+int run_t(bool fwd, const uint16_t* qkv, const uint16_t* o, const uint16_t* dO, const float* lse_in, uint16_t* out,
+          float* lse_out, int B, int S, int H, float scale, hipStream_t st) {
+  dim3 grid(B * H);
+  const size_t sm = fwd ? fwd_smem<HD, SP, TR>() : bwd_smem<HD, SP, TR>();
+  if (sm > 160 * 1024) return -3;
+  const void* fn = fwd ? (const void*)attn_fwd_kernel<HD, SP, TR> : (const void*)attn_bwd_kernel<HD, SP, TR>;
+  static bool attr_set[2] = {false, false};
+  if (sm > 64 * 1024 && !attr_set[fwd ? 0 : 1]) {
+    hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
+    attr_set[fwd ? 0 : 1] = true;
+  }
+  if (fwd)
+    attn_fwd_kernel<HD, SP, TR><<<grid, 256, sm, st>>>(qkv, out, lse_out, S, H, scale);
+  else
+    attn_bwd_kernel<HD, SP, TR><<<grid, 256, sm, st>>>(qkv, o, dO, lse_in, out, S, H, scale);
+  return 0;
+}
+
+template <int HD, int SP>
+int run(bool fwd, const uint16_t* qkv, const uint16_t* o, const uint16_t* dO, const float* lse_in, uint16_t* out,
+        float* lse_out, int B, int S, int H, float scale, hipStream_t st) {
+  if (g_use_tr) return run_t<HD, SP, true>(fwd, qkv, o, dO, lse_in, out, lse_out, B, S, H, scale, st);
+  return run_t<HD, SP, false>(fwd, qkv, o, dO, lse_in, out, lse_out, B, S, H, scale, st);
+}
+
+template <int HD>
+int dispatch_sp(bool fwd, const uint16_t* qkv, const uint16_t* o, const uint16_t* dO, const float* lse_in,
+                uint16_t* out, float* lse_out, int B, int S, int H, float scale, hipStream_t st) {
+  if (S <= 32) return run<HD, 32>(fwd, qkv, o, dO, lse_in, out, lse_out, B, S, H, scale, st);
+  if (S <= 64) return run<HD, 64>(fwd, qkv, o, dO, lse_in, out, lse_out, B, S, H, scale, st);
+  if (S <= 128) return run<HD, 128>(fwd, qkv, o, dO, lse_in, out, lse_out, B, S, H, scale, st);
+  if (S <= 224) return run<HD, 224>(fwd, qkv, o, dO, lse_in, out, lse_out, B, S, H, scale, st);
+  return -2;
+}
+
+}  // namespace
+
+int jm_attn_max_seq() { return 224; }
+void jm_attn_set_tr(int v) { g_use_tr = v; }
+
+int jm_attn_fwd(const uint16_t* qkv, uint16_t* o, float* lse, int B, int S, int H, int hd, hipStream_t st) {
+  const float scale = 1.f / sqrtf((float)hd);
+  if (hd == 32) return dispatch_sp<32>(true, qkv, nullptr, nullptr, nullptr, o, lse, B, S, H, scale, st);
+  if (hd == 64) return dispatch_sp<64>(true, qkv, nullptr, nullptr, nullptr, o, lse, B, S, H, scale, st);
+  return -1;
+}
+
+int jm_attn_bwd(const uint16_t* qkv, const uint16_t* o, const uint16_t* dO, const float* lse, uint16_t* dqkv, int B,
+                int S, int H, int hd, hipStream_t st) {
+  const float scale = 1.f / sqrtf((float)hd);
+  if (hd == 32) return dispatch_sp<32>(false, qkv, o, dO, lse, dqkv, nullptr, B, S, H, scale, st);
+  if (hd == 64) return dispatch_sp<64>(false, qkv, o, dO, lse, dqkv, nullptr, B, S, H, scale, st);
+  return -1;
+}

@@ -1,0 +1,260 @@
+// PyTorch bindings of the jumbo_mae_tpu_amd HIP kernels.
+// Kernels live in *.hip translation units with a plain pointer + hipStream_t interface; this file
+// only validates tensors, allocates outputs with the caching allocator and launches on the
+// current HIP stream (so everything is HIP-graph capturable).
+#include <torch/extension.h>
+#include <c10/hip/HIPStream.h>
+#include <hip/hip_runtime.h>
+
+// ---- kernel entry points (see *.hip)
+int jm_layernorm_fwd(const float* x, long sB, long sT, int B, int T, int D, const float* gamma, const float* beta,
+                     float eps, void* y, int out_bf16, float* mean, float* rstd, hipStream_t st);
+int jm_layernorm_bwd(const void* dy, int dy_bf16, const float* x, long sB, long sT, int B, int T, int D,
+                     const float* mean, const float* rstd, const float* gamma, float* dx, float* dgamma, float* dbeta,
+                     int accum_params, hipStream_t st);
+int jm_gelu_fwd(const uint16_t* h, uint16_t* a, long n, hipStream_t st);
+int jm_gelu_bwd(const uint16_t* h, const uint16_t* da, uint16_t* dh, float* bias_grad, int M, int N, hipStream_t st);
+int jm_colsum_bf16(const uint16_t* x, float* acc, int M, int N, hipStream_t st);
+int jm_residual_fwd(const float* x, long sB, long sT, int B, int T, int D, const uint16_t* y, const float* scale,
+                    const float* mask, float* out, hipStream_t st);
+int jm_residual_bwd(const float* dout, const uint16_t* y, const float* scale, const float* mask, float* dscale,
+                    uint16_t* dy, int B, int T, int D, hipStream_t st);
+int jm_attn_fwd(const uint16_t* qkv, uint16_t* o, float* lse, int B, int S, int H, int hd, hipStream_t st);
+int jm_attn_bwd(const uint16_t* qkv, const uint16_t* o, const uint16_t* dO, const float* lse, uint16_t* dqkv, int B,
+                int S, int H, int hd, hipStream_t st);
+int jm_attn_max_seq();
+void jm_attn_set_tr(int v);
+void jm_opt_sumsq(const float* x, const int* chunks, int nchunks, float* out, hipStream_t st);
+void jm_opt_adamw(float* p, const float* g, float* mu, float* nu, uint16_t* shadow, const int* chunks, int nchunks,
+                  const float* meta, const float* hyper, const float* gnorm_sq, hipStream_t st);
+void jm_opt_lamb_phase1(const float* p, const float* g, float* mu, float* nu, float* u, const int* chunks, int nchunks,
+                        const float* meta, const float* hyper, const float* gnorm_sq, float* norms, hipStream_t st);
+void jm_opt_lars_norms(const float* p, const float* g, const int* chunks, int nchunks, const float* hyper,
+                       const float* gnorm_sq, float* norms, hipStream_t st);
+void jm_opt_apply_trust(float* p, const float* u_or_g, float* trace, uint16_t* shadow, const int* chunks, int nchunks,
+                        const float* meta, const float* hyper, const float* norms, const float* gnorm_sq, int mode,
+                        float momentum, float trust_coef, hipStream_t st);
+void jm_opt_sgd(float* p, const float* g, float* trace, uint16_t* shadow, const int* chunks, int nchunks,
+                const float* meta, const float* hyper, const float* gnorm_sq, float momentum, hipStream_t st);
+int jm_patchify_normalize(const uint8_t* img, float* out, int B, int H, int W, int p, hipStream_t st);
+
+namespace {
+
+hipStream_t stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+#define CHECK_CUDA(x) TORCH_CHECK((x).is_cuda(), #x " must be a GPU tensor")
+#define CHECK_CONTIG(x) TORCH_CHECK((x).is_contiguous(), #x " must be contiguous")
+#define CHECK_DT(x, d) TORCH_CHECK((x).scalar_type() == (d), #x " has wrong dtype")
+
+const uint16_t* bf(const torch::Tensor& t) { return reinterpret_cast<const uint16_t*>(t.data_ptr()); }
+uint16_t* bfm(torch::Tensor& t) { return reinterpret_cast<uint16_t*>(t.data_ptr()); }
+const float* fopt(const c10::optional<torch::Tensor>& t) {
+  return t.has_value() && t->defined() ? t->data_ptr<float>() : nullptr;
+}
+float* fopt_m(c10::optional<torch::Tensor>& t) { return t.has_value() && t->defined() ? t->data_ptr<float>() : nullptr; }
+
+void check_rc(int rc, const char* what) { TORCH_CHECK(rc == 0, what, ": unsupported shape (rc=", rc, ")"); }
+
+// ------------------------------------------------------------------------------ layernorm
+std::vector<torch::Tensor> layernorm_fwd(torch::Tensor x, torch::Tensor gamma, torch::Tensor beta, double eps,
+                                         py::object out_dtype) {
+  CHECK_CUDA(x);
+  TORCH_CHECK(x.dim() == 3 && x.stride(2) == 1, "x must be [B,T,D] with contiguous last dim");
+  CHECK_DT(x, torch::kFloat32);
+  CHECK_CONTIG(gamma);
+  CHECK_CONTIG(beta);
+  const auto odt = torch::python::detail::py_object_to_dtype(out_dtype);
+  const int B = x.size(0), T = x.size(1), D = x.size(2);
+  auto y = torch::empty({(long)B * T, D}, x.options().dtype(odt));
+  auto mean = torch::empty({(long)B * T}, x.options());
+  auto rstd = torch::empty({(long)B * T}, x.options());
+  TORCH_CHECK(odt == torch::kBFloat16 || odt == torch::kFloat32, "out dtype must be bf16/fp32");
+  check_rc(jm_layernorm_fwd(x.data_ptr<float>(), x.stride(0), x.stride(1), B, T, D, gamma.data_ptr<float>(),
+                            beta.data_ptr<float>(), (float)eps, y.data_ptr(), odt == torch::kBFloat16,
+                            mean.data_ptr<float>(), rstd.data_ptr<float>(), stream()),
+           "layernorm_fwd");
+  return {y, mean, rstd};
+}
+
+torch::Tensor layernorm_bwd(torch::Tensor dy, torch::Tensor x, torch::Tensor mean, torch::Tensor rstd,
+                            torch::Tensor gamma, torch::Tensor dgamma, torch::Tensor dbeta, bool accum) {
+  CHECK_CONTIG(dy);
+  TORCH_CHECK(x.dim() == 3 && x.stride(2) == 1, "x must be [B,T,D]");
+  const int B = x.size(0), T = x.size(1), D = x.size(2);
+  TORCH_CHECK(dy.numel() == (long)B * T * D, "dy shape");
+  auto dx = torch::empty({B, T, D}, x.options());
+  const bool dyb = dy.scalar_type() == torch::kBFloat16;
+  TORCH_CHECK(dyb || dy.scalar_type() == torch::kFloat32, "dy dtype");
+  check_rc(jm_layernorm_bwd(dy.data_ptr(), dyb, x.data_ptr<float>(), x.stride(0), x.stride(1), B, T, D,
+                            mean.data_ptr<float>(), rstd.data_ptr<float>(), gamma.data_ptr<float>(),
+                            dx.data_ptr<float>(), dgamma.data_ptr<float>(), dbeta.data_ptr<float>(), accum, stream()),
+           "layernorm_bwd");
+  return dx;
+}
+
+// ------------------------------------------------------------------------------ elementwise
+torch::Tensor gelu_fwd(torch::Tensor h) {
+  CHECK_CONTIG(h);
+  CHECK_DT(h, torch::kBFloat16);
+  auto a = torch::empty_like(h);
+  check_rc(jm_gelu_fwd(bf(h), bfm(a), h.numel(), stream()), "gelu_fwd");
+  return a;
+}
+
+torch::Tensor gelu_bwd(torch::Tensor h, torch::Tensor da, c10::optional<torch::Tensor> bias_grad) {
+  CHECK_CONTIG(h);
+  CHECK_CONTIG(da);
+  CHECK_DT(h, torch::kBFloat16);
+  CHECK_DT(da, torch::kBFloat16);
+  const int N = h.size(-1);
+  const int M = h.numel() / N;
+  auto dh = torch::empty_like(h);
+  check_rc(jm_gelu_bwd(bf(h), bf(da), bfm(dh), fopt_m(bias_grad), M, N, stream()), "gelu_bwd");
+  return dh;
+}
+
+void colsum(torch::Tensor x, torch::Tensor acc) {
+  CHECK_CONTIG(x);
+  CHECK_DT(x, torch::kBFloat16);
+  const int N = x.size(-1);
+  const int M = x.numel() / N;
+  check_rc(jm_colsum_bf16(bf(x), acc.data_ptr<float>(), M, N, stream()), "colsum");
+}
+
+torch::Tensor residual_fwd(torch::Tensor x, torch::Tensor y, c10::optional<torch::Tensor> scale,
+                           c10::optional<torch::Tensor> mask) {
+  TORCH_CHECK(x.dim() == 3 && x.stride(2) == 1, "x must be [B,T,D]");
+  CHECK_DT(x, torch::kFloat32);
+  CHECK_CONTIG(y);
+  CHECK_DT(y, torch::kBFloat16);
+  const int B = x.size(0), T = x.size(1), D = x.size(2);
+  auto out = torch::empty({B, T, D}, x.options());
+  check_rc(jm_residual_fwd(x.data_ptr<float>(), x.stride(0), x.stride(1), B, T, D, bf(y), fopt(scale), fopt(mask),
+                           out.data_ptr<float>(), stream()),
+           "residual_fwd");
+  return out;
+}
+
+torch::Tensor residual_bwd(torch::Tensor dout, c10::optional<torch::Tensor> y, c10::optional<torch::Tensor> scale,
+                           c10::optional<torch::Tensor> mask, c10::optional<torch::Tensor> dscale, py::object ydtype) {
+  CHECK_CONTIG(dout);
+  CHECK_DT(dout, torch::kFloat32);
+  const int B = dout.size(0), T = dout.size(1), D = dout.size(2);
+  const auto odt = torch::python::detail::py_object_to_dtype(ydtype);
+  TORCH_CHECK(odt == torch::kBFloat16, "residual_bwd: y must be bf16");
+  auto dy = torch::empty({(long)B * T, D}, dout.options().dtype(odt));
+  const uint16_t* yp = (y.has_value() && y->defined()) ? bf(*y) : nullptr;
+  check_rc(jm_residual_bwd(dout.data_ptr<float>(), yp, fopt(scale), fopt(mask), fopt_m(dscale), bfm(dy), B, T, D,
+                           stream()),
+           "residual_bwd");
+  return dy;
+}
+
+// ------------------------------------------------------------------------------ attention
+std::vector<torch::Tensor> attn_fwd(torch::Tensor qkv, int64_t heads) {
+  CHECK_CONTIG(qkv);
+  CHECK_DT(qkv, torch::kBFloat16);
+  const int B = qkv.size(0), S = qkv.size(1), D3 = qkv.size(2);
+  const int D = D3 / 3, hd = D / heads;
+  auto o = torch::empty({B, S, D}, qkv.options());
+  auto lse = torch::empty({B, (long)heads, S}, qkv.options().dtype(torch::kFloat32));
+  check_rc(jm_attn_fwd(bf(qkv), bfm(o), lse.data_ptr<float>(), B, S, heads, hd, stream()), "attn_fwd");
+  return {o, lse};
+}
+
+torch::Tensor attn_bwd(torch::Tensor dO, torch::Tensor qkv, torch::Tensor o, torch::Tensor lse, int64_t heads) {
+  CHECK_CONTIG(dO);
+  CHECK_CONTIG(qkv);
+  CHECK_CONTIG(o);
+  CHECK_DT(dO, torch::kBFloat16);
+  const int B = qkv.size(0), S = qkv.size(1), D3 = qkv.size(2);
+  const int D = D3 / 3, hd = D / heads;
+  auto dqkv = torch::empty_like(qkv);
+  check_rc(jm_attn_bwd(bf(qkv), bf(o), bf(dO), lse.data_ptr<float>(), bfm(dqkv), B, S, heads, hd, stream()),
+           "attn_bwd");
+  return dqkv;
+}
+
+// ------------------------------------------------------------------------------ optimizer
+int nch(const torch::Tensor& chunks) { return chunks.size(0); }
+const int* chp(const torch::Tensor& chunks) { return chunks.data_ptr<int>(); }
+uint16_t* shadow_ptr(c10::optional<torch::Tensor>& s) {
+  return (s.has_value() && s->defined()) ? reinterpret_cast<uint16_t*>(s->data_ptr()) : nullptr;
+}
+
+void opt_sumsq(torch::Tensor x, torch::Tensor chunks, torch::Tensor out) {
+  jm_opt_sumsq(x.data_ptr<float>(), chp(chunks), nch(chunks), out.data_ptr<float>(), stream());
+}
+
+void opt_adamw(torch::Tensor p, torch::Tensor g, torch::Tensor mu, torch::Tensor nu, c10::optional<torch::Tensor> shadow,
+               torch::Tensor chunks, torch::Tensor meta, torch::Tensor hyper, torch::Tensor gnorm_sq) {
+  jm_opt_adamw(p.data_ptr<float>(), g.data_ptr<float>(), mu.data_ptr<float>(), nu.data_ptr<float>(),
+               shadow_ptr(shadow), chp(chunks), nch(chunks), meta.data_ptr<float>(), hyper.data_ptr<float>(),
+               gnorm_sq.data_ptr<float>(), stream());
+}
+
+void opt_lamb_phase1(torch::Tensor p, torch::Tensor g, torch::Tensor mu, torch::Tensor nu, torch::Tensor u,
+                     torch::Tensor chunks, torch::Tensor meta, torch::Tensor hyper, torch::Tensor gnorm_sq,
+                     torch::Tensor norms) {
+  jm_opt_lamb_phase1(p.data_ptr<float>(), g.data_ptr<float>(), mu.data_ptr<float>(), nu.data_ptr<float>(),
+                     u.data_ptr<float>(), chp(chunks), nch(chunks), meta.data_ptr<float>(), hyper.data_ptr<float>(),
+                     gnorm_sq.data_ptr<float>(), norms.data_ptr<float>(), stream());
+}
+
+void opt_lars_norms(torch::Tensor p, torch::Tensor g, torch::Tensor chunks, torch::Tensor hyper,
+                    torch::Tensor gnorm_sq, torch::Tensor norms) {
+  jm_opt_lars_norms(p.data_ptr<float>(), g.data_ptr<float>(), chp(chunks), nch(chunks), hyper.data_ptr<float>(),
+                    gnorm_sq.data_ptr<float>(), norms.data_ptr<float>(), stream());
+}
+
+void opt_apply_trust(torch::Tensor p, torch::Tensor u_or_g, c10::optional<torch::Tensor> trace,
+                     c10::optional<torch::Tensor> shadow, torch::Tensor chunks, torch::Tensor meta, torch::Tensor hyper,
+                     torch::Tensor norms, torch::Tensor gnorm_sq, int64_t mode, double momentum, double trust_coef) {
+  jm_opt_apply_trust(p.data_ptr<float>(), u_or_g.data_ptr<float>(), fopt_m(trace), shadow_ptr(shadow), chp(chunks),
+                     nch(chunks), meta.data_ptr<float>(), hyper.data_ptr<float>(), norms.data_ptr<float>(),
+                     gnorm_sq.data_ptr<float>(), (int)mode, (float)momentum, (float)trust_coef, stream());
+}
+
+void opt_sgd(torch::Tensor p, torch::Tensor g, torch::Tensor trace, c10::optional<torch::Tensor> shadow,
+             torch::Tensor chunks, torch::Tensor meta, torch::Tensor hyper, torch::Tensor gnorm_sq, double momentum) {
+  jm_opt_sgd(p.data_ptr<float>(), g.data_ptr<float>(), trace.data_ptr<float>(), shadow_ptr(shadow), chp(chunks),
+             nch(chunks), meta.data_ptr<float>(), hyper.data_ptr<float>(), gnorm_sq.data_ptr<float>(),
+             (float)momentum, stream());
+}
+
+// ------------------------------------------------------------------------------ MAE
+torch::Tensor patchify_normalize(torch::Tensor img, int64_t p) {
+  CHECK_CONTIG(img);
+  CHECK_DT(img, torch::kUInt8);
+  const int B = img.size(0), H = img.size(2), W = img.size(3);
+  TORCH_CHECK(img.size(1) == 3, "expects 3 channels");
+  const int n = (H / p) * (W / p);
+  auto out = torch::empty({B, n, (long)p * p * 3}, img.options().dtype(torch::kFloat32));
+  check_rc(jm_patchify_normalize(img.data_ptr<uint8_t>(), out.data_ptr<float>(), B, H, W, p, stream()),
+           "patchify_normalize");
+  return out;
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_C, m) {
+  m.doc() = "jumbo_mae_tpu_amd CDNA4 (gfx950) HIP kernels";
+  m.def("layernorm_fwd", &layernorm_fwd);
+  m.def("layernorm_bwd", &layernorm_bwd);
+  m.def("gelu_fwd", &gelu_fwd);
+  m.def("gelu_bwd", &gelu_bwd, py::arg("h"), py::arg("da"), py::arg("bias_grad") = py::none());
+  m.def("colsum", &colsum);
+  m.def("residual_fwd", &residual_fwd);
+  m.def("residual_bwd", &residual_bwd);
+  m.def("attn_fwd", &attn_fwd);
+  m.def("attn_bwd", &attn_bwd);
+  m.def("attn_max_seq", &jm_attn_max_seq);
+  m.def("attn_set_tr", &jm_attn_set_tr);
+  m.def("opt_sumsq", &opt_sumsq);
+  m.def("opt_adamw", &opt_adamw);
+  m.def("opt_lamb_phase1", &opt_lamb_phase1);
+  m.def("opt_lars_norms", &opt_lars_norms);
+  m.def("opt_apply_trust", &opt_apply_trust);
+  m.def("opt_sgd", &opt_sgd);
+  m.def("patchify_normalize", &patchify_normalize);
+}

@@ -1,0 +1,110 @@
+// Shared device helpers for the jumbo_mae_tpu_amd CDNA4 (gfx950) kernels.
+// Wave size is 64 on CDNA: every reduction below is a 64-lane butterfly.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <hip/hip_bf16.h>
+#include <stdint.h>
+
+#define JM_DEVICE __device__ __forceinline__
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8_t;
+typedef __attribute__((ext_vector_type(4))) float f32x4_t;
+typedef __attribute__((ext_vector_type(4))) short s16x4_t;
+typedef __attribute__((ext_vector_type(8))) short s16x8_t;
+typedef uint16_t bf16_raw;
+
+constexpr int WAVE = 64;
+
+JM_DEVICE float bf2f(uint16_t v) { return __uint_as_float(((uint32_t)v) << 16); }
+
+JM_DEVICE uint16_t f2bf(float f) {
+  // round-to-nearest-even; hipcc lowers the builtin conversion to v_cvt_pk_bf16_f32 on gfx950,
+  // which keeps NaNs NaN (MI355X_MICROARCH.md "Correctness boundaries").
+  __hip_bfloat16 h = __float2bfloat16(f);
+  return *reinterpret_cast<uint16_t*>(&h);
+}
+
+JM_DEVICE uint32_t pack_bf2(float a, float b) {
+  return (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16);
+}
+
+template <typename T> JM_DEVICE float to_f(T v);
+template <> JM_DEVICE float to_f<float>(float v) { return v; }
+template <> JM_DEVICE float to_f<uint16_t>(uint16_t v) { return bf2f(v); }
+
+template <typename T> JM_DEVICE T from_f(float v);
+template <> JM_DEVICE float from_f<float>(float v) { return v; }
+template <> JM_DEVICE uint16_t from_f<uint16_t>(float v) { return f2bf(v); }
+
+JM_DEVICE float wave_sum(float v) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m, WAVE);
+  return v;
+}
+
+JM_DEVICE float wave_max(float v) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) v = fmaxf(v, __shfl_xor(v, m, WAVE));
+  return v;
+}
+
+// 8 x bf16 <-> 8 x float through one 16-byte access
+struct bf16x8_u {
+  union {
+    uint4 u;
+    uint16_t h[8];
+  };
+};
+
+JM_DEVICE void load8(const uint16_t* p, float* f) {
+  bf16x8_u v;
+  v.u = *reinterpret_cast<const uint4*>(p);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) f[i] = bf2f(v.h[i]);
+}
+
+JM_DEVICE void store8(uint16_t* p, const float* f) {
+  bf16x8_u v;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) v.h[i] = f2bf(f[i]);
+  *reinterpret_cast<uint4*>(p) = v.u;
+}
+
+JM_DEVICE void load8(const float* p, float* f) {
+  float4 a = *reinterpret_cast<const float4*>(p);
+  float4 b = *reinterpret_cast<const float4*>(p + 4);
+  f[0] = a.x; f[1] = a.y; f[2] = a.z; f[3] = a.w;
+  f[4] = b.x; f[5] = b.y; f[6] = b.z; f[7] = b.w;
+}
+
+JM_DEVICE void store8(float* p, const float* f) {
+  *reinterpret_cast<float4*>(p) = make_float4(f[0], f[1], f[2], f[3]);
+  *reinterpret_cast<float4*>(p + 4) = make_float4(f[4], f[5], f[6], f[7]);
+}
+
+JM_DEVICE void load4(const float* p, float* f) {
+  float4 a = *reinterpret_cast<const float4*>(p);
+  f[0] = a.x; f[1] = a.y; f[2] = a.z; f[3] = a.w;
+}
+JM_DEVICE void store4(float* p, const float* f) {
+  *reinterpret_cast<float4*>(p) = make_float4(f[0], f[1], f[2], f[3]);
+}
+JM_DEVICE void load4(const uint16_t* p, float* f) {
+  uint2 v = *reinterpret_cast<const uint2*>(p);
+  f[0] = __uint_as_float(v.x << 16); f[1] = __uint_as_float(v.x & 0xffff0000u);
+  f[2] = __uint_as_float(v.y << 16); f[3] = __uint_as_float(v.y & 0xffff0000u);
+}
+JM_DEVICE void store4(uint16_t* p, const float* f) {
+  uint2 v;
+  v.x = pack_bf2(f[0], f[1]);
+  v.y = pack_bf2(f[2], f[3]);
+  *reinterpret_cast<uint2*>(p) = v;
+}
+
+#define JM_CHECK(x)                                                                  \
+  do {                                                                               \
+    hipError_t e_ = (x);                                                             \
+    if (e_ != hipSuccess) {                                                          \
+      fprintf(stderr, "HIP error %s at %s:%d\n", hipGetErrorString(e_), __FILE__, __LINE__); \
+    }                                                                                \
+  } while (0)

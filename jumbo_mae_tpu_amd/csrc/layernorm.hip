@@ -1,0 +1,225 @@
+// LayerNorm forward / backward for gfx950 (Flax LayerNorm semantics: eps inside rsqrt, biased
+// variance, scale + bias; reference modeling.py:155-156,177-179,238,282).
+//
+// Layout: input x is the fp32 residual stream viewed as [B, T, D] with arbitrary batch / token
+// strides (so the CLS rows x[:, :3] reshaped to [B, 1, 3D] and the patch rows x[:, 3:] are read
+// in place, no gather copies).  One 64-lane wave owns one row; each lane keeps V float4 of the
+// row in registers (D <= 256*V), so x is read exactly once.  Output rows are contiguous [B*T, D]
+// in bf16 (GEMM operand) or fp32.
+//
+// Backward: one wave per row for dx, while dgamma/dbeta are reduced per wave in registers over a
+// grid-stride row loop, then across the block's waves with LDS float atomics, then ONE global
+// atomicAdd per column per block straight into the flat fp32 gradient buffer.
+#include "common.h"
+
+namespace {
+
+template <int V, typename TO>
+__global__ __launch_bounds__(256) void ln_fwd_kernel(const float* __restrict__ x, long sB, long sT, int T,
+                                                     int rows, int D, const float* __restrict__ gamma,
+                                                     const float* __restrict__ beta, float eps,
+                                                     TO* __restrict__ y, float* __restrict__ mean_out,
+                                                     float* __restrict__ rstd_out) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + wave;
+  if (row >= rows) return;
+  const int b = row / T, t = row - b * T;
+  const float* xr = x + b * sB + t * sT;
+  float v[V][4];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < V; ++i) {
+    const int col = (i * 64 + lane) * 4;
+    if (col < D) {
+      load4(xr + col, v[i]);
+    } else {
+      v[i][0] = v[i][1] = v[i][2] = v[i][3] = 0.f;
+    }
+    s += v[i][0] + v[i][1] + v[i][2] + v[i][3];
+  }
+  const float mean = wave_sum(s) / D;
+  float s2 = 0.f;
+#pragma unroll
+  for (int i = 0; i < V; ++i) {
+    const int col = (i * 64 + lane) * 4;
+    if (col < D) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float d = v[i][j] - mean;
+        s2 += d * d;
+      }
+    }
+  }
+  const float rstd = rsqrtf(wave_sum(s2) / D + eps);
+  TO* yr = y + (long)row * D;
+#pragma unroll
+  for (int i = 0; i < V; ++i) {
+    const int col = (i * 64 + lane) * 4;
+    if (col < D) {
+      float gg[4], bb[4], o[4];
+      load4(gamma + col, gg);
+      load4(beta + col, bb);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) o[j] = (v[i][j] - mean) * rstd * gg[j] + bb[j];
+      store4(yr + col, o);
+    }
+  }
+  if (lane == 0) {
+    mean_out[row] = mean;
+    rstd_out[row] = rstd;
+  }
+}
+
+template <int V, typename TI>
+__global__ __launch_bounds__(256) void ln_bwd_kernel(const TI* __restrict__ dy, const float* __restrict__ x,
+                                                     long sB, long sT, int T, int rows, int D,
+                                                     const float* __restrict__ mean, const float* __restrict__ rstd,
+                                                     const float* __restrict__ gamma, float* __restrict__ dx,
+                                                     float* __restrict__ dgamma, float* __restrict__ dbeta,
+                                                     int accum_params) {
+  extern __shared__ __attribute__((aligned(16))) float red[];  // [2*D]
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  if (accum_params) {
+    for (int i = threadIdx.x; i < 2 * D; i += 256) red[i] = 0.f;
+    __syncthreads();
+  }
+  float dg[V][4], db[V][4], gg[V][4];
+#pragma unroll
+  for (int i = 0; i < V; ++i) {
+    const int col = (i * 64 + lane) * 4;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) dg[i][j] = db[i][j] = 0.f;
+    if (col < D) load4(gamma + col, gg[i]);
+  }
+  for (int row = blockIdx.x * 4 + wave; row < rows; row += gridDim.x * 4) {
+    const int b = row / T, t = row - b * T;
+    const float* xr = x + b * sB + t * sT;
+    const TI* dyr = dy + (long)row * D;
+    const float mu = mean[row], rs = rstd[row];
+    float xh[V][4], g[V][4];
+    float sg = 0.f, sgx = 0.f;
+#pragma unroll
+    for (int i = 0; i < V; ++i) {
+      const int col = (i * 64 + lane) * 4;
+      if (col < D) {
+        float xv[4], dv[4];
+        load4(xr + col, xv);
+        load4(dyr + col, dv);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          xh[i][j] = (xv[j] - mu) * rs;
+          g[i][j] = dv[j] * gg[i][j];
+          sg += g[i][j];
+          sgx += g[i][j] * xh[i][j];
+          dg[i][j] += dv[j] * xh[i][j];
+          db[i][j] += dv[j];
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) xh[i][j] = g[i][j] = 0.f;
+      }
+    }
+    sg = wave_sum(sg) / D;
+    sgx = wave_sum(sgx) / D;
+    float* dxr = dx + (long)row * D;
+#pragma unroll
+    for (int i = 0; i < V; ++i) {
+      const int col = (i * 64 + lane) * 4;
+      if (col < D) {
+        float o[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) o[j] = rs * (g[i][j] - sg - xh[i][j] * sgx);
+        store4(dxr + col, o);
+      }
+    }
+  }
+  if (!accum_params) return;
+#pragma unroll
+  for (int i = 0; i < V; ++i) {
+    const int col = (i * 64 + lane) * 4;
+    if (col < D) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        atomicAdd(&red[col + j], dg[i][j]);
+        atomicAdd(&red[D + col + j], db[i][j]);
+      }
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < D; i += 256) {
+    atomicAdd(&dgamma[i], red[i]);
+    atomicAdd(&dbeta[i], red[D + i]);
+  }
+}
+
+template <typename TO>
+void launch_fwd(int V, dim3 grid, hipStream_t st, const float* x, long sB, long sT, int T, int rows, int D,
+                const float* g, const float* b, float eps, TO* y, float* m, float* r) {
+#define JM_LNF(VV) \
+  case VV: ln_fwd_kernel<VV, TO><<<grid, 256, 0, st>>>(x, sB, sT, T, rows, D, g, b, eps, y, m, r); break;
+  switch (V) {
+    JM_LNF(1) JM_LNF(2) JM_LNF(3) JM_LNF(4) JM_LNF(6) JM_LNF(8) JM_LNF(9) JM_LNF(12) JM_LNF(16)
+    default: break;
+  }
+#undef JM_LNF
+}
+
+template <typename TI>
+void launch_bwd(int V, dim3 grid, size_t smem, hipStream_t st, const TI* dy, const float* x, long sB, long sT,
+                int T, int rows, int D, const float* m, const float* r, const float* g, float* dx, float* dg,
+                float* db, int acc) {
+#define JM_LNB(VV)                                                                                  \
+  case VV:                                                                                          \
+    ln_bwd_kernel<VV, TI><<<grid, 256, smem, st>>>(dy, x, sB, sT, T, rows, D, m, r, g, dx, dg, db, acc); \
+    break;
+  switch (V) {
+    JM_LNB(1) JM_LNB(2) JM_LNB(3) JM_LNB(4) JM_LNB(6) JM_LNB(8) JM_LNB(9) JM_LNB(12) JM_LNB(16)
+    default: break;
+  }
+#undef JM_LNB
+}
+
+int pick_v(int D) {
+  const int need = (D + 255) / 256;
+  const int opts[] = {1, 2, 3, 4, 6, 8, 9, 12, 16};
+  for (int o : opts)
+    if (o >= need) return o;
+  return -1;
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------------- host entry points
+int jm_layernorm_fwd(const float* x, long sB, long sT, int B, int T, int D, const float* gamma,
+                     const float* beta, float eps, void* y, int out_bf16, float* mean, float* rstd,
+                     hipStream_t st) {
+  const int V = pick_v(D);
+  if (V < 0 || (D % 4) != 0) return -1;
+  const int rows = B * T;
+  dim3 grid((rows + 3) / 4);
+  if (out_bf16)
+    launch_fwd<uint16_t>(V, grid, st, x, sB, sT, T, rows, D, gamma, beta, eps, (uint16_t*)y, mean, rstd);
+  else
+    launch_fwd<float>(V, grid, st, x, sB, sT, T, rows, D, gamma, beta, eps, (float*)y, mean, rstd);
+  return 0;
+}
+
+int jm_layernorm_bwd(const void* dy, int dy_bf16, const float* x, long sB, long sT, int B, int T, int D,
+                     const float* mean, const float* rstd, const float* gamma, float* dx, float* dgamma,
+                     float* dbeta, int accum_params, hipStream_t st) {
+  const int V = pick_v(D);
+  if (V < 0 || (D % 4) != 0) return -1;
+  const int rows = B * T;
+  int nb = (rows + 3) / 4;
+  // grid-stride: enough waves to stream, few enough blocks that the per-block column atomics stay cheap
+  if (nb > 1024) nb = 1024;
+  dim3 grid(nb);
+  const size_t smem = accum_params ? 2 * D * sizeof(float) : 0;
+  if (dy_bf16)
+    launch_bwd<uint16_t>(V, grid, smem, st, (const uint16_t*)dy, x, sB, sT, T, rows, D, mean, rstd, gamma, dx,
+                         dgamma, dbeta, accum_params);
+  else
+    launch_bwd<float>(V, grid, smem, st, (const float*)dy, x, sB, sT, T, rows, D, mean, rstd, gamma, dx, dgamma,
+                      dbeta, accum_params);
+  return 0;
+}

@@ -1,0 +1,107 @@
+"""MAE pretraining task module.
+
+Parity: ``PretrainModule`` (/root/reference/src/pretraining.py:76-122) and the MAE branch of
+``ViT.__call__`` (/root/reference/src/modeling.py:245-267).  Owns ``image_mask_embedding``
+(1,1,d), ``decoder_proj`` (D->d) and ``decoder_image_output`` (d->p*p*3).
+
+Differences by design (documented in SURVEY.md §2.9):
+* Q2 fixed: the number of mask tokens is ``N - keep`` (the reference uses ``int(N*ratio)``,
+  which silently clamps a gather when ``int(N*ratio) + int(N*(1-ratio)) != N``).
+* mask-first embedding (see models/vit.py docstring); the final encoder LayerNorm feeds the
+  decoder projection directly in the compute dtype.
+* the decoder's final LayerNorm and the prediction GEMM only run on the 196 patch rows (the
+  reference computes them for the 3 CLS rows too and then discards those rows).
+"""
+
+from __future__ import annotations
+
+import torch
+
+from ..config import DecoderConfig, ViTConfig
+from ..data.constants import IMAGENET_DEFAULT_MEAN, IMAGENET_DEFAULT_STD
+from ..ops import functional as Fn
+from ..ops import mae as mae_ops
+from ..ops.params_fn import param_value
+from ..utils.mae import masking_ids
+from .params import ParamStore, trunc_normal_
+from .vit import Dense, JumboViT, MAEDecoder
+
+
+class PretrainModel:
+    def __init__(self, vit_cfg: ViTConfig, dec_cfg: DecoderConfig, norm_pix_loss: bool = False,
+                 mask_mode: str = "shared"):
+        assert vit_cfg.image_mask_ratio is not None
+        self.cfg, self.dec_cfg = vit_cfg, dec_cfg
+        self.norm_pix_loss = norm_pix_loss
+        self.mask_mode = mask_mode
+        self.store = ParamStore()
+        s = self.store
+        self.encoder = JumboViT(s, vit_cfg, ("model",))
+        d = dec_cfg.dec_dim
+        self.mask_token = s.handle(s.add(("image_mask_embedding",), (1, 1, d), trunc_normal_))
+        self.decoder_proj = Dense(s, ("decoder_proj",), vit_cfg.dim, d)
+        s.pad()
+        self.decoder = MAEDecoder(s, dec_cfg, ("decoder_model",))
+        self.decoder_image_output = Dense(s, ("decoder_image_output",), d, vit_cfg.patch_size ** 2 * 3)
+        s.pad()
+
+    # ------------------------------------------------------------------------ setup
+    def to(self, device, compute_dtype=torch.float32, seed: int = 0):
+        g = torch.Generator(device=device).manual_seed(seed)
+        self.store.finalize(device, compute_dtype, g)
+        return self
+
+    @property
+    def device(self):
+        return self.store.master.device
+
+    # ------------------------------------------------------------------------ forward
+    def normalize(self, images_u8: torch.Tensor) -> torch.Tensor:
+        """uint8 NCHW -> normalized float32 patches [B, N, p*p*3] (pretraining.py:90-91,113)."""
+        return mae_ops.normalized_patches(images_u8, self.cfg.patch_size)
+
+    def draw_mask(self, batch: int, noise_rng: torch.Generator | None, noise: torch.Tensor | None = None):
+        n = self.cfg.seq_patches
+        if noise is None:
+            shape = (n,) if self.mask_mode == "shared" else (batch, n)
+            noise = torch.rand(shape, generator=noise_rng, device=self.device)
+        return masking_ids(noise, self.cfg.keep_len)
+
+    def forward(self, images_u8: torch.Tensor, rngs: dict | None = None, det: bool = False,
+                noise: torch.Tensor | None = None) -> dict:
+        rngs = rngs or {}
+        cfg = self.cfg
+        B = images_u8.shape[0]
+        C = cfg.num_cls_tokens
+        N, K = cfg.seq_patches, cfg.keep_len
+        patches = self.normalize(images_u8)  # fp32 [B, N, 768]
+        ids_shuffle, ids_restore, ids_keep, mask = self.draw_mask(B, rngs.get("noise"), noise)
+        kept = mae_ops.gather_patches(patches, ids_keep)
+        drop = rngs.get("dropout")
+        x = self.encoder.embed(kept, ids_keep)
+        # encoder always runs with det=False (pretraining.py:92, quirk Q3)
+        x = self.encoder.blocks(x, drop, det=False)
+        h = self.encoder.norm(x)  # [B*(C+K), D]
+        y = self.decoder_proj(h).view(B, C + K, -1)
+        dec_in = mae_ops.unshuffle(y, param_value(self.mask_token).view(-1), ids_restore,
+                                   self.decoder.posemb_table(y.device), C)
+        xd = self.decoder.blocks(dec_in, drop, det=det)
+        hd = self.decoder.dec_norm(xd[:, C:])  # [B*N, d] only patch rows are predicted
+        pred = self.decoder_image_output(hd)  # [B*N, p*p*3]
+        if mask.dim() == 1:
+            mask = mask.unsqueeze(0).expand(B, N)
+        loss = mae_ops.masked_mse(pred.view(B, N, -1), patches, mask, self.norm_pix_loss)
+        return {"loss": loss}
+
+    __call__ = forward
+
+    # ------------------------------------------------------------------------ params
+    def flax_params(self) -> dict:
+        return self.store.to_flax_tree()
+
+    def load_flax_params(self, tree: dict, strict: bool = True):
+        return self.store.load_flax_tree(tree, strict=strict)
+
+
+IMAGENET_MEAN = IMAGENET_DEFAULT_MEAN
+IMAGENET_STD = IMAGENET_DEFAULT_STD

@@ -1,0 +1,282 @@
+"""Flat parameter store: fp32 master / compute-dtype shadow / fp32 gradient in three flat buffers.
+
+Design (MI355X-first, no reference counterpart): every Flax leaf of the reference parameter
+tree is one *segment* of three contiguous device buffers:
+
+* ``master``  fp32, what the optimizer updates (the reference keeps fp32 params),
+* ``shadow``  bf16 copy read by the GEMM / attention kernels; it is rewritten by the fused
+  optimizer kernel in the same pass that updates the master, so no per-step cast kernel is
+  needed (a weight shared by all layers -- the jumbo MLP -- is therefore cast zero times),
+* ``grad``    fp32, written *directly* by the backward kernels (wgrad GEMMs accumulate with
+  beta=1 into it), which makes gradient accumulation across micro-steps and across the L
+  uses of the shared jumbo MLP free, and lets the data-parallel reducer all-reduce contiguous
+  buckets without packing copies.
+
+Segments keep the per-leaf granularity of the Flax tree so that optimizer semantics that are
+per leaf (LAMB / LARS trust ratios, the ``kernel`` weight-decay mask, layer-wise LR decay
+labels) are exactly those of optax on the reference tree.  Storage layout is chosen for the
+kernels (e.g. Dense kernels are stored out x in), and converted to the Flax layout only at
+checkpoint time.  Segments are padded to 64 elements (256 B) so vector kernels never straddle.
+"""
+
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+from typing import Callable, Iterable
+
+import numpy as np
+import torch
+
+ALIGN = 64
+
+
+@dataclass
+class Segment:
+    path: tuple[str, ...]
+    shape: tuple[int, ...]  # storage shape
+    flax_shape: tuple[int, ...]
+    to_flax: Callable[[np.ndarray], np.ndarray]
+    from_flax: Callable[[np.ndarray], np.ndarray]
+    init: Callable[[torch.Generator, tuple[int, ...]], torch.Tensor]
+    offset: int = 0
+    trainable: bool = True
+    use_count: int = 0  # backward uses per step, for the reducer readiness protocol
+
+    @property
+    def numel(self) -> int:
+        return int(math.prod(self.shape))
+
+    @property
+    def key(self) -> str:
+        return "/".join(self.path)
+
+    @property
+    def is_kernel(self) -> bool:
+        """optax mask used by the reference: leaf key == "kernel" (pretraining.py:230)."""
+        return self.path[-1] == "kernel"
+
+
+def identity(a: np.ndarray) -> np.ndarray:
+    return a
+
+
+class Handle:
+    """A view over one or more *adjacent* segments (e.g. wq|wk|wv as one QKV weight)."""
+
+    def __init__(self, store: "ParamStore", segs: list[Segment], shape: tuple[int, ...]):
+        self.store = store
+        self.segs = segs
+        self.shape = shape
+        self.start = segs[0].offset
+        self.numel = int(math.prod(shape))
+        for a, b in zip(segs[:-1], segs[1:]):
+            assert b.offset == a.offset + a.numel, "fused handle segments must be contiguous"
+        assert self.numel == sum(s.numel for s in segs)
+        self._param: torch.nn.Parameter | None = None
+
+    def _view(self, flat: torch.Tensor) -> torch.Tensor:
+        return flat[self.start:self.start + self.numel].view(self.shape)
+
+    @property
+    def master(self) -> torch.Tensor:
+        return self._view(self.store.master)
+
+    @property
+    def shadow(self) -> torch.Tensor:
+        return self._view(self.store.shadow)
+
+    @property
+    def grad(self) -> torch.Tensor:
+        return self._view(self.store.grad)
+
+    @property
+    def param(self) -> torch.nn.Parameter:
+        """Leaf tensor aliasing the master storage; passed to autograd Functions as an input
+        so autograd records the op (its gradient is never returned through autograd)."""
+        if self._param is None or self._param.data_ptr() != self.master.data_ptr():
+            self._param = torch.nn.Parameter(self.master, requires_grad=self.segs[0].trainable)
+        return self._param
+
+    def weight(self) -> torch.Tensor:
+        """Tensor the compute kernels read (bf16 shadow on GPU, master on fp32 runs)."""
+        return self.shadow
+
+    def accumulate_grad(self, g: torch.Tensor) -> None:
+        if not self.segs[0].trainable:
+            return
+        self.grad.add_(g.reshape(self.shape).to(torch.float32))
+        self.store.mark_ready(self)
+
+    def ready(self) -> None:
+        self.store.mark_ready(self)
+
+    def note_use(self) -> None:
+        """Record one differentiable forward use (the reducer expects one ``ready`` per use)."""
+        if self.store.use_hooks and self.segs[0].trainable and torch.is_grad_enabled():
+            for fn in self.store.use_hooks:
+                fn(self)
+
+
+class ParamStore:
+    def __init__(self):
+        self.segments: list[Segment] = []
+        self.by_key: dict[str, Segment] = {}
+        self.master: torch.Tensor | None = None
+        self.shadow: torch.Tensor | None = None
+        self.grad: torch.Tensor | None = None
+        self.total = 0
+        self.finalized = False
+        self.compute_dtype = torch.float32
+        self.hooks: list[Callable[[Handle], None]] = []
+        self.use_hooks: list[Callable[[Handle], None]] = []
+        self._handles: list[Handle] = []
+
+    # ---------------------------------------------------------------- building
+    def add(self, path: Iterable[str], shape: tuple[int, ...], init, flax_shape=None,
+            to_flax=identity, from_flax=identity, trainable: bool = True) -> Segment:
+        assert not self.finalized
+        path = tuple(path)
+        seg = Segment(path=path, shape=tuple(shape), flax_shape=tuple(flax_shape or shape),
+                      to_flax=to_flax, from_flax=from_flax, init=init, trainable=trainable)
+        key = seg.key
+        assert key not in self.by_key, f"duplicate param {key}"
+        seg.offset = self.total
+        self.total += seg.numel
+        self.segments.append(seg)
+        self.by_key[key] = seg
+        return seg
+
+    def pad(self) -> None:
+        """Align the next segment to ALIGN elements (keeps fused handles contiguous otherwise)."""
+        self.total = (self.total + ALIGN - 1) // ALIGN * ALIGN
+
+    def handle(self, segs: list[Segment] | Segment, shape: tuple[int, ...] | None = None) -> Handle:
+        if isinstance(segs, Segment):
+            segs = [segs]
+        h = Handle(self, segs, tuple(shape) if shape is not None else segs[0].shape)
+        self._handles.append(h)
+        return h
+
+    def finalize(self, device, compute_dtype=torch.float32, generator: torch.Generator | None = None) -> None:
+        self.pad()
+        self.compute_dtype = compute_dtype
+        self.master = torch.zeros(self.total, dtype=torch.float32, device=device)
+        self.grad = torch.zeros(self.total, dtype=torch.float32, device=device)
+        if compute_dtype == torch.float32:
+            self.shadow = self.master
+        else:
+            self.shadow = torch.zeros(self.total, dtype=compute_dtype, device=device)
+        self.finalized = True
+        self.initialize(generator)
+
+    def initialize(self, generator: torch.Generator | None = None) -> None:
+        g = generator or torch.Generator().manual_seed(0)
+        with torch.no_grad():
+            for s in self.segments:
+                v = s.init(g, s.shape).to(torch.float32)
+                self.master[s.offset:s.offset + s.numel].copy_(v.reshape(-1))
+        self.sync_shadow()
+
+    def sync_shadow(self) -> None:
+        if self.shadow is not self.master:
+            with torch.no_grad():
+                self.shadow.copy_(self.master)
+
+    # ---------------------------------------------------------------- grads
+    def zero_grad(self) -> None:
+        self.grad.zero_()
+
+    def mark_ready(self, h: Handle) -> None:
+        for fn in self.hooks:
+            fn(h)
+
+    def seg_view(self, flat: torch.Tensor, seg: Segment) -> torch.Tensor:
+        return flat[seg.offset:seg.offset + seg.numel].view(seg.shape)
+
+    # ---------------------------------------------------------------- flax tree IO
+    def to_flax_tree(self, prefix: tuple[str, ...] = ()) -> dict:
+        tree: dict = {}
+        master = self.master.detach().float().cpu().numpy()
+        for s in self.segments:
+            arr = master[s.offset:s.offset + s.numel].reshape(s.shape)
+            arr = np.ascontiguousarray(s.to_flax(arr).astype(np.float32))
+            assert tuple(arr.shape) == s.flax_shape, (s.key, arr.shape, s.flax_shape)
+            node = tree
+            for k in s.path[:-1]:
+                node = node.setdefault(k, {})
+            node[s.path[-1]] = arr
+        return tree
+
+    def load_flax_tree(self, tree: dict, strict: bool = False, subtree: tuple[str, ...] = ()) -> tuple[int, int]:
+        """Copy leaves that exist in ``tree`` (and match shape). Returns (loaded, total)."""
+        loaded = 0
+        total = 0
+        with torch.no_grad():
+            for s in self.segments:
+                if subtree and s.path[:len(subtree)] != subtree:
+                    continue
+                total += 1
+                node = tree
+                ok = True
+                for k in s.path:
+                    if isinstance(node, dict) and k in node:
+                        node = node[k]
+                    else:
+                        ok = False
+                        break
+                if not ok:
+                    if strict:
+                        raise KeyError(s.key)
+                    continue
+                arr = np.asarray(node, dtype=np.float32)
+                if tuple(arr.shape) != s.flax_shape:
+                    if strict:
+                        raise ValueError(f"shape mismatch {s.key}: {arr.shape} vs {s.flax_shape}")
+                    continue
+                v = torch.from_numpy(np.ascontiguousarray(s.from_flax(arr)).reshape(-1))
+                self.master[s.offset:s.offset + s.numel].copy_(v)
+                loaded += 1
+        self.sync_shadow()
+        return loaded, total
+
+    def num_params(self, trainable_only: bool = False) -> int:
+        return sum(s.numel for s in self.segments if (s.trainable or not trainable_only))
+
+
+# ---------------------------------------------------------------------- initializers
+def trunc_normal_(generator: torch.Generator, shape, std: float = 0.02) -> torch.Tensor:
+    """jax.nn.initializers.truncated_normal(0.02): samples N(0,1) truncated to [-2,2], scaled by
+    std / 0.87962566 (the std of the unit truncated normal) so the result has std ``std``."""
+    # inverse-CDF sampling of the truncated normal on the generator's device (deterministic per
+    # seed and device type; ranks are made identical by a broadcast from rank 0)
+    lo, hi = -2.0, 2.0
+    u = torch.rand(tuple(shape), generator=generator, dtype=torch.float64, device=generator.device)
+    a = torch.special.ndtr(torch.tensor(lo, dtype=torch.float64, device=u.device))
+    b = torch.special.ndtr(torch.tensor(hi, dtype=torch.float64, device=u.device))
+    x = torch.special.ndtri(a + u * (b - a))
+    x = x.clamp(lo, hi)
+    return (x * (std / 0.87962566103423978)).to(torch.float32)
+
+
+def zeros_(generator, shape) -> torch.Tensor:
+    return torch.zeros(tuple(shape), dtype=torch.float32)
+
+
+def ones_(generator, shape) -> torch.Tensor:
+    return torch.ones(tuple(shape), dtype=torch.float32)
+
+
+def const_(value: float):
+    def f(generator, shape):
+        return torch.full(tuple(shape), value, dtype=torch.float32)
+    return f
+
+
+def trunc_normal_t(std: float = 0.02):
+    """Initializer for an out x in stored Dense kernel: draw in Flax (in, out) order, then
+    transpose, so a given seed produces the same weights as a Flax-layout draw would."""
+    def f(generator, shape):
+        out, inn = shape[0], int(np.prod(shape[1:]))
+        return trunc_normal_(generator, (inn, out), std).t().contiguous().reshape(shape)
+    return f

@@ -1,0 +1,329 @@
+"""Jumbo ViT encoder, MAE decoder and classification head on the flat ParamStore.
+
+Parity map (reference /root/reference/src/modeling.py):
+  PatchEmbed ............ :106-124  (16x16/16 conv == GEMM over (ph,pw,c)-ordered patches)
+  Attention ............. :127-138  (wq|wk|wv fused into one GEMM over adjacent segments)
+  FeedForward ........... :141-148
+  ViTLayer .............. :150-167  (decoder block)
+  JumboLayer ............ :169-206  (encoder block: CLS tokens -> shared jumbo MLP)
+  LinearCLS ............. :209-219  (SyncBatchNorm + Dense)
+  ViT ................... :221-274  (shared jumbo_mlp built once, passed to every layer)
+  MAEDecoder ............ :276-298
+
+Parameter names/shapes are those of the Flax tree so that checkpoints are
+interchangeable.  MAE mode is *mask-first*: the random permutation is drawn before the patch
+embedding and only the kept patches are embedded (bit-for-bit the same math as embedding all
+196 patches and gathering afterwards, 4x fewer patch-embed FLOPs).
+"""
+
+from __future__ import annotations
+
+import math
+
+import numpy as np
+import torch
+
+from ..config import DecoderConfig, ViTConfig
+from ..ops import functional as Fn
+from ..ops.params_fn import param_value
+from ..utils.posemb import fixed_sincos2d_embeddings
+from .params import Handle, ParamStore, const_, ones_, trunc_normal_, trunc_normal_t, zeros_
+
+
+# ------------------------------------------------------------------------- layout helpers
+def _dense_kernel(store: ParamStore, path, in_shape, out_shape, trainable=True):
+    """Dense/DenseGeneral kernel stored out x in; Flax layout in_shape + out_shape."""
+    fin, fout = int(np.prod(in_shape)), int(np.prod(out_shape))
+    flax_shape = tuple(in_shape) + tuple(out_shape)
+    return store.add(
+        path, (fout, fin), trunc_normal_t(0.02), flax_shape=flax_shape,
+        to_flax=lambda a, fs=flax_shape: a.T.reshape(fs),
+        from_flax=lambda a, fi=fin, fo=fout: a.reshape(fi, fo).T,
+        trainable=trainable,
+    )
+
+
+def _bias(store: ParamStore, path, out_shape, trainable=True):
+    n = int(np.prod(out_shape))
+    return store.add(path, (n,), zeros_, flax_shape=tuple(out_shape),
+                     to_flax=lambda a, s=tuple(out_shape): a.reshape(s),
+                     from_flax=lambda a, n=n: a.reshape(n), trainable=trainable)
+
+
+class Dense:
+    def __init__(self, store, path, in_dim, out_dim, trainable=True):
+        self.k = store.handle(_dense_kernel(store, path + ("kernel",), (in_dim,), (out_dim,), trainable))
+        self.b = store.handle(_bias(store, path + ("bias",), (out_dim,), trainable))
+
+    def __call__(self, x, gelu=False):
+        return Fn.linear(x, self.k, self.b, gelu=gelu)
+
+
+class LayerNorm:
+    def __init__(self, store, path, dim, trainable=True):
+        self.g = store.handle(store.add(path + ("scale",), (dim,), ones_, trainable=trainable))
+        self.b = store.handle(store.add(path + ("bias",), (dim,), zeros_, trainable=trainable))
+
+    def __call__(self, x, out_dtype=None):
+        return Fn.layer_norm(x, self.g, self.b, out_dtype)
+
+
+class FeedForward:
+    """Dense(4*dim) -> gelu(tanh) -> dropout -> Dense(dim) -> dropout (modeling.py:141-148)."""
+
+    def __init__(self, store, path, dim, hidden, dropout=0.0, trainable=True):
+        self.w1 = Dense(store, path + ("w1",), dim, hidden, trainable)
+        self.w2 = Dense(store, path + ("w2",), hidden, dim, trainable)
+        self.dropout = dropout
+
+    def __call__(self, x, rng=None, det=True):
+        h = self.w1(x, gelu=True)
+        h = _dropout(h, self.dropout, rng, det)
+        y = self.w2(h)
+        return _dropout(y, self.dropout, rng, det)
+
+
+class Attention:
+    """Multi-head self-attention; wq|wk|wv are adjacent segments read as one [3D, D] GEMM."""
+
+    def __init__(self, store, path, dim, heads, dropout=0.0, trainable=True):
+        hd = dim // heads
+        self.dim, self.heads, self.dropout = dim, heads, dropout
+        ks = [_dense_kernel(store, path + (n, "kernel"), (dim,), (heads, hd), trainable) for n in ("wq", "wk", "wv")]
+        bs = [_bias(store, path + (n, "bias"), (heads, hd), trainable) for n in ("wq", "wk", "wv")]
+        self.qkv_k = store.handle(ks, (3 * dim, dim))
+        self.qkv_b = store.handle(bs, (3 * dim,))
+        self.wo_k = store.handle(_dense_kernel(store, path + ("wo", "kernel"), (heads, hd), (dim,), trainable))
+        self.wo_b = store.handle(_bias(store, path + ("wo", "bias"), (dim,), trainable))
+
+    def __call__(self, x2d, B, S, rng=None, det=True):
+        qkv = Fn.linear(x2d, self.qkv_k, self.qkv_b).view(B, S, 3 * self.dim)
+        if self.dropout > 0 and not det:
+            o = _attention_with_dropout(qkv, self.heads, self.dropout, rng)
+        else:
+            o = Fn.attention(qkv, self.heads)
+        y = Fn.linear(o.view(B * S, self.dim), self.wo_k, self.wo_b)
+        return _dropout(y, self.dropout, rng, det)
+
+
+def _dropout(x, rate, rng, det):
+    if rate <= 0.0 or det:
+        return x
+    keep = 1.0 - rate
+    m = torch.rand(x.shape, generator=rng, device=x.device) < keep
+    return torch.where(m, x / keep, torch.zeros_like(x))
+
+
+def _attention_with_dropout(qkv, heads, rate, rng):
+    """Rare path (all presets use dropout 0): unfused attention with dropout on the probs."""
+    B, S, three_d = qkv.shape
+    D = three_d // 3
+    hd = D // heads
+    q, k, v = qkv.view(B, S, 3, heads, hd).unbind(2)
+    z = torch.einsum("bqhd,bkhd->bhqk", q.float() / math.sqrt(hd), k.float())
+    p = _dropout(torch.softmax(z, -1), rate, rng, False)
+    return torch.einsum("bhqk,bkhd->bqhd", p, v.float()).reshape(B, S, D).to(qkv.dtype)
+
+
+def droppath_mask(rate: float, batch: int, rng, device, det: bool):
+    """Per-sample keep mask / keep_prob (Flax Dropout with broadcast_dims), or None."""
+    if rate <= 0.0 or det:
+        return None
+    keep = 1.0 - rate
+    m = (torch.rand((batch,), generator=rng, device=device) < keep).float() / keep
+    return m
+
+
+# ---------------------------------------------------------------------------------- blocks
+class JumboLayer:
+    """Encoder block (modeling.py:169-206)."""
+
+    def __init__(self, store, path, cfg: ViTConfig, jumbo_mlp: FeedForward, trainable=True):
+        D, J = cfg.dim, cfg.jumbo_dim
+        self.cfg = cfg
+        self.C = cfg.num_cls_tokens
+        self.attn = Attention(store, path + ("attn",), D, cfg.heads, cfg.dropout, trainable)
+        self.ff = FeedForward(store, path + ("ff",), D, cfg.hidden_dim, cfg.dropout, trainable)
+        self.norm1 = LayerNorm(store, path + ("norm1",), D, trainable)
+        self.norm2 = LayerNorm(store, path + ("norm2",), D, trainable)
+        self.norm3 = LayerNorm(store, path + ("norm3",), J, trainable)
+        self.jumbo_mlp = jumbo_mlp
+        self.scale1 = self.scale2 = self.scale3 = None
+        if cfg.layerscale:
+            self.scale1 = store.handle(store.add(path + ("scale1",), (D,), const_(1e-4), trainable=trainable))
+            self.scale2 = store.handle(store.add(path + ("scale2",), (D,), const_(1e-4), trainable=trainable))
+            self.scale3 = store.handle(store.add(path + ("scale3",), (J,), const_(1e-4), trainable=trainable))
+
+    def __call__(self, x, rng=None, det=True):
+        B, S, D = x.shape
+        C = self.C
+        p = self.cfg.droppath
+        h = self.norm1(x)
+        a = self.attn(h, B, S, rng, det)
+        x = Fn.residual(x, a, self.scale1, droppath_mask(p, B, rng, x.device, det))
+
+        # NB: the jumbo residual is added to the *normalized* CLS token (modeling.py:197-199),
+        # so the CLS stream is re-normalized by norm3 in every layer.
+        cls = x[:, :C].reshape(B, 1, C * D)
+        hc = self.norm3(cls, out_dtype=torch.float32)  # [B, J] fp32 residual base
+        yc = self.jumbo_mlp(hc.to(self.norm3.g.store.compute_dtype), rng, det)
+        xc = Fn.residual(hc.view(B, 1, C * D), yc, self.scale3, droppath_mask(p, B, rng, x.device, det))
+
+        pt = x[:, C:]
+        hp = self.norm2(pt)
+        yp = self.ff(hp, rng, det)
+        xp = Fn.residual(pt, yp, self.scale2, droppath_mask(p, B, rng, x.device, det))
+        return torch.cat([xc.view(B, C, D), xp], 1)
+
+
+class ViTLayer:
+    """Standard pre-LN block used by the MAE decoder (modeling.py:150-167)."""
+
+    def __init__(self, store, path, dim, heads, layerscale, dropout, droppath, trainable=True):
+        self.attn = Attention(store, path + ("attn",), dim, heads, dropout, trainable)
+        self.ff = FeedForward(store, path + ("ff",), dim, 4 * dim, dropout, trainable)
+        self.norm1 = LayerNorm(store, path + ("norm1",), dim, trainable)
+        self.norm2 = LayerNorm(store, path + ("norm2",), dim, trainable)
+        self.droppath = droppath
+        self.scale1 = self.scale2 = None
+        if layerscale:
+            self.scale1 = store.handle(store.add(path + ("scale1",), (dim,), const_(1e-4), trainable=trainable))
+            self.scale2 = store.handle(store.add(path + ("scale2",), (dim,), const_(1e-4), trainable=trainable))
+
+    def __call__(self, x, rng=None, det=True):
+        B, S, D = x.shape
+        h = self.norm1(x)
+        a = self.attn(h, B, S, rng, det)
+        x = Fn.residual(x, a, self.scale1, droppath_mask(self.droppath, B, rng, x.device, det))
+        h = self.norm2(x)
+        f = self.ff(h, rng, det)
+        return Fn.residual(x, f, self.scale2, droppath_mask(self.droppath, B, rng, x.device, det))
+
+
+# ------------------------------------------------------------------------------ encoder
+class JumboViT:
+    """Jumbo ViT encoder (modeling.py:221-274).  Segments are allocated so that the flat
+    buffer order is the reverse of backward readiness (good all-reduce buckets)."""
+
+    def __init__(self, store: ParamStore, cfg: ViTConfig, prefix=("model",), trainable=True):
+        self.cfg = cfg
+        D, p, g = cfg.dim, cfg.patch_size, cfg.grid
+        P = prefix
+        # embed/wte: HWIO (p,p,3,D) == GEMM kernel [(ph,pw,c), D], stored D x (p*p*3)
+        self.wte_k = store.handle(_dense_kernel(store, P + ("embed", "wte", "kernel"), (p, p, 3), (D,), trainable))
+        self.wte_b = store.handle(_bias(store, P + ("embed", "wte", "bias"), (D,), trainable))
+        self.wpe = None
+        if cfg.posemb == "learnable":
+            self.wpe = store.handle(store.add(P + ("embed", "wpe"), (g * g, D), trunc_normal_,
+                                              flax_shape=(g, g, D),
+                                              to_flax=lambda a, s=(g, g, D): a.reshape(s),
+                                              from_flax=lambda a, n=g * g, d=D: a.reshape(n, d),
+                                              trainable=trainable))
+        self.cls_tokens = store.handle(store.add(P + ("cls_tokens",), (1, cfg.num_cls_tokens, D), zeros_,
+                                                 trainable=trainable))
+        self.jumbo_mlp = FeedForward(store, P + ("jumbo_mlp",), cfg.jumbo_dim, 4 * cfg.jumbo_dim,
+                                     cfg.dropout, trainable)
+        store.pad()
+        self.layers = []
+        for i in range(cfg.layers):
+            self.layers.append(JumboLayer(store, P + (f"layer_{i}",), cfg, self.jumbo_mlp, trainable))
+            store.pad()
+        self.norm = LayerNorm(store, P + ("norm",), D, trainable)
+        store.pad()
+        self._posemb_cache = {}
+
+    def posemb_table(self, device) -> torch.Tensor | None:
+        """Constant sincos table [g*g, D] (fp32), or None for learnable posemb."""
+        if self.cfg.posemb != "sincos2d":
+            return None
+        key = str(device)
+        if key not in self._posemb_cache:
+            g = self.cfg.grid
+            self._posemb_cache[key] = fixed_sincos2d_embeddings(g, g, self.cfg.dim, device).reshape(g * g, -1)
+        return self._posemb_cache[key]
+
+    def embed(self, patches: torch.Tensor, ids: torch.Tensor | None) -> torch.Tensor:
+        """patches: [B, n, p*p*3] normalized pixels (already gathered at ``ids`` when given).
+        Returns [B, C + n, D] fp32 residual stream."""
+        B, n, K = patches.shape
+        dt = self.wte_k.store.compute_dtype
+        e = Fn.linear(patches.reshape(B * n, K).to(dt), self.wte_k, self.wte_b).float().view(B, n, -1)
+        if self.wpe is not None:
+            pos = param_value(self.wpe)
+        else:
+            pos = self.posemb_table(patches.device)
+        if ids is not None:
+            pos = pos[ids] if ids.dim() == 1 else pos[ids]
+        e = e + pos
+        cls = param_value(self.cls_tokens).expand(B, -1, -1)
+        return torch.cat([cls, e], 1)
+
+    def blocks(self, x: torch.Tensor, rng=None, det=True) -> torch.Tensor:
+        x = _dropout(x, self.cfg.dropout, rng, det)
+        for layer in self.layers:
+            if self.cfg.grad_ckpt and torch.is_grad_enabled():
+                x = torch.utils.checkpoint.checkpoint(layer, x, rng, det, use_reentrant=False)
+            else:
+                x = layer(x, rng, det)
+        return x
+
+
+class MAEDecoder:
+    """MAE decoder (modeling.py:276-298); fixed sincos posemb on patch tokens only."""
+
+    def __init__(self, store: ParamStore, cfg: DecoderConfig, prefix=("decoder_model",)):
+        self.cfg = cfg
+        self.layers = []
+        for i in range(cfg.dec_layers):
+            self.layers.append(ViTLayer(store, prefix + (f"dec_layer_{i}",), cfg.dec_dim, cfg.dec_heads,
+                                        cfg.dec_layerscale, cfg.dec_dropout, cfg.dec_droppath))
+            store.pad()
+        self.dec_norm = LayerNorm(store, prefix + ("dec_norm",), cfg.dec_dim)
+        store.pad()
+        self._posemb_cache = {}
+
+    def posemb_table(self, device) -> torch.Tensor:
+        key = str(device)
+        if key not in self._posemb_cache:
+            g = self.cfg.grid
+            self._posemb_cache[key] = fixed_sincos2d_embeddings(g, g, self.cfg.dec_dim, device).reshape(g * g, -1)
+        return self._posemb_cache[key]
+
+    def blocks(self, x, rng=None, det=True):
+        for layer in self.layers:
+            if self.cfg.grad_ckpt and torch.is_grad_enabled():
+                x = torch.utils.checkpoint.checkpoint(layer, x, rng, det, use_reentrant=False)
+            else:
+                x = layer(x, rng, det)
+        return x
+
+
+# --------------------------------------------------------------------------------- heads
+class LinearCLS:
+    """[SyncBatchNorm] -> Dense(labels) on the 3*D jumbo token (modeling.py:209-219)."""
+
+    def __init__(self, store: ParamStore, path, dim: int, labels: int, batch_norm: bool):
+        self.batch_norm = batch_norm
+        self.bn_scale = self.bn_bias = None
+        if batch_norm:
+            self.bn_scale = store.handle(store.add(path + ("BatchNorm_0", "scale"), (dim,), ones_))
+            self.bn_bias = store.handle(store.add(path + ("BatchNorm_0", "bias"), (dim,), zeros_))
+        self.dense = Dense(store, path + ("Dense_0",), dim, labels)
+        store.pad()
+        self.dim = dim
+        # Flax BatchNorm running statistics (collection "batch_stats")
+        self.running_mean: torch.Tensor | None = None
+        self.running_var: torch.Tensor | None = None
+
+    def init_stats(self, device):
+        if self.batch_norm:
+            self.running_mean = torch.zeros(self.dim, device=device)
+            self.running_var = torch.ones(self.dim, device=device)
+
+    def __call__(self, x: torch.Tensor, det: bool, group=None) -> torch.Tensor:
+        if self.batch_norm:
+            from ..parallel.syncbn import sync_batch_norm
+            x = sync_batch_norm(x, self.bn_scale, self.bn_bias, self.running_mean, self.running_var,
+                                training=not det, momentum=0.99, eps=1e-5, group=group)
+        dt = self.dense.k.store.compute_dtype
+        return self.dense(x.to(dt)).float()

@@ -1,0 +1,211 @@
+"""Fused optimizers over the flat parameter store, with optax semantics.
+
+Parity (reference):
+  adamw  = optax.adamw(lr, b1, b2, eps, weight_decay, mask=kernel)      pretraining.py:223-233
+  lamb   = modified_lamb: scale_by_adam -> add_decayed_weights(mask) ->
+           masked(scale_by_trust_ratio, mask) -> scale_by_lr            utils.py:124-139
+  lars   = optax.lars(lr, momentum=0.9): add_decayed_weights(0) ->
+           scale_by_trust_ratio(0.001) -> scale_by_lr -> trace(0.9)      finetuning.py:230-234
+  sgd    = optax.sgd(lr, momentum=0.9): trace(0.9) -> scale_by_lr       finetuning.py:225-229
+  LLRD   = chain(tx, multi_transform(scale(lr_decay**(L-i)), label))   pretraining.py:234-241
+  clip   = chain(clip_by_global_norm(c), tx)                            pretraining.py:242-243
+  LR     = inject_hyperparams(schedule)(count), count from 0            pretraining.py:221-259
+
+Execution: on the GPU every optimizer is ONE fused pass over the flat fp32 master / grad /
+moment buffers driven by a chunk table (multi-tensor apply), which also rewrites the bf16
+shadow weights; LAMB/LARS add one per-segment norm pass (trust ratios are per Flax leaf,
+exactly like optax on the reference tree).  Per-step scalars (lr, bias corrections, clip
+factor) live in a small device tensor so the step is HIP-graph capturable.  The torch path
+(CPU) implements the same math with per-element metadata vectors.
+"""
+
+from __future__ import annotations
+
+import re
+
+import torch
+
+from ..models.params import ParamStore
+from ..ops import _ext
+from .schedule import WarmupCosine
+
+CHUNK = 65536  # elements per chunk of the multi-tensor table
+
+
+def layer_index(path: tuple[str, ...], num_layers: int) -> int:
+    """get_layer_index_fn (/root/reference/src/utils.py:142-147)."""
+    if path[0] == "model" and len(path) > 1 and path[1].startswith("layer_"):
+        return int(re.match(r"layer_(\d+)", path[1]).group(1)) + 1
+    if path[0] == "model" and len(path) > 1 and path[1] == "embed":
+        return 0
+    return num_layers
+
+
+class FlatOptimizer:
+    KINDS = ("adamw", "lamb", "lars", "sgd")
+
+    def __init__(self, store: ParamStore, kind: str, schedule: WarmupCosine, *, b1=0.9, b2=0.999,
+                 eps=1e-8, weight_decay=0.0, lr_decay=1.0, num_layers=12, clip_grad=0.0,
+                 momentum=0.9, trust_coefficient=0.001):
+        assert kind in self.KINDS, kind
+        self.store, self.kind, self.schedule = store, kind, schedule
+        self.b1, self.b2, self.eps = b1, b2, eps
+        self.weight_decay = weight_decay if kind in ("adamw", "lamb") else 0.0
+        self.lr_decay, self.num_layers = lr_decay, num_layers
+        self.clip_grad = clip_grad
+        self.momentum, self.trust_coefficient = momentum, trust_coefficient
+        self.count = 0  # optax inject_hyperparams count (host mirror)
+        self.last_lr = schedule(0)
+        dev = store.master.device
+        n = store.total
+        segs = store.segments
+        self.nseg = len(segs)
+        # ---- per-segment metadata: [decay flag, llrd scale, trust flag]
+        meta = torch.zeros(self.nseg, 4, dtype=torch.float32)
+        for i, s in enumerate(segs):
+            decay = 1.0 if (s.is_kernel and self.weight_decay > 0) else 0.0
+            llrd = lr_decay ** (num_layers - layer_index(s.path, num_layers)) if lr_decay < 1.0 else 1.0
+            trust = 1.0 if (kind == "lars" or (kind == "lamb" and s.is_kernel)) else 0.0
+            meta[i] = torch.tensor([decay, llrd, trust, 1.0 if s.trainable else 0.0])
+        self.meta = meta.to(dev)
+        # ---- chunk table for the multi-tensor kernels: [start, length, segment]
+        rows = []
+        for i, s in enumerate(segs):
+            for st in range(0, s.numel, CHUNK):
+                rows.append((s.offset + st, min(CHUNK, s.numel - st), i))
+        self.chunks = torch.tensor(rows, dtype=torch.int64).to(torch.int32).to(dev)
+        # ---- state
+        self.mu = torch.zeros(n, dtype=torch.float32, device=dev) if kind in ("adamw", "lamb") else None
+        self.nu = torch.zeros(n, dtype=torch.float32, device=dev) if kind in ("adamw", "lamb") else None
+        self.trace = torch.zeros(n, dtype=torch.float32, device=dev) if kind in ("lars", "sgd") else None
+        self.hyper = torch.zeros(8, dtype=torch.float32, device=dev)
+        self.norms = torch.zeros(self.nseg, 2, dtype=torch.float32, device=dev)
+        self.gnorm_sq = torch.zeros(1, dtype=torch.float32, device=dev)
+        self._tmp = None
+        self._torch_meta = None
+
+    # ---------------------------------------------------------------- helpers
+    def _elem_meta(self):
+        """Per-element metadata for the torch path (built lazily)."""
+        if self._torch_meta is None:
+            s = self.store
+            seg_id = torch.zeros(s.total, dtype=torch.int64, device=s.master.device)
+            valid = torch.zeros(s.total, dtype=torch.bool, device=s.master.device)
+            for i, seg in enumerate(s.segments):
+                seg_id[seg.offset:seg.offset + seg.numel] = i
+                valid[seg.offset:seg.offset + seg.numel] = True
+            m = self.meta[seg_id]
+            self._torch_meta = (seg_id, valid, m[:, 0], m[:, 1], m[:, 2] > 0, m[:, 3] > 0)
+        return self._torch_meta
+
+    def _seg_norm_sq(self, x: torch.Tensor, seg_id: torch.Tensor, valid: torch.Tensor) -> torch.Tensor:
+        out = torch.zeros(self.nseg, dtype=torch.float32, device=x.device)
+        out.index_add_(0, seg_id[valid], (x[valid] * x[valid]))
+        return out
+
+    # ---------------------------------------------------------------- step
+    def step(self) -> float:
+        """Apply one optimizer update from ``store.grad``; returns the learning rate used."""
+        lr = float(self.schedule(self.count))
+        t = self.count + 1
+        bc1 = 1.0 - self.b1 ** t
+        bc2 = 1.0 - self.b2 ** t
+        s = self.store
+        if s.master.is_cuda and _ext.use_hip(s.master):
+            self._step_hip(lr, bc1, bc2)
+        else:
+            self._step_torch(lr, bc1, bc2)
+        self.count += 1
+        self.last_lr = lr
+        return lr
+
+    def _clip_scale_torch(self, g: torch.Tensor) -> torch.Tensor:
+        if self.clip_grad <= 0:
+            return torch.ones((), device=g.device)
+        gn = torch.sqrt((g * g).sum())
+        return torch.where(gn < self.clip_grad, torch.ones_like(gn), self.clip_grad / gn)
+
+    @torch.no_grad()
+    def _step_torch(self, lr, bc1, bc2):
+        s = self.store
+        p, g = s.master, s.grad
+        seg_id, valid, decay, llrd, trust_m, trainable = self._elem_meta()
+        g = g * self._clip_scale_torch(g)
+        if self.kind in ("adamw", "lamb"):
+            self.mu.mul_(self.b1).add_((1 - self.b1) * g)
+            self.nu.mul_(self.b2).add_((1 - self.b2) * g * g)
+            u = (self.mu / bc1) / (torch.sqrt(self.nu / bc2) + self.eps)
+            u = u + self.weight_decay * decay * p
+            if self.kind == "lamb":
+                pn = torch.sqrt(self._seg_norm_sq(p, seg_id, valid))
+                un = torch.sqrt(self._seg_norm_sq(u, seg_id, valid))
+                tr = pn / un
+                tr = torch.where((pn == 0) | (un == 0), torch.ones_like(tr), tr)
+                u = torch.where(trust_m, u * tr[seg_id], u)
+            upd = -lr * u * llrd
+        elif self.kind == "lars":
+            u = g  # weight_decay 0 (reference passes none)
+            pn = torch.sqrt(self._seg_norm_sq(p, seg_id, valid))
+            un = torch.sqrt(self._seg_norm_sq(u, seg_id, valid))
+            tr = self.trust_coefficient * pn / un
+            tr = torch.where((pn == 0) | (un == 0), torch.ones_like(tr), tr)
+            u = u * tr[seg_id]
+            u = -lr * u
+            self.trace.mul_(self.momentum).add_(u)
+            upd = self.trace * llrd
+        else:  # sgd
+            self.trace.mul_(self.momentum).add_(g)
+            upd = -lr * self.trace * llrd
+        upd = torch.where(trainable & valid, upd, torch.zeros_like(upd))
+        p.add_(upd)
+        s.sync_shadow()
+
+    @torch.no_grad()
+    def _step_hip(self, lr, bc1, bc2):
+        ext = _ext.load()
+        s = self.store
+        shadow = s.shadow if s.shadow is not s.master else None
+        # hyper = [lr, bc1, bc2, clip, b1, b2, eps, wd]
+        self.hyper.copy_(torch.tensor([lr, bc1, bc2, self.clip_grad, self.b1, self.b2, self.eps,
+                                       self.weight_decay], dtype=torch.float32), non_blocking=True)
+        if self.clip_grad > 0:
+            self.gnorm_sq.zero_()
+            ext.opt_sumsq(s.grad, self.chunks, self.gnorm_sq)
+        else:
+            self.gnorm_sq.fill_(-1.0)
+        if self.kind == "adamw":
+            ext.opt_adamw(s.master, s.grad, self.mu, self.nu, shadow, self.chunks, self.meta,
+                          self.hyper, self.gnorm_sq)
+        elif self.kind == "lamb":
+            if self._tmp is None:
+                self._tmp = torch.empty_like(s.master)
+            self.norms.zero_()
+            ext.opt_lamb_phase1(s.master, s.grad, self.mu, self.nu, self._tmp, self.chunks, self.meta,
+                                self.hyper, self.gnorm_sq, self.norms)
+            ext.opt_apply_trust(s.master, self._tmp, None, shadow, self.chunks, self.meta, self.hyper,
+                                self.norms, self.gnorm_sq, 0, 0.0, 1.0)
+        elif self.kind == "lars":
+            self.norms.zero_()
+            ext.opt_lars_norms(s.master, s.grad, self.chunks, self.hyper, self.gnorm_sq, self.norms)
+            ext.opt_apply_trust(s.master, s.grad, self.trace, shadow, self.chunks, self.meta, self.hyper,
+                                self.norms, self.gnorm_sq, 1, self.momentum, self.trust_coefficient)
+        else:
+            ext.opt_sgd(s.master, s.grad, self.trace, shadow, self.chunks, self.meta, self.hyper,
+                        self.gnorm_sq, self.momentum)
+
+    # ---------------------------------------------------------------- state io
+    def state_dict(self) -> dict:
+        d = {"kind": self.kind, "count": self.count}
+        for k in ("mu", "nu", "trace"):
+            v = getattr(self, k)
+            if v is not None:
+                d[k] = v.detach().cpu()
+        return d
+
+    def load_state_dict(self, d: dict) -> None:
+        assert d["kind"] == self.kind
+        self.count = int(d["count"])
+        for k in ("mu", "nu", "trace"):
+            if k in d and getattr(self, k) is not None:
+                getattr(self, k).copy_(d[k])
+        self.last_lr = self.schedule(max(self.count - 1, 0))

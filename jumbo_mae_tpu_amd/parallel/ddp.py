@@ -1,0 +1,146 @@
+"""Data-parallel gradient reducer over the flat fp32 gradient buffer, overlapped with backward.
+
+Reference: ``jax.lax.pmean(grads, axis_name="batch")`` inside the pmap'd training step
+(/root/reference/src/pretraining.py:150, finetuning.py:144).
+
+MI355X design:
+* The gradient buffer is ONE contiguous fp32 allocation whose segment order is the reverse of
+  backward readiness (models build params in forward order).  Buckets are contiguous slices
+  cut from the end of the buffer, so bucket k becomes complete while backward is still
+  computing bucket k+1 -- no packing copies, RCCL reduces the buffer in place.
+* Readiness is counted per segment: every forward use of a parameter bumps its pending count,
+  every backward write decrements it (``Handle.ready``), so a weight shared by all layers --
+  the jumbo MLP -- is reduced only after its last (layer-0) contribution.
+* When a bucket is complete its ``all_reduce(AVG)`` is issued asynchronously on RCCL's stream;
+  ``finish()`` waits for all of them (and flushes buckets that had unused segments).
+* Bucket size defaults to 64 MiB: large enough for the ring's bandwidth regime on xGMI
+  (7 links x ~150 GB/s per MI355X), small enough that the first bucket starts early.
+* With ``grad_accum > 1`` call ``set_sync(False)`` on the non-final micro-steps (no-sync
+  accumulation, CC2).
+"""
+
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+from ..models.params import Handle, ParamStore
+from . import dist as pdist
+
+
+class GradReducer:
+    def __init__(self, store: ParamStore, group=None, bucket_mb: float = 64.0, overlap: bool = True,
+                 reduce_dtype: torch.dtype = torch.float32, seg_filter=None):
+        self.store = store
+        self.group = group
+        self.world = dist.get_world_size(group) if (dist.is_available() and dist.is_initialized()) else 1
+        self.enabled = self.world > 1
+        self.overlap = overlap and self.enabled
+        self.sync = True
+        self.reduce_dtype = reduce_dtype
+        segs = [s for s in store.segments if s.trainable and (seg_filter is None or seg_filter(s))]
+        self.seg_index = {id(s): i for i, s in enumerate(segs)}
+        # -------- buckets from the end of the flat buffer
+        limit = int(bucket_mb * 1024 * 1024 / 4)
+        buckets: list[list[int]] = []
+        cur: list[int] = []
+        size = 0
+        for i in range(len(segs) - 1, -1, -1):
+            s = segs[i]
+            if cur and size + s.numel > limit:
+                buckets.append(cur)
+                cur, size = [], 0
+            cur.append(i)
+            size += s.numel
+        if cur:
+            buckets.append(cur)
+        self.segs = segs
+        self.buckets = []
+        self.seg_bucket = [0] * len(segs)
+        for bi, idxs in enumerate(buckets):
+            lo = min(segs[i].offset for i in idxs)
+            hi = max(segs[i].offset + segs[i].numel for i in idxs)
+            self.buckets.append((lo, hi, idxs))
+            for i in idxs:
+                self.seg_bucket[i] = bi
+        self.pending_uses = [0] * len(segs)
+        self.bucket_left = [len(b[2]) for b in self.buckets]
+        self.launched = [False] * len(self.buckets)
+        self.works = []
+        self._compressed = {}
+        if self.enabled:
+            store.hooks.append(self._on_ready)
+            store.use_hooks.append(self._on_use)
+
+    # ---------------------------------------------------------------- protocol
+    def set_sync(self, sync: bool) -> None:
+        self.sync = sync
+
+    def begin_step(self) -> None:
+        self.pending_uses = [0] * len(self.segs)
+        self.bucket_left = [len(b[2]) for b in self.buckets]
+        self.launched = [False] * len(self.buckets)
+        self.works = []
+
+    def _on_use(self, h: Handle) -> None:
+        for s in h.segs:
+            i = self.seg_index.get(id(s))
+            if i is not None:
+                self.pending_uses[i] += 1
+
+    def _on_ready(self, h: Handle) -> None:
+        if not (self.overlap and self.sync):
+            return
+        for s in h.segs:
+            i = self.seg_index.get(id(s))
+            if i is None:
+                continue
+            self.pending_uses[i] -= 1
+            if self.pending_uses[i] == 0:
+                b = self.seg_bucket[i]
+                self.bucket_left[b] -= 1
+                if self.bucket_left[b] == 0:
+                    self._launch(b)
+
+    def _launch(self, b: int) -> None:
+        if self.launched[b]:
+            return
+        self.launched[b] = True
+        lo, hi, _ = self.buckets[b]
+        view = self.store.grad[lo:hi]
+        if self.reduce_dtype != torch.float32:
+            buf = view.to(self.reduce_dtype)
+            self._compressed[b] = buf
+            w = self._allreduce(buf)
+        else:
+            w = self._allreduce(view)
+        self.works.append((b, w))
+
+    def _allreduce(self, t: torch.Tensor):
+        if dist.get_backend(self.group) == "nccl":
+            return dist.all_reduce(t, op=dist.ReduceOp.AVG, group=self.group, async_op=True)
+        w = dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+        return (w, t)
+
+    def finish(self) -> None:
+        """Launch any bucket not yet reduced (unused segments / no overlap) and wait for all."""
+        if not self.enabled or not self.sync:
+            return
+        for b in range(len(self.buckets)):
+            if not self.launched[b]:
+                self._launch(b)
+        for b, w in self.works:
+            if isinstance(w, tuple):
+                w[0].wait()
+                w[1].div_(self.world)
+            else:
+                w.wait()
+            if b in self._compressed:
+                lo, hi, _ = self.buckets[b]
+                self.store.grad[lo:hi].copy_(self._compressed.pop(b))
+        self.works = []
+
+    def stats(self) -> dict:
+        sizes = [(hi - lo) * 4 / 2**20 for lo, hi, _ in self.buckets]
+        return {"buckets": len(self.buckets), "bucket_mb_max": max(sizes) if sizes else 0.0,
+                "bucket_mb_min": min(sizes) if sizes else 0.0}

@@ -1,0 +1,60 @@
+"""Data-parallel train / eval step engine.
+
+Reference: the pmap'd ``training_step`` / ``validation_step`` (/root/reference/src/pretraining.py:
+125-167, finetuning.py:109-165).  One step = zero the flat grad buffer, run ``grad_accum``
+micro-steps (forward, backward with the gradient writes fused into the backward kernels,
+RCCL bucket all-reduce overlapped with the last micro-step's backward), one fused optimizer
+pass.  Metrics stay on the device; they are averaged over ranks lazily when logged (the
+reference pmean's them every step, CC3, which is a blocking host round trip we avoid).
+"""
+
+from __future__ import annotations
+
+import torch
+
+from ..optim.flat import FlatOptimizer
+from ..parallel.ddp import GradReducer
+from ..utils.rng import RngStreams
+
+
+class Trainer:
+    def __init__(self, model, optimizer: FlatOptimizer, reducer: GradReducer | None = None,
+                 rngs: RngStreams | None = None, grad_accum: int = 1):
+        self.model = model
+        self.opt = optimizer
+        self.reducer = reducer
+        self.rngs = rngs
+        self.grad_accum = grad_accum
+
+    @property
+    def store(self):
+        return self.model.store
+
+    def train_step(self, micro_batches) -> dict:
+        """micro_batches: list (len grad_accum) of argument tuples for ``model.forward``."""
+        n = len(micro_batches)
+        self.store.zero_grad()
+        if self.reducer is not None:
+            self.reducer.begin_step()
+        metrics_acc = None
+        rng = self.rngs.as_dict() if self.rngs is not None else {}
+        for i, args in enumerate(micro_batches):
+            if self.reducer is not None:
+                self.reducer.set_sync(i == n - 1)
+            out = self.model(*args, rngs=rng, det=False)
+            loss = out["loss"]
+            (loss / n).backward()
+            m = {k: v.detach().float() for k, v in out.items()}
+            metrics_acc = m if metrics_acc is None else {k: metrics_acc[k] + m[k] for k in m}
+        if self.reducer is not None:
+            self.reducer.set_sync(True)
+            self.reducer.finish()
+        lr = self.opt.step()
+        metrics = {k: v / n for k, v in metrics_acc.items()}
+        metrics["learning_rate"] = lr
+        return metrics
+
+    @torch.no_grad()
+    def eval_step(self, args) -> dict:
+        rng = self.rngs.as_dict() if self.rngs is not None else {}
+        return self.model.evaluate(*args, rngs=rng)
