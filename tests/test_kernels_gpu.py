@@ -150,8 +150,13 @@ def test_optimizer_hip_matches_torch(kind, clip):
     dc = DecoderConfig(dec_layers=1, dec_dim=32, dec_heads=2, image_size=32, patch_size=8)
     sched = warmup_cosine_decay_schedule(1e-6, 1e-2, 3, 10, 1e-5)
     res = []
+    init = None
     for dev, dt in (("cuda", torch.bfloat16), ("cpu", torch.float32)):
         m = PretrainModel(vc, dc).to(dev, dt, seed=0)
+        if init is None:
+            init = m.store.master.cpu().clone()
+        m.store.master.copy_(init)
+        m.store.sync_shadow()
         opt = FlatOptimizer(m.store, kind, sched, b1=0.9, b2=0.95, eps=1e-8, weight_decay=0.05,
                             lr_decay=0.75, num_layers=2, clip_grad=clip)
         gen = torch.Generator().manual_seed(1)
