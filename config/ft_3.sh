@@ -1,0 +1,3 @@
+#!/usr/bin/env bash
+# ft.sh sweep point: learning rate 1.0e-3, color jitter 0.3.
+LR=1.0e-3 COLOR_JITTER=0.3 NAME=ft_3 exec "$(dirname "$0")/ft.sh" "$@"

@@ -1,0 +1,8 @@
+#!/usr/bin/env bash
+# Finetune grid: weight decay {0.08, 0.09} x learning rate {1e-3, 3e-3}, layer decay 0.65.
+for wd in 0.08 0.09; do
+  for lr in 1e-3 3e-3; do
+    echo "Running with weight_decay=${wd}, learning_rate=${lr}"
+    WD=$wd LR=$lr LR_DECAY=0.65 NAME="loop_2_wd${wd}_lr${lr}" bash "$(dirname "$0")/ft.sh" "$@"
+  done
+done

@@ -1,0 +1,197 @@
+"""Checkpoint IO: async params writer, resume sidecar, pretrained-param loading.
+
+Reference:
+  save_checkpoint_in_background ... /root/reference/src/utils.py:55-63 (a bare thread per save,
+                                    writing ``{output_dir}/{name}-{postfix}.msgpack`` via gopen)
+  load_pretrained_params .......... /root/reference/src/utils.py:150-202
+  save sites ...................... main_pretrain.py:77-90 (``last`` every eval, ``best`` on
+                                    improvement)
+Changes by design:
+  * ONE writer thread with a FIFO queue and write-to-temp + atomic rename: two saves of the same
+    file can no longer interleave, and a crash never leaves a torn checkpoint.
+  * a ``{name}-{postfix}.state.pt`` sidecar with optimizer moments, step, RNG streams,
+    BatchNorm running stats and data position enables ``--resume`` (the reference has none).
+  * ``load_pretrained_params`` implements the intended behaviour (quirk Q6): it loads the
+    pretrained ``model/*`` encoder subtree into the freshly initialised finetune tree, keeps the
+    new head, and can resize a learnable position table.
+"""
+
+from __future__ import annotations
+
+import os
+import queue
+import subprocess
+import threading
+
+import numpy as np
+
+from .msgpack_flax import msgpack_restore, msgpack_serialize
+
+
+# ------------------------------------------------------------------------------ gopen
+def read_bytes(url: str) -> bytes:
+    """Local path, ``file://``, or ``pipe:<cmd>`` (stdout of a shell command, e.g. gsutil cat)."""
+    if url.startswith("pipe:"):
+        return subprocess.run(url[5:], shell=True, check=True, capture_output=True).stdout
+    if url.startswith("file://"):
+        url = url[7:]
+    with open(url, "rb") as f:
+        return f.read()
+
+
+def write_bytes(url: str, data: bytes) -> None:
+    if url.startswith("pipe:"):
+        subprocess.run(url[5:], shell=True, check=True, input=data)
+        return
+    if url.startswith("file://"):
+        url = url[7:]
+    d = os.path.dirname(url)
+    if d:
+        os.makedirs(d, exist_ok=True)
+    tmp = f"{url}.tmp.{os.getpid()}"
+    with open(tmp, "wb") as f:
+        f.write(data)
+        f.flush()
+        os.fsync(f.fileno())
+    os.replace(tmp, url)
+
+
+# ------------------------------------------------------------------------------ writer
+class AsyncCheckpointWriter:
+    """Single background writer thread; ``submit`` returns immediately."""
+
+    def __init__(self):
+        self.q: queue.Queue = queue.Queue()
+        self.errors: list[BaseException] = []
+        self.t = threading.Thread(target=self._run, name="ckpt-writer", daemon=True)
+        self.t.start()
+
+    def _run(self):
+        while True:
+            item = self.q.get()
+            if item is None:
+                self.q.task_done()
+                return
+            url, payload = item
+            try:
+                data = payload() if callable(payload) else payload
+                write_bytes(url, data)
+            except BaseException as e:  # pragma: no cover - surfaced by flush()
+                self.errors.append(e)
+            finally:
+                self.q.task_done()
+
+    def submit(self, url: str, payload) -> None:
+        self.q.put((url, payload))
+
+    def flush(self) -> None:
+        self.q.join()
+        if self.errors:
+            raise self.errors.pop(0)
+
+    def close(self) -> None:
+        self.flush()
+        self.q.put(None)
+        self.t.join(timeout=60)
+
+
+_WRITER: AsyncCheckpointWriter | None = None
+
+
+def writer() -> AsyncCheckpointWriter:
+    global _WRITER
+    if _WRITER is None:
+        _WRITER = AsyncCheckpointWriter()
+    return _WRITER
+
+
+def ckpt_path(output_dir: str, name: str, postfix: str, ext: str = "msgpack") -> str:
+    return os.path.join(output_dir, f"{name}-{postfix}.{ext}")
+
+
+def save_checkpoint_in_background(output_dir: str, name: str, params_bytes: bytes, postfix: str = "last") -> str:
+    url = ckpt_path(output_dir, name, postfix)
+    writer().submit(url, params_bytes)
+    return url
+
+
+def save_params(output_dir: str, name: str, tree: dict, postfix: str = "last") -> str:
+    return save_checkpoint_in_background(output_dir, name, msgpack_serialize(tree), postfix)
+
+
+def load_params(url: str) -> dict:
+    return msgpack_restore(read_bytes(url))
+
+
+# ------------------------------------------------------------------------------ resume
+def save_resume_state(path: str, state: dict) -> None:
+    import io
+
+    import torch
+
+    buf = io.BytesIO()
+    torch.save(state, buf)
+    writer().submit(path, buf.getvalue())
+
+
+def load_resume_state(path: str) -> dict:
+    import io
+
+    import torch
+
+    return torch.load(io.BytesIO(read_bytes(path)), map_location="cpu", weights_only=True)
+
+
+# ------------------------------------------------------------------------------ pretrained
+def _resize_posemb(arr: np.ndarray, shape) -> np.ndarray:
+    """Bicubic resize of a (g, g, D) learnable table to ``shape`` (finetune at a new resolution)."""
+    import torch
+    import torch.nn.functional as F
+
+    t = torch.from_numpy(np.asarray(arr, dtype=np.float32)).permute(2, 0, 1)[None]
+    t = F.interpolate(t, size=tuple(shape[:2]), mode="bicubic", align_corners=False)
+    return t[0].permute(1, 2, 0).numpy()
+
+
+def load_pretrained_params(url: str, params: dict, log=print) -> dict:
+    """Merge the ``model`` subtree of a pretrained checkpoint into ``params`` (a Flax tree).
+
+    Leaves that exist in both with equal shapes are taken from the checkpoint; the new head and
+    any other leaf missing from the checkpoint keep their fresh initialisation; a learnable
+    ``embed/wpe`` of a different grid is resized bicubically.
+    """
+    new = load_params(url)
+    src = new.get("model", new)
+    dst = params["model"]
+    overlap = len(set(src).intersection(dst))
+    log(f"[*] load pretrained params with overlap of {overlap}/{len(dst)}")
+
+    loaded = [0]
+
+    def merge(d, s, path=()):
+        for k, v in d.items():
+            if k not in s:
+                continue
+            if isinstance(v, dict):
+                if isinstance(s[k], dict):
+                    merge(v, s[k], path + (k,))
+                continue
+            sv = np.asarray(s[k])
+            if sv.shape == np.shape(v):
+                d[k] = sv.astype(np.float32)
+                loaded[0] += 1
+            elif path[-1:] == ("embed",) and k == "wpe" and sv.ndim == 3:
+                d[k] = _resize_posemb(sv, np.shape(v))
+                loaded[0] += 1
+                log(f"[*] resized embed/wpe {sv.shape} -> {np.shape(v)}")
+            else:
+                log(f"[!] shape mismatch for {'/'.join(path + (k,))}: {sv.shape} vs {np.shape(v)} (kept init)")
+
+    if "head" in dst:
+        head = dst["head"]
+        merge(dst, {k: v for k, v in src.items() if k != "head"})
+        dst["head"] = head
+    else:
+        merge(dst, src)
+    log(f"[*] {loaded[0]} pretrained leaves loaded")
+    return params

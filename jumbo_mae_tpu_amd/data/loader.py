@@ -1,0 +1,179 @@
+"""Training / validation data loaders.
+
+Reference ``create_dataloaders`` (/root/reference/src/dataset.py:100-161) with helpers
+``repeat_samples`` / ``collate_and_shuffle`` / ``collate_and_pad`` (:85-97).
+* train: infinite cycle over deterministically shuffled shards, split by rank then by worker,
+  sample shuffle buffer, decode, repeated augmentation (``augment_repeats`` deep copies, and the
+  collate re-orders the batch as batch[0::r] + batch[1::r] + ... so the copies of one image land
+  far apart), per-rank batch = train_batch_size // world_size // grad_accum, drop_last.
+* valid: one pass, rank split, last batch padded with ``-1`` (uint8 images become 255, labels -1).
+* ``synthetic:N[:C]`` shard spec: N random images with C classes (plumbing tests / benchmarks;
+  no dataset is reachable offline).
+Per-rank split replaces the reference's per-host split (one process per GPU here).
+"""
+
+from __future__ import annotations
+
+import copy
+import itertools
+import random
+from functools import partial
+
+import numpy as np
+import torch
+from torch.utils.data import DataLoader, IterableDataset, get_worker_info
+
+from . import shards as S
+from .transforms import create_transforms
+
+
+def repeat_samples(samples, repeats: int = 1):
+    for s in samples:
+        for _ in range(repeats):
+            yield copy.deepcopy(s)
+
+
+def _stack(items):
+    first = items[0]
+    if isinstance(first, tuple):
+        return tuple(_stack([it[i] for it in items]) for i in range(len(first)))
+    if isinstance(first, np.ndarray):
+        return torch.from_numpy(np.stack(items))
+    if isinstance(first, torch.Tensor):
+        return torch.stack(items)
+    return torch.tensor(items)
+
+
+def collate_and_shuffle(batch, repeats: int = 1):
+    return _stack(sum([batch[i::repeats] for i in range(repeats)], []))
+
+
+def _minus_one_like(x):
+    if isinstance(x, np.ndarray):
+        # torch.full_like(uint8, -1) wraps to 255 in the reference; numpy 2 refuses -1 for uint8
+        return np.full_like(x, np.iinfo(x.dtype).max if x.dtype.kind == "u" else -1)
+    return -1
+
+
+def collate_and_pad(batch, batch_size: int = 1):
+    first = batch[0]
+    if isinstance(first, tuple):
+        pad = tuple(_minus_one_like(x) for x in first)
+    else:
+        pad = _minus_one_like(first)
+    return _stack(list(batch) + [pad] * (batch_size - len(batch)))
+
+
+class ShardDataset(IterableDataset):
+    def __init__(self, spec, mode: str, transform, train: bool, repeats: int = 1, seed: int = 0,
+                 rank: int = 0, world: int = 1, shuffle_buffer: int = 2000, image_size: int = 224):
+        self.spec, self.mode, self.transform, self.train = spec, mode, transform, train
+        self.repeats, self.seed, self.rank, self.world = repeats, seed, rank, world
+        self.shuffle_buffer = shuffle_buffer
+        self.image_size = image_size
+        # validation batches always carry a label so that padded rows (-1) can be masked out
+        self.with_label = mode in ("finetune", "linear") or not train
+        self.synthetic = isinstance(spec, str) and spec.startswith("synthetic:")
+        self.urls = [] if self.synthetic else S.shard_list(spec)
+
+    # raw (decoded) samples of this rank/worker, one epoch
+    def _raw(self, epoch: int, wid: int, nw: int):
+        if self.synthetic:
+            parts = self.spec.split(":")
+            n = int(parts[1])
+            ncls = int(parts[2]) if len(parts) > 2 else 1000
+            idx = range(n)
+            idx = itertools.islice(idx, self.rank * nw + wid, None, self.world * nw)
+            for i in idx:
+                rs = np.random.default_rng(i + (epoch * 7919 if self.train else 0))
+                arr = rs.integers(0, 256, (self.image_size + 32, self.image_size + 32, 3), dtype=np.uint8)
+                from PIL import Image
+                yield {"jpg": Image.fromarray(arr), "cls": int(rs.integers(0, ncls))}
+            return
+        urls = S.epoch_shards(self.urls, self.seed, epoch, shuffle=self.train)
+        total = self.world * nw
+        if len(urls) >= total:
+            mine = S.split(S.split(urls, self.rank, self.world), wid, nw)
+            sample_filter = None
+        else:  # fewer shards than consumers: split samples instead of shards
+            mine = urls
+            sample_filter = (self.rank * nw + wid, total)
+        handler = S.ignore_and_continue if self.train else None
+        it = itertools.chain.from_iterable(S.tar_samples(u, handler) for u in mine)
+        if sample_filter is not None:
+            it = itertools.islice(it, sample_filter[0], None, sample_filter[1])
+        if self.train:
+            it = S.detshuffle(it, self.shuffle_buffer, self.seed * 7 + epoch * 131 + self.rank * 17 + wid)
+        for s in it:
+            try:
+                out = {"jpg": S.decode_pil(s["jpg"])}
+                if self.with_label:
+                    out["cls"] = S.decode_cls(s["cls"]) if "cls" in s else 0
+                yield out
+            except Exception:
+                if not self.train:
+                    raise
+                continue
+
+    def __iter__(self):
+        info = get_worker_info()
+        wid, nw = (info.id, info.num_workers) if info is not None else (0, 1)
+        random.seed(self.seed * 1000 + self.rank * 97 + wid)
+        np.random.seed((self.seed * 1000 + self.rank * 97 + wid) % (2 ** 32))
+        epoch = 0
+        while True:
+            raw = self._raw(epoch, wid, nw)
+            if self.train and self.repeats > 1:
+                raw = repeat_samples(raw, self.repeats)
+            for s in raw:
+                img = self.transform(s["jpg"])
+                yield (img, s["cls"]) if self.with_label else img
+            if not self.train:
+                return
+            epoch += 1
+
+
+def create_dataloaders(args, rank: int = 0, world: int = 1):
+    """Returns (train_loader | None, valid_loader | None) like dataset.py:100-161."""
+    train_t, valid_t = create_transforms(args.random_crop, args.image_size, args.auto_augment, args.color_jitter,
+                                         args.random_erasing, args.test_crop_ratio)
+    train_dl = valid_dl = None
+    pin = torch.cuda.is_available()
+    if getattr(args, "train_dataset_shards", None):
+        ds = ShardDataset(args.train_dataset_shards, args.mode, train_t, True, args.augment_repeats,
+                          args.shuffle_seed, rank, world, image_size=args.image_size)
+        bs = args.train_batch_size // world // args.grad_accum
+        nw = args.train_loader_workers
+        train_dl = DataLoader(ds, batch_size=bs, num_workers=nw,
+                              collate_fn=partial(collate_and_shuffle, repeats=args.augment_repeats),
+                              drop_last=True, pin_memory=pin, prefetch_factor=4 if nw > 0 else None,
+                              persistent_workers=nw > 0)
+    if getattr(args, "valid_dataset_shards", None):
+        ds = ShardDataset(args.valid_dataset_shards, args.mode, valid_t, False, 1, 0, rank, world,
+                          image_size=args.image_size)
+        bs = args.valid_batch_size // world
+        nw = args.valid_loader_workers
+        valid_dl = DataLoader(ds, batch_size=bs, num_workers=nw, collate_fn=partial(collate_and_pad, batch_size=bs),
+                              drop_last=False, pin_memory=pin, prefetch_factor=4 if nw > 0 else None,
+                              persistent_workers=nw > 0)
+    return train_dl, valid_dl
+
+
+class SyntheticGPUImages:
+    """Infinite GPU-resident random uint8 batches (benchmarks: no host decode / H2D in the loop)."""
+
+    def __init__(self, batch: int, image_size: int, device, labels: int = 0, seed: int = 0, pool: int = 2):
+        g = torch.Generator(device=device).manual_seed(seed)
+        self.imgs = [torch.randint(0, 256, (batch, 3, image_size, image_size), dtype=torch.uint8, device=device,
+                                   generator=g) for _ in range(pool)]
+        self.labels = [torch.randint(0, max(labels, 1), (batch,), device=device, generator=g) for _ in range(pool)]
+        self.with_labels = labels > 0
+        self.i = 0
+
+    def __iter__(self):
+        return self
+
+    def __next__(self):
+        k = self.i % len(self.imgs)
+        self.i += 1
+        return (self.imgs[k], self.labels[k]) if self.with_labels else self.imgs[k]

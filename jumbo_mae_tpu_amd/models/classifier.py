@@ -1,0 +1,141 @@
+"""Finetune / linear-probe task module.
+
+Parity: ``FinetuneModule`` (/root/reference/src/finetuning.py:78-106), ``CRITERION_COLLECTION``
+(:39-42), the classifier branch of ``ViT.__call__`` (modeling.py:268-274) and ``validation_step``
+(finetuning.py:157-165).
+
+* labels: int -> one-hot; training applies label smoothing then Mixup/CutMix;
+* logits = head(LN(x)[:, :3].reshape(B, 3D)) -- only the 3 CLS rows go through the final LN
+  (per-row op, identical result);
+* linear probing: the encoder runs without autograd (== ``stop_gradient``) and the head is
+  SyncBatchNorm + Dense;
+* accuracy = membership of the top-1 / top-5 predictions in the arg-max label set.
+Fixes: RNG streams advance every step (quirk Q4); validation loss is the true per-sample masked
+mean (the reference multiplies the batch-mean loss, padded samples included, by the valid count).
+"""
+
+from __future__ import annotations
+
+import torch
+import torch.nn.functional as F
+
+from ..config import ViTConfig
+from ..ops import functional as Fn
+from ..ops import mae as mae_ops
+from ..utils.mae import extract_patches_nchw
+from ..utils.mixup import Mixup, smooth_labels
+from .params import ParamStore
+from .vit import JumboViT, LinearCLS
+
+
+def softmax_cross_entropy(logits, labels):
+    return -(labels * F.log_softmax(logits, -1)).sum(-1)
+
+
+def sigmoid_bce(logits, labels):
+    t = (labels > 0).to(logits.dtype)
+    return F.binary_cross_entropy_with_logits(logits, t, reduction="none").mean(-1)
+
+
+CRITERION_COLLECTION = {"ce": softmax_cross_entropy, "bce": sigmoid_bce}
+
+
+class FinetuneModel:
+    def __init__(self, cfg: ViTConfig, mixup: Mixup | None = None, label_smoothing: float = 0.0,
+                 criterion: str = "ce", group=None):
+        assert cfg.labels > 0
+        self.cfg = cfg
+        self.store = ParamStore()
+        s = self.store
+        trainable_encoder = not cfg.linear_probing
+        self.encoder = JumboViT(s, cfg, ("model",), trainable=trainable_encoder)
+        self.head = LinearCLS(s, ("model", "head"), cfg.jumbo_dim, cfg.labels, cfg.batch_norm)
+        self.mixup = mixup or Mixup(0.0, 0.0)
+        self.label_smoothing = label_smoothing if criterion == "ce" else 0.0
+        self.criterion = CRITERION_COLLECTION[criterion]
+        self.group = group
+
+    def to(self, device, compute_dtype=torch.float32, seed: int = 0):
+        g = torch.Generator(device=device).manual_seed(seed)
+        self.store.finalize(device, compute_dtype, g)
+        self.head.init_stats(device)
+        return self
+
+    @property
+    def device(self):
+        return self.store.master.device
+
+    # ---------------------------------------------------------------- pieces
+    def patches(self, images_u8, labels, rngs, det):
+        p = self.cfg.patch_size
+        if det or not self.mixup.active:
+            return mae_ops.normalized_patches(images_u8, p), labels
+        x = mae_ops.normalize_images(images_u8)
+        x, labels = self.mixup(x, labels, rngs.get("mixup") if rngs else None)
+        return extract_patches_nchw(x, p).contiguous(), labels
+
+    def features(self, patches, rngs=None, det=True):
+        cfg = self.cfg
+        B = patches.shape[0]
+        drop = rngs.get("dropout") if rngs else None
+        x = self.encoder.embed(patches, None)
+        x = self.encoder.blocks(x, drop, det)
+        C = cfg.num_cls_tokens
+        h = Fn.layer_norm(x[:, :C], self.encoder.norm.g, self.encoder.norm.b, torch.float32)
+        return h.reshape(B, C * cfg.dim)
+
+    def logits(self, images_u8, labels=None, rngs=None, det=True):
+        patches, labels = self.patches(images_u8, labels, rngs, det)
+        if self.cfg.linear_probing:
+            with torch.no_grad():
+                feats = self.features(patches, rngs, det)
+        else:
+            feats = self.features(patches, rngs, det)
+        return self.head(feats, det, self.group), labels
+
+    # ---------------------------------------------------------------- train / eval
+    def forward(self, images_u8, labels, rngs=None, det=False):
+        labels = self._prep_labels(labels)
+        if not det:
+            labels = smooth_labels(labels, self.label_smoothing)
+        logits, labels = self.logits(images_u8, labels, rngs, det)
+        loss = self.criterion(logits, labels).mean()
+        acc1, acc5 = self.accuracy(logits, labels)
+        return {"loss": loss, "acc1": acc1.float().mean(), "acc5": acc5.float().mean()}
+
+    __call__ = forward
+
+    def _prep_labels(self, labels):
+        if labels.dim() == 1:
+            labels = F.one_hot(labels.long().clamp(min=0), self.cfg.labels)
+        return labels.float()
+
+    @staticmethod
+    def accuracy(logits, labels):
+        lab = labels == labels.max(-1, keepdim=True).values
+        k = min(5, logits.shape[-1])
+        top = logits.topk(k, -1).indices
+        accs = torch.gather(lab, 1, top)
+        return accs[:, 0], accs.any(-1)
+
+    @torch.no_grad()
+    def evaluate(self, images_u8, labels, rngs=None) -> dict:
+        """Sums over valid (label != -1) samples, like validation_step (finetuning.py:157-165)."""
+        valid = (labels != -1)
+        lab = self._prep_labels(torch.where(valid, labels, torch.zeros_like(labels)))
+        logits, _ = self.logits(images_u8, lab, rngs, det=True)
+        loss = self.criterion(logits, lab)
+        acc1, acc5 = self.accuracy(logits, lab)
+        v = valid.float()
+        return {"loss": (loss * v).sum(), "acc1": (acc1.float() * v).sum(), "acc5": (acc5.float() * v).sum(),
+                "num_samples": v.sum()}
+
+    # ---------------------------------------------------------------- params
+    def flax_params(self) -> dict:
+        return self.store.to_flax_tree()
+
+    def batch_stats(self) -> dict | None:
+        if not self.cfg.batch_norm:
+            return None
+        return {"model": {"head": {"BatchNorm_0": {"mean": self.head.running_mean.cpu().numpy(),
+                                                   "var": self.head.running_var.cpu().numpy()}}}}

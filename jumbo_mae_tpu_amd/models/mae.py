@@ -68,7 +68,7 @@ class PretrainModel:
         return masking_ids(noise, self.cfg.keep_len)
 
     def forward(self, images_u8: torch.Tensor, rngs: dict | None = None, det: bool = False,
-                noise: torch.Tensor | None = None) -> dict:
+                noise: torch.Tensor | None = None, per_sample: bool = False) -> dict:
         rngs = rngs or {}
         cfg = self.cfg
         B = images_u8.shape[0]
@@ -90,10 +90,18 @@ class PretrainModel:
         pred = self.decoder_image_output(hd)  # [B*N, p*p*3]
         if mask.dim() == 1:
             mask = mask.unsqueeze(0).expand(B, N)
-        loss = mae_ops.masked_mse(pred.view(B, N, -1), patches, mask, self.norm_pix_loss)
+        loss = mae_ops.masked_mse(pred.view(B, N, -1), patches, mask, self.norm_pix_loss, per_sample)
         return {"loss": loss}
 
     __call__ = forward
+
+    @torch.no_grad()
+    def evaluate(self, images_u8: torch.Tensor, valid: torch.Tensor | None = None, rngs: dict | None = None) -> dict:
+        """validation_step (pretraining.py:162-167): random masking and droppath stay active
+        (det=False, quirk Q3); returns sums over valid images (fix for Q7: true mean later)."""
+        per = self.forward(images_u8, rngs, det=False, per_sample=True)["loss"]
+        v = torch.ones_like(per) if valid is None else valid.float()
+        return {"loss": (per * v).sum(), "num_samples": v.sum()}
 
     # ------------------------------------------------------------------------ params
     def flax_params(self) -> dict:

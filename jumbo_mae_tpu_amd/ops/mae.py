@@ -66,6 +66,10 @@ def norm_pix(target: torch.Tensor) -> torch.Tensor:
     return (target - mean) / torch.sqrt(var + 1e-6)
 
 
-def masked_mse(pred: torch.Tensor, target: torch.Tensor, mask: torch.Tensor, norm_pix_loss: bool) -> torch.Tensor:
+def masked_mse(pred: torch.Tensor, target: torch.Tensor, mask: torch.Tensor, norm_pix_loss: bool,
+               per_sample: bool = False) -> torch.Tensor:
     t = norm_pix(target) if norm_pix_loss else target
+    if per_sample:  # mean over masked patches of each image (patch_mse_loss before the batch mean)
+        per_patch = (t - pred.float()).square().mean(-1)
+        return (per_patch * mask).sum(-1) / mask.sum(-1)
     return patch_mse_loss(pred.float(), t, mask)
