@@ -182,8 +182,12 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const uint16_t* __restric
 }
 
 // -------------------------------------------------------------------------------- backward
+// waves per backward workgroup: 8 when the LDS budget allows (decoder, hd 32), else 4
+template <int HD, int SP>
+constexpr int bwd_waves() { return (SP >= 128 && HD == 32) ? 8 : 4; }
+
 template <int HD, int SP, bool TR>
-__global__ __launch_bounds__(256) void attn_bwd_kernel(const uint16_t* __restrict__ qkv,
+__global__ __launch_bounds__((64 * bwd_waves<HD, SP>())) void attn_bwd_kernel(const uint16_t* __restrict__ qkv,
                                                        const uint16_t* __restrict__ o,
                                                        const uint16_t* __restrict__ dO,
                                                        const float* __restrict__ lse,
@@ -193,8 +197,10 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(const uint16_t* __restric
   constexpr int NT = SP / 16;
   constexpr int KK = HD / 32;
   constexpr int DT = HD / 16;
-  constexpr int QC = 64;  // query rows per dS chunk
-  constexpr int NKW = (NT + 3) / 4;  // key tiles per wave
+  constexpr int NW = bwd_waves<HD, SP>();
+  constexpr int NTH = 64 * NW;
+  constexpr int QC = 16 * NW;             // query rows per dS chunk: one q tile per wave for dQ
+  constexpr int NKW = (NT + NW - 1) / NW;  // key tiles per wave
   extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
   uint16_t* Qs = smem;
   uint16_t* Ks = Qs + SP * RS;
@@ -222,13 +228,13 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(const uint16_t* __restric
   uint16_t* dKg = dqkv + (long)b * S * ts + (H + h) * HD;
   uint16_t* dVg = dqkv + (long)b * S * ts + (2 * H + h) * HD;
 
-  for (int i = threadIdx.x; i < SP; i += 256) {
+  for (int i = threadIdx.x; i < SP; i += NTH) {
     delta_s[i] = 0.f;
     lse_s[i] = i < S ? lse[((long)b * H + h) * S + i] * LOG2E : INFINITY;
   }
   __syncthreads();
   constexpr int CPR = HD / 8;
-  for (int i = threadIdx.x; i < SP * CPR; i += 256) {
+  for (int i = threadIdx.x; i < SP * CPR; i += NTH) {
     const int r = i / CPR, c = (i % CPR) * 8;
     uint4 qv = make_uint4(0, 0, 0, 0), kv = qv, vv = qv, dv = qv;
     float dsum = 0.f;
@@ -278,7 +284,7 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(const uint16_t* __restric
   for (int qc = 0; qc * QC < SP; ++qc) {
 #pragma unroll
     for (int w = 0; w < NKW; ++w) {
-      const int kt = wave + 4 * w;
+      const int kt = wave + NW * w;
       if (kt < NT) {
         bf16x8_t kf[KK], vf[KK];
 #pragma unroll
@@ -373,7 +379,7 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(const uint16_t* __restric
   // write dK, dV of this wave's key tiles: acc[dt][i] = X^T[d = dt*16+4g+i][key = kt*16+l16]
 #pragma unroll
   for (int w = 0; w < NKW; ++w) {
-    const int kt = wave + 4 * w;
+    const int kt = wave + NW * w;
     const int key = kt * 16 + l16;
     if (kt < NT && key < S) {
 #pragma unroll
@@ -392,7 +398,8 @@ template <int HD, int SP, bool TR>
 size_t fwd_smem() { return (size_t)(SP * (HD + 8) + (TR ? SP * (HD + 8) : HD * (SP + 8))) * 2; }
 template <int HD, int SP, bool TR>
 size_t bwd_smem() {
-  return (size_t)(4 * SP * (HD + 8) + (TR ? 0 : 3 * HD * (SP + 8)) + 64 * (SP + 8)) * 2 + 2 * SP * sizeof(float);
+  return (size_t)(4 * SP * (HD + 8) + (TR ? 0 : 3 * HD * (SP + 8)) + 16 * bwd_waves<HD, SP>() * (SP + 8)) * 2 +
+         2 * SP * sizeof(float);
 }
 
 int g_use_tr = 1;  // runtime switch (tests run both variants)
@@ -412,7 +419,7 @@ int run_t(bool fwd, const uint16_t* qkv, const uint16_t* o, const uint16_t* dO, 
   if (fwd)
     attn_fwd_kernel<HD, SP, TR><<<grid, 256, sm, st>>>(qkv, out, lse_out, S, H, scale);
   else
-    attn_bwd_kernel<HD, SP, TR><<<grid, 256, sm, st>>>(qkv, o, dO, lse_in, out, S, H, scale);
+    attn_bwd_kernel<HD, SP, TR><<<grid, 64 * bwd_waves<HD, SP>(), sm, st>>>(qkv, o, dO, lse_in, out, S, H, scale);
   return 0;
 }
 

@@ -11,10 +11,12 @@ int jm_layernorm_fwd(const float* x, long sB, long sT, int B, int T, int D, cons
                      float eps, void* y, int out_bf16, float* mean, float* rstd, hipStream_t st);
 int jm_layernorm_bwd(const void* dy, int dy_bf16, const float* x, long sB, long sT, int B, int T, int D,
                      const float* mean, const float* rstd, const float* gamma, float* dx, float* dgamma, float* dbeta,
-                     int accum_params, hipStream_t st);
+                     int accum_params, float* ws, hipStream_t st);
+int jm_layernorm_bwd_blocks(int rows);
 int jm_gelu_fwd(const uint16_t* h, uint16_t* a, long n, hipStream_t st);
 int jm_gelu_bwd(const uint16_t* h, const uint16_t* da, uint16_t* dh, float* bias_grad, int M, int N, hipStream_t st);
 int jm_colsum_bf16(const uint16_t* x, float* acc, int M, int N, hipStream_t st);
+int jm_splitk_reduce_add(const float* part, float* g, long n, int S, hipStream_t st);
 int jm_residual_fwd(const float* x, long sB, long sT, int B, int T, int D, const uint16_t* y, const float* scale,
                     const float* mask, float* out, hipStream_t st);
 int jm_residual_bwd(const float* dout, const uint16_t* y, const float* scale, const float* mask, float* dscale,
@@ -85,9 +87,11 @@ torch::Tensor layernorm_bwd(torch::Tensor dy, torch::Tensor x, torch::Tensor mea
   auto dx = torch::empty({B, T, D}, x.options());
   const bool dyb = dy.scalar_type() == torch::kBFloat16;
   TORCH_CHECK(dyb || dy.scalar_type() == torch::kFloat32, "dy dtype");
+  auto ws = torch::empty({accum ? (long)jm_layernorm_bwd_blocks(B * T) * 2 * D : 1}, x.options());
   check_rc(jm_layernorm_bwd(dy.data_ptr(), dyb, x.data_ptr<float>(), x.stride(0), x.stride(1), B, T, D,
                             mean.data_ptr<float>(), rstd.data_ptr<float>(), gamma.data_ptr<float>(),
-                            dx.data_ptr<float>(), dgamma.data_ptr<float>(), dbeta.data_ptr<float>(), accum, stream()),
+                            dx.data_ptr<float>(), dgamma.data_ptr<float>(), dbeta.data_ptr<float>(), accum,
+                            ws.data_ptr<float>(), stream()),
            "layernorm_bwd");
   return dx;
 }
@@ -119,6 +123,13 @@ void colsum(torch::Tensor x, torch::Tensor acc) {
   const int N = x.size(-1);
   const int M = x.numel() / N;
   check_rc(jm_colsum_bf16(bf(x), acc.data_ptr<float>(), M, N, stream()), "colsum");
+}
+
+void splitk_reduce_add(torch::Tensor part, torch::Tensor g) {
+  CHECK_CONTIG(part);
+  TORCH_CHECK(g.is_contiguous() && g.numel() * part.size(0) == part.numel(), "splitk_reduce_add shapes");
+  check_rc(jm_splitk_reduce_add(part.data_ptr<float>(), g.data_ptr<float>(), g.numel(), part.size(0), stream()),
+           "splitk_reduce_add");
 }
 
 torch::Tensor residual_fwd(torch::Tensor x, torch::Tensor y, c10::optional<torch::Tensor> scale,
@@ -244,6 +255,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("gelu_fwd", &gelu_fwd);
   m.def("gelu_bwd", &gelu_bwd, py::arg("h"), py::arg("da"), py::arg("bias_grad") = py::none());
   m.def("colsum", &colsum);
+  m.def("splitk_reduce_add", &splitk_reduce_add);
   m.def("residual_fwd", &residual_fwd);
   m.def("residual_bwd", &residual_bwd);
   m.def("attn_fwd", &attn_fwd);

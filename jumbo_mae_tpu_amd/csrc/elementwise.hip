@@ -60,12 +60,16 @@ __global__ __launch_bounds__(256) void rowcol_kernel(const void* __restrict__ in
                                                      uint16_t* __restrict__ out, float* __restrict__ acc,
                                                      const float* __restrict__ scale, const float* __restrict__ mask,
                                                      int M, int N, int T, int rows_per_block) {
-  extern __shared__ __attribute__((aligned(16))) float red[];  // [N]
-  const ColPlan p = col_plan(N);
+  extern __shared__ __attribute__((aligned(16))) float red_s[];  // [<= 2048] block's columns
+  // 2-D grid: blockIdx.y picks a chunk of <= 2048 columns, blockIdx.x a slab of rows
+  const int c0 = blockIdx.y * 2048;
+  const int nc = (N - c0) < 2048 ? (N - c0) : 2048;
+  const ColPlan p = col_plan(nc);
   const int slot = threadIdx.x / p.tpr, c = threadIdx.x % p.tpr;
   const bool active = slot < p.rps;
+  float* red = red_s - c0;  // index with absolute column
   if (acc) {
-    for (int i = threadIdx.x; i < N; i += 256) red[i] = 0.f;
+    for (int i = threadIdx.x; i < nc; i += 256) red_s[i] = 0.f;
     __syncthreads();
   }
   const int r_begin = blockIdx.x * rows_per_block;
@@ -73,7 +77,7 @@ __global__ __launch_bounds__(256) void rowcol_kernel(const void* __restrict__ in
   if (r_end > M) r_end = M;
   if (active) {
     for (int cg = c; cg < p.cgs; cg += p.tpr) {
-      const int col = cg * 8;
+      const int col = c0 + cg * 8;
       float s[8];
 #pragma unroll
       for (int j = 0; j < 8; ++j) s[j] = 0.f;
@@ -86,36 +90,54 @@ __global__ __launch_bounds__(256) void rowcol_kernel(const void* __restrict__ in
           for (int j = 0; j < 8; ++j) sc[j] = 1.f;
         }
       }
-      for (int r = r_begin + slot; r < r_end; r += p.rps) {
-        const long off = (long)r * N + col;
-        if (MODE == 0) {
-          float v[8];
-          load8((const uint16_t*)in0 + off, v);
+      // U rows per trip: all loads of a trip are issued before any use (memory-level parallelism;
+      // one load per trip left this loop latency-bound at ~55 % of HBM bandwidth)
+      constexpr int U = 4;
+      for (int r0 = r_begin + slot; r0 < r_end; r0 += U * p.rps) {
+        float a[U][8], b[U][8];
 #pragma unroll
-          for (int j = 0; j < 8; ++j) s[j] += v[j];
-        } else if (MODE == 1) {
-          float hv[8], dv[8];
-          load8((const uint16_t*)in0 + off, hv);
-          load8(in1 + off, dv);
-#pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            // round dh to bf16 first so the bias grad equals the colsum of what the GEMMs consume
-            dv[j] = bf2f(f2bf(dv[j] * gelu_grad(hv[j])));
-            s[j] += dv[j];
+        for (int u = 0; u < U; ++u) {
+          const int r = r0 + u * p.rps;
+          if (r < r_end) {
+            const long off = (long)r * N + col;
+            if (MODE == 0) {
+              load8((const uint16_t*)in0 + off, a[u]);
+            } else if (MODE == 1) {
+              load8((const uint16_t*)in0 + off, a[u]);
+              load8(in1 + off, b[u]);
+            } else {
+              load8((const float*)in0 + off, a[u]);
+              if (scale) load8(in1 + off, b[u]);
+            }
           }
-          store8(out + off, dv);
-        } else {
-          float dv[8], yv[8], o[8];
-          load8((const float*)in0 + off, dv);
-          const float m = mask ? mask[r / T] : 1.f;
-          if (scale) load8(in1 + off, yv);
+        }
 #pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            const float md = m * dv[j];
-            o[j] = md * sc[j];
-            if (scale) s[j] += md * yv[j];
+        for (int u = 0; u < U; ++u) {
+          const int r = r0 + u * p.rps;
+          if (r >= r_end) break;
+          const long off = (long)r * N + col;
+          if (MODE == 0) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) s[j] += a[u][j];
+          } else if (MODE == 1) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+              // round dh to bf16 first so the bias grad equals the colsum of what the GEMMs consume
+              b[u][j] = bf2f(f2bf(b[u][j] * gelu_grad(a[u][j])));
+              s[j] += b[u][j];
+            }
+            store8(out + off, b[u]);
+          } else {
+            float o[8];
+            const float m = mask ? mask[r / T] : 1.f;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+              const float md = m * a[u][j];
+              o[j] = md * sc[j];
+              if (scale) s[j] += md * b[u][j];
+            }
+            store8(out + off, o);
           }
-          store8(out + off, o);
         }
       }
       if (acc) {
@@ -126,7 +148,7 @@ __global__ __launch_bounds__(256) void rowcol_kernel(const void* __restrict__ in
   }
   if (acc) {
     __syncthreads();
-    for (int i = threadIdx.x; i < N; i += 256) atomicAdd(&acc[i], red[i]);
+    for (int i = threadIdx.x; i < nc; i += 256) atomicAdd(&acc[c0 + i], red_s[i]);
   }
 }
 
@@ -167,19 +189,22 @@ int grid_for(long work, int per_thread_items = 1) {
 template <int MODE>
 void launch_rowcol(const void* in0, const uint16_t* in1, uint16_t* out, float* acc, const float* scale,
                    const float* mask, int M, int N, int T, hipStream_t st) {
-  // each row-slot should walk >= 16 rows; cap the grid so the per-block atomics stay cheap
-  const int cgs = N / 8;
+  // 2-D grid: column chunks of 2048 x row slabs; each row-slot walks >= 16 rows, ~2048 blocks
+  // in total so the per-block column atomics stay cheap
+  const int ncol = (N + 2047) / 2048;
+  const int cgs = (N < 2048 ? N : 2048) / 8;
   const int tpr = cgs < 256 ? cgs : 256;
   const int rps = 256 / tpr;
   int rows_per_block = rps * 16;
   int nb = (M + rows_per_block - 1) / rows_per_block;
-  if (nb > 2048) {
-    nb = 2048;
+  const int cap = 2048 / ncol > 1 ? 2048 / ncol : 1;
+  if (nb > cap) {
+    nb = cap;
     rows_per_block = (M + nb - 1) / nb;
   }
   if (nb < 1) nb = 1;
-  const size_t smem = acc ? N * sizeof(float) : 0;
-  rowcol_kernel<MODE><<<nb, 256, smem, st>>>(in0, in1, out, acc, scale, mask, M, N, T, rows_per_block);
+  const size_t smem = acc ? 2048 * sizeof(float) : 0;
+  rowcol_kernel<MODE><<<dim3(nb, ncol), 256, smem, st>>>(in0, in1, out, acc, scale, mask, M, N, T, rows_per_block);
 }
 
 }  // namespace
@@ -215,5 +240,33 @@ int jm_residual_bwd(const float* dout, const uint16_t* y, const float* scale, co
                     uint16_t* dy, int B, int T, int D, hipStream_t st) {
   if (D % 8) return -1;
   launch_rowcol<2>(dout, y, dy, dscale, scale, mask, B * T, D, T, st);
+  return 0;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Split-K epilogue of the weight-gradient GEMMs: g[i] += sum_s part[s][i] (fp32), one pass.
+namespace {
+__global__ __launch_bounds__(256) void splitk_reduce_add_kernel(const float* __restrict__ part,
+                                                                float* __restrict__ g, long n4, int S) {
+  const long n = n4 * 4;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n4; i += (long)gridDim.x * 256) {
+    float acc[4];
+    load4(g + i * 4, acc);
+    for (int s = 0; s < S; ++s) {
+      float v[4];
+      load4(part + (long)s * n + i * 4, v);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[j] += v[j];
+    }
+    store4(g + i * 4, acc);
+  }
+}
+}  // namespace
+
+int jm_splitk_reduce_add(const float* part, float* g, long n, int S, hipStream_t st) {
+  if (n % 4) return -1;
+  long blocks = (n / 4 + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  splitk_reduce_add_kernel<<<(int)blocks, 256, 0, st>>>(part, g, n / 4, S);
   return 0;
 }

@@ -134,22 +134,65 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const TI* __restrict__ dy, 
     }
   }
   if (!accum_params) return;
+  // merge the 4 waves' partials through LDS in turn (float4, conflict-free, no atomics), then
+  // one coalesced store of the block partial [dgamma | dbeta] into the workspace row
+  for (int w = 0; w < 4; ++w) {
+    if (wave == w) {
 #pragma unroll
-  for (int i = 0; i < V; ++i) {
-    const int col = (i * 64 + lane) * 4;
-    if (col < D) {
+      for (int i = 0; i < V; ++i) {
+        const int col = (i * 64 + lane) * 4;
+        if (col < D) {
+          float a[4], c[4];
+          if (w == 0) {
+            a[0] = a[1] = a[2] = a[3] = 0.f;
+            c[0] = c[1] = c[2] = c[3] = 0.f;
+          } else {
+            load4(red + col, a);
+            load4(red + D + col, c);
+          }
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        atomicAdd(&red[col + j], dg[i][j]);
-        atomicAdd(&red[D + col + j], db[i][j]);
+          for (int j = 0; j < 4; ++j) {
+            a[j] += dg[i][j];
+            c[j] += db[i][j];
+          }
+          store4(red + col, a);
+          store4(red + D + col, c);
+        }
       }
     }
+    __syncthreads();
   }
-  __syncthreads();
-  for (int i = threadIdx.x; i < D; i += 256) {
-    atomicAdd(&dgamma[i], red[i]);
-    atomicAdd(&dbeta[i], red[D + i]);
+  float* out = dgamma;  // == workspace [gridDim.x, 2*D] on this path
+  for (int i = threadIdx.x * 4; i < 2 * D; i += 256 * 4) {
+    float a[4];
+    load4(red + i, a);
+    store4(out + (long)blockIdx.x * 2 * D + i, a);
   }
+}
+
+// dgamma += sum_b ws[b][0:D], dbeta += sum_b ws[b][D:2D]; grid.y splits the partial rows.
+__global__ __launch_bounds__(256) void ln_param_reduce_kernel(const float* __restrict__ ws, int nb, int D,
+                                                              float* __restrict__ dgamma, float* __restrict__ dbeta) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= 2 * D) return;
+  const int per = (nb + gridDim.y - 1) / gridDim.y;
+  const int b0 = blockIdx.y * per;
+  int b1 = b0 + per;
+  if (b1 > nb) b1 = nb;
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  int b = b0;
+  for (; b + 3 < b1; b += 4) {
+    s0 += ws[(long)b * 2 * D + i];
+    s1 += ws[(long)(b + 1) * 2 * D + i];
+    s2 += ws[(long)(b + 2) * 2 * D + i];
+    s3 += ws[(long)(b + 3) * 2 * D + i];
+  }
+  for (; b < b1; ++b) s0 += ws[(long)b * 2 * D + i];
+  const float s = (s0 + s1) + (s2 + s3);
+  if (i < D)
+    atomicAdd(&dgamma[i], s);
+  else
+    atomicAdd(&dbeta[i - D], s);
 }
 
 template <typename TO>
@@ -204,22 +247,31 @@ int jm_layernorm_fwd(const float* x, long sB, long sT, int B, int T, int D, cons
   return 0;
 }
 
+int jm_layernorm_bwd_blocks(int rows) {
+  // grid-stride over rows: 1024 blocks x 4 waves = 4 waves per SIMD streaming; each block writes
+  // one [2*D] partial (no atomics in the hot kernel)
+  int nb = (rows + 3) / 4;
+  return nb > 1024 ? 1024 : nb;
+}
+
 int jm_layernorm_bwd(const void* dy, int dy_bf16, const float* x, long sB, long sT, int B, int T, int D,
                      const float* mean, const float* rstd, const float* gamma, float* dx, float* dgamma,
-                     float* dbeta, int accum_params, hipStream_t st) {
+                     float* dbeta, int accum_params, float* ws, hipStream_t st) {
   const int V = pick_v(D);
   if (V < 0 || (D % 4) != 0) return -1;
   const int rows = B * T;
-  int nb = (rows + 3) / 4;
-  // grid-stride: enough waves to stream, few enough blocks that the per-block column atomics stay cheap
-  if (nb > 1024) nb = 1024;
+  const int nb = jm_layernorm_bwd_blocks(rows);
   dim3 grid(nb);
   const size_t smem = accum_params ? 2 * D * sizeof(float) : 0;
   if (dy_bf16)
     launch_bwd<uint16_t>(V, grid, smem, st, (const uint16_t*)dy, x, sB, sT, T, rows, D, mean, rstd, gamma, dx,
-                         dgamma, dbeta, accum_params);
+                         ws, nullptr, accum_params);
   else
-    launch_bwd<float>(V, grid, smem, st, (const float*)dy, x, sB, sT, T, rows, D, mean, rstd, gamma, dx, dgamma,
-                      dbeta, accum_params);
+    launch_bwd<float>(V, grid, smem, st, (const float*)dy, x, sB, sT, T, rows, D, mean, rstd, gamma, dx, ws,
+                      nullptr, accum_params);
+  if (accum_params) {
+    const int ysplit = nb >= 64 ? 16 : 1;
+    ln_param_reduce_kernel<<<dim3((2 * D + 255) / 256, ysplit), 256, 0, st>>>(ws, nb, D, dgamma, dbeta);
+  }
   return 0;
 }

@@ -37,11 +37,35 @@ def _hip(t: torch.Tensor) -> bool:
     return _ext.use_hip(t)
 
 
+def wgrad_split(M: int, N: int, K: int) -> int:
+    """Split-K factor for a weight-gradient GEMM (reduction over M tokens, N x K output).
+
+    The output of a wgrad is small (0.25-38 M elements) while the reduction is 25k-100k long, so a
+    single GEMM has only 4-200 256x256 output tiles for 256 CUs (measured 160-690 TF/s on MI355X,
+    profiles/r1_gemm_wgrad_alternatives.log).  Splitting M into S chunks of one strided-batched
+    GEMM gives S x tiles workgroups (fp32 partials, reduced after): ~4x tiles-per-CU target."""
+    tiles = max(1, (N // 256) * (K // 256))
+    s = 1
+    while s < 16 and tiles * s * 2 <= 256 and M % (s * 2) == 0 and M // (s * 2) >= 2048:
+        s *= 2
+    return s
+
+
 def _gemm_wgrad(h: Handle, dy: torch.Tensor, x: torch.Tensor) -> None:
     """grad[h] += dy^T @ x  (fp32 accumulate; bf16 inputs on GPU)."""
     g = h.grad
     if dy.is_cuda and dy.dtype != torch.float32:
-        torch.addmm(g, dy.t(), x, out_dtype=torch.float32, out=g)
+        M, N = dy.shape
+        K = x.shape[1]
+        s = wgrad_split(M, N, K)
+        if s > 1:
+            part = torch.bmm(dy.view(s, M // s, N).transpose(1, 2), x.view(s, M // s, K), out_dtype=torch.float32)
+            if _hip(part):
+                _ext.load().splitk_reduce_add(part, g)  # g += sum_s part[s], one fused pass
+            else:
+                g.add_(part.sum(0))
+        else:
+            torch.addmm(g, dy.t(), x, out_dtype=torch.float32, out=g)
     else:
         g.addmm_(dy.t().float(), x.float())
 
