@@ -10,17 +10,18 @@
 int jm_layernorm_fwd(const float* x, long sB, long sT, int B, int T, int D, const float* gamma, const float* beta,
                      float eps, void* y, int out_bf16, float* mean, float* rstd, hipStream_t st);
 int jm_layernorm_bwd(const void* dy, int dy_bf16, const float* x, long sB, long sT, int B, int T, int D,
-                     const float* mean, const float* rstd, const float* gamma, float* dx, float* dgamma, float* dbeta,
-                     int accum_params, float* ws, hipStream_t st);
+                     const float* mean, const float* rstd, const float* gamma, float* dx_ptr, long oB, long oT,
+                     const float* dres, long rB, long rT, float* dgamma, float* dbeta, int accum_params, float* ws,
+                     hipStream_t st);
 int jm_layernorm_bwd_blocks(int rows);
 int jm_gelu_fwd(const uint16_t* h, uint16_t* a, long n, hipStream_t st);
 int jm_gelu_bwd(const uint16_t* h, const uint16_t* da, uint16_t* dh, float* bias_grad, int M, int N, hipStream_t st);
 int jm_colsum_bf16(const uint16_t* x, float* acc, int M, int N, hipStream_t st);
 int jm_splitk_reduce_add(const float* part, float* g, long n, int S, hipStream_t st);
 int jm_residual_fwd(const float* x, long sB, long sT, int B, int T, int D, const uint16_t* y, const float* scale,
-                    const float* mask, float* out, hipStream_t st);
-int jm_residual_bwd(const float* dout, const uint16_t* y, const float* scale, const float* mask, float* dscale,
-                    uint16_t* dy, int B, int T, int D, hipStream_t st);
+                    const float* mask, float* out, long oB, long oT, hipStream_t st);
+int jm_residual_bwd(const float* dout, long dB, long dT, const uint16_t* y, const float* scale, const float* mask,
+                    float* dscale, uint16_t* dy, int B, int T, int D, hipStream_t st);
 int jm_attn_fwd(const uint16_t* qkv, uint16_t* o, float* lse, int B, int S, int H, int hd, hipStream_t st);
 int jm_attn_bwd(const uint16_t* qkv, const uint16_t* o, const uint16_t* dO, const float* lse, uint16_t* dqkv, int B,
                 int S, int H, int hd, hipStream_t st);
@@ -79,19 +80,34 @@ std::vector<torch::Tensor> layernorm_fwd(torch::Tensor x, torch::Tensor gamma, t
 }
 
 torch::Tensor layernorm_bwd(torch::Tensor dy, torch::Tensor x, torch::Tensor mean, torch::Tensor rstd,
-                            torch::Tensor gamma, torch::Tensor dgamma, torch::Tensor dbeta, bool accum) {
+                            torch::Tensor gamma, torch::Tensor dgamma, torch::Tensor dbeta, bool accum,
+                            c10::optional<torch::Tensor> dres, c10::optional<torch::Tensor> out) {
   CHECK_CONTIG(dy);
   TORCH_CHECK(x.dim() == 3 && x.stride(2) == 1, "x must be [B,T,D]");
   const int B = x.size(0), T = x.size(1), D = x.size(2);
   TORCH_CHECK(dy.numel() == (long)B * T * D, "dy shape");
-  auto dx = torch::empty({B, T, D}, x.options());
+  torch::Tensor dx;
+  if (out.has_value() && out->defined()) {
+    dx = *out;
+    TORCH_CHECK(dx.dim() == 3 && dx.size(0) == B && dx.size(1) == T && dx.size(2) == D && dx.stride(2) == 1, "out view");
+  } else {
+    dx = torch::empty({B, T, D}, x.options());
+  }
+  const float* rp = nullptr;
+  long rB = 0, rT = 0;
+  if (dres.has_value() && dres->defined()) {
+    TORCH_CHECK(dres->dim() == 3 && dres->size(0) == B && dres->size(1) == T && dres->stride(2) == 1, "dres view");
+    rp = dres->data_ptr<float>();
+    rB = dres->stride(0);
+    rT = dres->stride(1);
+  }
   const bool dyb = dy.scalar_type() == torch::kBFloat16;
   TORCH_CHECK(dyb || dy.scalar_type() == torch::kFloat32, "dy dtype");
   auto ws = torch::empty({accum ? (long)jm_layernorm_bwd_blocks(B * T) * 2 * D : 1}, x.options());
   check_rc(jm_layernorm_bwd(dy.data_ptr(), dyb, x.data_ptr<float>(), x.stride(0), x.stride(1), B, T, D,
                             mean.data_ptr<float>(), rstd.data_ptr<float>(), gamma.data_ptr<float>(),
-                            dx.data_ptr<float>(), dgamma.data_ptr<float>(), dbeta.data_ptr<float>(), accum,
-                            ws.data_ptr<float>(), stream()),
+                            dx.data_ptr<float>(), dx.stride(0), dx.stride(1), rp, rB, rT, dgamma.data_ptr<float>(),
+                            dbeta.data_ptr<float>(), accum, ws.data_ptr<float>(), stream()),
            "layernorm_bwd");
   return dx;
 }
@@ -133,30 +149,37 @@ void splitk_reduce_add(torch::Tensor part, torch::Tensor g) {
 }
 
 torch::Tensor residual_fwd(torch::Tensor x, torch::Tensor y, c10::optional<torch::Tensor> scale,
-                           c10::optional<torch::Tensor> mask) {
+                           c10::optional<torch::Tensor> mask, c10::optional<torch::Tensor> out_opt) {
   TORCH_CHECK(x.dim() == 3 && x.stride(2) == 1, "x must be [B,T,D]");
   CHECK_DT(x, torch::kFloat32);
   CHECK_CONTIG(y);
   CHECK_DT(y, torch::kBFloat16);
   const int B = x.size(0), T = x.size(1), D = x.size(2);
-  auto out = torch::empty({B, T, D}, x.options());
+  torch::Tensor out;
+  if (out_opt.has_value() && out_opt->defined()) {
+    out = *out_opt;
+    TORCH_CHECK(out.dim() == 3 && out.size(0) == B && out.size(1) == T && out.size(2) == D && out.stride(2) == 1,
+                "out view");
+  } else {
+    out = torch::empty({B, T, D}, x.options());
+  }
   check_rc(jm_residual_fwd(x.data_ptr<float>(), x.stride(0), x.stride(1), B, T, D, bf(y), fopt(scale), fopt(mask),
-                           out.data_ptr<float>(), stream()),
+                           out.data_ptr<float>(), out.stride(0), out.stride(1), stream()),
            "residual_fwd");
   return out;
 }
 
 torch::Tensor residual_bwd(torch::Tensor dout, c10::optional<torch::Tensor> y, c10::optional<torch::Tensor> scale,
                            c10::optional<torch::Tensor> mask, c10::optional<torch::Tensor> dscale, py::object ydtype) {
-  CHECK_CONTIG(dout);
+  TORCH_CHECK(dout.dim() == 3 && dout.stride(2) == 1, "dout must be a [B,T,D] view");
   CHECK_DT(dout, torch::kFloat32);
   const int B = dout.size(0), T = dout.size(1), D = dout.size(2);
   const auto odt = torch::python::detail::py_object_to_dtype(ydtype);
   TORCH_CHECK(odt == torch::kBFloat16, "residual_bwd: y must be bf16");
   auto dy = torch::empty({(long)B * T, D}, dout.options().dtype(odt));
   const uint16_t* yp = (y.has_value() && y->defined()) ? bf(*y) : nullptr;
-  check_rc(jm_residual_bwd(dout.data_ptr<float>(), yp, fopt(scale), fopt(mask), fopt_m(dscale), bfm(dy), B, T, D,
-                           stream()),
+  check_rc(jm_residual_bwd(dout.data_ptr<float>(), dout.stride(0), dout.stride(1), yp, fopt(scale), fopt(mask),
+                           fopt_m(dscale), bfm(dy), B, T, D, stream()),
            "residual_bwd");
   return dy;
 }
@@ -251,12 +274,15 @@ torch::Tensor patchify_normalize(torch::Tensor img, int64_t p) {
 PYBIND11_MODULE(_C, m) {
   m.doc() = "jumbo_mae_tpu_amd CDNA4 (gfx950) HIP kernels";
   m.def("layernorm_fwd", &layernorm_fwd);
-  m.def("layernorm_bwd", &layernorm_bwd);
+  m.def("layernorm_bwd", &layernorm_bwd, py::arg("dy"), py::arg("x"), py::arg("mean"), py::arg("rstd"),
+        py::arg("gamma"), py::arg("dgamma"), py::arg("dbeta"), py::arg("accum"), py::arg("dres") = py::none(),
+        py::arg("out") = py::none());
   m.def("gelu_fwd", &gelu_fwd);
   m.def("gelu_bwd", &gelu_bwd, py::arg("h"), py::arg("da"), py::arg("bias_grad") = py::none());
   m.def("colsum", &colsum);
   m.def("splitk_reduce_add", &splitk_reduce_add);
-  m.def("residual_fwd", &residual_fwd);
+  m.def("residual_fwd", &residual_fwd, py::arg("x"), py::arg("y"), py::arg("scale"), py::arg("mask"),
+        py::arg("out") = py::none());
   m.def("residual_bwd", &residual_bwd);
   m.def("attn_fwd", &attn_fwd);
   m.def("attn_bwd", &attn_bwd);

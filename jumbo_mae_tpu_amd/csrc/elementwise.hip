@@ -59,7 +59,7 @@ template <int MODE>
 __global__ __launch_bounds__(256) void rowcol_kernel(const void* __restrict__ in0, const uint16_t* __restrict__ in1,
                                                      uint16_t* __restrict__ out, float* __restrict__ acc,
                                                      const float* __restrict__ scale, const float* __restrict__ mask,
-                                                     int M, int N, int T, int rows_per_block) {
+                                                     int M, int N, int T, int rows_per_block, long sB, long sT) {
   extern __shared__ __attribute__((aligned(16))) float red_s[];  // [<= 2048] block's columns
   // 2-D grid: blockIdx.y picks a chunk of <= 2048 columns, blockIdx.x a slab of rows
   const int c0 = blockIdx.y * 2048;
@@ -105,8 +105,8 @@ __global__ __launch_bounds__(256) void rowcol_kernel(const void* __restrict__ in
             } else if (MODE == 1) {
               load8((const uint16_t*)in0 + off, a[u]);
               load8(in1 + off, b[u]);
-            } else {
-              load8((const float*)in0 + off, a[u]);
+            } else {  // dout is a [B, T, D] view with strides (sB, sT, 1)
+              load8((const float*)in0 + (r / T) * sB + (r % T) * sT + col, a[u]);
               if (scale) load8(in1 + off, b[u]);
             }
           }
@@ -156,7 +156,7 @@ __global__ __launch_bounds__(256) void residual_fwd_kernel(const float* __restri
                                                            const uint16_t* __restrict__ y,
                                                            const float* __restrict__ scale,
                                                            const float* __restrict__ mask, float* __restrict__ out,
-                                                           int rows, int D) {
+                                                           int rows, int D, long oB, long oT) {
   const int cgs = D / 8;
   const long total = (long)rows * cgs;
   for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
@@ -175,7 +175,7 @@ __global__ __launch_bounds__(256) void residual_fwd_kernel(const float* __restri
     }
 #pragma unroll
     for (int j = 0; j < 8; ++j) xv[j] += m * sc[j] * yv[j];
-    store8(out + (long)row * D + col, xv);
+    store8(out + b * oB + t * oT + col, xv);
   }
 }
 
@@ -188,7 +188,7 @@ int grid_for(long work, int per_thread_items = 1) {
 
 template <int MODE>
 void launch_rowcol(const void* in0, const uint16_t* in1, uint16_t* out, float* acc, const float* scale,
-                   const float* mask, int M, int N, int T, hipStream_t st) {
+                   const float* mask, int M, int N, int T, hipStream_t st, long sB = 0, long sT = 0) {
   // 2-D grid: column chunks of 2048 x row slabs; each row-slot walks >= 16 rows, ~2048 blocks
   // in total so the per-block column atomics stay cheap
   const int ncol = (N + 2047) / 2048;
@@ -204,7 +204,8 @@ void launch_rowcol(const void* in0, const uint16_t* in1, uint16_t* out, float* a
   }
   if (nb < 1) nb = 1;
   const size_t smem = acc ? 2048 * sizeof(float) : 0;
-  rowcol_kernel<MODE><<<dim3(nb, ncol), 256, smem, st>>>(in0, in1, out, acc, scale, mask, M, N, T, rows_per_block);
+  rowcol_kernel<MODE><<<dim3(nb, ncol), 256, smem, st>>>(in0, in1, out, acc, scale, mask, M, N, T, rows_per_block,
+                                                          sB, sT);
 }
 
 }  // namespace
@@ -229,17 +230,17 @@ int jm_colsum_bf16(const uint16_t* x, float* acc, int M, int N, hipStream_t st) 
 }
 
 int jm_residual_fwd(const float* x, long sB, long sT, int B, int T, int D, const uint16_t* y, const float* scale,
-                    const float* mask, float* out, hipStream_t st) {
+                    const float* mask, float* out, long oB, long oT, hipStream_t st) {
   if (D % 8) return -1;
   const long work = (long)B * T * (D / 8);
-  residual_fwd_kernel<<<grid_for(work), 256, 0, st>>>(x, sB, sT, T, y, scale, mask, out, B * T, D);
+  residual_fwd_kernel<<<grid_for(work), 256, 0, st>>>(x, sB, sT, T, y, scale, mask, out, B * T, D, oB, oT);
   return 0;
 }
 
-int jm_residual_bwd(const float* dout, const uint16_t* y, const float* scale, const float* mask, float* dscale,
-                    uint16_t* dy, int B, int T, int D, hipStream_t st) {
+int jm_residual_bwd(const float* dout, long dB, long dT, const uint16_t* y, const float* scale, const float* mask,
+                    float* dscale, uint16_t* dy, int B, int T, int D, hipStream_t st) {
   if (D % 8) return -1;
-  launch_rowcol<2>(dout, y, dy, dscale, scale, mask, B * T, D, T, st);
+  launch_rowcol<2>(dout, y, dy, dscale, scale, mask, B * T, D, T, st, dB, dT);
   return 0;
 }
 

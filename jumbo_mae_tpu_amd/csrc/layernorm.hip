@@ -70,11 +70,20 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const float* __restrict__ x
   }
 }
 
+// dx output and optional residual-gradient input, both [B, T, D] views with their own strides:
+// dx = LN'(dy) (+ dres), i.e. the residual-stream gradient add is fused into the LN backward.
+struct LnBwdIO {
+  float* dx;
+  long oB, oT;
+  const float* dres;
+  long rB, rT;
+};
+
 template <int V, typename TI>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(const TI* __restrict__ dy, const float* __restrict__ x,
                                                      long sB, long sT, int T, int rows, int D,
                                                      const float* __restrict__ mean, const float* __restrict__ rstd,
-                                                     const float* __restrict__ gamma, float* __restrict__ dx,
+                                                     const float* __restrict__ gamma, LnBwdIO io,
                                                      float* __restrict__ dgamma, float* __restrict__ dbeta,
                                                      int accum_params) {
   extern __shared__ __attribute__((aligned(16))) float red[];  // [2*D]
@@ -121,14 +130,16 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const TI* __restrict__ dy, 
     }
     sg = wave_sum(sg) / D;
     sgx = wave_sum(sgx) / D;
-    float* dxr = dx + (long)row * D;
+    float* dxr = io.dx + b * io.oB + t * io.oT;
+    const float* rr = io.dres ? io.dres + b * io.rB + t * io.rT : nullptr;
 #pragma unroll
     for (int i = 0; i < V; ++i) {
       const int col = (i * 64 + lane) * 4;
       if (col < D) {
-        float o[4];
+        float o[4], rv[4] = {0.f, 0.f, 0.f, 0.f};
+        if (rr) load4(rr + col, rv);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) o[j] = rs * (g[i][j] - sg - xh[i][j] * sgx);
+        for (int j = 0; j < 4; ++j) o[j] = rs * (g[i][j] - sg - xh[i][j] * sgx) + rv[j];
         store4(dxr + col, o);
       }
     }
@@ -209,7 +220,7 @@ void launch_fwd(int V, dim3 grid, hipStream_t st, const float* x, long sB, long 
 
 template <typename TI>
 void launch_bwd(int V, dim3 grid, size_t smem, hipStream_t st, const TI* dy, const float* x, long sB, long sT,
-                int T, int rows, int D, const float* m, const float* r, const float* g, float* dx, float* dg,
+                int T, int rows, int D, const float* m, const float* r, const float* g, LnBwdIO dx, float* dg,
                 float* db, int acc) {
 #define JM_LNB(VV)                                                                                  \
   case VV:                                                                                          \
@@ -255,8 +266,10 @@ int jm_layernorm_bwd_blocks(int rows) {
 }
 
 int jm_layernorm_bwd(const void* dy, int dy_bf16, const float* x, long sB, long sT, int B, int T, int D,
-                     const float* mean, const float* rstd, const float* gamma, float* dx, float* dgamma,
-                     float* dbeta, int accum_params, float* ws, hipStream_t st) {
+                     const float* mean, const float* rstd, const float* gamma, float* dx_ptr, long oB, long oT,
+                     const float* dres, long rB, long rT, float* dgamma, float* dbeta, int accum_params, float* ws,
+                     hipStream_t st) {
+  const LnBwdIO dx{dx_ptr, oB, oT, dres, rB, rT};
   const int V = pick_v(D);
   if (V < 0 || (D % 4) != 0) return -1;
   const int rows = B * T;

@@ -19,15 +19,23 @@ embedding and only the kept patches are embedded (bit-for-bit the same math as e
 from __future__ import annotations
 
 import math
+import os
 
 import numpy as np
 import torch
 
 from ..config import DecoderConfig, ViTConfig
+from ..ops import blocks
 from ..ops import functional as Fn
 from ..ops.params_fn import param_value
 from ..utils.posemb import fixed_sincos2d_embeddings
 from .params import Handle, ParamStore, const_, ones_, trunc_normal_, trunc_normal_t, zeros_
+
+
+def use_fused_blocks() -> bool:
+    """One autograd node per transformer block (ops/blocks.py); JMAE_PER_OP=1 selects the per-op
+    autograd graph instead (same kernels, used by tests to cross-check the hand-written backward)."""
+    return os.environ.get("JMAE_PER_OP", "0") != "1"
 
 
 # ------------------------------------------------------------------------- layout helpers
@@ -158,6 +166,11 @@ class JumboLayer:
         B, S, D = x.shape
         C = self.C
         p = self.cfg.droppath
+        if use_fused_blocks() and (self.cfg.dropout <= 0.0 or det):
+            m1 = droppath_mask(p, B, rng, x.device, det)
+            m3 = droppath_mask(p, B, rng, x.device, det)
+            m2 = droppath_mask(p, B, rng, x.device, det)
+            return blocks.jumbo_block(self, x, m1, m2, m3)
         h = self.norm1(x)
         a = self.attn(h, B, S, rng, det)
         x = Fn.residual(x, a, self.scale1, droppath_mask(p, B, rng, x.device, det))
@@ -192,6 +205,10 @@ class ViTLayer:
 
     def __call__(self, x, rng=None, det=True):
         B, S, D = x.shape
+        if use_fused_blocks() and (self.attn.dropout <= 0.0 or det):
+            m1 = droppath_mask(self.droppath, B, rng, x.device, det)
+            m2 = droppath_mask(self.droppath, B, rng, x.device, det)
+            return blocks.vit_block(self, x, m1, m2)
         h = self.norm1(x)
         a = self.attn(h, B, S, rng, det)
         x = Fn.residual(x, a, self.scale1, droppath_mask(self.droppath, B, rng, x.device, det))

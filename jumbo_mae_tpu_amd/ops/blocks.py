@@ -1,0 +1,163 @@
+"""Fused transformer-block autograd Functions (one autograd node per layer).
+
+A block's forward is a fixed chain of fused kernels and GEMMs; its backward is written out by
+hand so that (i) the residual-stream gradient never goes through autograd's generic adds,
+slice-backward zero fills or concat copies -- the passthrough add is fused into the LayerNorm
+backward kernel and the CLS / patch halves of the Jumbo merge are read and written as strided
+views in place; (ii) exactly the tensors the kernels need are saved; (iii) every parameter
+gradient is accumulated straight into the flat fp32 buffer and the DP reducer is told as soon as
+it is final.
+
+JumboBlock = JumboLayer (/root/reference/src/modeling.py:169-206):
+    x1 = x + dp1(s1 * Attn(LN1 x))
+    c  = LN3(x1[:, :3].reshape(B, 3D));  c' = c + dp3(s3 * JumboMLP(c))     (shared MLP)
+    p' = x1[:, 3:] + dp2(s2 * FF(LN2 x1[:, 3:]))
+    x2 = concat(c'.reshape(B, 3, D), p')
+ViTBlock = ViTLayer (modeling.py:150-167), the MAE decoder block.
+"""
+
+from __future__ import annotations
+
+import torch
+
+from . import prims as P
+
+
+def _attn_fwd(attn, h1, B, S):
+    qkv = P.linear_fwd(h1, attn.qkv_k, attn.qkv_b)
+    o, lse = P.attn_fwd(qkv.view(B, S, -1), attn.heads)
+    a = P.linear_fwd(o.view(B * S, -1), attn.wo_k, attn.wo_b)
+    return qkv, o, lse, a
+
+
+def _attn_bwd(attn, da, h1, qkv, o, lse, B, S):
+    do = P.linear_bwd(da, o.view(B * S, -1), attn.wo_k, attn.wo_b)
+    dqkv = P.attn_bwd(do, qkv.view(B, S, -1), o, lse, attn.heads)
+    return P.linear_bwd(dqkv.view(B * S, -1), h1, attn.qkv_k, attn.qkv_b)
+
+
+def _ff_fwd(ff, h):
+    pre = P.linear_fwd(h, ff.w1.k, ff.w1.b)
+    g = P.gelu_fwd(pre)
+    y = P.linear_fwd(g, ff.w2.k, ff.w2.b)
+    return pre, g, y
+
+
+def _ff_bwd(ff, dy, h, pre, g):
+    dg = P.linear_bwd(dy, g, ff.w2.k, ff.w2.b)
+    dpre, bias_done = P.gelu_bwd(pre, dg, ff.w1.b if ff.w1.k.segs[0].trainable else None)
+    return P.linear_bwd(dpre, h, ff.w1.k, ff.w1.b, bias_done=bias_done)
+
+
+def _note_uses(*handles):
+    for h in handles:
+        if h is not None:
+            h.note_use()
+
+
+def _attn_handles(attn):
+    return (attn.qkv_k, attn.qkv_b, attn.wo_k, attn.wo_b)
+
+
+def _ff_handles(ff):
+    return (ff.w1.k, ff.w1.b, ff.w2.k, ff.w2.b)
+
+
+class JumboBlockFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, anchor, layer, m1, m2, m3):
+        B, S, D = x.shape
+        C = layer.C
+        J = C * D
+        dt = layer.norm1.g.store.compute_dtype
+        h1, mu1, rs1 = P.ln_fwd(x, layer.norm1.g, layer.norm1.b, dt)
+        qkv, o, lse, a = _attn_fwd(layer.attn, h1, B, S)
+        x1 = P.residual_fwd(x, a, layer.scale1, m1)
+        # jumbo branch: LN3 on the concatenated CLS tokens, residual on the *normalized* value
+        cls_in = x1[:, :C].reshape(B, 1, J)
+        hc, muc, rsc = P.ln_fwd(cls_in, layer.norm3.g, layer.norm3.b, torch.float32)
+        hcb = hc.to(dt)
+        jpre, jg, jy = _ff_fwd(layer.jumbo_mlp, hcb)
+        # patch branch
+        pin = x1[:, C:]
+        hp, mup, rsp = P.ln_fwd(pin, layer.norm2.g, layer.norm2.b, dt)
+        fpre, fg, fy = _ff_fwd(layer.ff, hp)
+        x2 = torch.empty_like(x1)
+        P.residual_fwd(hc.view(B, 1, J), jy, layer.scale3, m3, out=x2[:, :C].reshape(B, 1, J))
+        P.residual_fwd(pin, fy, layer.scale2, m2, out=x2[:, C:])
+        ctx.save_for_backward(x, mu1, rs1, h1, qkv, o, lse, a, x1, muc, rsc, hcb, jpre, jg, jy,
+                              hp, mup, rsp, fpre, fg, fy, m1, m2, m3)
+        ctx.layer = layer
+        return x2
+
+    @staticmethod
+    def backward(ctx, dx2):
+        (x, mu1, rs1, h1, qkv, o, lse, a, x1, muc, rsc, hcb, jpre, jg, jy,
+         hp, mup, rsp, fpre, fg, fy, m1, m2, m3) = ctx.saved_tensors
+        layer = ctx.layer
+        B, S, D = x.shape
+        C = layer.C
+        J = C * D
+        dt = h1.dtype
+        dx2 = dx2.contiguous()
+        dx1 = torch.empty_like(dx2)
+        # ---- patch branch: dx1[:, C:] = dx2[:, C:] + LN2'(FF'(s2 * dp2 * dx2[:, C:]))
+        dfy = P.residual_bwd(dx2[:, C:], fy, layer.scale2, m2, dt)
+        dhp = _ff_bwd(layer.ff, dfy, hp, fpre, fg)
+        P.ln_bwd(dhp, x1[:, C:], mup, rsp, layer.norm2.g, layer.norm2.b, dres=dx2[:, C:], out=dx1[:, C:])
+        # ---- jumbo branch: d hc = dx2_cls + JumboMLP'(s3 * dp3 * dx2_cls); dx1_cls = LN3'(d hc)
+        dcls = dx2[:, :C].reshape(B, 1, J)
+        djy = P.residual_bwd(dcls, jy, layer.scale3, m3, dt)
+        dhcb = _ff_bwd(layer.jumbo_mlp, djy, hcb, jpre, jg)
+        dhc = dcls.reshape(B, J) + dhcb.float()
+        P.ln_bwd(dhc, x1[:, :C].reshape(B, 1, J), muc, rsc, layer.norm3.g, layer.norm3.b,
+                 out=dx1[:, :C].reshape(B, 1, J))
+        # ---- attention branch: dx = dx1 + LN1'(Attn'(s1 * dp1 * dx1))
+        da = P.residual_bwd(dx1, a, layer.scale1, m1, dt)
+        dh1 = _attn_bwd(layer.attn, da, h1, qkv, o, lse, B, S)
+        dx = P.ln_bwd(dh1, x, mu1, rs1, layer.norm1.g, layer.norm1.b, dres=dx1, out=dx1)
+        return dx, None, None, None, None, None
+
+
+def jumbo_block(layer, x, m1=None, m2=None, m3=None):
+    _note_uses(layer.norm1.g, layer.norm1.b, layer.norm2.g, layer.norm2.b, layer.norm3.g, layer.norm3.b,
+               layer.scale1, layer.scale2, layer.scale3, *_attn_handles(layer.attn), *_ff_handles(layer.ff),
+               *_ff_handles(layer.jumbo_mlp))
+    return JumboBlockFn.apply(x.contiguous(), layer.norm1.g.param, layer, m1, m2, m3)
+
+
+class ViTBlockFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, anchor, layer, m1, m2):
+        B, S, D = x.shape
+        dt = layer.norm1.g.store.compute_dtype
+        h1, mu1, rs1 = P.ln_fwd(x, layer.norm1.g, layer.norm1.b, dt)
+        qkv, o, lse, a = _attn_fwd(layer.attn, h1, B, S)
+        x1 = P.residual_fwd(x, a, layer.scale1, m1)
+        h2, mu2, rs2 = P.ln_fwd(x1, layer.norm2.g, layer.norm2.b, dt)
+        fpre, fg, fy = _ff_fwd(layer.ff, h2)
+        x2 = P.residual_fwd(x1, fy, layer.scale2, m2)
+        ctx.save_for_backward(x, mu1, rs1, h1, qkv, o, lse, a, x1, mu2, rs2, h2, fpre, fg, fy, m1, m2)
+        ctx.layer = layer
+        return x2
+
+    @staticmethod
+    def backward(ctx, dx2):
+        x, mu1, rs1, h1, qkv, o, lse, a, x1, mu2, rs2, h2, fpre, fg, fy, m1, m2 = ctx.saved_tensors
+        layer = ctx.layer
+        B, S, D = x.shape
+        dt = h1.dtype
+        dx2 = dx2.contiguous()
+        dfy = P.residual_bwd(dx2, fy, layer.scale2, m2, dt)
+        dh2 = _ff_bwd(layer.ff, dfy, h2, fpre, fg)
+        dx1 = P.ln_bwd(dh2, x1, mu2, rs2, layer.norm2.g, layer.norm2.b, dres=dx2)  # never write autograd's dx2
+        da = P.residual_bwd(dx1, a, layer.scale1, m1, dt)
+        dh1 = _attn_bwd(layer.attn, da, h1, qkv, o, lse, B, S)
+        dx = P.ln_bwd(dh1, x, mu1, rs1, layer.norm1.g, layer.norm1.b, dres=dx1, out=dx1)
+        return dx, None, None, None, None
+
+
+def vit_block(layer, x, m1=None, m2=None):
+    _note_uses(layer.norm1.g, layer.norm1.b, layer.norm2.g, layer.norm2.b, layer.scale1, layer.scale2,
+               *_attn_handles(layer.attn), *_ff_handles(layer.ff))
+    return ViTBlockFn.apply(x.contiguous(), layer.norm1.g.param, layer, m1, m2)

@@ -1,0 +1,233 @@
+"""Raw (non-autograd) primitives of the hot path with device dispatch.
+
+GPU: fused CDNA4 HIP kernels (``jumbo_mae_tpu_amd._C``) + hipBLASLt GEMMs.  CPU: plain fp32
+PyTorch that transcribes the reference math (the oracle).  Both the per-op autograd Functions
+(ops/functional.py) and the fused transformer-block Functions (ops/blocks.py) are built from
+these, so there is exactly one implementation of every op per device.
+
+Parameter-gradient side effects: every ``*_bwd`` accumulates the gradients of the parameters it
+owns into the flat fp32 gradient buffer and signals readiness to the data-parallel reducer.
+"""
+
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn.functional as F
+
+from ..models.params import Handle
+from . import _ext
+
+LN_EPS = 1e-6
+_GELU_C = math.sqrt(2.0 / math.pi)
+
+
+def hip(t: torch.Tensor) -> bool:
+    return _ext.use_hip(t)
+
+
+def _trainable(h: Handle | None) -> bool:
+    return h is not None and h.segs[0].trainable
+
+
+# ------------------------------------------------------------------------------ GEMMs
+def wgrad_split(M: int, N: int, K: int) -> int:
+    """Split-K factor for a weight-gradient GEMM (reduction over M tokens, N x K output).
+
+    A wgrad output is small (0.25-38 M elements) while its reduction is 25k-100k long, so one
+    GEMM has only 4-200 256x256 output tiles for 256 CUs (measured 160-690 TF/s on MI355X,
+    profiles/r1_gemm_wgrad_alternatives.log).  Splitting M into S chunks of one strided-batched
+    GEMM gives S x tiles workgroups (fp32 partials, summed by one fused pass)."""
+    tiles = max(1, (N // 256) * (K // 256))
+    s = 1
+    while s < 16 and tiles * s * 2 <= 256 and M % (s * 2) == 0 and M // (s * 2) >= 2048:
+        s *= 2
+    return s
+
+
+def wgrad(h: Handle, dy: torch.Tensor, x: torch.Tensor) -> None:
+    """grad[h] += dy^T @ x  (fp32 accumulate; bf16 inputs on GPU)."""
+    g = h.grad
+    if dy.is_cuda and dy.dtype != torch.float32:
+        M, N = dy.shape
+        K = x.shape[1]
+        s = wgrad_split(M, N, K)
+        if s > 1:
+            part = torch.bmm(dy.view(s, M // s, N).transpose(1, 2), x.view(s, M // s, K), out_dtype=torch.float32)
+            if hip(part):
+                _ext.load().splitk_reduce_add(part, g)
+            else:
+                g.add_(part.sum(0))
+        else:
+            torch.addmm(g, dy.t(), x, out_dtype=torch.float32, out=g)
+    else:
+        g.addmm_(dy.t().float(), x.float())
+
+
+def bias_grad(hb: Handle, dy: torch.Tensor) -> None:
+    if hip(dy):
+        _ext.load().colsum(dy, hb.grad)
+    else:
+        hb.grad.add_(dy.sum(0, dtype=torch.float32))
+
+
+def linear_fwd(x2: torch.Tensor, hw: Handle, hb: Handle | None) -> torch.Tensor:
+    w = hw.weight()
+    if hb is not None:
+        return torch.addmm(hb.weight(), x2, w.t())
+    return x2 @ w.t()
+
+
+def linear_bwd(dy: torch.Tensor, x2: torch.Tensor, hw: Handle, hb: Handle | None, need_dx: bool = True,
+               bias_done: bool = False):
+    """dx = dy @ W (if needed); grad W += dy^T x; grad b += colsum(dy) (unless fused upstream)."""
+    dx = dy @ hw.weight() if need_dx else None
+    if _trainable(hw):
+        wgrad(hw, dy, x2)
+        hw.ready()
+        if hb is not None:
+            if not bias_done:
+                bias_grad(hb, dy)
+            hb.ready()
+    return dx
+
+
+# ------------------------------------------------------------------------------ gelu
+def gelu_fwd(h: torch.Tensor) -> torch.Tensor:
+    if hip(h):
+        return _ext.load().gelu_fwd(h)
+    return F.gelu(h, approximate="tanh")
+
+
+def gelu_bwd(h: torch.Tensor, da: torch.Tensor, hb: Handle | None = None) -> tuple[torch.Tensor, bool]:
+    """dh = da * gelu'(h); when ``hb`` is given its bias gradient (colsum dh) is fused in.
+    Returns (dh, bias_done)."""
+    if hip(h):
+        bg = hb.grad if _trainable(hb) else None
+        return _ext.load().gelu_bwd(h, da.contiguous(), bg), bg is not None
+    hf = h.float()
+    u = _GELU_C * (hf + 0.044715 * hf ** 3)
+    t = torch.tanh(u)
+    d = 0.5 * (1 + t) + 0.5 * hf * (1 - t * t) * _GELU_C * (1 + 3 * 0.044715 * hf * hf)
+    return (da.float() * d).to(h.dtype), False
+
+
+# ------------------------------------------------------------------------------ layernorm
+def ln_fwd(x3: torch.Tensor, hg: Handle, hb: Handle, out_dtype):
+    """x3: fp32 [B, T, D] view -> (y [B*T, D], mean, rstd)."""
+    B, T, D = x3.shape
+    if hip(x3):
+        return _ext.load().layernorm_fwd(x3, hg.master, hb.master, LN_EPS, out_dtype)
+    xf = x3.reshape(B * T, D).float()
+    mean = xf.mean(-1)
+    var = (xf - mean[:, None]).square().mean(-1)
+    rstd = torch.rsqrt(var + LN_EPS)
+    y = ((xf - mean[:, None]) * rstd[:, None] * hg.master + hb.master).to(out_dtype)
+    return y, mean, rstd
+
+
+def ln_bwd(dy: torch.Tensor, x3: torch.Tensor, mean, rstd, hg: Handle, hb: Handle, dres=None, out=None):
+    """dx = LN'(dy) (+ dres) written to ``out`` (a [B,T,D] view) or a new tensor; accumulates
+    dgamma / dbeta."""
+    B, T, D = x3.shape
+    dy = dy.contiguous()
+    tr = _trainable(hg)
+    if hip(x3):
+        dx = _ext.load().layernorm_bwd(dy, x3, mean, rstd, hg.master, hg.grad, hb.grad, tr, dres, out)
+    else:
+        xf = x3.reshape(B * T, D).float()
+        xhat = (xf - mean[:, None]) * rstd[:, None]
+        dyf = dy.reshape(B * T, D).float()
+        if tr:
+            hg.grad.add_((dyf * xhat).sum(0))
+            hb.grad.add_(dyf.sum(0))
+        g = dyf * hg.master
+        dx = rstd[:, None] * (g - g.mean(-1, keepdim=True) - xhat * (g * xhat).mean(-1, keepdim=True))
+        dx = dx.reshape(B, T, D)
+        if dres is not None:
+            dx = dx + dres
+        if out is not None:
+            out.copy_(dx)
+            dx = out
+    if tr:
+        hg.ready()
+        hb.ready()
+    return dx
+
+
+# ------------------------------------------------------------------------------ residual
+def residual_fwd(x3: torch.Tensor, y2: torch.Tensor, hs: Handle | None, mask, out=None) -> torch.Tensor:
+    """out[b,t] = x[b,t] + mask[b] * s * y[b*T+t]  (x, out: fp32 [B,T,D] views)."""
+    B, T, D = x3.shape
+    if hip(x3):
+        return _ext.load().residual_fwd(x3, y2.reshape(B * T, D), hs.master if hs is not None else None, mask, out)
+    r = y2.float().reshape(B, T, D)
+    if hs is not None:
+        r = r * hs.master
+    if mask is not None:
+        r = r * mask.view(B, 1, 1)
+    res = x3.float() + r
+    if out is not None:
+        out.copy_(res)
+        return out
+    return res
+
+
+def residual_bwd(dout3: torch.Tensor, y2: torch.Tensor | None, hs: Handle | None, mask, ydtype) -> torch.Tensor:
+    """dy = mask[b] * s * dout (in ``ydtype``); ds += sum mask*dout*y."""
+    B, T, D = dout3.shape
+    if hs is None and mask is None:
+        dy = dout3.reshape(B * T, D).to(ydtype)
+    elif hip(dout3) and ydtype == torch.bfloat16:
+        dy = _ext.load().residual_bwd(dout3, y2, hs.master if hs is not None else None, mask,
+                                      hs.grad if _trainable(hs) else None, ydtype)
+    else:
+        d = dout3.float()
+        if mask is not None:
+            d = d * mask.view(B, 1, 1)
+        if hs is not None:
+            if _trainable(hs):
+                hs.grad.add_((d * y2.float().reshape(B, T, D)).sum((0, 1)))
+            d = d * hs.master
+        dy = d.reshape(B * T, D).to(ydtype)
+    if _trainable(hs):
+        hs.ready()
+    return dy
+
+
+# ------------------------------------------------------------------------------ attention
+def attn_fwd(qkv: torch.Tensor, heads: int):
+    """qkv [B, S, 3*D] -> (o [B, S, D], lse [B, H, S])."""
+    B, S, three_d = qkv.shape
+    D = three_d // 3
+    hd = D // heads
+    if hip(qkv):
+        return _ext.load().attn_fwd(qkv, heads)
+    q, k, v = qkv.float().view(B, S, 3, heads, hd).unbind(2)
+    z = torch.einsum("bqhd,bkhd->bhqk", q / math.sqrt(hd), k)
+    lse = torch.logsumexp(z, -1)
+    p = torch.exp(z - lse[..., None])
+    o = torch.einsum("bhqk,bkhd->bqhd", p, v).reshape(B, S, D).to(qkv.dtype)
+    return o, lse
+
+
+def attn_bwd(do: torch.Tensor, qkv: torch.Tensor, o: torch.Tensor, lse: torch.Tensor, heads: int) -> torch.Tensor:
+    B, S, three_d = qkv.shape
+    D = three_d // 3
+    hd = D // heads
+    do = do.contiguous().view(B, S, D)
+    if hip(qkv):
+        return _ext.load().attn_bwd(do, qkv, o, lse, heads)
+    q, k, v = qkv.float().view(B, S, 3, heads, hd).unbind(2)
+    dof = do.float().view(B, S, heads, hd)
+    sc = 1.0 / math.sqrt(hd)
+    z = torch.einsum("bqhd,bkhd->bhqk", q * sc, k)
+    p = torch.exp(z - lse[..., None])
+    dv = torch.einsum("bhqk,bqhd->bkhd", p, dof)
+    dp = torch.einsum("bqhd,bkhd->bhqk", dof, v)
+    delta = (dof * o.float().view(B, S, heads, hd)).sum(-1).permute(0, 2, 1)
+    ds = p * (dp - delta[..., None])
+    dq = torch.einsum("bhqk,bkhd->bqhd", ds, k) * sc
+    dk = torch.einsum("bhqk,bqhd->bkhd", ds, q) * sc
+    return torch.stack([dq, dk, dv], 2).reshape(B, S, three_d).to(qkv.dtype)

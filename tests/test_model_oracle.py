@@ -88,3 +88,27 @@ def test_finetune_grads_match_oracle():
     ref.backward()
     assert abs(out["loss"].item() - ref.item()) < 1e-5
     _grads_match(m.store, tp)
+
+
+def test_fused_blocks_match_per_op_with_droppath(monkeypatch):
+    """The hand-written block backward (ops/blocks.py) == autograd over the per-op graph,
+    with droppath + layerscale active (same RNG draws -> same masks)."""
+    from jumbo_mae_tpu_amd.utils.rng import RngStreams
+    vc = ViTConfig(layers=2, dim=32, heads=4, labels=0, image_size=32, patch_size=8, posemb="sincos2d",
+                   layerscale=True, droppath=0.3)
+    dc = DecoderConfig(dec_layers=2, dec_dim=16, dec_heads=2, image_size=32, patch_size=8, dec_layerscale=True,
+                       dec_droppath=0.3)
+    imgs = torch.randint(0, 256, (4, 3, 32, 32), dtype=torch.uint8)
+    noise = torch.rand(16)
+    res = []
+    for per_op in ("0", "1"):
+        monkeypatch.setenv("JMAE_PER_OP", per_op)
+        m = PretrainModel(vc, dc).to("cpu", seed=0)
+        with torch.no_grad():
+            m.store.master.add_(torch.linspace(-0.02, 0.02, m.store.total))
+        rng = RngStreams({"dropout": 5}, 0, "cpu").as_dict()
+        loss = m(imgs, rngs=rng, noise=noise)["loss"]
+        loss.backward()
+        res.append((loss.item(), m.store.grad.clone()))
+    assert abs(res[0][0] - res[1][0]) < 1e-6
+    assert torch.allclose(res[0][1], res[1][1], atol=1e-6, rtol=1e-4)
