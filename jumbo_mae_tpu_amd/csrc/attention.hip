@@ -191,7 +191,11 @@ __global__ __launch_bounds__((64 * bwd_waves<HD, SP>())) void attn_bwd_kernel(co
                                                        const uint16_t* __restrict__ o,
                                                        const uint16_t* __restrict__ dO,
                                                        const float* __restrict__ lse,
-                                                       uint16_t* __restrict__ dqkv, int S, int H, float scale) {
+                                                       uint16_t* __restrict__ dqkv, int S, int H, float scale,
+                                                       float* __restrict__ dbp) {
+  // dbp (optional): per-sample partial column sums of dqkv, [B][3*H*HD] fp32 -- the QKV Dense
+  // bias gradient fused in (summed over b by jm_splitk_reduce_add), taken from the fp32 MFMA
+  // accumulators so dqkv is never re-read.
   constexpr int RS = HD + 8;  // row-major image stride
   constexpr int TS = SP + 8;  // transposed image stride
   constexpr int NT = SP / 16;
@@ -213,6 +217,7 @@ __global__ __launch_bounds__((64 * bwd_waves<HD, SP>())) void attn_bwd_kernel(co
   uint16_t* dSs = Kt + (TR ? 0 : HD * TS);
   float* lse_s = reinterpret_cast<float*>(dSs + QC * TS);
   float* delta_s = lse_s + SP;
+  float* bsum = delta_s + SP;  // [3 * HD] block column sums of dQ | dK | dV
 
   const int bh = blockIdx.x;
   const int b = bh / H, h = bh - (bh / H) * H;
@@ -228,6 +233,7 @@ __global__ __launch_bounds__((64 * bwd_waves<HD, SP>())) void attn_bwd_kernel(co
   uint16_t* dKg = dqkv + (long)b * S * ts + (H + h) * HD;
   uint16_t* dVg = dqkv + (long)b * S * ts + (2 * H + h) * HD;
 
+  for (int i = threadIdx.x; i < 3 * HD; i += NTH) bsum[i] = 0.f;
   for (int i = threadIdx.x; i < SP; i += NTH) {
     delta_s[i] = 0.f;
     lse_s[i] = i < S ? lse[((long)b * H + h) * S + i] * LOG2E : INFINITY;
@@ -364,6 +370,15 @@ __global__ __launch_bounds__((64 * bwd_waves<HD, SP>())) void attn_bwd_kernel(co
             dq[dt] = mfma(ka, bop, dq[dt]);
           }
         }
+        if (dbp != nullptr) {  // column sums of this dQ tile (padded query rows are 0)
+#pragma unroll
+          for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              const float v = row16_sum(dq[dt][i]);
+              if (l16 == 0) atomicAdd(&bsum[dt * 16 + 4 * g + i], v * scale);
+            }
+        }
         const int q = qt * 16 + l16;
         if (q < S) {
 #pragma unroll
@@ -392,6 +407,31 @@ __global__ __launch_bounds__((64 * bwd_waves<HD, SP>())) void attn_bwd_kernel(co
       }
     }
   }
+  if (dbp != nullptr) {
+    // lane (l16, g) holds column d = dt*16 + 4g + i of 16 keys: sum the key tiles, the 16 lanes
+    // of the DPP row, then the waves through LDS
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        float sk = 0.f, sv = 0.f;
+#pragma unroll
+        for (int w = 0; w < NKW; ++w) {
+          sk += dkacc[w][dt][i];
+          sv += dvacc[w][dt][i];
+        }
+        sk = row16_sum(sk);
+        sv = row16_sum(sv);
+        if (l16 == 0) {
+          const int d = dt * 16 + 4 * g + i;
+          atomicAdd(&bsum[HD + d], sk * scale);
+          atomicAdd(&bsum[2 * HD + d], sv);
+        }
+      }
+    __syncthreads();
+    float* dst = dbp + (long)b * ts + h * HD;
+    for (int i = threadIdx.x; i < 3 * HD; i += NTH) dst[(i / HD) * H * HD + (i % HD)] = bsum[i];
+  }
 }
 
 template <int HD, int SP, bool TR>
@@ -399,7 +439,7 @@ size_t fwd_smem() { return (size_t)(SP * (HD + 8) + (TR ? SP * (HD + 8) : HD * (
 template <int HD, int SP, bool TR>
 size_t bwd_smem() {
   return (size_t)(4 * SP * (HD + 8) + (TR ? 0 : 3 * HD * (SP + 8)) + 16 * bwd_waves<HD, SP>() * (SP + 8)) * 2 +
-         2 * SP * sizeof(float);
+         (2 * SP + 3 * HD) * sizeof(float);
 }
 
 int g_use_tr = 1;  // runtime switch (tests run both variants)
@@ -419,7 +459,8 @@ int run_t(bool fwd, const uint16_t* qkv, const uint16_t* o, const uint16_t* dO, 
   if (fwd)
     attn_fwd_kernel<HD, SP, TR><<<grid, 256, sm, st>>>(qkv, out, lse_out, S, H, scale);
   else
-    attn_bwd_kernel<HD, SP, TR><<<grid, 64 * bwd_waves<HD, SP>(), sm, st>>>(qkv, o, dO, lse_in, out, S, H, scale);
+    attn_bwd_kernel<HD, SP, TR><<<grid, 64 * bwd_waves<HD, SP>(), sm, st>>>(qkv, o, dO, lse_in, out, S, H, scale,
+                                                                          lse_out);
   return 0;
 }
 
@@ -452,10 +493,11 @@ int jm_attn_fwd(const uint16_t* qkv, uint16_t* o, float* lse, int B, int S, int 
   return -1;
 }
 
+// dbias_part: optional [B][3*H*hd] fp32 per-sample column sums of dqkv (see attn_bwd_kernel)
 int jm_attn_bwd(const uint16_t* qkv, const uint16_t* o, const uint16_t* dO, const float* lse, uint16_t* dqkv, int B,
-                int S, int H, int hd, hipStream_t st) {
+                int S, int H, int hd, float* dbias_part, hipStream_t st) {
   const float scale = 1.f / sqrtf((float)hd);
-  if (hd == 32) return dispatch_sp<32>(false, qkv, o, dO, lse, dqkv, nullptr, B, S, H, scale, st);
-  if (hd == 64) return dispatch_sp<64>(false, qkv, o, dO, lse, dqkv, nullptr, B, S, H, scale, st);
+  if (hd == 32) return dispatch_sp<32>(false, qkv, o, dO, lse, dqkv, dbias_part, B, S, H, scale, st);
+  if (hd == 64) return dispatch_sp<64>(false, qkv, o, dO, lse, dqkv, dbias_part, B, S, H, scale, st);
   return -1;
 }

@@ -21,10 +21,10 @@ int jm_splitk_reduce_add(const float* part, float* g, long n, int S, hipStream_t
 int jm_residual_fwd(const float* x, long sB, long sT, int B, int T, int D, const uint16_t* y, const float* scale,
                     const float* mask, float* out, long oB, long oT, hipStream_t st);
 int jm_residual_bwd(const float* dout, long dB, long dT, const uint16_t* y, const float* scale, const float* mask,
-                    float* dscale, uint16_t* dy, int B, int T, int D, hipStream_t st);
+                    float* dscale, uint16_t* dy, int B, int T, int D, float* dbias, hipStream_t st);
 int jm_attn_fwd(const uint16_t* qkv, uint16_t* o, float* lse, int B, int S, int H, int hd, hipStream_t st);
 int jm_attn_bwd(const uint16_t* qkv, const uint16_t* o, const uint16_t* dO, const float* lse, uint16_t* dqkv, int B,
-                int S, int H, int hd, hipStream_t st);
+                int S, int H, int hd, float* dbias_part, hipStream_t st);
 int jm_attn_max_seq();
 void jm_attn_set_tr(int v);
 void jm_opt_sumsq(const float* x, const int* chunks, int nchunks, float* out, hipStream_t st);
@@ -170,7 +170,8 @@ torch::Tensor residual_fwd(torch::Tensor x, torch::Tensor y, c10::optional<torch
 }
 
 torch::Tensor residual_bwd(torch::Tensor dout, c10::optional<torch::Tensor> y, c10::optional<torch::Tensor> scale,
-                           c10::optional<torch::Tensor> mask, c10::optional<torch::Tensor> dscale, py::object ydtype) {
+                           c10::optional<torch::Tensor> mask, c10::optional<torch::Tensor> dscale, py::object ydtype,
+                           c10::optional<torch::Tensor> dbias) {
   TORCH_CHECK(dout.dim() == 3 && dout.stride(2) == 1, "dout must be a [B,T,D] view");
   CHECK_DT(dout, torch::kFloat32);
   const int B = dout.size(0), T = dout.size(1), D = dout.size(2);
@@ -179,7 +180,7 @@ torch::Tensor residual_bwd(torch::Tensor dout, c10::optional<torch::Tensor> y, c
   auto dy = torch::empty({(long)B * T, D}, dout.options().dtype(odt));
   const uint16_t* yp = (y.has_value() && y->defined()) ? bf(*y) : nullptr;
   check_rc(jm_residual_bwd(dout.data_ptr<float>(), dout.stride(0), dout.stride(1), yp, fopt(scale), fopt(mask),
-                           fopt_m(dscale), bfm(dy), B, T, D, stream()),
+                           fopt_m(dscale), bfm(dy), B, T, D, fopt_m(dbias), stream()),
            "residual_bwd");
   return dy;
 }
@@ -196,7 +197,10 @@ std::vector<torch::Tensor> attn_fwd(torch::Tensor qkv, int64_t heads) {
   return {o, lse};
 }
 
-torch::Tensor attn_bwd(torch::Tensor dO, torch::Tensor qkv, torch::Tensor o, torch::Tensor lse, int64_t heads) {
+// dbias (optional, fp32 [3D]) += column sums of dqkv (the QKV Dense bias gradient), taken from
+// the kernel's fp32 accumulators as per-sample partials and reduced here.
+torch::Tensor attn_bwd(torch::Tensor dO, torch::Tensor qkv, torch::Tensor o, torch::Tensor lse, int64_t heads,
+                       c10::optional<torch::Tensor> dbias) {
   CHECK_CONTIG(dO);
   CHECK_CONTIG(qkv);
   CHECK_CONTIG(o);
@@ -204,8 +208,16 @@ torch::Tensor attn_bwd(torch::Tensor dO, torch::Tensor qkv, torch::Tensor o, tor
   const int B = qkv.size(0), S = qkv.size(1), D3 = qkv.size(2);
   const int D = D3 / 3, hd = D / heads;
   auto dqkv = torch::empty_like(qkv);
-  check_rc(jm_attn_bwd(bf(qkv), bf(o), bf(dO), lse.data_ptr<float>(), bfm(dqkv), B, S, heads, hd, stream()),
+  torch::Tensor part;
+  if (dbias) {
+    TORCH_CHECK(dbias->is_contiguous() && dbias->scalar_type() == torch::kFloat32 && dbias->numel() == D3,
+                "attn_bwd: dbias must be contiguous fp32 [3D]");
+    part = torch::empty({B, D3}, qkv.options().dtype(torch::kFloat32));
+  }
+  float* pp = dbias ? part.data_ptr<float>() : nullptr;
+  check_rc(jm_attn_bwd(bf(qkv), bf(o), bf(dO), lse.data_ptr<float>(), bfm(dqkv), B, S, heads, hd, pp, stream()),
            "attn_bwd");
+  if (dbias) check_rc(jm_splitk_reduce_add(pp, dbias->data_ptr<float>(), D3, B, stream()), "attn_bwd dbias");
   return dqkv;
 }
 
@@ -283,9 +295,11 @@ PYBIND11_MODULE(_C, m) {
   m.def("splitk_reduce_add", &splitk_reduce_add);
   m.def("residual_fwd", &residual_fwd, py::arg("x"), py::arg("y"), py::arg("scale"), py::arg("mask"),
         py::arg("out") = py::none());
-  m.def("residual_bwd", &residual_bwd);
+  m.def("residual_bwd", &residual_bwd, py::arg("dout"), py::arg("y"), py::arg("scale"), py::arg("mask"),
+        py::arg("dscale"), py::arg("ydtype"), py::arg("dbias") = py::none());
   m.def("attn_fwd", &attn_fwd);
-  m.def("attn_bwd", &attn_bwd);
+  m.def("attn_bwd", &attn_bwd, py::arg("dO"), py::arg("qkv"), py::arg("o"), py::arg("lse"), py::arg("heads"),
+        py::arg("dbias") = py::none());
   m.def("attn_max_seq", &jm_attn_max_seq);
   m.def("attn_set_tr", &jm_attn_set_tr);
   m.def("opt_sumsq", &opt_sumsq);

@@ -36,10 +36,30 @@ template <typename T> JM_DEVICE T from_f(float v);
 template <> JM_DEVICE float from_f<float>(float v) { return v; }
 template <> JM_DEVICE uint16_t from_f<uint16_t>(float v) { return f2bf(v); }
 
-JM_DEVICE float wave_sum(float v) {
-#pragma unroll
-  for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m, WAVE);
+// DPP lane moves (VALU, no LDS round trip like __shfl_xor's ds_bpermute)
+template <int CTRL>
+JM_DEVICE float dpp_mov(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF, true));
+}
+
+// sum over the 16 lanes of each DPP row; every lane of the row gets the result.
+// Requires the whole row active.
+JM_DEVICE float row16_sum(float v) {
+  v += dpp_mov<0xB1>(v);   // quad_perm [1,0,3,2]
+  v += dpp_mov<0x4E>(v);   // quad_perm [2,3,0,1]
+  v += dpp_mov<0x141>(v);  // row_half_mirror
+  v += dpp_mov<0x140>(v);  // row_mirror
   return v;
+}
+
+// full-wave sum (wave-uniform result); requires all 64 lanes active
+JM_DEVICE float wave_sum(float v) {
+  v = row16_sum(v);
+  const int i = __builtin_bit_cast(int, v);
+  return (__builtin_bit_cast(float, __builtin_amdgcn_readlane(i, 0)) +
+          __builtin_bit_cast(float, __builtin_amdgcn_readlane(i, 16))) +
+         (__builtin_bit_cast(float, __builtin_amdgcn_readlane(i, 32)) +
+          __builtin_bit_cast(float, __builtin_amdgcn_readlane(i, 48)));
 }
 
 JM_DEVICE float wave_max(float v) {

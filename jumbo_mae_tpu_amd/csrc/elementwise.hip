@@ -54,13 +54,15 @@ JM_DEVICE ColPlan col_plan(int N) {
 
 // MODE 0: colsum(dy)          -> acc
 // MODE 1: gelu_bwd(h, da)     -> out (bf16), acc += colsum(out)
-// MODE 2: residual_bwd        -> out = m*s*dout (bf16, dout fp32), acc += colsum(m*dout*y)
+// MODE 2: residual_bwd        -> out = m*s*dout (bf16, dout fp32), acc += colsum(m*dout*y),
+//                                acc2 += colsum(out)  (bias gradient of the Dense that produced y)
 template <int MODE>
 __global__ __launch_bounds__(256) void rowcol_kernel(const void* __restrict__ in0, const uint16_t* __restrict__ in1,
                                                      uint16_t* __restrict__ out, float* __restrict__ acc,
                                                      const float* __restrict__ scale, const float* __restrict__ mask,
-                                                     int M, int N, int T, int rows_per_block, long sB, long sT) {
-  extern __shared__ __attribute__((aligned(16))) float red_s[];  // [<= 2048] block's columns
+                                                     int M, int N, int T, int rows_per_block, long sB, long sT,
+                                                     float* __restrict__ acc2) {
+  extern __shared__ __attribute__((aligned(16))) float red_s[];  // [2][<= 2048] block's columns
   // 2-D grid: blockIdx.y picks a chunk of <= 2048 columns, blockIdx.x a slab of rows
   const int c0 = blockIdx.y * 2048;
   const int nc = (N - c0) < 2048 ? (N - c0) : 2048;
@@ -68,8 +70,9 @@ __global__ __launch_bounds__(256) void rowcol_kernel(const void* __restrict__ in
   const int slot = threadIdx.x / p.tpr, c = threadIdx.x % p.tpr;
   const bool active = slot < p.rps;
   float* red = red_s - c0;  // index with absolute column
-  if (acc) {
-    for (int i = threadIdx.x; i < nc; i += 256) red_s[i] = 0.f;
+  float* red2 = red_s + 2048 - c0;
+  if (acc || acc2) {
+    for (int i = threadIdx.x; i < 4096; i += 256) red_s[i] = 0.f;
     __syncthreads();
   }
   const int r_begin = blockIdx.x * rows_per_block;
@@ -78,9 +81,9 @@ __global__ __launch_bounds__(256) void rowcol_kernel(const void* __restrict__ in
   if (active) {
     for (int cg = c; cg < p.cgs; cg += p.tpr) {
       const int col = c0 + cg * 8;
-      float s[8];
+      float s[8], s2[8];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) s[j] = 0.f;
+      for (int j = 0; j < 8; ++j) s[j] = s2[j] = 0.f;
       float sc[8];
       if (MODE == 2) {
         if (scale) {
@@ -135,6 +138,7 @@ __global__ __launch_bounds__(256) void rowcol_kernel(const void* __restrict__ in
               const float md = m * a[u][j];
               o[j] = md * sc[j];
               if (scale) s[j] += md * b[u][j];
+              s2[j] += bf2f(f2bf(o[j]));  // colsum of the bf16 values the GEMMs consume
             }
             store8(out + off, o);
           }
@@ -144,12 +148,17 @@ __global__ __launch_bounds__(256) void rowcol_kernel(const void* __restrict__ in
 #pragma unroll
         for (int j = 0; j < 8; ++j) atomicAdd(&red[col + j], s[j]);
       }
+      if (MODE == 2 && acc2) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) atomicAdd(&red2[col + j], s2[j]);
+      }
     }
   }
-  if (acc) {
-    __syncthreads();
+  if (acc || acc2) __syncthreads();
+  if (acc)
     for (int i = threadIdx.x; i < nc; i += 256) atomicAdd(&acc[c0 + i], red_s[i]);
-  }
+  if (MODE == 2 && acc2)
+    for (int i = threadIdx.x; i < nc; i += 256) atomicAdd(&acc2[c0 + i], red_s[2048 + i]);
 }
 
 __global__ __launch_bounds__(256) void residual_fwd_kernel(const float* __restrict__ x, long sB, long sT, int T,
@@ -188,7 +197,8 @@ int grid_for(long work, int per_thread_items = 1) {
 
 template <int MODE>
 void launch_rowcol(const void* in0, const uint16_t* in1, uint16_t* out, float* acc, const float* scale,
-                   const float* mask, int M, int N, int T, hipStream_t st, long sB = 0, long sT = 0) {
+                   const float* mask, int M, int N, int T, hipStream_t st, long sB = 0, long sT = 0,
+                   float* acc2 = nullptr) {
   // 2-D grid: column chunks of 2048 x row slabs; each row-slot walks >= 16 rows, ~2048 blocks
   // in total so the per-block column atomics stay cheap
   const int ncol = (N + 2047) / 2048;
@@ -203,9 +213,9 @@ void launch_rowcol(const void* in0, const uint16_t* in1, uint16_t* out, float* a
     rows_per_block = (M + nb - 1) / nb;
   }
   if (nb < 1) nb = 1;
-  const size_t smem = acc ? 2048 * sizeof(float) : 0;
+  const size_t smem = (acc || acc2) ? 4096 * sizeof(float) : 0;
   rowcol_kernel<MODE><<<dim3(nb, ncol), 256, smem, st>>>(in0, in1, out, acc, scale, mask, M, N, T, rows_per_block,
-                                                          sB, sT);
+                                                          sB, sT, acc2);
 }
 
 }  // namespace
@@ -238,28 +248,49 @@ int jm_residual_fwd(const float* x, long sB, long sT, int B, int T, int D, const
 }
 
 int jm_residual_bwd(const float* dout, long dB, long dT, const uint16_t* y, const float* scale, const float* mask,
-                    float* dscale, uint16_t* dy, int B, int T, int D, hipStream_t st) {
+                    float* dscale, uint16_t* dy, int B, int T, int D, float* dbias, hipStream_t st) {
   if (D % 8) return -1;
-  launch_rowcol<2>(dout, y, dy, dscale, scale, mask, B * T, D, T, st, dB, dT);
+  launch_rowcol<2>(dout, y, dy, dscale, scale, mask, B * T, D, T, st, dB, dT, dbias);
   return 0;
 }
 
 // ---------------------------------------------------------------------------------------------
 // Split-K epilogue of the weight-gradient GEMMs: g[i] += sum_s part[s][i] (fp32), one pass.
 namespace {
+// g[i] += sum_s part[s][i].  grid.y > 1 splits the S partials into slices that are summed with
+// atomics: used when n is small and S large (per-sample bias partials, n = 3D, S = batch).
 __global__ __launch_bounds__(256) void splitk_reduce_add_kernel(const float* __restrict__ part,
                                                                 float* __restrict__ g, long n4, int S) {
   const long n = n4 * 4;
+  const int per = (S + gridDim.y - 1) / gridDim.y;
+  const int s0 = blockIdx.y * per;
+  const int s1 = min(S, s0 + per);
   for (long i = blockIdx.x * 256L + threadIdx.x; i < n4; i += (long)gridDim.x * 256) {
-    float acc[4];
-    load4(g + i * 4, acc);
-    for (int s = 0; s < S; ++s) {
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+    int s = s0;
+    for (; s + 1 < s1; s += 2) {
+      float v[4], w[4];
+      load4(part + (long)s * n + i * 4, v);
+      load4(part + (long)(s + 1) * n + i * 4, w);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[j] += v[j] + w[j];
+    }
+    if (s < s1) {
       float v[4];
       load4(part + (long)s * n + i * 4, v);
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[j] += v[j];
     }
-    store4(g + i * 4, acc);
+    if (gridDim.y == 1) {
+      float o[4];
+      load4(g + i * 4, o);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) o[j] += acc[j];
+      store4(g + i * 4, o);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) atomicAdd(g + i * 4 + j, acc[j]);
+    }
   }
 }
 }  // namespace
@@ -268,6 +299,8 @@ int jm_splitk_reduce_add(const float* part, float* g, long n, int S, hipStream_t
   if (n % 4) return -1;
   long blocks = (n / 4 + 255) / 256;
   if (blocks > 4096) blocks = 4096;
-  splitk_reduce_add_kernel<<<(int)blocks, 256, 0, st>>>(part, g, n / 4, S);
+  int ys = 1;  // slice the partials until the launch has ~512 workgroups of >= 8 rows each
+  while (blocks * ys < 512 && S / (ys * 2) >= 8) ys *= 2;
+  splitk_reduce_add_kernel<<<dim3((unsigned)blocks, ys), 256, 0, st>>>(part, g, n / 4, S);
   return 0;
 }

@@ -30,10 +30,10 @@ def _attn_fwd(attn, h1, B, S):
     return qkv, o, lse, a
 
 
-def _attn_bwd(attn, da, h1, qkv, o, lse, B, S):
-    do = P.linear_bwd(da, o.view(B * S, -1), attn.wo_k, attn.wo_b)
-    dqkv = P.attn_bwd(do, qkv.view(B, S, -1), o, lse, attn.heads)
-    return P.linear_bwd(dqkv.view(B * S, -1), h1, attn.qkv_k, attn.qkv_b)
+def _attn_bwd(attn, da, h1, qkv, o, lse, B, S, wo_bias_done=False):
+    do = P.linear_bwd(da, o.view(B * S, -1), attn.wo_k, attn.wo_b, bias_done=wo_bias_done)
+    dqkv, bd = P.attn_bwd(do, qkv.view(B, S, -1), o, lse, attn.heads, attn.qkv_b)
+    return P.linear_bwd(dqkv.view(B * S, -1), h1, attn.qkv_k, attn.qkv_b, bias_done=bd)
 
 
 def _ff_fwd(ff, h):
@@ -43,8 +43,8 @@ def _ff_fwd(ff, h):
     return pre, g, y
 
 
-def _ff_bwd(ff, dy, h, pre, g):
-    dg = P.linear_bwd(dy, g, ff.w2.k, ff.w2.b)
+def _ff_bwd(ff, dy, h, pre, g, w2_bias_done=False):
+    dg = P.linear_bwd(dy, g, ff.w2.k, ff.w2.b, bias_done=w2_bias_done)
     dpre, bias_done = P.gelu_bwd(pre, dg, ff.w1.b if ff.w1.k.segs[0].trainable else None)
     return P.linear_bwd(dpre, h, ff.w1.k, ff.w1.b, bias_done=bias_done)
 
@@ -102,19 +102,19 @@ class JumboBlockFn(torch.autograd.Function):
         dx2 = dx2.contiguous()
         dx1 = torch.empty_like(dx2)
         # ---- patch branch: dx1[:, C:] = dx2[:, C:] + LN2'(FF'(s2 * dp2 * dx2[:, C:]))
-        dfy = P.residual_bwd(dx2[:, C:], fy, layer.scale2, m2, dt)
-        dhp = _ff_bwd(layer.ff, dfy, hp, fpre, fg)
+        dfy, bd = P.residual_bwd(dx2[:, C:], fy, layer.scale2, m2, dt, layer.ff.w2.b)
+        dhp = _ff_bwd(layer.ff, dfy, hp, fpre, fg, bd)
         P.ln_bwd(dhp, x1[:, C:], mup, rsp, layer.norm2.g, layer.norm2.b, dres=dx2[:, C:], out=dx1[:, C:])
         # ---- jumbo branch: d hc = dx2_cls + JumboMLP'(s3 * dp3 * dx2_cls); dx1_cls = LN3'(d hc)
         dcls = dx2[:, :C].reshape(B, 1, J)
-        djy = P.residual_bwd(dcls, jy, layer.scale3, m3, dt)
-        dhcb = _ff_bwd(layer.jumbo_mlp, djy, hcb, jpre, jg)
+        djy, bd = P.residual_bwd(dcls, jy, layer.scale3, m3, dt, layer.jumbo_mlp.w2.b)
+        dhcb = _ff_bwd(layer.jumbo_mlp, djy, hcb, jpre, jg, bd)
         dhc = dcls.reshape(B, J) + dhcb.float()
         P.ln_bwd(dhc, x1[:, :C].reshape(B, 1, J), muc, rsc, layer.norm3.g, layer.norm3.b,
                  out=dx1[:, :C].reshape(B, 1, J))
         # ---- attention branch: dx = dx1 + LN1'(Attn'(s1 * dp1 * dx1))
-        da = P.residual_bwd(dx1, a, layer.scale1, m1, dt)
-        dh1 = _attn_bwd(layer.attn, da, h1, qkv, o, lse, B, S)
+        da, bd = P.residual_bwd(dx1, a, layer.scale1, m1, dt, layer.attn.wo_b)
+        dh1 = _attn_bwd(layer.attn, da, h1, qkv, o, lse, B, S, bd)
         dx = P.ln_bwd(dh1, x, mu1, rs1, layer.norm1.g, layer.norm1.b, dres=dx1, out=dx1)
         return dx, None, None, None, None, None
 
@@ -148,11 +148,11 @@ class ViTBlockFn(torch.autograd.Function):
         B, S, D = x.shape
         dt = h1.dtype
         dx2 = dx2.contiguous()
-        dfy = P.residual_bwd(dx2, fy, layer.scale2, m2, dt)
-        dh2 = _ff_bwd(layer.ff, dfy, h2, fpre, fg)
+        dfy, bd = P.residual_bwd(dx2, fy, layer.scale2, m2, dt, layer.ff.w2.b)
+        dh2 = _ff_bwd(layer.ff, dfy, h2, fpre, fg, bd)
         dx1 = P.ln_bwd(dh2, x1, mu2, rs2, layer.norm2.g, layer.norm2.b, dres=dx2)  # never write autograd's dx2
-        da = P.residual_bwd(dx1, a, layer.scale1, m1, dt)
-        dh1 = _attn_bwd(layer.attn, da, h1, qkv, o, lse, B, S)
+        da, bd = P.residual_bwd(dx1, a, layer.scale1, m1, dt, layer.attn.wo_b)
+        dh1 = _attn_bwd(layer.attn, da, h1, qkv, o, lse, B, S, bd)
         dx = P.ln_bwd(dh1, x, mu1, rs1, layer.norm1.g, layer.norm1.b, dres=dx1, out=dx1)
         return dx, None, None, None, None
 

@@ -123,7 +123,7 @@ class _Residual(torch.autograd.Function):
     def backward(ctx, dout):
         y2, mask = ctx.saved_tensors
         dout = dout.contiguous()
-        dy = P.residual_bwd(dout, y2, ctx.hs, mask, ctx.ydtype)
+        dy, _ = P.residual_bwd(dout, y2, ctx.hs, mask, ctx.ydtype)
         return dout, dy.reshape(ctx.yshape), None, None, None
 
 
@@ -147,7 +147,7 @@ class _Attention(torch.autograd.Function):
     @staticmethod
     def backward(ctx, do):
         qkv, o, lse = ctx.saved_tensors
-        return P.attn_bwd(do, qkv, o, lse, ctx.heads), None
+        return P.attn_bwd(do, qkv, o, lse, ctx.heads)[0], None
 
 
 def attention(qkv: torch.Tensor, heads: int) -> torch.Tensor:

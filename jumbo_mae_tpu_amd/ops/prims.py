@@ -174,14 +174,20 @@ def residual_fwd(x3: torch.Tensor, y2: torch.Tensor, hs: Handle | None, mask, ou
     return res
 
 
-def residual_bwd(dout3: torch.Tensor, y2: torch.Tensor | None, hs: Handle | None, mask, ydtype) -> torch.Tensor:
-    """dy = mask[b] * s * dout (in ``ydtype``); ds += sum mask*dout*y."""
+def residual_bwd(dout3: torch.Tensor, y2: torch.Tensor | None, hs: Handle | None, mask, ydtype,
+                 hbias: Handle | None = None):
+    """dy = mask[b] * s * dout (in ``ydtype``); ds += sum mask*dout*y.  When ``hbias`` (the bias of
+    the Dense that produced y) is given, its gradient colsum(dy) is fused into the same pass.
+    Returns (dy, bias_done)."""
     B, T, D = dout3.shape
-    if hs is None and mask is None:
-        dy = dout3.reshape(B * T, D).to(ydtype)
-    elif hip(dout3) and ydtype == torch.bfloat16:
+    bg = hbias.grad if _trainable(hbias) else None
+    if hip(dout3) and ydtype == torch.bfloat16 and (hs is not None or mask is not None or bg is not None):
         dy = _ext.load().residual_bwd(dout3, y2, hs.master if hs is not None else None, mask,
-                                      hs.grad if _trainable(hs) else None, ydtype)
+                                      hs.grad if _trainable(hs) else None, ydtype, bg)
+        done = bg is not None
+    elif hs is None and mask is None:
+        dy = dout3.reshape(B * T, D).to(ydtype)
+        done = False
     else:
         d = dout3.float()
         if mask is not None:
@@ -191,9 +197,10 @@ def residual_bwd(dout3: torch.Tensor, y2: torch.Tensor | None, hs: Handle | None
                 hs.grad.add_((d * y2.float().reshape(B, T, D)).sum((0, 1)))
             d = d * hs.master
         dy = d.reshape(B * T, D).to(ydtype)
+        done = False
     if _trainable(hs):
         hs.ready()
-    return dy
+    return dy, done
 
 
 # ------------------------------------------------------------------------------ attention
@@ -212,13 +219,17 @@ def attn_fwd(qkv: torch.Tensor, heads: int):
     return o, lse
 
 
-def attn_bwd(do: torch.Tensor, qkv: torch.Tensor, o: torch.Tensor, lse: torch.Tensor, heads: int) -> torch.Tensor:
+def attn_bwd(do: torch.Tensor, qkv: torch.Tensor, o: torch.Tensor, lse: torch.Tensor, heads: int,
+             hbias: Handle | None = None):
+    """-> (dqkv [B, S, 3D], bias_done).  When ``hbias`` (the QKV Dense bias) is given, its gradient
+    colsum(dqkv) is fused into the HIP kernel."""
     B, S, three_d = qkv.shape
     D = three_d // 3
     hd = D // heads
     do = do.contiguous().view(B, S, D)
     if hip(qkv):
-        return _ext.load().attn_bwd(do, qkv, o, lse, heads)
+        bg = hbias.grad if _trainable(hbias) else None
+        return _ext.load().attn_bwd(do, qkv, o, lse, heads, bg), bg is not None
     q, k, v = qkv.float().view(B, S, 3, heads, hd).unbind(2)
     dof = do.float().view(B, S, heads, hd)
     sc = 1.0 / math.sqrt(hd)
@@ -230,4 +241,4 @@ def attn_bwd(do: torch.Tensor, qkv: torch.Tensor, o: torch.Tensor, lse: torch.Te
     ds = p * (dp - delta[..., None])
     dq = torch.einsum("bhqk,bkhd->bqhd", ds, k) * sc
     dk = torch.einsum("bhqk,bqhd->bkhd", ds, q) * sc
-    return torch.stack([dq, dk, dv], 2).reshape(B, S, three_d).to(qkv.dtype)
+    return torch.stack([dq, dk, dv], 2).reshape(B, S, three_d).to(qkv.dtype), False

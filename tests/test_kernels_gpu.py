@@ -120,6 +120,11 @@ def test_attention(ext, B, S, H, hd, tr):
     assert (lse.double() - lser).abs().max().item() < 2e-2
     do = torch.randn(B, S, D, device="cuda").bfloat16()
     dqkv = ext.attn_bwd(do, qkv, o, lse, H)
+    dbias = torch.full((3 * D,), 0.5, device="cuda")
+    dqkv2 = ext.attn_bwd(do, qkv, o, lse, H, dbias)  # fused QKV-bias colsum (accumulates)
+    assert torch.equal(dqkv, dqkv2)
+    ref_b = dqkv.double().sum((0, 1)) + 0.5
+    assert (dbias.double() - ref_b).abs().max().item() < 2e-2 * ref_b.abs().max().item() + 1e-2
     qr = qkv.double().requires_grad_()
     o2, _ = _attn_ref(qr, H)
     o2.backward(do.double())
@@ -128,6 +133,15 @@ def test_attention(ext, B, S, H, hd, tr):
     for i in range(3):
         assert rel(d[:, :, i], g[:, :, i]) < 2e-2, i
     ext.attn_set_tr(1)
+
+
+@pytest.mark.parametrize("S,n", [(4, 4096), (512, 3072), (37, 1024)])
+def test_splitk_reduce_add(ext, S, n):
+    part = torch.randn(S, n, device="cuda")
+    g = torch.randn(n, device="cuda")
+    ref = g.double() + part.double().sum(0)
+    ext.splitk_reduce_add(part, g)
+    assert (g.double() - ref).abs().max().item() < 1e-4
 
 
 def test_patchify(ext):
