@@ -39,6 +39,15 @@ void jm_opt_apply_trust(float* p, const float* u_or_g, float* trace, uint16_t* s
                         float momentum, float trust_coef, hipStream_t st);
 void jm_opt_sgd(float* p, const float* g, float* trace, uint16_t* shadow, const int* chunks, int nchunks,
                 const float* meta, const float* hyper, const float* gnorm_sq, float momentum, hipStream_t st);
+struct GemmEpi {
+  const float* bias;
+  uint16_t* out;
+  long ldo;
+  uint16_t* out2;
+};
+int jm_gemm_nt(const uint16_t* A, long lda, const uint16_t* B, long ldb, int M, int N, int K, int epi,
+               const GemmEpi& ep, hipStream_t st);
+void jm_gemm_set_variant(int wn, int group);
 int jm_patchify_normalize(const uint8_t* img, float* out, int B, int H, int W, int p, hipStream_t st);
 
 namespace {
@@ -283,6 +292,31 @@ torch::Tensor patchify_normalize(torch::Tensor img, int64_t p) {
 
 }  // namespace
 
+// ------------------------------------------------------------------------------ GEMM
+// C[M, N] = A[M, K] . B[N, K]^T (+ bias) in bf16 (fp32 accumulate); gelu=true also returns
+// gelu(C) (the pre-activation C is what the backward needs).  A / B rows may be strided.
+std::vector<torch::Tensor> gemm_nt(torch::Tensor A, torch::Tensor B, c10::optional<torch::Tensor> bias, bool gelu) {
+  CHECK_DT(A, torch::kBFloat16);
+  CHECK_DT(B, torch::kBFloat16);
+  TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && A.size(1) == B.size(1), "gemm_nt: A [M,K], B [N,K]");
+  TORCH_CHECK(A.stride(1) == 1 && B.stride(1) == 1, "gemm_nt: K must be contiguous");
+  const int M = A.size(0), N = B.size(0), K = A.size(1);
+  auto out = torch::empty({M, N}, A.options());
+  torch::Tensor out2;
+  GemmEpi ep{nullptr, bfm(out), N, nullptr};
+  if (bias) {
+    TORCH_CHECK(bias->is_contiguous() && bias->scalar_type() == torch::kFloat32 && bias->numel() == N, "gemm_nt bias");
+    ep.bias = bias->data_ptr<float>();
+  }
+  if (gelu) {
+    out2 = torch::empty({M, N}, A.options());
+    ep.out2 = bfm(out2);
+  }
+  check_rc(jm_gemm_nt(bf(A), A.stride(0), bf(B), B.stride(0), M, N, K, gelu ? 1 : 0, ep, stream()), "gemm_nt");
+  if (gelu) return {out, out2};
+  return {out};
+}
+
 PYBIND11_MODULE(_C, m) {
   m.doc() = "jumbo_mae_tpu_amd CDNA4 (gfx950) HIP kernels";
   m.def("layernorm_fwd", &layernorm_fwd);
@@ -301,6 +335,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("attn_bwd", &attn_bwd, py::arg("dO"), py::arg("qkv"), py::arg("o"), py::arg("lse"), py::arg("heads"),
         py::arg("dbias") = py::none());
   m.def("attn_max_seq", &jm_attn_max_seq);
+  m.def("gemm_set_variant", &jm_gemm_set_variant, py::arg("wn"), py::arg("group") = 8);
+  m.def("gemm_nt", &gemm_nt, py::arg("A"), py::arg("B"), py::arg("bias") = py::none(), py::arg("gelu") = false);
   m.def("attn_set_tr", &jm_attn_set_tr);
   m.def("opt_sumsq", &opt_sumsq);
   m.def("opt_adamw", &opt_adamw);

@@ -36,6 +36,16 @@ template <typename T> JM_DEVICE T from_f(float v);
 template <> JM_DEVICE float from_f<float>(float v) { return v; }
 template <> JM_DEVICE uint16_t from_f<uint16_t>(float v) { return f2bf(v); }
 
+// tanh through one v_exp_f32 + one reciprocal (libm tanhf is a long software sequence);
+// saturates correctly at +-inf, absolute error ~1e-7
+JM_DEVICE float jm_tanh(float u) { return 1.f - 2.f * __builtin_amdgcn_rcpf(1.f + __expf(2.f * u)); }
+
+// flax nn.gelu(approximate=True): 0.5 x (1 + tanh(sqrt(2/pi) (x + 0.044715 x^3)))
+JM_DEVICE float gelu_tanh_f(float x) {
+  const float u = 0.7978845608028654f * (x + 0.044715f * x * x * x);
+  return 0.5f * x * (1.f + jm_tanh(u));
+}
+
 // DPP lane moves (VALU, no LDS round trip like __shfl_xor's ds_bpermute)
 template <int CTRL>
 JM_DEVICE float dpp_mov(float v) {

@@ -19,12 +19,12 @@ constexpr float GELU_A = 0.044715f;
 
 JM_DEVICE float gelu_f(float h) {
   const float u = GELU_C * (h + GELU_A * h * h * h);
-  return 0.5f * h * (1.f + tanhf(u));
+  return 0.5f * h * (1.f + jm_tanh(u));
 }
 
 JM_DEVICE float gelu_grad(float h) {
   const float u = GELU_C * (h + GELU_A * h * h * h);
-  const float t = tanhf(u);
+  const float t = jm_tanh(u);
   return 0.5f * (1.f + t) + 0.5f * h * (1.f - t * t) * GELU_C * (1.f + 3.f * GELU_A * h * h);
 }
 

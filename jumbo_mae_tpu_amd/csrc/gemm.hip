@@ -1,0 +1,290 @@
+// MFMA GEMM for gfx950 with fused epilogues: C[M, N] = A[M, K] . B[N, K]^T (+ epilogue).
+//
+// Both operands are K-contiguous ("NT"), which is the layout of every forward Dense of the model
+// (activations [tokens, in] x weights [out, in]) and of the data-gradient GEMMs when they are fed
+// the transposed bf16 weight shadow.  bf16 in, fp32 accumulate.
+//
+// Tiling (CDNA4, 64-wide waves): one 512-thread workgroup (8 waves, 2 along M x 4 along N) owns a
+// 256 x 256 output tile; each wave a 128 x 64 sub-tile = 8 x 4 v_mfma_f32_16x16x32_bf16 tiles
+// (128 accumulator VGPRs).  K is consumed in 32-deep steps staged global -> LDS with
+// global_load_lds_dwordx4 (no VGPR round trip) through a 4-stage ring of 32 KB stages, issued 3
+// steps ahead.  One barrier per step, placed in the MIDDLE of the step: a wave issues the first
+// half of its MFMAs, then waits (counted vmcnt) for its own loads of step t+1 and joins the
+// barrier -- its MFMAs keep the matrix pipe busy meanwhile -- and then reads step t+1's fragments
+// interleaved with the second half of step t's MFMAs (fragments double-buffered in registers).
+//
+// LDS image: row-major [256][32] bf16 per operand (64 B rows), 16-byte chunks XOR-swizzled by
+// 2 * ((row >> 2) & 1) -- applied to the per-lane GLOBAL source address (glds writes lane-linear)
+// and to the ds_read address; with ds_read_b128's lane groups ({0-3,12-15,20-27}, ...) every
+// fragment read is conflict-free.
+//
+// MFMA orientation: the B fragment is the MFMA "A" operand, so each lane's accumulator holds four
+// consecutive output COLUMNS of one row -- bias / activation / residual epilogues work on float4
+// runs.
+//
+// Workgroup -> tile map: bijective XCD remap (consecutive tile ids share an XCD and its L2), then
+// groups of 8 row-tiles sweep the column tiles.
+#include <type_traits>
+
+#include "common.h"
+
+namespace {
+
+constexpr int BM = 256, BN = 256, BK = 32, NST = 4;
+constexpr int STAGE = (BM + BN) * BK;  // elements per ring stage (A then B): 32 KB
+
+typedef __attribute__((address_space(3))) void lds_void_t;
+
+// buffer_load_dwordx4 ... lds: 16 B per lane straight into LDS (wave-uniform LDS base + 16 * lane).
+// Buffer addressing keeps ONE 32-bit VGPR per load (SGPR base + per-step SGPR offset), and the
+// range check zero-fills rows past the operand's end (ragged M / N tiles need no clamping).
+JM_DEVICE __amdgpu_buffer_rsrc_t make_rsrc(const uint16_t* base, long bytes) {
+  const int n = bytes >= 0xffffffffL ? -1 : (int)bytes;
+  return __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, n, 0x00020000);
+}
+
+JM_DEVICE void blds16(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff, uint16_t* l) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void_t*)(l), 16, voff, soff, 0, 0);
+}
+
+JM_DEVICE bf16x8_t lds8(const uint16_t* p) { return *reinterpret_cast<const bf16x8_t*>(p); }
+
+JM_DEVICE f32x4_t mfma16(bf16x8_t a, bf16x8_t b, f32x4_t c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+JM_DEVICE int swz(int row) { return ((row >> 2) & 1) << 1; }
+
+template <int NTW>
+struct Frags {
+  bf16x8_t b[NTW], a[8];
+};
+
+}  // namespace
+
+struct GemmEpi {
+  const float* bias;  // [N] fp32 or null
+  uint16_t* out;      // bf16 [M, ldo]
+  long ldo;
+  uint16_t* out2;     // EPI_GELU: gelu(out) bf16 [M, ldo]
+};
+
+enum { EPI_STORE = 0, EPI_GELU = 1 };
+
+namespace {
+
+// acc[mt][nt][i] = C[mb + mt*16 + l16][nb + nt*16 + 4g + i]
+template <int EPI, int NTW>
+JM_DEVICE void epilogue(const f32x4_t (&acc)[8][NTW], const GemmEpi& ep, int M, int N, int mb, int nb, int l16,
+                        int g) {
+#pragma unroll
+  for (int nt = 0; nt < NTW; ++nt) {
+    const int n = nb + nt * 16 + 4 * g;
+    if (n >= N) continue;
+    float bv[4] = {0.f, 0.f, 0.f, 0.f};
+    if (ep.bias) load4(ep.bias + n, bv);
+#pragma unroll
+    for (int mt = 0; mt < 8; ++mt) {
+      const int m = mb + mt * 16 + l16;
+      if (m >= M) continue;
+      float v[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) v[i] = acc[mt][nt][i] + bv[i];
+      store4(ep.out + (long)m * ep.ldo + n, v);
+      if (EPI == EPI_GELU) {
+        float gv[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) gv[i] = gelu_tanh_f(bf2f(f2bf(v[i])));
+        store4(ep.out2 + (long)m * ep.ldo + n, gv);
+      }
+    }
+  }
+}
+
+JM_DEVICE void tile_of(int M, int N, int GROUP_M, int& m0, int& n0) {
+  const int nM = (M + BM - 1) / BM, nN = (N + BN - 1) / BN;
+  const int nwg = nM * nN;
+  const int orig = blockIdx.x;
+  const int xcd = orig & 7, q = nwg >> 3, r = nwg & 7;
+  const int wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+  const int per_group = GROUP_M * nN;
+  const int first_m = (wg / per_group) * GROUP_M;
+  const int gsz = min(nM - first_m, GROUP_M);
+  m0 = (first_m + (wg % per_group) % gsz) * BM;
+  n0 = ((wg % per_group) / gsz) * BN;
+}
+
+// WN waves along N (2 along M): WN = 4 -> 8 waves of 128 x 64 (2 waves / SIMD);
+// WN = 2 -> 4 waves of 128 x 128 (1 wave / SIMD, accumulators in AGPRs)
+template <int EPI, int WN>
+__global__ __launch_bounds__(128 * WN, 1) void gemm_nt_kernel(const uint16_t* __restrict__ A, long lda,
+                                                              const uint16_t* __restrict__ B, long ldb, int M,
+                                                              int N, int K, GemmEpi ep, int GROUP_M) {
+  constexpr int NW = 2 * WN;          // waves
+  constexpr int NTW = BN / WN / 16;   // 16-wide column tiles per wave
+  constexpr int RND = 16 / NW;        // glds rounds per operand and stage
+  extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
+  const int tid = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+  const int l16 = lane & 15, g = lane >> 4;
+  const int wr = wave / WN, wc = wave % WN;
+
+  int m0, n0;
+  tile_of(M, N, GROUP_M, m0, n0);
+
+  // ---- per-lane swizzled source offsets: RND rounds x NW waves x 16 rows per operand and stage
+  const __amdgpu_buffer_rsrc_t ra = make_rsrc(A + (long)m0 * lda, (long)(M - m0) * lda * 2);
+  const __amdgpu_buffer_rsrc_t rb = make_rsrc(B + (long)n0 * ldb, (long)(N - n0) * ldb * 2);
+  uint32_t a_src[RND], b_src[RND];  // byte offsets
+#pragma unroll
+  for (int rr = 0; rr < RND; ++rr) {
+    const int row = rr * 16 * NW + wave * 16 + (lane >> 2);
+    const int c = (lane & 3) ^ swz(row);
+    a_src[rr] = (uint32_t)((row * lda + c * 8) * 2);
+    b_src[rr] = (uint32_t)((row * ldb + c * 8) * 2);
+  }
+  auto issue = [&](int t) {
+    const uint32_t k0b = t * BK * 2;
+    uint16_t* la = smem + (t % NST) * STAGE;
+    uint16_t* lb = la + BM * BK;
+#pragma unroll
+    for (int rr = 0; rr < RND; ++rr) {
+      blds16(ra, a_src[rr], k0b, la + (rr * 16 * NW + wave * 16) * BK);
+      blds16(rb, b_src[rr], k0b, lb + (rr * 16 * NW + wave * 16) * BK);
+    }
+  };
+  // fragment reads: row * 32 + swizzled chunk * 8; swz(row) == swz(l16) for these rows
+  const int ch = (g ^ swz(l16)) * 8;
+  const int a_off = (wr * 128 + l16) * BK + ch;
+  const int b_off = BM * BK + (wc * NTW * 16 + l16) * BK + ch;
+  auto read = [&](int t, Frags<NTW>& f) {
+    const uint16_t* base = smem + (t % NST) * STAGE;
+#pragma unroll
+    for (int nt = 0; nt < NTW; ++nt) f.b[nt] = lds8(base + b_off + nt * 16 * BK);
+#pragma unroll
+    for (int mt = 0; mt < 8; ++mt) f.a[mt] = lds8(base + a_off + mt * 16 * BK);
+  };
+
+  f32x4_t acc[8][NTW];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < NTW; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  // one K step: MFMAs of cur (rows 0-3 | barrier for step t+1 | rows 4-7 beside the reads of
+  // nxt).  KIND: 3 = steady (issue t+3, 2 stages left in flight), 2 / 1 = ring draining,
+  // 0 = last step.  Compile-time so each step is one basic block the scheduler can interleave.
+  auto wait_bar = [&](auto outstanding_stages) {  // vmcnt counts this thread's glds (2 * RND per stage)
+    constexpr int N = decltype(outstanding_stages)::value * 2 * RND;
+    if constexpr (N == 16) asm volatile("s_waitcnt vmcnt(16) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  };
+  auto step = [&](auto kind, int t, Frags<NTW>& cur, Frags<NTW>& nxt) {
+    constexpr int KIND = decltype(kind)::value;
+    if constexpr (KIND == 3) issue(t + 3);
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < NTW; ++nt) acc[mt][nt] = mfma16(cur.b[nt], cur.a[mt], acc[mt][nt]);
+    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (KIND > 0) wait_bar(std::integral_constant<int, KIND - 1>{});
+    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (KIND > 0) read(t + 1, nxt);
+#pragma unroll
+    for (int mt = 4; mt < 8; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < NTW; ++nt) acc[mt][nt] = mfma16(cur.b[nt], cur.a[mt], acc[mt][nt]);
+    if constexpr (KIND > 0) {
+      constexpr int NR = NTW + 8, NM = 4 * NTW, PER = NM / NR;  // reads, MFMAs, MFMAs per read
+#pragma unroll
+      for (int i = 0; i < NR; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);    // 1 ds_read of the next step
+        __builtin_amdgcn_sched_group_barrier(0x008, PER, 0);  // MFMAs
+      }
+      __builtin_amdgcn_sched_group_barrier(0x008, NM - PER * NR, 0);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  using K3 = std::integral_constant<int, 3>;
+  using K2 = std::integral_constant<int, 2>;
+  using K1 = std::integral_constant<int, 1>;
+  using K0 = std::integral_constant<int, 0>;
+
+  const int nk = K / BK;  // even, >= 2 (host checks K % 64 == 0)
+  issue(0);
+  issue(1);
+  if (nk > 2) {
+    issue(2);
+    wait_bar(std::integral_constant<int, 2>{});
+  } else {
+    wait_bar(std::integral_constant<int, 1>{});
+  }
+  __builtin_amdgcn_sched_barrier(0);
+  Frags<NTW> f0, f1;
+  read(0, f0);
+  int t = 0;
+  for (; t + 4 < nk; t += 2) {
+    step(K3{}, t, f0, f1);
+    step(K3{}, t + 1, f1, f0);
+  }
+  if (nk - t == 4) {
+    step(K3{}, t, f0, f1);
+    step(K2{}, t + 1, f1, f0);
+    t += 2;
+  }
+  step(K1{}, t, f0, f1);
+  step(K0{}, t + 1, f1, f0);
+
+  epilogue<EPI, NTW>(acc, ep, M, N, m0 + wr * 128, n0 + wc * NTW * 16, l16, g);
+}
+
+size_t jm_gemm_smem() { return (size_t)NST * STAGE * sizeof(uint16_t); }
+
+// returns 0 on success, <0 on unsupported shape
+int g_gemm_wn = 4;     // runtime switches for A/B (jm_gemm_set_variant)
+int g_gemm_group = 8;
+
+template <int EPI, int WN>
+void launch_nt(const uint16_t* A, long lda, const uint16_t* B, long ldb, int M, int N, int K, const GemmEpi& ep,
+               int nwg, hipStream_t st) {
+  static bool attr = false;
+  const size_t sm = jm_gemm_smem();
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)gemm_nt_kernel<EPI, WN>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
+    attr = true;
+  }
+  gemm_nt_kernel<EPI, WN><<<nwg, 128 * WN, sm, st>>>(A, lda, B, ldb, M, N, K, ep, g_gemm_group);
+}
+
+template <int EPI>
+void launch_epi(const uint16_t* A, long lda, const uint16_t* B, long ldb, int M, int N, int K, const GemmEpi& ep,
+                int nwg, hipStream_t st) {
+  if (g_gemm_wn == 4)
+    launch_nt<EPI, 4>(A, lda, B, ldb, M, N, K, ep, nwg, st);
+  else
+    launch_nt<EPI, 2>(A, lda, B, ldb, M, N, K, ep, nwg, st);
+}
+
+}  // namespace
+
+void jm_gemm_set_variant(int wn, int group) {
+  g_gemm_wn = wn;
+  g_gemm_group = group;
+}
+
+// returns 0 on success, <0 on unsupported shape
+int jm_gemm_nt(const uint16_t* A, long lda, const uint16_t* B, long ldb, int M, int N, int K, int epi,
+               const GemmEpi& ep, hipStream_t st) {
+  if (K % (2 * BK) || N % 4 || M <= 0 || N <= 0) return -1;
+  if ((long)M * lda * 2 >= (1L << 32) || (long)N * ldb * 2 >= (1L << 32)) return -2;
+  const int nwg = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
+  if (epi == EPI_STORE)
+    launch_epi<EPI_STORE>(A, lda, B, ldb, M, N, K, ep, nwg, st);
+  else if (epi == EPI_GELU)
+    launch_epi<EPI_GELU>(A, lda, B, ldb, M, N, K, ep, nwg, st);
+  else
+    return -3;
+  return 0;
+}

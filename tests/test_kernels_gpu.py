@@ -181,3 +181,22 @@ def test_optimizer_hip_matches_torch(kind, clip):
         if dev == "cuda":
             assert torch.allclose(m.store.shadow.float().cpu(), m.store.master.cpu(), rtol=1e-2, atol=1e-3)
     assert rel(res[0], res[1]) < 1e-5
+
+
+@pytest.mark.parametrize("variant", [4, 2])
+@pytest.mark.parametrize("M,N,K,gelu", [(512, 256, 64, False), (300, 196, 128, True), (1000, 1536, 512, False),
+                                        (257, 260, 192, True)])
+def test_gemm_nt(ext, M, N, K, gelu, variant):
+    """Hand-written MFMA GEMM (csrc/gemm.hip) vs an fp32 reference, ragged M / N included."""
+    ext.gemm_set_variant(variant)
+    torch.manual_seed(0)
+    x = (torch.rand(M, K, device="cuda") * 2 - 1).bfloat16()
+    w = ((torch.rand(N, K, device="cuda") * 2 - 1) * 0.1).bfloat16()
+    b = torch.randn(N, device="cuda") * 0.1
+    outs = ext.gemm_nt(x, w, b, gelu)
+    ref = x.float() @ w.float().t() + b
+    assert rel(outs[0], ref) < 1e-2
+    if gelu:
+        g_ref = torch.nn.functional.gelu(outs[0].float(), approximate="tanh")
+        assert rel(outs[1], g_ref) < 1e-2
+    ext.gemm_set_variant(4, 8)

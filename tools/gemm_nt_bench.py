@@ -1,0 +1,92 @@
+"""Our MFMA GEMM (ext.gemm_nt) vs hipBLASLt (torch) on the flagship ViT-L Jumbo-MAE shapes.
+
+    python tools/gemm_nt_bench.py [--iters N] [--only name,...]
+
+fwd shapes: x[M,K] @ W[N,K]^T + b.  dgrad shapes: dy[M,N] @ W[N,K] given to our kernel as
+NT against the transposed weight W^T[K,N].  Interleaved timing in one process (A/B rounds)."""
+
+import argparse
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from jumbo_mae_tpu_amd.ops import _ext  # noqa: E402
+
+FWD = {
+    "enc_qkv": (26624, 3072, 1024), "enc_wo": (26624, 1024, 1024), "enc_ff1": (25088, 4096, 1024),
+    "enc_ff2": (25088, 1024, 4096), "jumbo1": (512, 12288, 3072), "jumbo2": (512, 3072, 12288),
+    "dec_qkv": (101888, 1536, 512), "dec_wo": (101888, 512, 512), "dec_ff1": (101888, 2048, 512),
+    "dec_ff2": (101888, 512, 2048),
+}
+
+
+def timeit(fn, iters):
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(iters):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) * 1e3 / iters
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--only", default="")
+    ap.add_argument("--kinds", default="fwd,fwd_gelu,dgrad")
+    ap.add_argument("--variant", type=int, default=4, help="waves along N (2 or 4)")
+    ap.add_argument("--group", type=int, default=8, help="row tiles per column sweep")
+    a = ap.parse_args()
+    ext = _ext.load()
+    ext.gemm_set_variant(a.variant, a.group)
+    names = [n for n in FWD if not a.only or n in a.only.split(",")]
+    tot = {"ours": 0.0, "blas": 0.0}
+    for kind in a.kinds.split(","):
+        for name in names:
+            M, N, K = FWD[name]
+            if kind == "fwd_gelu" and name not in ("enc_ff1", "dec_ff1", "jumbo1"):
+                continue
+            if kind == "dgrad":  # dX[M,K] = dy[M,N] @ W[N,K]  ->  NT with B = W^T [K, N]
+                M, N, K = M, K, N
+            x = (torch.rand(M, K, device="cuda") * 2 - 1).bfloat16()
+            w = ((torch.rand(N, K, device="cuda") * 2 - 1) * 0.05).bfloat16()
+            b = torch.randn(N, device="cuda") * 0.1
+            bb = b.bfloat16()
+            gelu = kind == "fwd_gelu"
+            if kind == "dgrad":
+                wm = w.t().contiguous()  # W as the model stores it: [N_fwd, K_fwd] = w^T
+                ours = lambda: ext.gemm_nt(x, w, None, False)  # noqa: E731
+                blas = lambda: x @ wm  # noqa: E731
+            elif gelu:
+                ours = lambda: ext.gemm_nt(x, w, b, True)  # noqa: E731
+                blas = lambda: torch.nn.functional.gelu(torch.addmm(bb, x, w.t()), approximate="tanh")  # noqa: E731
+            else:
+                ours = lambda: ext.gemm_nt(x, w, b, False)  # noqa: E731
+                blas = lambda: torch.addmm(bb, x, w.t())  # noqa: E731
+            out = ours()
+            ref = torch.addmm(b, x.float(), w.float().t())
+            err = ((out[0].float() - ref).abs().max() / ref.abs().max()).item()
+            if gelu:
+                g_ref = torch.nn.functional.gelu(out[0].float(), approximate="tanh")
+                err = max(err, ((out[1].float() - g_ref).abs().max() / g_ref.abs().max()).item())
+            blas()
+            torch.cuda.synchronize()
+            to, tb = [], []
+            for _ in range(a.rounds):
+                to.append(timeit(ours, a.iters))
+                tb.append(timeit(blas, a.iters))
+            to, tb = min(to), min(tb)
+            fl = 2.0 * M * N * K
+            tot["ours"] += to
+            tot["blas"] += tb
+            print(f"{kind:8s} {name:8s} M={M:6d} N={N:5d} K={K:5d}  ours {to:8.1f} us {fl / to / 1e6:6.0f} TF | "
+                  f"hipBLASLt {tb:8.1f} us {fl / tb / 1e6:6.0f} TF | x{tb / to:4.2f}  relerr {err:.1e}", flush=True)
+    print(f"total ours {tot['ours']:.0f} us  hipBLASLt {tot['blas']:.0f} us")
+
+
+if __name__ == "__main__":
+    main()
