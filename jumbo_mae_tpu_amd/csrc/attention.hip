@@ -138,7 +138,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const uint16_t* __restric
     for (int kt = 0; kt < NT; ++kt) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const float p = exp2f(sc[kt][i] - m);
+        const float p = __builtin_amdgcn_exp2f(sc[kt][i] - m);
         sc[kt][i] = p;
         l += p;
       }
@@ -317,7 +317,7 @@ __global__ __launch_bounds__((64 * bwd_waves<HD, SP>())) void attn_bwd_kernel(co
 #pragma unroll
               for (int i = 0; i < 4; ++i) {
                 const int q = q0 + 4 * g + i;
-                const float p = key < S ? exp2f(s[i] * sl2 - lse_s[q]) : 0.f;
+                const float p = key < S ? __builtin_amdgcn_exp2f(s[i] * sl2 - lse_s[q]) : 0.f;
                 const float ds = p * (dp[i] - delta_s[q]);
                 pf[4 * half + i] = p;
                 df[4 * half + i] = ds;
@@ -434,6 +434,293 @@ __global__ __launch_bounds__((64 * bwd_waves<HD, SP>())) void attn_bwd_kernel(co
   }
 }
 
+// ------------------------------------------------------------------ backward, compact variant
+// Same math and MFMA orientation as attn_bwd_kernel, re-laid out so two or more workgroups fit a
+// CU (their barriers and staging then overlap each other's MFMA work):
+//  * Q, dO, K images are unpadded [SP][HD] rows with the 16-byte chunks XOR-swizzled by aswz(row)
+//    (a GF(2) map found by exhaustive search: conflict-free for the ds_read_b128 fragment reads AND
+//    the ds_read_b64_tr_b16 transposed reads, 64 B and 128 B rows alike);
+//  * V never enters LDS: each wave only needs V rows of its own key tiles -> registers;
+//  * dS is stored TRANSPOSED ([key][64 queries], same swizzle): one ds_write_b64 of 4 consecutive
+//    queries per lane instead of four 2-byte stores, read back for dQ with the transposing read.
+// 4 waves, 64-query chunks, one 16-query dQ tile per wave per chunk.
+JM_DEVICE int aswz(int row) {
+  return ((row >> 2) & 1) | ((((row >> 2) ^ (row >> 3)) & 1) << 1) | (((row >> 1) & 1) << 2);
+}
+
+// element offset of (row, col) in a swizzled image of NCH 16-byte chunks per row
+template <int NCH>
+JM_DEVICE int swo(int row, int col) {
+  return row * (NCH * 8) + ((((col >> 3) ^ aswz(row)) & (NCH - 1)) << 3) + (col & 7);
+}
+
+template <int HD, int SP>
+constexpr size_t bwd2_smem() {
+  return (size_t)(3 * SP * HD + SP * 64) * 2 + (2 * SP + 3 * HD) * sizeof(float);
+}
+
+template <int HD, int SP>
+__global__ __launch_bounds__(256) void attn_bwd2_kernel(const uint16_t* __restrict__ qkv,
+                                                        const uint16_t* __restrict__ o,
+                                                        const uint16_t* __restrict__ dO,
+                                                        const float* __restrict__ lse,
+                                                        uint16_t* __restrict__ dqkv, int S, int H, float scale,
+                                                        float* __restrict__ dbp) {
+  constexpr int NW = 4, NTH = 256, QC = 64;
+  constexpr int NT = SP / 16, KK = HD / 32, DT = HD / 16;
+  constexpr int NKW = (NT + NW - 1) / NW;
+  constexpr int NCH = HD / 8;  // 16-byte chunks per Q / dO / K row
+  extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
+  uint16_t* Qs = smem;
+  uint16_t* dOs = Qs + SP * HD;
+  uint16_t* Ks = dOs + SP * HD;
+  uint16_t* dSt = Ks + SP * HD;  // [SP][QC], 8 chunks per row
+  float* lse_s = reinterpret_cast<float*>(dSt + SP * QC);
+  float* delta_s = lse_s + SP;
+  float* bsum = delta_s + SP;
+
+  const int bh = blockIdx.x;
+  const int b = bh / H, h = bh - (bh / H) * H;
+  const long ts = 3L * H * HD;
+  const long os = (long)H * HD;
+  const uint16_t* base = qkv + (long)b * S * ts;
+  const uint16_t* Qg = base + h * HD;
+  const uint16_t* Kg = base + (H + h) * HD;
+  const uint16_t* Vg = base + (2 * H + h) * HD;
+  const uint16_t* Og = o + (long)b * S * os + h * HD;
+  const uint16_t* dOg = dO + (long)b * S * os + h * HD;
+  uint16_t* dQg = dqkv + (long)b * S * ts + h * HD;
+  uint16_t* dKg = dqkv + (long)b * S * ts + (H + h) * HD;
+  uint16_t* dVg = dqkv + (long)b * S * ts + (2 * H + h) * HD;
+
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int l16 = lane & 15, g = lane >> 4;
+
+  // V fragments of this wave's key tiles straight from global (B operand of dP = dO V^T)
+  bf16x8_t vf[NKW][KK];
+#pragma unroll
+  for (int w = 0; w < NKW; ++w) {
+    const int key = (wave + NW * w) * 16 + l16;
+#pragma unroll
+    for (int kk = 0; kk < KK; ++kk) {
+      s16x8_t z = {0, 0, 0, 0, 0, 0, 0, 0};
+      vf[w][kk] = __builtin_bit_cast(bf16x8_t, z);
+      if (key < S) vf[w][kk] = ld8(Vg + (long)key * ts + 32 * kk + 8 * g);
+    }
+  }
+  for (int i = threadIdx.x; i < 3 * HD; i += NTH) bsum[i] = 0.f;
+  for (int i = threadIdx.x; i < SP; i += NTH) {
+    delta_s[i] = 0.f;
+    lse_s[i] = i < S ? lse[((long)b * H + h) * S + i] * LOG2E : INFINITY;
+  }
+  __syncthreads();
+  // staging: all global loads of the thread first (one latency), then LDS writes; delta = O . dO
+  constexpr int NIT = (SP * NCH + NTH - 1) / NTH;
+  uint4 qv[NIT], kv[NIT], dv[NIT], ov[NIT];
+#pragma unroll
+  for (int it = 0; it < NIT; ++it) {
+    const int i = it * NTH + threadIdx.x;
+    const int r = i / NCH, c = (i % NCH) * 8;
+    qv[it] = kv[it] = dv[it] = ov[it] = make_uint4(0, 0, 0, 0);
+    if (i < SP * NCH && r < S) {
+      qv[it] = *reinterpret_cast<const uint4*>(Qg + r * ts + c);
+      kv[it] = *reinterpret_cast<const uint4*>(Kg + r * ts + c);
+      dv[it] = *reinterpret_cast<const uint4*>(dOg + r * os + c);
+      ov[it] = *reinterpret_cast<const uint4*>(Og + r * os + c);
+    }
+  }
+#pragma unroll
+  for (int it = 0; it < NIT; ++it) {
+    const int i = it * NTH + threadIdx.x;
+    const int r = i / NCH, c = (i % NCH) * 8;
+    if (i < SP * NCH) {
+      const int off = swo<NCH>(r, c);
+      *reinterpret_cast<uint4*>(Qs + off) = qv[it];
+      *reinterpret_cast<uint4*>(Ks + off) = kv[it];
+      *reinterpret_cast<uint4*>(dOs + off) = dv[it];
+      if (r < S) {
+        const uint32_t* ow = reinterpret_cast<const uint32_t*>(&ov[it]);
+        const uint32_t* dw = reinterpret_cast<const uint32_t*>(&dv[it]);
+        float dsum = 0.f;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          dsum += __uint_as_float(ow[j] << 16) * __uint_as_float(dw[j] << 16);
+          dsum += __uint_as_float(ow[j] & 0xffff0000u) * __uint_as_float(dw[j] & 0xffff0000u);
+        }
+        atomicAdd(&delta_s[r], dsum);
+      }
+    }
+  }
+  __syncthreads();
+
+  const float sl2 = scale * LOG2E;
+  // Every swizzled address below is (16-row-aligned base) + (per-lane constant): aswz depends on
+  // row bits 1-3 only, and all bases are multiples of 16 rows.
+  int o_frag[KK];  // fragment row l16, chunk 4kk + g
+#pragma unroll
+  for (int kk = 0; kk < KK; ++kk) o_frag[kk] = swo<NCH>(l16, 32 * kk + 8 * g);
+  int o_tr[DT][2];  // transposing reads of rows 4g + l16/4 (+16), columns dt*16 + 4 (l16 & 3)
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt) {
+    o_tr[dt][0] = swo<NCH>(4 * g + (l16 >> 2), dt * 16 + 4 * (l16 & 3));
+    o_tr[dt][1] = swo<NCH>(4 * g + (l16 >> 2) + 16, dt * 16 + 4 * (l16 & 3));
+  }
+  int o_dsw[QC / 16];  // dS^T store: row l16, queries 16 j + 4 g .. + 3
+#pragma unroll
+  for (int j = 0; j < QC / 16; ++j) o_dsw[j] = swo<8>(l16, 16 * j + 4 * g);
+  const int krow = 8 * g + (l16 >> 2);  // dQ transposing reads: rows 32 s + krow (+4)
+  int o_dsr[2], o_kt[DT][2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    o_dsr[u] = swo<8>(krow + 4 * u, wave * 16 + 4 * (l16 & 3));
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) o_kt[dt][u] = swo<NCH>(krow + 4 * u, dt * 16 + 4 * (l16 & 3));
+  }
+
+  bf16x8_t kf[NKW][KK];
+  f32x4_t dvacc[NKW][DT], dkacc[NKW][DT];
+#pragma unroll
+  for (int w = 0; w < NKW; ++w) {
+#pragma unroll
+    for (int kk = 0; kk < KK; ++kk) kf[w][kk] = ld8(Ks + (wave + NW * w) * 16 * HD + o_frag[kk]);
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) {
+      dvacc[w][dt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+      dkacc[w][dt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    }
+  }
+
+  for (int qc = 0; qc * QC < SP; ++qc) {
+#pragma unroll
+    for (int w = 0; w < NKW; ++w) {
+      const int kt = wave + NW * w;
+      if (kt < NT) {
+        const float kmask = kt * 16 + l16 < S ? 1.f : 0.f;  // padded keys: P = 0
+        uint16_t* dsw = dSt + kt * 16 * QC;
+#pragma unroll
+        for (int r = 0; r < QC / 32; ++r) {
+          const int qbase = qc * QC + 32 * r;
+          if (qbase < SP) {
+            float pf[8], df[8];
+#pragma unroll
+            for (int half = 0; half < 2; ++half) {
+              const int q0 = qbase + 16 * half;
+              f32x4_t sacc = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+              for (int kk = 0; kk < KK; ++kk) {
+                sacc = mfma(ld8(Qs + q0 * HD + o_frag[kk]), kf[w][kk], sacc);
+                dp = mfma(ld8(dOs + q0 * HD + o_frag[kk]), vf[w][kk], dp);
+              }
+              // sacc[i] = S[q = q0 + 4g + i][key]
+              const float4 l4 = *reinterpret_cast<const float4*>(lse_s + q0 + 4 * g);
+              const float4 d4 = *reinterpret_cast<const float4*>(delta_s + q0 + 4 * g);
+              const float lv[4] = {l4.x, l4.y, l4.z, l4.w}, dv[4] = {d4.x, d4.y, d4.z, d4.w};
+#pragma unroll
+              for (int i = 0; i < 4; ++i) {
+                const float p = kmask * __builtin_amdgcn_exp2f(sacc[i] * sl2 - lv[i]);
+                pf[4 * half + i] = p;
+                df[4 * half + i] = p * (dp[i] - dv[i]);
+              }
+              uint2 pk;
+              pk.x = pack_bf2(df[4 * half], df[4 * half + 1]);
+              pk.y = pack_bf2(df[4 * half + 2], df[4 * half + 3]);
+              *reinterpret_cast<uint2*>(dsw + o_dsw[2 * r + half]) = pk;
+            }
+            const bf16x8_t pb = pack8(pf);
+            const bf16x8_t dsb = pack8(df);
+#pragma unroll
+            for (int dt = 0; dt < DT; ++dt) {
+              const uint16_t* dor = dOs + qbase * HD;
+              const uint16_t* qr = Qs + qbase * HD;
+              const bf16x8_t a_do = cat44(tr4(dor + o_tr[dt][0]), tr4(dor + o_tr[dt][1]));
+              const bf16x8_t a_q = cat44(tr4(qr + o_tr[dt][0]), tr4(qr + o_tr[dt][1]));
+              dvacc[w][dt] = mfma(a_do, pb, dvacc[w][dt]);
+              dkacc[w][dt] = mfma(a_q, dsb, dkacc[w][dt]);
+            }
+          }
+        }
+      }
+    }
+    __syncthreads();
+    // dQ^T[d][q] = sum_key K^T[d][key] dS^T[key][q] for this wave's 16 queries of the chunk
+    {
+      const int qt = qc * (QC / 16) + wave;
+      if (qt < NT) {
+        f32x4_t dq[DT];
+#pragma unroll
+        for (int dt = 0; dt < DT; ++dt) dq[dt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < SP / 32; ++s) {
+          const uint16_t* dsr = dSt + 32 * s * QC;
+          const uint16_t* kr = Ks + 32 * s * HD;
+          const bf16x8_t bop = cat44(tr4(dsr + o_dsr[0]), tr4(dsr + o_dsr[1]));
+#pragma unroll
+          for (int dt = 0; dt < DT; ++dt) {
+            const bf16x8_t ka = cat44(tr4(kr + o_kt[dt][0]), tr4(kr + o_kt[dt][1]));
+            dq[dt] = mfma(ka, bop, dq[dt]);
+          }
+        }
+        if (dbp != nullptr) {
+#pragma unroll
+          for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              const float v = row16_sum(dq[dt][i]);
+              if (l16 == 0) atomicAdd(&bsum[dt * 16 + 4 * g + i], v * scale);
+            }
+        }
+        const int q = qt * 16 + l16;
+        if (q < S) {
+#pragma unroll
+          for (int dt = 0; dt < DT; ++dt) {
+            float v[4] = {dq[dt][0] * scale, dq[dt][1] * scale, dq[dt][2] * scale, dq[dt][3] * scale};
+            store4(dQg + (long)q * ts + dt * 16 + 4 * g, v);
+          }
+        }
+      }
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int w = 0; w < NKW; ++w) {
+    const int kt = wave + NW * w;
+    const int key = kt * 16 + l16;
+    if (kt < NT && key < S) {
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt) {
+        float kv[4] = {dkacc[w][dt][0] * scale, dkacc[w][dt][1] * scale, dkacc[w][dt][2] * scale,
+                       dkacc[w][dt][3] * scale};
+        float vv[4] = {dvacc[w][dt][0], dvacc[w][dt][1], dvacc[w][dt][2], dvacc[w][dt][3]};
+        store4(dKg + (long)key * ts + dt * 16 + 4 * g, kv);
+        store4(dVg + (long)key * ts + dt * 16 + 4 * g, vv);
+      }
+    }
+  }
+  if (dbp != nullptr) {
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        float sk = 0.f, sv = 0.f;
+#pragma unroll
+        for (int w = 0; w < NKW; ++w) {
+          sk += dkacc[w][dt][i];
+          sv += dvacc[w][dt][i];
+        }
+        sk = row16_sum(sk);
+        sv = row16_sum(sv);
+        if (l16 == 0) {
+          const int d = dt * 16 + 4 * g + i;
+          atomicAdd(&bsum[HD + d], sk * scale);
+          atomicAdd(&bsum[2 * HD + d], sv);
+        }
+      }
+    __syncthreads();
+    float* dst = dbp + (long)b * ts + h * HD;
+    for (int i = threadIdx.x; i < 3 * HD; i += NTH) dst[(i / HD) * H * HD + (i % HD)] = bsum[i];
+  }
+}
+
 template <int HD, int SP, bool TR>
 size_t fwd_smem() { return (size_t)(SP * (HD + 8) + (TR ? SP * (HD + 8) : HD * (SP + 8))) * 2; }
 template <int HD, int SP, bool TR>
@@ -442,7 +729,7 @@ size_t bwd_smem() {
          (2 * SP + 3 * HD) * sizeof(float);
 }
 
-int g_use_tr = 1;  // runtime switch (tests run both variants)
+int g_use_tr = 2;  // runtime switch: 2 = compact backward (bwd2) + TR forward, 1 = TR, 0 = transposed images
 
 template <int HD, int SP, bool TR>
 int run_t(bool fwd, const uint16_t* qkv, const uint16_t* o, const uint16_t* dO, const float* lse_in, uint16_t* out,
@@ -465,8 +752,24 @@ int run_t(bool fwd, const uint16_t* qkv, const uint16_t* o, const uint16_t* dO, 
 }
 
 template <int HD, int SP>
+int run_bwd2(const uint16_t* qkv, const uint16_t* o, const uint16_t* dO, const float* lse_in, uint16_t* out,
+             float* dbias_part, int B, int S, int H, float scale, hipStream_t st) {
+  constexpr size_t sm = bwd2_smem<HD, SP>();
+  if (sm > 160 * 1024) return -3;
+  static bool attr_set = false;
+  if (sm > 64 * 1024 && !attr_set) {
+    (void)hipFuncSetAttribute((const void*)attn_bwd2_kernel<HD, SP>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)sm);
+    attr_set = true;
+  }
+  attn_bwd2_kernel<HD, SP><<<dim3(B * H), 256, sm, st>>>(qkv, o, dO, lse_in, out, S, H, scale, dbias_part);
+  return 0;
+}
+
+template <int HD, int SP>
 int run(bool fwd, const uint16_t* qkv, const uint16_t* o, const uint16_t* dO, const float* lse_in, uint16_t* out,
         float* lse_out, int B, int S, int H, float scale, hipStream_t st) {
+  if (g_use_tr == 2 && !fwd) return run_bwd2<HD, SP>(qkv, o, dO, lse_in, out, lse_out, B, S, H, scale, st);
   if (g_use_tr) return run_t<HD, SP, true>(fwd, qkv, o, dO, lse_in, out, lse_out, B, S, H, scale, st);
   return run_t<HD, SP, false>(fwd, qkv, o, dO, lse_in, out, lse_out, B, S, H, scale, st);
 }
