@@ -50,6 +50,7 @@ def main():
     from jumbo_mae_tpu_amd.parallel import dist as pdist
     from jumbo_mae_tpu_amd.parallel.ddp import GradReducer
     from jumbo_mae_tpu_amd.train.engine import Trainer
+    from jumbo_mae_tpu_amd.utils.flops import mfu, pretrain_fwd_flops_per_image
     from jumbo_mae_tpu_amd.utils.rng import RngStreams
 
     info = pdist.init_distributed()
@@ -137,6 +138,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
+            "mfu_bf16_dense": round(mfu(value, pretrain_fwd_flops_per_image(vc, dc), world), 4),
             "dtype": "bf16",
             "data": "synthetic uint8 224x224 images on GPU, random-init weights",
             "config": {

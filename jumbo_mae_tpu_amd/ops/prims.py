@@ -204,12 +204,23 @@ def residual_bwd(dout3: torch.Tensor, y2: torch.Tensor | None, hs: Handle | None
 
 
 # ------------------------------------------------------------------------------ attention
+def _attn_hip(qkv: torch.Tensor, heads: int) -> bool:
+    """The fused whole-sequence-in-LDS kernels cover S <= attn_max_seq() (224: every flagship
+    shape) and head dims 32 / 64; longer sequences (e.g. finetuning at 448 px,
+    S = 787) take the PyTorch composition below (fp32 softmax, same numerics)."""
+    if not hip(qkv):
+        return False
+    B, S, three_d = qkv.shape
+    hd = three_d // 3 // heads
+    return S <= _ext.load().attn_max_seq() and hd in (32, 64)
+
+
 def attn_fwd(qkv: torch.Tensor, heads: int):
     """qkv [B, S, 3*D] -> (o [B, S, D], lse [B, H, S])."""
     B, S, three_d = qkv.shape
     D = three_d // 3
     hd = D // heads
-    if hip(qkv):
+    if _attn_hip(qkv, heads):
         return _ext.load().attn_fwd(qkv, heads)
     q, k, v = qkv.float().view(B, S, 3, heads, hd).unbind(2)
     z = torch.einsum("bqhd,bkhd->bhqk", q / math.sqrt(hd), k)
@@ -227,7 +238,7 @@ def attn_bwd(do: torch.Tensor, qkv: torch.Tensor, o: torch.Tensor, lse: torch.Te
     D = three_d // 3
     hd = D // heads
     do = do.contiguous().view(B, S, D)
-    if hip(qkv):
+    if _attn_hip(qkv, heads):
         bg = hbias.grad if _trainable(hbias) else None
         return _ext.load().attn_bwd(do, qkv, o, lse, heads, bg), bg is not None
     q, k, v = qkv.float().view(B, S, 3, heads, hd).unbind(2)

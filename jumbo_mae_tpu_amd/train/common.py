@@ -144,3 +144,21 @@ def check_finite(metrics: dict, step: int):
     v = metrics.get("train/loss")
     if v is not None and not (v == v and abs(v) != float("inf")):
         raise FloatingPointError(f"non-finite training loss at step {step}: {v}")
+
+
+class PerfClock:
+    """perf/* log keys: images/sec, step time and MFU over each log window."""
+
+    def __init__(self, start_step: int, global_batch: int, fwd_flops_per_image: float, world_size: int):
+        self.t, self.step = time.time(), start_step
+        self.batch, self.flops, self.world = global_batch, fwd_flops_per_image, world_size
+
+    def summary(self, step: int) -> dict:
+        from ..utils.flops import mfu
+        now = time.time()
+        dt = max(now - self.t, 1e-9)
+        n = max(step - self.step, 1)
+        ips = n * self.batch / dt
+        self.t, self.step = now, step
+        return {"perf/images_per_sec": ips, "perf/step_ms": 1e3 * dt / n,
+                "perf/mfu": mfu(ips, self.flops, self.world)}

@@ -15,11 +15,14 @@ import torch
 from ..optim.flat import FlatOptimizer
 from ..parallel.ddp import GradReducer
 from ..utils.rng import RngStreams
+from ..utils.trace import trace_range
 
 
 class Trainer:
     def __init__(self, model, optimizer: FlatOptimizer, reducer: GradReducer | None = None,
-                 rngs: RngStreams | None = None, grad_accum: int = 1):
+                 rngs: RngStreams | None = None, grad_accum: int = 1, skip_nonfinite: bool = False):
+        self.skip_nonfinite = skip_nonfinite
+        self.skipped_steps = 0
         self.model = model
         self.opt = optimizer
         self.reducer = reducer
@@ -41,15 +44,27 @@ class Trainer:
         for i, args in enumerate(micro_batches):
             if self.reducer is not None:
                 self.reducer.set_sync(i == n - 1)
-            out = self.model(*args, rngs=rng, det=False)
+            with trace_range("fwd"):
+                out = self.model(*args, rngs=rng, det=False)
             loss = out["loss"]
-            (loss / n).backward()
+            with trace_range("bwd"):
+                (loss / n).backward()
             m = {k: v.detach().float() for k, v in out.items()}
             metrics_acc = m if metrics_acc is None else {k: metrics_acc[k] + m[k] for k in m}
         if self.reducer is not None:
-            self.reducer.set_sync(True)
-            self.reducer.finish()
-        lr = self.opt.step()
+            with trace_range("allreduce_wait"):
+                self.reducer.set_sync(True)
+                self.reducer.finish()
+        if self.skip_nonfinite:
+            # opt-in guard (one host sync per step): drop the update of a step whose loss is
+            # not finite instead of poisoning the weights / optimizer moments
+            if not bool(torch.isfinite(metrics_acc["loss"]).item()):
+                self.skipped_steps += 1
+                metrics = {k: v / n for k, v in metrics_acc.items()}
+                metrics["learning_rate"] = self.opt.last_lr if hasattr(self.opt, "last_lr") else 0.0
+                return metrics
+        with trace_range("optimizer"):
+            lr = self.opt.step()
         metrics = {k: v / n for k, v in metrics_acc.items()}
         metrics["learning_rate"] = lr
         return metrics

@@ -21,7 +21,9 @@ from ..config import ViTConfig
 from ..data.loader import create_dataloaders
 from ..models.classifier import FinetuneModel
 from ..parallel import dist as pdist
+from ..utils.flops import finetune_fwd_flops_per_image
 from ..utils.mixup import Mixup
+from ..utils.trace import set_enabled as set_trace_ranges
 from ..utils.rng import RngStreams
 from . import common as C
 from .cli import finetune_parser
@@ -54,6 +56,7 @@ def evaluate(model, loader, rngs, device) -> dict:
 
 def main(args) -> dict:
     info = pdist.init_distributed(args.device)
+    set_trace_ranges(args.trace_ranges)
     device = info.device
     log = print if info.is_main else (lambda *a, **k: None)
     dtype = C.compute_dtype(args, device)
@@ -72,7 +75,7 @@ def main(args) -> dict:
     reducer = C.make_reducer(args, model.store)
     rngs = RngStreams({"mixup": args.mixup_seed, "dropout": args.dropout_seed, "noise": args.noise_seed},
                       info.rank, device)
-    trainer = Trainer(model, opt, reducer, rngs, args.grad_accum)
+    trainer = Trainer(model, opt, reducer, rngs, args.grad_accum, skip_nonfinite=args.skip_nonfinite)
     start = C.maybe_resume(args, model, opt, rngs, log)
 
     def extra():
@@ -92,6 +95,7 @@ def main(args) -> dict:
     max_acc1 = 0.0
     it = C.DevicePrefetcher(train_loader, device) if train_loader is not None else None
     t0 = time.time()
+    perf = C.PerfClock(start, args.train_batch_size, finetune_fwd_flops_per_image(model.cfg), info.world_size)
     for step in range(start + 1, args.training_steps + 1):
         micro = [tuple(next(it)) for _ in range(args.grad_accum)]
         metrics = trainer.train_step(micro)
@@ -99,6 +103,7 @@ def main(args) -> dict:
         if args.log_interval > 0 and step % args.log_interval == 0:
             summ = meter.summary("train/")
             summ["processed_samples"] = step * args.train_batch_size
+            summ.update(perf.summary(step))
             C.check_finite(summ, step)
             if info.is_main:
                 logger.log(summ, step)

@@ -21,7 +21,9 @@ from ..config import DecoderConfig, ViTConfig
 from ..data.loader import create_dataloaders
 from ..models.mae import PretrainModel
 from ..parallel import dist as pdist
+from ..utils.flops import pretrain_fwd_flops_per_image
 from ..utils.rng import RngStreams
+from ..utils.trace import set_enabled as set_trace_ranges
 from . import common as C
 from .cli import pretrain_parser
 from .engine import Trainer
@@ -56,6 +58,7 @@ def evaluate(model, loader, rngs, device) -> dict:
 
 def main(args) -> dict:
     info = pdist.init_distributed(args.device)
+    set_trace_ranges(args.trace_ranges)
     device = info.device
     log = print if info.is_main else (lambda *a, **k: None)
     dtype = C.compute_dtype(args, device)
@@ -67,7 +70,7 @@ def main(args) -> dict:
     reducer = C.make_reducer(args, model.store)
     rngs = RngStreams({"mixup": args.mixup_seed, "dropout": args.dropout_seed, "noise": args.noise_seed},
                       info.rank, device)
-    trainer = Trainer(model, opt, reducer, rngs, args.grad_accum)
+    trainer = Trainer(model, opt, reducer, rngs, args.grad_accum, skip_nonfinite=args.skip_nonfinite)
     start = C.maybe_resume(args, model, opt, rngs, log)
 
     train_loader, valid_loader = create_dataloaders(args, info.rank, info.world_size)
@@ -82,7 +85,8 @@ def main(args) -> dict:
     min_val_loss = 1e9
     it = C.DevicePrefetcher(train_loader, device) if train_loader is not None else None
     t0 = time.time()
-    last_t, last_step = t0, start
+    perf = C.PerfClock(start, args.train_batch_size, pretrain_fwd_flops_per_image(model.cfg, model.dec_cfg),
+                       info.world_size)
     for step in range(start + 1, args.training_steps + 1):
         micro = []
         for _ in range(args.grad_accum):
@@ -92,10 +96,8 @@ def main(args) -> dict:
         meter.update(**metrics)
         if args.log_interval > 0 and step % args.log_interval == 0:
             summ = meter.summary("train/")
-            now = time.time()
             summ["processed_samples"] = step * args.train_batch_size
-            summ["perf/images_per_sec"] = (step - last_step) * args.train_batch_size / max(now - last_t, 1e-9)
-            last_t, last_step = now, step
+            summ.update(perf.summary(step))
             C.check_finite(summ, step)
             if info.is_main:
                 logger.log(summ, step)

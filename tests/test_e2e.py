@@ -63,3 +63,27 @@ def test_finetune_and_linear(tmp_path, mode, opt, lr):
     res = FT.main(args)
     assert 0.0 <= res["val/acc1"] <= 1.0 and res["val/acc5"] >= res["val/acc1"]
     assert os.path.exists(os.path.join(out, "f-best.msgpack"))
+
+
+def test_skip_nonfinite_step_leaves_weights_untouched():
+    """--skip-nonfinite: a step whose loss is NaN applies no update."""
+    import torch
+
+    from jumbo_mae_tpu_amd.config import DecoderConfig, ViTConfig
+    from jumbo_mae_tpu_amd.models.mae import PretrainModel
+    from jumbo_mae_tpu_amd.optim.flat import FlatOptimizer
+    from jumbo_mae_tpu_amd.train.engine import Trainer
+    vc = ViTConfig(layers=1, dim=32, heads=4, labels=0, image_size=32, patch_size=8, posemb="sincos2d")
+    dc = DecoderConfig(dec_layers=1, dec_dim=16, dec_heads=2, image_size=32, patch_size=8)
+    m = PretrainModel(vc, dc).to("cpu")
+    opt = FlatOptimizer(m.store, "adamw", lambda c: 1e-3, weight_decay=0.05)
+    tr = Trainer(m, opt, skip_nonfinite=True)
+    imgs = torch.randint(0, 256, (2, 3, 32, 32), dtype=torch.uint8)
+    tr.train_step([(imgs,)])
+    assert tr.skipped_steps == 0
+    with torch.no_grad():
+        m.store.master[0] = float("nan")  # poisons the patch-embedding kernel -> NaN loss
+    before = m.store.master.clone()
+    tr.train_step([(imgs,)])
+    assert tr.skipped_steps == 1
+    assert torch.equal(torch.nan_to_num(m.store.master, nan=7.0), torch.nan_to_num(before, nan=7.0))

@@ -200,3 +200,22 @@ def test_gemm_nt(ext, M, N, K, gelu, variant):
         g_ref = torch.nn.functional.gelu(outs[0].float(), approximate="tanh")
         assert rel(outs[1], g_ref) < 1e-2
     ext.gemm_set_variant(4, 8)
+
+
+def test_attention_long_sequence_path():
+    """S > attn_max_seq() (finetune at 448 px: S = 787) takes the PyTorch composition; check it
+    against the fp64 reference incl. gradients (prims level)."""
+    from jumbo_mae_tpu_amd.ops import prims as P
+    torch.manual_seed(0)
+    B, S, H, hd = 2, 300, 4, 64
+    qkv = (torch.randn(B, S, 3 * H * hd, device="cuda") * 1.5).bfloat16()
+    o, lse = P.attn_fwd(qkv, H)
+    orf, lser = _attn_ref(qkv, H)
+    assert rel(o, orf) < 1e-2
+    do = torch.randn(B, S, H * hd, device="cuda").bfloat16()
+    dqkv, done = P.attn_bwd(do, qkv, o, lse, H)
+    assert not done
+    qr = qkv.double().requires_grad_()
+    o2, _ = _attn_ref(qr, H)
+    o2.backward(do.double())
+    assert rel(dqkv, qr.grad) < 2e-2

@@ -75,3 +75,13 @@ def test_sincos_table_values():
     np.testing.assert_allclose(t[3, 5, 256:384], np.sin(3 * freqs), atol=1e-5)
     np.testing.assert_allclose(t[3, 5, 384:], np.cos(3 * freqs), atol=1e-5)
     assert abs(freqs[-1] - 1e-4) < 1e-12
+
+
+def test_flop_counts_match_baseline():
+    """Forward FLOPs/image of SURVEY.md §2.2 / BASELINE.md (20.7 GF ViT-B, 45.3 GF ViT-L) within 2%."""
+    from jumbo_mae_tpu_amd.config import decoder_config, vit_config
+    from jumbo_mae_tpu_amd.utils.flops import mfu, pretrain_fwd_flops_per_image
+    for name, ref in (("vit_base_patch16", 20.7e9), ("vit_large_patch16", 45.3e9)):
+        f = pretrain_fwd_flops_per_image(vit_config(name, labels=0, posemb="sincos2d"), decoder_config())
+        assert abs(f - ref) / ref < 0.02, (name, f)
+    assert abs(mfu(1000.0, 1e12, 2, peak=1e15) - 1.5) < 1e-9
