@@ -116,7 +116,9 @@ JM_DEVICE void tile_of(int M, int N, int GROUP_M, int& m0, int& n0) {
 
 // WN waves along N (2 along M): WN = 4 -> 8 waves of 128 x 64 (2 waves / SIMD);
 // WN = 2 -> 4 waves of 128 x 128 (1 wave / SIMD, accumulators in AGPRs)
-template <int EPI, int WN>
+// ABL (diagnostics only, tools/gemm_nt_bench.py --variant 41/42/44): 1 = no in-loop staging
+// loads, 2 = no barrier / vmcnt wait, 4 = no fragment re-reads.  Outputs are wrong by design.
+template <int EPI, int WN, int ABL = 0>
 __global__ __launch_bounds__(128 * WN, 1) void gemm_nt_kernel(const uint16_t* __restrict__ A, long lda,
                                                               const uint16_t* __restrict__ B, long ldb, int M,
                                                               int N, int K, GemmEpi ep, int GROUP_M) {
@@ -183,15 +185,16 @@ __global__ __launch_bounds__(128 * WN, 1) void gemm_nt_kernel(const uint16_t* __
   };
   auto step = [&](auto kind, int t, Frags<NTW>& cur, Frags<NTW>& nxt) {
     constexpr int KIND = decltype(kind)::value;
-    if constexpr (KIND == 3) issue(t + 3);
+    if constexpr (KIND == 3 && !(ABL & 1)) issue(t + 3);
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
       for (int nt = 0; nt < NTW; ++nt) acc[mt][nt] = mfma16(cur.b[nt], cur.a[mt], acc[mt][nt]);
     __builtin_amdgcn_sched_barrier(0);
-    if constexpr (KIND > 0) wait_bar(std::integral_constant<int, KIND - 1>{});
+    if constexpr (KIND > 0 && !(ABL & 2)) wait_bar(std::integral_constant<int, (ABL & 1) ? 0 : KIND - 1>{});
     __builtin_amdgcn_sched_barrier(0);
-    if constexpr (KIND > 0) read(t + 1, nxt);
+    if constexpr (KIND > 0 && !(ABL & 4)) read(t + 1, nxt);
+    if constexpr (KIND > 0 && (ABL & 4)) nxt = cur;
 #pragma unroll
     for (int mt = 4; mt < 8; ++mt)
 #pragma unroll
@@ -246,16 +249,17 @@ size_t jm_gemm_smem() { return (size_t)NST * STAGE * sizeof(uint16_t); }
 int g_gemm_wn = 4;     // runtime switches for A/B (jm_gemm_set_variant)
 int g_gemm_group = 8;
 
-template <int EPI, int WN>
+template <int EPI, int WN, int ABL = 0>
 void launch_nt(const uint16_t* A, long lda, const uint16_t* B, long ldb, int M, int N, int K, const GemmEpi& ep,
                int nwg, hipStream_t st) {
   static bool attr = false;
   const size_t sm = jm_gemm_smem();
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)gemm_nt_kernel<EPI, WN>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
+    (void)hipFuncSetAttribute((const void*)gemm_nt_kernel<EPI, WN, ABL>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)sm);
     attr = true;
   }
-  gemm_nt_kernel<EPI, WN><<<nwg, 128 * WN, sm, st>>>(A, lda, B, ldb, M, N, K, ep, g_gemm_group);
+  gemm_nt_kernel<EPI, WN, ABL><<<nwg, 128 * WN, sm, st>>>(A, lda, B, ldb, M, N, K, ep, g_gemm_group);
 }
 
 template <int EPI>
@@ -263,6 +267,14 @@ void launch_epi(const uint16_t* A, long lda, const uint16_t* B, long ldb, int M,
                 int nwg, hipStream_t st) {
   if (g_gemm_wn == 4)
     launch_nt<EPI, 4>(A, lda, B, ldb, M, N, K, ep, nwg, st);
+  else if (EPI == EPI_STORE && g_gemm_wn == 41)
+    launch_nt<EPI, 4, 1>(A, lda, B, ldb, M, N, K, ep, nwg, st);
+  else if (EPI == EPI_STORE && g_gemm_wn == 42)
+    launch_nt<EPI, 4, 2>(A, lda, B, ldb, M, N, K, ep, nwg, st);
+  else if (EPI == EPI_STORE && g_gemm_wn == 44)
+    launch_nt<EPI, 4, 4>(A, lda, B, ldb, M, N, K, ep, nwg, st);
+  else if (EPI == EPI_STORE && g_gemm_wn == 47)
+    launch_nt<EPI, 4, 7>(A, lda, B, ldb, M, N, K, ep, nwg, st);
   else
     launch_nt<EPI, 2>(A, lda, B, ldb, M, N, K, ep, nwg, st);
 }

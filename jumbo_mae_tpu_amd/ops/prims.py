@@ -12,6 +12,7 @@ owns into the flat fp32 gradient buffer and signals readiness to the data-parall
 from __future__ import annotations
 
 import math
+import os
 
 import torch
 import torch.nn.functional as F
@@ -79,16 +80,64 @@ def linear_fwd(x2: torch.Tensor, hw: Handle, hb: Handle | None) -> torch.Tensor:
     return x2 @ w.t()
 
 
+# ------------------------------------------------------------------ weight-gradient stream
+# The weight-gradient GEMMs are off the backward critical path (nothing in the backward reads
+# them), so they run on a second HIP stream: hipBLASLt's 4-wave, <=256-VGPR workgroups leave
+# room on every CU for the memory-bound LayerNorm / GELU / residual / attention kernels of the
+# data-gradient chain, which then execute underneath them instead of after them.  The chain's
+# tensors are pinned for the side stream with record_stream; the DP reducer launches its
+# all-reduces from this stream and the trainer joins it before the optimizer.
+_side = {"stream": None, "enabled": os.environ.get("JMAE_WGRAD_STREAM", "1") == "1", "cb": False}
+
+
+def _end_of_backward() -> None:
+    _side["cb"] = False
+    join_wgrad_stream()
+
+
+def wgrad_stream():
+    """The side stream (created lazily), or None when disabled / not on a GPU."""
+    if not _side["enabled"] or not torch.cuda.is_available():
+        return None
+    if _side["stream"] is None:
+        _side["stream"] = torch.cuda.Stream()
+    return _side["stream"]
+
+
+def set_wgrad_stream(enabled: bool) -> None:
+    _side["enabled"] = bool(enabled)
+
+
+def join_wgrad_stream() -> None:
+    """Make the current stream wait for every queued weight-gradient GEMM."""
+    s = _side["stream"]
+    if s is not None:
+        torch.cuda.current_stream().wait_stream(s)
+
+
 def linear_bwd(dy: torch.Tensor, x2: torch.Tensor, hw: Handle, hb: Handle | None, need_dx: bool = True,
                bias_done: bool = False):
     """dx = dy @ W (if needed); grad W += dy^T x; grad b += colsum(dy) (unless fused upstream)."""
     dx = dy @ hw.weight() if need_dx else None
     if _trainable(hw):
-        wgrad(hw, dy, x2)
+        side = wgrad_stream() if dy.is_cuda else None
+        if side is not None:
+            if not _side["cb"]:  # the backward pass returns only after joining the side stream
+                torch.autograd.Variable._execution_engine.queue_callback(_end_of_backward)
+                _side["cb"] = True
+            side.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(side):
+                wgrad(hw, dy, x2)
+                if hb is not None and not bias_done:
+                    bias_grad(hb, dy)
+            dy.record_stream(side)
+            x2.record_stream(side)
+        else:
+            wgrad(hw, dy, x2)
+            if hb is not None and not bias_done:
+                bias_grad(hb, dy)
         hw.ready()
         if hb is not None:
-            if not bias_done:
-                bias_grad(hb, dy)
             hb.ready()
     return dx
 

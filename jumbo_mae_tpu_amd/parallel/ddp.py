@@ -118,12 +118,23 @@ class GradReducer:
 
     def _allreduce(self, t: torch.Tensor):
         if dist.get_backend(self.group) == "nccl":
+            # issue from the weight-gradient stream (ops/prims.py) after it has caught up with
+            # the main stream: RCCL then waits for the GEMM that wrote the bucket's last kernel
+            # gradient without stalling the backward chain on the main stream
+            from ..ops.prims import wgrad_stream
+            side = wgrad_stream() if t.is_cuda else None
+            if side is not None:
+                side.wait_stream(torch.cuda.current_stream())
+                with torch.cuda.stream(side):
+                    return dist.all_reduce(t, op=dist.ReduceOp.AVG, group=self.group, async_op=True)
             return dist.all_reduce(t, op=dist.ReduceOp.AVG, group=self.group, async_op=True)
         w = dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
         return (w, t)
 
     def finish(self) -> None:
         """Launch any bucket not yet reduced (unused segments / no overlap) and wait for all."""
+        from ..ops.prims import join_wgrad_stream
+        join_wgrad_stream()
         if not self.enabled or not self.sync:
             return
         for b in range(len(self.buckets)):

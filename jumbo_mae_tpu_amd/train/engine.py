@@ -12,6 +12,7 @@ from __future__ import annotations
 
 import torch
 
+from ..ops.prims import join_wgrad_stream
 from ..optim.flat import FlatOptimizer
 from ..parallel.ddp import GradReducer
 from ..utils.rng import RngStreams
@@ -51,6 +52,7 @@ class Trainer:
                 (loss / n).backward()
             m = {k: v.detach().float() for k, v in out.items()}
             metrics_acc = m if metrics_acc is None else {k: metrics_acc[k] + m[k] for k in m}
+        join_wgrad_stream()  # weight-gradient GEMMs run on a side stream (ops/prims.py)
         if self.reducer is not None:
             with trace_range("allreduce_wait"):
                 self.reducer.set_sync(True)
