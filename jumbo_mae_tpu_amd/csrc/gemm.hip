@@ -116,6 +116,56 @@ JM_DEVICE void tile_of(int M, int N, int GROUP_M, int& m0, int& n0) {
 
 // WN waves along N (2 along M): WN = 4 -> 8 waves of 128 x 64 (2 waves / SIMD);
 // WN = 2 -> 4 waves of 128 x 128 (1 wave / SIMD, accumulators in AGPRs)
+// Coalesced epilogue through LDS (the staging ring is free once the K loop has drained):
+// (1) every wave adds the bias to its accumulators, rounds to bf16 and writes its sub-tile into
+//     a [256][256] bf16 image whose 16-byte chunks are XOR-swizzled by (row & 15) -- the
+//     ds_write_b64 of 16 rows x 8 B and the ds_read_b128 row reads are both conflict-free;
+// (2) the workgroup streams the tile out row by row, 16 B per lane, 512 B per row: full 128 B
+//     lines instead of 16 rows x 32 B per store instruction.  GELU is applied in (2) to the
+//     rounded pre-activation, which is exactly what the backward will see.
+template <int EPI, int NTW, int NTH>
+JM_DEVICE void epilogue_lds(const f32x4_t (&acc)[8][NTW], const GemmEpi& ep, uint16_t* cs, int M, int N, int m0,
+                            int n0, int wr, int wc, int l16, int g) {
+  constexpr int RB = BN;  // elements per LDS image row
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+#pragma unroll
+  for (int nt = 0; nt < NTW; ++nt) {
+    const int nl = wc * NTW * 16 + nt * 16 + 4 * g;  // tile-local column
+    float bv[4] = {0.f, 0.f, 0.f, 0.f};
+    if (ep.bias && n0 + nl < N) load4(ep.bias + n0 + nl, bv);
+#pragma unroll
+    for (int mt = 0; mt < 8; ++mt) {
+      const int r = wr * 128 + mt * 16 + l16;
+      uint2 pk;
+      pk.x = pack_bf2(acc[mt][nt][0] + bv[0], acc[mt][nt][1] + bv[1]);
+      pk.y = pack_bf2(acc[mt][nt][2] + bv[2], acc[mt][nt][3] + bv[3]);
+      const int chunk = (nl >> 3) ^ (r & 15);
+      *reinterpret_cast<uint2*>(cs + r * RB + chunk * 8 + (nl & 7)) = pk;
+    }
+  }
+  __syncthreads();
+  constexpr int LPR = BN / 8;         // lanes per row (16 B each)
+  constexpr int RPP = NTH / LPR;      // rows per pass
+  const int tid = threadIdx.x;
+  const int c = tid % LPR;
+  const bool col_ok = n0 + c * 8 < N;
+#pragma unroll 4
+  for (int r = tid / LPR; r < BM; r += RPP) {
+    const int m = m0 + r;
+    const uint4 v = *reinterpret_cast<const uint4*>(cs + r * RB + ((c ^ (r & 15)) << 3));
+    if (m < M && col_ok) {
+      *reinterpret_cast<uint4*>(ep.out + (long)m * ep.ldo + n0 + c * 8) = v;
+      if (EPI == EPI_GELU) {
+        float f[8];
+        const uint16_t* h = reinterpret_cast<const uint16_t*>(&v);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) f[j] = gelu_tanh_f(bf2f(h[j]));
+        store8(ep.out2 + (long)m * ep.ldo + n0 + c * 8, f);
+      }
+    }
+  }
+}
+
 // ABL (diagnostics only, tools/gemm_nt_bench.py --variant 41/42/44): 1 = no in-loop staging
 // loads, 2 = no barrier / vmcnt wait, 4 = no fragment re-reads.  Outputs are wrong by design.
 template <int EPI, int WN, int ABL = 0>
@@ -240,7 +290,10 @@ __global__ __launch_bounds__(128 * WN, 1) void gemm_nt_kernel(const uint16_t* __
   step(K1{}, t, f0, f1);
   step(K0{}, t + 1, f1, f0);
 
-  epilogue<EPI, NTW>(acc, ep, M, N, m0 + wr * 128, n0 + wc * NTW * 16, l16, g);
+  if (N % 8 == 0)
+    epilogue_lds<EPI, NTW, 128 * WN>(acc, ep, smem, M, N, m0, n0, wr, wc, l16, g);
+  else
+    epilogue<EPI, NTW>(acc, ep, M, N, m0 + wr * 128, n0 + wc * NTW * 16, l16, g);
 }
 
 size_t jm_gemm_smem() { return (size_t)NST * STAGE * sizeof(uint16_t); }

@@ -37,8 +37,7 @@ def _attn_bwd(attn, da, h1, qkv, o, lse, B, S, wo_bias_done=False):
 
 
 def _ff_fwd(ff, h):
-    pre = P.linear_fwd(h, ff.w1.k, ff.w1.b)
-    g = P.gelu_fwd(pre)
+    pre, g = P.linear_gelu_fwd(h, ff.w1.k, ff.w1.b)
     y = P.linear_fwd(g, ff.w2.k, ff.w2.b)
     return pre, g, y
 

@@ -29,12 +29,11 @@ class _Linear(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, wp, bp, hw: Handle, hb: Handle | None, gelu: bool):
         x2 = x.reshape(-1, x.shape[-1])
-        h = P.linear_fwd(x2, hw, hb)
         if gelu:
-            out = P.gelu_fwd(h)
+            h, out = P.linear_gelu_fwd(x2, hw, hb)
             ctx.save_for_backward(x2, h)
         else:
-            out = h
+            out = h = P.linear_fwd(x2, hw, hb)
             ctx.save_for_backward(x2)
         ctx.hw, ctx.hb, ctx.gelu = hw, hb, gelu
         ctx.xshape = x.shape

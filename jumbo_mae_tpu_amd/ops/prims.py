@@ -73,11 +73,47 @@ def bias_grad(hb: Handle, dy: torch.Tensor) -> None:
         hb.grad.add_(dy.sum(0, dtype=torch.float32))
 
 
+_GEMM_MODE = os.environ.get("JMAE_GEMM", "auto")  # auto | blas | ours
+
+
+def use_our_gemm(M: int, N: int, K: int, fused_gelu: bool = False) -> bool:
+    """Pick the hand-written MFMA GEMM (csrc/gemm.hip) over hipBLASLt for a forward Dense.
+
+    Measured on MI355X (profiles/r1_gemm_nt_vs_hipblaslt.txt): with its LDS-staged epilogue the
+    256x256-tile kernel wins on short-K shapes whose tile count fills the last wave of 256 CUs
+    (decoder QKV 1.48x, decoder FF1+GELU 1.42x, encoder QKV 1.05x) and loses where one partial
+    wave dominates (it has no stream-K) or K is long.  A fused GELU epilogue also saves a full
+    read+write pass, which makes the FF1 shapes worth it at parity."""
+    if _GEMM_MODE == "blas":
+        return False
+    if K % 64 or N % 8 or M < 4096:
+        return False
+    if _GEMM_MODE == "ours":
+        return True
+    if K > 1024:
+        return False
+    tiles = -(-M // 256) * -(-N // 256)
+    fill = tiles / (-(-tiles // 256) * 256)
+    return fused_gelu or fill >= 0.9
+
+
 def linear_fwd(x2: torch.Tensor, hw: Handle, hb: Handle | None) -> torch.Tensor:
     w = hw.weight()
+    if hip(x2) and x2.dtype == torch.bfloat16 and use_our_gemm(x2.shape[0], w.shape[0], x2.shape[1]):
+        return _ext.load().gemm_nt(x2, w, hb.master if hb is not None else None, False)[0]
     if hb is not None:
         return torch.addmm(hb.weight(), x2, w.t())
     return x2 @ w.t()
+
+
+def linear_gelu_fwd(x2: torch.Tensor, hw: Handle, hb: Handle | None):
+    """(pre, gelu(pre)) of a Dense followed by the tanh GELU; one fused GEMM when it pays."""
+    w = hw.weight()
+    if hip(x2) and x2.dtype == torch.bfloat16 and use_our_gemm(x2.shape[0], w.shape[0], x2.shape[1], True):
+        pre, g = _ext.load().gemm_nt(x2, w, hb.master if hb is not None else None, True)
+        return pre, g
+    pre = linear_fwd(x2, hw, hb)
+    return pre, gelu_fwd(pre)
 
 
 # ------------------------------------------------------------------ weight-gradient stream
