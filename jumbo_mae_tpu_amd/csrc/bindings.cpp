@@ -44,6 +44,8 @@ struct GemmEpi {
   uint16_t* out;
   long ldo;
   uint16_t* out2;
+  const uint16_t* aux;
+  float* colpart;
 };
 int jm_gemm_nt(const uint16_t* A, long lda, const uint16_t* B, long ldb, int M, int N, int K, int epi,
                const GemmEpi& ep, hipStream_t st);
@@ -303,7 +305,7 @@ std::vector<torch::Tensor> gemm_nt(torch::Tensor A, torch::Tensor B, c10::option
   const int M = A.size(0), N = B.size(0), K = A.size(1);
   auto out = torch::empty({M, N}, A.options());
   torch::Tensor out2;
-  GemmEpi ep{nullptr, bfm(out), N, nullptr};
+  GemmEpi ep{nullptr, bfm(out), N, nullptr, nullptr, nullptr};
   if (bias) {
     TORCH_CHECK(bias->is_contiguous() && bias->scalar_type() == torch::kFloat32 && bias->numel() == N, "gemm_nt bias");
     ep.bias = bias->data_ptr<float>();
@@ -315,6 +317,32 @@ std::vector<torch::Tensor> gemm_nt(torch::Tensor A, torch::Tensor B, c10::option
   check_rc(jm_gemm_nt(bf(A), A.stride(0), bf(B), B.stride(0), M, N, K, gelu ? 1 : 0, ep, stream()), "gemm_nt");
   if (gelu) return {out, out2};
   return {out};
+}
+
+// dh[M, N] = (A[M, K] . B[N, K]^T) * gelu'(pre[M, N]) -- FF2 data gradient through the GELU,
+// B = W2^T; dbias (fp32 [N], optional) += column sums of dh (the FF1 bias gradient).
+torch::Tensor gemm_nt_dgelu(torch::Tensor A, torch::Tensor B, torch::Tensor pre, c10::optional<torch::Tensor> dbias) {
+  CHECK_DT(A, torch::kBFloat16);
+  CHECK_DT(B, torch::kBFloat16);
+  CHECK_DT(pre, torch::kBFloat16);
+  TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && A.size(1) == B.size(1), "gemm_nt_dgelu: A [M,K], B [N,K]");
+  TORCH_CHECK(A.stride(1) == 1 && B.stride(1) == 1, "gemm_nt_dgelu: K must be contiguous");
+  const int M = A.size(0), N = B.size(0), K = A.size(1);
+  TORCH_CHECK(pre.is_contiguous() && pre.size(0) == M && pre.size(1) == N, "gemm_nt_dgelu: pre [M,N]");
+  auto out = torch::empty({M, N}, A.options());
+  torch::Tensor part;
+  GemmEpi ep{nullptr, bfm(out), N, nullptr, bf(pre), nullptr};
+  const int nM = (M + 255) / 256;
+  if (dbias) {
+    TORCH_CHECK(dbias->is_contiguous() && dbias->scalar_type() == torch::kFloat32 && dbias->numel() == N,
+                "gemm_nt_dgelu dbias");
+    part = torch::empty({nM, N}, A.options().dtype(torch::kFloat32));
+    ep.colpart = part.data_ptr<float>();
+  }
+  check_rc(jm_gemm_nt(bf(A), A.stride(0), bf(B), B.stride(0), M, N, K, 2, ep, stream()), "gemm_nt_dgelu");
+  if (dbias) check_rc(jm_splitk_reduce_add(part.data_ptr<float>(), dbias->data_ptr<float>(), N, nM, stream()),
+                      "gemm_nt_dgelu dbias");
+  return out;
 }
 
 PYBIND11_MODULE(_C, m) {
@@ -336,6 +364,7 @@ PYBIND11_MODULE(_C, m) {
         py::arg("dbias") = py::none());
   m.def("attn_max_seq", &jm_attn_max_seq);
   m.def("gemm_set_variant", &jm_gemm_set_variant, py::arg("wn"), py::arg("group") = 8);
+  m.def("gemm_nt_dgelu", &gemm_nt_dgelu, py::arg("A"), py::arg("B"), py::arg("pre"), py::arg("dbias") = py::none());
   m.def("gemm_nt", &gemm_nt, py::arg("A"), py::arg("B"), py::arg("bias") = py::none(), py::arg("gelu") = false);
   m.def("attn_set_tr", &jm_attn_set_tr);
   m.def("opt_sumsq", &opt_sumsq);

@@ -46,6 +46,13 @@ JM_DEVICE float gelu_tanh_f(float x) {
   return 0.5f * x * (1.f + jm_tanh(u));
 }
 
+// d/dx of gelu_tanh_f
+JM_DEVICE float gelu_grad_f(float x) {
+  const float c = 0.7978845608028654f, a = 0.044715f;
+  const float t = jm_tanh(c * (x + a * x * x * x));
+  return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * c * (1.f + 3.f * a * x * x);
+}
+
 // DPP lane moves (VALU, no LDS round trip like __shfl_xor's ds_bpermute)
 template <int CTRL>
 JM_DEVICE float dpp_mov(float v) {

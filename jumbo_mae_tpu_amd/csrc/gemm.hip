@@ -63,13 +63,18 @@ struct Frags {
 }  // namespace
 
 struct GemmEpi {
-  const float* bias;  // [N] fp32 or null
-  uint16_t* out;      // bf16 [M, ldo]
+  const float* bias;     // [N] fp32 or null
+  uint16_t* out;         // bf16 [M, ldo]
   long ldo;
-  uint16_t* out2;     // EPI_GELU: gelu(out) bf16 [M, ldo]
+  uint16_t* out2;        // EPI_GELU: gelu(out) bf16 [M, ldo]
+  const uint16_t* aux;   // EPI_DGELU: pre-activation h bf16 [M, ldo]
+  float* colpart;        // EPI_DGELU: per-row-tile column sums of out, [ceil(M/256)][N] fp32 (or null)
 };
 
-enum { EPI_STORE = 0, EPI_GELU = 1 };
+// EPI_STORE: out = acc (+bias); EPI_GELU: out = acc (+bias), out2 = gelu(out);
+// EPI_DGELU: out = bf16(acc) * gelu'(aux) -- the data gradient through the FF GELU -- with the
+// following Dense's bias gradient (column sums of out) as per-tile partials.
+enum { EPI_STORE = 0, EPI_GELU = 1, EPI_DGELU = 2 };
 
 namespace {
 
@@ -149,12 +154,25 @@ JM_DEVICE void epilogue_lds(const f32x4_t (&acc)[8][NTW], const GemmEpi& ep, uin
   const int tid = threadIdx.x;
   const int c = tid % LPR;
   const bool col_ok = n0 + c * 8 < N;
+  float csum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll 4
   for (int r = tid / LPR; r < BM; r += RPP) {
     const int m = m0 + r;
     const uint4 v = *reinterpret_cast<const uint4*>(cs + r * RB + ((c ^ (r & 15)) << 3));
     if (m < M && col_ok) {
-      *reinterpret_cast<uint4*>(ep.out + (long)m * ep.ldo + n0 + c * 8) = v;
+      if (EPI == EPI_DGELU) {
+        float f[8], hp[8];
+        const uint16_t* dg = reinterpret_cast<const uint16_t*>(&v);
+        load8(ep.aux + (long)m * ep.ldo + n0 + c * 8, hp);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          f[j] = bf2f(f2bf(bf2f(dg[j]) * gelu_grad_f(hp[j])));
+          csum[j] += f[j];
+        }
+        store8(ep.out + (long)m * ep.ldo + n0 + c * 8, f);
+      } else {
+        *reinterpret_cast<uint4*>(ep.out + (long)m * ep.ldo + n0 + c * 8) = v;
+      }
       if (EPI == EPI_GELU) {
         float f[8];
         const uint16_t* h = reinterpret_cast<const uint16_t*>(&v);
@@ -162,6 +180,21 @@ JM_DEVICE void epilogue_lds(const f32x4_t (&acc)[8][NTW], const GemmEpi& ep, uin
         for (int j = 0; j < 8; ++j) f[j] = gelu_tanh_f(bf2f(h[j]));
         store8(ep.out2 + (long)m * ep.ldo + n0 + c * 8, f);
       }
+    }
+  }
+  if (EPI == EPI_DGELU && ep.colpart != nullptr) {
+    // column sums of this row tile: RPP threads share a column chunk -> reduce through LDS
+    float* red = reinterpret_cast<float*>(cs);
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < 8; ++j) red[tid * 8 + j] = csum[j];
+    __syncthreads();
+    for (int col = tid; col < BN; col += NTH) {
+      const int cc = col >> 3, j = col & 7;
+      float acc = 0.f;
+#pragma unroll
+      for (int q = 0; q < RPP; ++q) acc += red[(cc + q * LPR) * 8 + j];
+      if (n0 + col < N) ep.colpart[(long)(m0 / BM) * N + n0 + col] = acc;
     }
   }
 }
@@ -349,6 +382,8 @@ int jm_gemm_nt(const uint16_t* A, long lda, const uint16_t* B, long ldb, int M, 
     launch_epi<EPI_STORE>(A, lda, B, ldb, M, N, K, ep, nwg, st);
   else if (epi == EPI_GELU)
     launch_epi<EPI_GELU>(A, lda, B, ldb, M, N, K, ep, nwg, st);
+  else if (epi == EPI_DGELU && N % 8 == 0)
+    launch_epi<EPI_DGELU>(A, lda, B, ldb, M, N, K, ep, nwg, st);
   else
     return -3;
   return 0;

@@ -74,6 +74,8 @@ class Handle:
             assert b.offset == a.offset + a.numel, "fused handle segments must be contiguous"
         assert self.numel == sum(s.numel for s in segs)
         self._param: torch.nn.Parameter | None = None
+        self._wt: torch.Tensor | None = None
+        self._wt_version = -1
 
     def _view(self, flat: torch.Tensor) -> torch.Tensor:
         return flat[self.start:self.start + self.numel].view(self.shape)
@@ -101,6 +103,18 @@ class Handle:
     def weight(self) -> torch.Tensor:
         """Tensor the compute kernels read (bf16 shadow on GPU, master on fp32 runs)."""
         return self.shadow
+
+    def weight_t(self) -> torch.Tensor:
+        """Transposed copy of ``weight()`` ([in, out] for a Dense kernel stored out x in), the
+        K-contiguous B operand of a data-gradient GEMM on the NT MFMA kernel.  Refreshed lazily
+        once per shadow update (``ParamStore.version``)."""
+        if self._wt is None or self._wt_version != self.store.version:
+            w = self.weight()
+            if self._wt is None:
+                self._wt = torch.empty((w.shape[1], w.shape[0]), dtype=w.dtype, device=w.device)
+            self._wt.copy_(w.t())
+            self._wt_version = self.store.version
+        return self._wt
 
     def accumulate_grad(self, g: torch.Tensor) -> None:
         if not self.segs[0].trainable:
@@ -131,6 +145,7 @@ class ParamStore:
         self.hooks: list[Callable[[Handle], None]] = []
         self.use_hooks: list[Callable[[Handle], None]] = []
         self._handles: list[Handle] = []
+        self.version = 0  # bumped whenever the shadow changes (optimizer step, sync, load)
 
     # ---------------------------------------------------------------- building
     def add(self, path: Iterable[str], shape: tuple[int, ...], init, flax_shape=None,
@@ -179,6 +194,7 @@ class ParamStore:
         self.sync_shadow()
 
     def sync_shadow(self) -> None:
+        self.version += 1
         if self.shadow is not self.master:
             with torch.no_grad():
                 self.shadow.copy_(self.master)

@@ -43,8 +43,8 @@ def _ff_fwd(ff, h):
 
 
 def _ff_bwd(ff, dy, h, pre, g, w2_bias_done=False):
-    dg = P.linear_bwd(dy, g, ff.w2.k, ff.w2.b, bias_done=w2_bias_done)
-    dpre, bias_done = P.gelu_bwd(pre, dg, ff.w1.b if ff.w1.k.segs[0].trainable else None)
+    hb1 = ff.w1.b if ff.w1.k.segs[0].trainable else None
+    dpre, bias_done = P.linear_gelu_bwd(dy, g, pre, ff.w2.k, ff.w2.b, hb1, w2_bias_done)
     return P.linear_bwd(dpre, h, ff.w1.k, ff.w1.b, bias_done=bias_done)
 
 

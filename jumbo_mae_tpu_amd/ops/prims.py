@@ -74,6 +74,7 @@ def bias_grad(hb: Handle, dy: torch.Tensor) -> None:
 
 
 _GEMM_MODE = os.environ.get("JMAE_GEMM", "auto")  # auto | blas | ours
+_DGRAD_OURS = os.environ.get("JMAE_DGRAD", "1") == "1"  # data-gradient GEMMs on the MFMA kernel
 
 
 def use_our_gemm(M: int, N: int, K: int, fused_gelu: bool = False) -> bool:
@@ -123,7 +124,9 @@ def linear_gelu_fwd(x2: torch.Tensor, hw: Handle, hb: Handle | None):
 # data-gradient chain, which then execute underneath them instead of after them.  The chain's
 # tensors are pinned for the side stream with record_stream; the DP reducer launches its
 # all-reduces from this stream and the trainer joins it before the optimizer.
-_side = {"stream": None, "enabled": os.environ.get("JMAE_WGRAD_STREAM", "1") == "1", "cb": False}
+# Off by default: measured on MI355X it gains 1-2 % on most runs but some runs collapse to
+# 0.4-0.6x (the two queues' kernels interfere), which is not acceptable for a benchmark path.
+_side = {"stream": None, "enabled": os.environ.get("JMAE_WGRAD_STREAM", "0") == "1", "cb": False}
 
 
 def _end_of_backward() -> None:
@@ -151,10 +154,18 @@ def join_wgrad_stream() -> None:
         torch.cuda.current_stream().wait_stream(s)
 
 
+def linear_dgrad(dy: torch.Tensor, hw: Handle) -> torch.Tensor:
+    """dx = dy @ W: on the MFMA kernel against the transposed weight copy when it wins."""
+    w = hw.weight()
+    if _DGRAD_OURS and hip(dy) and dy.dtype == torch.bfloat16 and use_our_gemm(dy.shape[0], w.shape[1], w.shape[0]):
+        return _ext.load().gemm_nt(dy.contiguous(), hw.weight_t(), None, False)[0]
+    return dy @ w
+
+
 def linear_bwd(dy: torch.Tensor, x2: torch.Tensor, hw: Handle, hb: Handle | None, need_dx: bool = True,
                bias_done: bool = False):
     """dx = dy @ W (if needed); grad W += dy^T x; grad b += colsum(dy) (unless fused upstream)."""
-    dx = dy @ hw.weight() if need_dx else None
+    dx = linear_dgrad(dy, hw) if need_dx else None
     if _trainable(hw):
         side = wgrad_stream() if dy.is_cuda else None
         if side is not None:
@@ -176,6 +187,25 @@ def linear_bwd(dy: torch.Tensor, x2: torch.Tensor, hw: Handle, hb: Handle | None
         if hb is not None:
             hb.ready()
     return dx
+
+
+def linear_gelu_bwd(dy: torch.Tensor, g: torch.Tensor, pre: torch.Tensor, hw2: Handle, hb2: Handle | None,
+                    hb1: Handle | None, bias2_done: bool = False):
+    """Backward of ``y = Dense2(gelu(pre))`` down to d pre: returns (dpre, bias1_done).
+
+    Fused path: one MFMA GEMM dy . W2 whose epilogue multiplies by gelu'(pre) and emits the
+    column sums of dpre (= the gradient of Dense1's bias ``hb1``), so the GEMM output dg never
+    makes an HBM round trip.  W2's own gradients (wgrad, bias) are queued as usual."""
+    w2 = hw2.weight()
+    M, N, K = dy.shape[0], w2.shape[1], w2.shape[0]
+    if (_DGRAD_OURS and hip(dy) and dy.dtype == torch.bfloat16 and N % 8 == 0
+            and use_our_gemm(M, N, K, fused_gelu=True)):
+        bg = hb1.grad if _trainable(hb1) else None
+        dpre = _ext.load().gemm_nt_dgelu(dy.contiguous(), hw2.weight_t(), pre.contiguous(), bg)
+        linear_bwd(dy, g, hw2, hb2, need_dx=False, bias_done=bias2_done)
+        return dpre, bg is not None
+    dg = linear_bwd(dy, g, hw2, hb2, bias_done=bias2_done)
+    return gelu_bwd(pre, dg, hb1)
 
 
 # ------------------------------------------------------------------------------ gelu

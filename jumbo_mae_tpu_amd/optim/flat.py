@@ -116,6 +116,7 @@ class FlatOptimizer:
         else:
             self._step_torch(lr, bc1, bc2)
         self.count += 1
+        self.store.version += 1  # shadow rewritten: transposed weight copies are stale
         self.last_lr = lr
         return lr
 

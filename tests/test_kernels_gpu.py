@@ -219,3 +219,21 @@ def test_attention_long_sequence_path():
     o2, _ = _attn_ref(qr, H)
     o2.backward(do.double())
     assert rel(dqkv, qr.grad) < 2e-2
+
+
+@pytest.mark.parametrize("M,N,K", [(512, 256, 64), (1000, 1536, 512), (300, 512, 128)])
+def test_gemm_nt_dgelu(ext, M, N, K):
+    """FF2 data gradient through the GELU with the FF1 bias gradient (csrc/gemm.hip EPI_DGELU)."""
+    torch.manual_seed(0)
+    dy = (torch.rand(M, K, device="cuda") * 2 - 1).bfloat16()
+    w2t = ((torch.rand(N, K, device="cuda") * 2 - 1) * 0.1).bfloat16()
+    pre = (torch.randn(M, N, device="cuda") * 2).bfloat16()
+    db = torch.full((N,), 0.25, device="cuda")
+    out = ext.gemm_nt_dgelu(dy, w2t, pre, db)
+    dg = (dy.float() @ w2t.float().t()).bfloat16().float()
+    x = pre.float()
+    t = torch.tanh(0.7978845608028654 * (x + 0.044715 * x ** 3))
+    d = 0.5 * (1 + t) + 0.5 * x * (1 - t * t) * 0.7978845608028654 * (1 + 3 * 0.044715 * x * x)
+    ref = dg * d
+    assert rel(out, ref) < 1e-2
+    assert rel(db - 0.25, ref.sum(0)) < 1e-2

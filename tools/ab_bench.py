@@ -1,0 +1,77 @@
+"""Interleaved A/B of runtime switches on the flagship step (one process, one device).
+
+    python tools/ab_bench.py --configs "blas:JMAE_GEMM=blas" "auto:" --rounds 4 --steps 6
+
+Each config is a list of ``KEY=VALUE`` switches applied to ``ops.prims`` module state between
+rounds (same model, same data, same device -> no cross-process / cross-device variance).
+Supported keys: JMAE_GEMM (auto|blas|ours), JMAE_DGRAD (0|1), JMAE_WGRAD_STREAM (0|1).
+Prints per-config median / min ms per step."""
+
+import argparse
+import os
+import statistics
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def apply(P, cfg: str):
+    for kv in filter(None, cfg.split(",")):
+        k, v = kv.split("=")
+        if k == "JMAE_GEMM":
+            P._GEMM_MODE = v
+        elif k == "JMAE_DGRAD":
+            P._DGRAD_OURS = v == "1"
+        elif k == "JMAE_WGRAD_STREAM":
+            P.set_wgrad_stream(v == "1")
+        else:
+            raise ValueError(k)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--configs", nargs="+", required=True, help="name:KEY=V,KEY=V")
+    ap.add_argument("--rounds", type=int, default=4)
+    ap.add_argument("--steps", type=int, default=6)
+    ap.add_argument("--model", default="vit_large_patch16")
+    a = ap.parse_args()
+    from jumbo_mae_tpu_amd.config import decoder_config, vit_config
+    from jumbo_mae_tpu_amd.models.mae import PretrainModel
+    from jumbo_mae_tpu_amd.ops import prims as P
+    from jumbo_mae_tpu_amd.optim.flat import FlatOptimizer
+    from jumbo_mae_tpu_amd.train.engine import Trainer
+    from jumbo_mae_tpu_amd.utils.rng import RngStreams
+    dev = torch.device("cuda")
+    vc = vit_config(a.model, labels=0, posemb="sincos2d", image_mask_ratio=0.75, droppath=0.0, dropout=0.0)
+    dc = decoder_config(dec_droppath=0.0)
+    model = PretrainModel(vc, dc).to(dev, torch.bfloat16, seed=0)
+    opt = FlatOptimizer(model.store, "adamw", lambda c: 1e-4, b1=0.9, b2=0.95, weight_decay=0.05,
+                        num_layers=vc.layers)
+    tr = Trainer(model, opt, None, RngStreams({"noise": 0, "dropout": 0, "mixup": 0}, 0, dev))
+    gen = torch.Generator(device=dev).manual_seed(0)
+    pool = [torch.randint(0, 256, (512, 3, 224, 224), dtype=torch.uint8, device=dev, generator=gen)
+            for _ in range(2)]
+    cfgs = [c.split(":", 1) for c in a.configs]
+    times = {n: [] for n, _ in cfgs}
+    it = 0
+    for r in range(a.rounds + 1):  # round 0 = warmup of every config
+        for name, cfg in cfgs:
+            apply(P, cfg)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(a.steps):
+                tr.train_step([(pool[it % 2],)])
+                it += 1
+            torch.cuda.synchronize()
+            if r > 0:
+                times[name].append((time.perf_counter() - t0) * 1e3 / a.steps)
+    for name, ts in times.items():
+        print(f"{name:24s} median {statistics.median(ts):8.2f} ms  min {min(ts):8.2f} ms  "
+              f"({512 * 1e3 / statistics.median(ts):7.1f} img/s)  rounds {['%.1f' % t for t in ts]}", flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -50,14 +50,22 @@ def main():
             M, N, K = FWD[name]
             if kind == "fwd_gelu" and name not in ("enc_ff1", "dec_ff1", "jumbo1"):
                 continue
-            if kind == "dgrad":  # dX[M,K] = dy[M,N] @ W[N,K]  ->  NT with B = W^T [K, N]
+            if kind == "dgrad_gelu" and name not in ("enc_ff2", "dec_ff2"):
+                continue
+            if kind in ("dgrad", "dgrad_gelu"):  # dX[M,K] = dy[M,N] @ W[N,K]  ->  NT with B = W^T [K, N]
                 M, N, K = M, K, N
             x = (torch.rand(M, K, device="cuda") * 2 - 1).bfloat16()
             w = ((torch.rand(N, K, device="cuda") * 2 - 1) * 0.05).bfloat16()
             b = torch.randn(N, device="cuda") * 0.1
             bb = b.bfloat16()
             gelu = kind == "fwd_gelu"
-            if kind == "dgrad":
+            if kind == "dgrad_gelu":
+                wm = w.t().contiguous()
+                pre = (torch.randn(M, N, device="cuda") * 2).bfloat16()
+                dbg = torch.zeros(N, device="cuda")
+                ours = lambda: (ext.gemm_nt_dgelu(x, w, pre, dbg),)  # noqa: E731
+                blas = lambda: ext.gelu_bwd(pre, x @ wm, dbg)  # noqa: E731
+            elif kind == "dgrad":
                 wm = w.t().contiguous()  # W as the model stores it: [N_fwd, K_fwd] = w^T
                 ours = lambda: ext.gemm_nt(x, w, None, False)  # noqa: E731
                 blas = lambda: x @ wm  # noqa: E731
@@ -68,7 +76,7 @@ def main():
                 ours = lambda: ext.gemm_nt(x, w, b, False)  # noqa: E731
                 blas = lambda: torch.addmm(bb, x, w.t())  # noqa: E731
             out = ours()
-            ref = torch.addmm(b, x.float(), w.float().t())
+            ref = torch.addmm(b, x.float(), w.float().t()) if kind != "dgrad_gelu" else out[0].float()
             err = ((out[0].float() - ref).abs().max() / ref.abs().max()).item()
             if gelu:
                 g_ref = torch.nn.functional.gelu(out[0].float(), approximate="tanh")
