@@ -18,6 +18,7 @@ int jm_gelu_fwd(const uint16_t* h, uint16_t* a, long n, hipStream_t st);
 int jm_gelu_bwd(const uint16_t* h, const uint16_t* da, uint16_t* dh, float* bias_grad, int M, int N, hipStream_t st);
 int jm_colsum_bf16(const uint16_t* x, float* acc, int M, int N, hipStream_t st);
 int jm_splitk_reduce_add(const float* part, float* g, long n, int S, hipStream_t st);
+int jm_transpose_bf16(const uint16_t* src, uint16_t* dst, int R, int C, hipStream_t st);
 int jm_residual_fwd(const float* x, long sB, long sT, int B, int T, int D, const uint16_t* y, const float* scale,
                     const float* mask, float* out, long oB, long oT, hipStream_t st);
 int jm_residual_bwd(const float* dout, long dB, long dT, const uint16_t* y, const float* scale, const float* mask,
@@ -345,6 +346,17 @@ torch::Tensor gemm_nt_dgelu(torch::Tensor A, torch::Tensor B, torch::Tensor pre,
   return out;
 }
 
+// dst [C, R] = src [R, C]^T (bf16, both contiguous)
+void transpose_bf16(torch::Tensor src, torch::Tensor dst) {
+  CHECK_CONTIG(src);
+  CHECK_CONTIG(dst);
+  CHECK_DT(src, torch::kBFloat16);
+  CHECK_DT(dst, torch::kBFloat16);
+  TORCH_CHECK(src.dim() == 2 && dst.dim() == 2 && dst.size(0) == src.size(1) && dst.size(1) == src.size(0),
+              "transpose_bf16 shapes");
+  check_rc(jm_transpose_bf16(bf(src), bfm(dst), src.size(0), src.size(1), stream()), "transpose_bf16");
+}
+
 PYBIND11_MODULE(_C, m) {
   m.doc() = "jumbo_mae_tpu_amd CDNA4 (gfx950) HIP kernels";
   m.def("layernorm_fwd", &layernorm_fwd);
@@ -355,6 +367,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("gelu_bwd", &gelu_bwd, py::arg("h"), py::arg("da"), py::arg("bias_grad") = py::none());
   m.def("colsum", &colsum);
   m.def("splitk_reduce_add", &splitk_reduce_add);
+  m.def("transpose_bf16", &transpose_bf16);
   m.def("residual_fwd", &residual_fwd, py::arg("x"), py::arg("y"), py::arg("scale"), py::arg("mask"),
         py::arg("out") = py::none());
   m.def("residual_bwd", &residual_bwd, py::arg("dout"), py::arg("y"), py::arg("scale"), py::arg("mask"),

@@ -304,3 +304,49 @@ int jm_splitk_reduce_add(const float* part, float* g, long n, int S, hipStream_t
   splitk_reduce_add_kernel<<<dim3((unsigned)blocks, ys), 256, 0, st>>>(part, g, n / 4, S);
   return 0;
 }
+
+// ------------------------------------------------------------------ bf16 transpose
+// dst[C][R] = src[R][C]^T through a 64 x 64 LDS tile: 16-byte coalesced reads and writes on both
+// sides (the transposed weight copies read by the data-gradient MFMA GEMM).  The LDS tile rows
+// are padded by one 4-byte word so the column reads of 2-byte elements do not pile onto a bank.
+namespace {
+constexpr int TT = 64;
+__global__ __launch_bounds__(256) void transpose_bf16_kernel(const uint16_t* __restrict__ src, uint16_t* __restrict__ dst,
+                                                             int R, int C) {
+  __shared__ uint16_t tile[TT][TT + 2];
+  const int r0 = blockIdx.y * TT, c0 = blockIdx.x * TT;
+  const int t = threadIdx.x;
+  // read: 64 rows x 64 cols = 512 chunks of 8 -> 2 per thread
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int i = t + k * 256;
+    const int r = i >> 3, c = (i & 7) * 8;
+    if (r0 + r < R && c0 + c < C) {
+      const uint4 v = *reinterpret_cast<const uint4*>(src + (long)(r0 + r) * C + c0 + c);
+      const uint16_t* h = reinterpret_cast<const uint16_t*>(&v);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) tile[r][c + j] = h[j];
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int i = t + k * 256;
+    const int c = i >> 3, r = (i & 7) * 8;  // output row c (source column), 8 source rows
+    if (c0 + c < C && r0 + r < R) {
+      uint4 v;
+      uint16_t* h = reinterpret_cast<uint16_t*>(&v);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) h[j] = tile[r + j][c];
+      *reinterpret_cast<uint4*>(dst + (long)(c0 + c) * R + r0 + r) = v;
+    }
+  }
+}
+}  // namespace
+
+int jm_transpose_bf16(const uint16_t* src, uint16_t* dst, int R, int C, hipStream_t st) {
+  if (R % 8 || C % 8) return -1;
+  dim3 grid((C + TT - 1) / TT, (R + TT - 1) / TT);
+  transpose_bf16_kernel<<<grid, 256, 0, st>>>(src, dst, R, C);
+  return 0;
+}

@@ -112,7 +112,11 @@ class Handle:
             w = self.weight()
             if self._wt is None:
                 self._wt = torch.empty((w.shape[1], w.shape[0]), dtype=w.dtype, device=w.device)
-            self._wt.copy_(w.t())
+            from ..ops import _ext  # noqa: PLC0415 (models must import without the extension)
+            if _ext.use_hip(w) and w.dtype == torch.bfloat16 and w.shape[0] % 8 == 0 and w.shape[1] % 8 == 0:
+                _ext.load().transpose_bf16(w, self._wt)
+            else:
+                self._wt.copy_(w.t())
             self._wt_version = self.store.version
         return self._wt
 

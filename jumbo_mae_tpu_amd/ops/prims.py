@@ -77,7 +77,14 @@ _GEMM_MODE = os.environ.get("JMAE_GEMM", "auto")  # auto | blas | ours
 _DGRAD_OURS = os.environ.get("JMAE_DGRAD", "1") == "1"  # data-gradient GEMMs on the MFMA kernel
 
 
-def use_our_gemm(M: int, N: int, K: int, fused_gelu: bool = False) -> bool:
+# flagship shapes the rule below would reject but where the MFMA kernel measured faster
+# (tools/gemm_nt_bench.py, profiles/r1_gemm_nt_vs_hipblaslt_v2.txt): ViT-L encoder QKV / Wo and
+# MAE-decoder Wo data gradients (1.05x, 1.08x, 1.11x), decoder Wo forward (1.02x)
+_OURS_MEASURED = {"dgrad": {(26624, 1024, 3072), (26624, 1024, 1024), (101888, 512, 512)},
+                  "fwd": {(101888, 512, 512)}}
+
+
+def use_our_gemm(M: int, N: int, K: int, fused_gelu: bool = False, kind: str = "fwd") -> bool:
     """Pick the hand-written MFMA GEMM (csrc/gemm.hip) over hipBLASLt for a forward Dense.
 
     Measured on MI355X (profiles/r1_gemm_nt_vs_hipblaslt.txt): with its LDS-staged epilogue the
@@ -90,6 +97,8 @@ def use_our_gemm(M: int, N: int, K: int, fused_gelu: bool = False) -> bool:
     if K % 64 or N % 8 or M < 4096:
         return False
     if _GEMM_MODE == "ours":
+        return True
+    if (M, N, K) in _OURS_MEASURED.get(kind, ()):
         return True
     if K > 1024:
         return False
@@ -157,7 +166,8 @@ def join_wgrad_stream() -> None:
 def linear_dgrad(dy: torch.Tensor, hw: Handle) -> torch.Tensor:
     """dx = dy @ W: on the MFMA kernel against the transposed weight copy when it wins."""
     w = hw.weight()
-    if _DGRAD_OURS and hip(dy) and dy.dtype == torch.bfloat16 and use_our_gemm(dy.shape[0], w.shape[1], w.shape[0]):
+    if (_DGRAD_OURS and hip(dy) and dy.dtype == torch.bfloat16
+            and use_our_gemm(dy.shape[0], w.shape[1], w.shape[0], kind="dgrad")):
         return _ext.load().gemm_nt(dy.contiguous(), hw.weight_t(), None, False)[0]
     return dy @ w
 
@@ -199,7 +209,7 @@ def linear_gelu_bwd(dy: torch.Tensor, g: torch.Tensor, pre: torch.Tensor, hw2: H
     w2 = hw2.weight()
     M, N, K = dy.shape[0], w2.shape[1], w2.shape[0]
     if (_DGRAD_OURS and hip(dy) and dy.dtype == torch.bfloat16 and N % 8 == 0
-            and use_our_gemm(M, N, K, fused_gelu=True)):
+            and use_our_gemm(M, N, K, fused_gelu=True, kind="dgrad")):
         bg = hb1.grad if _trainable(hb1) else None
         dpre = _ext.load().gemm_nt_dgelu(dy.contiguous(), hw2.weight_t(), pre.contiguous(), bg)
         linear_bwd(dy, g, hw2, hb2, need_dx=False, bias_done=bias2_done)

@@ -237,3 +237,11 @@ def test_gemm_nt_dgelu(ext, M, N, K):
     ref = dg * d
     assert rel(out, ref) < 1e-2
     assert rel(db - 0.25, ref.sum(0)) < 1e-2
+
+
+@pytest.mark.parametrize("R,C", [(1024, 3072), (512, 2048), (72, 136)])
+def test_transpose_bf16(ext, R, C):
+    x = torch.randn(R, C, device="cuda").bfloat16()
+    y = torch.empty(C, R, device="cuda", dtype=torch.bfloat16)
+    ext.transpose_bf16(x, y)
+    assert torch.equal(y, x.t())
