@@ -51,6 +51,9 @@ struct GemmEpi {
 int jm_gemm_nt(const uint16_t* A, long lda, const uint16_t* B, long ldb, int M, int N, int K, int epi,
                const GemmEpi& ep, hipStream_t st);
 void jm_gemm_set_variant(int wn, int group);
+int jm_gemm_tn_plan(int M, int N, int K, int* S_out);
+int jm_gemm_tn(const uint16_t* A, long lda, const uint16_t* B, long ldb, int M, int N, int K, int sps, int S,
+               float* G, long ldo, float* partial, hipStream_t st);
 int jm_patchify_normalize(const uint8_t* img, float* out, int B, int H, int W, int p, hipStream_t st);
 
 namespace {
@@ -357,6 +360,27 @@ void transpose_bf16(torch::Tensor src, torch::Tensor dst) {
   check_rc(jm_transpose_bf16(bf(src), bfm(dst), src.size(0), src.size(1), stream()), "transpose_bf16");
 }
 
+// weight gradient G[N, K] += dy[M, N]^T . x[M, K] on the TN MFMA kernel (split over M, fp32
+// partial tiles reduced into G); returns the number of M splits used
+int64_t gemm_tn_wgrad(torch::Tensor dy, torch::Tensor x, torch::Tensor g) {
+  CHECK_DT(dy, torch::kBFloat16);
+  CHECK_DT(x, torch::kBFloat16);
+  TORCH_CHECK(dy.dim() == 2 && x.dim() == 2 && dy.size(0) == x.size(0), "gemm_tn_wgrad: dy [M,N], x [M,K]");
+  TORCH_CHECK(dy.stride(1) == 1 && x.stride(1) == 1, "gemm_tn_wgrad: rows must be contiguous");
+  const int M = dy.size(0), N = dy.size(1), K = x.size(1);
+  TORCH_CHECK(g.is_contiguous() && g.scalar_type() == torch::kFloat32 && g.numel() == (long)N * K, "gemm_tn_wgrad g");
+  int S = 1;
+  const int sps = jm_gemm_tn_plan(M, N, K, &S);
+  torch::Tensor part;
+  if (S > 1) part = torch::empty({S, (long)N * K}, g.options());
+  check_rc(jm_gemm_tn(bf(dy), dy.stride(0), bf(x), x.stride(0), M, N, K, sps, S, g.data_ptr<float>(), K,
+                      S > 1 ? part.data_ptr<float>() : nullptr, stream()),
+           "gemm_tn_wgrad");
+  if (S > 1) check_rc(jm_splitk_reduce_add(part.data_ptr<float>(), g.data_ptr<float>(), (long)N * K, S, stream()),
+                      "gemm_tn_wgrad reduce");
+  return S;
+}
+
 PYBIND11_MODULE(_C, m) {
   m.doc() = "jumbo_mae_tpu_amd CDNA4 (gfx950) HIP kernels";
   m.def("layernorm_fwd", &layernorm_fwd);
@@ -376,6 +400,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("attn_bwd", &attn_bwd, py::arg("dO"), py::arg("qkv"), py::arg("o"), py::arg("lse"), py::arg("heads"),
         py::arg("dbias") = py::none());
   m.def("attn_max_seq", &jm_attn_max_seq);
+  m.def("gemm_tn_wgrad", &gemm_tn_wgrad);
   m.def("gemm_set_variant", &jm_gemm_set_variant, py::arg("wn"), py::arg("group") = 8);
   m.def("gemm_nt_dgelu", &gemm_nt_dgelu, py::arg("A"), py::arg("B"), py::arg("pre"), py::arg("dbias") = py::none());
   m.def("gemm_nt", &gemm_nt, py::arg("A"), py::arg("B"), py::arg("bias") = py::none(), py::arg("gelu") = false);

@@ -1,0 +1,277 @@
+// Weight-gradient MFMA GEMM for gfx950:  G[N][K] += sum_m A[m][n] * B[m][k]
+// (A = dY [M, N], B = X [M, K], both bf16 row-major; G fp32 = the flat gradient of a Dense
+// kernel stored out x in).  Both operands are M-major ("TN"): the reduction runs down the rows.
+//
+// The outputs are small (0.25-38 M elements) and the reduction long (25k-100k rows), so the M
+// range is split over S workgroups per 256 x 256 output tile, S chosen on the host so that
+// tiles x S fills whole waves of the 256 CUs; the S fp32 partial tiles are summed (+= into G)
+// by jm_splitk_reduce_add.  With S = 1 the epilogue accumulates into G directly.
+//
+// Per workgroup: 8 waves (2 x 4), each a 128 (n) x 64 (k) sub-tile = 8 x 4 MFMA 16x16x32 tiles.
+// 32 rows of M per step are staged with buffer_load ... lds into a 4-stage ring of [32][256] bf16
+// images (512 B rows) for each operand; the MFMA operands need 8 consecutive M per lane, i.e.
+// COLUMNS of those images, which ds_read_b64_tr_b16 delivers (two reads of 4 rows each).  The
+// images' 16-byte chunks are XOR-swizzled by tswz(row) so the 32 lanes of a transposing read
+// (8 rows x 32 B) cover all 64 banks.  Same mid-step barrier pipeline as gemm.hip.
+#include <type_traits>
+
+#include "common.h"
+
+namespace {
+
+constexpr int TN_ = 256, TK_ = 256, BS = 32, NST = 4, NTH = 512;
+constexpr int STAGE = (TN_ + TK_) * BS;  // elements per ring stage
+
+typedef __attribute__((address_space(3))) void lds_void_t;
+
+JM_DEVICE __amdgpu_buffer_rsrc_t make_rsrc(const uint16_t* base, long bytes) {
+  const int n = bytes >= 0xffffffffL ? -1 : (int)bytes;
+  return __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, n, 0x00020000);
+}
+
+JM_DEVICE void blds16(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff, uint16_t* l) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void_t*)(l), 16, voff, soff, 0, 0);
+}
+
+JM_DEVICE f32x4_t mfma16(bf16x8_t a, bf16x8_t b, f32x4_t c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+// ds_read_b64_tr_b16 as inline asm: through the builtin, hipcc cannot tell these LDS reads from
+// the in-flight LDS-DMA writes and drains vmcnt(0) before each one (the whole prefetch ring).
+// The lgkmcnt waits for the results are therefore explicit (wait_lds) and fenced with
+// sched_barrier so no MFMA is hoisted above them.
+JM_DEVICE s16x4_t tr4(const uint16_t* p) {
+  s16x4_t r;
+  const uint32_t a = (uint32_t)(size_t)((const __attribute__((address_space(3))) uint16_t*)p);
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(r) : "v"(a));
+  return r;
+}
+
+JM_DEVICE void wait_lds() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+JM_DEVICE bf16x8_t cat44(s16x4_t lo, s16x4_t hi) {
+  s16x8_t s;
+  s[0] = lo[0]; s[1] = lo[1]; s[2] = lo[2]; s[3] = lo[3];
+  s[4] = hi[0]; s[5] = hi[1]; s[6] = hi[2]; s[7] = hi[3];
+  return __builtin_bit_cast(bf16x8_t, s);
+}
+
+// chunk XOR (in 16-byte units, even so 32-byte pairs stay together): rows {0-3, 8-11} and
+// {4-7, 12-15} -- the two row sets of one transposing read -- land on 8 distinct 32-byte slots
+JM_DEVICE int tswz(int row) { return ((row & 3) | (((row >> 3) & 1) << 2)) << 1; }
+
+// element offset of (row, col) in a [32][256] stage image
+JM_DEVICE int toff(int row, int col) { return row * 256 + ((((col >> 3) ^ tswz(row)) & 31) << 3) + (col & 7); }
+
+struct TFrags {
+  bf16x8_t b[4], a[8];
+};
+
+template <int ACC>  // ACC = 1: G += tile (S == 1), 0: store the fp32 partial tile
+__global__ __launch_bounds__(NTH, 1) void gemm_tn_kernel(const uint16_t* __restrict__ A, long lda,
+                                                         const uint16_t* __restrict__ B, long ldb, int M, int N,
+                                                         int K, int steps_per_split, float* __restrict__ out,
+                                                         long ldo, long split_stride) {
+  extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
+  const int tid = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+  const int l16 = lane & 15, g = lane >> 4;
+  const int wr = wave >> 2, wc = wave & 3;
+
+  // ---- block -> (split, tile): split-major so concurrently running blocks share M rows
+  const int nK = K / TK_;
+  const int tiles = (N / TN_) * nK;
+  const int nwg = gridDim.x;
+  const int orig = blockIdx.x;
+  const int xcd = orig & 7, q = nwg >> 3, r = nwg & 7;
+  const int wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+  const int split = wg / tiles, tile = wg - split * tiles;
+  const int n0 = (tile / nK) * TN_, k0 = (tile % nK) * TK_;
+  const int m_begin = split * steps_per_split * BS;
+  const int rows = min(M - m_begin, steps_per_split * BS);  // > 0 (host guarantees)
+  int nk = (rows + BS - 1) / BS;
+  nk += nk & 1;  // even: the pipeline runs in pairs; rows past the split read zeros
+  if (nk < 2) nk = 2;
+
+  const __amdgpu_buffer_rsrc_t ra = make_rsrc(A + (long)m_begin * lda + n0, (long)rows * lda * 2);
+  const __amdgpu_buffer_rsrc_t rb = make_rsrc(B + (long)m_begin * ldb + k0, (long)rows * ldb * 2);
+  // staging: each wave-instruction moves 2 rows x 512 B; 16 per operand and stage -> 2 rounds
+  uint32_t a_src[2], b_src[2];
+#pragma unroll
+  for (int rr = 0; rr < 2; ++rr) {
+    const int row = rr * 16 + wave * 2 + (lane >> 5);
+    const int c = (lane & 31) ^ tswz(row);
+    a_src[rr] = (uint32_t)((row * lda + c * 8) * 2);
+    b_src[rr] = (uint32_t)((row * ldb + c * 8) * 2);
+  }
+  auto issue = [&](int t) {
+    uint16_t* la = smem + (t % NST) * STAGE;
+    uint16_t* lb = la + BS * TN_;
+    const uint32_t sa = (uint32_t)(t * BS * lda * 2), sb = (uint32_t)(t * BS * ldb * 2);
+#pragma unroll
+    for (int rr = 0; rr < 2; ++rr) {
+      blds16(ra, a_src[rr], sa, la + (rr * 16 + wave * 2) * TN_);
+      blds16(rb, b_src[rr], sb, lb + (rr * 16 + wave * 2) * TK_);
+    }
+  };
+  // transposing fragment reads: rows 8g + l16/4 (+4), columns base + 4 (l16 & 3)
+  const int r1 = 8 * g + (l16 >> 2);
+  const int cl = 4 * (l16 & 3);
+  // fragment i of a step: i < 4 -> b[i] (X columns), else a[i - 4] (dY columns)
+  auto read_one = [&](int t, TFrags& f, int i) {
+    const uint16_t* la = smem + (t % NST) * STAGE;
+    const uint16_t* lb = la + BS * TN_;
+    if (i < 4) {
+      const int col = wc * 64 + i * 16 + cl;
+      f.b[i] = cat44(tr4(lb + toff(r1, col)), tr4(lb + toff(r1 + 4, col)));
+    } else {
+      const int col = wr * 128 + (i - 4) * 16 + cl;
+      f.a[i - 4] = cat44(tr4(la + toff(r1, col)), tr4(la + toff(r1 + 4, col)));
+    }
+  };
+
+  f32x4_t acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  auto wait_bar = [&](auto outstanding_stages) {  // 4 loads per stage per thread
+    constexpr int W = decltype(outstanding_stages)::value * 4;
+    if constexpr (W == 8) asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    if constexpr (W == 4) asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    if constexpr (W == 0) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  };
+  auto step = [&](auto kind, int t, TFrags& cur, TFrags& nxt) {
+    constexpr int KIND = decltype(kind)::value;
+    wait_lds();  // cur's transposing reads (issued during the previous step) have landed
+    if constexpr (KIND == 3) issue(t + 3);
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) acc[mt][nt] = mfma16(cur.b[nt], cur.a[mt], acc[mt][nt]);
+    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (KIND > 0) wait_bar(std::integral_constant<int, KIND - 1>{});
+    __builtin_amdgcn_sched_barrier(0);
+    // second half: one fragment of the next step (2 transposing reads) per MFMA
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      if constexpr (KIND > 0) {
+        if (i < 12) read_one(t + 1, nxt, i);
+      }
+      const int mt = 4 + i / 4, nt = i % 4;
+      acc[mt][nt] = mfma16(cur.b[nt], cur.a[mt], acc[mt][nt]);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+  using K3 = std::integral_constant<int, 3>;
+  using K2 = std::integral_constant<int, 2>;
+  using K1 = std::integral_constant<int, 1>;
+  using K0 = std::integral_constant<int, 0>;
+
+  issue(0);
+  issue(1);
+  if (nk > 2) {
+    issue(2);
+    wait_bar(std::integral_constant<int, 2>{});
+  } else {
+    wait_bar(std::integral_constant<int, 1>{});
+  }
+  __builtin_amdgcn_sched_barrier(0);
+  TFrags f0, f1;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) read_one(0, f0, i);
+  int t = 0;
+  for (; t + 4 < nk; t += 2) {
+    step(K3{}, t, f0, f1);
+    step(K3{}, t + 1, f1, f0);
+  }
+  if (nk - t == 4) {
+    step(K3{}, t, f0, f1);
+    step(K2{}, t + 1, f1, f0);
+    t += 2;
+  }
+  step(K1{}, t, f0, f1);
+  step(K0{}, t + 1, f1, f0);
+
+  // ---- epilogue: acc[mt][nt][i] = G[n0 + wr*128 + mt*16 + l16][k0 + wc*64 + nt*16 + 4g + i]
+  float* dst = out + (ACC ? 0 : (long)split * split_stride);
+#pragma unroll
+  for (int mt = 0; mt < 8; ++mt) {
+    const int n = n0 + wr * 128 + mt * 16 + l16;
+    float* row = dst + (long)n * ldo + k0 + wc * 64 + 4 * g;
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+      float v[4] = {acc[mt][nt][0], acc[mt][nt][1], acc[mt][nt][2], acc[mt][nt][3]};
+      if (ACC) {
+        float o[4];
+        load4(row + nt * 16, o);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[i] += o[i];
+      }
+      store4(row + nt * 16, v);
+    }
+  }
+}
+
+}  // namespace
+
+size_t jm_gemm_tn_smem() { return (size_t)NST * STAGE * sizeof(uint16_t); }
+
+// Split of the M range: returns steps (of 32 rows) per split; *S_out = number of splits.
+// Picks the split count that minimises an estimate of (waves of 256 CUs) x (steps per split +
+// epilogue) + the fp32 partial-tile traffic of the reduction.
+int jm_gemm_tn_plan(int M, int N, int K, int* S_out) {
+  const int tiles = (N / TN_) * (K / TK_);
+  const int steps = (M + BS - 1) / BS;
+  double best = 1e30;
+  int best_sps = steps + (steps & 1), best_S = 1;
+  for (int S = 1; S <= 128; ++S) {
+    int sps = (steps + S - 1) / S;
+    sps += sps & 1;
+    if (sps < 4 && S > 1) break;
+    const int s_eff = (steps + sps - 1) / sps;
+    const long wgs = (long)tiles * s_eff;
+    const long waves = (wgs + 255) / 256;
+    const double t_steps = (double)waves * (sps + 12);                       // ~1 us per step
+    const double t_red = s_eff > 1 ? (double)s_eff * N * K * 8.0 / 5.0e12 * 1e6 : 0.0;  // us
+    const double est = t_steps + t_red;
+    if (est < best) {
+      best = est;
+      best_sps = sps;
+      best_S = s_eff;
+    }
+  }
+  *S_out = best_S;
+  return best_sps;
+}
+
+// G[N][K] (ldo) += A[M][N]^T . B[M][K]; partial: [S][N][K] fp32 workspace when S > 1 (else null)
+int jm_gemm_tn(const uint16_t* A, long lda, const uint16_t* B, long ldb, int M, int N, int K, int sps, int S,
+               float* G, long ldo, float* partial, hipStream_t st) {
+  if (N % TN_ || K % TK_ || M <= 0) return -1;
+  if ((long)M * lda * 2 >= (1L << 32) || (long)M * ldb * 2 >= (1L << 32)) return -2;
+  const int tiles = (N / TN_) * (K / TK_);
+  const size_t sm = jm_gemm_tn_smem();
+  if (S == 1) {
+    static bool attr = false;
+    if (!attr) {
+      (void)hipFuncSetAttribute((const void*)gemm_tn_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
+      attr = true;
+    }
+    gemm_tn_kernel<1><<<tiles, NTH, sm, st>>>(A, lda, B, ldb, M, N, K, sps, G, ldo, 0);
+  } else {
+    if (partial == nullptr) return -3;
+    static bool attr = false;
+    if (!attr) {
+      (void)hipFuncSetAttribute((const void*)gemm_tn_kernel<0>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
+      attr = true;
+    }
+    gemm_tn_kernel<0><<<tiles * S, NTH, sm, st>>>(A, lda, B, ldb, M, N, K, sps, partial, K, (long)N * K);
+  }
+  return 0;
+}

@@ -47,12 +47,23 @@ def wgrad_split(M: int, N: int, K: int) -> int:
     return s
 
 
+_WGRAD_OURS = os.environ.get("JMAE_WGRAD", "1") == "1"
+
+
 def wgrad(h: Handle, dy: torch.Tensor, x: torch.Tensor) -> None:
-    """grad[h] += dy^T @ x  (fp32 accumulate; bf16 inputs on GPU)."""
+    """grad[h] += dy^T @ x  (fp32 accumulate; bf16 inputs on GPU).
+
+    GPU: the TN MFMA kernel (csrc/gemm_tn.hip, M split into fp32 partial tiles) for every shape
+    with 256-aligned N, K and M >= 4096 -- 1.11-1.37x the hipBLASLt split-K path on the ViT-L
+    Jumbo-MAE shapes (profiles/r1_wgrad_tn_vs_hipblaslt.txt); hipBLASLt otherwise."""
     g = h.grad
     if dy.is_cuda and dy.dtype != torch.float32:
         M, N = dy.shape
         K = x.shape[1]
+        if (_WGRAD_OURS and hip(dy) and dy.dtype == torch.bfloat16 and x.dtype == torch.bfloat16
+                and N % 256 == 0 and K % 256 == 0 and M >= 4096 and dy.stride(1) == 1 and x.stride(1) == 1):
+            _ext.load().gemm_tn_wgrad(dy, x, g)
+            return
         s = wgrad_split(M, N, K)
         if s > 1:
             part = torch.bmm(dy.view(s, M // s, N).transpose(1, 2), x.view(s, M // s, K), out_dtype=torch.float32)
@@ -73,7 +84,7 @@ def bias_grad(hb: Handle, dy: torch.Tensor) -> None:
         hb.grad.add_(dy.sum(0, dtype=torch.float32))
 
 
-_GEMM_MODE = os.environ.get("JMAE_GEMM", "auto")  # auto | blas | ours
+_GEMM_MODE = os.environ.get("JMAE_GEMM", "auto")  # auto | blas | ours (forward / dgrad routing)
 _DGRAD_OURS = os.environ.get("JMAE_DGRAD", "1") == "1"  # data-gradient GEMMs on the MFMA kernel
 
 

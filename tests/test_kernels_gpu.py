@@ -245,3 +245,16 @@ def test_transpose_bf16(ext, R, C):
     y = torch.empty(C, R, device="cuda", dtype=torch.bfloat16)
     ext.transpose_bf16(x, y)
     assert torch.equal(y, x.t())
+
+
+@pytest.mark.parametrize("M,N,K", [(4096, 256, 512), (3000, 512, 256), (512, 768, 1024), (26624, 1024, 256)])
+def test_gemm_tn_wgrad(ext, M, N, K):
+    """Weight-gradient TN MFMA GEMM (csrc/gemm_tn.hip): G += dy^T x, split over M, ragged M."""
+    torch.manual_seed(0)
+    dy = (torch.rand(M, N, device="cuda") * 2 - 1).bfloat16()
+    x = (torch.rand(M, K, device="cuda") * 2 - 1).bfloat16()
+    g = torch.randn(N, K, device="cuda")
+    ref = g.double() + dy.double().t() @ x.double()
+    S = ext.gemm_tn_wgrad(dy, x, g)
+    assert S >= 1
+    assert rel(g, ref) < 1e-4

@@ -4,7 +4,7 @@
 
 Each config is a list of ``KEY=VALUE`` switches applied to ``ops.prims`` module state between
 rounds (same model, same data, same device -> no cross-process / cross-device variance).
-Supported keys: JMAE_GEMM (auto|blas|ours), JMAE_DGRAD (0|1), JMAE_WGRAD_STREAM (0|1).
+Supported keys: JMAE_GEMM (auto|blas|ours), JMAE_DGRAD (0|1), JMAE_WGRAD (0|1), JMAE_WGRAD_STREAM (0|1).
 Prints per-config median / min ms per step."""
 
 import argparse
@@ -27,6 +27,8 @@ def apply(P, cfg: str):
             P._DGRAD_OURS = v == "1"
         elif k == "JMAE_WGRAD_STREAM":
             P.set_wgrad_stream(v == "1")
+        elif k == "JMAE_WGRAD":
+            P._WGRAD_OURS = v == "1"
         else:
             raise ValueError(k)
 
