@@ -76,6 +76,8 @@ class Handle:
         self._param: torch.nn.Parameter | None = None
         self._wt: torch.Tensor | None = None
         self._wt_version = -1
+        self.defer_wgrad = False   # batch this weight's gradient GEMMs (weights shared by layers)
+        self.deferred: list = []   # queued (dy, x) pairs of the current backward pass
 
     def _view(self, flat: torch.Tensor) -> torch.Tensor:
         return flat[self.start:self.start + self.numel].view(self.shape)

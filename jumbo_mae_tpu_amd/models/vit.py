@@ -240,6 +240,10 @@ class JumboViT:
                                                  trainable=trainable))
         self.jumbo_mlp = FeedForward(store, P + ("jumbo_mlp",), cfg.jumbo_dim, 4 * cfg.jumbo_dim,
                                      cfg.dropout, trainable)
+        # shared by every layer: its weight gradients are batched into one GEMM over all layers'
+        # rows at the end of backward (ops/prims.py linear_bwd / flush_deferred_wgrads)
+        self.jumbo_mlp.w1.k.defer_wgrad = True
+        self.jumbo_mlp.w2.k.defer_wgrad = True
         store.pad()
         self.layers = []
         for i in range(cfg.layers):

@@ -154,6 +154,42 @@ def _end_of_backward() -> None:
     join_wgrad_stream()
 
 
+# ------------------------------------------------------------- deferred (batched) wgrad
+# A weight used by every layer -- the shared jumbo MLP -- gets 24 weight-gradient GEMMs of only
+# 512 rows (one per layer, ~400 TF/s on hipBLASLt).  Their (dy, x) pairs are queued and, at the
+# end of the backward pass, concatenated into ONE GEMM over 24 x 512 rows on the TN MFMA kernel.
+# The DP reducer is told the segment is ready only then (one ``ready`` per queued use).
+_deferred: dict = {"handles": [], "cb": False, "enabled": os.environ.get("JMAE_DEFER_WGRAD", "1") == "1"}
+
+
+def flush_deferred_wgrads() -> None:
+    _deferred["cb"] = False
+    hs, _deferred["handles"] = _deferred["handles"], []
+    for h in hs:
+        pairs, h.deferred = h.deferred, []
+        if not pairs:
+            continue
+        dy = torch.cat([p[0] for p in pairs]) if len(pairs) > 1 else pairs[0][0]
+        x = torch.cat([p[1] for p in pairs]) if len(pairs) > 1 else pairs[0][1]
+        wgrad(h, dy, x)
+        for _ in pairs:
+            h.ready()
+
+
+def _defer_wgrad(hw: Handle, dy: torch.Tensor, x2: torch.Tensor) -> bool:
+    """Queue (dy, x) for the batched GEMM; False when not inside an autograd backward pass."""
+    if not _deferred["cb"]:
+        try:
+            torch.autograd.Variable._execution_engine.queue_callback(flush_deferred_wgrads)
+        except RuntimeError:
+            return False
+        _deferred["cb"] = True
+    if not hw.deferred:
+        _deferred["handles"].append(hw)
+    hw.deferred.append((dy, x2))
+    return True
+
+
 def wgrad_stream():
     """The side stream (created lazily), or None when disabled / not on a GPU."""
     if not _side["enabled"] or not torch.cuda.is_available():
@@ -187,6 +223,12 @@ def linear_bwd(dy: torch.Tensor, x2: torch.Tensor, hw: Handle, hb: Handle | None
                bias_done: bool = False):
     """dx = dy @ W (if needed); grad W += dy^T x; grad b += colsum(dy) (unless fused upstream)."""
     dx = linear_dgrad(dy, hw) if need_dx else None
+    if _trainable(hw) and hw.defer_wgrad and _deferred["enabled"] and hip(dy) and _defer_wgrad(hw, dy, x2):
+        if hb is not None:
+            if not bias_done:
+                bias_grad(hb, dy)
+            hb.ready()
+        return dx
     if _trainable(hw):
         side = wgrad_stream() if dy.is_cuda else None
         if side is not None:

@@ -29,6 +29,8 @@ def apply(P, cfg: str):
             P.set_wgrad_stream(v == "1")
         elif k == "JMAE_WGRAD":
             P._WGRAD_OURS = v == "1"
+        elif k == "JMAE_DEFER_WGRAD":
+            P._deferred["enabled"] = v == "1"
         else:
             raise ValueError(k)
 

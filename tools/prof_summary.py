@@ -6,7 +6,7 @@ cat = {}
 for r in rows:
     n = r["Name"]; t = float(r["TotalDurationNs"]) / 1e6 / steps
     if n.startswith("Cijk") or n.startswith("Custom_Cijk"): k = "GEMM(hipBLASLt)"
-    elif "gemm_nt_kernel" in n: k = "GEMM (ours, MFMA)"
+    elif "gemm_nt_kernel" in n or "gemm_tn_kernel" in n: k = "GEMM (ours, MFMA)"
     elif "attn" in n: k = "attention"
     elif "ln_" in n: k = "layernorm"
     elif "rowcol" in n or "gelu" in n or "residual" in n: k = "fused elementwise (ours)"
