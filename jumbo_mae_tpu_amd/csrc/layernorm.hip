@@ -70,6 +70,89 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const float* __restrict__ x
   }
 }
 
+// Residual add fused with the LayerNorm that reads its result (the block's second LN):
+//   x1[b,t] = x[b,t] + mask[b] * scale * y[b*T+t]          (written, the residual stream)
+//   h[b, t-T0] = LN(x1[b,t]) for t >= T0 (bf16), with its mean / rstd
+// Rows t < T0 (the Jumbo CLS tokens, normalized jointly by LN3 elsewhere) only get the add.
+// Saves the LN's re-read of x1 from HBM.
+struct ResLnIO {
+  const float* x;
+  long sB, sT;
+  const uint16_t* y;  // [B*T, D] bf16
+  const float* scale;
+  const float* mask;
+  float* x1;
+  long oB, oT;
+  uint16_t* h;        // [B*(T-T0), D]
+  float* mean;
+  float* rstd;
+};
+
+template <int V>
+__global__ __launch_bounds__(256) void res_ln_fwd_kernel(ResLnIO io, int T, int T0, int rows, int D,
+                                                         const float* __restrict__ gamma,
+                                                         const float* __restrict__ beta, float eps) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + wave;
+  if (row >= rows) return;
+  const int b = row / T, t = row - b * T;
+  const float* xr = io.x + b * io.sB + t * io.sT;
+  const uint16_t* yr = io.y + (long)row * D;
+  float* x1r = io.x1 + b * io.oB + t * io.oT;
+  const float m = io.mask ? io.mask[b] : 1.f;
+  float v[V][4];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < V; ++i) {
+    const int col = (i * 64 + lane) * 4;
+    if (col < D) {
+      float xv[4], yv[4], sc[4] = {1.f, 1.f, 1.f, 1.f};
+      load4(xr + col, xv);
+      load4(yr + col, yv);
+      if (io.scale) load4(io.scale + col, sc);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[i][j] = xv[j] + m * sc[j] * yv[j];
+      store4(x1r + col, v[i]);
+    } else {
+      v[i][0] = v[i][1] = v[i][2] = v[i][3] = 0.f;
+    }
+    s += v[i][0] + v[i][1] + v[i][2] + v[i][3];
+  }
+  if (t < T0) return;  // wave-uniform
+  const float mean = wave_sum(s) / D;
+  float s2 = 0.f;
+#pragma unroll
+  for (int i = 0; i < V; ++i) {
+    const int col = (i * 64 + lane) * 4;
+    if (col < D) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float d = v[i][j] - mean;
+        s2 += d * d;
+      }
+    }
+  }
+  const float rstd = rsqrtf(wave_sum(s2) / D + eps);
+  const long hrow = (long)b * (T - T0) + (t - T0);
+  uint16_t* hr = io.h + hrow * D;
+#pragma unroll
+  for (int i = 0; i < V; ++i) {
+    const int col = (i * 64 + lane) * 4;
+    if (col < D) {
+      float gg[4], bb[4], o[4];
+      load4(gamma + col, gg);
+      load4(beta + col, bb);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) o[j] = (v[i][j] - mean) * rstd * gg[j] + bb[j];
+      store4(hr + col, o);
+    }
+  }
+  if (lane == 0) {
+    io.mean[hrow] = mean;
+    io.rstd[hrow] = rstd;
+  }
+}
+
 // dx output and optional residual-gradient input, both [B, T, D] views with their own strides:
 // dx = LN'(dy) (+ dres), i.e. the residual-stream gradient add is fused into the LN backward.
 struct LnBwdIO {
@@ -255,6 +338,24 @@ int jm_layernorm_fwd(const float* x, long sB, long sT, int B, int T, int D, cons
     launch_fwd<uint16_t>(V, grid, st, x, sB, sT, T, rows, D, gamma, beta, eps, (uint16_t*)y, mean, rstd);
   else
     launch_fwd<float>(V, grid, st, x, sB, sT, T, rows, D, gamma, beta, eps, (float*)y, mean, rstd);
+  return 0;
+}
+
+int jm_residual_ln_fwd(const float* x, long sB, long sT, const uint16_t* y, const float* scale, const float* mask,
+                       float* x1, long oB, long oT, uint16_t* h, float* mean, float* rstd, int B, int T, int T0,
+                       int D, const float* gamma, const float* beta, float eps, hipStream_t st) {
+  const ResLnIO io{x, sB, sT, y, scale, mask, x1, oB, oT, h, mean, rstd};
+  const int V = pick_v(D);
+  if (V < 0 || (D % 4) != 0) return -1;
+  const int rows = B * T;
+  dim3 grid((rows + 3) / 4);
+#define JM_RLN(VV) \
+  case VV: res_ln_fwd_kernel<VV><<<grid, 256, 0, st>>>(io, T, T0, rows, D, gamma, beta, eps); break;
+  switch (V) {
+    JM_RLN(1) JM_RLN(2) JM_RLN(3) JM_RLN(4) JM_RLN(6) JM_RLN(8) JM_RLN(9) JM_RLN(12) JM_RLN(16)
+    default: return -1;
+  }
+#undef JM_RLN
   return 0;
 }
 

@@ -71,7 +71,8 @@ class JumboBlockFn(torch.autograd.Function):
         dt = layer.norm1.g.store.compute_dtype
         h1, mu1, rs1 = P.ln_fwd(x, layer.norm1.g, layer.norm1.b, dt)
         qkv, o, lse, a = _attn_fwd(layer.attn, h1, B, S)
-        x1 = P.residual_fwd(x, a, layer.scale1, m1)
+        # residual + LN2 of the patch rows in one pass
+        x1, hp, mup, rsp = P.residual_ln_fwd(x, a, layer.scale1, m1, layer.norm2.g, layer.norm2.b, C)
         # jumbo branch: LN3 on the concatenated CLS tokens, residual on the *normalized* value
         cls_in = x1[:, :C].reshape(B, 1, J)
         hc, muc, rsc = P.ln_fwd(cls_in, layer.norm3.g, layer.norm3.b, torch.float32)
@@ -79,7 +80,6 @@ class JumboBlockFn(torch.autograd.Function):
         jpre, jg, jy = _ff_fwd(layer.jumbo_mlp, hcb)
         # patch branch
         pin = x1[:, C:]
-        hp, mup, rsp = P.ln_fwd(pin, layer.norm2.g, layer.norm2.b, dt)
         fpre, fg, fy = _ff_fwd(layer.ff, hp)
         x2 = torch.empty_like(x1)
         P.residual_fwd(hc.view(B, 1, J), jy, layer.scale3, m3, out=x2[:, :C].reshape(B, 1, J))
@@ -132,8 +132,7 @@ class ViTBlockFn(torch.autograd.Function):
         dt = layer.norm1.g.store.compute_dtype
         h1, mu1, rs1 = P.ln_fwd(x, layer.norm1.g, layer.norm1.b, dt)
         qkv, o, lse, a = _attn_fwd(layer.attn, h1, B, S)
-        x1 = P.residual_fwd(x, a, layer.scale1, m1)
-        h2, mu2, rs2 = P.ln_fwd(x1, layer.norm2.g, layer.norm2.b, dt)
+        x1, h2, mu2, rs2 = P.residual_ln_fwd(x, a, layer.scale1, m1, layer.norm2.g, layer.norm2.b, 0)
         fpre, fg, fy = _ff_fwd(layer.ff, h2)
         x2 = P.residual_fwd(x1, fy, layer.scale2, m2)
         ctx.save_for_backward(x, mu1, rs1, h1, qkv, o, lse, a, x1, mu2, rs2, h2, fpre, fg, fy, m1, m2)

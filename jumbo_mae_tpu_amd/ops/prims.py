@@ -352,6 +352,19 @@ def residual_fwd(x3: torch.Tensor, y2: torch.Tensor, hs: Handle | None, mask, ou
     return res
 
 
+def residual_ln_fwd(x3: torch.Tensor, y2: torch.Tensor, hs: Handle | None, mask, hg: Handle, hb: Handle,
+                    t0: int = 0):
+    """x1 = x + mask*s*y (fresh [B,T,D] fp32) and the LayerNorm of its rows t >= t0 in one pass:
+    returns (x1, h [B*(T-t0), D] bf16, mean, rstd).  The fused kernel saves the LN's re-read of x1."""
+    B, T, D = x3.shape
+    if hip(x3) and y2.dtype == torch.bfloat16:
+        return tuple(_ext.load().residual_ln_fwd(x3, y2.reshape(B * T, D), hs.master if hs is not None else None,
+                                                 mask, hg.master, hb.master, LN_EPS, t0))
+    x1 = residual_fwd(x3, y2, hs, mask)
+    h, mean, rstd = ln_fwd(x1[:, t0:], hg, hb, hg.store.compute_dtype)
+    return x1, h, mean, rstd
+
+
 def residual_bwd(dout3: torch.Tensor, y2: torch.Tensor | None, hs: Handle | None, mask, ydtype,
                  hbias: Handle | None = None):
     """dy = mask[b] * s * dout (in ``ydtype``); ds += sum mask*dout*y.  When ``hbias`` (the bias of

@@ -258,3 +258,22 @@ def test_gemm_tn_wgrad(ext, M, N, K):
     S = ext.gemm_tn_wgrad(dy, x, g)
     assert S >= 1
     assert rel(g, ref) < 1e-4
+
+
+@pytest.mark.parametrize("T0", [0, 3])
+@pytest.mark.parametrize("with_scale", [False, True])
+def test_residual_ln_fwd(ext, T0, with_scale):
+    """Fused residual + LayerNorm == residual_fwd followed by layernorm_fwd (bit-identical math)."""
+    torch.manual_seed(0)
+    B, T, D = 5, 52, 1024
+    x = torch.randn(B, T, D, device="cuda")
+    y = torch.randn(B * T, D, device="cuda").bfloat16()
+    s = torch.rand(D, device="cuda") if with_scale else None
+    mask = (torch.rand(B, device="cuda") > 0.3).float() / 0.7
+    g, b = torch.rand(D, device="cuda") + 0.5, torch.randn(D, device="cuda")
+    x1, h, mu, rs = ext.residual_ln_fwd(x, y, s, mask, g, b, 1e-6, T0)
+    x1r = ext.residual_fwd(x, y, s, mask)
+    hr, mur, rsr = ext.layernorm_fwd(x1r[:, T0:], g, b, 1e-6, torch.bfloat16)
+    assert torch.equal(x1, x1r)
+    assert (h.float() - hr.float()).abs().max().item() <= 0.0625
+    assert torch.allclose(mu, mur, atol=1e-6) and torch.allclose(rs, rsr, rtol=1e-5)
