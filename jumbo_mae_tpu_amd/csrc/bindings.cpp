@@ -50,7 +50,10 @@ struct GemmEpi {
   uint16_t* out2;
   const uint16_t* aux;
   float* colpart;
+  float* part;
+  int splits;
 };
+int jm_splitk_reduce_bf16(const float* part, int S, long n, int N, const float* bias, uint16_t* out, hipStream_t st);
 int jm_gemm_nt(const uint16_t* A, long lda, const uint16_t* B, long ldb, int M, int N, int K, int epi,
                const GemmEpi& ep, hipStream_t st);
 void jm_gemm_set_variant(int wn, int group);
@@ -312,7 +315,7 @@ std::vector<torch::Tensor> gemm_nt(torch::Tensor A, torch::Tensor B, c10::option
   const int M = A.size(0), N = B.size(0), K = A.size(1);
   auto out = torch::empty({M, N}, A.options());
   torch::Tensor out2;
-  GemmEpi ep{nullptr, bfm(out), N, nullptr, nullptr, nullptr};
+  GemmEpi ep{nullptr, bfm(out), N, nullptr, nullptr, nullptr, nullptr, 1};
   if (bias) {
     TORCH_CHECK(bias->is_contiguous() && bias->scalar_type() == torch::kFloat32 && bias->numel() == N, "gemm_nt bias");
     ep.bias = bias->data_ptr<float>();
@@ -324,6 +327,27 @@ std::vector<torch::Tensor> gemm_nt(torch::Tensor A, torch::Tensor B, c10::option
   check_rc(jm_gemm_nt(bf(A), A.stride(0), bf(B), B.stride(0), M, N, K, gelu ? 1 : 0, ep, stream()), "gemm_nt");
   if (gelu) return {out, out2};
   return {out};
+}
+
+// split-K: C[M, N] = A[M, K] . B[N, K]^T (+ bias) in bf16 via S fp32 partial products
+torch::Tensor gemm_nt_splitk(torch::Tensor A, torch::Tensor B, c10::optional<torch::Tensor> bias, int64_t splits) {
+  CHECK_DT(A, torch::kBFloat16);
+  CHECK_DT(B, torch::kBFloat16);
+  TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && A.size(1) == B.size(1), "gemm_nt_splitk: A [M,K], B [N,K]");
+  TORCH_CHECK(A.stride(1) == 1 && B.stride(1) == 1, "gemm_nt_splitk: K must be contiguous");
+  const int M = A.size(0), N = B.size(0), K = A.size(1);
+  auto out = torch::empty({M, N}, A.options());
+  auto part = torch::empty({splits, (long)M * N}, A.options().dtype(torch::kFloat32));
+  GemmEpi ep{nullptr, bfm(out), N, nullptr, nullptr, nullptr, part.data_ptr<float>(), (int)splits};
+  check_rc(jm_gemm_nt(bf(A), A.stride(0), bf(B), B.stride(0), M, N, K, 3, ep, stream()), "gemm_nt_splitk");
+  const float* bp = nullptr;
+  if (bias) {
+    TORCH_CHECK(bias->is_contiguous() && bias->scalar_type() == torch::kFloat32 && bias->numel() == N, "bias");
+    bp = bias->data_ptr<float>();
+  }
+  check_rc(jm_splitk_reduce_bf16(part.data_ptr<float>(), (int)splits, (long)M * N, N, bp, bfm(out), stream()),
+           "gemm_nt_splitk reduce");
+  return out;
 }
 
 // dh[M, N] = (A[M, K] . B[N, K]^T) * gelu'(pre[M, N]) -- FF2 data gradient through the GELU,
@@ -338,7 +362,7 @@ torch::Tensor gemm_nt_dgelu(torch::Tensor A, torch::Tensor B, torch::Tensor pre,
   TORCH_CHECK(pre.is_contiguous() && pre.size(0) == M && pre.size(1) == N, "gemm_nt_dgelu: pre [M,N]");
   auto out = torch::empty({M, N}, A.options());
   torch::Tensor part;
-  GemmEpi ep{nullptr, bfm(out), N, nullptr, bf(pre), nullptr};
+  GemmEpi ep{nullptr, bfm(out), N, nullptr, bf(pre), nullptr, nullptr, 1};
   const int nM = (M + 255) / 256;
   if (dbias) {
     TORCH_CHECK(dbias->is_contiguous() && dbias->scalar_type() == torch::kFloat32 && dbias->numel() == N,
@@ -431,6 +455,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("attn_max_seq", &jm_attn_max_seq);
   m.def("gemm_tn_wgrad", &gemm_tn_wgrad);
   m.def("gemm_set_variant", &jm_gemm_set_variant, py::arg("wn"), py::arg("group") = 8);
+  m.def("gemm_nt_splitk", &gemm_nt_splitk, py::arg("A"), py::arg("B"), py::arg("bias") = py::none(),
+        py::arg("splits") = 8);
   m.def("gemm_nt_dgelu", &gemm_nt_dgelu, py::arg("A"), py::arg("B"), py::arg("pre"), py::arg("dbias") = py::none());
   m.def("gemm_nt", &gemm_nt, py::arg("A"), py::arg("B"), py::arg("bias") = py::none(), py::arg("gelu") = false);
   m.def("attn_set_tr", &jm_attn_set_tr);

@@ -350,3 +350,38 @@ int jm_transpose_bf16(const uint16_t* src, uint16_t* dst, int R, int C, hipStrea
   transpose_bf16_kernel<<<grid, 256, 0, st>>>(src, dst, R, C);
   return 0;
 }
+
+// ------------------------------------------------------------------ split-K finish
+// out[m][n] (bf16) = sum_s part[s][m][n] (+ bias[n]): the epilogue of a split-K NT GEMM
+namespace {
+__global__ __launch_bounds__(256) void splitk_reduce_bf16_kernel(const float* __restrict__ part, int S, long n8,
+                                                                 int N, const float* __restrict__ bias,
+                                                                 uint16_t* __restrict__ out) {
+  const long total = n8 * 8;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n8; i += (long)gridDim.x * 256) {
+    float acc[8];
+    load8(part + i * 8, acc);
+    for (int s = 1; s < S; ++s) {
+      float v[8];
+      load8(part + (long)s * total + i * 8, v);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] += v[j];
+    }
+    if (bias) {
+      float b[8];
+      load8(bias + (i * 8) % N, b);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] += b[j];
+    }
+    store8(out + i * 8, acc);
+  }
+}
+}  // namespace
+
+int jm_splitk_reduce_bf16(const float* part, int S, long n, int N, const float* bias, uint16_t* out, hipStream_t st) {
+  if (n % 8 || N % 8) return -1;
+  long blocks = (n / 8 + 255) / 256;
+  if (blocks > 8192) blocks = 8192;
+  splitk_reduce_bf16_kernel<<<(int)blocks, 256, 0, st>>>(part, S, n / 8, N, bias, out);
+  return 0;
+}

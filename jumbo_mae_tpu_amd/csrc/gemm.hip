@@ -69,12 +69,17 @@ struct GemmEpi {
   uint16_t* out2;        // EPI_GELU: gelu(out) bf16 [M, ldo]
   const uint16_t* aux;   // EPI_DGELU: pre-activation h bf16 [M, ldo]
   float* colpart;        // EPI_DGELU: per-row-tile column sums of out, [ceil(M/256)][N] fp32 (or null)
+  float* part;           // EPI_PARTIAL: [splits][M][N] fp32 split-K partial products
+  int splits;            // K splits (1 = none)
 };
 
 // EPI_STORE: out = acc (+bias); EPI_GELU: out = acc (+bias), out2 = gelu(out);
 // EPI_DGELU: out = bf16(acc) * gelu'(aux) -- the data gradient through the FF GELU -- with the
 // following Dense's bias gradient (column sums of out) as per-tile partials.
-enum { EPI_STORE = 0, EPI_GELU = 1, EPI_DGELU = 2 };
+// EPI_PARTIAL: split-K -- each (tile, split) workgroup stores its fp32 partial tile; the sum (+bias,
+// bf16) is taken by jm_splitk_reduce_bf16.  For small-M, long-K GEMMs (the jumbo MLP: 512 rows,
+// K = 12288) whose 24 output tiles would otherwise occupy 24 of 256 CUs.
+enum { EPI_STORE = 0, EPI_GELU = 1, EPI_DGELU = 2, EPI_PARTIAL = 3 };
 
 namespace {
 
@@ -106,12 +111,16 @@ JM_DEVICE void epilogue(const f32x4_t (&acc)[8][NTW], const GemmEpi& ep, int M, 
   }
 }
 
-JM_DEVICE void tile_of(int M, int N, int GROUP_M, int& m0, int& n0) {
+JM_DEVICE void tile_of(int M, int N, int GROUP_M, int& m0, int& n0, int splits = 1, int* split = nullptr) {
   const int nM = (M + BM - 1) / BM, nN = (N + BN - 1) / BN;
-  const int nwg = nM * nN;
+  const int nwg = nM * nN * splits;
   const int orig = blockIdx.x;
   const int xcd = orig & 7, q = nwg >> 3, r = nwg & 7;
-  const int wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+  int wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+  if (split) {  // split-major: concurrently running blocks work on the same K range
+    *split = wg / (nM * nN);
+    wg -= *split * (nM * nN);
+  }
   const int per_group = GROUP_M * nN;
   const int first_m = (wg / per_group) * GROUP_M;
   const int gsz = min(nM - first_m, GROUP_M);
@@ -214,12 +223,19 @@ __global__ __launch_bounds__(128 * WN, 1) void gemm_nt_kernel(const uint16_t* __
   const int l16 = lane & 15, g = lane >> 4;
   const int wr = wave / WN, wc = wave % WN;
 
-  int m0, n0;
-  tile_of(M, N, GROUP_M, m0, n0);
+  int m0, n0, split = 0;
+  tile_of(M, N, GROUP_M, m0, n0, EPI == EPI_PARTIAL ? ep.splits : 1, EPI == EPI_PARTIAL ? &split : nullptr);
+  int k_begin = 0;
+  if (EPI == EPI_PARTIAL) {  // this split's K range, in units of 64
+    const int ku = K / 64;
+    const int ku0 = split * ku / ep.splits, ku1 = (split + 1) * ku / ep.splits;
+    k_begin = ku0 * 64;
+    K = (ku1 - ku0) * 64;
+  }
 
   // ---- per-lane swizzled source offsets: RND rounds x NW waves x 16 rows per operand and stage
-  const __amdgpu_buffer_rsrc_t ra = make_rsrc(A + (long)m0 * lda, (long)(M - m0) * lda * 2);
-  const __amdgpu_buffer_rsrc_t rb = make_rsrc(B + (long)n0 * ldb, (long)(N - n0) * ldb * 2);
+  const __amdgpu_buffer_rsrc_t ra = make_rsrc(A + (long)m0 * lda + k_begin, (long)(M - m0) * lda * 2 - 2L * k_begin);
+  const __amdgpu_buffer_rsrc_t rb = make_rsrc(B + (long)n0 * ldb + k_begin, (long)(N - n0) * ldb * 2 - 2L * k_begin);
   uint32_t a_src[RND], b_src[RND];  // byte offsets
 #pragma unroll
   for (int rr = 0; rr < RND; ++rr) {
@@ -323,7 +339,21 @@ __global__ __launch_bounds__(128 * WN, 1) void gemm_nt_kernel(const uint16_t* __
   step(K1{}, t, f0, f1);
   step(K0{}, t + 1, f1, f0);
 
-  if (N % 8 == 0)
+  if (EPI == EPI_PARTIAL) {
+    float* dst = ep.part + (long)split * M * N;
+#pragma unroll
+    for (int mt = 0; mt < 8; ++mt) {
+      const int m = m0 + wr * 128 + mt * 16 + l16;
+      if (m >= M) continue;
+#pragma unroll
+      for (int nt = 0; nt < NTW; ++nt) {
+        const int n = n0 + wc * NTW * 16 + nt * 16 + 4 * g;
+        if (n >= N) continue;
+        float v[4] = {acc[mt][nt][0], acc[mt][nt][1], acc[mt][nt][2], acc[mt][nt][3]};
+        store4(dst + (long)m * N + n, v);
+      }
+    }
+  } else if (N % 8 == 0)
     epilogue_lds<EPI, NTW, 128 * WN>(acc, ep, smem, M, N, m0, n0, wr, wc, l16, g);
   else
     epilogue<EPI, NTW>(acc, ep, M, N, m0 + wr * 128, n0 + wc * NTW * 16, l16, g);
@@ -377,8 +407,11 @@ int jm_gemm_nt(const uint16_t* A, long lda, const uint16_t* B, long ldb, int M, 
                const GemmEpi& ep, hipStream_t st) {
   if (K % (2 * BK) || N % 4 || M <= 0 || N <= 0) return -1;
   if ((long)M * lda * 2 >= (1L << 32) || (long)N * ldb * 2 >= (1L << 32)) return -2;
-  const int nwg = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
-  if (epi == EPI_STORE)
+  const int nwg = ((M + BM - 1) / BM) * ((N + BN - 1) / BN) * (epi == EPI_PARTIAL ? ep.splits : 1);
+  if (epi == EPI_PARTIAL && (ep.splits < 1 || (K / 64) < ep.splits)) return -4;
+  if (epi == EPI_PARTIAL)
+    launch_epi<EPI_PARTIAL>(A, lda, B, ldb, M, N, K, ep, nwg, st);
+  else if (epi == EPI_STORE)
     launch_epi<EPI_STORE>(A, lda, B, ldb, M, N, K, ep, nwg, st);
   else if (epi == EPI_GELU)
     launch_epi<EPI_GELU>(A, lda, B, ldb, M, N, K, ep, nwg, st);

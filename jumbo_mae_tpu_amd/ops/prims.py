@@ -118,8 +118,23 @@ def use_our_gemm(M: int, N: int, K: int, fused_gelu: bool = False, kind: str = "
     return fused_gelu or fill >= 0.9
 
 
+def splitk_plan(M: int, N: int, K: int) -> int:
+    """Split-K factor for a small-M, long-K GEMM on the MFMA kernel (0 = not this path): the
+    jumbo MLP's 512-row GEMMs with K = 12288 have only 24 output tiles for 256 CUs."""
+    if _GEMM_MODE == "blas" or M > 2048 or K < 4096 or K % 64 or N % 8:
+        return 0
+    tiles = -(-M // 256) * -(-N // 256)
+    if tiles > 64:
+        return 0
+    return max(2, min(256 // tiles, K // 512, 32))
+
+
 def linear_fwd(x2: torch.Tensor, hw: Handle, hb: Handle | None) -> torch.Tensor:
     w = hw.weight()
+    if hip(x2) and x2.dtype == torch.bfloat16:
+        s = splitk_plan(x2.shape[0], w.shape[0], x2.shape[1])
+        if s:
+            return _ext.load().gemm_nt_splitk(x2, w, hb.master if hb is not None else None, s)
     if hip(x2) and x2.dtype == torch.bfloat16 and use_our_gemm(x2.shape[0], w.shape[0], x2.shape[1]):
         return _ext.load().gemm_nt(x2, w, hb.master if hb is not None else None, False)[0]
     if hb is not None:
@@ -213,6 +228,10 @@ def join_wgrad_stream() -> None:
 def linear_dgrad(dy: torch.Tensor, hw: Handle) -> torch.Tensor:
     """dx = dy @ W: on the MFMA kernel against the transposed weight copy when it wins."""
     w = hw.weight()
+    if _DGRAD_OURS and hip(dy) and dy.dtype == torch.bfloat16:
+        s = splitk_plan(dy.shape[0], w.shape[1], w.shape[0])
+        if s:
+            return _ext.load().gemm_nt_splitk(dy.contiguous(), hw.weight_t(), None, s)
     if (_DGRAD_OURS and hip(dy) and dy.dtype == torch.bfloat16
             and use_our_gemm(dy.shape[0], w.shape[1], w.shape[0], kind="dgrad")):
         return _ext.load().gemm_nt(dy.contiguous(), hw.weight_t(), None, False)[0]

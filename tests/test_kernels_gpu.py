@@ -277,3 +277,15 @@ def test_residual_ln_fwd(ext, T0, with_scale):
     assert torch.equal(x1, x1r)
     assert (h.float() - hr.float()).abs().max().item() <= 0.0625
     assert torch.allclose(mu, mur, atol=1e-6) and torch.allclose(rs, rsr, rtol=1e-5)
+
+
+@pytest.mark.parametrize("M,N,K,S", [(512, 3072, 12288, 10), (300, 512, 4096, 3), (512, 256, 1024, 16)])
+def test_gemm_nt_splitk(ext, M, N, K, S):
+    """Split-K MFMA GEMM (fp32 partial tiles + bf16 reduce with bias), ragged M."""
+    torch.manual_seed(0)
+    x = (torch.rand(M, K, device="cuda") * 2 - 1).bfloat16()
+    w = ((torch.rand(N, K, device="cuda") * 2 - 1) * 0.05).bfloat16()
+    b = torch.randn(N, device="cuda") * 0.1
+    out = ext.gemm_nt_splitk(x, w, b, S)
+    ref = x.float() @ w.float().t() + b
+    assert rel(out, ref) < 1e-2

@@ -52,6 +52,8 @@ def main():
                 continue
             if kind == "dgrad_gelu" and name not in ("enc_ff2", "dec_ff2"):
                 continue
+            if kind == "splitk" and name not in ("jumbo1", "jumbo2"):
+                continue
             if kind in ("dgrad", "dgrad_gelu"):  # dX[M,K] = dy[M,N] @ W[N,K]  ->  NT with B = W^T [K, N]
                 M, N, K = M, K, N
             x = (torch.rand(M, K, device="cuda") * 2 - 1).bfloat16()
@@ -59,7 +61,12 @@ def main():
             b = torch.randn(N, device="cuda") * 0.1
             bb = b.bfloat16()
             gelu = kind == "fwd_gelu"
-            if kind == "dgrad_gelu":
+            if kind == "splitk":
+                from jumbo_mae_tpu_amd.ops.prims import splitk_plan
+                S = max(2, splitk_plan(M, N, K))
+                ours = lambda: (ext.gemm_nt_splitk(x, w, b, S),)  # noqa: E731
+                blas = lambda: torch.addmm(bb, x, w.t())  # noqa: E731
+            elif kind == "dgrad_gelu":
                 wm = w.t().contiguous()
                 pre = (torch.randn(M, N, device="cuda") * 2).bfloat16()
                 dbg = torch.zeros(N, device="cuda")
