@@ -359,6 +359,242 @@ __global__ __launch_bounds__(128 * WN, 1) void gemm_nt_kernel(const uint16_t* __
     epilogue<EPI, NTW>(acc, ep, M, N, m0 + wr * 128, n0 + wc * NTW * 16, l16, g);
 }
 
+// ------------------------------------------------------------------ persistent variant
+// One workgroup per CU walks its tiles (bid, bid + G, ...) as ONE stream of K steps: the ring's
+// look-ahead loads run straight into the next tile, so a tile's prologue latency is hidden behind
+// the previous tile's last steps and its epilogue.  The epilogue stages C through the single ring
+// slot that is free at a tile boundary (the other three hold the next tile's first stages), in
+// four passes of 64 rows; raw s_barrier + lgkmcnt waits keep the in-flight prefetch alive.
+JM_DEVICE void bar_lds() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// LDS traffic of the persistent epilogue goes through inline asm: hipcc cannot tell the staging
+// slot from the ring slots the next tile's DMA is filling, and would put vmcnt(0) (= drain the
+// whole prefetch) in front of every compiler-visible LDS access.  Same for global loads, hence
+// the bias is staged in LDS once at kernel start.
+JM_DEVICE uint32_t lds_addr(const void* p) {
+  return (uint32_t)(size_t)((const __attribute__((address_space(3))) char*)p);
+}
+JM_DEVICE void ds_w64(uint32_t a, uint2 v) { asm volatile("ds_write_b64 %0, %1" ::"v"(a), "v"(v) : "memory"); }
+JM_DEVICE uint4 ds_r128(uint32_t a) {
+  uint4 r;
+  asm volatile("ds_read_b128 %0, %1" : "=v"(r) : "v"(a));
+  return r;
+}
+JM_DEVICE void wait_lgkm() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+template <int EPI>
+JM_DEVICE void epilogue_chunked(const f32x4_t (&acc)[8][4], const GemmEpi& ep, const float* bias_lds,
+                                uint16_t* cs, int M, int N, int m0, int n0, int wr, int wc, int l16, int g) {
+  static_assert(EPI == EPI_STORE || EPI == EPI_GELU, "persistent epilogue: store / gelu only");
+  constexpr int NTH = 512, LPR = BN / 8, RPP = NTH / LPR;  // 32 lanes per 512 B row, 16 rows per sweep
+  const int tid = threadIdx.x;
+  const int c = tid % LPR;
+  const bool col_ok = n0 + c * 8 < N;
+  const uint32_t csa = lds_addr(cs);
+  const uint32_t ba = bias_lds ? lds_addr(bias_lds) : 0u;
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {  // rows [64 p, 64 p + 64): waves with wr == p / 2, mt in 4 (p % 2) + 0..3
+    if (wr == (p >> 1)) {
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) {
+        const int nl = wc * 64 + nt * 16 + 4 * g;
+        float bv[4] = {0.f, 0.f, 0.f, 0.f};
+        if (bias_lds) {  // re-read per pass: keeps 16 VGPRs free for the next tile's fragments
+          const uint4 r = ds_r128(ba + 4 * min(n0 + nl, N - 4));
+          wait_lgkm();
+          if (n0 + nl < N) {
+            bv[0] = __uint_as_float(r.x);
+            bv[1] = __uint_as_float(r.y);
+            bv[2] = __uint_as_float(r.z);
+            bv[3] = __uint_as_float(r.w);
+          }
+        }
+#pragma unroll
+        for (int mm = 0; mm < 4; ++mm) {
+          const int mt = (p & 1) * 4 + mm;
+          const int rl = mm * 16 + l16;
+          uint2 pk;
+          pk.x = pack_bf2(acc[mt][nt][0] + bv[0], acc[mt][nt][1] + bv[1]);
+          pk.y = pack_bf2(acc[mt][nt][2] + bv[2], acc[mt][nt][3] + bv[3]);
+          ds_w64(csa + 2 * (rl * BN + (((nl >> 3) ^ (rl & 15)) << 3) + (nl & 7)), pk);
+        }
+      }
+    }
+    bar_lds();
+    uint4 v[64 / RPP];
+#pragma unroll
+    for (int k = 0; k < 64 / RPP; ++k) {
+      const int rl = tid / LPR + k * RPP;
+      v[k] = ds_r128(csa + 2 * (rl * BN + ((c ^ (rl & 15)) << 3)));
+    }
+    wait_lgkm();
+#pragma unroll
+    for (int k = 0; k < 64 / RPP; ++k) {
+      const int m = m0 + p * 64 + tid / LPR + k * RPP;
+      if (m < M && col_ok) {
+        *reinterpret_cast<uint4*>(ep.out + (long)m * ep.ldo + n0 + c * 8) = v[k];
+        if (EPI == EPI_GELU) {
+          float f[8];
+          const uint16_t* h = reinterpret_cast<const uint16_t*>(&v[k]);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) f[j] = gelu_tanh_f(bf2f(h[j]));
+          store8(ep.out2 + (long)m * ep.ldo + n0 + c * 8, f);
+        }
+      }
+    }
+    bar_lds();
+  }
+}
+
+template <int EPI>
+__global__ __launch_bounds__(512, 1) void gemm_nt_persist_kernel(const uint16_t* __restrict__ A, long lda,
+                                                                 const uint16_t* __restrict__ B, long ldb, int M,
+                                                                 int N, int K, GemmEpi ep, int GROUP_M) {
+  constexpr int NW = 8, NTW = 4, RND = 2;
+  extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
+  const int tid = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+  const int l16 = lane & 15, g = lane >> 4;
+  const int wr = wave >> 2, wc = wave & 3;
+  const int nM = (M + BM - 1) / BM, nN = (N + BN - 1) / BN, tiles = nM * nN;
+  const int G = gridDim.x;  // multiple of 8
+  // workgroups of one XCD (bid % 8) take consecutive slots -> tiles in flight together are
+  // neighbours in the grouped order
+  const int slot = (blockIdx.x & 7) * (G >> 3) + (blockIdx.x >> 3);
+  const int my_tiles = slot < tiles ? (tiles - slot + G - 1) / G : 0;
+  const int nk = K / BK;
+  const int total = my_tiles * nk;
+  if (total == 0) return;
+  float* bias_lds = nullptr;
+  if (ep.bias) {  // whole bias into LDS behind the ring, before any DMA is in flight
+    bias_lds = reinterpret_cast<float*>(smem + NST * STAGE);
+    for (int i = tid; i < N; i += 512) bias_lds[i] = ep.bias[i];
+    __syncthreads();
+  }
+  auto tile_coords = [&](int j, int& m0, int& n0) {
+    const int wg = slot + j * G;
+    const int per_group = GROUP_M * nN;
+    const int first_m = (wg / per_group) * GROUP_M;
+    const int gsz = min(nM - first_m, GROUP_M);
+    m0 = (first_m + (wg % per_group) % gsz) * BM;
+    n0 = ((wg % per_group) / gsz) * BN;
+  };
+  uint32_t a_src[RND], b_src[RND];
+#pragma unroll
+  for (int rr = 0; rr < RND; ++rr) {
+    const int row = rr * 16 * NW + wave * 16 + (lane >> 2);
+    const int c = (lane & 3) ^ swz(row);
+    a_src[rr] = (uint32_t)((row * lda + c * 8) * 2);
+    b_src[rr] = (uint32_t)((row * ldb + c * 8) * 2);
+  }
+  auto issue = [&](int u) {  // stage u of this workgroup's stream
+    const int j = u / nk, t = u - j * nk;
+    int m0, n0;
+    tile_coords(j, m0, n0);
+    const __amdgpu_buffer_rsrc_t ra = make_rsrc(A + (long)m0 * lda, (long)(M - m0) * lda * 2);
+    const __amdgpu_buffer_rsrc_t rb = make_rsrc(B + (long)n0 * ldb, (long)(N - n0) * ldb * 2);
+    const uint32_t k0b = t * BK * 2;
+    uint16_t* la = smem + (u % NST) * STAGE;
+    uint16_t* lb = la + BM * BK;
+#pragma unroll
+    for (int rr = 0; rr < RND; ++rr) {
+      blds16(ra, a_src[rr], k0b, la + (rr * 16 * NW + wave * 16) * BK);
+      blds16(rb, b_src[rr], k0b, lb + (rr * 16 * NW + wave * 16) * BK);
+    }
+  };
+  const int ch = (g ^ swz(l16)) * 8;
+  const int a_off = (wr * 128 + l16) * BK + ch;
+  const int b_off = BM * BK + (wc * NTW * 16 + l16) * BK + ch;
+  auto read = [&](int u, Frags<NTW>& f) {
+    const uint16_t* base = smem + (u % NST) * STAGE;
+#pragma unroll
+    for (int nt = 0; nt < NTW; ++nt) f.b[nt] = lds8(base + b_off + nt * 16 * BK);
+#pragma unroll
+    for (int mt = 0; mt < 8; ++mt) f.a[mt] = lds8(base + a_off + mt * 16 * BK);
+  };
+  f32x4_t acc[8][NTW];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < NTW; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  auto wait_bar = [&](auto outstanding_stages) {
+    constexpr int W = decltype(outstanding_stages)::value * 2 * RND;
+    if constexpr (W == 8) asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    if constexpr (W == 4) asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    if constexpr (W == 0) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  };
+  auto step = [&](auto kind, int u, Frags<NTW>& cur, Frags<NTW>& nxt) {
+    constexpr int KIND = decltype(kind)::value;
+    if constexpr (KIND == 3) issue(u + 3);
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < NTW; ++nt) acc[mt][nt] = mfma16(cur.b[nt], cur.a[mt], acc[mt][nt]);
+    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (KIND > 0) wait_bar(std::integral_constant<int, KIND - 1>{});
+    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (KIND > 0) read(u + 1, nxt);
+#pragma unroll
+    for (int mt = 4; mt < 8; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < NTW; ++nt) acc[mt][nt] = mfma16(cur.b[nt], cur.a[mt], acc[mt][nt]);
+    if constexpr (KIND > 0) {
+#pragma unroll
+      for (int i = 0; i < 12; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      }
+      __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  auto finish_tile = [&](int u_next) {  // u_next = first step of the next tile
+    const int j = u_next / nk - 1;
+    int m0, n0;
+    tile_coords(j, m0, n0);
+    // the slot of the step just consumed is free: the others hold the next tile's stages
+    epilogue_chunked<EPI>(acc, ep, bias_lds, smem + ((u_next - 1) % NST) * STAGE, M, N, m0, n0, wr, wc, l16, g);
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int jj = 0; jj < NTW; ++jj) acc[i][jj] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  };
+  using K3 = std::integral_constant<int, 3>;
+  using K2 = std::integral_constant<int, 2>;
+  using K1 = std::integral_constant<int, 1>;
+  using K0 = std::integral_constant<int, 0>;
+
+  issue(0);
+  issue(1);
+  if (total > 2) {
+    issue(2);
+    wait_bar(std::integral_constant<int, 2>{});
+  } else {
+    wait_bar(std::integral_constant<int, 1>{});
+  }
+  __builtin_amdgcn_sched_barrier(0);
+  Frags<NTW> f0, f1;
+  read(0, f0);
+  int u = 0;
+  for (; u + 4 < total; u += 2) {
+    step(K3{}, u, f0, f1);
+    step(K3{}, u + 1, f1, f0);
+    if ((u + 2) % nk == 0) finish_tile(u + 2);
+  }
+  if (total - u == 4) {
+    step(K3{}, u, f0, f1);
+    step(K2{}, u + 1, f1, f0);
+    u += 2;
+    if (u % nk == 0) finish_tile(u);
+  }
+  step(K1{}, u, f0, f1);
+  step(K0{}, u + 1, f1, f0);
+  finish_tile(u + 2);
+}
+
 size_t jm_gemm_smem() { return (size_t)NST * STAGE * sizeof(uint16_t); }
 
 // returns 0 on success, <0 on unsupported shape
@@ -378,11 +614,38 @@ void launch_nt(const uint16_t* A, long lda, const uint16_t* B, long ldb, int M, 
   gemm_nt_kernel<EPI, WN, ABL><<<nwg, 128 * WN, sm, st>>>(A, lda, B, ldb, M, N, K, ep, g_gemm_group);
 }
 
+int g_num_cus = 0;
+
+template <int EPI>
+void launch_persist(const uint16_t* A, long lda, const uint16_t* B, long ldb, int M, int N, int K,
+                    const GemmEpi& ep, int tiles, hipStream_t st) {
+  const size_t sm = jm_gemm_smem() + (ep.bias ? (size_t)N * sizeof(float) : 0);
+  static size_t attr = 0;
+  if (attr < sm) {
+    (void)hipFuncSetAttribute((const void*)gemm_nt_persist_kernel<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)sm);
+    attr = sm;
+  }
+  if (g_num_cus == 0) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    hipDeviceProp_t prop;
+    (void)hipGetDeviceProperties(&prop, dev);
+    g_num_cus = prop.multiProcessorCount;
+  }
+  int grid = g_num_cus < tiles ? g_num_cus : tiles;
+  grid = (grid + 7) / 8 * 8;  // the XCD slot mapping assumes a multiple of 8
+  gemm_nt_persist_kernel<EPI><<<grid, 512, sm, st>>>(A, lda, B, ldb, M, N, K, ep, g_gemm_group);
+}
+
 template <int EPI>
 void launch_epi(const uint16_t* A, long lda, const uint16_t* B, long ldb, int M, int N, int K, const GemmEpi& ep,
                 int nwg, hipStream_t st) {
-  if (g_gemm_wn == 4)
-    launch_nt<EPI, 4>(A, lda, B, ldb, M, N, K, ep, nwg, st);
+  if constexpr (EPI == EPI_STORE || EPI == EPI_GELU) {
+    if (g_gemm_wn == 5 && N % 8 == 0 && N <= 8192) return launch_persist<EPI>(A, lda, B, ldb, M, N, K, ep, nwg, st);
+  }
+  if (g_gemm_wn == 2)
+    launch_nt<EPI, 2>(A, lda, B, ldb, M, N, K, ep, nwg, st);
   else if (EPI == EPI_STORE && g_gemm_wn == 41)
     launch_nt<EPI, 4, 1>(A, lda, B, ldb, M, N, K, ep, nwg, st);
   else if (EPI == EPI_STORE && g_gemm_wn == 42)
@@ -391,8 +654,8 @@ void launch_epi(const uint16_t* A, long lda, const uint16_t* B, long ldb, int M,
     launch_nt<EPI, 4, 4>(A, lda, B, ldb, M, N, K, ep, nwg, st);
   else if (EPI == EPI_STORE && g_gemm_wn == 47)
     launch_nt<EPI, 4, 7>(A, lda, B, ldb, M, N, K, ep, nwg, st);
-  else
-    launch_nt<EPI, 2>(A, lda, B, ldb, M, N, K, ep, nwg, st);
+  else  // 4, and 5 for the epilogues the persistent kernel does not cover
+    launch_nt<EPI, 4>(A, lda, B, ldb, M, N, K, ep, nwg, st);
 }
 
 }  // namespace

@@ -4,7 +4,8 @@
 
 Each config is a list of ``KEY=VALUE`` switches applied to ``ops.prims`` module state between
 rounds (same model, same data, same device -> no cross-process / cross-device variance).
-Supported keys: JMAE_GEMM (auto|blas|ours), JMAE_DGRAD (0|1), JMAE_WGRAD (0|1), JMAE_WGRAD_STREAM (0|1).
+Supported keys: JMAE_GEMM (auto|blas|ours), JMAE_DGRAD (0|1), JMAE_WGRAD (0|1), JMAE_WGRAD_STREAM (0|1),
+GEMM_VARIANT (4|5 = persistent NT kernel).
 Prints per-config median / min ms per step."""
 
 import argparse
@@ -29,6 +30,9 @@ def apply(P, cfg: str):
             P.set_wgrad_stream(v == "1")
         elif k == "JMAE_WGRAD":
             P._WGRAD_OURS = v == "1"
+        elif k == "GEMM_VARIANT":
+            from jumbo_mae_tpu_amd.ops import _ext
+            _ext.load(True).gemm_set_variant(int(v), 8)
         elif k == "JMAE_DEFER_WGRAD":
             P._deferred["enabled"] = v == "1"
         else:
