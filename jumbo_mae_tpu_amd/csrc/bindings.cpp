@@ -6,13 +6,15 @@
 #include <c10/hip/HIPStream.h>
 #include <hip/hip_runtime.h>
 
+#include "jm_api.h"
+
 // ---- kernel entry points (see *.hip)
 int jm_layernorm_fwd(const float* x, long sB, long sT, int B, int T, int D, const float* gamma, const float* beta,
                      float eps, void* y, int out_bf16, float* mean, float* rstd, hipStream_t st);
 int jm_layernorm_bwd(const void* dy, int dy_bf16, const float* x, long sB, long sT, int B, int T, int D,
                      const float* mean, const float* rstd, const float* gamma, float* dx_ptr, long oB, long oT,
                      const float* dres, long rB, long rT, float* dgamma, float* dbeta, int accum_params, float* ws,
-                     hipStream_t st);
+                     const JmLnRes* res, hipStream_t st);
 int jm_layernorm_bwd_blocks(int rows);
 int jm_residual_ln_fwd(const float* x, long sB, long sT, const uint16_t* y, const float* scale, const float* mask,
                        float* x1, long oB, long oT, uint16_t* h, float* mean, float* rstd, int B, int T, int T0,
@@ -25,7 +27,7 @@ int jm_transpose_bf16(const uint16_t* src, uint16_t* dst, int R, int C, hipStrea
 int jm_residual_fwd(const float* x, long sB, long sT, int B, int T, int D, const uint16_t* y, const float* scale,
                     const float* mask, float* out, long oB, long oT, hipStream_t st);
 int jm_residual_bwd(const float* dout, long dB, long dT, const uint16_t* y, const float* scale, const float* mask,
-                    float* dscale, uint16_t* dy, int B, int T, int D, float* dbias, hipStream_t st);
+                    float* dscale, uint16_t* dy, int B, int T, int D, float* dbias, long yB, long yT, hipStream_t st);
 int jm_attn_fwd(const uint16_t* qkv, uint16_t* o, float* lse, int B, int S, int H, int hd, hipStream_t st);
 int jm_attn_bwd(const uint16_t* qkv, const uint16_t* o, const uint16_t* dO, const float* lse, uint16_t* dqkv, int B,
                 int S, int H, int hd, float* dbias_part, hipStream_t st);
@@ -100,9 +102,15 @@ std::vector<torch::Tensor> layernorm_fwd(torch::Tensor x, torch::Tensor gamma, t
   return {y, mean, rstd};
 }
 
-torch::Tensor layernorm_bwd(torch::Tensor dy, torch::Tensor x, torch::Tensor mean, torch::Tensor rstd,
-                            torch::Tensor gamma, torch::Tensor dgamma, torch::Tensor dbeta, bool accum,
-                            c10::optional<torch::Tensor> dres, c10::optional<torch::Tensor> out) {
+// res_*: optional fused residual backward of the consumer of dx (see JmLnRes); returns [dx] or
+// [dx, dy_res] (dy_res written into res_out, a [B, T - T0, D] view, or a new [B*(T-T0), D] tensor)
+std::vector<torch::Tensor> layernorm_bwd(torch::Tensor dy, torch::Tensor x, torch::Tensor mean, torch::Tensor rstd,
+                                         torch::Tensor gamma, torch::Tensor dgamma, torch::Tensor dbeta, bool accum,
+                                         c10::optional<torch::Tensor> dres, c10::optional<torch::Tensor> out,
+                                         c10::optional<torch::Tensor> res_y, c10::optional<torch::Tensor> res_scale,
+                                         c10::optional<torch::Tensor> res_mask, c10::optional<torch::Tensor> res_dscale,
+                                         c10::optional<torch::Tensor> res_dbias, int64_t res_T0,
+                                         c10::optional<torch::Tensor> res_out) {
   CHECK_CONTIG(dy);
   TORCH_CHECK(x.dim() == 3 && x.stride(2) == 1, "x must be [B,T,D]");
   const int B = x.size(0), T = x.size(1), D = x.size(2);
@@ -124,13 +132,45 @@ torch::Tensor layernorm_bwd(torch::Tensor dy, torch::Tensor x, torch::Tensor mea
   }
   const bool dyb = dy.scalar_type() == torch::kBFloat16;
   TORCH_CHECK(dyb || dy.scalar_type() == torch::kFloat32, "dy dtype");
-  auto ws = torch::empty({accum ? (long)jm_layernorm_bwd_blocks(B * T) * 2 * D : 1}, x.options());
+  const bool has_res = res_y.has_value() && res_y->defined();
+  JmLnRes res{};
+  torch::Tensor dyr;
+  if (has_res) {
+    const int Tr = T - (int)res_T0;
+    TORCH_CHECK(res_T0 >= 0 && Tr > 0, "res_T0");
+    const auto& y = *res_y;
+    CHECK_DT(y, torch::kBFloat16);
+    long yB, yT;
+    if (y.dim() == 3) {  // [B, Tr, D] view
+      TORCH_CHECK(y.size(0) == B && y.size(1) == Tr && y.size(2) == D && y.stride(2) == 1, "res_y view");
+      yB = y.stride(0);
+      yT = y.stride(1);
+    } else {
+      TORCH_CHECK(y.is_contiguous() && y.numel() == (long)B * Tr * D, "res_y shape");
+      yB = (long)Tr * D;
+      yT = D;
+    }
+    if (res_out.has_value() && res_out->defined()) {  // same view layout as y (e.g. rows of a shared buffer)
+      dyr = *res_out;
+      CHECK_DT(dyr, torch::kBFloat16);
+      TORCH_CHECK(dyr.sizes() == y.sizes() && dyr.strides() == y.strides(), "res_out must match res_y's view");
+    } else {
+      TORCH_CHECK(y.is_contiguous(), "res_y view needs res_out");
+      dyr = torch::empty_like(y);
+    }
+    res = JmLnRes{bf(y), bfm(dyr), yB, yT, fopt(res_scale), fopt(res_mask), (int)res_T0, fopt_m(res_dscale),
+                  fopt_m(res_dbias)};
+  }
+  const int NP = has_res ? 4 : 2;
+  auto ws = torch::empty({(accum || has_res) ? (long)jm_layernorm_bwd_blocks(B * T) * NP * D : 1}, x.options());
   check_rc(jm_layernorm_bwd(dy.data_ptr(), dyb, x.data_ptr<float>(), x.stride(0), x.stride(1), B, T, D,
                             mean.data_ptr<float>(), rstd.data_ptr<float>(), gamma.data_ptr<float>(),
                             dx.data_ptr<float>(), dx.stride(0), dx.stride(1), rp, rB, rT, dgamma.data_ptr<float>(),
-                            dbeta.data_ptr<float>(), accum, ws.data_ptr<float>(), stream()),
+                            dbeta.data_ptr<float>(), accum, ws.data_ptr<float>(), has_res ? &res : nullptr,
+                            stream()),
            "layernorm_bwd");
-  return dx;
+  if (has_res) return {dx, dyr};
+  return {dx};
 }
 
 // ------------------------------------------------------------------------------ elementwise
@@ -190,18 +230,49 @@ torch::Tensor residual_fwd(torch::Tensor x, torch::Tensor y, c10::optional<torch
   return out;
 }
 
+// y / out: contiguous [B*T, D] or [B, T, D] views (out must then share y's strides; out given
+// with y absent: its own strides)
 torch::Tensor residual_bwd(torch::Tensor dout, c10::optional<torch::Tensor> y, c10::optional<torch::Tensor> scale,
                            c10::optional<torch::Tensor> mask, c10::optional<torch::Tensor> dscale, py::object ydtype,
-                           c10::optional<torch::Tensor> dbias) {
+                           c10::optional<torch::Tensor> dbias, c10::optional<torch::Tensor> out) {
   TORCH_CHECK(dout.dim() == 3 && dout.stride(2) == 1, "dout must be a [B,T,D] view");
   CHECK_DT(dout, torch::kFloat32);
   const int B = dout.size(0), T = dout.size(1), D = dout.size(2);
   const auto odt = torch::python::detail::py_object_to_dtype(ydtype);
   TORCH_CHECK(odt == torch::kBFloat16, "residual_bwd: y must be bf16");
-  auto dy = torch::empty({(long)B * T, D}, dout.options().dtype(odt));
-  const uint16_t* yp = (y.has_value() && y->defined()) ? bf(*y) : nullptr;
-  check_rc(jm_residual_bwd(dout.data_ptr<float>(), dout.stride(0), dout.stride(1), yp, fopt(scale), fopt(mask),
-                           fopt_m(dscale), bfm(dy), B, T, D, fopt_m(dbias), stream()),
+  const bool has_y = y.has_value() && y->defined();
+  auto strides_of = [&](const torch::Tensor& t, long& sb, long& st_) {
+    if (t.dim() == 3) {
+      TORCH_CHECK(t.size(0) == B && t.size(1) == T && t.size(2) == D && t.stride(2) == 1, "residual_bwd view");
+      sb = t.stride(0);
+      st_ = t.stride(1);
+    } else {
+      TORCH_CHECK(t.is_contiguous() && t.numel() == (long)B * T * D, "residual_bwd shape");
+      sb = (long)T * D;
+      st_ = D;
+    }
+  };
+  long yB = (long)T * D, yT = D;
+  if (has_y) strides_of(*y, yB, yT);
+  torch::Tensor dy;
+  if (out.has_value() && out->defined()) {
+    dy = *out;
+    CHECK_DT(dy, odt);
+    long oB, oT;
+    strides_of(dy, oB, oT);
+    if (has_y) {
+      TORCH_CHECK(oB == yB && oT == yT, "residual_bwd: out must share y's strides");
+    } else {
+      yB = oB;
+      yT = oT;
+    }
+  } else {
+    TORCH_CHECK(yB == (long)T * D && yT == D, "residual_bwd: a strided y needs out");
+    dy = torch::empty({(long)B * T, D}, dout.options().dtype(odt));
+  }
+  check_rc(jm_residual_bwd(dout.data_ptr<float>(), dout.stride(0), dout.stride(1), has_y ? bf(*y) : nullptr,
+                           fopt(scale), fopt(mask), fopt_m(dscale), bfm(dy), B, T, D, fopt_m(dbias), yB, yT,
+                           stream()),
            "residual_bwd");
   return dy;
 }
@@ -438,7 +509,9 @@ PYBIND11_MODULE(_C, m) {
   m.def("layernorm_fwd", &layernorm_fwd);
   m.def("layernorm_bwd", &layernorm_bwd, py::arg("dy"), py::arg("x"), py::arg("mean"), py::arg("rstd"),
         py::arg("gamma"), py::arg("dgamma"), py::arg("dbeta"), py::arg("accum"), py::arg("dres") = py::none(),
-        py::arg("out") = py::none());
+        py::arg("out") = py::none(), py::arg("res_y") = py::none(), py::arg("res_scale") = py::none(),
+        py::arg("res_mask") = py::none(), py::arg("res_dscale") = py::none(), py::arg("res_dbias") = py::none(),
+        py::arg("res_T0") = 0, py::arg("res_out") = py::none());
   m.def("gelu_fwd", &gelu_fwd);
   m.def("gelu_bwd", &gelu_bwd, py::arg("h"), py::arg("da"), py::arg("bias_grad") = py::none());
   m.def("colsum", &colsum);
@@ -448,7 +521,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("residual_fwd", &residual_fwd, py::arg("x"), py::arg("y"), py::arg("scale"), py::arg("mask"),
         py::arg("out") = py::none());
   m.def("residual_bwd", &residual_bwd, py::arg("dout"), py::arg("y"), py::arg("scale"), py::arg("mask"),
-        py::arg("dscale"), py::arg("ydtype"), py::arg("dbias") = py::none());
+        py::arg("dscale"), py::arg("ydtype"), py::arg("dbias") = py::none(), py::arg("out") = py::none());
   m.def("attn_fwd", &attn_fwd);
   m.def("attn_bwd", &attn_bwd, py::arg("dO"), py::arg("qkv"), py::arg("o"), py::arg("lse"), py::arg("heads"),
         py::arg("dbias") = py::none());

@@ -61,7 +61,7 @@ __global__ __launch_bounds__(256) void rowcol_kernel(const void* __restrict__ in
                                                      uint16_t* __restrict__ out, float* __restrict__ acc,
                                                      const float* __restrict__ scale, const float* __restrict__ mask,
                                                      int M, int N, int T, int rows_per_block, long sB, long sT,
-                                                     float* __restrict__ acc2) {
+                                                     float* __restrict__ acc2, long yB, long yT) {
   extern __shared__ __attribute__((aligned(16))) float red_s[];  // [2][<= 2048] block's columns
   // 2-D grid: blockIdx.y picks a chunk of <= 2048 columns, blockIdx.x a slab of rows
   const int c0 = blockIdx.y * 2048;
@@ -110,7 +110,7 @@ __global__ __launch_bounds__(256) void rowcol_kernel(const void* __restrict__ in
               load8(in1 + off, b[u]);
             } else {  // dout is a [B, T, D] view with strides (sB, sT, 1)
               load8((const float*)in0 + (r / T) * sB + (r % T) * sT + col, a[u]);
-              if (scale) load8(in1 + off, b[u]);
+              if (scale) load8(in1 + (r / T) * yB + (r % T) * yT + col, b[u]);
             }
           }
         }
@@ -140,7 +140,7 @@ __global__ __launch_bounds__(256) void rowcol_kernel(const void* __restrict__ in
               if (scale) s[j] += md * b[u][j];
               s2[j] += bf2f(f2bf(o[j]));  // colsum of the bf16 values the GEMMs consume
             }
-            store8(out + off, o);
+            store8(out + (r / T) * yB + (r % T) * yT + col, o);
           }
         }
       }
@@ -198,7 +198,11 @@ int grid_for(long work, int per_thread_items = 1) {
 template <int MODE>
 void launch_rowcol(const void* in0, const uint16_t* in1, uint16_t* out, float* acc, const float* scale,
                    const float* mask, int M, int N, int T, hipStream_t st, long sB = 0, long sT = 0,
-                   float* acc2 = nullptr) {
+                   float* acc2 = nullptr, long yB = -1, long yT = -1) {
+  if (yB < 0) {  // y / out contiguous [M, N]
+    yB = (long)T * N;
+    yT = N;
+  }
   // 2-D grid: column chunks of 2048 x row slabs; each row-slot walks >= 16 rows, ~2048 blocks
   // in total so the per-block column atomics stay cheap
   const int ncol = (N + 2047) / 2048;
@@ -215,7 +219,7 @@ void launch_rowcol(const void* in0, const uint16_t* in1, uint16_t* out, float* a
   if (nb < 1) nb = 1;
   const size_t smem = (acc || acc2) ? 4096 * sizeof(float) : 0;
   rowcol_kernel<MODE><<<dim3(nb, ncol), 256, smem, st>>>(in0, in1, out, acc, scale, mask, M, N, T, rows_per_block,
-                                                          sB, sT, acc2);
+                                                          sB, sT, acc2, yB, yT);
 }
 
 }  // namespace
@@ -248,9 +252,9 @@ int jm_residual_fwd(const float* x, long sB, long sT, int B, int T, int D, const
 }
 
 int jm_residual_bwd(const float* dout, long dB, long dT, const uint16_t* y, const float* scale, const float* mask,
-                    float* dscale, uint16_t* dy, int B, int T, int D, float* dbias, hipStream_t st) {
+                    float* dscale, uint16_t* dy, int B, int T, int D, float* dbias, long yB, long yT, hipStream_t st) {
   if (D % 8) return -1;
-  launch_rowcol<2>(dout, y, dy, dscale, scale, mask, B * T, D, T, st, dB, dT, dbias);
+  launch_rowcol<2>(dout, y, dy, dscale, scale, mask, B * T, D, T, st, dB, dT, dbias, yB, yT);
   return 0;
 }
 

@@ -11,6 +11,7 @@
 // grid-stride row loop, then across the block's waves with LDS float atomics, then ONE global
 // atomicAdd per column per block straight into the flat fp32 gradient buffer.
 #include "common.h"
+#include "jm_api.h"
 
 namespace {
 
@@ -162,33 +163,54 @@ struct LnBwdIO {
   long rB, rT;
 };
 
-template <int V, typename TI>
+// Optional fused residual backward of the branch that FEEDS on dx (the next op of the backward
+// pass): rows t >= T0 of the LN's [B, T] grid are residual targets,
+//   dyr(b, t) = bf16(mask[b] * scale * dx(b, t))        at y/dy + b * yB + (t - T0) * yT,
+//   dscale += colsum(mask * dx * y),  dbias += colsum(dyr)   (bias of the Dense that produced y).
+// Replaces a separate residual_bwd pass that re-read dx from HBM.
+struct LnResIO {
+  const uint16_t* y;
+  uint16_t* dy;
+  long yB, yT;
+  const float* scale;
+  const float* mask;
+  int T0;
+};
+
+// partial rows in ws: [dgamma | dbeta] (NP = 2) or [dgamma | dbeta | dscale | dbias] (NP = 4)
+template <int V, typename TI, bool RES>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(const TI* __restrict__ dy, const float* __restrict__ x,
                                                      long sB, long sT, int T, int rows, int D,
                                                      const float* __restrict__ mean, const float* __restrict__ rstd,
-                                                     const float* __restrict__ gamma, LnBwdIO io,
-                                                     float* __restrict__ dgamma, float* __restrict__ dbeta,
-                                                     int accum_params) {
-  extern __shared__ __attribute__((aligned(16))) float red[];  // [2*D]
+                                                     const float* __restrict__ gamma, LnBwdIO io, LnResIO rio,
+                                                     float* __restrict__ ws, int accum_params) {
+  constexpr int NP = RES ? 4 : 2;
+  extern __shared__ __attribute__((aligned(16))) float red[];  // [NP*D]
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  if (accum_params) {
-    for (int i = threadIdx.x; i < 2 * D; i += 256) red[i] = 0.f;
-    __syncthreads();
-  }
-  float dg[V][4], db[V][4], gg[V][4];
+  const bool partials = accum_params || RES;
+  float acc[NP][V][4], gg[V][4], sc[V][4];
 #pragma unroll
   for (int i = 0; i < V; ++i) {
     const int col = (i * 64 + lane) * 4;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) dg[i][j] = db[i][j] = 0.f;
-    if (col < D) load4(gamma + col, gg[i]);
+    for (int j = 0; j < 4; ++j) {
+#pragma unroll
+      for (int k = 0; k < NP; ++k) acc[k][i][j] = 0.f;
+      sc[i][j] = 1.f;
+    }
+    if (col < D) {
+      load4(gamma + col, gg[i]);
+      if (RES && rio.scale) load4(rio.scale + col, sc[i]);
+    }
   }
   for (int row = blockIdx.x * 4 + wave; row < rows; row += gridDim.x * 4) {
     const int b = row / T, t = row - b * T;
     const float* xr = x + b * sB + t * sT;
     const TI* dyr = dy + (long)row * D;
     const float mu = mean[row], rs = rstd[row];
-    float xh[V][4], g[V][4];
+    const bool rrow = RES && t >= rio.T0;
+    const long yoff = RES ? b * rio.yB + (long)(t - rio.T0) * rio.yT : 0;
+    float xh[V][4], g[V][4], yv[V][4];
     float sg = 0.f, sgx = 0.f;
 #pragma unroll
     for (int i = 0; i < V; ++i) {
@@ -197,14 +219,15 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const TI* __restrict__ dy, 
         float xv[4], dv[4];
         load4(xr + col, xv);
         load4(dyr + col, dv);
+        if (RES && rrow && rio.scale) load4(rio.y + yoff + col, yv[i]);
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           xh[i][j] = (xv[j] - mu) * rs;
           g[i][j] = dv[j] * gg[i][j];
           sg += g[i][j];
           sgx += g[i][j] * xh[i][j];
-          dg[i][j] += dv[j] * xh[i][j];
-          db[i][j] += dv[j];
+          acc[0][i][j] += dv[j] * xh[i][j];
+          acc[1][i][j] += dv[j];
         }
       } else {
 #pragma unroll
@@ -215,6 +238,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const TI* __restrict__ dy, 
     sgx = wave_sum(sgx) / D;
     float* dxr = io.dx + b * io.oB + t * io.oT;
     const float* rr = io.dres ? io.dres + b * io.rB + t * io.rT : nullptr;
+    const float m = (RES && rio.mask) ? rio.mask[b] : 1.f;
 #pragma unroll
     for (int i = 0; i < V; ++i) {
       const int col = (i * 64 + lane) * 4;
@@ -224,51 +248,62 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const TI* __restrict__ dy, 
 #pragma unroll
         for (int j = 0; j < 4; ++j) o[j] = rs * (g[i][j] - sg - xh[i][j] * sgx) + rv[j];
         store4(dxr + col, o);
+        if (RES && rrow) {
+          float d[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const float md = m * o[j];
+            d[j] = md * sc[i][j];
+            if (rio.scale) acc[2][i][j] += md * yv[i][j];
+            acc[3 % NP][i][j] += bf2f(f2bf(d[j]));  // colsum of the bf16 values the GEMMs consume
+          }
+          store4(rio.dy + yoff + col, d);
+        }
       }
     }
   }
-  if (!accum_params) return;
+  if (!partials) return;
   // merge the 4 waves' partials through LDS in turn (float4, conflict-free, no atomics), then
-  // one coalesced store of the block partial [dgamma | dbeta] into the workspace row
+  // one coalesced store of the block partial row into the workspace
   for (int w = 0; w < 4; ++w) {
     if (wave == w) {
 #pragma unroll
       for (int i = 0; i < V; ++i) {
         const int col = (i * 64 + lane) * 4;
         if (col < D) {
-          float a[4], c[4];
-          if (w == 0) {
-            a[0] = a[1] = a[2] = a[3] = 0.f;
-            c[0] = c[1] = c[2] = c[3] = 0.f;
-          } else {
-            load4(red + col, a);
-            load4(red + D + col, c);
-          }
 #pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            a[j] += dg[i][j];
-            c[j] += db[i][j];
+          for (int k = 0; k < NP; ++k) {
+            float a[4] = {0.f, 0.f, 0.f, 0.f};
+            if (w > 0) load4(red + k * D + col, a);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) a[j] += acc[k][i][j];
+            store4(red + k * D + col, a);
           }
-          store4(red + col, a);
-          store4(red + D + col, c);
         }
       }
     }
     __syncthreads();
   }
-  float* out = dgamma;  // == workspace [gridDim.x, 2*D] on this path
-  for (int i = threadIdx.x * 4; i < 2 * D; i += 256 * 4) {
+  for (int i = threadIdx.x * 4; i < NP * D; i += 256 * 4) {
     float a[4];
     load4(red + i, a);
-    store4(out + (long)blockIdx.x * 2 * D + i, a);
+    store4(ws + (long)blockIdx.x * NP * D + i, a);
   }
 }
 
-// dgamma += sum_b ws[b][0:D], dbeta += sum_b ws[b][D:2D]; grid.y splits the partial rows.
-__global__ __launch_bounds__(256) void ln_param_reduce_kernel(const float* __restrict__ ws, int nb, int D,
-                                                              float* __restrict__ dgamma, float* __restrict__ dbeta) {
+// out_k[c] += sum_b ws[b][k*D + c] for the NP partial vectors (null outputs skipped); grid.y
+// splits the partial rows.
+struct ParamOuts {
+  float* p[4];
+};
+
+__global__ __launch_bounds__(256) void ln_param_reduce_kernel(const float* __restrict__ ws, int nb, int D, int NP,
+                                                              ParamOuts outs) {
   const int i = blockIdx.x * 256 + threadIdx.x;
-  if (i >= 2 * D) return;
+  if (i >= NP * D) return;
+  float* dst = outs.p[i / D];
+  if (dst == nullptr) return;
+  const long ld = (long)NP * D;
   const int per = (nb + gridDim.y - 1) / gridDim.y;
   const int b0 = blockIdx.y * per;
   int b1 = b0 + per;
@@ -276,17 +311,13 @@ __global__ __launch_bounds__(256) void ln_param_reduce_kernel(const float* __res
   float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
   int b = b0;
   for (; b + 3 < b1; b += 4) {
-    s0 += ws[(long)b * 2 * D + i];
-    s1 += ws[(long)(b + 1) * 2 * D + i];
-    s2 += ws[(long)(b + 2) * 2 * D + i];
-    s3 += ws[(long)(b + 3) * 2 * D + i];
+    s0 += ws[(long)b * ld + i];
+    s1 += ws[(long)(b + 1) * ld + i];
+    s2 += ws[(long)(b + 2) * ld + i];
+    s3 += ws[(long)(b + 3) * ld + i];
   }
-  for (; b < b1; ++b) s0 += ws[(long)b * 2 * D + i];
-  const float s = (s0 + s1) + (s2 + s3);
-  if (i < D)
-    atomicAdd(&dgamma[i], s);
-  else
-    atomicAdd(&dbeta[i - D], s);
+  for (; b < b1; ++b) s0 += ws[(long)b * ld + i];
+  atomicAdd(&dst[i % D], (s0 + s1) + (s2 + s3));
 }
 
 template <typename TO>
@@ -301,13 +332,13 @@ void launch_fwd(int V, dim3 grid, hipStream_t st, const float* x, long sB, long 
 #undef JM_LNF
 }
 
-template <typename TI>
+template <typename TI, bool RES>
 void launch_bwd(int V, dim3 grid, size_t smem, hipStream_t st, const TI* dy, const float* x, long sB, long sT,
-                int T, int rows, int D, const float* m, const float* r, const float* g, LnBwdIO dx, float* dg,
-                float* db, int acc) {
-#define JM_LNB(VV)                                                                                  \
-  case VV:                                                                                          \
-    ln_bwd_kernel<VV, TI><<<grid, 256, smem, st>>>(dy, x, sB, sT, T, rows, D, m, r, g, dx, dg, db, acc); \
+                int T, int rows, int D, const float* m, const float* r, const float* g, LnBwdIO dx, LnResIO rio,
+                float* ws, int acc) {
+#define JM_LNB(VV)                                                                                        \
+  case VV:                                                                                                \
+    ln_bwd_kernel<VV, TI, RES><<<grid, 256, smem, st>>>(dy, x, sB, sT, T, rows, D, m, r, g, dx, rio, ws, acc); \
     break;
   switch (V) {
     JM_LNB(1) JM_LNB(2) JM_LNB(3) JM_LNB(4) JM_LNB(6) JM_LNB(8) JM_LNB(9) JM_LNB(12) JM_LNB(16)
@@ -369,23 +400,38 @@ int jm_layernorm_bwd_blocks(int rows) {
 int jm_layernorm_bwd(const void* dy, int dy_bf16, const float* x, long sB, long sT, int B, int T, int D,
                      const float* mean, const float* rstd, const float* gamma, float* dx_ptr, long oB, long oT,
                      const float* dres, long rB, long rT, float* dgamma, float* dbeta, int accum_params, float* ws,
-                     hipStream_t st) {
+                     const JmLnRes* res, hipStream_t st) {
   const LnBwdIO dx{dx_ptr, oB, oT, dres, rB, rT};
   const int V = pick_v(D);
   if (V < 0 || (D % 4) != 0) return -1;
   const int rows = B * T;
   const int nb = jm_layernorm_bwd_blocks(rows);
   dim3 grid(nb);
-  const size_t smem = accum_params ? 2 * D * sizeof(float) : 0;
-  if (dy_bf16)
-    launch_bwd<uint16_t>(V, grid, smem, st, (const uint16_t*)dy, x, sB, sT, T, rows, D, mean, rstd, gamma, dx,
-                         ws, nullptr, accum_params);
-  else
-    launch_bwd<float>(V, grid, smem, st, (const float*)dy, x, sB, sT, T, rows, D, mean, rstd, gamma, dx, ws,
-                      nullptr, accum_params);
-  if (accum_params) {
+  const int NP = res ? 4 : 2;
+  const bool partials = accum_params || res;
+  const size_t smem = partials ? NP * D * sizeof(float) : 0;
+  LnResIO rio{nullptr, nullptr, 0, 0, nullptr, nullptr, 0};
+  if (res) rio = LnResIO{res->y, res->dy, res->yB, res->yT, res->scale, res->mask, res->T0};
+  if (dy_bf16) {
+    if (res)
+      launch_bwd<uint16_t, true>(V, grid, smem, st, (const uint16_t*)dy, x, sB, sT, T, rows, D, mean, rstd, gamma,
+                                 dx, rio, ws, accum_params);
+    else
+      launch_bwd<uint16_t, false>(V, grid, smem, st, (const uint16_t*)dy, x, sB, sT, T, rows, D, mean, rstd, gamma,
+                                  dx, rio, ws, accum_params);
+  } else {
+    if (res)
+      launch_bwd<float, true>(V, grid, smem, st, (const float*)dy, x, sB, sT, T, rows, D, mean, rstd, gamma, dx, rio,
+                              ws, accum_params);
+    else
+      launch_bwd<float, false>(V, grid, smem, st, (const float*)dy, x, sB, sT, T, rows, D, mean, rstd, gamma, dx, rio,
+                               ws, accum_params);
+  }
+  if (partials) {
+    ParamOuts outs{{accum_params ? dgamma : nullptr, accum_params ? dbeta : nullptr,
+                    res ? res->dscale : nullptr, res ? res->dbias : nullptr}};
     const int ysplit = nb >= 64 ? 16 : 1;
-    ln_param_reduce_kernel<<<dim3((2 * D + 255) / 256, ysplit), 256, 0, st>>>(ws, nb, D, dgamma, dbeta);
+    ln_param_reduce_kernel<<<dim3((NP * D + 255) / 256, ysplit), 256, 0, st>>>(ws, nb, D, NP, outs);
   }
   return 0;
 }

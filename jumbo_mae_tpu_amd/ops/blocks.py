@@ -100,10 +100,9 @@ class JumboBlockFn(torch.autograd.Function):
         dt = h1.dtype
         dx2 = dx2.contiguous()
         dx1 = torch.empty_like(dx2)
-        # ---- patch branch: dx1[:, C:] = dx2[:, C:] + LN2'(FF'(s2 * dp2 * dx2[:, C:]))
-        dfy, bd = P.residual_bwd(dx2[:, C:], fy, layer.scale2, m2, dt, layer.ff.w2.b)
-        dhp = _ff_bwd(layer.ff, dfy, hp, fpre, fg, bd)
-        P.ln_bwd(dhp, x1[:, C:], mup, rsp, layer.norm2.g, layer.norm2.b, dres=dx2[:, C:], out=dx1[:, C:])
+        a3 = a.view(B, S, D)
+        da = torch.empty_like(a)
+        da3 = da.view(B, S, D)
         # ---- jumbo branch: d hc = dx2_cls + JumboMLP'(s3 * dp3 * dx2_cls); dx1_cls = LN3'(d hc)
         dcls = dx2[:, :C].reshape(B, 1, J)
         djy, bd = P.residual_bwd(dcls, jy, layer.scale3, m3, dt, layer.jumbo_mlp.w2.b)
@@ -111,8 +110,18 @@ class JumboBlockFn(torch.autograd.Function):
         dhc = dcls.reshape(B, J) + dhcb.float()
         P.ln_bwd(dhc, x1[:, :C].reshape(B, 1, J), muc, rsc, layer.norm3.g, layer.norm3.b,
                  out=dx1[:, :C].reshape(B, 1, J))
+        # attention-residual backward of the CLS rows (the patch rows ride on LN2' below, which
+        # also marks scale1 ready: it must come last)
+        P.residual_bwd(dx1[:, :C], a3[:, :C], layer.scale1, m1, dt, layer.attn.wo_b, out=da3[:, :C],
+                       mark_ready=False)
+        # ---- patch branch: dx1[:, C:] = dx2[:, C:] + LN2'(FF'(s2 * dp2 * dx2[:, C:]))
+        dfy, bd = P.residual_bwd(dx2[:, C:], fy, layer.scale2, m2, dt, layer.ff.w2.b)
+        dhp = _ff_bwd(layer.ff, dfy, hp, fpre, fg, bd)
+        # ... and the attention-residual backward of those rows in the same pass
+        _, _, bd = P.ln_bwd(dhp, x1[:, C:], mup, rsp, layer.norm2.g, layer.norm2.b, dres=dx2[:, C:],
+                            out=dx1[:, C:],
+                            res=P.ResSpec(a3[:, C:], layer.scale1, m1, layer.attn.wo_b, 0, da3[:, C:]))
         # ---- attention branch: dx = dx1 + LN1'(Attn'(s1 * dp1 * dx1))
-        da, bd = P.residual_bwd(dx1, a, layer.scale1, m1, dt, layer.attn.wo_b)
         dh1 = _attn_bwd(layer.attn, da, h1, qkv, o, lse, B, S, bd)
         dx = P.ln_bwd(dh1, x, mu1, rs1, layer.norm1.g, layer.norm1.b, dres=dx1, out=dx1)
         return dx, None, None, None, None, None
@@ -148,8 +157,9 @@ class ViTBlockFn(torch.autograd.Function):
         dx2 = dx2.contiguous()
         dfy, bd = P.residual_bwd(dx2, fy, layer.scale2, m2, dt, layer.ff.w2.b)
         dh2 = _ff_bwd(layer.ff, dfy, h2, fpre, fg, bd)
-        dx1 = P.ln_bwd(dh2, x1, mu2, rs2, layer.norm2.g, layer.norm2.b, dres=dx2)  # never write autograd's dx2
-        da, bd = P.residual_bwd(dx1, a, layer.scale1, m1, dt, layer.attn.wo_b)
+        # LN2' with the attention-residual backward of its dx fused in (never write autograd's dx2)
+        dx1, da, bd = P.ln_bwd(dh2, x1, mu2, rs2, layer.norm2.g, layer.norm2.b, dres=dx2,
+                               res=P.ResSpec(a, layer.scale1, m1, layer.attn.wo_b))
         dh1 = _attn_bwd(layer.attn, da, h1, qkv, o, lse, B, S, bd)
         dx = P.ln_bwd(dh1, x, mu1, rs1, layer.norm1.g, layer.norm1.b, dres=dx1, out=dx1)
         return dx, None, None, None, None

@@ -14,6 +14,8 @@ from __future__ import annotations
 import math
 import os
 
+from typing import NamedTuple
+
 import torch
 import torch.nn.functional as F
 
@@ -324,14 +326,41 @@ def ln_fwd(x3: torch.Tensor, hg: Handle, hb: Handle, out_dtype):
     return y, mean, rstd
 
 
-def ln_bwd(dy: torch.Tensor, x3: torch.Tensor, mean, rstd, hg: Handle, hb: Handle, dres=None, out=None):
+_FUSE_LN_RES = os.environ.get("JMAE_FUSE_LN_RES", "1") == "1"  # A/B switch (tools/ab_bench.py)
+
+
+class ResSpec(NamedTuple):
+    """Residual backward that consumes a LayerNorm backward's dx (fused into it by ``ln_bwd``):
+    for rows t >= t0, dy = mask[b] * s * dx in bf16; s.grad += colsum(mask * dx * y);
+    hbias.grad += colsum(dy).  ``y`` is the branch output of those rows ([B*(T-t0), D] contiguous
+    or a [B, T-t0, D] view); ``out`` an optional destination view with y's layout."""
+    y: torch.Tensor
+    hs: Handle | None
+    mask: torch.Tensor | None
+    hbias: Handle | None
+    t0: int = 0
+    out: torch.Tensor | None = None
+
+
+def ln_bwd(dy: torch.Tensor, x3: torch.Tensor, mean, rstd, hg: Handle, hb: Handle, dres=None, out=None,
+           res: ResSpec | None = None):
     """dx = LN'(dy) (+ dres) written to ``out`` (a [B,T,D] view) or a new tensor; accumulates
-    dgamma / dbeta."""
+    dgamma / dbeta.  With ``res`` the residual backward of dx's consumer rides on the same pass
+    and (dx, dy_res, bias_done) is returned (the separate pass would re-read dx from HBM)."""
     B, T, D = x3.shape
     dy = dy.contiguous()
     tr = _trainable(hg)
+    fused = res is not None and _FUSE_LN_RES and hip(x3) and res.y.dtype == torch.bfloat16
+    dyr = None
     if hip(x3):
-        dx = _ext.load().layernorm_bwd(dy, x3, mean, rstd, hg.master, hg.grad, hb.grad, tr, dres, out)
+        if fused:
+            hs, hbias = res.hs, res.hbias
+            dx, dyr = _ext.load().layernorm_bwd(
+                dy, x3, mean, rstd, hg.master, hg.grad, hb.grad, tr, dres, out, res.y,
+                hs.master if hs is not None else None, res.mask, hs.grad if _trainable(hs) else None,
+                hbias.grad if _trainable(hbias) else None, res.t0, res.out)
+        else:
+            dx = _ext.load().layernorm_bwd(dy, x3, mean, rstd, hg.master, hg.grad, hb.grad, tr, dres, out)[0]
     else:
         xf = x3.reshape(B * T, D).float()
         xhat = (xf - mean[:, None]) * rstd[:, None]
@@ -350,7 +379,14 @@ def ln_bwd(dy: torch.Tensor, x3: torch.Tensor, mean, rstd, hg: Handle, hb: Handl
     if tr:
         hg.ready()
         hb.ready()
-    return dx
+    if res is None:
+        return dx
+    if fused:
+        if _trainable(res.hs):
+            res.hs.ready()
+        return dx, dyr, _trainable(res.hbias)
+    dyr, done = residual_bwd(dx[:, res.t0:], res.y, res.hs, res.mask, res.y.dtype, res.hbias, out=res.out)
+    return dx, dyr, done
 
 
 # ------------------------------------------------------------------------------ residual
@@ -385,19 +421,17 @@ def residual_ln_fwd(x3: torch.Tensor, y2: torch.Tensor, hs: Handle | None, mask,
 
 
 def residual_bwd(dout3: torch.Tensor, y2: torch.Tensor | None, hs: Handle | None, mask, ydtype,
-                 hbias: Handle | None = None):
+                 hbias: Handle | None = None, out: torch.Tensor | None = None, mark_ready: bool = True):
     """dy = mask[b] * s * dout (in ``ydtype``); ds += sum mask*dout*y.  When ``hbias`` (the bias of
     the Dense that produced y) is given, its gradient colsum(dy) is fused into the same pass.
-    Returns (dy, bias_done)."""
+    ``y2``: [B*T, D] or a [B, T, D] view; ``out``: optional destination view with y2's layout.
+    ``mark_ready=False`` leaves s's reducer readiness to a later contributor.  Returns (dy, bias_done)."""
     B, T, D = dout3.shape
     bg = hbias.grad if _trainable(hbias) else None
     if hip(dout3) and ydtype == torch.bfloat16 and (hs is not None or mask is not None or bg is not None):
         dy = _ext.load().residual_bwd(dout3, y2, hs.master if hs is not None else None, mask,
-                                      hs.grad if _trainable(hs) else None, ydtype, bg)
+                                      hs.grad if _trainable(hs) else None, ydtype, bg, out)
         done = bg is not None
-    elif hs is None and mask is None:
-        dy = dout3.reshape(B * T, D).to(ydtype)
-        done = False
     else:
         d = dout3.float()
         if mask is not None:
@@ -406,9 +440,14 @@ def residual_bwd(dout3: torch.Tensor, y2: torch.Tensor | None, hs: Handle | None
             if _trainable(hs):
                 hs.grad.add_((d * y2.float().reshape(B, T, D)).sum((0, 1)))
             d = d * hs.master
-        dy = d.reshape(B * T, D).to(ydtype)
+        dy = d.to(ydtype)
+        if out is not None:
+            out.copy_(dy.reshape(out.shape))
+            dy = out
+        else:
+            dy = dy.reshape(B * T, D)
         done = False
-    if _trainable(hs):
+    if mark_ready and _trainable(hs):
         hs.ready()
     return dy, done
 

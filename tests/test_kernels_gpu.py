@@ -36,7 +36,7 @@ def test_layernorm(ext, D, out_dtype):
     dy = torch.randn_like(y)
     dg = torch.zeros(D, device="cuda")
     db = torch.zeros(D, device="cuda")
-    dx = ext.layernorm_bwd(dy, x, mean, rstd, g, dg, db, True)
+    dx = ext.layernorm_bwd(dy, x, mean, rstd, g, dg, db, True)[0]
     yr.backward(dy.double())
     assert rel(dx.reshape(-1, D), xr.grad.reshape(-1, D)) < 1e-4
     assert rel(dg, gr.grad) < 1e-4
@@ -289,3 +289,47 @@ def test_gemm_nt_splitk(ext, M, N, K, S):
     out = ext.gemm_nt_splitk(x, w, b, S)
     ref = x.float() @ w.float().t() + b
     assert rel(out, ref) < 1e-2
+
+
+@pytest.mark.parametrize("T0,view_y,with_scale", [(0, False, True), (3, False, True), (0, True, True),
+                                                  (3, True, False)])
+def test_layernorm_bwd_fused_residual(ext, T0, view_y, with_scale):
+    """LN backward with the consumer's residual backward fused in == layernorm_bwd followed by
+    residual_bwd on the rows t >= T0 (y as a contiguous slab or a strided view into a buffer)."""
+    torch.manual_seed(0)
+    B, T, D = 6, 52, 1024
+    x = torch.randn(B, T, D, device="cuda") * 2
+    g, bt = torch.rand(D, device="cuda") + 0.5, torch.randn(D, device="cuda")
+    _, mean, rstd = ext.layernorm_fwd(x, g, bt, 1e-6, torch.bfloat16)
+    dy = torch.randn(B * T, D, device="cuda").bfloat16()
+    dres = torch.randn(B, T, D, device="cuda")
+    Tr = T - T0
+    s = torch.rand(D, device="cuda") if with_scale else None
+    mask = (torch.rand(B, device="cuda") > 0.3).float() / 0.7
+    if view_y:
+        ybuf = torch.randn(B, T + 2, D, device="cuda").bfloat16()
+        y = ybuf[:, 2:2 + Tr]
+        obuf = torch.zeros_like(ybuf)
+        out = obuf[:, 2:2 + Tr]
+    else:
+        y = torch.randn(B * Tr, D, device="cuda").bfloat16()
+        out = None
+    z = lambda: torch.zeros(D, device="cuda")  # noqa: E731
+    dg1, db1, ds1, dbi1 = z(), z(), z(), z()
+    dx1, dyr = ext.layernorm_bwd(dy, x, mean, rstd, g, dg1, db1, True, dres, None, y, s, mask,
+                                 ds1 if with_scale else None, dbi1, T0, out)
+    dg2, db2, ds2, dbi2 = z(), z(), z(), z()
+    dx2 = ext.layernorm_bwd(dy, x, mean, rstd, g, dg2, db2, True, dres)[0]
+    assert torch.equal(dx1, dx2)
+    assert rel(dg1, dg2) < 1e-5 and rel(db1, db2) < 1e-5
+    if view_y:
+        o2 = torch.zeros_like(ybuf)
+        ref = ext.residual_bwd(dx2[:, T0:], y, s, mask, ds2 if with_scale else None, torch.bfloat16, dbi2,
+                               o2[:, 2:2 + Tr])
+        assert torch.equal(obuf, o2)  # nothing outside the view touched
+    else:
+        ref = ext.residual_bwd(dx2[:, T0:], y, s, mask, ds2 if with_scale else None, torch.bfloat16, dbi2)
+    assert torch.equal(dyr, ref)
+    if with_scale:
+        assert rel(ds1, ds2) < 1e-5
+    assert rel(dbi1, dbi2) < 1e-5

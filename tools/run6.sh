@@ -9,4 +9,4 @@ tail -3 gpurun_out/pytest_gpu.log
 timeout -k 10 400 python bench.py --steps 10 --warmup 3 > gpurun_out/bench.json 2> gpurun_out/bench.err || exit 1
 cat gpurun_out/bench.json
 cd /tmp
-timeout -k 10 500 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof -o run --output-format csv -- python $R/bench.py --steps 4 --warmup 2 > $R/gpurun_out/prof_bench.log 2>&1
+timeout -k 10 500 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof -o run --output-format csv -- python $R/bench.py --steps 12 --warmup 2 > $R/gpurun_out/prof_bench.log 2>&1

@@ -5,6 +5,6 @@ cd $R
 timeout -k 10 300 python -m jumbo_mae_tpu_amd.csrc.build > gpurun_out/build.log 2>&1 || { echo BUILD FAIL; tail -20 gpurun_out/build.log; exit 1; }
 cd /tmp
 timeout -k 10 200 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT -d $R/gpurun_out/apmc1 -o run --output-format csv -- python $R/tools/attn_bench.py --iters 2 > $R/gpurun_out/apmc1.log 2>&1 || exit 1
-timeout -k 10 200 rocprofv3 --kernel-trace --pmc SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_MFMA SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_LDS_IDX_ACTIVE GRBM_GUI_ACTIVE -d $R/gpurun_out/apmc2 -o run --output-format csv -- python $R/tools/attn_bench.py --iters 2 > $R/gpurun_out/apmc2.log 2>&1 || exit 1
+timeout -k 10 200 rocprofv3 --kernel-trace --pmc SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_MFMA SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_LDS_IDX_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE -d $R/gpurun_out/apmc2 -o run --output-format csv -- python $R/tools/attn_bench.py --iters 2 > $R/gpurun_out/apmc2.log 2>&1 || exit 1
 timeout -k 10 200 rocprofv3 --kernel-trace --pmc TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum -d $R/gpurun_out/apmc3 -o run --output-format csv -- python $R/tools/attn_bench.py --iters 2 > $R/gpurun_out/apmc3.log 2>&1 || exit 1
-echo done
+cd $R && python tools/pmc_summary.py gpurun_out/apmc1/run_counter_collection.csv gpurun_out/apmc2/run_counter_collection.csv gpurun_out/apmc3/run_counter_collection.csv > gpurun_out/apmc_summary.txt; echo done
