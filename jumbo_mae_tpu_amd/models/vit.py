@@ -162,7 +162,7 @@ class JumboLayer:
             self.scale2 = store.handle(store.add(path + ("scale2",), (D,), const_(1e-4), trainable=trainable))
             self.scale3 = store.handle(store.add(path + ("scale3",), (J,), const_(1e-4), trainable=trainable))
 
-    def __call__(self, x, rng=None, det=True):
+    def __call__(self, x, rng=None, det=True, link_in=None, link_out=None):
         B, S, D = x.shape
         C = self.C
         p = self.cfg.droppath
@@ -170,7 +170,7 @@ class JumboLayer:
             m1 = droppath_mask(p, B, rng, x.device, det)
             m3 = droppath_mask(p, B, rng, x.device, det)
             m2 = droppath_mask(p, B, rng, x.device, det)
-            return blocks.jumbo_block(self, x, m1, m2, m3)
+            return blocks.jumbo_block(self, x, m1, m2, m3, link_in, link_out)
         h = self.norm1(x)
         a = self.attn(h, B, S, rng, det)
         x = Fn.residual(x, a, self.scale1, droppath_mask(p, B, rng, x.device, det))
@@ -203,12 +203,12 @@ class ViTLayer:
             self.scale1 = store.handle(store.add(path + ("scale1",), (dim,), const_(1e-4), trainable=trainable))
             self.scale2 = store.handle(store.add(path + ("scale2",), (dim,), const_(1e-4), trainable=trainable))
 
-    def __call__(self, x, rng=None, det=True):
+    def __call__(self, x, rng=None, det=True, link_in=None, link_out=None):
         B, S, D = x.shape
         if use_fused_blocks() and (self.attn.dropout <= 0.0 or det):
             m1 = droppath_mask(self.droppath, B, rng, x.device, det)
             m2 = droppath_mask(self.droppath, B, rng, x.device, det)
-            return blocks.vit_block(self, x, m1, m2)
+            return blocks.vit_block(self, x, m1, m2, link_in, link_out)
         h = self.norm1(x)
         a = self.attn(h, B, S, rng, det)
         x = Fn.residual(x, a, self.scale1, droppath_mask(self.droppath, B, rng, x.device, det))
@@ -281,12 +281,22 @@ class JumboViT:
 
     def blocks(self, x: torch.Tensor, rng=None, det=True) -> torch.Tensor:
         x = _dropout(x, self.cfg.dropout, rng, det)
-        for layer in self.layers:
-            if self.cfg.grad_ckpt and torch.is_grad_enabled():
-                x = torch.utils.checkpoint.checkpoint(layer, x, rng, det, use_reentrant=False)
-            else:
-                x = layer(x, rng, det)
+        return _run_layers(self.layers, x, rng, det, self.cfg.grad_ckpt)
+
+
+def _run_layers(layers, x, rng, det, grad_ckpt):
+    """The layer loop; consecutive fused blocks are chained by ``blocks.Link`` hand-offs (not
+    under activation checkpointing, whose recompute would re-run forwards out of order)."""
+    if grad_ckpt and torch.is_grad_enabled():
+        for layer in layers:
+            x = torch.utils.checkpoint.checkpoint(layer, x, rng, det, use_reentrant=False)
         return x
+    link = None
+    for layer in layers:
+        nxt = blocks.Link() if blocks.LINKS and torch.is_grad_enabled() else None
+        x = layer(x, rng, det, link_in=link, link_out=nxt)
+        link = nxt
+    return x
 
 
 class MAEDecoder:
@@ -311,12 +321,7 @@ class MAEDecoder:
         return self._posemb_cache[key]
 
     def blocks(self, x, rng=None, det=True):
-        for layer in self.layers:
-            if self.cfg.grad_ckpt and torch.is_grad_enabled():
-                x = torch.utils.checkpoint.checkpoint(layer, x, rng, det, use_reentrant=False)
-            else:
-                x = layer(x, rng, det)
-        return x
+        return _run_layers(self.layers, x, rng, det, self.cfg.grad_ckpt)
 
 
 # --------------------------------------------------------------------------------- heads

@@ -18,9 +18,42 @@ ViTBlock = ViTLayer (modeling.py:150-167), the MAE decoder block.
 
 from __future__ import annotations
 
+import os
+
 import torch
 
 from . import prims as P
+
+
+LINKS = os.environ.get("JMAE_LINK_BLOCKS", "1") == "1"  # A/B switch (tools/ab_bench.py)
+
+
+class Link:
+    """Hand-off between two consecutive fused blocks (the model's layer loop creates one per
+    boundary).  The lower block's forward publishes its patch-branch residual (y, s2, mask, bias,
+    t0) as a ``P.ResSpec``; the upper block's backward fuses that residual's backward into its LN1
+    backward -- whose dx IS the lower block's dx2 -- and leaves dy / bias_done here, so the lower
+    block skips a pass that would re-read dx2 from HBM."""
+
+    __slots__ = ("spec", "dy", "done", "dx_key")
+
+    def __init__(self):
+        self.spec = None
+        self.dy = None
+        self.done = False
+        self.dx_key = None
+
+    def take(self, dx2: torch.Tensor):
+        """The fused dy if the upper block produced one for exactly this dx2, else None."""
+        if self.dy is None:
+            return None
+        if self.dx_key != (dx2.data_ptr(), tuple(dx2.shape)):
+            # the upper block already accumulated this residual's parameter gradients: falling
+            # back to a second residual backward would count them twice
+            raise RuntimeError("fused residual hand-off: dx2 is not the upper block's LN1 output")
+        dy, done = self.dy, self.done
+        self.dy = None
+        return dy, done
 
 
 def _attn_fwd(attn, h1, B, S):
@@ -64,7 +97,7 @@ def _ff_handles(ff):
 
 class JumboBlockFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, anchor, layer, m1, m2, m3):
+    def forward(ctx, x, anchor, layer, m1, m2, m3, link_in, link_out):
         B, S, D = x.shape
         C = layer.C
         J = C * D
@@ -87,6 +120,9 @@ class JumboBlockFn(torch.autograd.Function):
         ctx.save_for_backward(x, mu1, rs1, h1, qkv, o, lse, a, x1, muc, rsc, hcb, jpre, jg, jy,
                               hp, mup, rsp, fpre, fg, fy, m1, m2, m3)
         ctx.layer = layer
+        ctx.link_in, ctx.link_out = link_in, link_out
+        if link_out is not None:
+            link_out.spec = P.ResSpec(fy, layer.scale2, m2, layer.ff.w2.b, C)
         return x2
 
     @staticmethod
@@ -115,7 +151,11 @@ class JumboBlockFn(torch.autograd.Function):
         P.residual_bwd(dx1[:, :C], a3[:, :C], layer.scale1, m1, dt, layer.attn.wo_b, out=da3[:, :C],
                        mark_ready=False)
         # ---- patch branch: dx1[:, C:] = dx2[:, C:] + LN2'(FF'(s2 * dp2 * dx2[:, C:]))
-        dfy, bd = P.residual_bwd(dx2[:, C:], fy, layer.scale2, m2, dt, layer.ff.w2.b)
+        fused = ctx.link_out.take(dx2) if ctx.link_out is not None else None
+        if fused is not None:  # computed by the upper block's LN1 backward
+            dfy, bd = fused
+        else:
+            dfy, bd = P.residual_bwd(dx2[:, C:], fy, layer.scale2, m2, dt, layer.ff.w2.b)
         dhp = _ff_bwd(layer.ff, dfy, hp, fpre, fg, bd)
         # ... and the attention-residual backward of those rows in the same pass
         _, _, bd = P.ln_bwd(dhp, x1[:, C:], mup, rsp, layer.norm2.g, layer.norm2.b, dres=dx2[:, C:],
@@ -123,20 +163,32 @@ class JumboBlockFn(torch.autograd.Function):
                             res=P.ResSpec(a3[:, C:], layer.scale1, m1, layer.attn.wo_b, 0, da3[:, C:]))
         # ---- attention branch: dx = dx1 + LN1'(Attn'(s1 * dp1 * dx1))
         dh1 = _attn_bwd(layer.attn, da, h1, qkv, o, lse, B, S, bd)
-        dx = P.ln_bwd(dh1, x, mu1, rs1, layer.norm1.g, layer.norm1.b, dres=dx1, out=dx1)
-        return dx, None, None, None, None, None
+        dx = _ln1_bwd(ctx, dh1, x, mu1, rs1, layer, dx1)
+        return dx, None, None, None, None, None, None, None
 
 
-def jumbo_block(layer, x, m1=None, m2=None, m3=None):
+def _ln1_bwd(ctx, dh1, x, mu1, rs1, layer, dx1):
+    """dx = dx1 + LN1'(dh1) into dx1; with a lower fused block linked, its patch-branch residual
+    backward rides on the same pass (Link)."""
+    li = ctx.link_in
+    if li is None or li.spec is None:
+        return P.ln_bwd(dh1, x, mu1, rs1, layer.norm1.g, layer.norm1.b, dres=dx1, out=dx1)
+    dx, li.dy, li.done = P.ln_bwd(dh1, x, mu1, rs1, layer.norm1.g, layer.norm1.b, dres=dx1, out=dx1, res=li.spec)
+    li.dx_key = (dx.data_ptr(), tuple(dx.shape))
+    li.spec = None
+    return dx
+
+
+def jumbo_block(layer, x, m1=None, m2=None, m3=None, link_in: Link | None = None, link_out: Link | None = None):
     _note_uses(layer.norm1.g, layer.norm1.b, layer.norm2.g, layer.norm2.b, layer.norm3.g, layer.norm3.b,
                layer.scale1, layer.scale2, layer.scale3, *_attn_handles(layer.attn), *_ff_handles(layer.ff),
                *_ff_handles(layer.jumbo_mlp))
-    return JumboBlockFn.apply(x.contiguous(), layer.norm1.g.param, layer, m1, m2, m3)
+    return JumboBlockFn.apply(x.contiguous(), layer.norm1.g.param, layer, m1, m2, m3, link_in, link_out)
 
 
 class ViTBlockFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, anchor, layer, m1, m2):
+    def forward(ctx, x, anchor, layer, m1, m2, link_in, link_out):
         B, S, D = x.shape
         dt = layer.norm1.g.store.compute_dtype
         h1, mu1, rs1 = P.ln_fwd(x, layer.norm1.g, layer.norm1.b, dt)
@@ -146,6 +198,9 @@ class ViTBlockFn(torch.autograd.Function):
         x2 = P.residual_fwd(x1, fy, layer.scale2, m2)
         ctx.save_for_backward(x, mu1, rs1, h1, qkv, o, lse, a, x1, mu2, rs2, h2, fpre, fg, fy, m1, m2)
         ctx.layer = layer
+        ctx.link_in, ctx.link_out = link_in, link_out
+        if link_out is not None:
+            link_out.spec = P.ResSpec(fy, layer.scale2, m2, layer.ff.w2.b, 0)
         return x2
 
     @staticmethod
@@ -155,17 +210,21 @@ class ViTBlockFn(torch.autograd.Function):
         B, S, D = x.shape
         dt = h1.dtype
         dx2 = dx2.contiguous()
-        dfy, bd = P.residual_bwd(dx2, fy, layer.scale2, m2, dt, layer.ff.w2.b)
+        fused = ctx.link_out.take(dx2) if ctx.link_out is not None else None
+        if fused is not None:  # computed by the upper block's LN1 backward
+            dfy, bd = fused
+        else:
+            dfy, bd = P.residual_bwd(dx2, fy, layer.scale2, m2, dt, layer.ff.w2.b)
         dh2 = _ff_bwd(layer.ff, dfy, h2, fpre, fg, bd)
         # LN2' with the attention-residual backward of its dx fused in (never write autograd's dx2)
         dx1, da, bd = P.ln_bwd(dh2, x1, mu2, rs2, layer.norm2.g, layer.norm2.b, dres=dx2,
                                res=P.ResSpec(a, layer.scale1, m1, layer.attn.wo_b))
         dh1 = _attn_bwd(layer.attn, da, h1, qkv, o, lse, B, S, bd)
-        dx = P.ln_bwd(dh1, x, mu1, rs1, layer.norm1.g, layer.norm1.b, dres=dx1, out=dx1)
-        return dx, None, None, None, None
+        dx = _ln1_bwd(ctx, dh1, x, mu1, rs1, layer, dx1)
+        return dx, None, None, None, None, None, None
 
 
-def vit_block(layer, x, m1=None, m2=None):
+def vit_block(layer, x, m1=None, m2=None, link_in: Link | None = None, link_out: Link | None = None):
     _note_uses(layer.norm1.g, layer.norm1.b, layer.norm2.g, layer.norm2.b, layer.scale1, layer.scale2,
                *_attn_handles(layer.attn), *_ff_handles(layer.ff))
-    return ViTBlockFn.apply(x.contiguous(), layer.norm1.g.param, layer, m1, m2)
+    return ViTBlockFn.apply(x.contiguous(), layer.norm1.g.param, layer, m1, m2, link_in, link_out)
