@@ -359,6 +359,157 @@ __global__ __launch_bounds__(128 * WN, 1) void gemm_nt_kernel(const uint16_t* __
     epilogue<EPI, NTW>(acc, ep, M, N, m0 + wr * 128, n0 + wc * NTW * 16, l16, g);
 }
 
+// ------------------------------------------------------------------ 128-byte-row variant
+// Same tile, waves and epilogues as gemm_nt_kernel, but K is staged 64 deep: every operand row of
+// a stage is 128 contiguous bytes, so each global_load_lds piece maps to full 128 B L2 requests
+// (the 64 B rows of the 32-deep ring issue twice the requests for the same bytes).  Two 64 KB
+// slots (the LDS budget), one barrier per 64-deep stage placed in the middle of its second half:
+//   half A: MFMAs of k 0-31 (registers), reads of k 32-63 of the same slot beside them;
+//   half B: MFMAs of k 32-63 rows 0-3 | vmcnt(0) + barrier (stage u+1 landed, slot u free) |
+//           issue stage u+2 into slot u, reads of stage u+1's k 0-31 beside rows 4-7.
+// Chunks of a 128 B row are XOR-swizzled by (row >> 1) & 7: conflict-free ds_read_b128 for both
+// halves (brute-forced over the four lane groups).
+JM_DEVICE int swz64(int row) { return (row >> 1) & 7; }
+
+template <int EPI>
+__global__ __launch_bounds__(512, 1) void gemm_nt64_kernel(const uint16_t* __restrict__ A, long lda,
+                                                           const uint16_t* __restrict__ B, long ldb, int M, int N,
+                                                           int K, GemmEpi ep, int GROUP_M) {
+  constexpr int NW = 8, NTW = 4, BK2 = 64;
+  constexpr int STG = (BM + BN) * BK2;  // elements per slot: 64 KB
+  extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
+  const int tid = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+  const int l16 = lane & 15, g = lane >> 4;
+  const int wr = wave >> 2, wc = wave & 3;
+
+  int m0, n0, split = 0;
+  tile_of(M, N, GROUP_M, m0, n0, EPI == EPI_PARTIAL ? ep.splits : 1, EPI == EPI_PARTIAL ? &split : nullptr);
+  int k_begin = 0;
+  if (EPI == EPI_PARTIAL) {
+    const int ku = K / 64;
+    const int ku0 = split * ku / ep.splits, ku1 = (split + 1) * ku / ep.splits;
+    k_begin = ku0 * 64;
+    K = (ku1 - ku0) * 64;
+  }
+  const __amdgpu_buffer_rsrc_t ra = make_rsrc(A + (long)m0 * lda + k_begin, (long)(M - m0) * lda * 2 - 2L * k_begin);
+  const __amdgpu_buffer_rsrc_t rb = make_rsrc(B + (long)n0 * ldb + k_begin, (long)(N - n0) * ldb * 2 - 2L * k_begin);
+  // one glds piece = 8 rows x 128 B; per operand and stage 32 pieces, 4 per wave
+  uint32_t a_src[4], b_src[4];
+#pragma unroll
+  for (int rr = 0; rr < 4; ++rr) {
+    const int row = rr * 64 + wave * 8 + (lane >> 3);
+    const int c = (lane & 7) ^ swz64(row);
+    a_src[rr] = (uint32_t)((row * lda + c * 8) * 2);
+    b_src[rr] = (uint32_t)((row * ldb + c * 8) * 2);
+  }
+  auto issue = [&](int u) {
+    const uint32_t k0b = u * BK2 * 2;
+    uint16_t* la = smem + (u & 1) * STG;
+    uint16_t* lb = la + BM * BK2;
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) {
+      blds16(ra, a_src[rr], k0b, la + (rr * 64 + wave * 8) * BK2);
+      blds16(rb, b_src[rr], k0b, lb + (rr * 64 + wave * 8) * BK2);
+    }
+  };
+  const int ch0 = ((0 * 4 + g) ^ swz64(l16)) * 8, ch1 = ((1 * 4 + g) ^ swz64(l16)) * 8;
+  const int a_row = (wr * 128 + l16) * BK2, b_row = BM * BK2 + (wc * 64 + l16) * BK2;
+  auto read = [&](int u, auto half, Frags<NTW>& f) {
+    const int ch = decltype(half)::value ? ch1 : ch0;
+    const uint16_t* base = smem + (u & 1) * STG;
+#pragma unroll
+    for (int nt = 0; nt < NTW; ++nt) f.b[nt] = lds8(base + b_row + nt * 16 * BK2 + ch);
+#pragma unroll
+    for (int mt = 0; mt < 8; ++mt) f.a[mt] = lds8(base + a_row + mt * 16 * BK2 + ch);
+  };
+  f32x4_t acc[8][NTW];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < NTW; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  auto mfma_rows = [&](auto lo, const Frags<NTW>& f) {
+    constexpr int R0 = decltype(lo)::value;
+#pragma unroll
+    for (int mt = R0; mt < R0 + 4; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < NTW; ++nt) acc[mt][nt] = mfma16(f.b[nt], f.a[mt], acc[mt][nt]);
+  };
+  auto interleave = [&]() {  // 12 reads beside 16 MFMAs
+#pragma unroll
+    for (int i = 0; i < 12; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+    }
+    __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+  };
+  using H0 = std::integral_constant<int, 0>;
+  using H1 = std::integral_constant<int, 1>;
+  using R0 = std::integral_constant<int, 0>;
+  using R4 = std::integral_constant<int, 4>;
+  // KIND 2: steady (issue u + 2), 1: stage u + 1 exists but nothing left to issue, 0: last stage
+  auto stage = [&](auto kind, int u, Frags<NTW>& f0, Frags<NTW>& f1) {
+    constexpr int KIND = decltype(kind)::value;
+    mfma_rows(R0{}, f0);
+    __builtin_amdgcn_sched_barrier(0);
+    read(u, H1{}, f1);
+    mfma_rows(R4{}, f0);
+    interleave();
+    __builtin_amdgcn_sched_barrier(0);
+    mfma_rows(R0{}, f1);
+    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (KIND > 0) {
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      if constexpr (KIND == 2) issue(u + 2);
+      read(u + 1, H0{}, f0);
+      mfma_rows(R4{}, f1);
+      interleave();
+    } else {
+      mfma_rows(R4{}, f1);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  using K2 = std::integral_constant<int, 2>;
+  using K1 = std::integral_constant<int, 1>;
+  using K0 = std::integral_constant<int, 0>;
+
+  const int nst = K / BK2;  // >= 1 (host checks K % 64 == 0)
+  issue(0);
+  if (nst > 1) {
+    issue(1);
+    asm volatile("s_waitcnt vmcnt(8)\n\ts_barrier" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+  }
+  __builtin_amdgcn_sched_barrier(0);
+  Frags<NTW> f0, f1;
+  read(0, H0{}, f0);
+  int u = 0;
+  for (; u + 2 < nst; ++u) stage(K2{}, u, f0, f1);
+  if (u + 1 < nst) stage(K1{}, u++, f0, f1);
+  stage(K0{}, u, f0, f1);
+
+  if (EPI == EPI_PARTIAL) {
+    float* dst = ep.part + (long)split * M * N;
+#pragma unroll
+    for (int mt = 0; mt < 8; ++mt) {
+      const int m = m0 + wr * 128 + mt * 16 + l16;
+      if (m >= M) continue;
+#pragma unroll
+      for (int nt = 0; nt < NTW; ++nt) {
+        const int n = n0 + wc * NTW * 16 + nt * 16 + 4 * g;
+        if (n >= N) continue;
+        float v[4] = {acc[mt][nt][0], acc[mt][nt][1], acc[mt][nt][2], acc[mt][nt][3]};
+        store4(dst + (long)m * N + n, v);
+      }
+    }
+  } else if (N % 8 == 0)
+    epilogue_lds<EPI, NTW, 512>(acc, ep, smem, M, N, m0, n0, wr, wc, l16, g);
+  else
+    epilogue<EPI, NTW>(acc, ep, M, N, m0 + wr * 128, n0 + wc * NTW * 16, l16, g);
+}
+
 // ------------------------------------------------------------------ persistent variant
 // One workgroup per CU walks its tiles (bid, bid + G, ...) as ONE stream of K steps: the ring's
 // look-ahead loads run straight into the next tile, so a tile's prologue latency is hidden behind
@@ -598,7 +749,8 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_persist_kernel(const uint16_t*
 size_t jm_gemm_smem() { return (size_t)NST * STAGE * sizeof(uint16_t); }
 
 // returns 0 on success, <0 on unsupported shape
-int g_gemm_wn = 4;     // runtime switches for A/B (jm_gemm_set_variant)
+int g_gemm_wn = 6;     // runtime switches for A/B (jm_gemm_set_variant): 6 = 64-deep stages (default),
+                       // 4 = 32-deep ring, 2 = 4 waves, 5 = persistent, 4x = ablations
 int g_gemm_group = 8;
 
 template <int EPI, int WN, int ABL = 0>
@@ -639,8 +791,21 @@ void launch_persist(const uint16_t* A, long lda, const uint16_t* B, long ldb, in
 }
 
 template <int EPI>
+void launch_nt64(const uint16_t* A, long lda, const uint16_t* B, long ldb, int M, int N, int K, const GemmEpi& ep,
+                 int nwg, hipStream_t st) {
+  static bool attr = false;
+  const size_t sm = jm_gemm_smem();  // 2 x 64 KB slots == the 4 x 32 KB ring
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)gemm_nt64_kernel<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
+    attr = true;
+  }
+  gemm_nt64_kernel<EPI><<<nwg, 512, sm, st>>>(A, lda, B, ldb, M, N, K, ep, g_gemm_group);
+}
+
+template <int EPI>
 void launch_epi(const uint16_t* A, long lda, const uint16_t* B, long ldb, int M, int N, int K, const GemmEpi& ep,
                 int nwg, hipStream_t st) {
+  if (g_gemm_wn == 6) return launch_nt64<EPI>(A, lda, B, ldb, M, N, K, ep, nwg, st);
   if constexpr (EPI == EPI_STORE || EPI == EPI_GELU) {
     if (g_gemm_wn == 5 && N % 8 == 0 && N <= 8192) return launch_persist<EPI>(A, lda, B, ldb, M, N, K, ep, nwg, st);
   }

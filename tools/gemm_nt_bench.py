@@ -38,7 +38,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--only", default="")
     ap.add_argument("--kinds", default="fwd,fwd_gelu,dgrad")
-    ap.add_argument("--variant", type=int, default=4, help="waves along N (2 or 4)")
+    ap.add_argument("--variant", type=int, default=6, help="kernel variant (see jm_gemm_set_variant)")
     ap.add_argument("--group", type=int, default=8, help="row tiles per column sweep")
     a = ap.parse_args()
     ext = _ext.load()
