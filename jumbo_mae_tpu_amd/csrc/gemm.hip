@@ -371,13 +371,13 @@ __global__ __launch_bounds__(128 * WN, 1) void gemm_nt_kernel(const uint16_t* __
 // halves (brute-forced over the four lane groups).
 JM_DEVICE int swz64(int row) { return (row >> 1) & 7; }
 
-template <int EPI>
-__global__ __launch_bounds__(512, 1) void gemm_nt64_kernel(const uint16_t* __restrict__ A, long lda,
-                                                           const uint16_t* __restrict__ B, long ldb, int M, int N,
-                                                           int K, GemmEpi ep, int GROUP_M) {
+template <int EPI, bool LATE, bool PRIO>
+__attribute__((always_inline)) JM_DEVICE void nt64_body(const uint16_t* __restrict__ A, long lda,
+                                                        const uint16_t* __restrict__ B, long ldb, int M, int N,
+                                                        int K, const GemmEpi& ep, int GROUP_M, uint16_t* smem) {
   constexpr int NW = 8, NTW = 4, BK2 = 64;
   constexpr int STG = (BM + BN) * BK2;  // elements per slot: 64 KB
-  extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
+
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
   const int l16 = lane & 15, g = lane >> 4;
@@ -458,7 +458,14 @@ __global__ __launch_bounds__(512, 1) void gemm_nt64_kernel(const uint16_t* __res
     __builtin_amdgcn_sched_barrier(0);
     mfma_rows(R0{}, f1);
     __builtin_amdgcn_sched_barrier(0);
-    if constexpr (KIND > 0) {
+    if constexpr (KIND > 0 && LATE) {
+      mfma_rows(R4{}, f1);
+      __builtin_amdgcn_sched_barrier(0);
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      if constexpr (KIND == 2) issue(u + 2);
+      read(u + 1, H0{}, f0);
+    } else if constexpr (KIND > 0) {
       asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);
       if constexpr (KIND == 2) issue(u + 2);
@@ -475,6 +482,7 @@ __global__ __launch_bounds__(512, 1) void gemm_nt64_kernel(const uint16_t* __res
   using K0 = std::integral_constant<int, 0>;
 
   const int nst = K / BK2;  // >= 1 (host checks K % 64 == 0)
+  if (PRIO) __builtin_amdgcn_s_setprio(1);
   issue(0);
   if (nst > 1) {
     issue(1);
@@ -489,6 +497,7 @@ __global__ __launch_bounds__(512, 1) void gemm_nt64_kernel(const uint16_t* __res
   for (; u + 2 < nst; ++u) stage(K2{}, u, f0, f1);
   if (u + 1 < nst) stage(K1{}, u++, f0, f1);
   stage(K0{}, u, f0, f1);
+  if (PRIO) __builtin_amdgcn_s_setprio(0);
 
   if (EPI == EPI_PARTIAL) {
     float* dst = ep.part + (long)split * M * N;
@@ -508,6 +517,22 @@ __global__ __launch_bounds__(512, 1) void gemm_nt64_kernel(const uint16_t* __res
     epilogue_lds<EPI, NTW, 512>(acc, ep, smem, M, N, m0, n0, wr, wc, l16, g);
   else
     epilogue<EPI, NTW>(acc, ep, M, N, m0 + wr * 128, n0 + wc * NTW * 16, l16, g);
+}
+
+// SCHED (A/B): bit 0 = stagger -- waves 4-7 (the SIMD partners of waves 0-3) issue ALL their
+// half-B MFMAs before the barrier and read the next stage after it, so one wave of each SIMD pair
+// has matrix work queued while the other waits; bit 1 = s_setprio 1 for waves 4-7.  The two
+// halves run separately inlined bodies (no live ranges shared across the branch).
+template <int EPI, int SCHED = 0>
+__global__ __launch_bounds__(512, 1) void gemm_nt64_kernel(const uint16_t* __restrict__ A, long lda,
+                                                           const uint16_t* __restrict__ B, long ldb, int M, int N,
+                                                           int K, GemmEpi ep, int GROUP_M) {
+  extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
+  constexpr bool ST = SCHED & 1, PR = (SCHED & 2) != 0;
+  if (SCHED != 0 && __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) >= 4)
+    nt64_body<EPI, ST, PR>(A, lda, B, ldb, M, N, K, ep, GROUP_M, smem);
+  else
+    nt64_body<EPI, false, false>(A, lda, B, ldb, M, N, K, ep, GROUP_M, smem);
 }
 
 // ------------------------------------------------------------------ persistent variant
@@ -790,22 +815,26 @@ void launch_persist(const uint16_t* A, long lda, const uint16_t* B, long ldb, in
   gemm_nt_persist_kernel<EPI><<<grid, 512, sm, st>>>(A, lda, B, ldb, M, N, K, ep, g_gemm_group);
 }
 
-template <int EPI>
+template <int EPI, int SCHED>
 void launch_nt64(const uint16_t* A, long lda, const uint16_t* B, long ldb, int M, int N, int K, const GemmEpi& ep,
                  int nwg, hipStream_t st) {
   static bool attr = false;
   const size_t sm = jm_gemm_smem();  // 2 x 64 KB slots == the 4 x 32 KB ring
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)gemm_nt64_kernel<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
+    (void)hipFuncSetAttribute((const void*)gemm_nt64_kernel<EPI, SCHED>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)sm);
     attr = true;
   }
-  gemm_nt64_kernel<EPI><<<nwg, 512, sm, st>>>(A, lda, B, ldb, M, N, K, ep, g_gemm_group);
+  gemm_nt64_kernel<EPI, SCHED><<<nwg, 512, sm, st>>>(A, lda, B, ldb, M, N, K, ep, g_gemm_group);
 }
 
 template <int EPI>
 void launch_epi(const uint16_t* A, long lda, const uint16_t* B, long ldb, int M, int N, int K, const GemmEpi& ep,
                 int nwg, hipStream_t st) {
-  if (g_gemm_wn == 6) return launch_nt64<EPI>(A, lda, B, ldb, M, N, K, ep, nwg, st);
+  if (g_gemm_wn == 6) return launch_nt64<EPI, 0>(A, lda, B, ldb, M, N, K, ep, nwg, st);
+  if (g_gemm_wn == 7) return launch_nt64<EPI, 1>(A, lda, B, ldb, M, N, K, ep, nwg, st);
+  if (g_gemm_wn == 8) return launch_nt64<EPI, 3>(A, lda, B, ldb, M, N, K, ep, nwg, st);
+  if (g_gemm_wn == 9) return launch_nt64<EPI, 2>(A, lda, B, ldb, M, N, K, ep, nwg, st);
   if constexpr (EPI == EPI_STORE || EPI == EPI_GELU) {
     if (g_gemm_wn == 5 && N % 8 == 0 && N <= 8192) return launch_persist<EPI>(A, lda, B, ldb, M, N, K, ep, nwg, st);
   }

@@ -190,7 +190,7 @@ def test_optimizer_hip_matches_torch(kind, clip):
     assert rel(res[0], res[1]) < 1e-5
 
 
-@pytest.mark.parametrize("variant", [4, 2, 5, 6])
+@pytest.mark.parametrize("variant", [4, 2, 5, 6, 7, 8])
 @pytest.mark.parametrize("M,N,K,gelu", [(512, 256, 64, False), (300, 196, 128, True), (1000, 1536, 512, False),
                                         (257, 260, 192, True), (16100, 2048, 128, True), (40000, 520, 64, False)])
 def test_gemm_nt(ext, M, N, K, gelu, variant):
