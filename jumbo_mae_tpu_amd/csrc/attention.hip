@@ -721,6 +721,294 @@ __global__ __launch_bounds__(256) void attn_bwd2_kernel(const uint16_t* __restri
   }
 }
 
+// ------------------------------------------------------------------ backward, batched variant
+// attn_bwd2_kernel's layout with the per-key-tile work batched for instruction-level parallelism
+// (the decoder's hd = 32 backward was latency-bound: each 16-query slice ran LDS read -> MFMA ->
+// VALU -> LDS write in series).  Per 64-query chunk a wave now
+//  * loads ONCE the fragments that do not depend on the key tile -- Q / dO rows for S and dP, the
+//    transposed dO / Q fragments of the dV / dK products, lse and delta -- instead of once per key
+//    tile (NKW = 4 key tiles per wave at S = 199);
+//  * per key tile issues the 8 independent S / dP MFMAs back to back, then the softmax-gradient
+//    VALU of all four 16-query slices, then the 8 dV / dK MFMAs;
+//  * masks padded keys through the MFMA accumulator init (-1e30 for keys >= S) instead of a
+//    multiply per score.
+template <int HD, int SP>
+__global__ __launch_bounds__(256) void attn_bwd3_kernel(const uint16_t* __restrict__ qkv,
+                                                        const uint16_t* __restrict__ o,
+                                                        const uint16_t* __restrict__ dO,
+                                                        const float* __restrict__ lse,
+                                                        uint16_t* __restrict__ dqkv, int S, int H, float scale,
+                                                        float* __restrict__ dbp) {
+  constexpr int NW = 4, NTH = 256, QC = 64;
+  constexpr int NT = SP / 16, KK = HD / 32, DT = HD / 16;
+  constexpr int NKW = (NT + NW - 1) / NW;
+  constexpr int NCH = HD / 8;
+  extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
+  uint16_t* Qs = smem;
+  uint16_t* dOs = Qs + SP * HD;
+  uint16_t* Ks = dOs + SP * HD;
+  uint16_t* dSt = Ks + SP * HD;  // [SP][QC]
+  float* lse_s = reinterpret_cast<float*>(dSt + SP * QC);
+  float* delta_s = lse_s + SP;
+  float* bsum = delta_s + SP;
+
+  const int bh = blockIdx.x;
+  const int b = bh / H, h = bh - (bh / H) * H;
+  const long ts = 3L * H * HD;
+  const long os = (long)H * HD;
+  const uint16_t* base = qkv + (long)b * S * ts;
+  const uint16_t* Qg = base + h * HD;
+  const uint16_t* Kg = base + (H + h) * HD;
+  const uint16_t* Vg = base + (2 * H + h) * HD;
+  const uint16_t* Og = o + (long)b * S * os + h * HD;
+  const uint16_t* dOg = dO + (long)b * S * os + h * HD;
+  uint16_t* dQg = dqkv + (long)b * S * ts + h * HD;
+  uint16_t* dKg = dqkv + (long)b * S * ts + (H + h) * HD;
+  uint16_t* dVg = dqkv + (long)b * S * ts + (2 * H + h) * HD;
+
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int l16 = lane & 15, g = lane >> 4;
+
+  bf16x8_t vf[NKW][KK];
+  float kinit[NKW];
+#pragma unroll
+  for (int w = 0; w < NKW; ++w) {
+    const int key = (wave + NW * w) * 16 + l16;
+    kinit[w] = key < S ? 0.f : -1e30f;
+#pragma unroll
+    for (int kk = 0; kk < KK; ++kk) {
+      s16x8_t z = {0, 0, 0, 0, 0, 0, 0, 0};
+      vf[w][kk] = __builtin_bit_cast(bf16x8_t, z);
+      if (key < S) vf[w][kk] = ld8(Vg + (long)key * ts + 32 * kk + 8 * g);
+    }
+  }
+  for (int i = threadIdx.x; i < 3 * HD; i += NTH) bsum[i] = 0.f;
+  for (int i = threadIdx.x; i < SP; i += NTH) {
+    delta_s[i] = 0.f;
+    lse_s[i] = i < S ? lse[((long)b * H + h) * S + i] * LOG2E : INFINITY;
+  }
+  __syncthreads();
+  constexpr int NIT = (SP * NCH + NTH - 1) / NTH;
+  uint4 qv[NIT], kv[NIT], dv[NIT], ov[NIT];
+#pragma unroll
+  for (int it = 0; it < NIT; ++it) {
+    const int i = it * NTH + threadIdx.x;
+    const int r = i / NCH, c = (i % NCH) * 8;
+    qv[it] = kv[it] = dv[it] = ov[it] = make_uint4(0, 0, 0, 0);
+    if (i < SP * NCH && r < S) {
+      qv[it] = *reinterpret_cast<const uint4*>(Qg + r * ts + c);
+      kv[it] = *reinterpret_cast<const uint4*>(Kg + r * ts + c);
+      dv[it] = *reinterpret_cast<const uint4*>(dOg + r * os + c);
+      ov[it] = *reinterpret_cast<const uint4*>(Og + r * os + c);
+    }
+  }
+#pragma unroll
+  for (int it = 0; it < NIT; ++it) {
+    const int i = it * NTH + threadIdx.x;
+    const int r = i / NCH, c = (i % NCH) * 8;
+    if (i < SP * NCH) {
+      const int off = swo<NCH>(r, c);
+      *reinterpret_cast<uint4*>(Qs + off) = qv[it];
+      *reinterpret_cast<uint4*>(Ks + off) = kv[it];
+      *reinterpret_cast<uint4*>(dOs + off) = dv[it];
+      if (r < S) {
+        const uint32_t* ow = reinterpret_cast<const uint32_t*>(&ov[it]);
+        const uint32_t* dw = reinterpret_cast<const uint32_t*>(&dv[it]);
+        float dsum = 0.f;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          dsum += __uint_as_float(ow[j] << 16) * __uint_as_float(dw[j] << 16);
+          dsum += __uint_as_float(ow[j] & 0xffff0000u) * __uint_as_float(dw[j] & 0xffff0000u);
+        }
+        atomicAdd(&delta_s[r], dsum);
+      }
+    }
+  }
+  __syncthreads();
+
+  const float sl2 = scale * LOG2E;
+  int o_frag[KK];
+#pragma unroll
+  for (int kk = 0; kk < KK; ++kk) o_frag[kk] = swo<NCH>(l16, 32 * kk + 8 * g);
+  int o_tr[DT][2];
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt) {
+    o_tr[dt][0] = swo<NCH>(4 * g + (l16 >> 2), dt * 16 + 4 * (l16 & 3));
+    o_tr[dt][1] = swo<NCH>(4 * g + (l16 >> 2) + 16, dt * 16 + 4 * (l16 & 3));
+  }
+  int o_dsw[QC / 16];
+#pragma unroll
+  for (int j = 0; j < QC / 16; ++j) o_dsw[j] = swo<8>(l16, 16 * j + 4 * g);
+  const int krow = 8 * g + (l16 >> 2);
+  int o_dsr[2], o_kt[DT][2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    o_dsr[u] = swo<8>(krow + 4 * u, wave * 16 + 4 * (l16 & 3));
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) o_kt[dt][u] = swo<NCH>(krow + 4 * u, dt * 16 + 4 * (l16 & 3));
+  }
+
+  bf16x8_t kf[NKW][KK];
+  f32x4_t dvacc[NKW][DT], dkacc[NKW][DT];
+#pragma unroll
+  for (int w = 0; w < NKW; ++w) {
+#pragma unroll
+    for (int kk = 0; kk < KK; ++kk) kf[w][kk] = ld8(Ks + (wave + NW * w) * 16 * HD + o_frag[kk]);
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) {
+      dvacc[w][dt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+      dkacc[w][dt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    }
+  }
+
+  for (int qc = 0; qc * QC < SP; ++qc) {
+    const int q0 = qc * QC;
+    const int nr = (SP - q0) >= QC ? 2 : 1;  // 32-query blocks in this chunk (SP % 32 == 0)
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      if (r < nr) {
+        // ---- key-tile independent fragments of this 32-query block
+        const int qb = q0 + 32 * r;
+        bf16x8_t qf[2][KK], dof[2][KK], a_do[DT], a_q[DT];
+        float lv[2][4], dl[2][4];
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh) {
+#pragma unroll
+          for (int kk = 0; kk < KK; ++kk) {
+            qf[hh][kk] = ld8(Qs + (qb + 16 * hh) * HD + o_frag[kk]);
+            dof[hh][kk] = ld8(dOs + (qb + 16 * hh) * HD + o_frag[kk]);
+          }
+          const float4 l4 = *reinterpret_cast<const float4*>(lse_s + qb + 16 * hh + 4 * g);
+          const float4 d4 = *reinterpret_cast<const float4*>(delta_s + qb + 16 * hh + 4 * g);
+          lv[hh][0] = l4.x; lv[hh][1] = l4.y; lv[hh][2] = l4.z; lv[hh][3] = l4.w;
+          dl[hh][0] = d4.x; dl[hh][1] = d4.y; dl[hh][2] = d4.z; dl[hh][3] = d4.w;
+        }
+#pragma unroll
+        for (int dt = 0; dt < DT; ++dt) {
+          a_do[dt] = cat44(tr4(dOs + qb * HD + o_tr[dt][0]), tr4(dOs + qb * HD + o_tr[dt][1]));
+          a_q[dt] = cat44(tr4(Qs + qb * HD + o_tr[dt][0]), tr4(Qs + qb * HD + o_tr[dt][1]));
+        }
+#pragma unroll
+        for (int w = 0; w < NKW; ++w) {
+          const int kt = wave + NW * w;
+          if (kt < NT) {
+            const f32x4_t ki = {kinit[w], kinit[w], kinit[w], kinit[w]};
+            f32x4_t sacc[2], dp[2];
+#pragma unroll
+            for (int hh = 0; hh < 2; ++hh) {
+              sacc[hh] = ki;
+              dp[hh] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+              for (int kk = 0; kk < KK; ++kk) {
+                sacc[hh] = mfma(qf[hh][kk], kf[w][kk], sacc[hh]);
+                dp[hh] = mfma(dof[hh][kk], vf[w][kk], dp[hh]);
+              }
+            }
+            float pf[8], df[8];
+            uint16_t* dsw = dSt + kt * 16 * QC;
+#pragma unroll
+            for (int hh = 0; hh < 2; ++hh) {
+#pragma unroll
+              for (int i = 0; i < 4; ++i) {
+                const float p = __builtin_amdgcn_exp2f(sacc[hh][i] * sl2 - lv[hh][i]);
+                pf[4 * hh + i] = p;
+                df[4 * hh + i] = p * (dp[hh][i] - dl[hh][i]);
+              }
+              uint2 pk;
+              pk.x = pack_bf2(df[4 * hh], df[4 * hh + 1]);
+              pk.y = pack_bf2(df[4 * hh + 2], df[4 * hh + 3]);
+              *reinterpret_cast<uint2*>(dsw + o_dsw[2 * r + hh]) = pk;
+            }
+            const bf16x8_t pb = pack8(pf);
+            const bf16x8_t dsb = pack8(df);
+#pragma unroll
+            for (int dt = 0; dt < DT; ++dt) {
+              dvacc[w][dt] = mfma(a_do[dt], pb, dvacc[w][dt]);
+              dkacc[w][dt] = mfma(a_q[dt], dsb, dkacc[w][dt]);
+            }
+          }
+        }
+      }
+    }
+    __syncthreads();
+    {
+      const int qt = qc * (QC / 16) + wave;
+      if (qt < NT) {
+        f32x4_t dq[DT];
+#pragma unroll
+        for (int dt = 0; dt < DT; ++dt) dq[dt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s2 = 0; s2 < SP / 32; ++s2) {
+          const uint16_t* dsr = dSt + 32 * s2 * QC;
+          const uint16_t* kr = Ks + 32 * s2 * HD;
+          const bf16x8_t bop = cat44(tr4(dsr + o_dsr[0]), tr4(dsr + o_dsr[1]));
+#pragma unroll
+          for (int dt = 0; dt < DT; ++dt) {
+            const bf16x8_t ka = cat44(tr4(kr + o_kt[dt][0]), tr4(kr + o_kt[dt][1]));
+            dq[dt] = mfma(ka, bop, dq[dt]);
+          }
+        }
+        if (dbp != nullptr) {
+#pragma unroll
+          for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              const float v = row16_sum(dq[dt][i]);
+              if (l16 == 0) atomicAdd(&bsum[dt * 16 + 4 * g + i], v * scale);
+            }
+        }
+        const int q = qt * 16 + l16;
+        if (q < S) {
+#pragma unroll
+          for (int dt = 0; dt < DT; ++dt) {
+            float v[4] = {dq[dt][0] * scale, dq[dt][1] * scale, dq[dt][2] * scale, dq[dt][3] * scale};
+            store4(dQg + (long)q * ts + dt * 16 + 4 * g, v);
+          }
+        }
+      }
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int w = 0; w < NKW; ++w) {
+    const int kt = wave + NW * w;
+    const int key = kt * 16 + l16;
+    if (kt < NT && key < S) {
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt) {
+        float kv2[4] = {dkacc[w][dt][0] * scale, dkacc[w][dt][1] * scale, dkacc[w][dt][2] * scale,
+                        dkacc[w][dt][3] * scale};
+        float vv[4] = {dvacc[w][dt][0], dvacc[w][dt][1], dvacc[w][dt][2], dvacc[w][dt][3]};
+        store4(dKg + (long)key * ts + dt * 16 + 4 * g, kv2);
+        store4(dVg + (long)key * ts + dt * 16 + 4 * g, vv);
+      }
+    }
+  }
+  if (dbp != nullptr) {
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        float sk = 0.f, sv = 0.f;
+#pragma unroll
+        for (int w = 0; w < NKW; ++w) {
+          sk += dkacc[w][dt][i];
+          sv += dvacc[w][dt][i];
+        }
+        sk = row16_sum(sk);
+        sv = row16_sum(sv);
+        if (l16 == 0) {
+          const int d = dt * 16 + 4 * g + i;
+          atomicAdd(&bsum[HD + d], sk * scale);
+          atomicAdd(&bsum[2 * HD + d], sv);
+        }
+      }
+    __syncthreads();
+    float* dst = dbp + (long)b * ts + h * HD;
+    for (int i = threadIdx.x; i < 3 * HD; i += NTH) dst[(i / HD) * H * HD + (i % HD)] = bsum[i];
+  }
+}
+
 template <int HD, int SP, bool TR>
 size_t fwd_smem() { return (size_t)(SP * (HD + 8) + (TR ? SP * (HD + 8) : HD * (SP + 8))) * 2; }
 template <int HD, int SP, bool TR>
@@ -729,7 +1017,8 @@ size_t bwd_smem() {
          (2 * SP + 3 * HD) * sizeof(float);
 }
 
-int g_use_tr = 2;  // runtime switch: 2 = compact backward (bwd2) + TR forward, 1 = TR, 0 = transposed images
+int g_use_tr = 3;  // runtime switch: 3 = batched backward (bwd3) for hd 32, 2 = compact backward (bwd2) + TR
+                   // forward, 1 = TR, 0 = transposed images
 
 template <int HD, int SP, bool TR>
 int run_t(bool fwd, const uint16_t* qkv, const uint16_t* o, const uint16_t* dO, const float* lse_in, uint16_t* out,
@@ -762,6 +1051,18 @@ int run_bwd2(const uint16_t* qkv, const uint16_t* o, const uint16_t* dO, const f
                               (int)sm);
     attr_set = true;
   }
+  if constexpr (HD == 32) {
+    if (g_use_tr != 3) goto bwd2;
+    static bool attr3 = false;
+    if (sm > 64 * 1024 && !attr3) {
+      (void)hipFuncSetAttribute((const void*)attn_bwd3_kernel<HD, SP>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)sm);
+      attr3 = true;
+    }
+    attn_bwd3_kernel<HD, SP><<<dim3(B * H), 256, sm, st>>>(qkv, o, dO, lse_in, out, S, H, scale, dbias_part);
+    return 0;
+  }
+bwd2:
   attn_bwd2_kernel<HD, SP><<<dim3(B * H), 256, sm, st>>>(qkv, o, dO, lse_in, out, S, H, scale, dbias_part);
   return 0;
 }
@@ -769,7 +1070,7 @@ int run_bwd2(const uint16_t* qkv, const uint16_t* o, const uint16_t* dO, const f
 template <int HD, int SP>
 int run(bool fwd, const uint16_t* qkv, const uint16_t* o, const uint16_t* dO, const float* lse_in, uint16_t* out,
         float* lse_out, int B, int S, int H, float scale, hipStream_t st) {
-  if (g_use_tr == 2 && !fwd) return run_bwd2<HD, SP>(qkv, o, dO, lse_in, out, lse_out, B, S, H, scale, st);
+  if (g_use_tr >= 2 && !fwd) return run_bwd2<HD, SP>(qkv, o, dO, lse_in, out, lse_out, B, S, H, scale, st);
   if (g_use_tr) return run_t<HD, SP, true>(fwd, qkv, o, dO, lse_in, out, lse_out, B, S, H, scale, st);
   return run_t<HD, SP, false>(fwd, qkv, o, dO, lse_in, out, lse_out, B, S, H, scale, st);
 }

@@ -111,7 +111,7 @@ def _attn_ref(qkv, H):
     return o, lse
 
 
-@pytest.mark.parametrize("tr", [2, 1, 0])
+@pytest.mark.parametrize("tr", [3, 2, 1, 0])
 @pytest.mark.parametrize("B,S,H,hd", [(3, 52, 16, 64), (2, 199, 16, 32), (2, 17, 4, 32), (2, 100, 3, 64),
                                       (2, 199, 4, 64)])
 def test_attention(ext, B, S, H, hd, tr):
@@ -139,7 +139,7 @@ def test_attention(ext, B, S, H, hd, tr):
     d = dqkv.view(B, S, 3, D)
     for i in range(3):
         assert rel(d[:, :, i], g[:, :, i]) < 2e-2, i
-    ext.attn_set_tr(2)
+    ext.attn_set_tr(3)
 
 
 @pytest.mark.parametrize("S,n", [(4, 4096), (512, 3072), (37, 1024)])

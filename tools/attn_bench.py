@@ -21,8 +21,11 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--shapes", default="dec,enc")
+    ap.add_argument("--tr", type=int, default=-1, help="kernel variant (ext.attn_set_tr), -1 = default")
     a = ap.parse_args()
     ext = _ext.load()
+    if a.tr >= 0:
+        ext.attn_set_tr(a.tr)
     for name in a.shapes.split(","):
         B, S, H, hd = SHAPES[name]
         D = H * hd
