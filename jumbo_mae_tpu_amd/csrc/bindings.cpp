@@ -63,6 +63,19 @@ int jm_gemm_tn_plan(int M, int N, int K, int* S_out);
 int jm_gemm_tn(const uint16_t* A, long lda, const uint16_t* B, long ldb, int M, int N, int K, int sps, int S,
                float* G, long ldo, float* partial, hipStream_t st);
 int jm_patchify_normalize(const uint8_t* img, float* out, int B, int H, int W, int p, hipStream_t st);
+int jm_gather_patches(const uint8_t* img, const int* ids, long idsB, uint16_t* out, int B, int K, int H, int W, int p,
+                      hipStream_t st);
+int jm_embed_finish(const uint16_t* e, const float* pos, const int* ids, long idsB, const float* cls, float* out,
+                    int B, int C, int K, int D, hipStream_t st);
+int jm_unshuffle_fwd(const uint16_t* y, const float* tok, const int* restore, long rsB, const float* pos, float* out,
+                     int B, int C, int K, int N, int d, hipStream_t st);
+int jm_unshuffle_bwd_blocks(int B, int C, int N, int rows_per_block);
+int jm_unshuffle_bwd(const float* dout, const int* restore, long rsB, uint16_t* dy, float* part, int B, int C, int K,
+                     int N, int d, int rows_per_block, hipStream_t st);
+int jm_patch_mse_fwd(const uint16_t* pred, long ldp, const uint8_t* img, float* mse, long rows, int N, int H, int W,
+                     int p, int norm_pix, hipStream_t st);
+int jm_patch_mse_bwd(const uint16_t* pred, long ldp, const uint8_t* img, const float* dmse, uint16_t* dpred, long rows,
+                     int N, int H, int W, int p, int norm_pix, hipStream_t st);
 
 namespace {
 
@@ -74,6 +87,7 @@ hipStream_t stream() { return c10::hip::getCurrentHIPStream().stream(); }
 
 const uint16_t* bf(const torch::Tensor& t) { return reinterpret_cast<const uint16_t*>(t.data_ptr()); }
 uint16_t* bfm(torch::Tensor& t) { return reinterpret_cast<uint16_t*>(t.data_ptr()); }
+uint16_t* bfp(const torch::Tensor& t) { return reinterpret_cast<uint16_t*>(t.data_ptr()); }
 const float* fopt(const c10::optional<torch::Tensor>& t) {
   return t.has_value() && t->defined() ? t->data_ptr<float>() : nullptr;
 }
@@ -373,6 +387,116 @@ torch::Tensor patchify_normalize(torch::Tensor img, int64_t p) {
   return out;
 }
 
+// Index tensors: int32, 1-D (shared permutation, batch stride 0) or 2-D [B, n] (per sample).
+long ids_bstride(const torch::Tensor& ids) {
+  CHECK_DT(ids, torch::kInt32);
+  CHECK_CONTIG(ids);
+  TORCH_CHECK(ids.dim() == 1 || ids.dim() == 2, "ids must be 1-D or 2-D");
+  return ids.dim() == 1 ? 0 : ids.size(1);
+}
+
+torch::Tensor gather_patches(torch::Tensor img, torch::Tensor ids_keep, int64_t p) {
+  CHECK_CONTIG(img);
+  CHECK_DT(img, torch::kUInt8);
+  TORCH_CHECK(img.size(1) == 3, "expects 3 channels");
+  const long sb = ids_bstride(ids_keep);
+  const int B = img.size(0), H = img.size(2), W = img.size(3);
+  const int K = ids_keep.size(-1);
+  TORCH_CHECK(ids_keep.dim() == 1 || ids_keep.size(0) == B, "ids_keep batch mismatch");
+  auto out = torch::empty({(long)B * K, 3 * p * p}, img.options().dtype(torch::kBFloat16));
+  check_rc(jm_gather_patches(img.data_ptr<uint8_t>(), ids_keep.data_ptr<int>(), sb, bfp(out), B, K, H, W, p, stream()),
+           "gather_patches");
+  return out;
+}
+
+torch::Tensor embed_finish(torch::Tensor e, c10::optional<torch::Tensor> pos, torch::Tensor ids_keep, torch::Tensor cls,
+                           int64_t B) {
+  CHECK_CONTIG(e);
+  CHECK_DT(e, torch::kBFloat16);
+  CHECK_CONTIG(cls);
+  CHECK_DT(cls, torch::kFloat32);
+  const long sb = ids_bstride(ids_keep);
+  const int K = ids_keep.size(-1), D = e.size(1), C = cls.numel() / D;
+  TORCH_CHECK(e.size(0) == B * K, "embed_finish: e rows");
+  const float* pp = nullptr;
+  if (pos) {
+    CHECK_CONTIG((*pos));
+    CHECK_DT((*pos), torch::kFloat32);
+    TORCH_CHECK(pos->size(-1) == D, "pos dim");
+    pp = pos->data_ptr<float>();
+  }
+  auto out = torch::empty({B, C + K, D}, e.options().dtype(torch::kFloat32));
+  check_rc(jm_embed_finish(bfp(e), pp, ids_keep.data_ptr<int>(), sb, cls.data_ptr<float>(), out.data_ptr<float>(), B, C,
+                           K, D, stream()),
+           "embed_finish");
+  return out;
+}
+
+torch::Tensor unshuffle_fwd(torch::Tensor y, torch::Tensor tok, torch::Tensor ids_restore, torch::Tensor pos,
+                            int64_t C) {
+  CHECK_CONTIG(y);
+  CHECK_DT(y, torch::kBFloat16);
+  CHECK_CONTIG(tok);
+  CHECK_CONTIG(pos);
+  CHECK_DT(tok, torch::kFloat32);
+  CHECK_DT(pos, torch::kFloat32);
+  const long sb = ids_bstride(ids_restore);
+  const int B = y.size(0), d = y.size(2), K = y.size(1) - C, N = pos.size(0);
+  TORCH_CHECK(ids_restore.size(-1) == N && tok.numel() == d && pos.size(1) == d, "unshuffle_fwd shapes");
+  auto out = torch::empty({B, C + N, d}, y.options().dtype(torch::kFloat32));
+  check_rc(jm_unshuffle_fwd(bfp(y), tok.data_ptr<float>(), ids_restore.data_ptr<int>(), sb, pos.data_ptr<float>(),
+                            out.data_ptr<float>(), B, C, K, N, d, stream()),
+           "unshuffle_fwd");
+  return out;
+}
+
+// -> (dy bf16 [B, C+K, d], d mask_token fp32 [d])
+std::vector<torch::Tensor> unshuffle_bwd(torch::Tensor dout, torch::Tensor ids_restore, int64_t C, int64_t K) {
+  CHECK_CONTIG(dout);
+  CHECK_DT(dout, torch::kFloat32);
+  const long sb = ids_bstride(ids_restore);
+  const int B = dout.size(0), N = dout.size(1) - C, d = dout.size(2);
+  TORCH_CHECK(ids_restore.size(-1) == N, "unshuffle_bwd shapes");
+  const int rpb = 64;
+  const int nb = jm_unshuffle_bwd_blocks(B, C, N, rpb);
+  auto dy = torch::empty({B, C + K, d}, dout.options().dtype(torch::kBFloat16));
+  auto part = torch::empty({nb, d}, dout.options());
+  check_rc(jm_unshuffle_bwd(dout.data_ptr<float>(), ids_restore.data_ptr<int>(), sb, bfp(dy), part.data_ptr<float>(), B,
+                            C, K, N, d, rpb, stream()),
+           "unshuffle_bwd");
+  return {dy, part.sum(0)};
+}
+
+// pred: bf16 [B*N, P3] (row stride may exceed P3); -> per-patch MSE fp32 [B*N]
+torch::Tensor patch_mse_fwd(torch::Tensor pred, torch::Tensor img, int64_t p, bool norm_pix) {
+  CHECK_DT(pred, torch::kBFloat16);
+  TORCH_CHECK(pred.stride(1) == 1, "pred rows must be contiguous");
+  CHECK_CONTIG(img);
+  CHECK_DT(img, torch::kUInt8);
+  const int H = img.size(2), W = img.size(3), N = (H / p) * (W / p);
+  TORCH_CHECK(pred.size(0) == img.size(0) * N && pred.size(1) == 3 * p * p, "patch_mse_fwd shapes");
+  auto mse = torch::empty({pred.size(0)}, pred.options().dtype(torch::kFloat32));
+  check_rc(jm_patch_mse_fwd(bfp(pred), pred.stride(0), img.data_ptr<uint8_t>(), mse.data_ptr<float>(), pred.size(0), N,
+                            H, W, p, norm_pix, stream()),
+           "patch_mse_fwd");
+  return mse;
+}
+
+torch::Tensor patch_mse_bwd(torch::Tensor pred, torch::Tensor img, torch::Tensor dmse, int64_t p, bool norm_pix) {
+  CHECK_DT(pred, torch::kBFloat16);
+  TORCH_CHECK(pred.stride(1) == 1, "pred rows must be contiguous");
+  CHECK_CONTIG(img);
+  CHECK_CONTIG(dmse);
+  CHECK_DT(dmse, torch::kFloat32);
+  const int H = img.size(2), W = img.size(3), N = (H / p) * (W / p);
+  TORCH_CHECK(dmse.numel() == pred.size(0) && pred.size(0) == img.size(0) * N, "patch_mse_bwd shapes");
+  auto dpred = torch::empty({pred.size(0), pred.size(1)}, pred.options());
+  check_rc(jm_patch_mse_bwd(bfp(pred), pred.stride(0), img.data_ptr<uint8_t>(), dmse.data_ptr<float>(), bfp(dpred),
+                            pred.size(0), N, H, W, p, norm_pix, stream()),
+           "patch_mse_bwd");
+  return dpred;
+}
+
 }  // namespace
 
 // ------------------------------------------------------------------------------ GEMM
@@ -540,4 +664,10 @@ PYBIND11_MODULE(_C, m) {
   m.def("opt_apply_trust", &opt_apply_trust);
   m.def("opt_sgd", &opt_sgd);
   m.def("patchify_normalize", &patchify_normalize);
+  m.def("gather_patches", &gather_patches);
+  m.def("embed_finish", &embed_finish);
+  m.def("unshuffle_fwd", &unshuffle_fwd);
+  m.def("unshuffle_bwd", &unshuffle_bwd);
+  m.def("patch_mse_fwd", &patch_mse_fwd);
+  m.def("patch_mse_bwd", &patch_mse_bwd);
 }

@@ -111,8 +111,9 @@ JM_DEVICE void epilogue(const f32x4_t (&acc)[8][NTW], const GemmEpi& ep, int M, 
   }
 }
 
+template <int BNT = BN>
 JM_DEVICE void tile_of(int M, int N, int GROUP_M, int& m0, int& n0, int splits = 1, int* split = nullptr) {
-  const int nM = (M + BM - 1) / BM, nN = (N + BN - 1) / BN;
+  const int nM = (M + BM - 1) / BM, nN = (N + BNT - 1) / BNT;
   const int nwg = nM * nN * splits;
   const int orig = blockIdx.x;
   const int xcd = orig & 7, q = nwg >> 3, r = nwg & 7;
@@ -125,7 +126,7 @@ JM_DEVICE void tile_of(int M, int N, int GROUP_M, int& m0, int& n0, int splits =
   const int first_m = (wg / per_group) * GROUP_M;
   const int gsz = min(nM - first_m, GROUP_M);
   m0 = (first_m + (wg % per_group) % gsz) * BM;
-  n0 = ((wg % per_group) / gsz) * BN;
+  n0 = ((wg % per_group) / gsz) * BNT;
 }
 
 // WN waves along N (2 along M): WN = 4 -> 8 waves of 128 x 64 (2 waves / SIMD);
@@ -137,10 +138,10 @@ JM_DEVICE void tile_of(int M, int N, int GROUP_M, int& m0, int& n0, int splits =
 // (2) the workgroup streams the tile out row by row, 16 B per lane, 512 B per row: full 128 B
 //     lines instead of 16 rows x 32 B per store instruction.  GELU is applied in (2) to the
 //     rounded pre-activation, which is exactly what the backward will see.
-template <int EPI, int NTW, int NTH>
+template <int EPI, int NTW, int NTH, int BNT = BN>
 JM_DEVICE void epilogue_lds(const f32x4_t (&acc)[8][NTW], const GemmEpi& ep, uint16_t* cs, int M, int N, int m0,
                             int n0, int wr, int wc, int l16, int g) {
-  constexpr int RB = BN;  // elements per LDS image row
+  constexpr int RB = BNT;  // elements per LDS image row
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
 #pragma unroll
   for (int nt = 0; nt < NTW; ++nt) {
@@ -158,7 +159,7 @@ JM_DEVICE void epilogue_lds(const f32x4_t (&acc)[8][NTW], const GemmEpi& ep, uin
     }
   }
   __syncthreads();
-  constexpr int LPR = BN / 8;         // lanes per row (16 B each)
+  constexpr int LPR = BNT / 8;        // lanes per row (16 B each)
   constexpr int RPP = NTH / LPR;      // rows per pass
   const int tid = threadIdx.x;
   const int c = tid % LPR;
@@ -198,7 +199,7 @@ JM_DEVICE void epilogue_lds(const f32x4_t (&acc)[8][NTW], const GemmEpi& ep, uin
 #pragma unroll
     for (int j = 0; j < 8; ++j) red[tid * 8 + j] = csum[j];
     __syncthreads();
-    for (int col = tid; col < BN; col += NTH) {
+    for (int col = tid; col < BNT; col += NTH) {
       const int cc = col >> 3, j = col & 7;
       float acc = 0.f;
 #pragma unroll
@@ -535,6 +536,151 @@ __global__ __launch_bounds__(512, 1) void gemm_nt64_kernel(const uint16_t* __res
     nt64_body<EPI, false, false>(A, lda, B, ldb, M, N, K, ep, GROUP_M, smem);
 }
 
+// ------------------------------------------------------------------ half-width, 2 WGs per CU
+// 256 x 128 output tile, 4 waves (2 x 2, each the usual 128 x 64 sub-tile, 128 accumulator VGPRs),
+// 32-deep K steps through a 3-stage ring of 24 KB stages (72 KB): two workgroups fit on one CU
+// (2 x 72 KB LDS, 2 waves per SIMD).  While one workgroup runs its epilogue (VALU + a burst of
+// HBM stores that the whole chip issues at once with one workgroup per CU) the other keeps the
+// matrix pipe busy.  STAGGER delays the second resident set of workgroups by about half a tile so
+// that the two never reach their epilogues together; freed slots are refilled immediately, so
+// the offset persists for the rest of the launch.
+constexpr int BNH = 128, NSTH = 3, STAGEH = (BM + BNH) * BK;
+
+size_t jm_gemm_smem_half() { return (size_t)NSTH * STAGEH * sizeof(uint16_t); }
+
+template <int EPI, bool STAGGER>
+__global__ __launch_bounds__(256, 2) void gemm_nth_kernel(const uint16_t* __restrict__ A, long lda,
+                                                          const uint16_t* __restrict__ B, long ldb, int M, int N,
+                                                          int K, GemmEpi ep, int GROUP_M) {
+  constexpr int NW = 4, NTW = 4;
+  constexpr int RNDA = BM / 16 / NW, RNDB = BNH / 16 / NW;  // glds pieces (16 rows x 64 B) per wave
+  constexpr int PER_STAGE = RNDA + RNDB;                      // vmcnt units per stage
+  extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
+  const int tid = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+  const int l16 = lane & 15, g = lane >> 4;
+  const int wr = wave >> 1, wc = wave & 1;
+
+  if (STAGGER && blockIdx.x >= 256 && blockIdx.x < 512) {
+    for (int i = 0; i < K / 512; ++i) __builtin_amdgcn_s_sleep(127);
+  }
+  int m0, n0, split = 0;
+  tile_of<BNH>(M, N, GROUP_M, m0, n0, EPI == EPI_PARTIAL ? ep.splits : 1, EPI == EPI_PARTIAL ? &split : nullptr);
+  int k_begin = 0;
+  if (EPI == EPI_PARTIAL) {
+    const int ku = K / 64;
+    const int ku0 = split * ku / ep.splits, ku1 = (split + 1) * ku / ep.splits;
+    k_begin = ku0 * 64;
+    K = (ku1 - ku0) * 64;
+  }
+  const __amdgpu_buffer_rsrc_t ra = make_rsrc(A + (long)m0 * lda + k_begin, (long)(M - m0) * lda * 2 - 2L * k_begin);
+  const __amdgpu_buffer_rsrc_t rb = make_rsrc(B + (long)n0 * ldb + k_begin, (long)(N - n0) * ldb * 2 - 2L * k_begin);
+  uint32_t a_src[RNDA], b_src[RNDB];
+#pragma unroll
+  for (int rr = 0; rr < RNDA; ++rr) {
+    const int row = rr * 16 * NW + wave * 16 + (lane >> 2);
+    a_src[rr] = (uint32_t)((row * lda + ((lane & 3) ^ swz(row)) * 8) * 2);
+  }
+#pragma unroll
+  for (int rr = 0; rr < RNDB; ++rr) {
+    const int row = rr * 16 * NW + wave * 16 + (lane >> 2);
+    b_src[rr] = (uint32_t)((row * ldb + ((lane & 3) ^ swz(row)) * 8) * 2);
+  }
+  auto issue = [&](int t) {
+    const uint32_t k0b = t * BK * 2;
+    uint16_t* la = smem + (t % NSTH) * STAGEH;
+    uint16_t* lb = la + BM * BK;
+#pragma unroll
+    for (int rr = 0; rr < RNDA; ++rr) blds16(ra, a_src[rr], k0b, la + (rr * 16 * NW + wave * 16) * BK);
+#pragma unroll
+    for (int rr = 0; rr < RNDB; ++rr) blds16(rb, b_src[rr], k0b, lb + (rr * 16 * NW + wave * 16) * BK);
+  };
+  const int ch = (g ^ swz(l16)) * 8;
+  const int a_off = (wr * 128 + l16) * BK + ch;
+  const int b_off = BM * BK + (wc * NTW * 16 + l16) * BK + ch;
+  auto read = [&](int t, Frags<NTW>& f) {
+    const uint16_t* base = smem + (t % NSTH) * STAGEH;
+#pragma unroll
+    for (int nt = 0; nt < NTW; ++nt) f.b[nt] = lds8(base + b_off + nt * 16 * BK);
+#pragma unroll
+    for (int mt = 0; mt < 8; ++mt) f.a[mt] = lds8(base + a_off + mt * 16 * BK);
+  };
+  f32x4_t acc[8][NTW];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < NTW; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  auto wait_bar = [&](auto outstanding_stages) {
+    constexpr int W = decltype(outstanding_stages)::value * PER_STAGE;
+    if constexpr (W == 6) asm volatile("s_waitcnt vmcnt(6) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    if constexpr (W == 0) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    static_assert(W == 6 || W == 0, "vmcnt table");
+  };
+  // KIND 2: steady (issue t + 2, one stage in flight after t + 1 lands), 1: drain, 0: last step
+  auto step = [&](auto kind, int t, Frags<NTW>& cur, Frags<NTW>& nxt) {
+    constexpr int KIND = decltype(kind)::value;
+    if constexpr (KIND == 2) issue(t + 2);
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < NTW; ++nt) acc[mt][nt] = mfma16(cur.b[nt], cur.a[mt], acc[mt][nt]);
+    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (KIND > 0) wait_bar(std::integral_constant<int, KIND - 1>{});
+    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (KIND > 0) read(t + 1, nxt);
+#pragma unroll
+    for (int mt = 4; mt < 8; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < NTW; ++nt) acc[mt][nt] = mfma16(cur.b[nt], cur.a[mt], acc[mt][nt]);
+    if constexpr (KIND > 0) {
+#pragma unroll
+      for (int i = 0; i < 12; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      }
+      __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  using K2 = std::integral_constant<int, 2>;
+  using K1 = std::integral_constant<int, 1>;
+  using K0 = std::integral_constant<int, 0>;
+
+  const int nk = K / BK;  // even, >= 2
+  issue(0);
+  issue(1);
+  wait_bar(std::integral_constant<int, 1>{});
+  __builtin_amdgcn_sched_barrier(0);
+  Frags<NTW> f0, f1;
+  read(0, f0);
+  int t = 0;
+  for (; t + 3 < nk; t += 2) {
+    step(K2{}, t, f0, f1);
+    step(K2{}, t + 1, f1, f0);
+  }
+  step(K1{}, t, f0, f1);
+  step(K0{}, t + 1, f1, f0);
+
+  if (EPI == EPI_PARTIAL) {
+    float* dst = ep.part + (long)split * M * N;
+#pragma unroll
+    for (int mt = 0; mt < 8; ++mt) {
+      const int m = m0 + wr * 128 + mt * 16 + l16;
+      if (m >= M) continue;
+#pragma unroll
+      for (int nt = 0; nt < NTW; ++nt) {
+        const int n = n0 + wc * NTW * 16 + nt * 16 + 4 * g;
+        if (n >= N) continue;
+        float v[4] = {acc[mt][nt][0], acc[mt][nt][1], acc[mt][nt][2], acc[mt][nt][3]};
+        store4(dst + (long)m * N + n, v);
+      }
+    }
+  } else if (N % 8 == 0)
+    epilogue_lds<EPI, NTW, 256, BNH>(acc, ep, smem, M, N, m0, n0, wr, wc, l16, g);
+  else
+    epilogue<EPI, NTW>(acc, ep, M, N, m0 + wr * 128, n0 + wc * NTW * 16, l16, g);
+}
+
 // ------------------------------------------------------------------ persistent variant
 // One workgroup per CU walks its tiles (bid, bid + G, ...) as ONE stream of K steps: the ring's
 // look-ahead loads run straight into the next tile, so a tile's prologue latency is hidden behind
@@ -828,10 +974,26 @@ void launch_nt64(const uint16_t* A, long lda, const uint16_t* B, long ldb, int M
   gemm_nt64_kernel<EPI, SCHED><<<nwg, 512, sm, st>>>(A, lda, B, ldb, M, N, K, ep, g_gemm_group);
 }
 
+template <int EPI, bool STAGGER>
+void launch_nth(const uint16_t* A, long lda, const uint16_t* B, long ldb, int M, int N, int K, const GemmEpi& ep,
+                hipStream_t st) {
+  static bool attr = false;
+  const size_t sm = jm_gemm_smem_half();
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)gemm_nth_kernel<EPI, STAGGER>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)sm);
+    attr = true;
+  }
+  const int nwg = ((M + BM - 1) / BM) * ((N + BNH - 1) / BNH) * (EPI == EPI_PARTIAL ? ep.splits : 1);
+  gemm_nth_kernel<EPI, STAGGER><<<nwg, 256, sm, st>>>(A, lda, B, ldb, M, N, K, ep, g_gemm_group);
+}
+
 template <int EPI>
 void launch_epi(const uint16_t* A, long lda, const uint16_t* B, long ldb, int M, int N, int K, const GemmEpi& ep,
                 int nwg, hipStream_t st) {
   if (g_gemm_wn == 6) return launch_nt64<EPI, 0>(A, lda, B, ldb, M, N, K, ep, nwg, st);
+  if (g_gemm_wn == 10) return launch_nth<EPI, false>(A, lda, B, ldb, M, N, K, ep, st);
+  if (g_gemm_wn == 11) return launch_nth<EPI, true>(A, lda, B, ldb, M, N, K, ep, st);
   if (g_gemm_wn == 7) return launch_nt64<EPI, 1>(A, lda, B, ldb, M, N, K, ep, nwg, st);
   if (g_gemm_wn == 8) return launch_nt64<EPI, 3>(A, lda, B, ldb, M, N, K, ep, nwg, st);
   if (g_gemm_wn == 9) return launch_nt64<EPI, 2>(A, lda, B, ldb, M, N, K, ep, nwg, st);

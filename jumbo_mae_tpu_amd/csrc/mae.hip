@@ -48,3 +48,320 @@ int jm_patchify_normalize(const uint8_t* img, float* out, int B, int H, int W, i
   patchify_kernel<<<B * (H / p), 256, sm, st>>>(img, out, H, W, p);
   return 0;
 }
+
+// ----------------------------------------------------------------------------------------------
+// Mask-first MAE glue.  Index tensors are int32 with a batch
+// stride: 0 for the reference's per-rank shared permutation (utils_mae.py:88-102, quirk Q1), N
+// (or K) for per-sample masks.  None of these kernels materialises the fp32 patch tensor: the
+// encoder input and the loss target are both read straight from the uint8 images.
+namespace {
+
+// normalized pixel o (in (ph, pw, c) order) of patch (gy, gx) of image b
+JM_DEVICE float patch_pixel(const uint8_t* __restrict__ img, int b, int H, int W, int p, int gy, int gx, int o) {
+  const int ph = o / (3 * p);
+  const int r = o - ph * 3 * p;
+  const int pw = r / 3, c = r - (r / 3) * 3;
+  const float v = (float)img[(((long)b * 3 + c) * H + gy * p + ph) * W + gx * p + pw];
+  return (v * (1.f / 255.f) - c_mean[c]) * c_istd[c];
+}
+
+// K1+K3: kept patches of the normalized image as the bf16 patch-embed GEMM operand [B*K, 3p^2].
+// One thread writes 4 consecutive outputs (8-byte store).
+__global__ __launch_bounds__(256) void gather_patches_kernel(const uint8_t* __restrict__ img,
+                                                             const int* __restrict__ ids, long idsB,
+                                                             uint16_t* __restrict__ out, int B, int K, int H,
+                                                             int W, int p) {
+  const int P3 = 3 * p * p, q = P3 / 4, g = W / p;
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (long)B * K * q) return;
+  const long row = i / q;
+  const int o = (int)(i - row * q) * 4;
+  const int b = (int)(row / K), k = (int)(row - (long)b * K);
+  const int n = ids[b * idsB + k];
+  const int gy = n / g, gx = n - (n / g) * g;
+  float f[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) f[j] = patch_pixel(img, b, H, W, p, gy, gx, o + j);
+  store4(out + row * P3 + o, f);
+}
+
+// K2 epilogue + K4: x[b, t] = cls[t] (t < C); e[b*K + t - C] + pos[ids[t - C]] (t >= C), fp32.
+__global__ __launch_bounds__(256) void embed_finish_kernel(const uint16_t* __restrict__ e, const float* __restrict__ pos,
+                                                           const int* __restrict__ ids, long idsB,
+                                                           const float* __restrict__ cls, float* __restrict__ out,
+                                                           int B, int C, int K, int D) {
+  const int q = D / 4;
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (long)B * (C + K) * q) return;
+  const long row = i / q;
+  const int col = (int)(i - row * q) * 4;
+  const int b = (int)(row / (C + K)), t = (int)(row - (long)b * (C + K));
+  float f[4];
+  if (t < C) {
+    load4(cls + (long)t * D + col, f);
+  } else {
+    load4(e + ((long)b * K + t - C) * D + col, f);
+    if (pos != nullptr) {
+      float pp[4];
+      load4(pos + (long)ids[b * idsB + t - C] * D + col, pp);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) f[j] += pp[j];
+    }
+  }
+  store4(out + row * D + col, f);
+}
+
+// K13 forward: decoder input [B, C+N, d] fp32 = cat(cls, unshuffle(cat(kept, mask_token)) + pos).
+__global__ __launch_bounds__(256) void unshuffle_fwd_kernel(const uint16_t* __restrict__ y, const float* __restrict__ tok,
+                                                            const int* __restrict__ restore, long rsB,
+                                                            const float* __restrict__ pos, float* __restrict__ out,
+                                                            int B, int C, int K, int N, int d) {
+  const int q = d / 4;
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (long)B * (C + N) * q) return;
+  const long row = i / q;
+  const int col = (int)(i - row * q) * 4;
+  const int b = (int)(row / (C + N)), t = (int)(row - (long)b * (C + N));
+  float f[4];
+  if (t < C) {
+    load4(y + ((long)b * (C + K) + t) * d + col, f);
+  } else {
+    const int n = t - C;
+    const int j = restore[b * rsB + n];
+    if (j < K) load4(y + ((long)b * (C + K) + C + j) * d + col, f);
+    else load4(tok + col, f);
+    float pp[4];
+    load4(pos + (long)n * d + col, pp);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) f[u] += pp[u];
+  }
+  store4(out + row * d + col, f);
+}
+
+// K13 backward in one pass over dout [B, C+N, d]: kept and CLS rows are gathered into dy
+// [B, C+K, d] (bf16, the decoder_proj GEMM operand); mask-token rows are summed into per-block
+// column partials part[blockIdx.x][d] (atomic-free, reduced by the caller).  Each block owns a
+// contiguous range of ``rows_per_block`` rows; threads cover 4 columns each.
+__global__ __launch_bounds__(256) void unshuffle_bwd_kernel(const float* __restrict__ dout, const int* __restrict__ restore,
+                                                            long rsB, uint16_t* __restrict__ dy, float* __restrict__ part,
+                                                            int B, int C, int K, int N, int d, int rows_per_block) {
+  extern __shared__ float red[];  // [256 / q][d]
+  const int q = d / 4;
+  const int lanes = (256 / q) * q;
+  const int col = (threadIdx.x % q) * 4;
+  const int rg = threadIdx.x / q, nrg = 256 / q;
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  const long total = (long)B * (C + N);
+  const long r0 = (long)blockIdx.x * rows_per_block;
+  if (threadIdx.x < lanes) {
+    for (long row = r0 + rg; row < r0 + rows_per_block && row < total; row += nrg) {
+      const int b = (int)(row / (C + N)), t = (int)(row - (long)b * (C + N));
+      float f[4];
+      load4(dout + row * d + col, f);
+      if (t < C) {
+        store4(dy + ((long)b * (C + K) + t) * d + col, f);
+      } else {
+        const int j = restore[b * rsB + t - C];
+        if (j < K) {
+          store4(dy + ((long)b * (C + K) + C + j) * d + col, f);
+        } else {
+#pragma unroll
+          for (int u = 0; u < 4; ++u) acc[u] += f[u];
+        }
+      }
+    }
+    store4(red + rg * d + col, acc);
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < d; c += 256) {
+    float s = 0.f;
+    for (int g = 0; g < nrg; ++g) s += red[g * d + c];
+    part[(long)blockIdx.x * d + c] = s;
+  }
+}
+
+// target pixels of one patch row for a wave: lane holds elements o = lane + 64 * j.  The patch's
+// 3 x p x p uint8 pixels are first staged into the wave's LDS slice with coalesced row loads
+// (p = 16: 48 lanes x 16 B), then each lane picks its (ph, pw, c) elements from LDS.
+template <int NJ, bool P16>
+JM_DEVICE void patch_target(const uint8_t* __restrict__ img, long row, int N, int H, int W, int p_, int P3_,
+                            bool norm_pix, uint8_t* lds, float* t) {
+  const int p = P16 ? 16 : p_, P3 = P16 ? 768 : P3_;
+  const int g = W / p;
+  const int b = (int)(row / N), n = (int)(row - (long)b * N);
+  const int gy = n / g, gx = n - (n / g) * g;
+  const int lane = threadIdx.x & 63;
+  const uint8_t* src = img + ((long)b * 3 * H + gy * p) * W + gx * p;  // channel 0, first patch row
+  if (p == 16) {
+    if (lane < 48) {
+      const int c = lane >> 4, ph = lane & 15;
+      *reinterpret_cast<uint4*>(lds + lane * 16) =
+          *reinterpret_cast<const uint4*>(src + ((long)c * H + ph) * W);
+    }
+  } else {
+    for (int i = lane; i < P3; i += 64) {
+      const int c = i / (p * p), r = i - c * p * p;
+      const int ph = r / p, pw = r - (r / p) * p;
+      lds[i] = src[((long)c * H + ph) * W + pw];
+    }
+  }
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the wave's LDS writes have landed
+  __builtin_amdgcn_wave_barrier();
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int o = lane + 64 * j;
+    float v = 0.f;
+    if (o < P3) {
+      const int ph = o / (3 * p), r = o - ph * 3 * p;
+      const int pw = r / 3, c = r - (r / 3) * 3;
+      v = ((float)lds[(c * p + ph) * p + pw] * (1.f / 255.f) - c_mean[c]) * c_istd[c];
+    }
+    t[j] = v;
+  }
+  if (norm_pix) {  // per-patch (t - mean) / sqrt(var + 1e-6), biased var (pretraining.py:114-117)
+    float s = 0.f;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) s += t[j];
+    const float mean = wave_sum(s) / P3;
+    float v = 0.f;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int o = lane + 64 * j;
+      const float dlt = o < P3 ? t[j] - mean : 0.f;
+      v += dlt * dlt;
+    }
+    const float rs = rsqrtf(wave_sum(v) / P3 + 1e-6f);
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) t[j] = (t[j] - mean) * rs;
+  }
+}
+
+// K14 forward: per-patch mean squared error of the prediction vs the normalized target, one wave
+// per (image, patch) row.  mse[row] = mean_pix (t - pred)^2 (utils_mae.py:51-64 before masking).
+template <int NJ, bool P16>
+__global__ __launch_bounds__(256) void patch_mse_fwd_kernel(const uint16_t* __restrict__ pred, long ldp,
+                                                            const uint8_t* __restrict__ img, float* __restrict__ mse,
+                                                            long rows, int N, int H, int W, int p, int norm_pix) {
+  const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const int P3 = 3 * p * p;
+  __shared__ __attribute__((aligned(16))) uint8_t pix[4][64 * NJ];
+  float t[NJ];
+  patch_target<NJ, P16>(img, row, N, H, W, p, P3, norm_pix != 0, pix[threadIdx.x >> 6], t);
+  const int lane = threadIdx.x & 63;
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int o = lane + 64 * j;
+    if (o < P3) {
+      const float dlt = t[j] - bf2f(pred[row * ldp + o]);
+      s += dlt * dlt;
+    }
+  }
+  s = wave_sum(s);
+  if (lane == 0) mse[row] = s / P3;
+}
+
+// K14 backward: dpred[row] = dmse[row] * 2 / P3 * (pred - t); rows with dmse == 0 (the kept,
+// unmasked patches) are written as zeros without reading pred or the image.
+template <int NJ, bool P16>
+__global__ __launch_bounds__(256) void patch_mse_bwd_kernel(const uint16_t* __restrict__ pred, long ldp,
+                                                            const uint8_t* __restrict__ img,
+                                                            const float* __restrict__ dmse, uint16_t* __restrict__ dpred,
+                                                            long rows, int N, int H, int W, int p, int norm_pix) {
+  const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const int P3 = 3 * p * p;
+  const int lane = threadIdx.x & 63;
+  const float gsc = dmse[row];
+  if (gsc == 0.f) {
+    for (int o = lane; o < P3; o += 64) dpred[row * P3 + o] = 0;
+    return;
+  }
+  __shared__ __attribute__((aligned(16))) uint8_t pix[4][64 * NJ];
+  float t[NJ];
+  patch_target<NJ, P16>(img, row, N, H, W, p, P3, norm_pix != 0, pix[threadIdx.x >> 6], t);
+  const float k = 2.f * gsc / P3;
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int o = lane + 64 * j;
+    if (o < P3) dpred[row * P3 + o] = f2bf(k * (bf2f(pred[row * ldp + o]) - t[j]));
+  }
+}
+
+inline int cdiv(long a, long b) { return (int)((a + b - 1) / b); }
+
+}  // namespace
+
+int jm_gather_patches(const uint8_t* img, const int* ids, long idsB, uint16_t* out, int B, int K, int H, int W, int p,
+                      hipStream_t st) {
+  if ((3 * p * p) % 4 || H % p || W % p) return -1;
+  const long n = (long)B * K * (3 * p * p / 4);
+  if (n == 0) return 0;
+  gather_patches_kernel<<<cdiv(n, 256), 256, 0, st>>>(img, ids, idsB, out, B, K, H, W, p);
+  return 0;
+}
+
+int jm_embed_finish(const uint16_t* e, const float* pos, const int* ids, long idsB, const float* cls, float* out,
+                    int B, int C, int K, int D, hipStream_t st) {
+  if (D % 4) return -1;
+  const long n = (long)B * (C + K) * (D / 4);
+  if (n == 0) return 0;
+  embed_finish_kernel<<<cdiv(n, 256), 256, 0, st>>>(e, pos, ids, idsB, cls, out, B, C, K, D);
+  return 0;
+}
+
+int jm_unshuffle_fwd(const uint16_t* y, const float* tok, const int* restore, long rsB, const float* pos, float* out,
+                     int B, int C, int K, int N, int d, hipStream_t st) {
+  if (d % 4) return -1;
+  const long n = (long)B * (C + N) * (d / 4);
+  if (n == 0) return 0;
+  unshuffle_fwd_kernel<<<cdiv(n, 256), 256, 0, st>>>(y, tok, restore, rsB, pos, out, B, C, K, N, d);
+  return 0;
+}
+
+// returns the number of partial rows written to ``part`` (caller sizes part with jm_unshuffle_bwd_blocks)
+int jm_unshuffle_bwd_blocks(int B, int C, int N, int rows_per_block) {
+  return cdiv((long)B * (C + N), rows_per_block);
+}
+
+int jm_unshuffle_bwd(const float* dout, const int* restore, long rsB, uint16_t* dy, float* part, int B, int C, int K,
+                     int N, int d, int rows_per_block, hipStream_t st) {
+  if (d % 4 || d / 4 > 256) return -1;
+  const int nb = jm_unshuffle_bwd_blocks(B, C, N, rows_per_block);
+  const size_t sm = (size_t)(256 / (d / 4)) * d * sizeof(float);
+  unshuffle_bwd_kernel<<<nb, 256, sm, st>>>(dout, restore, rsB, dy, part, B, C, K, N, d, rows_per_block);
+  return 0;
+}
+
+int jm_patch_mse_fwd(const uint16_t* pred, long ldp, const uint8_t* img, float* mse, long rows, int N, int H, int W,
+                     int p, int norm_pix, hipStream_t st) {
+  const int P3 = 3 * p * p;
+  if (H % p || W % p || P3 > 64 * 16) return -1;
+  const int nb = cdiv(rows, 4);
+  if (p == 16) patch_mse_fwd_kernel<12, true><<<nb, 256, 0, st>>>(pred, ldp, img, mse, rows, N, H, W, p, norm_pix);
+  else if (P3 <= 64 * 4)
+    patch_mse_fwd_kernel<4, false><<<nb, 256, 0, st>>>(pred, ldp, img, mse, rows, N, H, W, p, norm_pix);
+  else if (P3 <= 64 * 12)
+    patch_mse_fwd_kernel<12, false><<<nb, 256, 0, st>>>(pred, ldp, img, mse, rows, N, H, W, p, norm_pix);
+  else patch_mse_fwd_kernel<16, false><<<nb, 256, 0, st>>>(pred, ldp, img, mse, rows, N, H, W, p, norm_pix);
+  return 0;
+}
+
+int jm_patch_mse_bwd(const uint16_t* pred, long ldp, const uint8_t* img, const float* dmse, uint16_t* dpred, long rows,
+                     int N, int H, int W, int p, int norm_pix, hipStream_t st) {
+  const int P3 = 3 * p * p;
+  if (H % p || W % p || P3 > 64 * 16) return -1;
+  const int nb = cdiv(rows, 4);
+  if (p == 16)
+    patch_mse_bwd_kernel<12, true><<<nb, 256, 0, st>>>(pred, ldp, img, dmse, dpred, rows, N, H, W, p, norm_pix);
+  else if (P3 <= 64 * 4)
+    patch_mse_bwd_kernel<4, false><<<nb, 256, 0, st>>>(pred, ldp, img, dmse, dpred, rows, N, H, W, p, norm_pix);
+  else if (P3 <= 64 * 12)
+    patch_mse_bwd_kernel<12, false><<<nb, 256, 0, st>>>(pred, ldp, img, dmse, dpred, rows, N, H, W, p, norm_pix);
+  else
+    patch_mse_bwd_kernel<16, false><<<nb, 256, 0, st>>>(pred, ldp, img, dmse, dpred, rows, N, H, W, p, norm_pix);
+  return 0;
+}

@@ -21,7 +21,6 @@ from ..config import DecoderConfig, ViTConfig
 from ..data.constants import IMAGENET_DEFAULT_MEAN, IMAGENET_DEFAULT_STD
 from ..ops import functional as Fn
 from ..ops import mae as mae_ops
-from ..ops.params_fn import param_value
 from ..utils.mae import masking_ids
 from .params import ParamStore, trunc_normal_
 from .vit import Dense, JumboViT, MAEDecoder
@@ -74,23 +73,22 @@ class PretrainModel:
         B = images_u8.shape[0]
         C = cfg.num_cls_tokens
         N, K = cfg.seq_patches, cfg.keep_len
-        patches = self.normalize(images_u8)  # fp32 [B, N, 768]
         ids_shuffle, ids_restore, ids_keep, mask = self.draw_mask(B, rngs.get("noise"), noise)
-        kept = mae_ops.gather_patches(patches, ids_keep)
+        # mask-first: only the kept patches are read (uint8 -> normalized bf16 GEMM rows)
+        rows = mae_ops.kept_patches(images_u8, ids_keep, cfg.patch_size, self.store.compute_dtype)
         drop = rngs.get("dropout")
-        x = self.encoder.embed(kept, ids_keep)
+        x = self.encoder.embed_rows(rows, ids_keep, B)
         # encoder always runs with det=False (pretraining.py:92, quirk Q3)
         x = self.encoder.blocks(x, drop, det=False)
         h = self.encoder.norm(x)  # [B*(C+K), D]
         y = self.decoder_proj(h).view(B, C + K, -1)
-        dec_in = mae_ops.unshuffle(y, param_value(self.mask_token).view(-1), ids_restore,
-                                   self.decoder.posemb_table(y.device), C)
+        dec_in = mae_ops.unshuffle_fused(y, self.mask_token, ids_restore, self.decoder.posemb_table(y.device), C)
         xd = self.decoder.blocks(dec_in, drop, det=det)
         hd = self.decoder.dec_norm(xd[:, C:])  # [B*N, d] only patch rows are predicted
         pred = self.decoder_image_output(hd)  # [B*N, p*p*3]
-        if mask.dim() == 1:
-            mask = mask.unsqueeze(0).expand(B, N)
-        loss = mae_ops.masked_mse(pred.view(B, N, -1), patches, mask, self.norm_pix_loss, per_sample)
+        # target pixels come straight from the uint8 images (no fp32 patch tensor)
+        per_patch = mae_ops.patch_mse(pred.view(B, N, -1), images_u8, cfg.patch_size, self.norm_pix_loss)
+        loss = mae_ops.masked_mean_loss(per_patch, mask, per_sample)
         return {"loss": loss}
 
     __call__ = forward

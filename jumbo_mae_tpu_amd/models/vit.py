@@ -27,7 +27,7 @@ import torch
 from ..config import DecoderConfig, ViTConfig
 from ..ops import blocks
 from ..ops import functional as Fn
-from ..ops.params_fn import param_value
+from ..ops import mae as mae_ops
 from ..utils.posemb import fixed_sincos2d_embeddings
 from .params import Handle, ParamStore, const_, ones_, trunc_normal_, trunc_normal_t, zeros_
 
@@ -268,16 +268,22 @@ class JumboViT:
         Returns [B, C + n, D] fp32 residual stream."""
         B, n, K = patches.shape
         dt = self.wte_k.store.compute_dtype
-        e = Fn.linear(patches.reshape(B * n, K).to(dt), self.wte_k, self.wte_b).float().view(B, n, -1)
-        if self.wpe is not None:
-            pos = param_value(self.wpe)
-        else:
-            pos = self.posemb_table(patches.device)
-        if ids is not None:
-            pos = pos[ids] if ids.dim() == 1 else pos[ids]
-        e = e + pos
-        cls = param_value(self.cls_tokens).expand(B, -1, -1)
-        return torch.cat([cls, e], 1)
+        return self.embed_rows(patches.reshape(B * n, K).to(dt), ids, B)
+
+    def embed_rows(self, rows: torch.Tensor, ids: torch.Tensor | None, B: int) -> torch.Tensor:
+        """rows: [B*n, p*p*3] patch pixels in the compute dtype (patch ``ids[.., j]`` of each image;
+        all patches in order when ``ids`` is None).  Patch-embed GEMM (bias fused), then one
+        kernel adds the posemb and writes the CLS + patch rows of the fp32 stream."""
+        e = Fn.linear(rows, self.wte_k, self.wte_b)
+        if ids is None:
+            ids = self._arange(rows.shape[0] // B, rows.device)
+        return mae_ops.embed_finish(e, self.cls_tokens, self.wpe, self.posemb_table(rows.device), ids, B)
+
+    def _arange(self, n, device):
+        key = ("arange", n, str(device))
+        if key not in self._posemb_cache:
+            self._posemb_cache[key] = torch.arange(n, device=device)
+        return self._posemb_cache[key]
 
     def blocks(self, x: torch.Tensor, rng=None, det=True) -> torch.Tensor:
         x = _dropout(x, self.cfg.dropout, rng, det)

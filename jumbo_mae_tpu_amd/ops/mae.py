@@ -73,3 +73,146 @@ def masked_mse(pred: torch.Tensor, target: torch.Tensor, mask: torch.Tensor, nor
         per_patch = (t - pred.float()).square().mean(-1)
         return (per_patch * mask).sum(-1) / mask.sum(-1)
     return patch_mse_loss(pred.float(), t, mask)
+
+
+# ------------------------------------------------------------------ fused mask-first glue (GPU)
+def _i32(ids: torch.Tensor) -> torch.Tensor:
+    return ids.to(torch.int32).contiguous()
+
+
+def kept_patches(images_u8: torch.Tensor, ids_keep: torch.Tensor, patch_size: int, dtype) -> torch.Tensor:
+    """Normalized pixels of the kept patches as the patch-embed GEMM operand [B*K, p*p*3].
+
+    GPU: one HIP kernel reads the uint8 images directly (K1 normalize + K3 gather fused, no fp32
+    patch tensor).  CPU: the torch composition (normalize -> patchify -> index_sequence)."""
+    B = images_u8.shape[0]
+    if _ext.use_hip(images_u8) and dtype == torch.bfloat16:
+        return _ext.load().gather_patches(images_u8.contiguous(), _i32(ids_keep), patch_size)
+    kept = index_sequence(normalized_patches(images_u8, patch_size), ids_keep)
+    return kept.reshape(B * kept.shape[1], -1).to(dtype)
+
+
+class _EmbedFinish(torch.autograd.Function):
+    """x[b] = cat(cls_tokens, e[b] + pos[ids]) -> fp32 [B, C+K, D]  (modeling.py:121-124,249-257).
+
+    Parameter gradients (cls_tokens, learnable wpe) go straight to the flat store."""
+
+    @staticmethod
+    def forward(ctx, e, cls_p, wpe_p, h_cls, h_wpe, pos, ids, B):
+        D = e.shape[-1]
+        C = h_cls.numel // D
+        K = ids.shape[-1]
+        if _ext.use_hip(e) and e.dtype == torch.bfloat16:
+            out = _ext.load().embed_finish(e.contiguous(), pos, _i32(ids), h_cls.master.contiguous(), B)
+        else:
+            ev = e.float().view(B, K, D)
+            if pos is not None:
+                ev = ev + (pos[ids] if ids.dim() == 1 else pos[ids])
+            out = torch.cat([h_cls.master.view(1, C, D).expand(B, C, D), ev], 1)
+        ctx.h_cls, ctx.h_wpe, ctx.C, ctx.B, ctx.K = h_cls, h_wpe, C, B, K
+        ctx.edtype = e.dtype
+        ctx.save_for_backward(ids)
+        return out
+
+    @staticmethod
+    def backward(ctx, dx):
+        (ids,) = ctx.saved_tensors
+        C, B, K = ctx.C, ctx.B, ctx.K
+        D = dx.shape[-1]
+        dpatch = dx[:, C:]
+        if ctx.h_cls.segs[0].trainable:
+            ctx.h_cls.accumulate_grad(dx[:, :C].sum(0))
+        h = ctx.h_wpe
+        if h is not None and h.segs[0].trainable:
+            if ids.dim() == 1:
+                h.grad.index_add_(0, ids, dpatch.sum(0))
+            else:
+                h.grad.index_add_(0, ids.reshape(-1), dpatch.reshape(-1, D))
+            h.ready()
+        de = dpatch.to(ctx.edtype).reshape(B * K, D)
+        return de, None, None, None, None, None, None, None
+
+
+def embed_finish(e: torch.Tensor, h_cls, h_wpe, pos: torch.Tensor | None, ids: torch.Tensor, B: int) -> torch.Tensor:
+    h_cls.note_use()
+    if h_wpe is not None:
+        h_wpe.note_use()
+        pos = h_wpe.master
+    return _EmbedFinish.apply(e, h_cls.param, h_wpe.param if h_wpe is not None else None, h_cls, h_wpe,
+                              pos, ids, B)
+
+
+class _Unshuffle(torch.autograd.Function):
+    """Decoder input assembly (K13, pretraining.py:95-106 + modeling.py:289-292) with the mask
+    token's gradient (sum over masked rows) written straight into the flat store."""
+
+    @staticmethod
+    def forward(ctx, y, tok_p, h_tok, ids_restore, pos, C):
+        ids32 = _i32(ids_restore)
+        out = _ext.load().unshuffle_fwd(y.contiguous(), h_tok.master.reshape(-1).contiguous(), ids32,
+                                        pos.contiguous(), C)
+        ctx.save_for_backward(ids32)
+        ctx.h_tok, ctx.C, ctx.K = h_tok, C, y.shape[1] - C
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        (ids32,) = ctx.saved_tensors
+        dy, dtok = _ext.load().unshuffle_bwd(dout.contiguous(), ids32, ctx.C, ctx.K)
+        if ctx.h_tok.segs[0].trainable:
+            ctx.h_tok.accumulate_grad(dtok)
+        return dy, None, None, None, None, None
+
+
+def unshuffle_fused(y: torch.Tensor, h_tok, ids_restore: torch.Tensor, pos: torch.Tensor, num_cls: int):
+    """GPU path of ``unshuffle`` taking the mask-token Handle; falls back to the torch
+    composition (autograd through ``param_value``) elsewhere."""
+    if _ext.use_hip(y) and y.dtype == torch.bfloat16 and y.shape[-1] % 4 == 0 and y.shape[-1] <= 1024:
+        h_tok.note_use()
+        return _Unshuffle.apply(y, h_tok.param, h_tok, ids_restore, pos, num_cls)
+    from .params_fn import param_value
+    return unshuffle(y, param_value(h_tok).view(-1), ids_restore, pos, num_cls)
+
+
+class _PatchMSE(torch.autograd.Function):
+    """Per-patch MSE vs the (optionally per-patch normalized) target computed from uint8 pixels
+    (K14): never materializes the target.  Returns fp32 [B, N]."""
+
+    @staticmethod
+    def forward(ctx, pred, images_u8, patch_size, norm_pix):
+        B = images_u8.shape[0]
+        pred2 = pred.reshape(-1, pred.shape[-1])
+        mse = _ext.load().patch_mse_fwd(pred2, images_u8.contiguous(), patch_size, norm_pix)
+        ctx.save_for_backward(pred2, images_u8)
+        ctx.p, ctx.norm_pix, ctx.pshape = patch_size, norm_pix, pred.shape
+        return mse.view(B, -1)
+
+    @staticmethod
+    def backward(ctx, dmse):
+        pred2, images_u8 = ctx.saved_tensors
+        dpred = _ext.load().patch_mse_bwd(pred2, images_u8.contiguous(), dmse.reshape(-1).contiguous().float(),
+                                          ctx.p, ctx.norm_pix)
+        return dpred.view(ctx.pshape), None, None, None
+
+
+def patch_mse(pred: torch.Tensor, images_u8: torch.Tensor, patch_size: int, norm_pix_loss: bool) -> torch.Tensor:
+    """mean_pix (target - pred)^2 per patch, [B, N] fp32 (utils_mae.py:51-64 before masking)."""
+    B = images_u8.shape[0]
+    if _ext.use_hip(pred) and pred.dtype == torch.bfloat16 and pred.stride(-1) == 1:
+        return _PatchMSE.apply(pred, images_u8, patch_size, bool(norm_pix_loss))
+    t = normalized_patches(images_u8, patch_size)
+    if norm_pix_loss:
+        t = norm_pix(t)
+    return (t - pred.float().view(B, t.shape[1], -1)).square().mean(-1)
+
+
+def masked_mean_loss(per_patch: torch.Tensor, mask: torch.Tensor, per_sample: bool = False) -> torch.Tensor:
+    """patch_mse_loss (utils_mae.py:51-64) from per-patch errors: masked mean per sample, then the
+    batch mean (per_sample=True returns the per-sample values)."""
+    if mask.dim() == 1:
+        mask = mask.unsqueeze(0).expand_as(per_patch)
+    if per_sample:
+        return (per_patch * mask).sum(-1) / mask.sum(-1)
+    valid_ratio = mask.sum(-1) / mask.shape[-1]
+    pp = torch.where(mask > 0.0, per_patch, torch.zeros_like(per_patch))
+    return (pp.mean(-1) / valid_ratio).mean()

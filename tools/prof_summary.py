@@ -6,10 +6,11 @@ cat = {}
 for r in rows:
     n = r["Name"]; t = float(r["TotalDurationNs"]) / 1e6 / steps
     if n.startswith("Cijk") or n.startswith("Custom_Cijk"): k = "GEMM(hipBLASLt)"
-    elif "gemm_nt_kernel" in n or "gemm_tn_kernel" in n: k = "GEMM (ours, MFMA)"
+    elif "gemm_nt" in n or "gemm_tn" in n or "gemm_persist" in n: k = "GEMM (ours, MFMA)"
     elif "attn" in n: k = "attention"
+    elif any(x in n for x in ("patch", "unshuffle", "embed_finish")): k = "mae glue (ours)"
     elif "ln_" in n: k = "layernorm"
-    elif "rowcol" in n or "gelu" in n or "residual" in n: k = "fused elementwise (ours)"
+    elif "rowcol" in n or "gelu" in n or "residual" in n or "splitk" in n or "transpose_bf16" in n: k = "fused elementwise (ours)"
     elif "adamw" in n or "opt" in n.lower() or "sumsq" in n: k = "optimizer"
     elif "at::native" in n: k = "torch native"
     else: k = "other"
