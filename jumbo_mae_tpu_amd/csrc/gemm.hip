@@ -138,7 +138,23 @@ JM_DEVICE void tile_of(int M, int N, int GROUP_M, int& m0, int& n0, int splits =
 // (2) the workgroup streams the tile out row by row, 16 B per lane, 512 B per row: full 128 B
 //     lines instead of 16 rows x 32 B per store instruction.  GELU is applied in (2) to the
 //     rounded pre-activation, which is exactly what the backward will see.
-template <int EPI, int NTW, int NTH, int BNT = BN>
+template <typename T>
+JM_DEVICE void st16(T* p, uint4 v, bool nts) {
+  typedef __attribute__((ext_vector_type(4))) unsigned int u32x4_t;
+  if (nts) __builtin_nontemporal_store(u32x4_t{v.x, v.y, v.z, v.w}, reinterpret_cast<u32x4_t*>(p));
+  else *reinterpret_cast<uint4*>(p) = v;
+}
+
+JM_DEVICE uint4 pack8(const float* f) {
+  uint4 v;
+  v.x = pack_bf2(f[0], f[1]);
+  v.y = pack_bf2(f[2], f[3]);
+  v.z = pack_bf2(f[4], f[5]);
+  v.w = pack_bf2(f[6], f[7]);
+  return v;
+}
+
+template <int EPI, int NTW, int NTH, int BNT = BN, bool NTS = false>
 JM_DEVICE void epilogue_lds(const f32x4_t (&acc)[8][NTW], const GemmEpi& ep, uint16_t* cs, int M, int N, int m0,
                             int n0, int wr, int wc, int l16, int g) {
   constexpr int RB = BNT;  // elements per LDS image row
@@ -179,16 +195,16 @@ JM_DEVICE void epilogue_lds(const f32x4_t (&acc)[8][NTW], const GemmEpi& ep, uin
           f[j] = bf2f(f2bf(bf2f(dg[j]) * gelu_grad_f(hp[j])));
           csum[j] += f[j];
         }
-        store8(ep.out + (long)m * ep.ldo + n0 + c * 8, f);
+        st16(ep.out + (long)m * ep.ldo + n0 + c * 8, pack8(f), NTS);
       } else {
-        *reinterpret_cast<uint4*>(ep.out + (long)m * ep.ldo + n0 + c * 8) = v;
+        st16(ep.out + (long)m * ep.ldo + n0 + c * 8, v, NTS);
       }
       if (EPI == EPI_GELU) {
         float f[8];
         const uint16_t* h = reinterpret_cast<const uint16_t*>(&v);
 #pragma unroll
         for (int j = 0; j < 8; ++j) f[j] = gelu_tanh_f(bf2f(h[j]));
-        store8(ep.out2 + (long)m * ep.ldo + n0 + c * 8, f);
+        st16(ep.out2 + (long)m * ep.ldo + n0 + c * 8, pack8(f), NTS);
       }
     }
   }
@@ -372,7 +388,7 @@ __global__ __launch_bounds__(128 * WN, 1) void gemm_nt_kernel(const uint16_t* __
 // halves (brute-forced over the four lane groups).
 JM_DEVICE int swz64(int row) { return (row >> 1) & 7; }
 
-template <int EPI, bool LATE, bool PRIO>
+template <int EPI, bool LATE, bool PRIO, bool NTS = false>
 __attribute__((always_inline)) JM_DEVICE void nt64_body(const uint16_t* __restrict__ A, long lda,
                                                         const uint16_t* __restrict__ B, long ldb, int M, int N,
                                                         int K, const GemmEpi& ep, int GROUP_M, uint16_t* smem) {
@@ -515,7 +531,7 @@ __attribute__((always_inline)) JM_DEVICE void nt64_body(const uint16_t* __restri
       }
     }
   } else if (N % 8 == 0)
-    epilogue_lds<EPI, NTW, 512>(acc, ep, smem, M, N, m0, n0, wr, wc, l16, g);
+    epilogue_lds<EPI, NTW, 512, BN, NTS>(acc, ep, smem, M, N, m0, n0, wr, wc, l16, g);
   else
     epilogue<EPI, NTW>(acc, ep, M, N, m0 + wr * 128, n0 + wc * NTW * 16, l16, g);
 }
@@ -530,10 +546,10 @@ __global__ __launch_bounds__(512, 1) void gemm_nt64_kernel(const uint16_t* __res
                                                            int K, GemmEpi ep, int GROUP_M) {
   extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
   constexpr bool ST = SCHED & 1, PR = (SCHED & 2) != 0;
-  if (SCHED != 0 && __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) >= 4)
+  if ((SCHED & 3) != 0 && __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) >= 4)
     nt64_body<EPI, ST, PR>(A, lda, B, ldb, M, N, K, ep, GROUP_M, smem);
   else
-    nt64_body<EPI, false, false>(A, lda, B, ldb, M, N, K, ep, GROUP_M, smem);
+    nt64_body<EPI, false, false, (SCHED & 4) != 0>(A, lda, B, ldb, M, N, K, ep, GROUP_M, smem);
 }
 
 // ------------------------------------------------------------------ half-width, 2 WGs per CU
@@ -920,7 +936,9 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_persist_kernel(const uint16_t*
 size_t jm_gemm_smem() { return (size_t)NST * STAGE * sizeof(uint16_t); }
 
 // returns 0 on success, <0 on unsupported shape
-int g_gemm_wn = 6;     // runtime switches for A/B (jm_gemm_set_variant): 6 = 64-deep stages (default),
+int g_gemm_wn = 12;    // runtime switches for A/B (jm_gemm_set_variant): 12 = 64-deep stages + nontemporal
+                       // epilogue stores (default; profiles/r1_gemm_nt_stores.txt), 6 = 64-deep stages,
+                       // 10/11 = 256x128 tiles, 2 WGs per CU (no stagger / stagger),
                        // 4 = 32-deep ring, 2 = 4 waves, 5 = persistent, 4x = ablations
 int g_gemm_group = 8;
 
@@ -992,6 +1010,7 @@ template <int EPI>
 void launch_epi(const uint16_t* A, long lda, const uint16_t* B, long ldb, int M, int N, int K, const GemmEpi& ep,
                 int nwg, hipStream_t st) {
   if (g_gemm_wn == 6) return launch_nt64<EPI, 0>(A, lda, B, ldb, M, N, K, ep, nwg, st);
+  if (g_gemm_wn == 12) return launch_nt64<EPI, 4>(A, lda, B, ldb, M, N, K, ep, nwg, st);
   if (g_gemm_wn == 10) return launch_nth<EPI, false>(A, lda, B, ldb, M, N, K, ep, st);
   if (g_gemm_wn == 11) return launch_nth<EPI, true>(A, lda, B, ldb, M, N, K, ep, st);
   if (g_gemm_wn == 7) return launch_nt64<EPI, 1>(A, lda, B, ldb, M, N, K, ep, nwg, st);

@@ -18,7 +18,7 @@ def ext():
 def _reset_gemm_variant(request):
     yield
     if "ext" in request.fixturenames:
-        request.getfixturevalue("ext").gemm_set_variant(6, 8)
+        request.getfixturevalue("ext").gemm_set_variant(12, 8)
 
 
 def rel(a, b):
@@ -190,7 +190,7 @@ def test_optimizer_hip_matches_torch(kind, clip):
     assert rel(res[0], res[1]) < 1e-5
 
 
-@pytest.mark.parametrize("variant", [4, 2, 5, 6, 7, 8, 10, 11])
+@pytest.mark.parametrize("variant", [4, 2, 5, 6, 7, 8, 10, 11, 12])
 @pytest.mark.parametrize("M,N,K,gelu", [(512, 256, 64, False), (300, 196, 128, True), (1000, 1536, 512, False),
                                         (257, 260, 192, True), (16100, 2048, 128, True), (40000, 520, 64, False)])
 def test_gemm_nt(ext, M, N, K, gelu, variant):
@@ -206,7 +206,7 @@ def test_gemm_nt(ext, M, N, K, gelu, variant):
     if gelu:
         g_ref = torch.nn.functional.gelu(outs[0].float(), approximate="tanh")
         assert rel(outs[1], g_ref) < 1e-2
-    ext.gemm_set_variant(6, 8)
+    ext.gemm_set_variant(12, 8)
 
 
 def test_attention_long_sequence_path():
@@ -228,7 +228,7 @@ def test_attention_long_sequence_path():
     assert rel(dqkv, qr.grad) < 2e-2
 
 
-@pytest.mark.parametrize("variant", [4, 6, 10, 11])
+@pytest.mark.parametrize("variant", [4, 6, 10, 11, 12])
 @pytest.mark.parametrize("M,N,K", [(512, 256, 64), (1000, 1536, 512), (300, 512, 128)])
 def test_gemm_nt_dgelu(ext, M, N, K, variant):
     """FF2 data gradient through the GELU with the FF1 bias gradient (csrc/gemm.hip EPI_DGELU)."""
@@ -288,7 +288,7 @@ def test_residual_ln_fwd(ext, T0, with_scale):
     assert torch.allclose(mu, mur, atol=1e-6) and torch.allclose(rs, rsr, rtol=1e-5)
 
 
-@pytest.mark.parametrize("variant", [4, 6, 10, 11])
+@pytest.mark.parametrize("variant", [4, 6, 10, 11, 12])
 @pytest.mark.parametrize("M,N,K,S", [(512, 3072, 12288, 10), (300, 512, 4096, 3), (512, 256, 1024, 16)])
 def test_gemm_nt_splitk(ext, M, N, K, S, variant):
     """Split-K MFMA GEMM (fp32 partial tiles + bf16 reduce with bias), ragged M."""

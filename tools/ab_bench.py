@@ -5,7 +5,7 @@
 Each config is a list of ``KEY=VALUE`` switches applied to ``ops.prims`` module state between
 rounds (same model, same data, same device -> no cross-process / cross-device variance).
 Supported keys: JMAE_GEMM (auto|blas|ours), JMAE_DGRAD (0|1), JMAE_WGRAD (0|1), JMAE_WGRAD_STREAM (0|1),
-GEMM_VARIANT (6 default, 4 = 32-deep ring, 5 = persistent).
+GEMM_VARIANT (12 default, 6 = plain stores, 4 = 32-deep ring, 5 = persistent).
 Prints per-config median / min ms per step."""
 
 import argparse
