@@ -12,6 +12,12 @@ RCCL gradient all-reduce, optimizer update.
 
   python bench.py [--gpus N] [--steps K] [--warmup W]
   torchrun --nproc-per-node N bench.py --gpus N ...   (driver launches N>1 like this)
+
+Secondary BASELINE.json configs (not the headline): ``--task finetune`` = ViT-B/16 end-to-end
+finetune with the config/ft.sh recipe (AdamW + LLRD 0.75, Mixup 0.8 / CutMix 1.0, label
+smoothing 0.1, droppath 0.1; global batch 1024 = 128 per GPU at 8 GPUs); ``--task linear`` =
+ViT-L/16 linear probe with the LARS recipe (frozen encoder, SyncBatchNorm + Dense head; global
+batch 16384 = 2048 per GPU at 8 GPUs).  Same synthetic-data / timing contract.
 """
 
 from __future__ import annotations
@@ -41,7 +47,10 @@ def main():
     ap.add_argument("--bucket-mb", type=float, default=64.0)
     ap.add_argument("--no-overlap", action="store_true")
     ap.add_argument("--profile-steps", type=int, default=0, help="extra steps under torch.profiler (debug)")
+    ap.add_argument("--task", default="pretrain", choices=["pretrain", "finetune", "linear"])
     args = ap.parse_args()
+    if args.task != "pretrain":
+        return bench_classifier(args)
 
     from jumbo_mae_tpu_amd.config import decoder_config, vit_config
     from jumbo_mae_tpu_amd.models.mae import PretrainModel
@@ -154,6 +163,93 @@ def main():
             },
         }
         print(json.dumps(out), flush=True)
+    pdist.cleanup()
+
+
+def bench_classifier(args):
+    """Finetune (ViT-B/16, config/ft.sh) or linear probe (ViT-L/16, LARS preset) step throughput."""
+    from jumbo_mae_tpu_amd.parallel import dist as pdist
+    from jumbo_mae_tpu_amd.train import common as C
+    from jumbo_mae_tpu_amd.train.cli import finetune_parser
+    from jumbo_mae_tpu_amd.train.engine import Trainer
+    from jumbo_mae_tpu_amd.train.finetune import build_model
+    from jumbo_mae_tpu_amd.utils.flops import finetune_fwd_flops_per_image, mfu
+    from jumbo_mae_tpu_amd.utils.rng import RngStreams
+
+    info = pdist.init_distributed()
+    dev = info.device
+    world = info.world_size
+    N = 1281167
+    if args.task == "finetune":
+        B = args.batch_per_gpu if args.batch_per_gpu != 512 else 128
+        gb = B * world
+        flags = ["--mode", "finetune", "--layers", "12", "--dim", "768", "--heads", "12", "--labels", "1000",
+                 "--posemb", "sincos2d", "--droppath", "0.1", "--mixup", "0.8", "--cutmix", "1.0",
+                 "--label-smoothing", "0.1", "--optimizer", "adamw", "--learning-rate", "3e-3",
+                 "--weight-decay", "0.05", "--lr-decay", "0.75", "--warmup-steps", str(N * 10 // 1024),
+                 "--training-steps", str(N * 110 // 1024)]
+        model_name, recipe = "vit_base_patch16 jumbo (3 CLS) finetune", "adamw llrd0.75 mixup0.8 cutmix1.0 ls0.1 dp0.1"
+    else:
+        B = args.batch_per_gpu if args.batch_per_gpu != 512 else 2048
+        gb = B * world
+        flags = ["--mode", "linear", "--layers", "24", "--dim", "1024", "--heads", "16", "--labels", "1000",
+                 "--posemb", "sincos2d", "--droppath", "0.0", "--mixup", "0.0", "--cutmix", "0.0",
+                 "--label-smoothing", "0.0", "--optimizer", "lars", "--learning-rate", "0.1",
+                 "--weight-decay", "0.0", "--warmup-steps", str(N * 10 // 16384),
+                 "--training-steps", str(N * 90 // 16384)]
+        model_name, recipe = "vit_large_patch16 jumbo (3 CLS) linear probe", "lars syncbn-head"
+    fargs = finetune_parser().parse_args(flags + ["--train-batch-size", str(gb), "--bucket-mb", str(args.bucket_mb)])
+    model = build_model(fargs, dev, torch.bfloat16, info.rank)
+    pdist.broadcast_(model.store.master)
+    model.store.sync_shadow()
+    peak = fargs.learning_rate * gb / 256 if fargs.optimizer == "lars" else fargs.learning_rate
+    opt = C.make_optimizer(fargs, model.store, peak, 1e-6)
+    reducer = C.make_reducer(fargs, model.store)
+    rngs = RngStreams({"mixup": 1, "dropout": 1, "noise": 1}, info.rank, dev)
+    trainer = Trainer(model, opt, reducer, rngs)
+    gen = torch.Generator(device=dev).manual_seed(1234 + info.rank)
+    pool = [(torch.randint(0, 256, (B, 3, 224, 224), dtype=torch.uint8, device=dev, generator=gen),
+             torch.randint(0, 1000, (B,), device=dev, generator=gen)) for _ in range(2)]
+    if info.is_main:
+        log(f"[bench] task={args.task} params={model.store.num_params()/1e6:.1f}M "
+            f"trainable={model.store.num_params(True)/1e6:.2f}M world={world} batch/gpu={B}")
+    it = 0
+
+    def step():
+        nonlocal it
+        m = trainer.train_step([pool[it % 2]])
+        it += 1
+        return m
+
+    for i in range(args.warmup):
+        m = step()
+        if info.is_main:
+            torch.cuda.synchronize()
+            log(f"[bench] warmup {i + 1}/{args.warmup} loss={m['loss'].item():.4f}")
+    pdist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        m = step()
+    pdist.barrier()
+    torch.cuda.synchronize()
+    elapsed = pdist.all_reduce_max_scalar(time.perf_counter() - t0, dev)
+    value = gb * args.steps / elapsed
+    fwd = finetune_fwd_flops_per_image(model.cfg)
+    util = mfu(value, fwd, world) if args.task == "finetune" else mfu(value, fwd, world) / 3.0
+    if info.is_main:
+        print(json.dumps({
+            "metric": f"{args.task} images/sec (whole node) " + ("ViT-B/16" if args.task == "finetune" else "ViT-L/16")
+            + " 224",
+            "value": round(value, 2), "unit": "images/sec", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1000.0, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "mfu_bf16_dense": round(util, 4), "dtype": "bf16",
+            "data": "synthetic uint8 224x224 images + random labels on GPU, random-init weights",
+            "config": {"model": model_name, "global_batch": gb, "seq_len": model.cfg.num_cls_tokens
+                       + model.cfg.seq_patches, "parallelism": f"dp{world}", "per_gpu_batch": B,
+                       "recipe": recipe, "final_loss": round(float(m["loss"].item()), 5)},
+        }), flush=True)
     pdist.cleanup()
 
 
