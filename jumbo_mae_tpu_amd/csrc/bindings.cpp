@@ -72,6 +72,8 @@ int jm_unshuffle_fwd(const uint16_t* y, const float* tok, const int* restore, lo
 int jm_unshuffle_bwd_blocks(int B, int C, int N, int rows_per_block);
 int jm_unshuffle_bwd(const float* dout, const int* restore, long rsB, uint16_t* dy, float* part, int B, int C, int K,
                      int N, int d, int rows_per_block, hipStream_t st);
+int jm_mix_patches(const uint8_t* img, const int* perm, uint16_t* out, int B, int H, int W, int p, int mode, float r,
+                   int y0, int y1, int x0, int x1, hipStream_t st);
 int jm_patch_mse_fwd(const uint16_t* pred, long ldp, const uint8_t* img, float* mse, long rows, int N, int H, int W,
                      int p, int norm_pix, hipStream_t st);
 int jm_patch_mse_bwd(const uint16_t* pred, long ldp, const uint8_t* img, const float* dmse, uint16_t* dpred, long rows,
@@ -467,6 +469,27 @@ std::vector<torch::Tensor> unshuffle_bwd(torch::Tensor dout, torch::Tensor ids_r
   return {dy, part.sum(0)};
 }
 
+// finetune input: [B*N, 3p^2] bf16 normalized patches of the (Mixup / CutMix) blended batch
+torch::Tensor mix_patches(torch::Tensor img, c10::optional<torch::Tensor> perm, int64_t p, int64_t mode, double ratio,
+                          std::vector<int64_t> box) {
+  CHECK_CONTIG(img);
+  CHECK_DT(img, torch::kUInt8);
+  TORCH_CHECK(img.size(1) == 3 && box.size() == 4, "mix_patches: 3 channels, box (y0, y1, x0, x1)");
+  const int B = img.size(0), H = img.size(2), W = img.size(3);
+  const int* pp = nullptr;
+  if (perm) {
+    CHECK_DT((*perm), torch::kInt32);
+    CHECK_CONTIG((*perm));
+    TORCH_CHECK(perm->numel() == B, "perm size");
+    pp = perm->data_ptr<int>();
+  }
+  auto out = torch::empty({(long)B * (H / p) * (W / p), 3 * p * p}, img.options().dtype(torch::kBFloat16));
+  check_rc(jm_mix_patches(img.data_ptr<uint8_t>(), pp, bfp(out), B, H, W, p, mode, (float)ratio, box[0], box[1], box[2],
+                          box[3], stream()),
+           "mix_patches");
+  return out;
+}
+
 // pred: bf16 [B*N, P3] (row stride may exceed P3); -> per-patch MSE fp32 [B*N]
 torch::Tensor patch_mse_fwd(torch::Tensor pred, torch::Tensor img, int64_t p, bool norm_pix) {
   CHECK_DT(pred, torch::kBFloat16);
@@ -502,7 +525,8 @@ torch::Tensor patch_mse_bwd(torch::Tensor pred, torch::Tensor img, torch::Tensor
 // ------------------------------------------------------------------------------ GEMM
 // C[M, N] = A[M, K] . B[N, K]^T (+ bias) in bf16 (fp32 accumulate); gelu=true also returns
 // gelu(C) (the pre-activation C is what the backward needs).  A / B rows may be strided.
-std::vector<torch::Tensor> gemm_nt(torch::Tensor A, torch::Tensor B, c10::optional<torch::Tensor> bias, bool gelu) {
+std::vector<torch::Tensor> gemm_nt(torch::Tensor A, torch::Tensor B, c10::optional<torch::Tensor> bias, bool gelu,
+                                   bool gelu_only) {
   CHECK_DT(A, torch::kBFloat16);
   CHECK_DT(B, torch::kBFloat16);
   TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && A.size(1) == B.size(1), "gemm_nt: A [M,K], B [N,K]");
@@ -515,12 +539,13 @@ std::vector<torch::Tensor> gemm_nt(torch::Tensor A, torch::Tensor B, c10::option
     TORCH_CHECK(bias->is_contiguous() && bias->scalar_type() == torch::kFloat32 && bias->numel() == N, "gemm_nt bias");
     ep.bias = bias->data_ptr<float>();
   }
-  if (gelu) {
+  if (gelu && !gelu_only) {
     out2 = torch::empty({M, N}, A.options());
     ep.out2 = bfm(out2);
   }
-  check_rc(jm_gemm_nt(bf(A), A.stride(0), bf(B), B.stride(0), M, N, K, gelu ? 1 : 0, ep, stream()), "gemm_nt");
-  if (gelu) return {out, out2};
+  const int epi = gelu_only ? 4 : (gelu ? 1 : 0);
+  check_rc(jm_gemm_nt(bf(A), A.stride(0), bf(B), B.stride(0), M, N, K, epi, ep, stream()), "gemm_nt");
+  if (gelu && !gelu_only) return {out, out2};
   return {out};
 }
 
@@ -655,7 +680,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("gemm_nt_splitk", &gemm_nt_splitk, py::arg("A"), py::arg("B"), py::arg("bias") = py::none(),
         py::arg("splits") = 8);
   m.def("gemm_nt_dgelu", &gemm_nt_dgelu, py::arg("A"), py::arg("B"), py::arg("pre"), py::arg("dbias") = py::none());
-  m.def("gemm_nt", &gemm_nt, py::arg("A"), py::arg("B"), py::arg("bias") = py::none(), py::arg("gelu") = false);
+  m.def("gemm_nt", &gemm_nt, py::arg("A"), py::arg("B"), py::arg("bias") = py::none(), py::arg("gelu") = false,
+        py::arg("gelu_only") = false);
   m.def("attn_set_tr", &jm_attn_set_tr);
   m.def("opt_sumsq", &opt_sumsq);
   m.def("opt_adamw", &opt_adamw);
@@ -669,5 +695,6 @@ PYBIND11_MODULE(_C, m) {
   m.def("unshuffle_fwd", &unshuffle_fwd);
   m.def("unshuffle_bwd", &unshuffle_bwd);
   m.def("patch_mse_fwd", &patch_mse_fwd);
+  m.def("mix_patches", &mix_patches);
   m.def("patch_mse_bwd", &patch_mse_bwd);
 }

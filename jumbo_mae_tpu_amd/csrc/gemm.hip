@@ -79,7 +79,9 @@ struct GemmEpi {
 // EPI_PARTIAL: split-K -- each (tile, split) workgroup stores its fp32 partial tile; the sum (+bias,
 // bf16) is taken by jm_splitk_reduce_bf16.  For small-M, long-K GEMMs (the jumbo MLP: 512 rows,
 // K = 12288) whose 24 output tiles would otherwise occupy 24 of 256 CUs.
-enum { EPI_STORE = 0, EPI_GELU = 1, EPI_DGELU = 2, EPI_PARTIAL = 3 };
+// EPI_GELU_ONLY: out = gelu(bf16(acc + bias)) alone -- inference (no backward needs the
+// pre-activation), half the epilogue bytes of EPI_GELU.
+enum { EPI_STORE = 0, EPI_GELU = 1, EPI_DGELU = 2, EPI_PARTIAL = 3, EPI_GELU_ONLY = 4 };
 
 namespace {
 
@@ -100,6 +102,10 @@ JM_DEVICE void epilogue(const f32x4_t (&acc)[8][NTW], const GemmEpi& ep, int M, 
       float v[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) v[i] = acc[mt][nt][i] + bv[i];
+      if (EPI == EPI_GELU_ONLY) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[i] = gelu_tanh_f(bf2f(f2bf(v[i])));
+      }
       store4(ep.out + (long)m * ep.ldo + n, v);
       if (EPI == EPI_GELU) {
         float gv[4];
@@ -195,6 +201,12 @@ JM_DEVICE void epilogue_lds(const f32x4_t (&acc)[8][NTW], const GemmEpi& ep, uin
           f[j] = bf2f(f2bf(bf2f(dg[j]) * gelu_grad_f(hp[j])));
           csum[j] += f[j];
         }
+        st16(ep.out + (long)m * ep.ldo + n0 + c * 8, pack8(f), NTS);
+      } else if (EPI == EPI_GELU_ONLY) {
+        float f[8];
+        const uint16_t* h = reinterpret_cast<const uint16_t*>(&v);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) f[j] = gelu_tanh_f(bf2f(h[j]));
         st16(ep.out + (long)m * ep.ldo + n0 + c * 8, pack8(f), NTS);
       } else {
         st16(ep.out + (long)m * ep.ldo + n0 + c * 8, v, NTS);
@@ -1053,6 +1065,8 @@ int jm_gemm_nt(const uint16_t* A, long lda, const uint16_t* B, long ldb, int M, 
     launch_epi<EPI_STORE>(A, lda, B, ldb, M, N, K, ep, nwg, st);
   else if (epi == EPI_GELU)
     launch_epi<EPI_GELU>(A, lda, B, ldb, M, N, K, ep, nwg, st);
+  else if (epi == EPI_GELU_ONLY)
+    launch_epi<EPI_GELU_ONLY>(A, lda, B, ldb, M, N, K, ep, nwg, st);
   else if (epi == EPI_DGELU && N % 8 == 0)
     launch_epi<EPI_DGELU>(A, lda, B, ldb, M, N, K, ep, nwg, st);
   else

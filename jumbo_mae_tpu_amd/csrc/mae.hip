@@ -365,3 +365,52 @@ int jm_patch_mse_bwd(const uint16_t* pred, long ldp, const uint8_t* img, const f
     patch_mse_bwd_kernel<16, false><<<nb, 256, 0, st>>>(pred, ldp, img, dmse, dpred, rows, N, H, W, p, norm_pix);
   return 0;
 }
+
+// ----------------------------------------------------------------------------------------------
+// K19 (finetune input): all patches of the normalized, Mixup- or CutMix-blended batch as the bf16
+// patch-embed operand [B*N, 3p^2], straight from uint8 (utils.py:66-111 semantics):
+//   mode 0: x[b];  mode 1 (mixup): r x[b] + (1 - r) x[perm[b]];
+//   mode 2 (cutmix): x[perm[b]] inside the pixel box [y0, y1) x [x0, x1), else x[b].
+namespace {
+__global__ __launch_bounds__(256) void mix_patches_kernel(const uint8_t* __restrict__ img, const int* __restrict__ perm,
+                                                          uint16_t* __restrict__ out, int B, int H, int W, int p,
+                                                          int mode, float r, int y0, int y1, int x0, int x1) {
+  const int P3 = 3 * p * p, q = P3 / 4, g = W / p, N = (H / p) * g;
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (long)B * N * q) return;
+  const long row = i / q;
+  const int o0 = (int)(i - row * q) * 4;
+  const int b = (int)(row / N), n = (int)(row - (long)b * N);
+  const int gy = n / g, gx = n - (n / g) * g;
+  const int bo = mode ? perm[b] : b;
+  float f[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int o = o0 + j;
+    const int ph = o / (3 * p);
+    const int rr = o - ph * 3 * p;
+    const int pw = rr / 3, c = rr - (rr / 3) * 3;
+    const int y = gy * p + ph, x = gx * p + pw;
+    const float a = patch_pixel(img, b, H, W, p, gy, gx, o);
+    if (mode == 1) {
+      f[j] = r * a + (1.f - r) * patch_pixel(img, bo, H, W, p, gy, gx, o);
+    } else if (mode == 2 && y >= y0 && y < y1 && x >= x0 && x < x1) {
+      f[j] = patch_pixel(img, bo, H, W, p, gy, gx, o);
+    } else {
+      f[j] = a;
+    }
+    (void)c;
+  }
+  store4(out + row * P3 + o0, f);
+}
+}  // namespace
+
+int jm_mix_patches(const uint8_t* img, const int* perm, uint16_t* out, int B, int H, int W, int p, int mode, float r,
+                   int y0, int y1, int x0, int x1, hipStream_t st) {
+  if ((3 * p * p) % 4 || H % p || W % p) return -1;
+  if (mode != 0 && perm == nullptr) return -2;
+  const long n = (long)B * (H / p) * (W / p) * (3 * p * p / 4);
+  if (n == 0) return 0;
+  mix_patches_kernel<<<cdiv(n, 256), 256, 0, st>>>(img, perm, out, B, H, W, p, mode, r, y0, y1, x0, x1);
+  return 0;
+}

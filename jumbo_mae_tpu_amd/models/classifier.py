@@ -22,7 +22,6 @@ import torch.nn.functional as F
 from ..config import ViTConfig
 from ..ops import functional as Fn
 from ..ops import mae as mae_ops
-from ..utils.mae import extract_patches_nchw
 from ..utils.mixup import Mixup, smooth_labels
 from .params import ParamStore
 from .vit import JumboViT, LinearCLS
@@ -67,30 +66,34 @@ class FinetuneModel:
 
     # ---------------------------------------------------------------- pieces
     def patches(self, images_u8, labels, rngs, det):
-        p = self.cfg.patch_size
-        if det or not self.mixup.active:
-            return mae_ops.normalized_patches(images_u8, p), labels
-        x = mae_ops.normalize_images(images_u8)
-        x, labels = self.mixup(x, labels, rngs.get("mixup") if rngs else None)
-        return extract_patches_nchw(x, p).contiguous(), labels
+        """(patch rows [B*N, p*p*3] in the compute dtype, labels) -- Mixup / CutMix applied when
+        training (one plan per batch; the blend is fused into the patch gather on the GPU)."""
+        B, _, H, W = images_u8.shape
+        plan = None
+        if not det and self.mixup.active:
+            plan = self.mixup.plan(B, H, W, images_u8.device, rngs.get("mixup") if rngs else None)
+        if labels is not None:
+            labels = Mixup.mix_labels(labels, plan)
+        rows = mae_ops.mixed_patches(images_u8, plan, self.cfg.patch_size, self.store.compute_dtype)
+        return rows, labels
 
-    def features(self, patches, rngs=None, det=True):
+    def features(self, rows, B, rngs=None, det=True):
         cfg = self.cfg
-        B = patches.shape[0]
         drop = rngs.get("dropout") if rngs else None
-        x = self.encoder.embed(patches, None)
+        x = self.encoder.embed_rows(rows, None, B)
         x = self.encoder.blocks(x, drop, det)
         C = cfg.num_cls_tokens
         h = Fn.layer_norm(x[:, :C], self.encoder.norm.g, self.encoder.norm.b, torch.float32)
         return h.reshape(B, C * cfg.dim)
 
     def logits(self, images_u8, labels=None, rngs=None, det=True):
-        patches, labels = self.patches(images_u8, labels, rngs, det)
+        B = images_u8.shape[0]
+        rows, labels = self.patches(images_u8, labels, rngs, det)
         if self.cfg.linear_probing:
             with torch.no_grad():
-                feats = self.features(patches, rngs, det)
+                feats = self.features(rows, B, rngs, det)
         else:
-            feats = self.features(patches, rngs, det)
+            feats = self.features(rows, B, rngs, det)
         return self.head(feats, det, self.group), labels
 
     # ---------------------------------------------------------------- train / eval

@@ -69,8 +69,8 @@ def _attn_bwd(attn, da, h1, qkv, o, lse, B, S, wo_bias_done=False):
     return P.linear_bwd(dqkv.view(B * S, -1), h1, attn.qkv_k, attn.qkv_b, bias_done=bd)
 
 
-def _ff_fwd(ff, h):
-    pre, g = P.linear_gelu_fwd(h, ff.w1.k, ff.w1.b)
+def _ff_fwd(ff, h, train=True):
+    pre, g = P.linear_gelu_fwd(h, ff.w1.k, ff.w1.b, need_pre=train)
     y = P.linear_fwd(g, ff.w2.k, ff.w2.b)
     return pre, g, y
 
@@ -97,7 +97,7 @@ def _ff_handles(ff):
 
 class JumboBlockFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, anchor, layer, m1, m2, m3, link_in, link_out):
+    def forward(ctx, x, anchor, layer, m1, m2, m3, link_in, link_out, train=True):
         B, S, D = x.shape
         C = layer.C
         J = C * D
@@ -110,10 +110,10 @@ class JumboBlockFn(torch.autograd.Function):
         cls_in = x1[:, :C].reshape(B, 1, J)
         hc, muc, rsc = P.ln_fwd(cls_in, layer.norm3.g, layer.norm3.b, torch.float32)
         hcb = hc.to(dt)
-        jpre, jg, jy = _ff_fwd(layer.jumbo_mlp, hcb)
+        jpre, jg, jy = _ff_fwd(layer.jumbo_mlp, hcb, train)
         # patch branch
         pin = x1[:, C:]
-        fpre, fg, fy = _ff_fwd(layer.ff, hp)
+        fpre, fg, fy = _ff_fwd(layer.ff, hp, train)
         x2 = torch.empty_like(x1)
         P.residual_fwd(hc.view(B, 1, J), jy, layer.scale3, m3, out=x2[:, :C].reshape(B, 1, J))
         P.residual_fwd(pin, fy, layer.scale2, m2, out=x2[:, C:])
@@ -164,7 +164,7 @@ class JumboBlockFn(torch.autograd.Function):
         # ---- attention branch: dx = dx1 + LN1'(Attn'(s1 * dp1 * dx1))
         dh1 = _attn_bwd(layer.attn, da, h1, qkv, o, lse, B, S, bd)
         dx = _ln1_bwd(ctx, dh1, x, mu1, rs1, layer, dx1)
-        return dx, None, None, None, None, None, None, None
+        return dx, None, None, None, None, None, None, None, None
 
 
 def _ln1_bwd(ctx, dh1, x, mu1, rs1, layer, dx1):
@@ -183,18 +183,19 @@ def jumbo_block(layer, x, m1=None, m2=None, m3=None, link_in: Link | None = None
     _note_uses(layer.norm1.g, layer.norm1.b, layer.norm2.g, layer.norm2.b, layer.norm3.g, layer.norm3.b,
                layer.scale1, layer.scale2, layer.scale3, *_attn_handles(layer.attn), *_ff_handles(layer.ff),
                *_ff_handles(layer.jumbo_mlp))
-    return JumboBlockFn.apply(x.contiguous(), layer.norm1.g.param, layer, m1, m2, m3, link_in, link_out)
+    return JumboBlockFn.apply(x.contiguous(), layer.norm1.g.param, layer, m1, m2, m3, link_in, link_out,
+                              torch.is_grad_enabled())
 
 
 class ViTBlockFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, anchor, layer, m1, m2, link_in, link_out):
+    def forward(ctx, x, anchor, layer, m1, m2, link_in, link_out, train=True):
         B, S, D = x.shape
         dt = layer.norm1.g.store.compute_dtype
         h1, mu1, rs1 = P.ln_fwd(x, layer.norm1.g, layer.norm1.b, dt)
         qkv, o, lse, a = _attn_fwd(layer.attn, h1, B, S)
         x1, h2, mu2, rs2 = P.residual_ln_fwd(x, a, layer.scale1, m1, layer.norm2.g, layer.norm2.b, 0)
-        fpre, fg, fy = _ff_fwd(layer.ff, h2)
+        fpre, fg, fy = _ff_fwd(layer.ff, h2, train)
         x2 = P.residual_fwd(x1, fy, layer.scale2, m2)
         ctx.save_for_backward(x, mu1, rs1, h1, qkv, o, lse, a, x1, mu2, rs2, h2, fpre, fg, fy, m1, m2)
         ctx.layer = layer
@@ -221,10 +222,11 @@ class ViTBlockFn(torch.autograd.Function):
                                res=P.ResSpec(a, layer.scale1, m1, layer.attn.wo_b))
         dh1 = _attn_bwd(layer.attn, da, h1, qkv, o, lse, B, S, bd)
         dx = _ln1_bwd(ctx, dh1, x, mu1, rs1, layer, dx1)
-        return dx, None, None, None, None, None, None
+        return dx, None, None, None, None, None, None, None
 
 
 def vit_block(layer, x, m1=None, m2=None, link_in: Link | None = None, link_out: Link | None = None):
     _note_uses(layer.norm1.g, layer.norm1.b, layer.norm2.g, layer.norm2.b, layer.scale1, layer.scale2,
                *_attn_handles(layer.attn), *_ff_handles(layer.ff))
-    return ViTBlockFn.apply(x.contiguous(), layer.norm1.g.param, layer, m1, m2, link_in, link_out)
+    return ViTBlockFn.apply(x.contiguous(), layer.norm1.g.param, layer, m1, m2, link_in, link_out,
+                            torch.is_grad_enabled())

@@ -216,3 +216,21 @@ def masked_mean_loss(per_patch: torch.Tensor, mask: torch.Tensor, per_sample: bo
     valid_ratio = mask.sum(-1) / mask.shape[-1]
     pp = torch.where(mask > 0.0, per_patch, torch.zeros_like(per_patch))
     return (pp.mean(-1) / valid_ratio).mean()
+
+
+def mixed_patches(images_u8: torch.Tensor, plan: dict | None, patch_size: int, dtype) -> torch.Tensor:
+    """All patches of the normalized (Mixup / CutMix blended, ``utils.mixup.Mixup.plan``) batch as
+    the patch-embed GEMM operand [B*N, p*p*3].  GPU: one HIP kernel from uint8 (K19 fused with
+    K1); CPU: normalize -> blend -> patchify in torch."""
+    from ..utils.mixup import Mixup
+
+    B = images_u8.shape[0]
+    if _ext.use_hip(images_u8) and dtype == torch.bfloat16:
+        if plan is None:
+            return _ext.load().mix_patches(images_u8.contiguous(), None, patch_size, 0, 1.0, [0, 0, 0, 0])
+        mode = 1 if plan["mode"] == "mixup" else 2
+        box = list(plan["box"]) if plan["box"] is not None else [0, 0, 0, 0]
+        return _ext.load().mix_patches(images_u8.contiguous(), _i32(plan["perm"]), patch_size, mode,
+                                       float(plan["ratio"]), box)
+    x = Mixup.mix_images(normalize_images(images_u8), plan)
+    return extract_patches_nchw(x, patch_size).reshape(B * (x.shape[-1] // patch_size) ** 2, -1).to(dtype)

@@ -144,10 +144,14 @@ def linear_fwd(x2: torch.Tensor, hw: Handle, hb: Handle | None) -> torch.Tensor:
     return x2 @ w.t()
 
 
-def linear_gelu_fwd(x2: torch.Tensor, hw: Handle, hb: Handle | None):
-    """(pre, gelu(pre)) of a Dense followed by the tanh GELU; one fused GEMM when it pays."""
+def linear_gelu_fwd(x2: torch.Tensor, hw: Handle, hb: Handle | None, need_pre: bool = True):
+    """(pre, gelu(pre)) of a Dense followed by the tanh GELU; one fused GEMM when it pays.
+    ``need_pre=False`` (inference: no backward will read it) returns (None, gelu) and the fused
+    epilogue writes only the activation."""
     w = hw.weight()
     if hip(x2) and x2.dtype == torch.bfloat16 and use_our_gemm(x2.shape[0], w.shape[0], x2.shape[1], True):
+        if not need_pre:
+            return None, _ext.load().gemm_nt(x2, w, hb.master if hb is not None else None, True, True)[0]
         pre, g = _ext.load().gemm_nt(x2, w, hb.master if hb is not None else None, True)
         return pre, g
     pre = linear_fwd(x2, hw, hb)

@@ -35,39 +35,71 @@ class Mixup:
     def _perm(self, n, device, gen):
         return torch.randperm(n, device=device, generator=gen)
 
-    def apply_mixup(self, images, labels, gen=None):
-        ratio = float(self.rs.beta(self.mixup_alpha, self.mixup_alpha))
-        perm = self._perm(images.shape[0], images.device, gen)
-        images = ratio * images + (1 - ratio) * images[perm]
-        labels = ratio * labels + (1 - ratio) * labels[perm]
-        return images, labels
+    # ---------------------------------------------------------------- batch plan
+    def plan(self, batch: int, height: int, width: int, device, gen=None) -> dict | None:
+        """Draw this batch's mixing decision (same RNG consumption order as the reference's
+        Mixup.__call__): ``{"mode": "mixup"|"cutmix", "ratio", "perm", "box"}`` where ``box`` =
+        (y0, y1, x0, x1) is the half-open pixel range taken from the permuted image and
+        ``label_w`` the weight of the own label.  None when mixing is off."""
+        if self.mixup_alpha == 0 and self.cutmix_alpha == 0:
+            return None
+        if self.mixup_alpha > 0 and self.cutmix_alpha > 0:
+            mode = "mixup" if self.rs.uniform() > 0.5 else "cutmix"
+        else:
+            mode = "mixup" if self.mixup_alpha > 0 else "cutmix"
+        if mode == "mixup":
+            ratio = float(self.rs.beta(self.mixup_alpha, self.mixup_alpha))
+            perm = self._perm(batch, device, gen)
+            return {"mode": mode, "ratio": ratio, "perm": perm, "box": None, "label_w": ratio}
+        ratio = float(self.rs.beta(self.cutmix_alpha, self.cutmix_alpha))
+        box = self._box(ratio, width, height)
+        perm = self._perm(batch, device, gen)
+        y0, y1, x0, x1 = box
+        label_w = 1.0 - float((y1 - y0) * (x1 - x0)) / float(height * width)
+        return {"mode": mode, "ratio": ratio, "perm": perm, "box": box, "label_w": label_w}
 
-    def random_bounding_box(self, ratio: float, width: int, height: int, device) -> torch.Tensor:
+    def _box(self, ratio: float, width: int, height: int):
+        """Pixel ranges of the CutMix box on the reference's linspace(0, 1, W|H) grid
+        (evaluated with torch's fp32 linspace so the edges match the mask formulation)."""
         size = (1 - ratio) ** 0.5
         xstart, ystart = self.rs.uniform(size=2)
-        xr = torch.linspace(0, 1, width, device=device)
-        yr = torch.linspace(0, 1, height, device=device)
-        xm = (xstart - 0.5 * size <= xr) & (xr < xstart + 0.5 * size)
-        ym = (ystart - 0.5 * size <= yr) & (yr < ystart + 0.5 * size)
-        return ~(ym[:, None] & xm[None, :])  # [H, W], True = keep own image
 
-    def apply_cutmix(self, images, labels, gen=None):
-        ratio = float(self.rs.beta(self.cutmix_alpha, self.cutmix_alpha))
+        def rng(start, n):
+            r = torch.linspace(0, 1, n)
+            inside = ((start - 0.5 * size <= r) & (r < start + 0.5 * size)).nonzero().flatten()
+            if inside.numel() == 0:
+                return 0, 0
+            return int(inside[0]), int(inside[-1]) + 1
+
+        x0, x1 = rng(xstart, width)
+        y0, y1 = rng(ystart, height)
+        if x0 == x1 or y0 == y1:
+            return 0, 0, 0, 0
+        return y0, y1, x0, x1
+
+    @staticmethod
+    def mix_labels(labels, plan):
+        if plan is None:
+            return labels
+        w = plan["label_w"]
+        return w * labels + (1 - w) * labels[plan["perm"]]
+
+    @staticmethod
+    def mix_images(images, plan):
+        """NCHW float images mixed per ``plan`` (torch composition; the HIP path fuses this into
+        the patch gather, ops/mae.py mixed_patches)."""
+        if plan is None:
+            return images
+        other = images[plan["perm"]]
+        if plan["mode"] == "mixup":
+            r = plan["ratio"]
+            return r * images + (1 - r) * other
+        y0, y1, x0, x1 = plan["box"]
         H, W = images.shape[-2:]
-        m = self.random_bounding_box(ratio, W, H, images.device).to(images.dtype)
-        label_w = m.mean()
-        perm = self._perm(images.shape[0], images.device, gen)
-        images = m * images + (1 - m) * images[perm]
-        labels = label_w * labels + (1 - label_w) * labels[perm]
-        return images, labels
+        keep = torch.ones((H, W), dtype=images.dtype, device=images.device)
+        keep[y0:y1, x0:x1] = 0
+        return keep * images + (1 - keep) * other
 
     def __call__(self, images, labels, gen=None):
-        if self.mixup_alpha == 0 and self.cutmix_alpha == 0:
-            return images, labels
-        if self.mixup_alpha > 0 and self.cutmix_alpha == 0:
-            return self.apply_mixup(images, labels, gen)
-        if self.mixup_alpha == 0 and self.cutmix_alpha > 0:
-            return self.apply_cutmix(images, labels, gen)
-        if self.rs.uniform() > 0.5:
-            return self.apply_mixup(images, labels, gen)
-        return self.apply_cutmix(images, labels, gen)
+        plan = self.plan(images.shape[0], images.shape[-2], images.shape[-1], images.device, gen)
+        return self.mix_images(images, plan), self.mix_labels(labels, plan)

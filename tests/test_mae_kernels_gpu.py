@@ -148,3 +148,51 @@ def test_pretrain_fused_glue_matches_torch_path(mask_mode, norm_pix, monkeypatch
         grads.append(model.store.grad.clone())
     assert abs(losses[0] - losses[1]) < 1e-3 * abs(losses[1])
     assert rel(grads[0], grads[1]) < 2e-2
+
+
+@pytest.mark.parametrize("M,N,K", [(1000, 1536, 512), (4096, 4096, 1024)])
+def test_gemm_gelu_only_epilogue(ext, M, N, K):
+    """Inference epilogue (activation only) == the activation output of the training epilogue."""
+    torch.manual_seed(3)
+    x = (torch.rand(M, K, device="cuda") * 2 - 1).bfloat16()
+    w = ((torch.rand(N, K, device="cuda") * 2 - 1) * 0.05).bfloat16()
+    b = torch.randn(N, device="cuda") * 0.1
+    pre, g = ext.gemm_nt(x, w, b, True)
+    (g_only,) = ext.gemm_nt(x, w, b, True, True)
+    assert torch.equal(g_only, g)
+
+
+def test_pretrain_loss_same_with_and_without_grad():
+    from jumbo_mae_tpu_amd.config import DecoderConfig, ViTConfig
+    from jumbo_mae_tpu_amd.models.mae import PretrainModel
+
+    vc = ViTConfig(layers=2, dim=256, heads=4, labels=0, image_size=224, patch_size=16, posemb="sincos2d",
+                   image_mask_ratio=0.75)
+    dc = DecoderConfig(dec_layers=2, dec_dim=128, dec_heads=4, image_size=224, patch_size=16)
+    model = PretrainModel(vc, dc).to("cuda", torch.bfloat16, seed=0)
+    img = _images(64, 224, seed=9)
+    noise = torch.rand(196, device="cuda", generator=torch.Generator(device="cuda").manual_seed(1))
+    l1 = model(img, noise=noise)["loss"].item()
+    with torch.no_grad():
+        l2 = model(img, noise=noise)["loss"].item()
+    assert l1 == l2
+
+
+@pytest.mark.parametrize("mode", ["none", "mixup", "cutmix"])
+def test_mix_patches(ext, mode):
+    from jumbo_mae_tpu_amd.utils.mixup import Mixup
+
+    B = 6
+    img = _images(B, 224, seed=11)
+    plan = None
+    if mode != "none":
+        for seed in range(50):  # find a plan of the requested kind
+            plan = Mixup(0.8, 1.0, seed=seed).plan(B, 224, 224, "cuda", torch.Generator(device="cuda").manual_seed(0))
+            if plan["mode"] == mode and (mode == "mixup" or plan["box"][1] > plan["box"][0]):
+                break
+    rows = mae_ops.mixed_patches(img, plan, 16, torch.bfloat16)
+    if plan:
+        ref = extract_patches_nchw(Mixup.mix_images(mae_ops.normalize_images(img), plan), 16)
+    else:
+        ref = _ref_patches(img, 16)
+    assert (rows.float() - ref.reshape(rows.shape)).abs().max().item() < 2e-2

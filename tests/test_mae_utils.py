@@ -85,3 +85,37 @@ def test_flop_counts_match_baseline():
         f = pretrain_fwd_flops_per_image(vit_config(name, labels=0, posemb="sincos2d"), decoder_config())
         assert abs(f - ref) / ref < 0.02, (name, f)
     assert abs(mfu(1000.0, 1e12, 2, peak=1e15) - 1.5) < 1e-9
+
+
+def test_mixup_plan_matches_reference_mask_formulation():
+    """CutMix box as pixel ranges == the reference's linspace-grid mask (utils.py:66-111), and
+    the own-label weight is the kept-area fraction; Mixup blends with ratio."""
+    import numpy as np
+
+    from jumbo_mae_tpu_amd.utils.mixup import Mixup
+
+    torch.manual_seed(0)
+    imgs = torch.rand(6, 3, 32, 24)
+    labels = torch.nn.functional.one_hot(torch.arange(6), 10).float()
+    for seed in range(20):
+        mx = Mixup(0.8, 1.0, seed=seed)
+        plan = mx.plan(6, 32, 24, "cpu", torch.Generator().manual_seed(seed))
+        out = Mixup.mix_images(imgs, plan)
+        other = imgs[plan["perm"]]
+        if plan["mode"] == "mixup":
+            ref = plan["ratio"] * imgs + (1 - plan["ratio"]) * other
+        else:
+            rs = np.random.default_rng(seed)
+            rs.uniform()  # mode draw
+            ratio = float(rs.beta(1.0, 1.0))
+            size = (1 - ratio) ** 0.5
+            xs, ys = rs.uniform(size=2)
+            xr, yr = torch.linspace(0, 1, 24), torch.linspace(0, 1, 32)
+            xm = (xs - 0.5 * size <= xr) & (xr < xs + 0.5 * size)
+            ym = (ys - 0.5 * size <= yr) & (yr < ys + 0.5 * size)
+            keep = (~(ym[:, None] & xm[None, :])).float()
+            ref = keep * imgs + (1 - keep) * other
+            assert abs(plan["label_w"] - keep.mean().item()) < 1e-6
+        assert torch.allclose(out, ref)
+        lab = Mixup.mix_labels(labels, plan)
+        assert torch.allclose(lab.sum(-1), torch.ones(6))
