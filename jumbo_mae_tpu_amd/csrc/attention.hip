@@ -181,6 +181,150 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const uint16_t* __restric
   }
 }
 
+// ------------------------------------------------------------------ forward, multi-head loop
+// Same math and LDS images as attn_fwd_kernel<HD, SP, true>, but one workgroup walks ``hpw``
+// consecutive (b, h) pairs: the next pair's K / V rows are loaded into registers right after
+// the current pair's images are in LDS, so their HBM latency hides behind the current pair's
+// MFMA / softmax work (the one-pair kernel stalls on every load phase); Q fragments of the next
+// query tile are prefetched the same way.
+template <int HD, int SP>
+__global__ __launch_bounds__(256) void attn_fwd_ml_kernel(const uint16_t* __restrict__ qkv, uint16_t* __restrict__ o,
+                                                          float* __restrict__ lse, int S, int H, int BH, int hpw,
+                                                          float scale) {
+  constexpr int KS = HD + 8;
+  constexpr int NT = SP / 16;
+  constexpr int KK = HD / 32;
+  constexpr int DT = HD / 16;
+  constexpr int CPR = HD / 8;
+  constexpr int LPT = (SP * CPR + 255) / 256;
+  extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
+  uint16_t* Ks = smem;
+  uint16_t* Vt = smem + SP * KS;
+  const long ts = 3L * H * HD;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int l16 = lane & 15, g = lane >> 4;
+  const float sl2 = scale * LOG2E;
+
+  uint4 kr[LPT], vr[LPT];
+  auto load = [&](int bh) {
+    const int b = bh / H, h = bh - (bh / H) * H;
+    const uint16_t* base = qkv + (long)b * S * ts;
+#pragma unroll
+    for (int j = 0; j < LPT; ++j) {
+      const int i = threadIdx.x + 256 * j;
+      const int r = i / CPR, c = (i % CPR) * 8;
+      kr[j] = make_uint4(0, 0, 0, 0);
+      vr[j] = make_uint4(0, 0, 0, 0);
+      if (i < SP * CPR && r < S) {
+        kr[j] = *reinterpret_cast<const uint4*>(base + (long)r * ts + (H + h) * HD + c);
+        vr[j] = *reinterpret_cast<const uint4*>(base + (long)r * ts + (2 * H + h) * HD + c);
+      }
+    }
+  };
+  auto store = [&]() {
+#pragma unroll
+    for (int j = 0; j < LPT; ++j) {
+      const int i = threadIdx.x + 256 * j;
+      const int r = i / CPR, c = (i % CPR) * 8;
+      if (i < SP * CPR) {
+        *reinterpret_cast<uint4*>(Ks + r * KS + c) = kr[j];
+        *reinterpret_cast<uint4*>(Vt + r * KS + c) = vr[j];
+      }
+    }
+  };
+  auto load_q = [&](const uint16_t* Qg, int qt, bf16x8_t (&qf)[KK]) {
+    const int q = qt * 16 + l16;
+#pragma unroll
+    for (int kk = 0; kk < KK; ++kk) {
+      if (q < S) {
+        qf[kk] = ld8(Qg + (long)q * ts + 32 * kk + 8 * g);
+      } else {
+        s16x8_t z = {0, 0, 0, 0, 0, 0, 0, 0};
+        qf[kk] = __builtin_bit_cast(bf16x8_t, z);
+      }
+    }
+  };
+
+  const int bh0 = blockIdx.x * hpw;
+  load(bh0);
+  for (int j = 0; j < hpw; ++j) {
+    const int bh = bh0 + j;
+    if (bh >= BH) break;
+    if (j > 0) __syncthreads();  // every wave is done reading the previous pair's images
+    store();
+    __syncthreads();
+    if (j + 1 < hpw && bh + 1 < BH) load(bh + 1);
+    const int b = bh / H, h = bh - (bh / H) * H;
+    const uint16_t* Qg = qkv + (long)b * S * ts + h * HD;
+    bf16x8_t qn[KK];
+    if (wave < NT) load_q(Qg, wave, qn);
+    for (int qt = wave; qt < NT; qt += 4) {
+      const int q = qt * 16 + l16;
+      bf16x8_t qf[KK];
+#pragma unroll
+      for (int kk = 0; kk < KK; ++kk) qf[kk] = qn[kk];
+      if (qt + 4 < NT) load_q(Qg, qt + 4, qn);
+      f32x4_t sc[NT];
+#pragma unroll
+      for (int kt = 0; kt < NT; ++kt) {
+        f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int kk = 0; kk < KK; ++kk) acc = mfma(ld8(Ks + (kt * 16 + l16) * KS + 32 * kk + 8 * g), qf[kk], acc);
+        sc[kt] = acc;
+      }
+      float m = -INFINITY;
+#pragma unroll
+      for (int kt = 0; kt < NT; ++kt) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int key = kt * 16 + 4 * g + i;
+          const float v = key < S ? sc[kt][i] * sl2 : -INFINITY;
+          sc[kt][i] = v;
+          m = fmaxf(m, v);
+        }
+      }
+      m = fmaxf(m, __shfl_xor(m, 16, WAVE));
+      m = fmaxf(m, __shfl_xor(m, 32, WAVE));
+      float l = 0.f;
+#pragma unroll
+      for (int kt = 0; kt < NT; ++kt) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float p = __builtin_amdgcn_exp2f(sc[kt][i] - m);
+          sc[kt][i] = p;
+          l += p;
+        }
+      }
+      l += __shfl_xor(l, 16, WAVE);
+      l += __shfl_xor(l, 32, WAVE);
+      f32x4_t oacc[DT];
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt) oacc[dt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < NT / 2; ++s) {
+        float pf[8] = {sc[2 * s][0], sc[2 * s][1], sc[2 * s][2], sc[2 * s][3],
+                       sc[2 * s + 1][0], sc[2 * s + 1][1], sc[2 * s + 1][2], sc[2 * s + 1][3]};
+        const bf16x8_t pb = pack8(pf);
+#pragma unroll
+        for (int dt = 0; dt < DT; ++dt) {
+          const uint16_t* vr2 = Vt + (32 * s + 4 * g + (l16 >> 2)) * KS + dt * 16 + 4 * (l16 & 3);
+          oacc[dt] = mfma(cat44(tr4(vr2), tr4(vr2 + 16 * KS)), pb, oacc[dt]);
+        }
+      }
+      if (q < S) {
+        const float inv = 1.f / l;
+        uint16_t* orow = o + ((long)b * S + q) * H * HD + h * HD;
+#pragma unroll
+        for (int dt = 0; dt < DT; ++dt) {
+          float v[4] = {oacc[dt][0] * inv, oacc[dt][1] * inv, oacc[dt][2] * inv, oacc[dt][3] * inv};
+          store4(orow + dt * 16 + 4 * g, v);
+        }
+        if (g == 0) lse[((long)b * H + h) * S + q] = (m + log2f(l)) * LN2;
+      }
+    }
+  }
+}
+
 // -------------------------------------------------------------------------------- backward
 // waves per backward workgroup: 8 when the LDS budget allows (decoder, hd 32), else 4
 template <int HD, int SP>
@@ -1067,9 +1211,32 @@ bwd2:
   return 0;
 }
 
+// runtime switch: (b, h) pairs per forward workgroup; 1 = one-pair kernel, 0 = auto: 4 for the
+// short encoder sequences (SP <= 64: 43 -> 39 us), 1 for the decoder, where the extra prefetch
+// registers cost an occupancy step (199 -> 215 us; profiles/r1_attn_fwd_ml.txt)
+int g_fwd_hpw = 0;
+
+template <int HD, int SP>
+int run_fwd_ml(const uint16_t* qkv, uint16_t* out, float* lse_out, int B, int S, int H, float scale, hipStream_t st) {
+  const size_t sm = fwd_smem<HD, SP, true>();
+  static bool attr_set = false;
+  if (sm > 64 * 1024 && !attr_set) {
+    (void)hipFuncSetAttribute((const void*)attn_fwd_ml_kernel<HD, SP>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)sm);
+    attr_set = true;
+  }
+  const int BH = B * H;
+  const int hpw = g_fwd_hpw > 0 ? g_fwd_hpw : 4;
+  const int grid = (BH + hpw - 1) / hpw;
+  attn_fwd_ml_kernel<HD, SP><<<grid, 256, sm, st>>>(qkv, out, lse_out, S, H, BH, hpw, scale);
+  return 0;
+}
+
 template <int HD, int SP>
 int run(bool fwd, const uint16_t* qkv, const uint16_t* o, const uint16_t* dO, const float* lse_in, uint16_t* out,
         float* lse_out, int B, int S, int H, float scale, hipStream_t st) {
+  if (fwd && g_use_tr && (g_fwd_hpw > 1 || (g_fwd_hpw == 0 && SP <= 64)))
+    return run_fwd_ml<HD, SP>(qkv, out, lse_out, B, S, H, scale, st);
   if (g_use_tr >= 2 && !fwd) return run_bwd2<HD, SP>(qkv, o, dO, lse_in, out, lse_out, B, S, H, scale, st);
   if (g_use_tr) return run_t<HD, SP, true>(fwd, qkv, o, dO, lse_in, out, lse_out, B, S, H, scale, st);
   return run_t<HD, SP, false>(fwd, qkv, o, dO, lse_in, out, lse_out, B, S, H, scale, st);
@@ -1089,6 +1256,7 @@ int dispatch_sp(bool fwd, const uint16_t* qkv, const uint16_t* o, const uint16_t
 
 int jm_attn_max_seq() { return 224; }
 void jm_attn_set_tr(int v) { g_use_tr = v; }
+void jm_attn_set_fwd_hpw(int v) { g_fwd_hpw = v < 0 ? 0 : v; }
 
 int jm_attn_fwd(const uint16_t* qkv, uint16_t* o, float* lse, int B, int S, int H, int hd, hipStream_t st) {
   const float scale = 1.f / sqrtf((float)hd);

@@ -33,6 +33,7 @@ int jm_attn_bwd(const uint16_t* qkv, const uint16_t* o, const uint16_t* dO, cons
                 int S, int H, int hd, float* dbias_part, hipStream_t st);
 int jm_attn_max_seq();
 void jm_attn_set_tr(int v);
+void jm_attn_set_fwd_hpw(int v);
 void jm_opt_sumsq(const float* x, const int* chunks, int nchunks, float* out, hipStream_t st);
 void jm_opt_adamw(float* p, const float* g, float* mu, float* nu, uint16_t* shadow, const int* chunks, int nchunks,
                   const float* meta, const float* hyper, const float* gnorm_sq, hipStream_t st);
@@ -683,6 +684,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("gemm_nt", &gemm_nt, py::arg("A"), py::arg("B"), py::arg("bias") = py::none(), py::arg("gelu") = false,
         py::arg("gelu_only") = false);
   m.def("attn_set_tr", &jm_attn_set_tr);
+  m.def("attn_set_fwd_hpw", &jm_attn_set_fwd_hpw);
   m.def("opt_sumsq", &opt_sumsq);
   m.def("opt_adamw", &opt_adamw);
   m.def("opt_lamb_phase1", &opt_lamb_phase1);

@@ -111,13 +111,14 @@ def _attn_ref(qkv, H):
     return o, lse
 
 
-@pytest.mark.parametrize("tr", [3, 2, 1, 0])
+@pytest.mark.parametrize("tr,hpw", [(3, 0), (3, 1), (2, 1), (1, 1), (0, 1), (3, 3), (3, 4)])
 @pytest.mark.parametrize("B,S,H,hd", [(3, 52, 16, 64), (2, 199, 16, 32), (2, 17, 4, 32), (2, 100, 3, 64),
                                       (2, 199, 4, 64)])
-def test_attention(ext, B, S, H, hd, tr):
+def test_attention(ext, B, S, H, hd, tr, hpw):
     if not tr and S > 128:
         pytest.skip("transposed-image variant exceeds LDS at this size (TR variant covers it)")
     ext.attn_set_tr(tr)
+    ext.attn_set_fwd_hpw(hpw)
     torch.manual_seed(0)
     D = H * hd
     qkv = (torch.randn(B, S, 3 * D, device="cuda") * 1.5).bfloat16()
@@ -140,6 +141,7 @@ def test_attention(ext, B, S, H, hd, tr):
     for i in range(3):
         assert rel(d[:, :, i], g[:, :, i]) < 2e-2, i
     ext.attn_set_tr(3)
+    ext.attn_set_fwd_hpw(0)
 
 
 @pytest.mark.parametrize("S,n", [(4, 4096), (512, 3072), (37, 1024)])

@@ -22,8 +22,11 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--shapes", default="dec,enc")
     ap.add_argument("--tr", type=int, default=-1, help="kernel variant (ext.attn_set_tr), -1 = default")
+    ap.add_argument("--hpw", type=int, default=0, help="forward (b, h) pairs per workgroup, 0 = default")
     a = ap.parse_args()
     ext = _ext.load()
+    if a.hpw > 0:
+        ext.attn_set_fwd_hpw(a.hpw)
     if a.tr >= 0:
         ext.attn_set_tr(a.tr)
     for name in a.shapes.split(","):
