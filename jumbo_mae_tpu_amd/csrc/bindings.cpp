@@ -63,6 +63,14 @@ void jm_gemm_set_variant(int wn, int group);
 int jm_gemm_tn_plan(int M, int N, int K, int* S_out);
 int jm_gemm_tn(const uint16_t* A, long lda, const uint16_t* B, long ldb, int M, int N, int K, int sps, int S,
                float* G, long ldo, float* partial, hipStream_t st);
+struct TnSegs {
+  const uint16_t* a[32];
+  const uint16_t* b[32];
+  int rows;
+  int n;
+};
+int jm_gemm_tn_seg(const TnSegs& segs, long lda, long ldb, int N, int K, int sps, int S, float* G, long ldo,
+                   float* partial, hipStream_t st);
 int jm_patchify_normalize(const uint8_t* img, float* out, int B, int H, int W, int p, hipStream_t st);
 int jm_gather_patches(const uint8_t* img, const int* ids, long idsB, uint16_t* out, int B, int K, int H, int W, int p,
                       hipStream_t st);
@@ -629,6 +637,42 @@ int64_t gemm_tn_wgrad(torch::Tensor dy, torch::Tensor x, torch::Tensor g) {
   return S;
 }
 
+// g[N, K] += sum_i dys[i]^T xs[i]: the reduction rows are the concatenation of the per-layer
+// blocks (all [rows, N] / [rows, K], same strides), read in place (no torch.cat copy)
+int64_t gemm_tn_wgrad_seg(std::vector<torch::Tensor> dys, std::vector<torch::Tensor> xs, torch::Tensor g) {
+  TORCH_CHECK(!dys.empty() && dys.size() == xs.size() && dys.size() <= 32, "gemm_tn_wgrad_seg: 1..32 blocks");
+  const auto& d0 = dys[0];
+  const auto& x0 = xs[0];
+  const int rows = d0.size(0), N = d0.size(1), K = x0.size(1);
+  TnSegs segs{};
+  segs.rows = rows;
+  segs.n = (int)dys.size();
+  for (size_t i = 0; i < dys.size(); ++i) {
+    CHECK_DT(dys[i], torch::kBFloat16);
+    CHECK_DT(xs[i], torch::kBFloat16);
+    TORCH_CHECK(dys[i].dim() == 2 && xs[i].dim() == 2 && dys[i].size(0) == rows && xs[i].size(0) == rows &&
+                    dys[i].size(1) == N && xs[i].size(1) == K,
+                "gemm_tn_wgrad_seg: block shapes differ");
+    TORCH_CHECK(dys[i].stride(1) == 1 && xs[i].stride(1) == 1 && dys[i].stride(0) == d0.stride(0) &&
+                    xs[i].stride(0) == x0.stride(0),
+                "gemm_tn_wgrad_seg: block strides differ");
+    segs.a[i] = bf(dys[i]);
+    segs.b[i] = bf(xs[i]);
+  }
+  TORCH_CHECK(g.is_contiguous() && g.scalar_type() == torch::kFloat32 && g.numel() == (long)N * K, "gemm_tn_wgrad_seg g");
+  const int M = rows * segs.n;
+  int S = 1;
+  const int sps = jm_gemm_tn_plan(M, N, K, &S);
+  torch::Tensor part;
+  if (S > 1) part = torch::empty({S, (long)N * K}, g.options());
+  check_rc(jm_gemm_tn_seg(segs, d0.stride(0), x0.stride(0), N, K, sps, S, g.data_ptr<float>(), K,
+                          S > 1 ? part.data_ptr<float>() : nullptr, stream()),
+           "gemm_tn_wgrad_seg");
+  if (S > 1) check_rc(jm_splitk_reduce_add(part.data_ptr<float>(), g.data_ptr<float>(), (long)N * K, S, stream()),
+                      "gemm_tn_wgrad_seg reduce");
+  return S;
+}
+
 // x1 = x + mask*scale*y ([B,T,D] fp32, fresh contiguous); h / mean / rstd = LN of rows t >= T0
 std::vector<torch::Tensor> residual_ln_fwd(torch::Tensor x, torch::Tensor y, c10::optional<torch::Tensor> scale,
                                            c10::optional<torch::Tensor> mask, torch::Tensor gamma,
@@ -677,6 +721,7 @@ PYBIND11_MODULE(_C, m) {
         py::arg("dbias") = py::none());
   m.def("attn_max_seq", &jm_attn_max_seq);
   m.def("gemm_tn_wgrad", &gemm_tn_wgrad);
+  m.def("gemm_tn_wgrad_seg", &gemm_tn_wgrad_seg);
   m.def("gemm_set_variant", &jm_gemm_set_variant, py::arg("wn"), py::arg("group") = 8);
   m.def("gemm_nt_splitk", &gemm_nt_splitk, py::arg("A"), py::arg("B"), py::arg("bias") = py::none(),
         py::arg("splits") = 8);

@@ -71,11 +71,25 @@ struct TFrags {
   bf16x8_t b[4], a[8];
 };
 
-template <int ACC>  // ACC = 1: G += tile (S == 1), 0: store the fp32 partial tile
+}  // namespace
+
+// Segmented M (the batched shared-jumbo-MLP weight gradient): the reduction rows are the
+// concatenation of ``n`` separately allocated [rows, lda] / [rows, ldb] blocks (one per layer),
+// read in place instead of being copied into one tensor first.
+struct TnSegs {
+  const uint16_t* a[32];
+  const uint16_t* b[32];
+  int rows;  // rows per block, multiple of the 32-row step
+  int n;
+};
+
+namespace {
+
+template <int ACC, bool SEG = false>  // ACC = 1: G += tile (S == 1), 0: store the fp32 partial tile
 __global__ __launch_bounds__(NTH, 1) void gemm_tn_kernel(const uint16_t* __restrict__ A, long lda,
                                                          const uint16_t* __restrict__ B, long ldb, int M, int N,
                                                          int K, int steps_per_split, float* __restrict__ out,
-                                                         long ldo, long split_stride) {
+                                                         long ldo, long split_stride, TnSegs segs = {}) {
   extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
@@ -97,8 +111,8 @@ __global__ __launch_bounds__(NTH, 1) void gemm_tn_kernel(const uint16_t* __restr
   nk += nk & 1;  // even: the pipeline runs in pairs; rows past the split read zeros
   if (nk < 2) nk = 2;
 
-  const __amdgpu_buffer_rsrc_t ra = make_rsrc(A + (long)m_begin * lda + n0, (long)rows * lda * 2);
-  const __amdgpu_buffer_rsrc_t rb = make_rsrc(B + (long)m_begin * ldb + k0, (long)rows * ldb * 2);
+  const __amdgpu_buffer_rsrc_t ra = make_rsrc(SEG ? segs.a[0] : A + (long)m_begin * lda + n0, SEG ? 0 : (long)rows * lda * 2);
+  const __amdgpu_buffer_rsrc_t rb = make_rsrc(SEG ? segs.b[0] : B + (long)m_begin * ldb + k0, SEG ? 0 : (long)rows * ldb * 2);
   // staging: each wave-instruction moves 2 rows x 512 B; 16 per operand and stage -> 2 rounds
   uint32_t a_src[2], b_src[2];
 #pragma unroll
@@ -111,11 +125,25 @@ __global__ __launch_bounds__(NTH, 1) void gemm_tn_kernel(const uint16_t* __restr
   auto issue = [&](int t) {
     uint16_t* la = smem + (t % NST) * STAGE;
     uint16_t* lb = la + BS * TN_;
-    const uint32_t sa = (uint32_t)(t * BS * lda * 2), sb = (uint32_t)(t * BS * ldb * 2);
+    if constexpr (SEG) {  // this step's 32 rows lie in one block; past the split: empty range (zeros)
+      const int row = m_begin + t * BS;
+      const int sg = min(row / segs.rows, segs.n - 1);
+      const int loc = row - sg * segs.rows;
+      const int left = row < m_begin + rows ? min(segs.rows - loc, m_begin + rows - row) : 0;
+      const __amdgpu_buffer_rsrc_t sra = make_rsrc(segs.a[sg] + (long)loc * lda + n0, (long)left * lda * 2);
+      const __amdgpu_buffer_rsrc_t srb = make_rsrc(segs.b[sg] + (long)loc * ldb + k0, (long)left * ldb * 2);
 #pragma unroll
-    for (int rr = 0; rr < 2; ++rr) {
-      blds16(ra, a_src[rr], sa, la + (rr * 16 + wave * 2) * TN_);
-      blds16(rb, b_src[rr], sb, lb + (rr * 16 + wave * 2) * TK_);
+      for (int rr = 0; rr < 2; ++rr) {
+        blds16(sra, a_src[rr], 0, la + (rr * 16 + wave * 2) * TN_);
+        blds16(srb, b_src[rr], 0, lb + (rr * 16 + wave * 2) * TK_);
+      }
+    } else {
+      const uint32_t sa = (uint32_t)(t * BS * lda * 2), sb = (uint32_t)(t * BS * ldb * 2);
+#pragma unroll
+      for (int rr = 0; rr < 2; ++rr) {
+        blds16(ra, a_src[rr], sa, la + (rr * 16 + wave * 2) * TN_);
+        blds16(rb, b_src[rr], sb, lb + (rr * 16 + wave * 2) * TK_);
+      }
     }
   };
   // transposing fragment reads: rows 8g + l16/4 (+4), columns base + 4 (l16 & 3)
@@ -272,6 +300,36 @@ int jm_gemm_tn(const uint16_t* A, long lda, const uint16_t* B, long ldb, int M, 
       attr = true;
     }
     gemm_tn_kernel<0><<<tiles * S, NTH, sm, st>>>(A, lda, B, ldb, M, N, K, sps, partial, K, (long)N * K);
+  }
+  return 0;
+}
+
+// Segmented-M variant of jm_gemm_tn: A / B rows come from segs (n blocks of segs.rows rows).
+int jm_gemm_tn_seg(const TnSegs& segs, long lda, long ldb, int N, int K, int sps, int S, float* G, long ldo,
+                   float* partial, hipStream_t st) {
+  if (N % TN_ || K % TK_ || segs.n < 1 || segs.n > 32 || segs.rows % BS) return -1;
+  if ((long)segs.rows * lda * 2 >= (1L << 32) || (long)segs.rows * ldb * 2 >= (1L << 32)) return -2;
+  const int M = segs.rows * segs.n;
+  const int tiles = (N / TN_) * (K / TK_);
+  const size_t sm = jm_gemm_tn_smem();
+  if (S == 1) {
+    static bool attr = false;
+    if (!attr) {
+      (void)hipFuncSetAttribute((const void*)gemm_tn_kernel<1, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)sm);
+      attr = true;
+    }
+    gemm_tn_kernel<1, true><<<tiles, NTH, sm, st>>>(nullptr, lda, nullptr, ldb, M, N, K, sps, G, ldo, 0, segs);
+  } else {
+    if (partial == nullptr) return -3;
+    static bool attr = false;
+    if (!attr) {
+      (void)hipFuncSetAttribute((const void*)gemm_tn_kernel<0, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)sm);
+      attr = true;
+    }
+    gemm_tn_kernel<0, true><<<tiles * S, NTH, sm, st>>>(nullptr, lda, nullptr, ldb, M, N, K, sps, partial, K,
+                                                        (long)N * K, segs);
   }
   return 0;
 }

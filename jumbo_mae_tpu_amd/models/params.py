@@ -150,6 +150,9 @@ class ParamStore:
         self.compute_dtype = torch.float32
         self.hooks: list[Callable[[Handle], None]] = []
         self.use_hooks: list[Callable[[Handle], None]] = []
+        # partial readiness: fn(handle, lo, hi) -- elements [lo, hi) of a single-segment handle's
+        # gradient are final (the DP reducer may start reducing that slice early)
+        self.partial_hooks: list[Callable[[Handle, int, int], None]] = []
         self._handles: list[Handle] = []
         self.version = 0  # bumped whenever the shadow changes (optimizer step, sync, load)
 
@@ -212,6 +215,10 @@ class ParamStore:
     def mark_ready(self, h: Handle) -> None:
         for fn in self.hooks:
             fn(h)
+
+    def mark_partial_ready(self, h: Handle, lo: int, hi: int) -> None:
+        for fn in self.partial_hooks:
+            fn(h, lo, hi)
 
     def seg_view(self, flat: torch.Tensor, seg: Segment) -> torch.Tensor:
         return flat[seg.offset:seg.offset + seg.numel].view(seg.shape)

@@ -52,13 +52,14 @@ def wgrad_split(M: int, N: int, K: int) -> int:
 _WGRAD_OURS = os.environ.get("JMAE_WGRAD", "1") == "1"
 
 
-def wgrad(h: Handle, dy: torch.Tensor, x: torch.Tensor) -> None:
-    """grad[h] += dy^T @ x  (fp32 accumulate; bf16 inputs on GPU).
+def wgrad(h: Handle, dy: torch.Tensor, x: torch.Tensor, rows: tuple[int, int] | None = None) -> None:
+    """grad[h] += dy^T @ x  (fp32 accumulate; bf16 inputs on GPU); ``rows`` = (r0, r1) restricts
+    it to gradient rows r0:r1 (``dy`` then holds only those output columns).
 
     GPU: the TN MFMA kernel (csrc/gemm_tn.hip, M split into fp32 partial tiles) for every shape
     with 256-aligned N, K and M >= 4096 -- 1.11-1.37x the hipBLASLt split-K path on the ViT-L
     Jumbo-MAE shapes (profiles/r1_wgrad_tn_vs_hipblaslt.txt); hipBLASLt otherwise."""
-    g = h.grad
+    g = h.grad if rows is None else h.grad[rows[0]:rows[1]]
     if dy.is_cuda and dy.dtype != torch.float32:
         M, N = dy.shape
         K = x.shape[1]
@@ -180,7 +181,30 @@ def _end_of_backward() -> None:
 # 512 rows (one per layer, ~400 TF/s on hipBLASLt).  Their (dy, x) pairs are queued and, at the
 # end of the backward pass, concatenated into ONE GEMM over 24 x 512 rows on the TN MFMA kernel.
 # The DP reducer is told the segment is ready only then (one ``ready`` per queued use).
-_deferred: dict = {"handles": [], "cb": False, "enabled": os.environ.get("JMAE_DEFER_WGRAD", "1") == "1"}
+_deferred: dict = {"handles": [], "cb": False, "enabled": os.environ.get("JMAE_DEFER_WGRAD", "1") == "1",
+                   "force": False,  # also on CPU / fp32 (tests of the deferred + partial-reduce path)
+                   "chunks": int(os.environ.get("JMAE_JUMBO_CHUNKS", "4")),
+                   "seg": os.environ.get("JMAE_SEG_WGRAD", "1") == "1"}  # in-place segmented GEMM
+
+
+def _row_chunks(n: int, want: int, align: int = 256) -> list[tuple[int, int]]:
+    """Split n gradient rows into <= ``want`` chunks whose sizes are multiples of ``align`` (256 =
+    the TN kernel's tile) when possible."""
+    for c in range(want, 1, -1):
+        if n % c == 0 and (n // c) % align == 0:
+            step = n // c
+            return [(i * step, (i + 1) * step) for i in range(c)]
+    return [(0, n)]
+
+
+def _seg_ok(dys, xs) -> bool:
+    """The per-layer (dy, x) blocks can feed the segmented TN kernel in place (no concat)."""
+    d0, x0 = dys[0], xs[0]
+    return (_WGRAD_OURS and _deferred["seg"] and hip(d0) and len(dys) <= 32 and d0.shape[0] % 32 == 0
+            and d0.shape[1] % 256 == 0 and x0.shape[1] % 256 == 0
+            and all(d.dtype == torch.bfloat16 and d.shape == d0.shape and d.stride() == d0.stride() for d in dys)
+            and all(x.dtype == torch.bfloat16 and x.shape == x0.shape and x.stride() == x0.stride() for x in xs)
+            and d0.stride(1) == 1 and x0.stride(1) == 1)
 
 
 def flush_deferred_wgrads() -> None:
@@ -190,9 +214,25 @@ def flush_deferred_wgrads() -> None:
         pairs, h.deferred = h.deferred, []
         if not pairs:
             continue
-        dy = torch.cat([p[0] for p in pairs]) if len(pairs) > 1 else pairs[0][0]
-        x = torch.cat([p[1] for p in pairs]) if len(pairs) > 1 else pairs[0][1]
-        wgrad(h, dy, x)
+        dys = [p[0] for p in pairs]
+        xs = [p[1] for p in pairs]
+        N, K = dys[0].shape[1], xs[0].shape[1]
+        chunks = [(0, N)]
+        if h.store.partial_hooks and len(h.segs) == 1:
+            chunks = _row_chunks(N, _deferred["chunks"], 256 if hip(dys[0]) else 32)
+        seg = _seg_ok(dys, xs)
+        if not seg:
+            dy = torch.cat(dys) if len(dys) > 1 else dys[0]
+            x = torch.cat(xs) if len(xs) > 1 else xs[0]
+        for r0, r1 in chunks:
+            if seg:  # the batched GEMM reads the 24 per-layer blocks in place
+                _ext.load().gemm_tn_wgrad_seg([d[:, r0:r1] for d in dys], xs, h.grad[r0:r1])
+            elif len(chunks) == 1:
+                wgrad(h, dy, x)
+            else:
+                wgrad(h, dy[:, r0:r1], x, rows=(r0, r1))
+            if len(chunks) > 1:  # these gradient rows are final: the DP reducer starts on them at once
+                h.store.mark_partial_ready(h, r0 * K, r1 * K)
         for _ in pairs:
             h.ready()
 
@@ -248,7 +288,8 @@ def linear_bwd(dy: torch.Tensor, x2: torch.Tensor, hw: Handle, hb: Handle | None
                bias_done: bool = False):
     """dx = dy @ W (if needed); grad W += dy^T x; grad b += colsum(dy) (unless fused upstream)."""
     dx = linear_dgrad(dy, hw) if need_dx else None
-    if _trainable(hw) and hw.defer_wgrad and _deferred["enabled"] and hip(dy) and _defer_wgrad(hw, dy, x2):
+    if (_trainable(hw) and hw.defer_wgrad and _deferred["enabled"] and (hip(dy) or _deferred["force"])
+            and _defer_wgrad(hw, dy, x2)):
         if hb is not None:
             if not bias_done:
                 bias_grad(hb, dy)

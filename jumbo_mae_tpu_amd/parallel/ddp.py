@@ -17,6 +17,11 @@ MI355X design:
   (7 links x ~150 GB/s per MI355X), small enough that the first bucket starts early.
 * With ``grad_accum > 1`` call ``set_sync(False)`` on the non-final micro-steps (no-sync
   accumulation, CC2).
+* Partial readiness: the shared jumbo-MLP weights are final only at the very end of backward
+  (their batched weight-gradient GEMM runs after layer 0).  Their GEMM is split into row chunks
+  (ops/prims.py flush_deferred_wgrads) and each chunk's slice is all-reduced as soon as it is
+  written (``ParamStore.mark_partial_ready``), so only the last chunk's reduction is exposed
+  instead of two 150 MB tensors (ViT-L).  Only single-segment buckets take partial launches.
 """
 
 from __future__ import annotations
@@ -68,9 +73,11 @@ class GradReducer:
         self.launched = [False] * len(self.buckets)
         self.works = []
         self._compressed = {}
+        self.partial_done = [0] * len(self.buckets)  # elements of a bucket already launched
         if self.enabled:
             store.hooks.append(self._on_ready)
             store.use_hooks.append(self._on_use)
+            store.partial_hooks.append(self._on_partial)
 
     # ---------------------------------------------------------------- protocol
     def set_sync(self, sync: bool) -> None:
@@ -80,7 +87,23 @@ class GradReducer:
         self.pending_uses = [0] * len(self.segs)
         self.bucket_left = [len(b[2]) for b in self.buckets]
         self.launched = [False] * len(self.buckets)
+        self.partial_done = [0] * len(self.buckets)
         self.works = []
+
+    def _on_partial(self, h: Handle, lo: int, hi: int) -> None:
+        """Elements [lo, hi) of single-segment handle ``h`` are final: reduce them now."""
+        if not (self.overlap and self.sync) or len(h.segs) != 1:
+            return
+        i = self.seg_index.get(id(h.segs[0]))
+        if i is None:
+            return
+        b = self.seg_bucket[i]
+        blo, bhi, idxs = self.buckets[b]
+        if len(idxs) != 1 or self.launched[b] or self.reduce_dtype != torch.float32:
+            return
+        off = self.segs[i].offset
+        self.works.append((b, self._allreduce(self.store.grad[off + lo:off + hi])))
+        self.partial_done[b] += hi - lo
 
     def _on_use(self, h: Handle) -> None:
         for s in h.segs:
@@ -107,6 +130,10 @@ class GradReducer:
             return
         self.launched[b] = True
         lo, hi, _ = self.buckets[b]
+        if self.partial_done[b]:
+            if self.partial_done[b] != hi - lo:
+                raise RuntimeError(f"bucket {b}: partial reductions cover {self.partial_done[b]} of {hi - lo}")
+            return
         view = self.store.grad[lo:hi]
         if self.reduce_dtype != torch.float32:
             buf = view.to(self.reduce_dtype)

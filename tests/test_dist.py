@@ -35,8 +35,11 @@ def _cfgs():
     return vc, dc
 
 
-def _dp_worker(rank, world, port, out, bucket_mb):
+def _dp_worker(rank, world, port, out, bucket_mb, defer=False):
     _init(rank, world, port)
+    from jumbo_mae_tpu_amd.ops import prims
+    prims._deferred["force"] = defer  # batched jumbo wgrad + chunked partial all-reduce (GPU path)
+    partial = []
     from jumbo_mae_tpu_amd.models.mae import PretrainModel
     from jumbo_mae_tpu_amd.parallel.ddp import GradReducer
     from jumbo_mae_tpu_amd.train.meter import AverageMeter
@@ -44,6 +47,7 @@ def _dp_worker(rank, world, port, out, bucket_mb):
     m = PretrainModel(vc, dc).to("cpu", seed=rank)  # different init per rank ...
     dist.broadcast(m.store.master, 0)               # ... made identical by the CC6 broadcast
     red = GradReducer(m.store, bucket_mb=bucket_mb)
+    m.store.partial_hooks.append(lambda h, lo, hi: partial.append((lo, hi)))
     g = torch.Generator().manual_seed(0)
     imgs = torch.randint(0, 256, (8, 3, 32, 32), dtype=torch.uint8, generator=g)
     noise = torch.rand(16, generator=g)
@@ -59,17 +63,18 @@ def _dp_worker(rank, world, port, out, bucket_mb):
     summ = meter.summary()
     if rank == 0:
         torch.save({"grad": m.store.grad.clone(), "launched_early": launched_early, "nb": len(red.buckets),
+                    "partial": len(partial),
                     "loss": summ["loss"], "master": m.store.master.clone()}, out)
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("bucket_mb", [64.0, 0.01])
-def test_dp_grads_equal_large_batch(bucket_mb):
+@pytest.mark.parametrize("bucket_mb,defer", [(64.0, False), (0.01, False), (0.01, True)])
+def test_dp_grads_equal_large_batch(bucket_mb, defer):
     from jumbo_mae_tpu_amd.models.mae import PretrainModel
     port = _free_port()
     with tempfile.TemporaryDirectory() as d:
         out = os.path.join(d, "r.pt")
-        mp.spawn(_dp_worker, args=(2, port, out, bucket_mb), nprocs=2, join=True)
+        mp.spawn(_dp_worker, args=(2, port, out, bucket_mb, defer), nprocs=2, join=True)
         res = torch.load(out, weights_only=True)
     vc, dc = _cfgs()
     ref = PretrainModel(vc, dc).to("cpu", seed=0)
@@ -83,6 +88,8 @@ def test_dp_grads_equal_large_batch(bucket_mb):
     assert abs(res["loss"] - loss.item()) < 1e-5
     if bucket_mb < 1:
         assert res["nb"] > 3 and res["launched_early"] > 0  # buckets reduced while backward still ran
+    if defer:  # jumbo w1 / w2 gradients reduced in row chunks as their batched GEMM writes them
+        assert res["partial"] == 7  # w1: 4 chunks of 96 rows, w2: 3 chunks of 32
 
 
 def _bn_worker(rank, world, port, out):

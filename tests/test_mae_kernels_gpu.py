@@ -196,3 +196,17 @@ def test_mix_patches(ext, mode):
     else:
         ref = _ref_patches(img, 16)
     assert (rows.float() - ref.reshape(rows.shape)).abs().max().item() < 2e-2
+
+
+@pytest.mark.parametrize("n,rows,N,K,cols", [(24, 512, 1024, 256, None), (5, 96, 512, 768, (256, 512)),
+                                            (3, 4096, 256, 512, None)])
+def test_gemm_tn_wgrad_segmented(ext, n, rows, N, K, cols):
+    """Batched weight gradient over per-layer blocks read in place == the concatenated GEMM."""
+    torch.manual_seed(4)
+    dys = [torch.randn(rows, N, device="cuda").bfloat16() for _ in range(n)]
+    xs = [torch.randn(rows, K, device="cuda").bfloat16() for _ in range(n)]
+    r0, r1 = cols if cols else (0, N)
+    g = torch.randn(r1 - r0, K, device="cuda")
+    ref = g.double() + torch.cat(dys)[:, r0:r1].double().t() @ torch.cat(xs).double()
+    ext.gemm_tn_wgrad_seg([d[:, r0:r1] for d in dys], xs, g)
+    assert rel(g, ref) < 1e-5

@@ -44,6 +44,8 @@ def apply(P, cfg: str):
             blocks.LINKS = v == "1"
         elif k == "JMAE_FUSE_LN_RES":
             P._FUSE_LN_RES = v == "1"
+        elif k == "JMAE_SEG_WGRAD":
+            P._deferred["seg"] = v == "1"
         elif k == "JMAE_DEFER_WGRAD":
             P._deferred["enabled"] = v == "1"
         else:
