@@ -16,6 +16,7 @@ int jm_layernorm_bwd(const void* dy, int dy_bf16, const float* x, long sB, long 
                      const float* dres, long rB, long rT, float* dgamma, float* dbeta, int accum_params, float* ws,
                      const JmLnRes* res, hipStream_t st);
 int jm_layernorm_bwd_blocks(int rows);
+void jm_ln_set_bwd_la(int v);
 int jm_residual_ln_fwd(const float* x, long sB, long sT, const uint16_t* y, const float* scale, const float* mask,
                        float* x1, long oB, long oT, uint16_t* h, float* mean, float* rstd, int B, int T, int T0,
                        int D, const float* gamma, const float* beta, float eps, hipStream_t st);
@@ -81,8 +82,8 @@ int jm_unshuffle_fwd(const uint16_t* y, const float* tok, const int* restore, lo
 int jm_unshuffle_bwd_blocks(int B, int C, int N, int rows_per_block);
 int jm_unshuffle_bwd(const float* dout, const int* restore, long rsB, uint16_t* dy, float* part, int B, int C, int K,
                      int N, int d, int rows_per_block, hipStream_t st);
-int jm_mix_patches(const uint8_t* img, const int* perm, uint16_t* out, int B, int H, int W, int p, int mode, float r,
-                   int y0, int y1, int x0, int x1, hipStream_t st);
+int jm_mix_patches(const uint8_t* img, const int* perm, const float* prm, const int* box, uint16_t* out, int B, int H,
+                   int W, int p, hipStream_t st);
 int jm_patch_mse_fwd(const uint16_t* pred, long ldp, const uint8_t* img, float* mse, long rows, int N, int H, int W,
                      int p, int norm_pix, hipStream_t st);
 int jm_patch_mse_bwd(const uint16_t* pred, long ldp, const uint8_t* img, const float* dmse, uint16_t* dpred, long rows,
@@ -479,23 +480,27 @@ std::vector<torch::Tensor> unshuffle_bwd(torch::Tensor dout, torch::Tensor ids_r
 }
 
 // finetune input: [B*N, 3p^2] bf16 normalized patches of the (Mixup / CutMix) blended batch
-torch::Tensor mix_patches(torch::Tensor img, c10::optional<torch::Tensor> perm, int64_t p, int64_t mode, double ratio,
-                          std::vector<int64_t> box) {
+torch::Tensor mix_patches(torch::Tensor img, c10::optional<torch::Tensor> perm, c10::optional<torch::Tensor> prm,
+                          c10::optional<torch::Tensor> box, int64_t p) {
   CHECK_CONTIG(img);
   CHECK_DT(img, torch::kUInt8);
-  TORCH_CHECK(img.size(1) == 3 && box.size() == 4, "mix_patches: 3 channels, box (y0, y1, x0, x1)");
+  TORCH_CHECK(img.size(1) == 3, "mix_patches: 3 channels");
   const int B = img.size(0), H = img.size(2), W = img.size(3);
   const int* pp = nullptr;
-  if (perm) {
+  const float* pr = nullptr;
+  const int* bx = nullptr;
+  if (prm) {
+    TORCH_CHECK(perm && box, "mix_patches: prm needs perm and box");
     CHECK_DT((*perm), torch::kInt32);
-    CHECK_CONTIG((*perm));
-    TORCH_CHECK(perm->numel() == B, "perm size");
+    CHECK_DT((*prm), torch::kFloat32);
+    CHECK_DT((*box), torch::kInt32);
+    TORCH_CHECK(perm->numel() == B && prm->numel() >= 2 && box->numel() == 4, "mix_patches: param sizes");
     pp = perm->data_ptr<int>();
+    pr = prm->data_ptr<float>();
+    bx = box->data_ptr<int>();
   }
   auto out = torch::empty({(long)B * (H / p) * (W / p), 3 * p * p}, img.options().dtype(torch::kBFloat16));
-  check_rc(jm_mix_patches(img.data_ptr<uint8_t>(), pp, bfp(out), B, H, W, p, mode, (float)ratio, box[0], box[1], box[2],
-                          box[3], stream()),
-           "mix_patches");
+  check_rc(jm_mix_patches(img.data_ptr<uint8_t>(), pp, pr, bx, bfp(out), B, H, W, p, stream()), "mix_patches");
   return out;
 }
 
@@ -729,6 +734,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("gemm_nt", &gemm_nt, py::arg("A"), py::arg("B"), py::arg("bias") = py::none(), py::arg("gelu") = false,
         py::arg("gelu_only") = false);
   m.def("attn_set_tr", &jm_attn_set_tr);
+  m.def("ln_set_bwd_la", &jm_ln_set_bwd_la);
   m.def("attn_set_fwd_hpw", &jm_attn_set_fwd_hpw);
   m.def("opt_sumsq", &opt_sumsq);
   m.def("opt_adamw", &opt_adamw);

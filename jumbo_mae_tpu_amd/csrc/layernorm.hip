@@ -178,24 +178,40 @@ struct LnResIO {
 };
 
 // partial rows in ws: [dgamma | dbeta] (NP = 2) or [dgamma | dbeta | dscale | dbias] (NP = 4)
-template <int V, typename TI, bool RES>
+// LA (LDS accumulation): the per-column parameter partials are added into the block's LDS row
+// with ds_add_f32 instead of living in registers across the row loop (64 fewer VGPRs at D=1024:
+// twice the waves per SIMD for this memory-bound kernel), and the residual-gradient input is
+// loaded together with x / dy so each row costs one HBM round trip instead of two.
+template <int V, typename TI, bool RES, bool LA = false>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(const TI* __restrict__ dy, const float* __restrict__ x,
                                                      long sB, long sT, int T, int rows, int D,
                                                      const float* __restrict__ mean, const float* __restrict__ rstd,
                                                      const float* __restrict__ gamma, LnBwdIO io, LnResIO rio,
                                                      float* __restrict__ ws, int accum_params) {
   constexpr int NP = RES ? 4 : 2;
+  constexpr int NA = LA ? 1 : NP;  // register accumulators kept (dummy when LA)
   extern __shared__ __attribute__((aligned(16))) float red[];  // [NP*D]
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const bool partials = accum_params || RES;
-  float acc[NP][V][4], gg[V][4], sc[V][4];
+  if (LA && partials) {
+    for (int i = threadIdx.x; i < NP * D; i += 256) red[i] = 0.f;
+    __syncthreads();
+  }
+  auto acc_add = [&](float (&acc)[NA][V][4], int k, int i, int j, float v) {
+    if constexpr (LA) {
+      atomicAdd(&red[k * D + (i * 64 + lane) * 4 + j], v);
+    } else {
+      acc[k % NA][i][j] += v;
+    }
+  };
+  float acc[NA][V][4], gg[V][4], sc[V][4];
 #pragma unroll
   for (int i = 0; i < V; ++i) {
     const int col = (i * 64 + lane) * 4;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
 #pragma unroll
-      for (int k = 0; k < NP; ++k) acc[k][i][j] = 0.f;
+      for (int k = 0; k < NA; ++k) acc[k][i][j] = 0.f;
       sc[i][j] = 1.f;
     }
     if (col < D) {
@@ -211,6 +227,8 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const TI* __restrict__ dy, 
     const bool rrow = RES && t >= rio.T0;
     const long yoff = RES ? b * rio.yB + (long)(t - rio.T0) * rio.yT : 0;
     float xh[V][4], g[V][4], yv[V][4];
+    float rvp[LA ? V : 1][4];
+    const float* rr = io.dres ? io.dres + b * io.rB + t * io.rT : nullptr;
     float sg = 0.f, sgx = 0.f;
 #pragma unroll
     for (int i = 0; i < V; ++i) {
@@ -220,14 +238,18 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const TI* __restrict__ dy, 
         load4(xr + col, xv);
         load4(dyr + col, dv);
         if (RES && rrow && rio.scale) load4(rio.y + yoff + col, yv[i]);
+        if constexpr (LA) {
+          if (rr) load4(rr + col, rvp[i]);
+          else rvp[i][0] = rvp[i][1] = rvp[i][2] = rvp[i][3] = 0.f;
+        }
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           xh[i][j] = (xv[j] - mu) * rs;
           g[i][j] = dv[j] * gg[i][j];
           sg += g[i][j];
           sgx += g[i][j] * xh[i][j];
-          acc[0][i][j] += dv[j] * xh[i][j];
-          acc[1][i][j] += dv[j];
+          acc_add(acc, 0, i, j, dv[j] * xh[i][j]);
+          acc_add(acc, 1, i, j, dv[j]);
         }
       } else {
 #pragma unroll
@@ -237,14 +259,18 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const TI* __restrict__ dy, 
     sg = wave_sum(sg) / D;
     sgx = wave_sum(sgx) / D;
     float* dxr = io.dx + b * io.oB + t * io.oT;
-    const float* rr = io.dres ? io.dres + b * io.rB + t * io.rT : nullptr;
     const float m = (RES && rio.mask) ? rio.mask[b] : 1.f;
 #pragma unroll
     for (int i = 0; i < V; ++i) {
       const int col = (i * 64 + lane) * 4;
       if (col < D) {
         float o[4], rv[4] = {0.f, 0.f, 0.f, 0.f};
-        if (rr) load4(rr + col, rv);
+        if constexpr (LA) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) rv[j] = rvp[i][j];
+        } else if (rr) {
+          load4(rr + col, rv);
+        }
 #pragma unroll
         for (int j = 0; j < 4; ++j) o[j] = rs * (g[i][j] - sg - xh[i][j] * sgx) + rv[j];
         store4(dxr + col, o);
@@ -254,8 +280,8 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const TI* __restrict__ dy, 
           for (int j = 0; j < 4; ++j) {
             const float md = m * o[j];
             d[j] = md * sc[i][j];
-            if (rio.scale) acc[2][i][j] += md * yv[i][j];
-            acc[3 % NP][i][j] += bf2f(f2bf(d[j]));  // colsum of the bf16 values the GEMMs consume
+            if (rio.scale) acc_add(acc, 2, i, j, md * yv[i][j]);
+            acc_add(acc, 3 % NP, i, j, bf2f(f2bf(d[j])));  // colsum of the bf16 values the GEMMs consume
           }
           store4(rio.dy + yoff + col, d);
         }
@@ -263,6 +289,15 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const TI* __restrict__ dy, 
     }
   }
   if (!partials) return;
+  if constexpr (LA) {
+    __syncthreads();
+    for (int i = threadIdx.x * 4; i < NP * D; i += 256 * 4) {
+      float a[4];
+      load4(red + i, a);
+      store4(ws + (long)blockIdx.x * NP * D + i, a);
+    }
+    return;
+  }
   // merge the 4 waves' partials through LDS in turn (float4, conflict-free, no atomics), then
   // one coalesced store of the block partial row into the workspace
   for (int w = 0; w < 4; ++w) {
@@ -276,7 +311,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const TI* __restrict__ dy, 
             float a[4] = {0.f, 0.f, 0.f, 0.f};
             if (w > 0) load4(red + k * D + col, a);
 #pragma unroll
-            for (int j = 0; j < 4; ++j) a[j] += acc[k][i][j];
+            for (int j = 0; j < 4; ++j) a[j] += acc[k % NA][i][j];
             store4(red + k * D + col, a);
           }
         }
@@ -332,13 +367,22 @@ void launch_fwd(int V, dim3 grid, hipStream_t st, const float* x, long sB, long 
 #undef JM_LNF
 }
 
+// runtime switch (A/B): LDS-accumulated parameter partials + early dres load.  Off: the ds_add_f32
+// accumulation made the ViT-L step 97.8 -> 122.2 ms despite the doubled occupancy
+// (profiles/r1_ab_ln_bwd_lds_acc.txt)
+int g_ln_bwd_la = 0;
+
 template <typename TI, bool RES>
 void launch_bwd(int V, dim3 grid, size_t smem, hipStream_t st, const TI* dy, const float* x, long sB, long sT,
                 int T, int rows, int D, const float* m, const float* r, const float* g, LnBwdIO dx, LnResIO rio,
                 float* ws, int acc) {
-#define JM_LNB(VV)                                                                                        \
-  case VV:                                                                                                \
-    ln_bwd_kernel<VV, TI, RES><<<grid, 256, smem, st>>>(dy, x, sB, sT, T, rows, D, m, r, g, dx, rio, ws, acc); \
+#define JM_LNB(VV)                                                                                          \
+  case VV:                                                                                                  \
+    if (g_ln_bwd_la && VV >= 2 && VV <= 4)                                                                  \
+      ln_bwd_kernel<VV, TI, RES, true><<<grid, 256, smem, st>>>(dy, x, sB, sT, T, rows, D, m, r, g, dx, rio, ws, \
+                                                                 acc);                                     \
+    else                                                                                                    \
+      ln_bwd_kernel<VV, TI, RES><<<grid, 256, smem, st>>>(dy, x, sB, sT, T, rows, D, m, r, g, dx, rio, ws, acc); \
     break;
   switch (V) {
     JM_LNB(1) JM_LNB(2) JM_LNB(3) JM_LNB(4) JM_LNB(6) JM_LNB(8) JM_LNB(9) JM_LNB(12) JM_LNB(16)
@@ -389,6 +433,8 @@ int jm_residual_ln_fwd(const float* x, long sB, long sT, const uint16_t* y, cons
 #undef JM_RLN
   return 0;
 }
+
+void jm_ln_set_bwd_la(int v) { g_ln_bwd_la = v; }
 
 int jm_layernorm_bwd_blocks(int rows) {
   // grid-stride over rows: 1024 blocks x 4 waves = 4 waves per SIMD streaming; each block writes

@@ -371,13 +371,25 @@ int jm_patch_mse_bwd(const uint16_t* pred, long ldp, const uint8_t* img, const f
 // patch-embed operand [B*N, 3p^2], straight from uint8 (utils.py:66-111 semantics):
 //   mode 0: x[b];  mode 1 (mixup): r x[b] + (1 - r) x[perm[b]];
 //   mode 2 (cutmix): x[perm[b]] inside the pixel box [y0, y1) x [x0, x1), else x[b].
+// The per-batch decisions live in DEVICE buffers (prm = [mode, ratio, ...], box = [y0, y1, x0, x1],
+// perm), written by the host step feeder: the launch has no host-varying arguments and can be
+// replayed from a HIP graph.  prm == nullptr: no mixing.
 namespace {
 __global__ __launch_bounds__(256) void mix_patches_kernel(const uint8_t* __restrict__ img, const int* __restrict__ perm,
-                                                          uint16_t* __restrict__ out, int B, int H, int W, int p,
-                                                          int mode, float r, int y0, int y1, int x0, int x1) {
+                                                          const float* __restrict__ prm, const int* __restrict__ box,
+                                                          uint16_t* __restrict__ out, int B, int H, int W, int p) {
   const int P3 = 3 * p * p, q = P3 / 4, g = W / p, N = (H / p) * g;
   const long i = (long)blockIdx.x * 256 + threadIdx.x;
   if (i >= (long)B * N * q) return;
+  const int mode = prm ? (int)prm[0] : 0;
+  const float r = prm ? prm[1] : 1.f;
+  int y0 = 0, y1 = 0, x0 = 0, x1 = 0;
+  if (mode == 2) {
+    y0 = box[0];
+    y1 = box[1];
+    x0 = box[2];
+    x1 = box[3];
+  }
   const long row = i / q;
   const int o0 = (int)(i - row * q) * 4;
   const int b = (int)(row / N), n = (int)(row - (long)b * N);
@@ -389,7 +401,7 @@ __global__ __launch_bounds__(256) void mix_patches_kernel(const uint8_t* __restr
     const int o = o0 + j;
     const int ph = o / (3 * p);
     const int rr = o - ph * 3 * p;
-    const int pw = rr / 3, c = rr - (rr / 3) * 3;
+    const int pw = rr / 3;
     const int y = gy * p + ph, x = gx * p + pw;
     const float a = patch_pixel(img, b, H, W, p, gy, gx, o);
     if (mode == 1) {
@@ -399,18 +411,17 @@ __global__ __launch_bounds__(256) void mix_patches_kernel(const uint8_t* __restr
     } else {
       f[j] = a;
     }
-    (void)c;
   }
   store4(out + row * P3 + o0, f);
 }
 }  // namespace
 
-int jm_mix_patches(const uint8_t* img, const int* perm, uint16_t* out, int B, int H, int W, int p, int mode, float r,
-                   int y0, int y1, int x0, int x1, hipStream_t st) {
+int jm_mix_patches(const uint8_t* img, const int* perm, const float* prm, const int* box, uint16_t* out, int B, int H,
+                   int W, int p, hipStream_t st) {
   if ((3 * p * p) % 4 || H % p || W % p) return -1;
-  if (mode != 0 && perm == nullptr) return -2;
+  if (prm != nullptr && (perm == nullptr || box == nullptr)) return -2;
   const long n = (long)B * (H / p) * (W / p) * (3 * p * p / 4);
   if (n == 0) return 0;
-  mix_patches_kernel<<<cdiv(n, 256), 256, 0, st>>>(img, perm, out, B, H, W, p, mode, r, y0, y1, x0, x1);
+  mix_patches_kernel<<<cdiv(n, 256), 256, 0, st>>>(img, perm, prm, box, out, B, H, W, p);
   return 0;
 }

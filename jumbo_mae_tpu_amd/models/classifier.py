@@ -39,6 +39,10 @@ def sigmoid_bce(logits, labels):
 CRITERION_COLLECTION = {"ce": softmax_cross_entropy, "bce": sigmoid_bce}
 
 
+def _capturing() -> bool:
+    return torch.cuda.is_available() and torch.cuda.is_current_stream_capturing()
+
+
 class FinetuneModel:
     def __init__(self, cfg: ViTConfig, mixup: Mixup | None = None, label_smoothing: float = 0.0,
                  criterion: str = "ce", group=None):
@@ -65,13 +69,28 @@ class FinetuneModel:
         return self.store.master.device
 
     # ---------------------------------------------------------------- pieces
+    micro_index = 0
+
+    def prepare_step(self, i: int, images_u8, labels=None) -> None:
+        """Host part of a train step (engine.Trainer.host_prepare): draw micro-batch ``i``'s Mixup /
+        CutMix decision; its device buffers are what the (possibly graph-replayed) forward reads."""
+        if not self.mixup.active:
+            return
+        if not hasattr(self, "_plans"):
+            self._plans = {}
+        B, _, H, W = images_u8.shape
+        self._plans[i] = self.mixup.plan(B, H, W, images_u8.device, tag=str(i))
+
     def patches(self, images_u8, labels, rngs, det):
         """(patch rows [B*N, p*p*3] in the compute dtype, labels) -- Mixup / CutMix applied when
         training (one plan per batch; the blend is fused into the patch gather on the GPU)."""
         B, _, H, W = images_u8.shape
         plan = None
         if not det and self.mixup.active:
-            plan = self.mixup.plan(B, H, W, images_u8.device, rngs.get("mixup") if rngs else None)
+            plans = getattr(self, "_plans", {})
+            plan = plans.pop(self.micro_index, None) if not _capturing() else plans.get(self.micro_index)
+            if plan is None:  # direct forward call without a prepared step: draw here
+                plan = self.mixup.plan(B, H, W, images_u8.device, rngs.get("mixup") if rngs else None)
         if labels is not None:
             labels = Mixup.mix_labels(labels, plan)
         rows = mae_ops.mixed_patches(images_u8, plan, self.cfg.patch_size, self.store.compute_dtype)
@@ -109,8 +128,9 @@ class FinetuneModel:
     __call__ = forward
 
     def _prep_labels(self, labels):
-        if labels.dim() == 1:
-            labels = F.one_hot(labels.long().clamp(min=0), self.cfg.labels)
+        if labels.dim() == 1:  # one-hot by scatter: F.one_hot validates the range with a host sync
+            idx = labels.long().clamp(0, self.cfg.labels - 1).view(-1, 1)
+            return torch.zeros(labels.shape[0], self.cfg.labels, device=labels.device).scatter_(1, idx, 1.0)
         return labels.float()
 
     @staticmethod

@@ -227,10 +227,8 @@ def mixed_patches(images_u8: torch.Tensor, plan: dict | None, patch_size: int, d
     B = images_u8.shape[0]
     if _ext.use_hip(images_u8) and dtype == torch.bfloat16:
         if plan is None:
-            return _ext.load().mix_patches(images_u8.contiguous(), None, patch_size, 0, 1.0, [0, 0, 0, 0])
-        mode = 1 if plan["mode"] == "mixup" else 2
-        box = list(plan["box"]) if plan["box"] is not None else [0, 0, 0, 0]
-        return _ext.load().mix_patches(images_u8.contiguous(), _i32(plan["perm"]), patch_size, mode,
-                                       float(plan["ratio"]), box)
+            return _ext.load().mix_patches(images_u8.contiguous(), None, None, None, patch_size)
+        d = plan["dev"]
+        return _ext.load().mix_patches(images_u8.contiguous(), d["perm"], d["params"], d["box"], patch_size)
     x = Mixup.mix_images(normalize_images(images_u8), plan)
     return extract_patches_nchw(x, patch_size).reshape(B * (x.shape[-1] // patch_size) ** 2, -1).to(dtype)

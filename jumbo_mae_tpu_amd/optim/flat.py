@@ -106,15 +106,35 @@ class FlatOptimizer:
     # ---------------------------------------------------------------- step
     def step(self) -> float:
         """Apply one optimizer update from ``store.grad``; returns the learning rate used."""
+        self.prepare()
+        self.launch()
+        return self.finish()
+
+    # A step in three parts so the device work can be captured in a HIP graph
+    # (runtime/graph.py): ``prepare`` (host: schedule value, bias corrections -> the static
+    # ``hyper`` device buffer through the step feeder), ``launch`` (device kernels only),
+    # ``finish`` (host bookkeeping).
+    def prepare(self) -> None:
         lr = float(self.schedule(self.count))
         t = self.count + 1
-        bc1 = 1.0 - self.b1 ** t
-        bc2 = 1.0 - self.b2 ** t
+        self._cur = (lr, 1.0 - self.b1 ** t, 1.0 - self.b2 ** t)
         s = self.store
         if s.master.is_cuda and _ext.use_hip(s.master):
-            self._step_hip(lr, bc1, bc2)
+            from ..runtime.feeder import feeder
+            lr, bc1, bc2 = self._cur
+            # hyper = [lr, bc1, bc2, clip, b1, b2, eps, wd]
+            self.hyper = feeder(s.master.device).put(
+                "opt_hyper", [lr, bc1, bc2, self.clip_grad, self.b1, self.b2, self.eps, self.weight_decay])
+
+    def launch(self) -> None:
+        s = self.store
+        if s.master.is_cuda and _ext.use_hip(s.master):
+            self._step_hip()
         else:
-            self._step_torch(lr, bc1, bc2)
+            self._step_torch(*self._cur)
+
+    def finish(self) -> float:
+        lr = self._cur[0]
         self.count += 1
         self.store.version += 1  # shadow rewritten: transposed weight copies are stale
         self.last_lr = lr
@@ -162,13 +182,10 @@ class FlatOptimizer:
         s.sync_shadow()
 
     @torch.no_grad()
-    def _step_hip(self, lr, bc1, bc2):
+    def _step_hip(self):
         ext = _ext.load()
         s = self.store
         shadow = s.shadow if s.shadow is not s.master else None
-        # hyper = [lr, bc1, bc2, clip, b1, b2, eps, wd]
-        self.hyper.copy_(torch.tensor([lr, bc1, bc2, self.clip_grad, self.b1, self.b2, self.eps,
-                                       self.weight_decay], dtype=torch.float32), non_blocking=True)
         if self.clip_grad > 0:
             self.gnorm_sq.zero_()
             ext.opt_sumsq(s.grad, self.chunks, self.gnorm_sq)

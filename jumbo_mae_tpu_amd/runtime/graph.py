@@ -1,0 +1,62 @@
+"""HIP-graph capture and replay of a whole train step (forward, backward, optimizer).
+
+MI355X-native replacement for a tracing compiler's launch-overhead removal: the step is captured
+once with ``torch.cuda.CUDAGraph`` (hipGraph on ROCm) and replayed every iteration, so ~800-1500
+kernel launches cost one graph launch and the GPU never waits for Python between kernels.
+
+What makes the step capturable (engine.Trainer splits it into host / device parts):
+* inputs: micro-batches are copied into static device tensors before each replay;
+* host-drawn values (learning-rate schedule, bias corrections, Mixup / CutMix decisions and
+  permutations) reach the step only through the step feeder's static device buffers
+  (runtime/feeder.py), written by ``Trainer.host_prepare`` outside the graph;
+* device RNG (MAE masking noise, droppath / dropout masks) uses the per-stream device
+  generators, registered with the graph so every replay advances their Philox offsets;
+* the step contains no host synchronisation (``--skip-nonfinite`` is refused in graph mode);
+* parameter gradients, optimizer moments, master weights and the bf16 shadow are persistent
+  buffers of the flat ParamStore -- the captured kernels update them in place.
+Scope: single-process steps (no DP reducer): RCCL collectives are not captured here.
+"""
+
+from __future__ import annotations
+
+import torch
+
+
+class GraphedTrainStep:
+    def __init__(self, trainer, example_micro_batches, warmup: int = 3):
+        if trainer.reducer is not None and trainer.reducer.enabled:
+            raise ValueError("HIP-graph step capture is single-process (no DP reducer)")
+        if trainer.skip_nonfinite:
+            raise ValueError("--skip-nonfinite needs a host sync per step; not capturable")
+        self.tr = trainer
+        self.static = [tuple(t.clone() for t in mb) for mb in example_micro_batches]
+        # warm up eagerly on a side stream (allocator pools, lazy weight copies, hipBLASLt plans)
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            for _ in range(warmup):
+                trainer.train_step(self.static)
+        torch.cuda.current_stream().wait_stream(side)
+        torch.cuda.synchronize()
+        self.graph = torch.cuda.CUDAGraph()
+        if trainer.rngs is not None:
+            for gen in trainer.rngs.gens.values():
+                self.graph.register_generator_state(gen)
+        trainer.host_prepare(self.static)
+        with torch.cuda.graph(self.graph):
+            self.out = trainer.device_step(self.static)
+        self.last_lr = trainer.host_finish()  # the capture ran the step once (as step `count`)
+        self.replays = 0
+
+    def __call__(self, micro_batches) -> dict:
+        for st, mb in zip(self.static, micro_batches):
+            for dst, src in zip(st, mb):
+                if dst.data_ptr() != src.data_ptr():
+                    dst.copy_(src, non_blocking=True)
+        self.tr.host_prepare(self.static)
+        self.graph.replay()
+        self.replays += 1
+        lr = self.tr.host_finish()
+        m = {k: v.clone() for k, v in self.out.items()}
+        m["learning_rate"] = lr
+        return m

@@ -36,6 +36,28 @@ class Trainer:
 
     def train_step(self, micro_batches) -> dict:
         """micro_batches: list (len grad_accum) of argument tuples for ``model.forward``."""
+        self.host_prepare(micro_batches)
+        metrics = self.device_step(micro_batches)
+        if metrics is None:  # non-finite loss, update skipped
+            return self._skipped
+        metrics["learning_rate"] = self.host_finish()
+        return metrics
+
+    # The step in three parts (runtime/graph.py captures ``device_step`` in a HIP graph and
+    # replays it; the host parts run before / after every replay):
+    #   host_prepare -- host-drawn per-step values (schedule, Mixup / CutMix decisions) into the
+    #                   step feeder's static device buffers;
+    #   device_step  -- device work only: zero grads, forward / backward per micro-batch, gradient
+    #                   reduction, optimizer kernels; returns device metric tensors;
+    #   host_finish  -- host bookkeeping (optimizer count, weight-shadow version); returns the lr.
+    def host_prepare(self, micro_batches) -> None:
+        prep = getattr(self.model, "prepare_step", None)
+        if prep is not None:
+            for i, args in enumerate(micro_batches):
+                prep(i, *args)
+        self.opt.prepare()
+
+    def device_step(self, micro_batches) -> dict | None:
         n = len(micro_batches)
         self.store.zero_grad()
         if self.reducer is not None:
@@ -45,6 +67,7 @@ class Trainer:
         for i, args in enumerate(micro_batches):
             if self.reducer is not None:
                 self.reducer.set_sync(i == n - 1)
+            self.model.micro_index = i
             with trace_range("fwd"):
                 out = self.model(*args, rngs=rng, det=False)
             loss = out["loss"]
@@ -57,19 +80,21 @@ class Trainer:
             with trace_range("allreduce_wait"):
                 self.reducer.set_sync(True)
                 self.reducer.finish()
+        metrics = {k: v / n for k, v in metrics_acc.items()}
         if self.skip_nonfinite:
             # opt-in guard (one host sync per step): drop the update of a step whose loss is
             # not finite instead of poisoning the weights / optimizer moments
             if not bool(torch.isfinite(metrics_acc["loss"]).item()):
                 self.skipped_steps += 1
-                metrics = {k: v / n for k, v in metrics_acc.items()}
                 metrics["learning_rate"] = self.opt.last_lr if hasattr(self.opt, "last_lr") else 0.0
-                return metrics
+                self._skipped = metrics
+                return None
         with trace_range("optimizer"):
-            lr = self.opt.step()
-        metrics = {k: v / n for k, v in metrics_acc.items()}
-        metrics["learning_rate"] = lr
+            self.opt.launch()
         return metrics
+
+    def host_finish(self) -> float:
+        return self.opt.finish()
 
     @torch.no_grad()
     def eval_step(self, args) -> dict:

@@ -32,15 +32,19 @@ class Mixup:
     def active(self) -> bool:
         return self.mixup_alpha > 0 or self.cutmix_alpha > 0
 
-    def _perm(self, n, device, gen):
-        return torch.randperm(n, device=device, generator=gen)
+    def _perm(self, n, device=None, gen=None):
+        """One permutation of the batch per mixed batch, drawn from the host generator (a step's
+        host draws all go through the step feeder, so the device work can replay from a graph)."""
+        return self.rs.permutation(n)
 
     # ---------------------------------------------------------------- batch plan
-    def plan(self, batch: int, height: int, width: int, device, gen=None) -> dict | None:
+    def plan(self, batch: int, height: int, width: int, device, gen=None, tag: str = "") -> dict | None:
         """Draw this batch's mixing decision (same RNG consumption order as the reference's
-        Mixup.__call__): ``{"mode": "mixup"|"cutmix", "ratio", "perm", "box"}`` where ``box`` =
-        (y0, y1, x0, x1) is the half-open pixel range taken from the permuted image and
-        ``label_w`` the weight of the own label.  None when mixing is off."""
+        Mixup.__call__): ``{"mode": "mixup"|"cutmix", "ratio", "perm", "box", "label_w"}`` where
+        ``box`` = (y0, y1, x0, x1) is the half-open pixel range taken from the permuted image and
+        ``label_w`` the weight of the own label.  On a GPU the decision is also delivered to static
+        device buffers (``dev``: params [mode, ratio, label_w], box, perm) through the step
+        feeder.  None when mixing is off."""
         if self.mixup_alpha == 0 and self.cutmix_alpha == 0:
             return None
         if self.mixup_alpha > 0 and self.cutmix_alpha > 0:
@@ -49,14 +53,29 @@ class Mixup:
             mode = "mixup" if self.mixup_alpha > 0 else "cutmix"
         if mode == "mixup":
             ratio = float(self.rs.beta(self.mixup_alpha, self.mixup_alpha))
-            perm = self._perm(batch, device, gen)
-            return {"mode": mode, "ratio": ratio, "perm": perm, "box": None, "label_w": ratio}
-        ratio = float(self.rs.beta(self.cutmix_alpha, self.cutmix_alpha))
-        box = self._box(ratio, width, height)
-        perm = self._perm(batch, device, gen)
-        y0, y1, x0, x1 = box
-        label_w = 1.0 - float((y1 - y0) * (x1 - x0)) / float(height * width)
-        return {"mode": mode, "ratio": ratio, "perm": perm, "box": box, "label_w": label_w}
+            box, label_w = None, ratio
+        else:
+            ratio = float(self.rs.beta(self.cutmix_alpha, self.cutmix_alpha))
+            box = self._box(ratio, width, height)
+            y0, y1, x0, x1 = box
+            label_w = 1.0 - float((y1 - y0) * (x1 - x0)) / float(height * width)
+        perm_np = self._perm(batch)
+        plan = {"mode": mode, "ratio": ratio, "box": box, "label_w": label_w}
+        device = torch.device(device)
+        if device.type == "cuda":
+            from ..runtime.feeder import feeder
+            f = feeder(device)
+            plan["dev"] = {
+                "params": f.put("mixup_params" + tag, [1.0 if mode == "mixup" else 2.0, ratio, label_w]),
+                "box": f.put("mixup_box" + tag, list(box) if box else [0, 0, 0, 0], dtype=torch.int32),
+                "perm": f.put("mixup_perm" + tag, perm_np, dtype=torch.int32),
+            }
+            plan["perm"] = plan["dev"]["perm"]  # int32, static (indexing casts inside the step)
+            plan["label_w_t"] = plan["dev"]["params"][2]
+        else:
+            plan["perm"] = torch.as_tensor(perm_np, dtype=torch.long)
+            plan["label_w_t"] = label_w
+        return plan
 
     def _box(self, ratio: float, width: int, height: int):
         """Pixel ranges of the CutMix box on the reference's linspace(0, 1, W|H) grid
@@ -81,8 +100,8 @@ class Mixup:
     def mix_labels(labels, plan):
         if plan is None:
             return labels
-        w = plan["label_w"]
-        return w * labels + (1 - w) * labels[plan["perm"]]
+        w = plan["label_w_t"]  # device scalar on a GPU (no host value enters the step)
+        return w * labels + (1 - w) * labels[plan["perm"].long()]
 
     @staticmethod
     def mix_images(images, plan):
@@ -90,7 +109,7 @@ class Mixup:
         the patch gather, ops/mae.py mixed_patches)."""
         if plan is None:
             return images
-        other = images[plan["perm"]]
+        other = images[plan["perm"].long().to(images.device)]
         if plan["mode"] == "mixup":
             r = plan["ratio"]
             return r * images + (1 - r) * other

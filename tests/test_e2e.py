@@ -62,7 +62,10 @@ def test_finetune_and_linear(tmp_path, mode, opt, lr):
         "--eval-interval", "4", "--output-dir", out, "--name", "f", *extra])
     res = FT.main(args)
     assert 0.0 <= res["val/acc1"] <= 1.0 and res["val/acc5"] >= res["val/acc1"]
-    assert os.path.exists(os.path.join(out, "f-best.msgpack"))
+    # reference semantics (main_finetune.py:86-88): "best" is written when val/acc1 beats the running
+    # maximum, which starts at 0
+    assert os.path.exists(os.path.join(out, "f-best.msgpack")) == (res.get("val/acc1/best", 0.0) > 0)
+    assert os.path.exists(os.path.join(out, "f-last.msgpack"))
 
 
 def test_skip_nonfinite_step_leaves_weights_untouched():

@@ -1,0 +1,88 @@
+"""HIP-graph capture / replay of the whole train step (runtime/graph.py) on MI355X."""
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _finetune(mixup: float, droppath: float):
+    from jumbo_mae_tpu_amd.config import ViTConfig
+    from jumbo_mae_tpu_amd.models.classifier import FinetuneModel
+    from jumbo_mae_tpu_amd.optim.flat import FlatOptimizer
+    from jumbo_mae_tpu_amd.optim.schedule import warmup_cosine_decay_schedule
+    from jumbo_mae_tpu_amd.train.engine import Trainer
+    from jumbo_mae_tpu_amd.utils.mixup import Mixup
+    from jumbo_mae_tpu_amd.utils.rng import RngStreams
+
+    vc = ViTConfig(layers=2, dim=256, heads=4, labels=10, image_size=64, patch_size=16, posemb="sincos2d",
+                   droppath=droppath)
+    m = FinetuneModel(vc, Mixup(mixup, mixup, seed=3), label_smoothing=0.1).to("cuda", torch.bfloat16, seed=0)
+    opt = FlatOptimizer(m.store, "adamw", warmup_cosine_decay_schedule(1e-6, 1e-3, 2, 20, 1e-6),
+                        weight_decay=0.05, lr_decay=0.75, num_layers=vc.layers)
+    return m, Trainer(m, opt, None, RngStreams({"mixup": 1, "dropout": 1, "noise": 1}, 0, "cuda"))
+
+
+def _batches(n, B=32, seed=0):
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    return [(torch.randint(0, 256, (B, 3, 64, 64), dtype=torch.uint8, device="cuda", generator=g),
+             torch.randint(0, 10, (B,), device="cuda", generator=g)) for _ in range(n)]
+
+
+def test_graphed_finetune_matches_eager():
+    """Deterministic config (no mixup / droppath): graph replays == eager steps."""
+    from jumbo_mae_tpu_amd.runtime.graph import GraphedTrainStep
+
+    data = _batches(8)
+    m1, t1 = _finetune(0.0, 0.0)
+    m2, t2 = _finetune(0.0, 0.0)
+    # the graph runner warms up (3 steps) and captures (1 step) on data[0]
+    gs = GraphedTrainStep(t2, [data[0]], warmup=3)
+    for _ in range(4):
+        t1.train_step([data[0]])
+    torch.cuda.synchronize()
+    assert torch.allclose(m1.store.master, m2.store.master, atol=1e-6, rtol=1e-5)
+    for i in range(1, 6):
+        a = t1.train_step([data[i]])
+        b = gs([data[i]])
+        assert abs(a["loss"].item() - b["loss"].item()) < 1e-4 * max(1.0, abs(a["loss"].item()))
+        assert abs(a["learning_rate"] - b["learning_rate"]) < 1e-12
+    torch.cuda.synchronize()
+    assert torch.allclose(m1.store.master, m2.store.master, atol=1e-5, rtol=1e-4)
+    assert gs.replays == 5
+
+
+def test_graphed_finetune_mixup_droppath_runs():
+    """Host-drawn Mixup / CutMix decisions and device RNG change between replays."""
+    from jumbo_mae_tpu_amd.runtime.graph import GraphedTrainStep
+
+    data = _batches(6)
+    m, t = _finetune(0.8, 0.1)
+    gs = GraphedTrainStep(t, [data[0]], warmup=2)
+    losses = [gs([data[i]])["loss"].item() for i in range(1, 6)]
+    assert all(l == l and 0 < l < 20 for l in losses)
+    assert len(set(round(l, 6) for l in losses)) == len(losses)
+
+
+def test_graphed_pretrain_runs_and_learns():
+    from jumbo_mae_tpu_amd.config import DecoderConfig, ViTConfig
+    from jumbo_mae_tpu_amd.models.mae import PretrainModel
+    from jumbo_mae_tpu_amd.optim.flat import FlatOptimizer
+    from jumbo_mae_tpu_amd.optim.schedule import warmup_cosine_decay_schedule
+    from jumbo_mae_tpu_amd.runtime.graph import GraphedTrainStep
+    from jumbo_mae_tpu_amd.train.engine import Trainer
+    from jumbo_mae_tpu_amd.utils.rng import RngStreams
+
+    vc = ViTConfig(layers=2, dim=256, heads=4, labels=0, image_size=64, patch_size=16, posemb="sincos2d",
+                   image_mask_ratio=0.75, droppath=0.1)
+    dc = DecoderConfig(dec_layers=2, dec_dim=128, dec_heads=4, image_size=64, patch_size=16)
+    m = PretrainModel(vc, dc).to("cuda", torch.bfloat16, seed=0)
+    opt = FlatOptimizer(m.store, "adamw", warmup_cosine_decay_schedule(1e-6, 2e-3, 2, 40, 1e-5), b2=0.95,
+                        weight_decay=0.05, num_layers=vc.layers)
+    t = Trainer(m, opt, None, RngStreams({"noise": 1, "dropout": 1}, 0, "cuda"))
+    img = _batches(1, B=64)[0][0]
+    gs = GraphedTrainStep(t, [(img,)], warmup=2)
+    losses = [gs([(img,)])["loss"].item() for _ in range(30)]
+    assert all(l == l for l in losses)
+    assert sum(losses[-5:]) < sum(losses[:5])  # same images, fresh masks each replay: it learns
+    assert len(set(round(l, 6) for l in losses[:5])) > 1  # masking noise advances per replay
