@@ -48,6 +48,8 @@ def main():
     ap.add_argument("--no-overlap", action="store_true")
     ap.add_argument("--profile-steps", type=int, default=0, help="extra steps under torch.profiler (debug)")
     ap.add_argument("--task", default="pretrain", choices=["pretrain", "finetune", "linear"])
+    ap.add_argument("--hip-graph", action="store_true",
+                    help="replay the captured train step from a HIP graph (single process; runtime/graph.py)")
     args = ap.parse_args()
     if args.task != "pretrain":
         return bench_classifier(args)
@@ -84,6 +86,8 @@ def main():
     reducer = GradReducer(store, bucket_mb=args.bucket_mb, overlap=not args.no_overlap) if world > 1 else None
     rngs = RngStreams({"noise": 0, "dropout": 0, "mixup": 0}, info.rank, dev)
     trainer = Trainer(model, opt, reducer, rngs, grad_accum=args.grad_accum)
+    from jumbo_mae_tpu_amd.runtime.graph import StepRunner
+    runner = StepRunner(trainer, hip_graph=args.hip_graph and world == 1)
 
     gen = torch.Generator(device=dev).manual_seed(1234 + info.rank)
     mb = B // args.grad_accum
@@ -102,7 +106,7 @@ def main():
         nonlocal it
         micro = [(pool[(it + j) % 2],) for j in range(args.grad_accum)]
         it += 1
-        return trainer.train_step(micro)
+        return runner(micro)
 
     t0 = time.time()
     for i in range(args.warmup):
@@ -158,6 +162,7 @@ def main():
                 "parallelism": f"dp{world}",
                 "per_gpu_batch": B,
                 "grad_accum": args.grad_accum,
+                "hip_graph": bool(runner.graphed is not None),
                 "optimizer": "adamw(0.9,0.95) wd0.05 warmup-cosine",
                 "final_loss": round(final_loss, 5),
             },
@@ -203,10 +208,14 @@ def bench_classifier(args):
     pdist.broadcast_(model.store.master)
     model.store.sync_shadow()
     peak = fargs.learning_rate * gb / 256 if fargs.optimizer == "lars" else fargs.learning_rate
-    opt = C.make_optimizer(fargs, model.store, peak, 1e-6)
+    import contextlib
+    with contextlib.redirect_stdout(sys.stderr):  # stdout carries only the JSON result line
+        opt = C.make_optimizer(fargs, model.store, peak, 1e-6)
     reducer = C.make_reducer(fargs, model.store)
     rngs = RngStreams({"mixup": 1, "dropout": 1, "noise": 1}, info.rank, dev)
     trainer = Trainer(model, opt, reducer, rngs)
+    from jumbo_mae_tpu_amd.runtime.graph import StepRunner
+    runner = StepRunner(trainer, hip_graph=args.hip_graph and world == 1)
     gen = torch.Generator(device=dev).manual_seed(1234 + info.rank)
     pool = [(torch.randint(0, 256, (B, 3, 224, 224), dtype=torch.uint8, device=dev, generator=gen),
              torch.randint(0, 1000, (B,), device=dev, generator=gen)) for _ in range(2)]
@@ -217,7 +226,7 @@ def bench_classifier(args):
 
     def step():
         nonlocal it
-        m = trainer.train_step([pool[it % 2]])
+        m = runner([pool[it % 2]])
         it += 1
         return m
 
@@ -248,6 +257,7 @@ def bench_classifier(args):
             "data": "synthetic uint8 224x224 images + random labels on GPU, random-init weights",
             "config": {"model": model_name, "global_batch": gb, "seq_len": model.cfg.num_cls_tokens
                        + model.cfg.seq_patches, "parallelism": f"dp{world}", "per_gpu_batch": B,
+                       "hip_graph": bool(runner.graphed is not None),
                        "recipe": recipe, "final_loss": round(float(m["loss"].item()), 5)},
         }), flush=True)
     pdist.cleanup()

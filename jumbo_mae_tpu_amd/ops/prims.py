@@ -81,7 +81,7 @@ def wgrad(h: Handle, dy: torch.Tensor, x: torch.Tensor, rows: tuple[int, int] | 
 
 
 def bias_grad(hb: Handle, dy: torch.Tensor) -> None:
-    if hip(dy):
+    if hip(dy) and dy.dtype == torch.bfloat16 and dy.shape[-1] % 8 == 0 and dy.stride(-1) == 1:
         _ext.load().colsum(dy, hb.grad)
     else:
         hb.grad.add_(dy.sum(0, dtype=torch.float32))

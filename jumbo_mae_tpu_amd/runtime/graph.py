@@ -22,14 +22,36 @@ from __future__ import annotations
 import torch
 
 
+def _state_tensors(trainer) -> list[torch.Tensor]:
+    """Persistent tensors a step mutates (restored after warm-up / capture with ``restore``)."""
+    ts = [trainer.store.master]
+    for k in ("mu", "nu", "trace"):
+        v = getattr(trainer.opt, k, None)
+        if v is not None:
+            ts.append(v)
+    head = getattr(trainer.model, "head", None)
+    for k in ("running_mean", "running_var"):
+        v = getattr(head, k, None) if head is not None else None
+        if isinstance(v, torch.Tensor):
+            ts.append(v)
+    return ts
+
+
 class GraphedTrainStep:
-    def __init__(self, trainer, example_micro_batches, warmup: int = 3):
+    """``restore=True`` (training drivers): the warm-up steps are undone afterwards --
+    weights, optimizer moments, BatchNorm statistics and the optimizer count are put back, so the
+    first replay is the run's first real step (device RNG streams simply continue)."""
+
+    def __init__(self, trainer, example_micro_batches, warmup: int = 3, restore: bool = False):
         if trainer.reducer is not None and trainer.reducer.enabled:
             raise ValueError("HIP-graph step capture is single-process (no DP reducer)")
         if trainer.skip_nonfinite:
             raise ValueError("--skip-nonfinite needs a host sync per step; not capturable")
         self.tr = trainer
         self.static = [tuple(t.clone() for t in mb) for mb in example_micro_batches]
+        snap = None
+        if restore:
+            snap = ([t.clone() for t in _state_tensors(trainer)], trainer.opt.count, trainer.opt.last_lr)
         # warm up eagerly on a side stream (allocator pools, lazy weight copies, hipBLASLt plans)
         side = torch.cuda.Stream()
         side.wait_stream(torch.cuda.current_stream())
@@ -43,10 +65,16 @@ class GraphedTrainStep:
             for gen in trainer.rngs.gens.values():
                 self.graph.register_generator_state(gen)
         trainer.host_prepare(self.static)
-        with torch.cuda.graph(self.graph):
+        with torch.cuda.graph(self.graph):  # recorded, not executed: no host_finish for it
             self.out = trainer.device_step(self.static)
-        self.last_lr = trainer.host_finish()  # the capture ran the step once (as step `count`)
         self.replays = 0
+        if snap is not None:
+            torch.cuda.synchronize()
+            for dst, src in zip(_state_tensors(trainer), snap[0]):
+                dst.copy_(src)
+            trainer.opt.count, trainer.opt.last_lr = snap[1], snap[2]
+            trainer.store.sync_shadow()
+            torch.cuda.synchronize()
 
     def __call__(self, micro_batches) -> dict:
         for st, mb in zip(self.static, micro_batches):
@@ -60,3 +88,20 @@ class GraphedTrainStep:
         m = {k: v.clone() for k, v in self.out.items()}
         m["learning_rate"] = lr
         return m
+
+
+class StepRunner:
+    """``trainer.train_step`` or, with ``hip_graph``, a GraphedTrainStep built on the first call
+    (drivers: ``--hip-graph``)."""
+
+    def __init__(self, trainer, hip_graph: bool = False):
+        self.tr = trainer
+        self.hip_graph = hip_graph
+        self.graphed = None
+
+    def __call__(self, micro_batches) -> dict:
+        if not self.hip_graph:
+            return self.tr.train_step(micro_batches)
+        if self.graphed is None:
+            self.graphed = GraphedTrainStep(self.tr, micro_batches, restore=True)
+        return self.graphed(micro_batches)

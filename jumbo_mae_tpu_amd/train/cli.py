@@ -83,6 +83,8 @@ def _extensions(p: argparse.ArgumentParser):
     g.add_argument("--device", default=None, help="cuda|cpu (default: cuda if available)")
     g.add_argument("--log-file-only", action="store_true", help="never use wandb even if installed")
     g.add_argument("--trace-ranges", action="store_true", help="roctx ranges per step phase (rocprofv3 --marker-trace)")
+    g.add_argument("--hip-graph", action="store_true",
+                   help="capture the whole train step once in a HIP graph and replay it (single process)")
     g.add_argument("--skip-nonfinite", action="store_true",
                    help="skip the update of a step whose loss is non-finite (one host sync per step); "
                         "default: abort at the next log step")

@@ -27,6 +27,7 @@ from ..utils.trace import set_enabled as set_trace_ranges
 from ..utils.rng import RngStreams
 from . import common as C
 from .cli import finetune_parser
+from ..runtime.graph import StepRunner
 from .engine import Trainer
 from .meter import AverageMeter, Logger
 
@@ -76,6 +77,7 @@ def main(args) -> dict:
     rngs = RngStreams({"mixup": args.mixup_seed, "dropout": args.dropout_seed, "noise": args.noise_seed},
                       info.rank, device)
     trainer = Trainer(model, opt, reducer, rngs, args.grad_accum, skip_nonfinite=args.skip_nonfinite)
+    run_step = StepRunner(trainer, hip_graph=args.hip_graph and device.type == "cuda" and info.world_size == 1)
     start = C.maybe_resume(args, model, opt, rngs, log)
 
     def extra():
@@ -98,7 +100,7 @@ def main(args) -> dict:
     perf = C.PerfClock(start, args.train_batch_size, finetune_fwd_flops_per_image(model.cfg), info.world_size)
     for step in range(start + 1, args.training_steps + 1):
         micro = [tuple(next(it)) for _ in range(args.grad_accum)]
-        metrics = trainer.train_step(micro)
+        metrics = run_step(micro)
         meter.update(**metrics)
         if args.log_interval > 0 and step % args.log_interval == 0:
             summ = meter.summary("train/")

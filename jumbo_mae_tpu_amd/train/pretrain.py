@@ -26,6 +26,7 @@ from ..utils.rng import RngStreams
 from ..utils.trace import set_enabled as set_trace_ranges
 from . import common as C
 from .cli import pretrain_parser
+from ..runtime.graph import StepRunner
 from .engine import Trainer
 from .meter import AverageMeter, Logger
 
@@ -71,6 +72,7 @@ def main(args) -> dict:
     rngs = RngStreams({"mixup": args.mixup_seed, "dropout": args.dropout_seed, "noise": args.noise_seed},
                       info.rank, device)
     trainer = Trainer(model, opt, reducer, rngs, args.grad_accum, skip_nonfinite=args.skip_nonfinite)
+    run_step = StepRunner(trainer, hip_graph=args.hip_graph and device.type == "cuda" and info.world_size == 1)
     start = C.maybe_resume(args, model, opt, rngs, log)
 
     train_loader, valid_loader = create_dataloaders(args, info.rank, info.world_size)
@@ -92,7 +94,7 @@ def main(args) -> dict:
         for _ in range(args.grad_accum):
             b = next(it)
             micro.append((b[0] if isinstance(b, (list, tuple)) else b,))
-        metrics = trainer.train_step(micro)
+        metrics = run_step(micro)
         meter.update(**metrics)
         if args.log_interval > 0 and step % args.log_interval == 0:
             summ = meter.summary("train/")

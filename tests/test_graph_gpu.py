@@ -36,9 +36,9 @@ def test_graphed_finetune_matches_eager():
     data = _batches(8)
     m1, t1 = _finetune(0.0, 0.0)
     m2, t2 = _finetune(0.0, 0.0)
-    # the graph runner warms up (3 steps) and captures (1 step) on data[0]
+    # the graph runner warms up (3 eager steps) on data[0]; the capture itself executes nothing
     gs = GraphedTrainStep(t2, [data[0]], warmup=3)
-    for _ in range(4):
+    for _ in range(3):
         t1.train_step([data[0]])
     torch.cuda.synchronize()
     assert torch.allclose(m1.store.master, m2.store.master, atol=1e-6, rtol=1e-5)
@@ -86,3 +86,18 @@ def test_graphed_pretrain_runs_and_learns():
     assert all(l == l for l in losses)
     assert sum(losses[-5:]) < sum(losses[:5])  # same images, fresh masks each replay: it learns
     assert len(set(round(l, 6) for l in losses[:5])) > 1  # masking noise advances per replay
+
+
+def test_graph_restore_undoes_warmup():
+    from jumbo_mae_tpu_amd.runtime.graph import GraphedTrainStep
+
+    data = _batches(3)
+    m1, t1 = _finetune(0.0, 0.0)
+    m2, t2 = _finetune(0.0, 0.0)
+    gs = GraphedTrainStep(t2, [data[0]], warmup=2, restore=True)
+    assert torch.equal(m1.store.master, m2.store.master) and t2.opt.count == 0
+    a = t1.train_step([data[1]])
+    b = gs([data[1]])
+    assert abs(a["loss"].item() - b["loss"].item()) < 1e-4 * max(1.0, abs(a["loss"].item()))
+    torch.cuda.synchronize()
+    assert torch.allclose(m1.store.master, m2.store.master, atol=1e-6, rtol=1e-5)
