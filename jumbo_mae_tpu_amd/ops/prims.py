@@ -94,8 +94,11 @@ _DGRAD_OURS = os.environ.get("JMAE_DGRAD", "1") == "1"  # data-gradient GEMMs on
 # flagship shapes the rule below would reject but where the MFMA kernel measured faster
 # (tools/gemm_nt_bench.py, profiles/r1_gemm_nt_vs_hipblaslt_v2.txt): ViT-L encoder QKV / Wo and
 # MAE-decoder Wo data gradients (1.05x, 1.08x, 1.11x), decoder Wo forward (1.02x)
-_OURS_MEASURED = {"dgrad": {(26624, 1024, 3072), (26624, 1024, 1024), (101888, 512, 512)},
-                  "fwd": {(101888, 512, 512)}}
+_OURS_MEASURED = {"dgrad": {(26624, 1024, 3072), (26624, 1024, 1024), (101888, 512, 512), (26624, 768, 768)},
+                  "fwd": {(101888, 512, 512), (26624, 768, 768)}}
+# ... and shapes the rule would accept where hipBLASLt measured faster (ViT-B encoder QKV forward,
+# 105 vs 98 us; profiles/r1_gemm_vitb_shapes.txt)
+_BLAS_MEASURED = {"fwd": {(26624, 2304, 768)}, "dgrad": set()}
 
 
 def use_our_gemm(M: int, N: int, K: int, fused_gelu: bool = False, kind: str = "fwd") -> bool:
@@ -114,6 +117,8 @@ def use_our_gemm(M: int, N: int, K: int, fused_gelu: bool = False, kind: str = "
         return True
     if (M, N, K) in _OURS_MEASURED.get(kind, ()):
         return True
+    if (M, N, K) in _BLAS_MEASURED.get(kind, ()) and not fused_gelu:
+        return False
     if K > 1024:
         return False
     tiles = -(-M // 256) * -(-N // 256)

@@ -19,6 +19,9 @@ FWD = {
     "enc_ff2": (25088, 1024, 4096), "jumbo1": (512, 12288, 3072), "jumbo2": (512, 3072, 12288),
     "dec_qkv": (101888, 1536, 512), "dec_wo": (101888, 512, 512), "dec_ff1": (101888, 2048, 512),
     "dec_ff2": (101888, 512, 2048),
+    # ViT-B/16 encoder (D = 768, J = 2304)
+    "b_qkv": (26624, 2304, 768), "b_wo": (26624, 768, 768), "b_ff1": (25088, 3072, 768),
+    "b_ff2": (25088, 768, 3072), "b_jumbo1": (512, 9216, 2304), "b_jumbo2": (512, 2304, 9216),
 }
 
 
@@ -48,9 +51,9 @@ def main():
     for kind in a.kinds.split(","):
         for name in names:
             M, N, K = FWD[name]
-            if kind == "fwd_gelu" and name not in ("enc_ff1", "dec_ff1", "jumbo1"):
+            if kind == "fwd_gelu" and name not in ("enc_ff1", "dec_ff1", "jumbo1", "b_ff1"):
                 continue
-            if kind == "dgrad_gelu" and name not in ("enc_ff2", "dec_ff2"):
+            if kind == "dgrad_gelu" and name not in ("enc_ff2", "dec_ff2", "b_ff2"):
                 continue
             if kind == "splitk" and name not in ("jumbo1", "jumbo2"):
                 continue
