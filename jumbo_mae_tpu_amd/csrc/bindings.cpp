@@ -47,20 +47,12 @@ void jm_opt_apply_trust(float* p, const float* u_or_g, float* trace, uint16_t* s
                         float momentum, float trust_coef, hipStream_t st);
 void jm_opt_sgd(float* p, const float* g, float* trace, uint16_t* shadow, const int* chunks, int nchunks,
                 const float* meta, const float* hyper, const float* gnorm_sq, float momentum, hipStream_t st);
-struct GemmEpi {
-  const float* bias;
-  uint16_t* out;
-  long ldo;
-  uint16_t* out2;
-  const uint16_t* aux;
-  float* colpart;
-  float* part;
-  int splits;
-};
 int jm_splitk_reduce_bf16(const float* part, int S, long n, int N, const float* bias, uint16_t* out, hipStream_t st);
 int jm_gemm_nt(const uint16_t* A, long lda, const uint16_t* B, long ldb, int M, int N, int K, int epi,
                const GemmEpi& ep, hipStream_t st);
 void jm_gemm_set_variant(int wn, int group);
+void jm_gemm_set_tail(int on);
+int jm_gemm_nt_tail_plan(int M, int N, int K, int epi, int* tail_r, long* ws_floats);
 int jm_gemm_tn_plan(int M, int N, int K, int* S_out);
 int jm_gemm_tn(const uint16_t* A, long lda, const uint16_t* B, long ldb, int M, int N, int K, int sps, int S,
                float* G, long ldo, float* partial, hipStream_t st);
@@ -539,6 +531,20 @@ torch::Tensor patch_mse_bwd(torch::Tensor pred, torch::Tensor img, torch::Tensor
 // ------------------------------------------------------------------------------ GEMM
 // C[M, N] = A[M, K] . B[N, K]^T (+ bias) in bf16 (fp32 accumulate); gelu=true also returns
 // gelu(C) (the pre-activation C is what the backward needs).  A / B rows may be strided.
+// tail split (gemm.hip jm_gemm_nt_tail_plan): workspace for the split-K partials of the last,
+// partly filled wave of output tiles; returns the number of tail tiles (0 = plain launch)
+int attach_tail(GemmEpi& ep, torch::Tensor& ws, int M, int N, int K, int epi, const torch::Tensor& like) {
+  int r = 0;
+  long n = 0;
+  const int S = jm_gemm_nt_tail_plan(M, N, K, epi, &r, &n);
+  if (S < 2) return 0;
+  ws = torch::empty({n}, like.options().dtype(torch::kFloat32));
+  ep.tail = ws.data_ptr<float>();
+  ep.tail_S = S;
+  ep.t_count = r;
+  return r;
+}
+
 std::vector<torch::Tensor> gemm_nt(torch::Tensor A, torch::Tensor B, c10::optional<torch::Tensor> bias, bool gelu,
                                    bool gelu_only) {
   CHECK_DT(A, torch::kBFloat16);
@@ -558,6 +564,8 @@ std::vector<torch::Tensor> gemm_nt(torch::Tensor A, torch::Tensor B, c10::option
     ep.out2 = bfm(out2);
   }
   const int epi = gelu_only ? 4 : (gelu ? 1 : 0);
+  torch::Tensor ws;
+  attach_tail(ep, ws, M, N, K, epi, A);
   check_rc(jm_gemm_nt(bf(A), A.stride(0), bf(B), B.stride(0), M, N, K, epi, ep, stream()), "gemm_nt");
   if (gelu && !gelu_only) return {out, out2};
   return {out};
@@ -597,12 +605,18 @@ torch::Tensor gemm_nt_dgelu(torch::Tensor A, torch::Tensor B, torch::Tensor pre,
   auto out = torch::empty({M, N}, A.options());
   torch::Tensor part;
   GemmEpi ep{nullptr, bfm(out), N, nullptr, bf(pre), nullptr, nullptr, 1};
-  const int nM = (M + 255) / 256;
+  torch::Tensor ws;
+  const int r = attach_tail(ep, ws, M, N, K, 2, A);
+  int nM = (M + 255) / 256;
   if (dbias) {
     TORCH_CHECK(dbias->is_contiguous() && dbias->scalar_type() == torch::kFloat32 && dbias->numel() == N,
                 "gemm_nt_dgelu dbias");
-    part = torch::empty({nM, N}, A.options().dtype(torch::kFloat32));
+    // tail tiles: their entries of the nM per-row-tile rows stay zero; the finish kernel writes
+    // 8 extra rows per tail tile
+    part = r ? torch::zeros({nM + 8 * r, N}, A.options().dtype(torch::kFloat32))
+             : torch::empty({nM, N}, A.options().dtype(torch::kFloat32));
     ep.colpart = part.data_ptr<float>();
+    nM += 8 * r;
   }
   check_rc(jm_gemm_nt(bf(A), A.stride(0), bf(B), B.stride(0), M, N, K, 2, ep, stream()), "gemm_nt_dgelu");
   if (dbias) check_rc(jm_splitk_reduce_add(part.data_ptr<float>(), dbias->data_ptr<float>(), N, nM, stream()),
@@ -728,6 +742,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("gemm_tn_wgrad", &gemm_tn_wgrad);
   m.def("gemm_tn_wgrad_seg", &gemm_tn_wgrad_seg);
   m.def("gemm_set_variant", &jm_gemm_set_variant, py::arg("wn"), py::arg("group") = 8);
+  m.def("gemm_set_tail", &jm_gemm_set_tail);
   m.def("gemm_nt_splitk", &gemm_nt_splitk, py::arg("A"), py::arg("B"), py::arg("bias") = py::none(),
         py::arg("splits") = 8);
   m.def("gemm_nt_dgelu", &gemm_nt_dgelu, py::arg("A"), py::arg("B"), py::arg("pre"), py::arg("dbias") = py::none());

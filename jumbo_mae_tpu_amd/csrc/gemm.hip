@@ -27,6 +27,7 @@
 #include <type_traits>
 
 #include "common.h"
+#include "jm_api.h"
 
 namespace {
 
@@ -62,16 +63,6 @@ struct Frags {
 
 }  // namespace
 
-struct GemmEpi {
-  const float* bias;     // [N] fp32 or null
-  uint16_t* out;         // bf16 [M, ldo]
-  long ldo;
-  uint16_t* out2;        // EPI_GELU: gelu(out) bf16 [M, ldo]
-  const uint16_t* aux;   // EPI_DGELU: pre-activation h bf16 [M, ldo]
-  float* colpart;        // EPI_DGELU: per-row-tile column sums of out, [ceil(M/256)][N] fp32 (or null)
-  float* part;           // EPI_PARTIAL: [splits][M][N] fp32 split-K partial products
-  int splits;            // K splits (1 = none)
-};
 
 // EPI_STORE: out = acc (+bias); EPI_GELU: out = acc (+bias), out2 = gelu(out);
 // EPI_DGELU: out = bf16(acc) * gelu'(aux) -- the data gradient through the FF GELU -- with the
@@ -81,7 +72,8 @@ struct GemmEpi {
 // K = 12288) whose 24 output tiles would otherwise occupy 24 of 256 CUs.
 // EPI_GELU_ONLY: out = gelu(bf16(acc + bias)) alone -- inference (no backward needs the
 // pre-activation), half the epilogue bytes of EPI_GELU.
-enum { EPI_STORE = 0, EPI_GELU = 1, EPI_DGELU = 2, EPI_PARTIAL = 3, EPI_GELU_ONLY = 4 };
+// EPI_TAIL: split-K partial tile of a tail-split launch, stored compact in ep.tail (see GemmEpi).
+enum { EPI_STORE = 0, EPI_GELU = 1, EPI_DGELU = 2, EPI_PARTIAL = 3, EPI_GELU_ONLY = 4, EPI_TAIL = 5 };
 
 namespace {
 
@@ -133,6 +125,29 @@ JM_DEVICE void tile_of(int M, int N, int GROUP_M, int& m0, int& n0, int splits =
   const int gsz = min(nM - first_m, GROUP_M);
   m0 = (first_m + (wg % per_group) % gsz) * BM;
   n0 = ((wg % per_group) / gsz) * BNT;
+}
+
+// tile g (grouped order: GROUP_M row tiles sweep the column tiles) -> (m0, n0)
+JM_DEVICE void tile_coords(int g, int M, int N, int GROUP_M, int& m0, int& n0) {
+  const int nM = (M + BM - 1) / BM, nN = (N + BN - 1) / BN;
+  const int per_group = GROUP_M * nN;
+  const int first_m = (g / per_group) * GROUP_M;
+  const int gsz = min(nM - first_m, GROUP_M);
+  m0 = (first_m + (g % per_group) % gsz) * BM;
+  n0 = ((g % per_group) / gsz) * BN;
+}
+
+// launch restricted to tiles [t_begin, t_begin + t_count) (x splits, split-major): bijective XCD
+// remap over this launch's grid, then the global grouped order
+JM_DEVICE void tile_of_range(int M, int N, int GROUP_M, int t_begin, int t_count, int splits, int& m0, int& n0,
+                             int& split, int& tg) {
+  const int nwg = t_count * splits;
+  const int orig = blockIdx.x;
+  const int xcd = orig & 7, q = nwg >> 3, r = nwg & 7;
+  int wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+  split = wg / t_count;
+  tg = wg - split * t_count;
+  tile_coords(t_begin + tg, M, N, GROUP_M, m0, n0);
 }
 
 // WN waves along N (2 along M): WN = 4 -> 8 waves of 128 x 64 (2 waves / SIMD);
@@ -412,12 +427,16 @@ __attribute__((always_inline)) JM_DEVICE void nt64_body(const uint16_t* __restri
   const int l16 = lane & 15, g = lane >> 4;
   const int wr = wave >> 2, wc = wave & 3;
 
-  int m0, n0, split = 0;
-  tile_of(M, N, GROUP_M, m0, n0, EPI == EPI_PARTIAL ? ep.splits : 1, EPI == EPI_PARTIAL ? &split : nullptr);
+  int m0, n0, split = 0, tg = 0;
+  if (ep.t_count > 0)
+    tile_of_range(M, N, GROUP_M, ep.t_begin, ep.t_count, EPI == EPI_TAIL ? ep.tail_S : 1, m0, n0, split, tg);
+  else
+    tile_of(M, N, GROUP_M, m0, n0, EPI == EPI_PARTIAL ? ep.splits : 1, EPI == EPI_PARTIAL ? &split : nullptr);
   int k_begin = 0;
-  if (EPI == EPI_PARTIAL) {
+  if (EPI == EPI_PARTIAL || EPI == EPI_TAIL) {
+    const int ns = EPI == EPI_TAIL ? ep.tail_S : ep.splits;
     const int ku = K / 64;
-    const int ku0 = split * ku / ep.splits, ku1 = (split + 1) * ku / ep.splits;
+    const int ku0 = split * ku / ns, ku1 = (split + 1) * ku / ns;
     k_begin = ku0 * 64;
     K = (ku1 - ku0) * 64;
   }
@@ -528,7 +547,19 @@ __attribute__((always_inline)) JM_DEVICE void nt64_body(const uint16_t* __restri
   stage(K0{}, u, f0, f1);
   if (PRIO) __builtin_amdgcn_s_setprio(0);
 
-  if (EPI == EPI_PARTIAL) {
+  if (EPI == EPI_TAIL) {  // compact fp32 partial tile: tail[split][tg][256][256] (rows past M unused)
+    float* dst = ep.tail + ((long)split * ep.t_count + tg) * (BM * BN);
+#pragma unroll
+    for (int mt = 0; mt < 8; ++mt) {
+      const int ml = wr * 128 + mt * 16 + l16;
+#pragma unroll
+      for (int nt = 0; nt < NTW; ++nt) {
+        const int nl = wc * NTW * 16 + nt * 16 + 4 * g;
+        float v[4] = {acc[mt][nt][0], acc[mt][nt][1], acc[mt][nt][2], acc[mt][nt][3]};
+        store4(dst + ml * BN + nl, v);
+      }
+    }
+  } else if (EPI == EPI_PARTIAL) {
     float* dst = ep.part + (long)split * M * N;
 #pragma unroll
     for (int mt = 0; mt < 8; ++mt) {
@@ -945,6 +976,78 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_persist_kernel(const uint16_t*
   finish_tile(u + 2);
 }
 
+// ------------------------------------------------------------------ tail split finish
+// Sums the tail_S compact fp32 partials of the tail tiles and applies the launch's epilogue
+// (same rounding points as epilogue_lds).  Block = 32 rows of one tail tile; thread = 4 rows x 8
+// columns.  EPI_DGELU: the 32-row column sums go to colpart row nM + 8 * tile + row block
+// (the caller zero-fills colpart and reduces all its rows).
+template <int EPI>
+__global__ __launch_bounds__(256) void tail_finish_kernel(GemmEpi ep, int M, int N, int GROUP_M) {
+  __shared__ float red[8][BN];
+  const int tg = blockIdx.x >> 3, rb = blockIdx.x & 7;
+  int m0, n0;
+  tile_coords(ep.t_begin + tg, M, N, GROUP_M, m0, n0);
+  const int tid = threadIdx.x, c = tid & 31, rr = tid >> 5;
+  const int n = n0 + c * 8;
+  float csum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  float bv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (ep.bias && n < N) load8(ep.bias + n, bv);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int rl = rb * 32 + rr + 8 * i;
+    const int m = m0 + rl;
+    if (m >= M || n >= N) continue;
+    float v[8];
+    load8(ep.tail + (long)tg * (BM * BN) + rl * BN + c * 8, v);
+    for (int sp = 1; sp < ep.tail_S; ++sp) {
+      float w[8];
+      load8(ep.tail + ((long)sp * ep.t_count + tg) * (BM * BN) + rl * BN + c * 8, w);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] += w[j];
+    }
+    uint16_t* o = ep.out + (long)m * ep.ldo + n;
+    if (EPI == EPI_DGELU) {
+      float hp[8], f[8];
+      load8(ep.aux + (long)m * ep.ldo + n, hp);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        f[j] = bf2f(f2bf(bf2f(f2bf(v[j])) * gelu_grad_f(hp[j])));
+        csum[j] += f[j];
+      }
+      store8(o, f);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = bf2f(f2bf(v[j] + bv[j]));  // the bf16 pre-activation
+      if (EPI == EPI_GELU_ONLY) {
+        float gq[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) gq[j] = gelu_tanh_f(v[j]);
+        store8(o, gq);
+      } else {
+        store8(o, v);
+      }
+      if (EPI == EPI_GELU) {
+        float gq[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) gq[j] = gelu_tanh_f(v[j]);
+        store8(ep.out2 + (long)m * ep.ldo + n, gq);
+      }
+    }
+  }
+  if (EPI == EPI_DGELU && ep.colpart != nullptr) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) red[rr][c * 8 + j] = csum[j];
+    __syncthreads();
+    if (n0 + tid < N) {
+      float a = 0.f;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) a += red[q][tid];
+      const int nM = (M + BM - 1) / BM;
+      ep.colpart[(long)(nM + tg * 8 + rb) * N + n0 + tid] = a;
+    }
+  }
+}
+
 size_t jm_gemm_smem() { return (size_t)NST * STAGE * sizeof(uint16_t); }
 
 // returns 0 on success, <0 on unsupported shape
@@ -1045,12 +1148,72 @@ void launch_epi(const uint16_t* A, long lda, const uint16_t* B, long ldb, int M,
     launch_nt<EPI, 4>(A, lda, B, ldb, M, N, K, ep, nwg, st);
 }
 
+
+// tail split of the last partial wave (A/B switch).  Off: measured slower on every shape it applies
+// to (enc FF1 199 -> 215 us, decoder Wo 70 -> 81 us; ViT-L step +0.9 ms, profiles/r1_gemm_tail_split.txt)
+// -- the last, sparsely filled wave already runs faster per tile than a full one
+int g_gemm_tail = 0;
+
+int num_cus() {
+  if (g_num_cus == 0) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    hipDeviceProp_t prop;
+    (void)hipGetDeviceProperties(&prop, dev);
+    g_num_cus = prop.multiProcessorCount;
+  }
+  return g_num_cus;
+}
+
+template <int EPI>
+void launch_tail(const uint16_t* A, long lda, const uint16_t* B, long ldb, int M, int N, int K, const GemmEpi& ep,
+                 int tiles, hipStream_t st) {
+  const int r = ep.t_count;  // tail tiles
+  GemmEpi em = ep;
+  em.t_begin = 0;
+  em.t_count = tiles - r;
+  launch_epi<EPI>(A, lda, B, ldb, M, N, K, em, tiles - r, st);
+  GemmEpi et = ep;
+  et.t_begin = tiles - r;
+  if (g_gemm_wn == 12)
+    launch_nt64<EPI_TAIL, 4>(A, lda, B, ldb, M, N, K, et, r * ep.tail_S, st);
+  else
+    launch_nt64<EPI_TAIL, 0>(A, lda, B, ldb, M, N, K, et, r * ep.tail_S, st);
+  tail_finish_kernel<EPI><<<r * 8, 256, 0, st>>>(et, M, N, g_gemm_group);
+}
+
 }  // namespace
 
 void jm_gemm_set_variant(int wn, int group) {
   g_gemm_wn = wn;
   g_gemm_group = group;
 }
+
+void jm_gemm_set_tail(int on) { g_gemm_tail = on; }
+
+// Tail split plan for an NT launch: the last wave of output tiles (tiles % CUs of them) fills only
+// part of the chip; when it is at most a quarter wave, those tiles run split-K S ways (compact fp32
+// partials, *ws_floats) and a finish kernel applies the epilogue.  Returns S (0 = no tail split);
+// *tail_r = number of tail tiles.
+int jm_gemm_nt_tail_plan(int M, int N, int K, int epi, int* tail_r, long* ws_floats) {
+  *tail_r = 0;
+  *ws_floats = 0;
+  if (!g_gemm_tail || (g_gemm_wn != 12 && g_gemm_wn != 6)) return 0;
+  if (!(epi == EPI_STORE || epi == EPI_GELU || epi == EPI_DGELU || epi == EPI_GELU_ONLY) || N % 8 || K % 128) return 0;
+  const int ncu = num_cus();
+  const int tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
+  if (tiles < ncu) return 0;
+  const int r = tiles % ncu;
+  if (r == 0 || r > ncu / 4) return 0;
+  int S = ncu / r;
+  if (S > K / 64) S = K / 64;
+  if (S > 8) S = 8;
+  if (S < 2) return 0;
+  *tail_r = r;
+  *ws_floats = (long)S * r * BM * BN;
+  return S;
+}
+
 
 // returns 0 on success, <0 on unsupported shape
 int jm_gemm_nt(const uint16_t* A, long lda, const uint16_t* B, long ldb, int M, int N, int K, int epi,
@@ -1059,6 +1222,15 @@ int jm_gemm_nt(const uint16_t* A, long lda, const uint16_t* B, long ldb, int M, 
   if ((long)M * lda * 2 >= (1L << 32) || (long)N * ldb * 2 >= (1L << 32)) return -2;
   const int nwg = ((M + BM - 1) / BM) * ((N + BN - 1) / BN) * (epi == EPI_PARTIAL ? ep.splits : 1);
   if (epi == EPI_PARTIAL && (ep.splits < 1 || (K / 64) < ep.splits)) return -4;
+  if (ep.tail != nullptr && ep.tail_S >= 2 && ep.t_count > 0) {  // tail split (jm_gemm_nt_tail_plan)
+    const int tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
+    if (epi == EPI_STORE) launch_tail<EPI_STORE>(A, lda, B, ldb, M, N, K, ep, tiles, st);
+    else if (epi == EPI_GELU) launch_tail<EPI_GELU>(A, lda, B, ldb, M, N, K, ep, tiles, st);
+    else if (epi == EPI_DGELU) launch_tail<EPI_DGELU>(A, lda, B, ldb, M, N, K, ep, tiles, st);
+    else if (epi == EPI_GELU_ONLY) launch_tail<EPI_GELU_ONLY>(A, lda, B, ldb, M, N, K, ep, tiles, st);
+    else return -3;
+    return 0;
+  }
   if (epi == EPI_PARTIAL)
     launch_epi<EPI_PARTIAL>(A, lda, B, ldb, M, N, K, ep, nwg, st);
   else if (epi == EPI_STORE)

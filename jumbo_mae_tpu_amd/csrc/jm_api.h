@@ -15,3 +15,22 @@ struct JmLnRes {
   float* dscale;
   float* dbias;
 };
+
+// Epilogue / output description of an NT GEMM launch (gemm.hip, bindings.cpp).
+struct GemmEpi {
+  const float* bias;     // [N] fp32 or null
+  uint16_t* out;         // bf16 [M, ldo]
+  long ldo;
+  uint16_t* out2;        // EPI_GELU: gelu(out) bf16 [M, ldo]
+  const uint16_t* aux;   // EPI_DGELU: pre-activation h bf16 [M, ldo]
+  float* colpart;        // EPI_DGELU: per-row-tile column sums of out, [ceil(M/256) (+ 8 * tail tiles)][N] fp32
+  float* part;           // EPI_PARTIAL: [splits][M][N] fp32 split-K partial products
+  int splits;            // K splits (1 = none)
+  // tail split (jm_gemm_nt_tail_plan): the last, partly filled wave of output tiles is computed
+  // split-K into the compact workspace tail[tail_S][tail_r][256][256] and finished by a reduce
+  // kernel that applies the epilogue; t_begin / t_count restrict a launch to a tile range.
+  float* tail;
+  int tail_S;
+  int t_begin;
+  int t_count;
+};

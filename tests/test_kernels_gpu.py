@@ -355,3 +355,31 @@ def test_layernorm_bwd_fused_residual(ext, T0, view_y, with_scale, la):
     if with_scale:
         assert rel(ds1, ds2) < 1e-5
     assert rel(dbi1, dbi2) < 1e-4  # colsums of bf16 values: rounding flips
+
+
+@pytest.mark.parametrize("kind", ["store", "gelu", "gelu_only", "dgelu"])
+@pytest.mark.parametrize("M,N,K", [(4352, 4096, 1024), (4200, 4096, 512)])
+def test_gemm_nt_tail_split(ext, kind, M, N, K):
+    """Last partial wave of tiles computed split-K + finish kernel == the plain launch."""
+    torch.manual_seed(5)
+    A = (torch.rand(M, K, device="cuda") * 2 - 1).bfloat16()
+    W = ((torch.rand(N, K, device="cuda") * 2 - 1) * 0.05).bfloat16()
+    b = torch.randn(N, device="cuda") * 0.1
+    pre = (torch.randn(M, N, device="cuda") * 2).bfloat16()
+    outs = []
+    for tail in (0, 1):
+        ext.gemm_set_tail(tail)
+        if kind == "dgelu":
+            db = torch.zeros(N, device="cuda")
+            outs.append((ext.gemm_nt_dgelu(A, W, pre, db), db))
+        else:
+            outs.append(tuple(ext.gemm_nt(A, W, b, kind != "store", kind == "gelu_only")))
+    ext.gemm_set_tail(0)
+    ref = A.float() @ W.float().t()
+    for o0, o1 in zip(outs[0], outs[1]):
+        assert o0.shape == o1.shape
+        assert rel(o1, o0) < 5e-3
+    if kind == "store":
+        assert rel(outs[1][0], ref + b) < 1e-2
+    if kind == "dgelu":
+        assert rel(outs[1][1], outs[0][1]) < 1e-3

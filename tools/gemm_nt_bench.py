@@ -43,8 +43,10 @@ def main():
     ap.add_argument("--kinds", default="fwd,fwd_gelu,dgrad")
     ap.add_argument("--variant", type=int, default=6, help="kernel variant (see jm_gemm_set_variant)")
     ap.add_argument("--group", type=int, default=8, help="row tiles per column sweep")
+    ap.add_argument("--tail", type=int, default=0, help="tail split of the last partial wave (1 = on)")
     a = ap.parse_args()
     ext = _ext.load()
+    ext.gemm_set_tail(a.tail)
     ext.gemm_set_variant(a.variant, a.group)
     names = [n for n in FWD if not a.only or n in a.only.split(",")]
     tot = {"ours": 0.0, "blas": 0.0}
