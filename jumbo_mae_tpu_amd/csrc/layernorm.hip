@@ -182,7 +182,9 @@ struct LnResIO {
 // with ds_add_f32 instead of living in registers across the row loop (64 fewer VGPRs at D=1024:
 // twice the waves per SIMD for this memory-bound kernel), and the residual-gradient input is
 // loaded together with x / dy so each row costs one HBM round trip instead of two.
-template <int V, typename TI, bool RES, bool LA = false>
+// ER (early residual-gradient load): dres is loaded together with x / dy in the first pass (one
+// HBM round trip per row instead of two) while the parameter partials stay in registers.
+template <int V, typename TI, bool RES, bool LA = false, bool ER = false>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(const TI* __restrict__ dy, const float* __restrict__ x,
                                                      long sB, long sT, int T, int rows, int D,
                                                      const float* __restrict__ mean, const float* __restrict__ rstd,
@@ -227,7 +229,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const TI* __restrict__ dy, 
     const bool rrow = RES && t >= rio.T0;
     const long yoff = RES ? b * rio.yB + (long)(t - rio.T0) * rio.yT : 0;
     float xh[V][4], g[V][4], yv[V][4];
-    float rvp[LA ? V : 1][4];
+    float rvp[(LA || ER) ? V : 1][4];
     const float* rr = io.dres ? io.dres + b * io.rB + t * io.rT : nullptr;
     float sg = 0.f, sgx = 0.f;
 #pragma unroll
@@ -238,7 +240,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const TI* __restrict__ dy, 
         load4(xr + col, xv);
         load4(dyr + col, dv);
         if (RES && rrow && rio.scale) load4(rio.y + yoff + col, yv[i]);
-        if constexpr (LA) {
+        if constexpr (LA || ER) {
           if (rr) load4(rr + col, rvp[i]);
           else rvp[i][0] = rvp[i][1] = rvp[i][2] = rvp[i][3] = 0.f;
         }
@@ -265,7 +267,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const TI* __restrict__ dy, 
       const int col = (i * 64 + lane) * 4;
       if (col < D) {
         float o[4], rv[4] = {0.f, 0.f, 0.f, 0.f};
-        if constexpr (LA) {
+        if constexpr (LA || ER) {
 #pragma unroll
           for (int j = 0; j < 4; ++j) rv[j] = rvp[i][j];
         } else if (rr) {
@@ -367,10 +369,11 @@ void launch_fwd(int V, dim3 grid, hipStream_t st, const float* x, long sB, long 
 #undef JM_LNF
 }
 
-// runtime switch (A/B): LDS-accumulated parameter partials + early dres load.  Off: the ds_add_f32
-// accumulation made the ViT-L step 97.8 -> 122.2 ms despite the doubled occupancy
-// (profiles/r1_ab_ln_bwd_lds_acc.txt)
-int g_ln_bwd_la = 0;
+// runtime switch (A/B): 0 = register partials, dres loaded after the row reduction; 1 = LDS-accumulated
+// parameter partials + early dres load (the ds_add_f32 accumulation made the ViT-L step 97.8 ->
+// 122.2 ms despite the doubled occupancy, profiles/r1_ab_ln_bwd_lds_acc.txt); 2 (default) = register
+// partials + early dres load: 97.96 -> 97.75 ms/step (profiles/r1_ab_ln_bwd_early_dres.txt)
+int g_ln_bwd_la = 2;
 
 template <typename TI, bool RES>
 void launch_bwd(int V, dim3 grid, size_t smem, hipStream_t st, const TI* dy, const float* x, long sB, long sT,
@@ -378,9 +381,12 @@ void launch_bwd(int V, dim3 grid, size_t smem, hipStream_t st, const TI* dy, con
                 float* ws, int acc) {
 #define JM_LNB(VV)                                                                                          \
   case VV:                                                                                                  \
-    if (g_ln_bwd_la && VV >= 2 && VV <= 4)                                                                  \
+    if (g_ln_bwd_la == 1 && VV >= 2 && VV <= 4)                                                             \
       ln_bwd_kernel<VV, TI, RES, true><<<grid, 256, smem, st>>>(dy, x, sB, sT, T, rows, D, m, r, g, dx, rio, ws, \
                                                                  acc);                                     \
+    else if (g_ln_bwd_la == 2 && VV >= 2 && VV <= 4)                                                        \
+      ln_bwd_kernel<VV, TI, RES, false, true><<<grid, 256, smem, st>>>(dy, x, sB, sT, T, rows, D, m, r, g, dx, \
+                                                                        rio, ws, acc);                      \
     else                                                                                                    \
       ln_bwd_kernel<VV, TI, RES><<<grid, 256, smem, st>>>(dy, x, sB, sT, T, rows, D, m, r, g, dx, rio, ws, acc); \
     break;
