@@ -168,3 +168,24 @@ def test_pretrain_driver_two_ranks_grad_accum():
         assert "val/loss" in res and res["val/loss"] > 0
         assert os.path.exists(os.path.join(d, "dd-last.msgpack"))
         assert os.path.exists(os.path.join(d, "dd-best.msgpack"))
+
+
+def test_allreduce_bench_gloo(tmp_path):
+    """tools/allreduce_bench.py (collective bandwidth sweep) runs on 2 gloo ranks and reports
+    all-reduce / reduce-scatter / all-gather bus bandwidth plus the ViT-L exposure model."""
+    import json
+    import subprocess
+    import sys
+
+    out = tmp_path / "sweep.json"
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(root, "tools", "allreduce_bench.py"), "--cpu", "--world", "2",
+                        "--sizes-mb", "0.25,1", "--iters", "2", "--warmup", "1", "--port", str(_free_port()),
+                        "--json", str(out)], capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    res = json.loads(out.read_text())
+    assert res["backend"] == "gloo" and len(res["collective_sweep"]) == 2
+    for row in res["collective_sweep"]:
+        assert row["world"] == 2
+        assert row["allreduce_busbw_GBs"] > 0 and row["reduce_scatter_busbw_GBs"] > 0 and row["all_gather_busbw_GBs"] > 0
+    assert res["model"]["vit_l_grad_allreduce_ms"] > res["model"]["vit_l_jumbo_tail_ms"] > 0

@@ -1,0 +1,154 @@
+"""Collective bandwidth sweep for the data-parallel gradient path.
+
+    torchrun --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 --master-port 29511 \
+        tools/allreduce_bench.py --sizes-mb 1,4,16,64,128,256,512 --dtype fp32
+    python tools/allreduce_bench.py --cpu --world 2          # gloo rehearsal on the host
+
+For each message size it times ``all_reduce`` (and optionally reduce_scatter / all_gather), one
+process per GPU over RCCL (backend ``nccl``), and reports
+
+    algbw = bytes / t            busbw = algbw * 2 (n - 1) / n      (ring all-reduce, nccl-tests)
+
+An 8 x MI355X node is fully connected by xGMI (7 links per GPU, ~153 GB/s each): a single ring is
+per-link bound (~153 GB/s busbw) while RCCL's multi-channel rings can use all 7 links.  The bucket
+size of ``parallel.ddp.GradReducer`` (``--bucket-mb``, default 64) should sit on the plateau of this
+curve; the sweep also reports the modelled exposed time of the ViT-L gradient all-reduce
+(1.62 GB fp32, of which the 302 MB shared jumbo-MLP gradient is the tail that cannot overlap).
+
+Rank 0 prints a table and one JSON line (``{"collective_sweep": [...]}``); times are the max over
+ranks of the per-iteration mean.
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+DTYPES = {"fp32": torch.float32, "bf16": torch.bfloat16}
+VIT_L_GRAD_BYTES = 404_901_632 * 4
+VIT_L_JUMBO_TAIL_BYTES = 75_512_832 * 4
+
+
+def _sync(dev):
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
+
+
+def _time(fn, iters: int, warmup: int, dev) -> float:
+    for _ in range(warmup):
+        fn()
+    _sync(dev)
+    dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        fn()
+    _sync(dev)
+    dt = (time.perf_counter() - t0) / iters
+    t = torch.tensor([dt], dtype=torch.float64, device=dev if dev.type == "cuda" else "cpu")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def sweep(sizes_mb, dtype: torch.dtype, iters: int, warmup: int, ops, dev) -> list[dict]:
+    n = dist.get_world_size()
+    esz = torch.tensor([], dtype=dtype).element_size()
+    rows = []
+    for mb in sizes_mb:
+        numel = max(n, int(mb * 2**20) // esz // n * n)
+        nbytes = numel * esz
+        buf = torch.ones(numel, dtype=dtype, device=dev)
+        res = {"size_mb": round(nbytes / 2**20, 3), "dtype": str(dtype).replace("torch.", ""), "world": n}
+        if "allreduce" in ops:
+            t = _time(lambda: dist.all_reduce(buf), iters, warmup, dev)
+            res["allreduce_ms"] = t * 1e3
+            res["allreduce_algbw_GBs"] = nbytes / t / 1e9
+            res["allreduce_busbw_GBs"] = nbytes / t / 1e9 * 2 * (n - 1) / n
+        if "reduce_scatter" in ops:
+            out = torch.empty(numel // n, dtype=dtype, device=dev)
+            t = _time(lambda: dist.reduce_scatter_tensor(out, buf), iters, warmup, dev)
+            res["reduce_scatter_ms"] = t * 1e3
+            res["reduce_scatter_busbw_GBs"] = nbytes / t / 1e9 * (n - 1) / n
+        if "all_gather" in ops:
+            part = torch.ones(numel // n, dtype=dtype, device=dev)
+            t = _time(lambda: dist.all_gather_into_tensor(buf, part), iters, warmup, dev)
+            res["all_gather_ms"] = t * 1e3
+            res["all_gather_busbw_GBs"] = nbytes / t / 1e9 * (n - 1) / n
+        rows.append(res)
+        del buf
+    return rows
+
+
+def model_exposed(rows: list[dict]) -> dict:
+    """ViT-L gradient all-reduce time at the best measured all-reduce bus bandwidth, and the part
+    that the backward pass cannot hide (the shared jumbo-MLP gradient, final after layer 0)."""
+    ar = [r for r in rows if "allreduce_busbw_GBs" in r]
+    if not ar:
+        return {}
+    best = max(ar, key=lambda r: r["allreduce_busbw_GBs"])
+    n = best["world"]
+    bw = best["allreduce_busbw_GBs"] * 1e9 / (2 * (n - 1) / n) if n > 1 else float("inf")
+    return {"best_busbw_GBs": best["allreduce_busbw_GBs"], "best_size_mb": best["size_mb"],
+            "vit_l_grad_allreduce_ms": VIT_L_GRAD_BYTES / bw * 1e3,
+            "vit_l_jumbo_tail_ms": VIT_L_JUMBO_TAIL_BYTES / bw * 1e3}
+
+
+def run(args, rank: int | None = None, world: int | None = None, port: int | None = None):
+    if rank is not None:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                          WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    from jumbo_mae_tpu_amd.parallel import dist as pdist
+
+    info = pdist.init_distributed("cpu" if args.cpu else None)
+    if not dist.is_initialized():  # world 1: a trivial group so the sweep still runs
+        dist.init_process_group("gloo" if info.device.type == "cpu" else "nccl", rank=0, world_size=1,
+                                init_method=f"tcp://127.0.0.1:{args.port}")
+    sizes = [float(s) for s in args.sizes_mb.split(",")]
+    rows = sweep(sizes, DTYPES[args.dtype], args.iters, args.warmup, args.ops.split(","), info.device)
+    if dist.get_rank() == 0:
+        for r in rows:
+            print("  ".join(f"{k}={v:.3f}" if isinstance(v, float) else f"{k}={v}" for k, v in r.items()),
+                  flush=True)
+        out = {"collective_sweep": rows, "model": model_exposed(rows), "backend": dist.get_backend()}
+        print(json.dumps(out), flush=True)
+        if args.json:
+            with open(args.json, "w") as f:
+                json.dump(out, f, indent=1)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--sizes-mb", default="1,4,16,64,128,256")
+    ap.add_argument("--dtype", default="fp32", choices=sorted(DTYPES))
+    ap.add_argument("--ops", default="allreduce,reduce_scatter,all_gather")
+    ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--cpu", action="store_true", help="gloo on the host (rehearsal)")
+    ap.add_argument("--world", type=int, default=0, help="spawn this many local ranks (with --cpu)")
+    ap.add_argument("--port", type=int, default=29517)
+    ap.add_argument("--json", default="")
+    args = ap.parse_args(argv)
+    if args.world > 1:
+        if not args.cpu:
+            raise SystemExit("--world spawns host ranks: use torchrun for GPU ranks")
+        mp.spawn(_spawn_entry, args=(args, args.world, args.port), nprocs=args.world, join=True)
+        return
+    run(args)
+
+
+def _spawn_entry(rank, args, world, port):
+    run(args, rank, world, port)
+
+
+if __name__ == "__main__":
+    main()
