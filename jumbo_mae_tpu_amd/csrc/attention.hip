@@ -59,6 +59,7 @@ JM_DEVICE f32x4_t mfma(bf16x8_t a, bf16x8_t b, f32x4_t c) {
 template <int HD, int SP, bool TR>
 __global__ __launch_bounds__(256) void attn_fwd_kernel(const uint16_t* __restrict__ qkv, uint16_t* __restrict__ o,
                                                        float* __restrict__ lse, int S, int H, float scale) {
+  JM_DGUARD(S >= 1 && S <= SP && blockDim.x == 256);
   constexpr int KS = HD + 8;  // K row stride (elements), 16-B aligned, breaks bank aliasing
   constexpr int VS = SP + 8;  // V^T row stride
   constexpr int NT = SP / 16;
@@ -191,6 +192,7 @@ template <int HD, int SP>
 __global__ __launch_bounds__(256) void attn_fwd_ml_kernel(const uint16_t* __restrict__ qkv, uint16_t* __restrict__ o,
                                                           float* __restrict__ lse, int S, int H, int BH, int hpw,
                                                           float scale) {
+  JM_DGUARD(S >= 1 && S <= SP && hpw >= 1 && blockDim.x == 256);
   constexpr int KS = HD + 8;
   constexpr int NT = SP / 16;
   constexpr int KK = HD / 32;
@@ -337,6 +339,7 @@ __global__ __launch_bounds__((64 * bwd_waves<HD, SP>())) void attn_bwd_kernel(co
                                                        const float* __restrict__ lse,
                                                        uint16_t* __restrict__ dqkv, int S, int H, float scale,
                                                        float* __restrict__ dbp) {
+  JM_DGUARD(S >= 1 && S <= SP);
   // dbp (optional): per-sample partial column sums of dqkv, [B][3*H*HD] fp32 -- the QKV Dense
   // bias gradient fused in (summed over b by jm_splitk_reduce_add), taken from the fp32 MFMA
   // accumulators so dqkv is never re-read.
@@ -610,6 +613,7 @@ __global__ __launch_bounds__(256) void attn_bwd2_kernel(const uint16_t* __restri
                                                         const float* __restrict__ lse,
                                                         uint16_t* __restrict__ dqkv, int S, int H, float scale,
                                                         float* __restrict__ dbp) {
+  JM_DGUARD(S >= 1 && S <= SP && blockDim.x == 256);
   constexpr int NW = 4, NTH = 256, QC = 64;
   constexpr int NT = SP / 16, KK = HD / 32, DT = HD / 16;
   constexpr int NKW = (NT + NW - 1) / NW;
@@ -883,6 +887,7 @@ __global__ __launch_bounds__(256) void attn_bwd3_kernel(const uint16_t* __restri
                                                         const float* __restrict__ lse,
                                                         uint16_t* __restrict__ dqkv, int S, int H, float scale,
                                                         float* __restrict__ dbp) {
+  JM_DGUARD(S >= 1 && S <= SP && blockDim.x == 256);
   constexpr int NW = 4, NTH = 256, QC = 64;
   constexpr int NT = SP / 16, KK = HD / 32, DT = HD / 16;
   constexpr int NKW = (NT + NW - 1) / NW;
@@ -1273,3 +1278,5 @@ int jm_attn_bwd(const uint16_t* qkv, const uint16_t* o, const uint16_t* dO, cons
   if (hd == 64) return dispatch_sp<64>(false, qkv, o, dO, lse, dqkv, dbias_part, B, S, H, scale, st);
   return -1;
 }
+
+JM_DEBUG_EXPORT(attention)

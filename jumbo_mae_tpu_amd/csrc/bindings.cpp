@@ -17,6 +17,16 @@ int jm_layernorm_bwd(const void* dy, int dy_bf16, const float* x, long sB, long 
                      const JmLnRes* res, hipStream_t st);
 int jm_layernorm_bwd_blocks(int rows);
 void jm_ln_set_bwd_la(int v);
+// debug build (-DJM_DEBUG): first failing soft-check line per kernel translation unit (0 = none;
+// reading clears it); always 0 in the release build
+int jm_debug_line_attention();
+int jm_debug_line_elementwise();
+int jm_debug_line_gemm();
+int jm_debug_line_gemm_tn();
+int jm_debug_line_layernorm();
+int jm_debug_line_mae();
+int jm_debug_line_optim();
+void jm_debug_selftest(int v, hipStream_t st);
 int jm_residual_ln_fwd(const float* x, long sB, long sT, const uint16_t* y, const float* scale, const float* mask,
                        float* x1, long oB, long oT, uint16_t* h, float* mean, float* rstd, int B, int T, int T0,
                        int D, const float* gamma, const float* beta, float eps, hipStream_t st);
@@ -717,7 +727,23 @@ std::vector<torch::Tensor> residual_ln_fwd(torch::Tensor x, torch::Tensor y, c10
   return {x1, h, mean, rstd};
 }
 
-PYBIND11_MODULE(_C, m) {
+py::dict debug_lines() {
+  py::dict d;
+  const std::pair<const char*, int (*)()> tus[] = {
+      {"attention", jm_debug_line_attention}, {"elementwise", jm_debug_line_elementwise},
+      {"gemm", jm_debug_line_gemm},           {"gemm_tn", jm_debug_line_gemm_tn},
+      {"layernorm", jm_debug_line_layernorm}, {"mae", jm_debug_line_mae},
+      {"optim", jm_debug_line_optim}};
+  for (const auto& t : tus) {
+    const int line = t.second();
+    if (line) d[t.first] = line;
+  }
+  return d;
+}
+
+void debug_selftest(int v) { jm_debug_selftest(v, stream()); }
+
+PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "jumbo_mae_tpu_amd CDNA4 (gfx950) HIP kernels";
   m.def("layernorm_fwd", &layernorm_fwd);
   m.def("layernorm_bwd", &layernorm_bwd, py::arg("dy"), py::arg("x"), py::arg("mean"), py::arg("rstd"),
@@ -765,4 +791,11 @@ PYBIND11_MODULE(_C, m) {
   m.def("patch_mse_fwd", &patch_mse_fwd);
   m.def("mix_patches", &mix_patches);
   m.def("patch_mse_bwd", &patch_mse_bwd);
+  m.def("debug_lines", &debug_lines);
+  m.def("debug_selftest", &debug_selftest);
+#ifdef JM_DEBUG
+  m.attr("debug_build") = true;
+#else
+  m.attr("debug_build") = false;
+#endif
 }

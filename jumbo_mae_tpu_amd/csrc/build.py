@@ -6,7 +6,18 @@ C++ compiled with g++; the shared object is linked with hipcc against libtorch. 
 cached by content hash so rebuilds only touch changed files.  Works without a GPU (cross
 compile), which is what ``__graft_entry__.build()`` relies on.
 
-Usage: ``python -m jumbo_mae_tpu_amd.csrc.build [--clean] [-j N]``
+Variants (``--variant``):
+  release  ``_C``        the production build;
+  debug    ``_C_debug``  every kernel with ``-DJM_DEBUG``: soft device checks (launch invariants
+                         at kernel entry, index ranges of the MAE gathers) recorded per translation
+                         unit and read back with ``debug_lines()``; selected at
+                         run time with ``JMAE_EXT=debug``;
+  asan     ``_C_asan``   host code (bindings + the host side of every kernel TU) built with
+                         AddressSanitizer (``-Xarch_host -fsanitize=address``; bindings also UBSan; device code is
+                         unchanged -- GPU ASan is not available on this pool); run python with
+                         ``LD_PRELOAD=$(gcc -print-file-name=libasan.so)`` and ``JMAE_EXT=asan``.
+
+Usage: ``python -m jumbo_mae_tpu_amd.csrc.build [--clean] [-j N] [--variant release|debug|asan]``
 """
 
 from __future__ import annotations
@@ -54,11 +65,14 @@ def _run(cmd):
     return r
 
 
-def so_path() -> Path:
-    return PKG / ("_C" + sysconfig.get_config_var("EXT_SUFFIX"))
+VARIANTS = {"release": "_C", "debug": "_C_debug", "asan": "_C_asan"}
 
 
-def build(jobs: int = 8, verbose: bool = True, clean: bool = False) -> Path:
+def so_path(variant: str = "release") -> Path:
+    return PKG / (VARIANTS[variant] + sysconfig.get_config_var("EXT_SUFFIX"))
+
+
+def build(jobs: int = 8, verbose: bool = True, clean: bool = False, variant: str = "release") -> Path:
     if clean and BUILD.exists():
         shutil.rmtree(BUILD)
     BUILD.mkdir(parents=True, exist_ok=True)
@@ -66,10 +80,22 @@ def build(jobs: int = 8, verbose: bool = True, clean: bool = False) -> Path:
     hdrs = sorted(HERE.glob("*.h"))
     kflags = ["--offload-arch=" + ARCH, "-O3", "-fPIC", "-std=c++17", "-I" + str(HERE),
               "-munsafe-fp-atomics", "-Wno-unused-result"]
+    name = VARIANTS[variant]
     cflags = ["-O2", "-fPIC", "-std=c++17", "-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1",
-              f"-D_GLIBCXX_USE_CXX11_ABI={abi}", "-DTORCH_EXTENSION_NAME=_C", "-DTORCH_API_INCLUDE_EXTENSION_H",
+              f"-D_GLIBCXX_USE_CXX11_ABI={abi}", f"-DTORCH_EXTENSION_NAME={name}", "-DTORCH_API_INCLUDE_EXTENSION_H",
               "-I" + os.path.join(ROCM, "include"), "-I" + sysconfig.get_paths()["include"]] + \
         ["-I" + p for p in incs] + ["-Wno-deprecated-declarations"]
+    lflags = []
+    if variant == "debug":
+        kflags.append("-DJM_DEBUG=1")
+        cflags.append("-DJM_DEBUG=1")
+    elif variant == "asan":
+        # ASan on the host side of every TU (clang, -Xarch_host) and ASan + UBSan on the g++-built
+        # bindings; the runtimes are gcc's (preloaded libasan, linked libubsan)
+        kflags += ["-Xarch_host", "-fsanitize=address", "-fno-omit-frame-pointer"]
+        cflags += ["-fsanitize=address", "-fsanitize=undefined", "-fno-omit-frame-pointer", "-g"]
+        ubsan = subprocess.run(["gcc", "-print-file-name=libubsan.so"], capture_output=True, text=True).stdout.strip()
+        lflags += [ubsan]
 
     jobs_list = []
     for k in KERNELS:
@@ -94,17 +120,17 @@ def build(jobs: int = 8, verbose: bool = True, clean: bool = False) -> Path:
             if verbose:
                 print(f"[jm-build]   built {futs[f].name}", flush=True)
     objs = [str(o) for o, _ in jobs_list]
-    out = so_path()
-    link_dig = _digest([Path(o) for o in objs], ["link"])
-    stamp = BUILD / f"link.{link_dig}.stamp"
+    out = so_path(variant)
+    link_dig = _digest([Path(o) for o in objs], ["link", variant] + lflags)
+    stamp = BUILD / f"link.{variant}.{link_dig}.stamp"
     if not (out.exists() and stamp.exists()):
         tmp = str(out) + ".tmp"
-        _run([HIPCC, "-shared", "-fPIC", "--offload-arch=" + ARCH, "-o", tmp] + objs +
+        _run([HIPCC, "-shared", "-fPIC", "--offload-arch=" + ARCH, "-o", tmp] + lflags + objs +
              ["-L" + torch_lib, "-Wl,-rpath," + torch_lib, "-lc10", "-ltorch", "-ltorch_cpu", "-ltorch_python",
               "-lc10_hip", "-ltorch_hip"])
         os.replace(tmp, out)
-        for s in BUILD.glob("link.*.stamp"):
-            s.unlink()
+        for old in BUILD.glob(f"link.{variant}.*.stamp"):
+            old.unlink()
         stamp.touch()
         if verbose:
             print(f"[jm-build] linked {out}", flush=True)
@@ -115,8 +141,9 @@ def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--clean", action="store_true")
     ap.add_argument("-j", type=int, default=8)
+    ap.add_argument("--variant", default="release", choices=sorted(VARIANTS))
     a = ap.parse_args(argv)
-    p = build(a.j, True, a.clean)
+    p = build(a.j, True, a.clean, a.variant)
     print(p)
 
 

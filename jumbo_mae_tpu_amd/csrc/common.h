@@ -138,6 +138,46 @@ JM_DEVICE void store4(uint16_t* p, const float* f) {
   *reinterpret_cast<uint2*>(p) = v;
 }
 
+// ------------------------------------------------------------------ debug build
+// build.py --debug compiles every kernel with -DJM_DEBUG into _C_debug.so.  Device checks there are
+// SOFT: a failing check records its source line in a per-translation-unit device word (first
+// failure wins) instead of trapping -- a trapping wave can take the whole GPU down -- and the host
+// reads and clears the words through debug_lines().  JM_DGUARD additionally returns from the kernel;
+// use it only at kernel entry on workgroup-uniform launch invariants (before any barrier), where a
+// violated assumption would otherwise turn into out-of-bounds accesses.
+#ifdef JM_DEBUG
+static __device__ int jm_dbg_line;
+JM_DEVICE void jm_dbg_fail(int line) { atomicCAS(&jm_dbg_line, 0, line); }
+#define JM_DASSERT(c)                     \
+  do {                                    \
+    if (!(c)) jm_dbg_fail(__LINE__);      \
+  } while (0)
+#define JM_DGUARD(c)                      \
+  do {                                    \
+    if (!(c)) {                           \
+      jm_dbg_fail(__LINE__);              \
+      return;                             \
+    }                                     \
+  } while (0)
+#define JM_DEBUG_EXPORT(tu)                                                         \
+  int jm_debug_line_##tu() {                                                        \
+    int v = 0, z = 0;                                                               \
+    (void)hipDeviceSynchronize();                                                   \
+    (void)hipMemcpyFromSymbol(&v, HIP_SYMBOL(jm_dbg_line), sizeof(int));            \
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(jm_dbg_line), &z, sizeof(int));              \
+    return v;                                                                       \
+  }
+#else
+#define JM_DASSERT(c) \
+  do {                \
+  } while (0)
+#define JM_DGUARD(c) \
+  do {               \
+  } while (0)
+#define JM_DEBUG_EXPORT(tu) \
+  int jm_debug_line_##tu() { return 0; }
+#endif
+
 #define JM_CHECK(x)                                                                  \
   do {                                                                               \
     hipError_t e_ = (x);                                                             \

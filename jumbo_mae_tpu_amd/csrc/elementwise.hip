@@ -389,3 +389,12 @@ int jm_splitk_reduce_bf16(const float* part, int S, long n, int N, const float* 
   splitk_reduce_bf16_kernel<<<(int)blocks, 256, 0, st>>>(part, S, n / 8, N, bias, out);
   return 0;
 }
+
+JM_DEBUG_EXPORT(elementwise)
+
+// debug-build self test: the check fails when v != 0 (exercises the soft-assert path end to end)
+namespace {
+__global__ __launch_bounds__(64) void debug_selftest_kernel(int v) { JM_DASSERT(v == 0); }
+}  // namespace
+
+void jm_debug_selftest(int v, hipStream_t st) { debug_selftest_kernel<<<1, 64, 0, st>>>(v); }

@@ -258,6 +258,7 @@ template <int EPI, int WN, int ABL = 0>
 __global__ __launch_bounds__(128 * WN, 1) void gemm_nt_kernel(const uint16_t* __restrict__ A, long lda,
                                                               const uint16_t* __restrict__ B, long ldb, int M,
                                                               int N, int K, GemmEpi ep, int GROUP_M) {
+  JM_DGUARD(blockDim.x == 128 * WN && K % 64 == 0 && M > 0 && N > 0);
   constexpr int NW = 2 * WN;          // waves
   constexpr int NTW = BN / WN / 16;   // 16-wide column tiles per wave
   constexpr int RND = 16 / NW;        // glds rounds per operand and stage
@@ -587,6 +588,7 @@ template <int EPI, int SCHED = 0>
 __global__ __launch_bounds__(512, 1) void gemm_nt64_kernel(const uint16_t* __restrict__ A, long lda,
                                                            const uint16_t* __restrict__ B, long ldb, int M, int N,
                                                            int K, GemmEpi ep, int GROUP_M) {
+  JM_DGUARD(blockDim.x == 512 && K % 64 == 0 && M > 0 && N > 0);
   extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
   constexpr bool ST = SCHED & 1, PR = (SCHED & 2) != 0;
   if ((SCHED & 3) != 0 && __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) >= 4)
@@ -611,6 +613,7 @@ template <int EPI, bool STAGGER>
 __global__ __launch_bounds__(256, 2) void gemm_nth_kernel(const uint16_t* __restrict__ A, long lda,
                                                           const uint16_t* __restrict__ B, long ldb, int M, int N,
                                                           int K, GemmEpi ep, int GROUP_M) {
+  JM_DGUARD(blockDim.x == 256 && K % 64 == 0 && M > 0 && N > 0);
   constexpr int NW = 4, NTW = 4;
   constexpr int RNDA = BM / 16 / NW, RNDB = BNH / 16 / NW;  // glds pieces (16 rows x 64 B) per wave
   constexpr int PER_STAGE = RNDA + RNDB;                      // vmcnt units per stage
@@ -1245,3 +1248,5 @@ int jm_gemm_nt(const uint16_t* A, long lda, const uint16_t* B, long ldb, int M, 
     return -3;
   return 0;
 }
+
+JM_DEBUG_EXPORT(gemm)

@@ -90,6 +90,7 @@ __global__ __launch_bounds__(NTH, 1) void gemm_tn_kernel(const uint16_t* __restr
                                                          const uint16_t* __restrict__ B, long ldb, int M, int N,
                                                          int K, int steps_per_split, float* __restrict__ out,
                                                          long ldo, long split_stride, TnSegs segs = {}) {
+  JM_DGUARD(blockDim.x == NTH && steps_per_split >= 1 && M > 0);
   extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
@@ -333,3 +334,5 @@ int jm_gemm_tn_seg(const TnSegs& segs, long lda, long ldb, int N, int K, int sps
   }
   return 0;
 }
+
+JM_DEBUG_EXPORT(gemm_tn)

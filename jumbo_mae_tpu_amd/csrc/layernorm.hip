@@ -190,6 +190,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const TI* __restrict__ dy, 
                                                      const float* __restrict__ mean, const float* __restrict__ rstd,
                                                      const float* __restrict__ gamma, LnBwdIO io, LnResIO rio,
                                                      float* __restrict__ ws, int accum_params) {
+  JM_DGUARD(blockDim.x == 256 && D % 4 == 0 && D <= V * 256);
   constexpr int NP = RES ? 4 : 2;
   constexpr int NA = LA ? 1 : NP;  // register accumulators kept (dummy when LA)
   extern __shared__ __attribute__((aligned(16))) float red[];  // [NP*D]
@@ -487,3 +488,5 @@ int jm_layernorm_bwd(const void* dy, int dy_bf16, const float* x, long sB, long 
   }
   return 0;
 }
+
+JM_DEBUG_EXPORT(layernorm)

@@ -78,6 +78,7 @@ __global__ __launch_bounds__(256) void gather_patches_kernel(const uint8_t* __re
   const int o = (int)(i - row * q) * 4;
   const int b = (int)(row / K), k = (int)(row - (long)b * K);
   const int n = ids[b * idsB + k];
+  JM_DASSERT(n >= 0 && n < (H / p) * g);
   const int gy = n / g, gx = n - (n / g) * g;
   float f[4];
 #pragma unroll
@@ -128,6 +129,7 @@ __global__ __launch_bounds__(256) void unshuffle_fwd_kernel(const uint16_t* __re
   } else {
     const int n = t - C;
     const int j = restore[b * rsB + n];
+    JM_DASSERT(j >= 0 && j < N);
     if (j < K) load4(y + ((long)b * (C + K) + C + j) * d + col, f);
     else load4(tok + col, f);
     float pp[4];
@@ -425,3 +427,5 @@ int jm_mix_patches(const uint8_t* img, const int* perm, const float* prm, const 
   mix_patches_kernel<<<cdiv(n, 256), 256, 0, st>>>(img, perm, prm, box, out, B, H, W, p);
   return 0;
 }
+
+JM_DEBUG_EXPORT(mae)

@@ -219,3 +219,5 @@ void jm_opt_sgd(float* p, const float* g, float* trace, uint16_t* shadow, const 
                 const float* meta, const float* hyper, const float* gnorm_sq, float momentum, hipStream_t st) {
   sgd_kernel<<<nchunks, 256, 0, st>>>(p, g, trace, shadow, (const Chunk*)chunks, meta, hyper, gnorm_sq, momentum);
 }
+
+JM_DEBUG_EXPORT(optim)
