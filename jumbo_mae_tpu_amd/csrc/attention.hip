@@ -612,8 +612,8 @@ __global__ __launch_bounds__(256) void attn_bwd2_kernel(const uint16_t* __restri
                                                         const uint16_t* __restrict__ dO,
                                                         const float* __restrict__ lse,
                                                         uint16_t* __restrict__ dqkv, int S, int H, float scale,
-                                                        float* __restrict__ dbp) {
-  JM_DGUARD(S >= 1 && S <= SP && blockDim.x == 256);
+                                                        float* __restrict__ dbp, int B, int ppw) {
+  JM_DGUARD(S >= 1 && S <= SP && blockDim.x == 256 && ppw >= 1);
   constexpr int NW = 4, NTH = 256, QC = 64;
   constexpr int NT = SP / 16, KK = HD / 32, DT = HD / 16;
   constexpr int NKW = (NT + NW - 1) / NW;
@@ -627,10 +627,48 @@ __global__ __launch_bounds__(256) void attn_bwd2_kernel(const uint16_t* __restri
   float* delta_s = lse_s + SP;
   float* bsum = delta_s + SP;
 
-  const int bh = blockIdx.x;
-  const int b = bh / H, h = bh - (bh / H) * H;
+  // one workgroup walks ``ppw`` batch elements of ONE head (blockIdx = bg * H + h): the QKV bias
+  // gradient partials stay in registers across them and are reduced across lanes once
+  const int h = blockIdx.x % H, bg = blockIdx.x / H;
   const long ts = 3L * H * HD;
   const long os = (long)H * HD;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int l16 = lane & 15, g = lane >> 4;
+  const float sl2 = scale * LOG2E;
+  // Every swizzled address below is (16-row-aligned base) + (per-lane constant): aswz depends on
+  // row bits 1-3 only, and all bases are multiples of 16 rows.
+  int o_frag[KK];  // fragment row l16, chunk 4kk + g
+#pragma unroll
+  for (int kk = 0; kk < KK; ++kk) o_frag[kk] = swo<NCH>(l16, 32 * kk + 8 * g);
+  int o_tr[DT][2];  // transposing reads of rows 4g + l16/4 (+16), columns dt*16 + 4 (l16 & 3)
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt) {
+    o_tr[dt][0] = swo<NCH>(4 * g + (l16 >> 2), dt * 16 + 4 * (l16 & 3));
+    o_tr[dt][1] = swo<NCH>(4 * g + (l16 >> 2) + 16, dt * 16 + 4 * (l16 & 3));
+  }
+  int o_dsw[QC / 16];  // dS^T store: row l16, queries 16 j + 4 g .. + 3
+#pragma unroll
+  for (int j = 0; j < QC / 16; ++j) o_dsw[j] = swo<8>(l16, 16 * j + 4 * g);
+  const int krow = 8 * g + (l16 >> 2);  // dQ transposing reads: rows 32 s + krow (+4)
+  int o_dsr[2], o_kt[DT][2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    o_dsr[u] = swo<8>(krow + 4 * u, wave * 16 + 4 * (l16 & 3));
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) o_kt[dt][u] = swo<NCH>(krow + 4 * u, dt * 16 + 4 * (l16 & 3));
+  }
+  // per-lane bias-gradient partials (columns dt * 16 + 4 g + i), summed over this lane's rows
+  float qb[DT][4], kb[DT][4], vb[DT][4];
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) qb[dt][i] = kb[dt][i] = vb[dt][i] = 0.f;
+  if (dbp != nullptr)
+    for (int i = threadIdx.x; i < 3 * HD; i += NTH) bsum[i] = 0.f;
+
+  for (int pj = 0; pj < ppw; ++pj) {
+  const int b = bg * ppw + pj;
+  if (b >= B) break;  // workgroup-uniform
   const uint16_t* base = qkv + (long)b * S * ts;
   const uint16_t* Qg = base + h * HD;
   const uint16_t* Kg = base + (H + h) * HD;
@@ -640,9 +678,6 @@ __global__ __launch_bounds__(256) void attn_bwd2_kernel(const uint16_t* __restri
   uint16_t* dQg = dqkv + (long)b * S * ts + h * HD;
   uint16_t* dKg = dqkv + (long)b * S * ts + (H + h) * HD;
   uint16_t* dVg = dqkv + (long)b * S * ts + (2 * H + h) * HD;
-
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int l16 = lane & 15, g = lane >> 4;
 
   // V fragments of this wave's key tiles straight from global (B operand of dP = dO V^T)
   bf16x8_t vf[NKW][KK];
@@ -656,7 +691,6 @@ __global__ __launch_bounds__(256) void attn_bwd2_kernel(const uint16_t* __restri
       if (key < S) vf[w][kk] = ld8(Vg + (long)key * ts + 32 * kk + 8 * g);
     }
   }
-  for (int i = threadIdx.x; i < 3 * HD; i += NTH) bsum[i] = 0.f;
   for (int i = threadIdx.x; i < SP; i += NTH) {
     delta_s[i] = 0.f;
     lse_s[i] = i < S ? lse[((long)b * H + h) * S + i] * LOG2E : INFINITY;
@@ -700,30 +734,6 @@ __global__ __launch_bounds__(256) void attn_bwd2_kernel(const uint16_t* __restri
     }
   }
   __syncthreads();
-
-  const float sl2 = scale * LOG2E;
-  // Every swizzled address below is (16-row-aligned base) + (per-lane constant): aswz depends on
-  // row bits 1-3 only, and all bases are multiples of 16 rows.
-  int o_frag[KK];  // fragment row l16, chunk 4kk + g
-#pragma unroll
-  for (int kk = 0; kk < KK; ++kk) o_frag[kk] = swo<NCH>(l16, 32 * kk + 8 * g);
-  int o_tr[DT][2];  // transposing reads of rows 4g + l16/4 (+16), columns dt*16 + 4 (l16 & 3)
-#pragma unroll
-  for (int dt = 0; dt < DT; ++dt) {
-    o_tr[dt][0] = swo<NCH>(4 * g + (l16 >> 2), dt * 16 + 4 * (l16 & 3));
-    o_tr[dt][1] = swo<NCH>(4 * g + (l16 >> 2) + 16, dt * 16 + 4 * (l16 & 3));
-  }
-  int o_dsw[QC / 16];  // dS^T store: row l16, queries 16 j + 4 g .. + 3
-#pragma unroll
-  for (int j = 0; j < QC / 16; ++j) o_dsw[j] = swo<8>(l16, 16 * j + 4 * g);
-  const int krow = 8 * g + (l16 >> 2);  // dQ transposing reads: rows 32 s + krow (+4)
-  int o_dsr[2], o_kt[DT][2];
-#pragma unroll
-  for (int u = 0; u < 2; ++u) {
-    o_dsr[u] = swo<8>(krow + 4 * u, wave * 16 + 4 * (l16 & 3));
-#pragma unroll
-    for (int dt = 0; dt < DT; ++dt) o_kt[dt][u] = swo<NCH>(krow + 4 * u, dt * 16 + 4 * (l16 & 3));
-  }
 
   bf16x8_t kf[NKW][KK];
   f32x4_t dvacc[NKW][DT], dkacc[NKW][DT];
@@ -808,15 +818,10 @@ __global__ __launch_bounds__(256) void attn_bwd2_kernel(const uint16_t* __restri
             dq[dt] = mfma(ka, bop, dq[dt]);
           }
         }
-        if (dbp != nullptr) {
 #pragma unroll
-          for (int dt = 0; dt < DT; ++dt)
+        for (int dt = 0; dt < DT; ++dt)
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
-              const float v = row16_sum(dq[dt][i]);
-              if (l16 == 0) atomicAdd(&bsum[dt * 16 + 4 * g + i], v * scale);
-            }
-        }
+          for (int i = 0; i < 4; ++i) qb[dt][i] += dq[dt][i];
         const int q = qt * 16 + l16;
         if (q < S) {
 #pragma unroll
@@ -844,27 +849,31 @@ __global__ __launch_bounds__(256) void attn_bwd2_kernel(const uint16_t* __restri
       }
     }
   }
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int w = 0; w < NKW; ++w) {
+        kb[dt][i] += dkacc[w][dt][i];
+        vb[dt][i] += dvacc[w][dt][i];
+      }
+  }  // batch elements
   if (dbp != nullptr) {
 #pragma unroll
     for (int dt = 0; dt < DT; ++dt)
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        float sk = 0.f, sv = 0.f;
-#pragma unroll
-        for (int w = 0; w < NKW; ++w) {
-          sk += dkacc[w][dt][i];
-          sv += dvacc[w][dt][i];
-        }
-        sk = row16_sum(sk);
-        sv = row16_sum(sv);
+        const float sq = row16_sum(qb[dt][i]), sk = row16_sum(kb[dt][i]), sv = row16_sum(vb[dt][i]);
         if (l16 == 0) {
           const int d = dt * 16 + 4 * g + i;
+          atomicAdd(&bsum[d], sq * scale);
           atomicAdd(&bsum[HD + d], sk * scale);
           atomicAdd(&bsum[2 * HD + d], sv);
         }
       }
     __syncthreads();
-    float* dst = dbp + (long)b * ts + h * HD;
+    float* dst = dbp + (long)bg * ts + h * HD;
     for (int i = threadIdx.x; i < 3 * HD; i += NTH) dst[(i / HD) * H * HD + (i % HD)] = bsum[i];
   }
 }
@@ -1189,6 +1198,15 @@ int run_t(bool fwd, const uint16_t* qkv, const uint16_t* o, const uint16_t* dO, 
   return 0;
 }
 
+// runtime switch: batch elements per bwd2 workgroup (one head each); 0 = auto (bwd_ppw)
+int g_bwd_ppw = 0;
+
+template <int HD, int SP>
+int bwd_ppw() {
+  if (g_bwd_ppw > 0) return g_bwd_ppw;
+  return 8;  // ViT-L encoder (S 52): 160 -> 140 us, finetune (S 199): 273 -> 256 us (profiles/r1_attn_bwd_ppw.txt)
+}
+
 template <int HD, int SP>
 int run_bwd2(const uint16_t* qkv, const uint16_t* o, const uint16_t* dO, const float* lse_in, uint16_t* out,
              float* dbias_part, int B, int S, int H, float scale, hipStream_t st) {
@@ -1212,7 +1230,11 @@ int run_bwd2(const uint16_t* qkv, const uint16_t* o, const uint16_t* dO, const f
     return 0;
   }
 bwd2:
-  attn_bwd2_kernel<HD, SP><<<dim3(B * H), 256, sm, st>>>(qkv, o, dO, lse_in, out, S, H, scale, dbias_part);
+  {
+    const int ppw = bwd_ppw<HD, SP>();
+    attn_bwd2_kernel<HD, SP><<<dim3(((B + ppw - 1) / ppw) * H), 256, sm, st>>>(qkv, o, dO, lse_in, out, S, H, scale,
+                                                                              dbias_part, B, ppw);
+  }
   return 0;
 }
 
@@ -1262,6 +1284,20 @@ int dispatch_sp(bool fwd, const uint16_t* qkv, const uint16_t* o, const uint16_t
 int jm_attn_max_seq() { return 224; }
 void jm_attn_set_tr(int v) { g_use_tr = v; }
 void jm_attn_set_fwd_hpw(int v) { g_fwd_hpw = v < 0 ? 0 : v; }
+void jm_attn_set_bwd_ppw(int v) { g_bwd_ppw = v < 0 ? 0 : v; }
+
+// rows of the dbias_part workspace that jm_attn_bwd writes: the bwd2 kernel folds ``ppw`` batch
+// elements into one row, every other backward writes one row per batch element
+int jm_attn_bwd_part_rows(int B, int S, int hd) {
+  const bool bwd2 = g_use_tr >= 2 && !(hd == 32 && g_use_tr == 3);
+  if (!bwd2 || S > 224 || (hd != 32 && hd != 64)) return B;
+  int ppw;
+  if (hd == 64)
+    ppw = S <= 32 ? bwd_ppw<64, 32>() : S <= 64 ? bwd_ppw<64, 64>() : S <= 128 ? bwd_ppw<64, 128>() : bwd_ppw<64, 224>();
+  else
+    ppw = S <= 32 ? bwd_ppw<32, 32>() : S <= 64 ? bwd_ppw<32, 64>() : S <= 128 ? bwd_ppw<32, 128>() : bwd_ppw<32, 224>();
+  return (B + ppw - 1) / ppw;
+}
 
 int jm_attn_fwd(const uint16_t* qkv, uint16_t* o, float* lse, int B, int S, int H, int hd, hipStream_t st) {
   const float scale = 1.f / sqrtf((float)hd);

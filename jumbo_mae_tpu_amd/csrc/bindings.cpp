@@ -45,6 +45,8 @@ int jm_attn_bwd(const uint16_t* qkv, const uint16_t* o, const uint16_t* dO, cons
 int jm_attn_max_seq();
 void jm_attn_set_tr(int v);
 void jm_attn_set_fwd_hpw(int v);
+void jm_attn_set_bwd_ppw(int v);
+int jm_attn_bwd_part_rows(int B, int S, int hd);
 void jm_opt_sumsq(const float* x, const int* chunks, int nchunks, float* out, hipStream_t st);
 void jm_opt_adamw(float* p, const float* g, float* mu, float* nu, uint16_t* shadow, const int* chunks, int nchunks,
                   const float* meta, const float* hyper, const float* gnorm_sq, hipStream_t st);
@@ -329,15 +331,16 @@ torch::Tensor attn_bwd(torch::Tensor dO, torch::Tensor qkv, torch::Tensor o, tor
   const int D = D3 / 3, hd = D / heads;
   auto dqkv = torch::empty_like(qkv);
   torch::Tensor part;
+  const int rows = jm_attn_bwd_part_rows(B, S, hd);
   if (dbias) {
     TORCH_CHECK(dbias->is_contiguous() && dbias->scalar_type() == torch::kFloat32 && dbias->numel() == D3,
                 "attn_bwd: dbias must be contiguous fp32 [3D]");
-    part = torch::empty({B, D3}, qkv.options().dtype(torch::kFloat32));
+    part = torch::empty({rows, D3}, qkv.options().dtype(torch::kFloat32));
   }
   float* pp = dbias ? part.data_ptr<float>() : nullptr;
   check_rc(jm_attn_bwd(bf(qkv), bf(o), bf(dO), lse.data_ptr<float>(), bfm(dqkv), B, S, heads, hd, pp, stream()),
            "attn_bwd");
-  if (dbias) check_rc(jm_splitk_reduce_add(pp, dbias->data_ptr<float>(), D3, B, stream()), "attn_bwd dbias");
+  if (dbias) check_rc(jm_splitk_reduce_add(pp, dbias->data_ptr<float>(), D3, rows, stream()), "attn_bwd dbias");
   return dqkv;
 }
 
@@ -777,6 +780,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("attn_set_tr", &jm_attn_set_tr);
   m.def("ln_set_bwd_la", &jm_ln_set_bwd_la);
   m.def("attn_set_fwd_hpw", &jm_attn_set_fwd_hpw);
+  m.def("attn_set_bwd_ppw", &jm_attn_set_bwd_ppw);
   m.def("opt_sumsq", &opt_sumsq);
   m.def("opt_adamw", &opt_adamw);
   m.def("opt_lamb_phase1", &opt_lamb_phase1);

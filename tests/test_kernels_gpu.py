@@ -20,6 +20,7 @@ def _reset_gemm_variant(request):
     if "ext" in request.fixturenames:
         request.getfixturevalue("ext").gemm_set_variant(12, 8)
         request.getfixturevalue("ext").ln_set_bwd_la(2)
+        request.getfixturevalue("ext").attn_set_bwd_ppw(0)
 
 
 def rel(a, b):
@@ -114,14 +115,16 @@ def _attn_ref(qkv, H):
     return o, lse
 
 
-@pytest.mark.parametrize("tr,hpw", [(3, 0), (3, 1), (2, 1), (1, 1), (0, 1), (3, 3), (3, 4)])
+@pytest.mark.parametrize("tr,hpw,ppw", [(3, 0, 0), (3, 1, 0), (2, 1, 0), (1, 1, 0), (0, 1, 0), (3, 3, 0), (3, 4, 0),
+                                        (3, 0, 1), (3, 0, 2), (2, 0, 3), (3, 0, 8)])
 @pytest.mark.parametrize("B,S,H,hd", [(3, 52, 16, 64), (2, 199, 16, 32), (2, 17, 4, 32), (2, 100, 3, 64),
                                       (2, 199, 4, 64)])
-def test_attention(ext, B, S, H, hd, tr, hpw):
+def test_attention(ext, B, S, H, hd, tr, hpw, ppw):
     if not tr and S > 128:
         pytest.skip("transposed-image variant exceeds LDS at this size (TR variant covers it)")
     ext.attn_set_tr(tr)
     ext.attn_set_fwd_hpw(hpw)
+    ext.attn_set_bwd_ppw(ppw)
     torch.manual_seed(0)
     D = H * hd
     qkv = (torch.randn(B, S, 3 * D, device="cuda") * 1.5).bfloat16()
@@ -145,6 +148,7 @@ def test_attention(ext, B, S, H, hd, tr, hpw):
         assert rel(d[:, :, i], g[:, :, i]) < 2e-2, i
     ext.attn_set_tr(3)
     ext.attn_set_fwd_hpw(0)
+    ext.attn_set_bwd_ppw(0)
 
 
 @pytest.mark.parametrize("S,n", [(4, 4096), (512, 3072), (37, 1024)])

@@ -42,6 +42,9 @@ def apply(P, cfg: str):
         elif k == "ATTN_HPW":
             from jumbo_mae_tpu_amd.ops import _ext
             _ext.load(True).attn_set_fwd_hpw(int(v))
+        elif k == "ATTN_PPW":
+            from jumbo_mae_tpu_amd.ops import _ext
+            _ext.load(True).attn_set_bwd_ppw(int(v))
         elif k == "ATTN_TR":
             from jumbo_mae_tpu_amd.ops import _ext
             _ext.load(True).attn_set_tr(int(v))

@@ -10,7 +10,8 @@ import sys
 
 import torch
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+# JMAE_ROOT: package tree to import (A/B of two builds, tools/run_attn_ab.sh)
+sys.path.insert(0, os.environ.get("JMAE_ROOT") or os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 from jumbo_mae_tpu_amd.ops import _ext  # noqa: E402
 
@@ -23,8 +24,11 @@ def main():
     ap.add_argument("--shapes", default="dec,enc")
     ap.add_argument("--tr", type=int, default=-1, help="kernel variant (ext.attn_set_tr), -1 = default")
     ap.add_argument("--hpw", type=int, default=0, help="forward (b, h) pairs per workgroup, 0 = default")
+    ap.add_argument("--ppw", type=int, default=0, help="backward batch elements per workgroup (bwd2), 0 = default")
     a = ap.parse_args()
     ext = _ext.load()
+    if a.ppw > 0:
+        ext.attn_set_bwd_ppw(a.ppw)
     if a.hpw > 0:
         ext.attn_set_fwd_hpw(a.hpw)
     if a.tr >= 0:

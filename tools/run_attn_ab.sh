@@ -6,7 +6,7 @@ cd $R
 for i in 1 2; do
 for v in old new; do
 if [ $v = old ]; then PP=$R/abtmp/old; else PP=$R; fi
-PYTHONPATH=$PP timeout -k 10 120 python tools/attn_bench.py --shapes dec,enc,ft > gpurun_out/attn_$v$i.txt 2>&1 || { cat gpurun_out/attn_$v$i.txt; exit 1; }
+JMAE_ROOT=$PP timeout -k 10 120 python tools/attn_bench.py --shapes dec,enc,ft > gpurun_out/attn_$v$i.txt 2>&1 || { cat gpurun_out/attn_$v$i.txt; exit 1; }
 echo "== $v $i"; grep -v amdgpu gpurun_out/attn_$v$i.txt
 done
 done
