@@ -72,6 +72,33 @@ def so_path(variant: str = "release") -> Path:
     return PKG / (VARIANTS[variant] + sysconfig.get_config_var("EXT_SUFFIX"))
 
 
+def io_so_path() -> Path:
+    return PKG / ("_io" + sysconfig.get_config_var("EXT_SUFFIX"))
+
+
+def build_io(verbose: bool = True) -> Path:
+    """Host-only pybind11 module ``_io`` (csrc/io/tario.cpp: native tar-shard reader); g++, no HIP."""
+    import pybind11
+
+    src = HERE / "io" / "tario.cpp"
+    flags = ["-O2", "-fPIC", "-shared", "-std=c++17", "-pthread", "-I" + pybind11.get_include(),
+             "-I" + sysconfig.get_paths()["include"], "-fvisibility=hidden"]
+    BUILD.mkdir(parents=True, exist_ok=True)
+    dig = _digest([src], flags)
+    stamp = BUILD / f"io.{dig}.stamp"
+    out = io_so_path()
+    if not (out.exists() and stamp.exists()):
+        tmp = str(out) + ".tmp"
+        _run(["g++"] + flags + [str(src), "-o", tmp])
+        os.replace(tmp, out)
+        for old in BUILD.glob("io.*.stamp"):
+            old.unlink()
+        stamp.touch()
+        if verbose:
+            print(f"[jm-build] linked {out}", flush=True)
+    return out
+
+
 def build(jobs: int = 8, verbose: bool = True, clean: bool = False, variant: str = "release") -> Path:
     if clean and BUILD.exists():
         shutil.rmtree(BUILD)
@@ -144,6 +171,7 @@ def main(argv=None):
     ap.add_argument("--variant", default="release", choices=sorted(VARIANTS))
     a = ap.parse_args(argv)
     p = build(a.j, True, a.clean, a.variant)
+    build_io()
     print(p)
 
 

@@ -99,7 +99,7 @@ class ShardDataset(IterableDataset):
             mine = urls
             sample_filter = (self.rank * nw + wid, total)
         handler = S.ignore_and_continue if self.train else None
-        it = itertools.chain.from_iterable(S.tar_samples(u, handler) for u in mine)
+        it = S.iter_samples(mine, handler)
         if sample_filter is not None:
             it = itertools.islice(it, sample_filter[0], None, sample_filter[1])
         if self.train:

@@ -7,12 +7,17 @@ Implemented here with the stdlib ``tarfile`` in streaming mode: brace-expanded s
 deterministic per-epoch shard shuffles, rank/worker splitting, sample grouping by key
 (``{key}.jpg`` + ``{key}.cls`` -> one sample), a deterministic shuffle buffer, and
 ``pipe:`` URLs (e.g. ``pipe:gsutil cat gs://...``) next to local files.
+
+Local shards are read by the native module ``jumbo_mae_tpu_amd._io`` when it is built
+(csrc/io/tario.cpp: tar parsing and file I/O on a pool of C++ threads with ordered read-ahead, the
+same sample stream as the Python reader); ``JMAE_NATIVE_IO=0`` forces the Python path.
 """
 
 from __future__ import annotations
 
 import io
 import itertools
+import os
 import random
 import re
 import subprocess
@@ -89,6 +94,47 @@ def tar_samples(url: str, handler=None) -> Iterator[dict]:
         if handler is None:
             raise
         handler(e)
+
+
+def _native():
+    if os.environ.get("JMAE_NATIVE_IO", "1") != "1":
+        return None
+    try:
+        from .. import _io
+    except ImportError:
+        return None
+    return _io
+
+
+def _local_path(url: str) -> str | None:
+    if url.startswith("pipe:"):
+        return None
+    return url[7:] if url.startswith("file://") else url
+
+
+def iter_samples(urls: list[str], handler=None, threads: int = 4) -> Iterator[dict]:
+    """Samples of several shards in order: ``chain(tar_samples(u, handler) for u in urls)``.
+
+    With the native reader every local shard is parsed by a C++ thread pool (``threads`` shards in
+    flight, samples handed out in shard order); a shard error is skipped when ``handler`` is given
+    (ignore_and_continue) and raised otherwise, after the samples read before the fault."""
+    nat = _native()
+    paths = [_local_path(u) for u in urls]
+    if nat is None or not urls or any(p is None for p in paths):
+        yield from itertools.chain.from_iterable(tar_samples(u, handler) for u in urls)
+        return
+    url_of = dict(zip(paths, urls))  # report the URL as given (file:// prefix kept)
+    reader = nat.ShardReader(paths, threads=threads, ignore_errors=handler is not None)
+    try:
+        for s in reader:
+            s["__url__"] = url_of.get(s["__url__"], s["__url__"])
+            yield s
+    except RuntimeError as e:
+        if handler is None:
+            raise
+        handler(e)
+    finally:
+        reader.close()
 
 
 def ignore_and_continue(exn) -> bool:
