@@ -10,7 +10,7 @@
 
 // ---- kernel entry points (see *.hip)
 int jm_layernorm_fwd(const float* x, long sB, long sT, int B, int T, int D, const float* gamma, const float* beta,
-                     float eps, void* y, int out_bf16, float* mean, float* rstd, hipStream_t st);
+                     float eps, void* y, int out_bf16, float* mean, float* rstd, hipStream_t st, uint16_t* y2 = nullptr);
 int jm_layernorm_bwd(const void* dy, int dy_bf16, const float* x, long sB, long sT, int B, int T, int D,
                      const float* mean, const float* rstd, const float* gamma, float* dx_ptr, long oB, long oT,
                      const float* dres, long rB, long rT, float* dgamma, float* dbeta, int accum_params, float* ws,
@@ -60,6 +60,8 @@ void jm_opt_apply_trust(float* p, const float* u_or_g, float* trace, uint16_t* s
 void jm_opt_sgd(float* p, const float* g, float* trace, uint16_t* shadow, const int* chunks, int nchunks,
                 const float* meta, const float* hyper, const float* gnorm_sq, float momentum, hipStream_t st);
 int jm_splitk_reduce_bf16(const float* part, int S, long n, int N, const float* bias, uint16_t* out, hipStream_t st);
+int jm_splitk_reduce_f32(const float* part, int S, int M, int N, const float* bias, const float* add, long add_ld,
+                         float* out, hipStream_t st);
 int jm_gemm_nt(const uint16_t* A, long lda, const uint16_t* B, long ldb, int M, int N, int K, int epi,
                const GemmEpi& ep, hipStream_t st);
 void jm_gemm_set_variant(int wn, int group);
@@ -112,8 +114,9 @@ float* fopt_m(c10::optional<torch::Tensor>& t) { return t.has_value() && t->defi
 void check_rc(int rc, const char* what) { TORCH_CHECK(rc == 0, what, ": unsupported shape (rc=", rc, ")"); }
 
 // ------------------------------------------------------------------------------ layernorm
+// also_bf16 (fp32 output only): a bf16 copy of y written by the same pass, returned 4th
 std::vector<torch::Tensor> layernorm_fwd(torch::Tensor x, torch::Tensor gamma, torch::Tensor beta, double eps,
-                                         py::object out_dtype) {
+                                         py::object out_dtype, bool also_bf16) {
   CHECK_CUDA(x);
   TORCH_CHECK(x.dim() == 3 && x.stride(2) == 1, "x must be [B,T,D] with contiguous last dim");
   CHECK_DT(x, torch::kFloat32);
@@ -125,10 +128,14 @@ std::vector<torch::Tensor> layernorm_fwd(torch::Tensor x, torch::Tensor gamma, t
   auto mean = torch::empty({(long)B * T}, x.options());
   auto rstd = torch::empty({(long)B * T}, x.options());
   TORCH_CHECK(odt == torch::kBFloat16 || odt == torch::kFloat32, "out dtype must be bf16/fp32");
+  TORCH_CHECK(!also_bf16 || odt == torch::kFloat32, "also_bf16 needs an fp32 output");
+  torch::Tensor y2;
+  if (also_bf16) y2 = torch::empty({(long)B * T, D}, x.options().dtype(torch::kBFloat16));
   check_rc(jm_layernorm_fwd(x.data_ptr<float>(), x.stride(0), x.stride(1), B, T, D, gamma.data_ptr<float>(),
                             beta.data_ptr<float>(), (float)eps, y.data_ptr(), odt == torch::kBFloat16,
-                            mean.data_ptr<float>(), rstd.data_ptr<float>(), stream()),
+                            mean.data_ptr<float>(), rstd.data_ptr<float>(), stream(), also_bf16 ? bfm(y2) : nullptr),
            "layernorm_fwd");
+  if (also_bf16) return {y, mean, rstd, y2};
   return {y, mean, rstd};
 }
 
@@ -585,7 +592,10 @@ std::vector<torch::Tensor> gemm_nt(torch::Tensor A, torch::Tensor B, c10::option
 }
 
 // split-K: C[M, N] = A[M, K] . B[N, K]^T (+ bias) in bf16 via S fp32 partial products
-torch::Tensor gemm_nt_splitk(torch::Tensor A, torch::Tensor B, c10::optional<torch::Tensor> bias, int64_t splits) {
+// add (optional fp32 [M, N] view, unit column stride): the result is returned in fp32 as
+// A.B^T (+ bias) + add, summed in the split-K reduction
+torch::Tensor gemm_nt_splitk(torch::Tensor A, torch::Tensor B, c10::optional<torch::Tensor> bias, int64_t splits,
+                             c10::optional<torch::Tensor> add) {
   CHECK_DT(A, torch::kBFloat16);
   CHECK_DT(B, torch::kBFloat16);
   TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && A.size(1) == B.size(1), "gemm_nt_splitk: A [M,K], B [N,K]");
@@ -599,6 +609,17 @@ torch::Tensor gemm_nt_splitk(torch::Tensor A, torch::Tensor B, c10::optional<tor
   if (bias) {
     TORCH_CHECK(bias->is_contiguous() && bias->scalar_type() == torch::kFloat32 && bias->numel() == N, "bias");
     bp = bias->data_ptr<float>();
+  }
+  if (add) {
+    CHECK_CUDA(*add);
+    CHECK_DT(*add, torch::kFloat32);
+    TORCH_CHECK(add->dim() == 2 && add->size(0) == M && add->size(1) == N && add->stride(1) == 1,
+                "gemm_nt_splitk: add must be fp32 [M, N] with unit column stride");
+    auto out32 = torch::empty({M, N}, A.options().dtype(torch::kFloat32));
+    check_rc(jm_splitk_reduce_f32(part.data_ptr<float>(), (int)splits, M, N, bp, add->data_ptr<float>(),
+                                  add->stride(0), out32.data_ptr<float>(), stream()),
+             "gemm_nt_splitk reduce f32");
+    return out32;
   }
   check_rc(jm_splitk_reduce_bf16(part.data_ptr<float>(), (int)splits, (long)M * N, N, bp, bfm(out), stream()),
            "gemm_nt_splitk reduce");
@@ -748,7 +769,8 @@ void debug_selftest(int v) { jm_debug_selftest(v, stream()); }
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "jumbo_mae_tpu_amd CDNA4 (gfx950) HIP kernels";
-  m.def("layernorm_fwd", &layernorm_fwd);
+  m.def("layernorm_fwd", &layernorm_fwd, py::arg("x"), py::arg("gamma"), py::arg("beta"), py::arg("eps"),
+        py::arg("out_dtype"), py::arg("also_bf16") = false);
   m.def("layernorm_bwd", &layernorm_bwd, py::arg("dy"), py::arg("x"), py::arg("mean"), py::arg("rstd"),
         py::arg("gamma"), py::arg("dgamma"), py::arg("dbeta"), py::arg("accum"), py::arg("dres") = py::none(),
         py::arg("out") = py::none(), py::arg("res_y") = py::none(), py::arg("res_scale") = py::none(),
@@ -773,7 +795,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_set_variant", &jm_gemm_set_variant, py::arg("wn"), py::arg("group") = 8);
   m.def("gemm_set_tail", &jm_gemm_set_tail);
   m.def("gemm_nt_splitk", &gemm_nt_splitk, py::arg("A"), py::arg("B"), py::arg("bias") = py::none(),
-        py::arg("splits") = 8);
+        py::arg("splits") = 8, py::arg("add") = py::none());
   m.def("gemm_nt_dgelu", &gemm_nt_dgelu, py::arg("A"), py::arg("B"), py::arg("pre"), py::arg("dbias") = py::none());
   m.def("gemm_nt", &gemm_nt, py::arg("A"), py::arg("B"), py::arg("bias") = py::none(), py::arg("gelu") = false,
         py::arg("gelu_only") = false);

@@ -382,6 +382,52 @@ __global__ __launch_bounds__(256) void splitk_reduce_bf16_kernel(const float* __
 }
 }  // namespace
 
+// out[m][n] (fp32, contiguous) = sum_s part[s][m][n] (+ bias[n]) + add[m * add_ld + n]: a split-K NT
+// GEMM whose result is summed into an fp32 residual-stream gradient (the shared jumbo MLP's input
+// gradient d hc = dx2_cls + W1 dpre) without a bf16 round trip and a separate add pass
+namespace {
+__global__ __launch_bounds__(256) void splitk_reduce_f32_kernel(const float* __restrict__ part, int S, long n4, int N,
+                                                                const float* __restrict__ bias,
+                                                                const float* __restrict__ add, long add_ld,
+                                                                float* __restrict__ out) {
+  const long total = n4 * 4;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n4; i += (long)gridDim.x * 256) {
+    float acc[4];
+    load4(part + i * 4, acc);
+    for (int s = 1; s < S; ++s) {
+      float v[4];
+      load4(part + (long)s * total + i * 4, v);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[j] += v[j];
+    }
+    const long m = (i * 4) / N, n = (i * 4) - m * N;
+    if (bias) {
+      float b[4];
+      load4(bias + n, b);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[j] += b[j];
+    }
+    if (add) {
+      float a[4];
+      load4(add + m * add_ld + n, a);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[j] += a[j];
+    }
+    store4(out + i * 4, acc);
+  }
+}
+}  // namespace
+
+int jm_splitk_reduce_f32(const float* part, int S, int M, int N, const float* bias, const float* add, long add_ld,
+                         float* out, hipStream_t st) {
+  if (N % 4 || add_ld % 4) return -1;
+  const long n = (long)M * N;
+  long blocks = (n / 4 + 255) / 256;
+  if (blocks > 8192) blocks = 8192;
+  splitk_reduce_f32_kernel<<<(int)blocks, 256, 0, st>>>(part, S, n / 4, N, bias, add, add_ld, out);
+  return 0;
+}
+
 int jm_splitk_reduce_bf16(const float* part, int S, long n, int N, const float* bias, uint16_t* out, hipStream_t st) {
   if (n % 8 || N % 8) return -1;
   long blocks = (n / 8 + 255) / 256;

@@ -20,7 +20,7 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const float* __restrict__ x
                                                      int rows, int D, const float* __restrict__ gamma,
                                                      const float* __restrict__ beta, float eps,
                                                      TO* __restrict__ y, float* __restrict__ mean_out,
-                                                     float* __restrict__ rstd_out) {
+                                                     float* __restrict__ rstd_out, uint16_t* __restrict__ y2) {
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + wave;
   if (row >= rows) return;
@@ -63,6 +63,7 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const float* __restrict__ x
 #pragma unroll
       for (int j = 0; j < 4; ++j) o[j] = (v[i][j] - mean) * rstd * gg[j] + bb[j];
       store4(yr + col, o);
+      if (y2 != nullptr) store4(y2 + (long)row * D + col, o);  // bf16 copy (GEMM operand)
     }
   }
   if (lane == 0) {
@@ -360,9 +361,9 @@ __global__ __launch_bounds__(256) void ln_param_reduce_kernel(const float* __res
 
 template <typename TO>
 void launch_fwd(int V, dim3 grid, hipStream_t st, const float* x, long sB, long sT, int T, int rows, int D,
-                const float* g, const float* b, float eps, TO* y, float* m, float* r) {
+                const float* g, const float* b, float eps, TO* y, float* m, float* r, uint16_t* y2) {
 #define JM_LNF(VV) \
-  case VV: ln_fwd_kernel<VV, TO><<<grid, 256, 0, st>>>(x, sB, sT, T, rows, D, g, b, eps, y, m, r); break;
+  case VV: ln_fwd_kernel<VV, TO><<<grid, 256, 0, st>>>(x, sB, sT, T, rows, D, g, b, eps, y, m, r, y2); break;
   switch (V) {
     JM_LNF(1) JM_LNF(2) JM_LNF(3) JM_LNF(4) JM_LNF(6) JM_LNF(8) JM_LNF(9) JM_LNF(12) JM_LNF(16)
     default: break;
@@ -411,15 +412,15 @@ int pick_v(int D) {
 // ------------------------------------------------------------------------- host entry points
 int jm_layernorm_fwd(const float* x, long sB, long sT, int B, int T, int D, const float* gamma,
                      const float* beta, float eps, void* y, int out_bf16, float* mean, float* rstd,
-                     hipStream_t st) {
+                     hipStream_t st, uint16_t* y2) {
   const int V = pick_v(D);
   if (V < 0 || (D % 4) != 0) return -1;
   const int rows = B * T;
   dim3 grid((rows + 3) / 4);
   if (out_bf16)
-    launch_fwd<uint16_t>(V, grid, st, x, sB, sT, T, rows, D, gamma, beta, eps, (uint16_t*)y, mean, rstd);
+    launch_fwd<uint16_t>(V, grid, st, x, sB, sT, T, rows, D, gamma, beta, eps, (uint16_t*)y, mean, rstd, nullptr);
   else
-    launch_fwd<float>(V, grid, st, x, sB, sT, T, rows, D, gamma, beta, eps, (float*)y, mean, rstd);
+    launch_fwd<float>(V, grid, st, x, sB, sT, T, rows, D, gamma, beta, eps, (float*)y, mean, rstd, y2);
   return 0;
 }
 

@@ -75,10 +75,10 @@ def _ff_fwd(ff, h, train=True):
     return pre, g, y
 
 
-def _ff_bwd(ff, dy, h, pre, g, w2_bias_done=False):
+def _ff_bwd(ff, dy, h, pre, g, w2_bias_done=False, dx_add=None):
     hb1 = ff.w1.b if ff.w1.k.segs[0].trainable else None
     dpre, bias_done = P.linear_gelu_bwd(dy, g, pre, ff.w2.k, ff.w2.b, hb1, w2_bias_done)
-    return P.linear_bwd(dpre, h, ff.w1.k, ff.w1.b, bias_done=bias_done)
+    return P.linear_bwd(dpre, h, ff.w1.k, ff.w1.b, bias_done=bias_done, dx_add=dx_add)
 
 
 def _note_uses(*handles):
@@ -108,8 +108,8 @@ class JumboBlockFn(torch.autograd.Function):
         x1, hp, mup, rsp = P.residual_ln_fwd(x, a, layer.scale1, m1, layer.norm2.g, layer.norm2.b, C)
         # jumbo branch: LN3 on the concatenated CLS tokens, residual on the *normalized* value
         cls_in = x1[:, :C].reshape(B, 1, J)
-        hc, muc, rsc = P.ln_fwd(cls_in, layer.norm3.g, layer.norm3.b, torch.float32)
-        hcb = hc.to(dt)
+        # fp32 hc for the residual and its compute-dtype copy for the jumbo MLP, one pass
+        hc, muc, rsc, hcb = P.ln_fwd(cls_in, layer.norm3.g, layer.norm3.b, torch.float32, dt)
         jpre, jg, jy = _ff_fwd(layer.jumbo_mlp, hcb, train)
         # patch branch
         pin = x1[:, C:]
@@ -142,8 +142,8 @@ class JumboBlockFn(torch.autograd.Function):
         # ---- jumbo branch: d hc = dx2_cls + JumboMLP'(s3 * dp3 * dx2_cls); dx1_cls = LN3'(d hc)
         dcls = dx2[:, :C].reshape(B, 1, J)
         djy, bd = P.residual_bwd(dcls, jy, layer.scale3, m3, dt, layer.jumbo_mlp.w2.b)
-        dhcb = _ff_bwd(layer.jumbo_mlp, djy, hcb, jpre, jg, bd)
-        dhc = dcls.reshape(B, J) + dhcb.float()
+        # d hc = dcls + JumboMLP'(...) in fp32, the add fused into the jumbo dgrad's split-K reduce
+        dhc = _ff_bwd(layer.jumbo_mlp, djy, hcb, jpre, jg, bd, dx_add=dcls.reshape(B, J))
         P.ln_bwd(dhc, x1[:, :C].reshape(B, 1, J), muc, rsc, layer.norm3.g, layer.norm3.b,
                  out=dx1[:, :C].reshape(B, 1, J))
         # attention-residual backward of the CLS rows (the patch rows ride on LN2' below, which

@@ -276,13 +276,20 @@ def join_wgrad_stream() -> None:
         torch.cuda.current_stream().wait_stream(s)
 
 
-def linear_dgrad(dy: torch.Tensor, hw: Handle) -> torch.Tensor:
-    """dx = dy @ W: on the MFMA kernel against the transposed weight copy when it wins."""
+def linear_dgrad(dy: torch.Tensor, hw: Handle, add: torch.Tensor | None = None) -> torch.Tensor:
+    """dx = dy @ W: on the MFMA kernel against the transposed weight copy when it wins.  With
+    ``add`` (fp32 [M, N]) the fp32 sum ``add + dy @ W`` is returned (fused into the split-K
+    reduction on the jumbo-MLP path)."""
     w = hw.weight()
     if _DGRAD_OURS and hip(dy) and dy.dtype == torch.bfloat16:
         s = splitk_plan(dy.shape[0], w.shape[1], w.shape[0])
         if s:
-            return _ext.load().gemm_nt_splitk(dy.contiguous(), hw.weight_t(), None, s)
+            if add is not None and add.stride(-1) == 1 and add.stride(0) % 4 == 0 and add.shape[1] % 4 == 0:
+                return _ext.load().gemm_nt_splitk(dy.contiguous(), hw.weight_t(), None, s, add)
+            dx = _ext.load().gemm_nt_splitk(dy.contiguous(), hw.weight_t(), None, s)
+            return dx if add is None else add + dx.float()
+    if add is not None:
+        return add + linear_dgrad(dy, hw).float()
     if (_DGRAD_OURS and hip(dy) and dy.dtype == torch.bfloat16
             and use_our_gemm(dy.shape[0], w.shape[1], w.shape[0], kind="dgrad")):
         return _ext.load().gemm_nt(dy.contiguous(), hw.weight_t(), None, False)[0]
@@ -290,9 +297,10 @@ def linear_dgrad(dy: torch.Tensor, hw: Handle) -> torch.Tensor:
 
 
 def linear_bwd(dy: torch.Tensor, x2: torch.Tensor, hw: Handle, hb: Handle | None, need_dx: bool = True,
-               bias_done: bool = False):
-    """dx = dy @ W (if needed); grad W += dy^T x; grad b += colsum(dy) (unless fused upstream)."""
-    dx = linear_dgrad(dy, hw) if need_dx else None
+               bias_done: bool = False, dx_add: torch.Tensor | None = None):
+    """dx = dy @ W (if needed; ``dx_add + dy @ W`` in fp32 with ``dx_add``); grad W += dy^T x;
+    grad b += colsum(dy) (unless fused upstream)."""
+    dx = linear_dgrad(dy, hw, dx_add) if need_dx else None
     if (_trainable(hw) and hw.defer_wgrad and _deferred["enabled"] and (hip(dy) or _deferred["force"])
             and _defer_wgrad(hw, dy, x2)):
         if hb is not None:
@@ -363,17 +371,21 @@ def gelu_bwd(h: torch.Tensor, da: torch.Tensor, hb: Handle | None = None) -> tup
 
 
 # ------------------------------------------------------------------------------ layernorm
-def ln_fwd(x3: torch.Tensor, hg: Handle, hb: Handle, out_dtype):
-    """x3: fp32 [B, T, D] view -> (y [B*T, D], mean, rstd)."""
+def ln_fwd(x3: torch.Tensor, hg: Handle, hb: Handle, out_dtype, also_dtype=None):
+    """x3: fp32 [B, T, D] view -> (y [B*T, D], mean, rstd); with ``also_dtype`` (fp32 ``y`` only) a
+    copy of y in that dtype is returned 4th, written by the same pass on the GPU."""
     B, T, D = x3.shape
     if hip(x3):
-        return _ext.load().layernorm_fwd(x3, hg.master, hb.master, LN_EPS, out_dtype)
+        if also_dtype is not None and out_dtype == torch.float32 and also_dtype == torch.bfloat16:
+            return tuple(_ext.load().layernorm_fwd(x3, hg.master, hb.master, LN_EPS, out_dtype, True))
+        out = tuple(_ext.load().layernorm_fwd(x3, hg.master, hb.master, LN_EPS, out_dtype))
+        return out if also_dtype is None else out + (out[0].to(also_dtype),)
     xf = x3.reshape(B * T, D).float()
     mean = xf.mean(-1)
     var = (xf - mean[:, None]).square().mean(-1)
     rstd = torch.rsqrt(var + LN_EPS)
     y = ((xf - mean[:, None]) * rstd[:, None] * hg.master + hb.master).to(out_dtype)
-    return y, mean, rstd
+    return (y, mean, rstd) if also_dtype is None else (y, mean, rstd, y.to(also_dtype))
 
 
 _FUSE_LN_RES = os.environ.get("JMAE_FUSE_LN_RES", "1") == "1"  # A/B switch (tools/ab_bench.py)

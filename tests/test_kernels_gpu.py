@@ -387,3 +387,35 @@ def test_gemm_nt_tail_split(ext, kind, M, N, K):
         assert rel(outs[1][0], ref + b) < 1e-2
     if kind == "dgelu":
         assert rel(outs[1][1], outs[0][1]) < 1e-3
+
+
+def test_layernorm_fwd_also_bf16(ext):
+    """fp32 LN output plus its bf16 copy from the same pass == .bfloat16() of the fp32 output."""
+    torch.manual_seed(0)
+    full = torch.randn(5, 7, 3072, device="cuda") * 2 + 0.5
+    x = full[:, 4:]  # strided [5, 3, 3072] view (the jumbo CLS rows)
+    g, b = torch.randn(3072, device="cuda"), torch.randn(3072, device="cuda")
+    y, m, r = ext.layernorm_fwd(x, g, b, 1e-6, torch.float32)
+    y2, m2, r2, yb = ext.layernorm_fwd(x, g, b, 1e-6, torch.float32, True)
+    assert torch.equal(y, y2) and torch.equal(m, m2) and torch.equal(r, r2)
+    assert yb.dtype == torch.bfloat16 and torch.equal(yb, y.bfloat16())
+
+
+def test_gemm_splitk_fused_fp32_add(ext):
+    """Split-K NT GEMM returning A.B^T + add in fp32 (add = a strided fp32 view, the jumbo-MLP input
+    gradient path) == fp32 reference; bias variant too."""
+    torch.manual_seed(0)
+    M, N, K = 512, 3072, 12288
+    A = (torch.randn(M, K, device="cuda") * 0.05).bfloat16()
+    B = (torch.randn(N, K, device="cuda") * 0.05).bfloat16()
+    big = torch.randn(M, 3, N, device="cuda")
+    add = big[:, 1]  # [M, N], row stride 3N
+    ref = A.float() @ B.float().t()
+    out = ext.gemm_nt_splitk(A, B, None, 10, add)
+    assert out.dtype == torch.float32 and out.shape == (M, N)
+    assert rel(out, ref + add) < 1e-5 + 1e-3 * ref.norm().item() / (ref + add).norm().item()
+    bias = torch.randn(N, device="cuda")
+    out_b = ext.gemm_nt_splitk(A, B, bias, 10, add)
+    assert rel(out_b, ref + bias + add) < 2e-3
+    # bf16 path unchanged
+    assert rel(ext.gemm_nt_splitk(A, B, None, 10), ref) < 1e-2
