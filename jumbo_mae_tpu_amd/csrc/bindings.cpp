@@ -15,7 +15,7 @@ int jm_layernorm_bwd(const void* dy, int dy_bf16, const float* x, long sB, long 
                      const float* mean, const float* rstd, const float* gamma, float* dx_ptr, long oB, long oT,
                      const float* dres, long rB, long rT, float* dgamma, float* dbeta, int accum_params, float* ws,
                      const JmLnRes* res, hipStream_t st);
-int jm_layernorm_bwd_blocks(int rows);
+int jm_layernorm_bwd_blocks(int rows, int D);
 void jm_ln_set_bwd_la(int v);
 // debug build (-DJM_DEBUG): first failing soft-check line per kernel translation unit (0 = none;
 // reading clears it); always 0 in the release build
@@ -199,7 +199,7 @@ std::vector<torch::Tensor> layernorm_bwd(torch::Tensor dy, torch::Tensor x, torc
                   fopt_m(res_dbias)};
   }
   const int NP = has_res ? 4 : 2;
-  auto ws = torch::empty({(accum || has_res) ? (long)jm_layernorm_bwd_blocks(B * T) * NP * D : 1}, x.options());
+  auto ws = torch::empty({(accum || has_res) ? (long)jm_layernorm_bwd_blocks(B * T, D) * NP * D : 1}, x.options());
   check_rc(jm_layernorm_bwd(dy.data_ptr(), dyb, x.data_ptr<float>(), x.stride(0), x.stride(1), B, T, D,
                             mean.data_ptr<float>(), rstd.data_ptr<float>(), gamma.data_ptr<float>(),
                             dx.data_ptr<float>(), dx.stride(0), dx.stride(1), rp, rB, rT, dgamma.data_ptr<float>(),

@@ -371,6 +371,155 @@ void launch_fwd(int V, dim3 grid, hipStream_t st, const float* x, long sB, long 
 #undef JM_LNF
 }
 
+// ------------------------------------------------------------------ wide rows, few of them
+// The jumbo branch's LN3 normalises B rows of J = 3D (2304 / 3072) values: with one row per wave
+// that is only B / 4 workgroups (128 for B = 512) and a 12-float4-per-lane chain per wave.  Here a
+// whole 256-thread workgroup owns a row (VW float4 per thread, block reduction through LDS), so
+// the grid has one workgroup per row.
+
+// sum over the 256 threads of the workgroup (every thread gets it); red: >= 4 floats of LDS
+JM_DEVICE float block_sum256(float v, float* red) {
+  const int wave = threadIdx.x >> 6;
+  v = wave_sum(v);
+  __syncthreads();  // red may still be read from a previous call
+  if ((threadIdx.x & 63) == 0) red[wave] = v;
+  __syncthreads();
+  return (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+template <int VW, typename TO>
+__global__ __launch_bounds__(256) void ln_fwd_wide_kernel(const float* __restrict__ x, long sB, long sT, int T,
+                                                          int rows, int D, const float* __restrict__ gamma,
+                                                          const float* __restrict__ beta, float eps,
+                                                          TO* __restrict__ y, float* __restrict__ mean_out,
+                                                          float* __restrict__ rstd_out, uint16_t* __restrict__ y2) {
+  JM_DGUARD(blockDim.x == 256 && D % 4 == 0 && D <= VW * 1024);
+  __shared__ float red[4];
+  const int row = blockIdx.x;
+  const int b = row / T, t = row - b * T;
+  const float* xr = x + b * sB + t * sT;
+  float v[VW][4];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < VW; ++i) {
+    const int col = (i * 256 + threadIdx.x) * 4;
+    if (col < D) {
+      load4(xr + col, v[i]);
+    } else {
+      v[i][0] = v[i][1] = v[i][2] = v[i][3] = 0.f;
+    }
+    s += (v[i][0] + v[i][1]) + (v[i][2] + v[i][3]);
+  }
+  const float mean = block_sum256(s, red) / D;
+  float s2 = 0.f;
+#pragma unroll
+  for (int i = 0; i < VW; ++i) {
+    const int col = (i * 256 + threadIdx.x) * 4;
+    if (col < D) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float d = v[i][j] - mean;
+        s2 += d * d;
+      }
+    }
+  }
+  const float rstd = rsqrtf(block_sum256(s2, red) / D + eps);
+#pragma unroll
+  for (int i = 0; i < VW; ++i) {
+    const int col = (i * 256 + threadIdx.x) * 4;
+    if (col < D) {
+      float gg[4], bb[4], o[4];
+      load4(gamma + col, gg);
+      load4(beta + col, bb);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) o[j] = (v[i][j] - mean) * rstd * gg[j] + bb[j];
+      store4(y + (long)row * D + col, o);
+      if (y2 != nullptr) store4(y2 + (long)row * D + col, o);
+    }
+  }
+  if (threadIdx.x == 0) {
+    mean_out[row] = mean;
+    rstd_out[row] = rstd;
+  }
+}
+
+// dx = LN'(dy) (+ dres); per-workgroup [dgamma | dbeta] partial rows in ws (grid-stride rows)
+template <int VW, typename TI>
+__global__ __launch_bounds__(256) void ln_bwd_wide_kernel(const TI* __restrict__ dy, const float* __restrict__ x,
+                                                          long sB, long sT, int T, int rows, int D,
+                                                          const float* __restrict__ mean,
+                                                          const float* __restrict__ rstd,
+                                                          const float* __restrict__ gamma, LnBwdIO io,
+                                                          float* __restrict__ ws, int accum_params) {
+  JM_DGUARD(blockDim.x == 256 && D % 4 == 0 && D <= VW * 1024);
+  __shared__ float red[4];
+  float ag[VW][4], ab[VW][4], gg[VW][4];
+#pragma unroll
+  for (int i = 0; i < VW; ++i) {
+    const int col = (i * 256 + threadIdx.x) * 4;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) ag[i][j] = ab[i][j] = gg[i][j] = 0.f;
+    if (col < D) load4(gamma + col, gg[i]);
+  }
+  for (int row = blockIdx.x; row < rows; row += gridDim.x) {  // workgroup-uniform
+    const int b = row / T, t = row - b * T;
+    const float* xr = x + b * sB + t * sT;
+    const TI* dyr = dy + (long)row * D;
+    const float* rr = io.dres ? io.dres + b * io.rB + t * io.rT : nullptr;
+    const float mu = mean[row], rs = rstd[row];
+    float xh[VW][4], g[VW][4], rv[VW][4];
+    float sg = 0.f, sgx = 0.f;
+#pragma unroll
+    for (int i = 0; i < VW; ++i) {
+      const int col = (i * 256 + threadIdx.x) * 4;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) xh[i][j] = g[i][j] = rv[i][j] = 0.f;
+      if (col < D) {
+        float xv[4], dv[4];
+        load4(xr + col, xv);
+        load4(dyr + col, dv);
+        if (rr) load4(rr + col, rv[i]);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          xh[i][j] = (xv[j] - mu) * rs;
+          g[i][j] = dv[j] * gg[i][j];
+          sg += g[i][j];
+          sgx += g[i][j] * xh[i][j];
+          ag[i][j] += dv[j] * xh[i][j];
+          ab[i][j] += dv[j];
+        }
+      }
+    }
+    sg = block_sum256(sg, red) / D;
+    sgx = block_sum256(sgx, red) / D;
+    float* dxr = io.dx + b * io.oB + t * io.oT;
+#pragma unroll
+    for (int i = 0; i < VW; ++i) {
+      const int col = (i * 256 + threadIdx.x) * 4;
+      if (col < D) {
+        float o[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) o[j] = rs * (g[i][j] - sg - xh[i][j] * sgx) + rv[i][j];
+        store4(dxr + col, o);
+      }
+    }
+  }
+  if (!accum_params) return;
+#pragma unroll
+  for (int i = 0; i < VW; ++i) {
+    const int col = (i * 256 + threadIdx.x) * 4;
+    if (col < D) {
+      store4(ws + (long)blockIdx.x * 2 * D + col, ag[i]);
+      store4(ws + (long)blockIdx.x * 2 * D + D + col, ab[i]);
+    }
+  }
+}
+
+// wide-row path: D > 1024 with at most this many rows (enough workgroups, few enough partials)
+constexpr int LN_WIDE_MAX_ROWS = 8192;
+int pick_vw(int D) { return D <= 2048 ? 2 : D <= 3072 ? 3 : D <= 4096 ? 4 : -1; }
+bool use_wide(int rows, int D) { return D > 1024 && rows <= LN_WIDE_MAX_ROWS && pick_vw(D) > 0; }
+
 // runtime switch (A/B): 0 = register partials, dres loaded after the row reduction; 1 = LDS-accumulated
 // parameter partials + early dres load (the ds_add_f32 accumulation made the ViT-L step 97.8 ->
 // 122.2 ms despite the doubled occupancy, profiles/r1_ab_ln_bwd_lds_acc.txt); 2 (default) = register
@@ -416,6 +565,22 @@ int jm_layernorm_fwd(const float* x, long sB, long sT, int B, int T, int D, cons
   const int V = pick_v(D);
   if (V < 0 || (D % 4) != 0) return -1;
   const int rows = B * T;
+  if (use_wide(rows, D)) {
+    const int VW = pick_vw(D);
+#define JM_LNFW(VV, TO, YP, Y2)                                                                                    \
+  case VV:                                                                                                         \
+    ln_fwd_wide_kernel<VV, TO><<<rows, 256, 0, st>>>(x, sB, sT, T, rows, D, gamma, beta, eps, YP, mean, rstd, Y2); \
+    break;
+    if (out_bf16) {
+      switch (VW) { JM_LNFW(2, uint16_t, (uint16_t*)y, nullptr) JM_LNFW(3, uint16_t, (uint16_t*)y, nullptr)
+                    JM_LNFW(4, uint16_t, (uint16_t*)y, nullptr) default: return -1; }
+    } else {
+      switch (VW) { JM_LNFW(2, float, (float*)y, y2) JM_LNFW(3, float, (float*)y, y2) JM_LNFW(4, float, (float*)y, y2)
+                    default: return -1; }
+    }
+#undef JM_LNFW
+    return 0;
+  }
   dim3 grid((rows + 3) / 4);
   if (out_bf16)
     launch_fwd<uint16_t>(V, grid, st, x, sB, sT, T, rows, D, gamma, beta, eps, (uint16_t*)y, mean, rstd, nullptr);
@@ -444,7 +609,9 @@ int jm_residual_ln_fwd(const float* x, long sB, long sT, const uint16_t* y, cons
 
 void jm_ln_set_bwd_la(int v) { g_ln_bwd_la = v; }
 
-int jm_layernorm_bwd_blocks(int rows) {
+int jm_layernorm_bwd_blocks(int rows, int D) {
+  // wide rows: one workgroup per row (at most 1024 workgroups, grid-stride beyond)
+  if (use_wide(rows, D)) return rows > 1024 ? 1024 : rows;
   // grid-stride over rows: 1024 blocks x 4 waves = 4 waves per SIMD streaming; each block writes
   // one [2*D] partial (no atomics in the hot kernel)
   int nb = (rows + 3) / 4;
@@ -459,10 +626,30 @@ int jm_layernorm_bwd(const void* dy, int dy_bf16, const float* x, long sB, long 
   const int V = pick_v(D);
   if (V < 0 || (D % 4) != 0) return -1;
   const int rows = B * T;
-  const int nb = jm_layernorm_bwd_blocks(rows);
+  const int nb = jm_layernorm_bwd_blocks(rows, D);
   dim3 grid(nb);
   const int NP = res ? 4 : 2;
   const bool partials = accum_params || res;
+  if (!res && use_wide(rows, D)) {
+    const int VW = pick_vw(D);
+#define JM_LNBW(VV, TI)                                                                                     \
+  case VV:                                                                                                  \
+    ln_bwd_wide_kernel<VV, TI><<<nb, 256, 0, st>>>((const TI*)dy, x, sB, sT, T, rows, D, mean, rstd, gamma, \
+                                                   dx, ws, accum_params);                                   \
+    break;
+    if (dy_bf16) {
+      switch (VW) { JM_LNBW(2, uint16_t) JM_LNBW(3, uint16_t) JM_LNBW(4, uint16_t) default: return -1; }
+    } else {
+      switch (VW) { JM_LNBW(2, float) JM_LNBW(3, float) JM_LNBW(4, float) default: return -1; }
+    }
+#undef JM_LNBW
+    if (accum_params) {
+      ParamOuts outs{{dgamma, dbeta, nullptr, nullptr}};
+      const int ysplit = nb >= 64 ? 16 : 1;
+      ln_param_reduce_kernel<<<dim3((2 * D + 255) / 256, ysplit), 256, 0, st>>>(ws, nb, D, 2, outs);
+    }
+    return 0;
+  }
   const size_t smem = partials ? NP * D * sizeof(float) : 0;
   LnResIO rio{nullptr, nullptr, 0, 0, nullptr, nullptr, 0};
   if (res) rio = LnResIO{res->y, res->dy, res->yB, res->yT, res->scale, res->mask, res->T0};
