@@ -29,7 +29,7 @@ int jm_debug_line_optim();
 void jm_debug_selftest(int v, hipStream_t st);
 int jm_residual_ln_fwd(const float* x, long sB, long sT, const uint16_t* y, const float* scale, const float* mask,
                        float* x1, long oB, long oT, uint16_t* h, float* mean, float* rstd, int B, int T, int T0,
-                       int D, const float* gamma, const float* beta, float eps, hipStream_t st);
+                       int D, const float* gamma, const float* beta, float eps, hipStream_t st, int R0 = 0);
 int jm_gelu_fwd(const uint16_t* h, uint16_t* a, long n, hipStream_t st);
 int jm_gelu_bwd(const uint16_t* h, const uint16_t* da, uint16_t* dh, float* bias_grad, int M, int N, hipStream_t st);
 int jm_colsum_bf16(const uint16_t* x, float* acc, int M, int N, hipStream_t st);
@@ -729,16 +729,27 @@ int64_t gemm_tn_wgrad_seg(std::vector<torch::Tensor> dys, std::vector<torch::Ten
 // x1 = x + mask*scale*y ([B,T,D] fp32, fresh contiguous); h / mean / rstd = LN of rows t >= T0
 std::vector<torch::Tensor> residual_ln_fwd(torch::Tensor x, torch::Tensor y, c10::optional<torch::Tensor> scale,
                                            c10::optional<torch::Tensor> mask, torch::Tensor gamma,
-                                           torch::Tensor beta, double eps, int64_t T0) {
+                                           torch::Tensor beta, double eps, int64_t T0, int64_t R0,
+                                           c10::optional<torch::Tensor> out) {
   CHECK_CUDA(x);
   TORCH_CHECK(x.dim() == 3 && x.stride(2) == 1, "x must be [B,T,D] with contiguous last dim");
   CHECK_DT(x, torch::kFloat32);
   CHECK_DT(y, torch::kBFloat16);
   CHECK_CONTIG(y);
   const int B = x.size(0), T = x.size(1), D = x.size(2);
-  TORCH_CHECK(y.numel() == (long)B * T * D, "residual_ln_fwd: y must be [B*T, D]");
+  TORCH_CHECK(R0 >= 0 && R0 < T, "residual_ln_fwd: R0");
+  TORCH_CHECK(y.numel() == (long)B * (T - R0) * D, "residual_ln_fwd: y must be [B*(T-R0), D]");
   TORCH_CHECK(T0 >= 0 && T0 < T, "residual_ln_fwd: T0");
-  auto x1 = torch::empty({B, T, D}, x.options());
+  TORCH_CHECK(R0 == 0 || out.has_value(), "residual_ln_fwd: R0 > 0 needs out (its rows t < R0 are inputs)");
+  torch::Tensor x1;
+  if (out) {
+    CHECK_DT(*out, torch::kFloat32);
+    TORCH_CHECK(out->dim() == 3 && out->size(0) == B && out->size(1) == T && out->size(2) == D && out->stride(2) == 1,
+                "residual_ln_fwd: out must be [B,T,D] with contiguous last dim");
+    x1 = *out;
+  } else {
+    x1 = torch::empty({B, T, D}, x.options());
+  }
   const long R = (long)B * (T - T0);
   auto h = torch::empty({R, D}, y.options());
   auto mean = torch::empty({R}, x.options());
@@ -746,7 +757,7 @@ std::vector<torch::Tensor> residual_ln_fwd(torch::Tensor x, torch::Tensor y, c10
   check_rc(jm_residual_ln_fwd(x.data_ptr<float>(), x.stride(0), x.stride(1), bf(y), fopt(scale), fopt(mask),
                               x1.data_ptr<float>(), x1.stride(0), x1.stride(1), bfm(h), mean.data_ptr<float>(),
                               rstd.data_ptr<float>(), B, T, T0, D, gamma.data_ptr<float>(), beta.data_ptr<float>(),
-                              (float)eps, stream()),
+                              (float)eps, stream(), (int)R0),
            "residual_ln_fwd");
   return {x1, h, mean, rstd};
 }
@@ -780,7 +791,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gelu_bwd", &gelu_bwd, py::arg("h"), py::arg("da"), py::arg("bias_grad") = py::none());
   m.def("colsum", &colsum);
   m.def("splitk_reduce_add", &splitk_reduce_add);
-  m.def("residual_ln_fwd", &residual_ln_fwd);
+  m.def("residual_ln_fwd", &residual_ln_fwd, py::arg("x"), py::arg("y"), py::arg("scale"), py::arg("mask"),
+        py::arg("gamma"), py::arg("beta"), py::arg("eps"), py::arg("T0"), py::arg("R0") = 0,
+        py::arg("out") = py::none());
   m.def("transpose_bf16", &transpose_bf16);
   m.def("residual_fwd", &residual_fwd, py::arg("x"), py::arg("y"), py::arg("scale"), py::arg("mask"),
         py::arg("out") = py::none());

@@ -90,17 +90,21 @@ struct ResLnIO {
   float* rstd;
 };
 
+// R0 > 0: only rows t >= R0 are residual targets (y holds [B*(T-R0), D] rows); rows t < R0 of x1
+// are already final and are only normalised (read from x1 itself) -- the jumbo block's CLS rows,
+// whose residual is the jumbo branch's, when the NEXT block's LN1 rides on this pass.
 template <int V>
-__global__ __launch_bounds__(256) void res_ln_fwd_kernel(ResLnIO io, int T, int T0, int rows, int D,
+__global__ __launch_bounds__(256) void res_ln_fwd_kernel(ResLnIO io, int T, int T0, int R0, int rows, int D,
                                                          const float* __restrict__ gamma,
                                                          const float* __restrict__ beta, float eps) {
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + wave;
   if (row >= rows) return;
   const int b = row / T, t = row - b * T;
-  const float* xr = io.x + b * io.sB + t * io.sT;
-  const uint16_t* yr = io.y + (long)row * D;
+  const bool rrow = t >= R0;  // wave-uniform
   float* x1r = io.x1 + b * io.oB + t * io.oT;
+  const float* xr = rrow ? io.x + b * io.sB + t * io.sT : x1r;
+  const uint16_t* yr = io.y + ((long)b * (T - R0) + (t - R0)) * D;
   const float m = io.mask ? io.mask[b] : 1.f;
   float v[V][4];
   float s = 0.f;
@@ -108,13 +112,19 @@ __global__ __launch_bounds__(256) void res_ln_fwd_kernel(ResLnIO io, int T, int 
   for (int i = 0; i < V; ++i) {
     const int col = (i * 64 + lane) * 4;
     if (col < D) {
-      float xv[4], yv[4], sc[4] = {1.f, 1.f, 1.f, 1.f};
+      float xv[4];
       load4(xr + col, xv);
-      load4(yr + col, yv);
-      if (io.scale) load4(io.scale + col, sc);
+      if (rrow) {
+        float yv[4], sc[4] = {1.f, 1.f, 1.f, 1.f};
+        load4(yr + col, yv);
+        if (io.scale) load4(io.scale + col, sc);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) v[i][j] = xv[j] + m * sc[j] * yv[j];
-      store4(x1r + col, v[i]);
+        for (int j = 0; j < 4; ++j) v[i][j] = xv[j] + m * sc[j] * yv[j];
+        store4(x1r + col, v[i]);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[i][j] = xv[j];
+      }
     } else {
       v[i][0] = v[i][1] = v[i][2] = v[i][3] = 0.f;
     }
@@ -591,14 +601,15 @@ int jm_layernorm_fwd(const float* x, long sB, long sT, int B, int T, int D, cons
 
 int jm_residual_ln_fwd(const float* x, long sB, long sT, const uint16_t* y, const float* scale, const float* mask,
                        float* x1, long oB, long oT, uint16_t* h, float* mean, float* rstd, int B, int T, int T0,
-                       int D, const float* gamma, const float* beta, float eps, hipStream_t st) {
+                       int D, const float* gamma, const float* beta, float eps, hipStream_t st, int R0) {
   const ResLnIO io{x, sB, sT, y, scale, mask, x1, oB, oT, h, mean, rstd};
+  if (R0 < 0 || R0 >= T) return -2;
   const int V = pick_v(D);
   if (V < 0 || (D % 4) != 0) return -1;
   const int rows = B * T;
   dim3 grid((rows + 3) / 4);
 #define JM_RLN(VV) \
-  case VV: res_ln_fwd_kernel<VV><<<grid, 256, 0, st>>>(io, T, T0, rows, D, gamma, beta, eps); break;
+  case VV: res_ln_fwd_kernel<VV><<<grid, 256, 0, st>>>(io, T, T0, R0, rows, D, gamma, beta, eps); break;
   switch (V) {
     JM_RLN(1) JM_RLN(2) JM_RLN(3) JM_RLN(4) JM_RLN(6) JM_RLN(8) JM_RLN(9) JM_RLN(12) JM_RLN(16)
     default: return -1;

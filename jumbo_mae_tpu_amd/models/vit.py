@@ -298,8 +298,13 @@ def _run_layers(layers, x, rng, det, grad_ckpt):
             x = torch.utils.checkpoint.checkpoint(layer, x, rng, det, use_reentrant=False)
         return x
     link = None
-    for layer in layers:
-        nxt = blocks.Link() if blocks.LINKS and torch.is_grad_enabled() else None
+    for i, layer in enumerate(layers):
+        nxt = None
+        if blocks.LINKS and torch.is_grad_enabled():
+            up = layers[i + 1] if i + 1 < len(layers) else None
+            # the upper block's LN1 rides on this block's last residual pass (forward hand-off)
+            ln1 = (up.norm1.g, up.norm1.b) if up is not None and blocks.FWD_LINKS else None
+            nxt = blocks.Link(ln1)
         x = layer(x, rng, det, link_in=link, link_out=nxt)
         link = nxt
     return x

@@ -26,6 +26,8 @@ from . import prims as P
 
 
 LINKS = os.environ.get("JMAE_LINK_BLOCKS", "1") == "1"  # A/B switch (tools/ab_bench.py)
+# forward hand-off of the upper block's LN1 (Link.ln1); A/B switch
+FWD_LINKS = os.environ.get("JMAE_FWD_LINKS", "1") == "1"
 
 
 class Link:
@@ -33,15 +35,34 @@ class Link:
     boundary).  The lower block's forward publishes its patch-branch residual (y, s2, mask, bias,
     t0) as a ``P.ResSpec``; the upper block's backward fuses that residual's backward into its LN1
     backward -- whose dx IS the lower block's dx2 -- and leaves dy / bias_done here, so the lower
-    block skips a pass that would re-read dx2 from HBM."""
+    block skips a pass that would re-read dx2 from HBM.
 
-    __slots__ = ("spec", "dy", "done", "dx_key")
+    Forward direction: when the layer loop names the upper block's LN1 (``ln1`` = (gamma, beta)
+    handles), the lower block computes that LayerNorm in the same pass as its last residual add and
+    leaves (h1, mean, rstd) here for the upper block, which would otherwise re-read x2 from HBM."""
 
-    def __init__(self):
+    __slots__ = ("spec", "dy", "done", "dx_key", "ln1", "h1")
+
+    def __init__(self, ln1=None):
         self.spec = None
         self.dy = None
         self.done = False
         self.dx_key = None
+        self.ln1 = ln1
+        self.h1 = None
+
+    def put_h1(self, x2: torch.Tensor, h1, mu, rs):
+        self.h1 = (x2.data_ptr(), tuple(x2.shape), h1, mu, rs)
+
+    def take_h1(self, x: torch.Tensor):
+        """(h1, mean, rstd) of LN1(x) if the lower block produced them for exactly this x."""
+        if self.h1 is None:
+            return None
+        ptr, shape, h1, mu, rs = self.h1
+        self.h1 = None
+        if (ptr, shape) != (x.data_ptr(), tuple(x.shape)):
+            return None
+        return h1, mu, rs
 
     def take(self, dx2: torch.Tensor):
         """The fused dy if the upper block produced one for exactly this dx2, else None."""
@@ -102,7 +123,7 @@ class JumboBlockFn(torch.autograd.Function):
         C = layer.C
         J = C * D
         dt = layer.norm1.g.store.compute_dtype
-        h1, mu1, rs1 = P.ln_fwd(x, layer.norm1.g, layer.norm1.b, dt)
+        h1, mu1, rs1 = _ln1_fwd(x, layer, link_in, dt)
         qkv, o, lse, a = _attn_fwd(layer.attn, h1, B, S)
         # residual + LN2 of the patch rows in one pass
         x1, hp, mup, rsp = P.residual_ln_fwd(x, a, layer.scale1, m1, layer.norm2.g, layer.norm2.b, C)
@@ -116,7 +137,12 @@ class JumboBlockFn(torch.autograd.Function):
         fpre, fg, fy = _ff_fwd(layer.ff, hp, train)
         x2 = torch.empty_like(x1)
         P.residual_fwd(hc.view(B, 1, J), jy, layer.scale3, m3, out=x2[:, :C].reshape(B, 1, J))
-        P.residual_fwd(pin, fy, layer.scale2, m2, out=x2[:, C:])
+        nl = link_out.ln1 if link_out is not None else None
+        if nl is not None:  # patch-row residual + the upper block's LN1 over all rows, one pass
+            _, h1n, mun, rsn = P.residual_ln_fwd(x1, fy, layer.scale2, m2, nl[0], nl[1], 0, C, out=x2)
+            link_out.put_h1(x2, h1n, mun, rsn)
+        else:
+            P.residual_fwd(pin, fy, layer.scale2, m2, out=x2[:, C:])
         ctx.save_for_backward(x, mu1, rs1, h1, qkv, o, lse, a, x1, muc, rsc, hcb, jpre, jg, jy,
                               hp, mup, rsp, fpre, fg, fy, m1, m2, m3)
         ctx.layer = layer
@@ -167,6 +193,14 @@ class JumboBlockFn(torch.autograd.Function):
         return dx, None, None, None, None, None, None, None, None
 
 
+def _ln1_fwd(x, layer, link_in, dt):
+    """LN1 of the block input, or the copy the lower block computed in its last residual pass."""
+    pre = link_in.take_h1(x) if link_in is not None else None
+    if pre is not None:
+        return pre
+    return P.ln_fwd(x, layer.norm1.g, layer.norm1.b, dt)
+
+
 def _ln1_bwd(ctx, dh1, x, mu1, rs1, layer, dx1):
     """dx = dx1 + LN1'(dh1) into dx1; with a lower fused block linked, its patch-branch residual
     backward rides on the same pass (Link)."""
@@ -192,11 +226,16 @@ class ViTBlockFn(torch.autograd.Function):
     def forward(ctx, x, anchor, layer, m1, m2, link_in, link_out, train=True):
         B, S, D = x.shape
         dt = layer.norm1.g.store.compute_dtype
-        h1, mu1, rs1 = P.ln_fwd(x, layer.norm1.g, layer.norm1.b, dt)
+        h1, mu1, rs1 = _ln1_fwd(x, layer, link_in, dt)
         qkv, o, lse, a = _attn_fwd(layer.attn, h1, B, S)
         x1, h2, mu2, rs2 = P.residual_ln_fwd(x, a, layer.scale1, m1, layer.norm2.g, layer.norm2.b, 0)
         fpre, fg, fy = _ff_fwd(layer.ff, h2, train)
-        x2 = P.residual_fwd(x1, fy, layer.scale2, m2)
+        nl = link_out.ln1 if link_out is not None else None
+        if nl is not None:  # last residual + the upper block's LN1, one pass
+            x2, h1n, mun, rsn = P.residual_ln_fwd(x1, fy, layer.scale2, m2, nl[0], nl[1], 0)
+            link_out.put_h1(x2, h1n, mun, rsn)
+        else:
+            x2 = P.residual_fwd(x1, fy, layer.scale2, m2)
         ctx.save_for_backward(x, mu1, rs1, h1, qkv, o, lse, a, x1, mu2, rs2, h2, fpre, fg, fy, m1, m2)
         ctx.layer = layer
         ctx.link_in, ctx.link_out = link_in, link_out

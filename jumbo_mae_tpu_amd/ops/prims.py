@@ -470,14 +470,21 @@ def residual_fwd(x3: torch.Tensor, y2: torch.Tensor, hs: Handle | None, mask, ou
 
 
 def residual_ln_fwd(x3: torch.Tensor, y2: torch.Tensor, hs: Handle | None, mask, hg: Handle, hb: Handle,
-                    t0: int = 0):
-    """x1 = x + mask*s*y (fresh [B,T,D] fp32) and the LayerNorm of its rows t >= t0 in one pass:
-    returns (x1, h [B*(T-t0), D] bf16, mean, rstd).  The fused kernel saves the LN's re-read of x1."""
+                    t0: int = 0, r0: int = 0, out: torch.Tensor | None = None):
+    """x1 = x + mask*s*y (fresh [B,T,D] fp32, or ``out``) and the LayerNorm of its rows t >= t0 in
+    one pass: returns (x1, h [B*(T-t0), D] bf16, mean, rstd).  The fused kernel saves the LN's re-read
+    of x1.  ``r0 > 0``: only rows t >= r0 get the residual (``y2`` holds those rows); rows t < r0
+    of ``out`` are already final and are only normalised."""
     B, T, D = x3.shape
     if hip(x3) and y2.dtype == torch.bfloat16:
-        return tuple(_ext.load().residual_ln_fwd(x3, y2.reshape(B * T, D), hs.master if hs is not None else None,
-                                                 mask, hg.master, hb.master, LN_EPS, t0))
-    x1 = residual_fwd(x3, y2, hs, mask)
+        return tuple(_ext.load().residual_ln_fwd(x3, y2.reshape(B * (T - r0), D),
+                                                 hs.master if hs is not None else None, mask, hg.master, hb.master,
+                                                 LN_EPS, t0, r0, out))
+    if r0 == 0 and out is None:
+        x1 = residual_fwd(x3, y2, hs, mask)
+    else:
+        x1 = out if out is not None else torch.empty_like(x3)
+        residual_fwd(x3[:, r0:], y2, hs, mask, out=x1[:, r0:])
     h, mean, rstd = ln_fwd(x1[:, t0:], hg, hb, hg.store.compute_dtype)
     return x1, h, mean, rstd
 

@@ -297,6 +297,32 @@ def test_residual_ln_fwd(ext, T0, with_scale):
     assert torch.allclose(mu, mur, atol=1e-6) and torch.allclose(rs, rsr, rtol=1e-5)
 
 
+@pytest.mark.parametrize("D", [512, 1024])
+def test_residual_ln_fwd_partial_rows(ext, D):
+    """R0 = 3 (the jumbo block's hand-off): rows t >= 3 get the residual into ``out``, rows t < 3 of
+    ``out`` are already final; the LayerNorm covers all rows == residual_fwd on the patch rows then
+    layernorm_fwd over the assembled tensor."""
+    torch.manual_seed(0)
+    B, T, C = 5, 52, 3
+    x = torch.randn(B, T, D, device="cuda")
+    y = torch.randn(B * (T - C), D, device="cuda").bfloat16()
+    s = torch.rand(D, device="cuda")
+    mask = (torch.rand(B, device="cuda") > 0.3).float() / 0.7
+    g, b = torch.rand(D, device="cuda") + 0.5, torch.randn(D, device="cuda")
+    out = torch.empty(B, T, D, device="cuda")
+    out[:, :C] = torch.randn(B, C, D, device="cuda")
+    cls = out[:, :C].clone()
+    x1, h, mu, rs = ext.residual_ln_fwd(x, y, s, mask, g, b, 1e-6, 0, C, out)
+    assert x1.data_ptr() == out.data_ptr() and torch.equal(out[:, :C], cls)
+    ref = torch.empty_like(out)
+    ref[:, :C] = cls
+    ref[:, C:] = ext.residual_fwd(x[:, C:], y, s, mask)
+    assert torch.equal(out, ref)
+    hr, mur, rsr = ext.layernorm_fwd(ref, g, b, 1e-6, torch.bfloat16)
+    assert (h.float() - hr.float()).abs().max().item() <= 0.0625
+    assert torch.allclose(mu, mur, atol=1e-6) and torch.allclose(rs, rsr, rtol=1e-5)
+
+
 @pytest.mark.parametrize("variant", [4, 6, 10, 11, 12])
 @pytest.mark.parametrize("M,N,K,S", [(512, 3072, 12288, 10), (300, 512, 4096, 3), (512, 256, 1024, 16)])
 def test_gemm_nt_splitk(ext, M, N, K, S, variant):

@@ -112,3 +112,38 @@ def test_fused_blocks_match_per_op_with_droppath(monkeypatch):
         res.append((loss.item(), m.store.grad.clone()))
     assert abs(res[0][0] - res[1][0]) < 1e-6
     assert torch.allclose(res[0][1], res[1][1], atol=1e-6, rtol=1e-4)
+
+
+def test_forward_links_fuse_upper_ln1(monkeypatch):
+    """Forward Link hand-off: each lower block computes the upper block's LN1 in its last residual
+    pass (ops/blocks.py Link.ln1) -- fewer standalone LayerNorms, identical loss and gradients."""
+    from jumbo_mae_tpu_amd.ops import blocks
+    from jumbo_mae_tpu_amd.utils.rng import RngStreams
+    vc = ViTConfig(layers=3, dim=32, heads=4, labels=0, image_size=32, patch_size=8, posemb="sincos2d",
+                   layerscale=True, droppath=0.2)
+    dc = DecoderConfig(dec_layers=3, dec_dim=16, dec_heads=2, image_size=32, patch_size=8, dec_layerscale=True)
+    imgs = torch.randint(0, 256, (4, 3, 32, 32), dtype=torch.uint8)
+    noise = torch.rand(16)
+    calls = {"hits": 0}
+    real = blocks.Link.take_h1
+
+    def counting(self, x):
+        out = real(self, x)
+        calls["hits"] += out is not None
+        return out
+
+    monkeypatch.setattr(blocks.Link, "take_h1", counting)
+    res = []
+    for fwd in (False, True):
+        monkeypatch.setattr(blocks, "FWD_LINKS", fwd)
+        calls["hits"] = 0
+        m = PretrainModel(vc, dc).to("cpu", seed=0)
+        with torch.no_grad():
+            m.store.master.add_(torch.linspace(-0.02, 0.02, m.store.total))
+        rng = RngStreams({"dropout": 5}, 0, "cpu").as_dict()
+        loss = m(imgs, rngs=rng, noise=noise)["loss"]
+        loss.backward()
+        res.append((loss.item(), m.store.grad.clone(), calls["hits"]))
+    assert (res[0][2], res[1][2]) == (0, 4)  # 2 encoder + 2 decoder upper-block LN1s handed over
+    assert abs(res[0][0] - res[1][0]) < 1e-6
+    assert torch.allclose(res[0][1], res[1][1], atol=1e-6, rtol=1e-4)

@@ -48,6 +48,9 @@ def apply(P, cfg: str):
         elif k == "ATTN_TR":
             from jumbo_mae_tpu_amd.ops import _ext
             _ext.load(True).attn_set_tr(int(v))
+        elif k == "JMAE_FWD_LINKS":
+            from jumbo_mae_tpu_amd.ops import blocks
+            blocks.FWD_LINKS = v == "1"
         elif k == "JMAE_LINK_BLOCKS":
             from jumbo_mae_tpu_amd.ops import blocks
             blocks.LINKS = v == "1"
