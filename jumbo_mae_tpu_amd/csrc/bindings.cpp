@@ -31,7 +31,8 @@ int jm_residual_ln_fwd(const float* x, long sB, long sT, const uint16_t* y, cons
                        float* x1, long oB, long oT, uint16_t* h, float* mean, float* rstd, int B, int T, int T0,
                        int D, const float* gamma, const float* beta, float eps, hipStream_t st, int R0 = 0);
 int jm_gelu_fwd(const uint16_t* h, uint16_t* a, long n, hipStream_t st);
-int jm_gelu_bwd(const uint16_t* h, const uint16_t* da, uint16_t* dh, float* bias_grad, int M, int N, hipStream_t st);
+int jm_gelu_bwd(const uint16_t* h, const uint16_t* da, uint16_t* dh, float* bias_grad, int M, int N, hipStream_t st,
+                int deriv = 0);
 int jm_colsum_bf16(const uint16_t* x, float* acc, int M, int N, hipStream_t st);
 int jm_splitk_reduce_add(const float* part, float* g, long n, int S, hipStream_t st);
 int jm_transpose_bf16(const uint16_t* src, uint16_t* dst, int R, int C, hipStream_t st);
@@ -219,7 +220,8 @@ torch::Tensor gelu_fwd(torch::Tensor h) {
   return a;
 }
 
-torch::Tensor gelu_bwd(torch::Tensor h, torch::Tensor da, c10::optional<torch::Tensor> bias_grad) {
+// deriv: h holds the saved gelu'(pre-activation) (EPI_GELU_D forward) -> dh = da * h
+torch::Tensor gelu_bwd(torch::Tensor h, torch::Tensor da, c10::optional<torch::Tensor> bias_grad, bool deriv) {
   CHECK_CONTIG(h);
   CHECK_CONTIG(da);
   CHECK_DT(h, torch::kBFloat16);
@@ -227,7 +229,7 @@ torch::Tensor gelu_bwd(torch::Tensor h, torch::Tensor da, c10::optional<torch::T
   const int N = h.size(-1);
   const int M = h.numel() / N;
   auto dh = torch::empty_like(h);
-  check_rc(jm_gelu_bwd(bf(h), bf(da), bfm(dh), fopt_m(bias_grad), M, N, stream()), "gelu_bwd");
+  check_rc(jm_gelu_bwd(bf(h), bf(da), bfm(dh), fopt_m(bias_grad), M, N, stream(), deriv ? 1 : 0), "gelu_bwd");
   return dh;
 }
 
@@ -565,8 +567,9 @@ int attach_tail(GemmEpi& ep, torch::Tensor& ws, int M, int N, int K, int epi, co
   return r;
 }
 
+// gelu_deriv (with gelu): returns {gelu'(h), gelu(h)} instead of {h, gelu(h)} (EPI_GELU_D)
 std::vector<torch::Tensor> gemm_nt(torch::Tensor A, torch::Tensor B, c10::optional<torch::Tensor> bias, bool gelu,
-                                   bool gelu_only) {
+                                   bool gelu_only, bool gelu_deriv) {
   CHECK_DT(A, torch::kBFloat16);
   CHECK_DT(B, torch::kBFloat16);
   TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && A.size(1) == B.size(1), "gemm_nt: A [M,K], B [N,K]");
@@ -583,7 +586,8 @@ std::vector<torch::Tensor> gemm_nt(torch::Tensor A, torch::Tensor B, c10::option
     out2 = torch::empty({M, N}, A.options());
     ep.out2 = bfm(out2);
   }
-  const int epi = gelu_only ? 4 : (gelu ? 1 : 0);
+  TORCH_CHECK(!gelu_deriv || (gelu && !gelu_only), "gemm_nt: gelu_deriv needs gelu and not gelu_only");
+  const int epi = gelu_only ? 4 : (gelu_deriv ? 6 : (gelu ? 1 : 0));
   torch::Tensor ws;
   attach_tail(ep, ws, M, N, K, epi, A);
   check_rc(jm_gemm_nt(bf(A), A.stride(0), bf(B), B.stride(0), M, N, K, epi, ep, stream()), "gemm_nt");
@@ -628,7 +632,9 @@ torch::Tensor gemm_nt_splitk(torch::Tensor A, torch::Tensor B, c10::optional<tor
 
 // dh[M, N] = (A[M, K] . B[N, K]^T) * gelu'(pre[M, N]) -- FF2 data gradient through the GELU,
 // B = W2^T; dbias (fp32 [N], optional) += column sums of dh (the FF1 bias gradient).
-torch::Tensor gemm_nt_dgelu(torch::Tensor A, torch::Tensor B, torch::Tensor pre, c10::optional<torch::Tensor> dbias) {
+// deriv: ``pre`` holds the saved gelu'(h) (EPI_GELU_D forward): the epilogue multiplies (EPI_DMUL)
+torch::Tensor gemm_nt_dgelu(torch::Tensor A, torch::Tensor B, torch::Tensor pre, c10::optional<torch::Tensor> dbias,
+                            bool deriv) {
   CHECK_DT(A, torch::kBFloat16);
   CHECK_DT(B, torch::kBFloat16);
   CHECK_DT(pre, torch::kBFloat16);
@@ -640,7 +646,8 @@ torch::Tensor gemm_nt_dgelu(torch::Tensor A, torch::Tensor B, torch::Tensor pre,
   torch::Tensor part;
   GemmEpi ep{nullptr, bfm(out), N, nullptr, bf(pre), nullptr, nullptr, 1};
   torch::Tensor ws;
-  const int r = attach_tail(ep, ws, M, N, K, 2, A);
+  const int epi = deriv ? 7 : 2;
+  const int r = attach_tail(ep, ws, M, N, K, epi, A);
   int nM = (M + 255) / 256;
   if (dbias) {
     TORCH_CHECK(dbias->is_contiguous() && dbias->scalar_type() == torch::kFloat32 && dbias->numel() == N,
@@ -652,7 +659,7 @@ torch::Tensor gemm_nt_dgelu(torch::Tensor A, torch::Tensor B, torch::Tensor pre,
     ep.colpart = part.data_ptr<float>();
     nM += 8 * r;
   }
-  check_rc(jm_gemm_nt(bf(A), A.stride(0), bf(B), B.stride(0), M, N, K, 2, ep, stream()), "gemm_nt_dgelu");
+  check_rc(jm_gemm_nt(bf(A), A.stride(0), bf(B), B.stride(0), M, N, K, epi, ep, stream()), "gemm_nt_dgelu");
   if (dbias) check_rc(jm_splitk_reduce_add(part.data_ptr<float>(), dbias->data_ptr<float>(), N, nM, stream()),
                       "gemm_nt_dgelu dbias");
   return out;
@@ -788,7 +795,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("res_mask") = py::none(), py::arg("res_dscale") = py::none(), py::arg("res_dbias") = py::none(),
         py::arg("res_T0") = 0, py::arg("res_out") = py::none());
   m.def("gelu_fwd", &gelu_fwd);
-  m.def("gelu_bwd", &gelu_bwd, py::arg("h"), py::arg("da"), py::arg("bias_grad") = py::none());
+  m.def("gelu_bwd", &gelu_bwd, py::arg("h"), py::arg("da"), py::arg("bias_grad") = py::none(),
+        py::arg("deriv") = false);
   m.def("colsum", &colsum);
   m.def("splitk_reduce_add", &splitk_reduce_add);
   m.def("residual_ln_fwd", &residual_ln_fwd, py::arg("x"), py::arg("y"), py::arg("scale"), py::arg("mask"),
@@ -809,9 +817,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_set_tail", &jm_gemm_set_tail);
   m.def("gemm_nt_splitk", &gemm_nt_splitk, py::arg("A"), py::arg("B"), py::arg("bias") = py::none(),
         py::arg("splits") = 8, py::arg("add") = py::none());
-  m.def("gemm_nt_dgelu", &gemm_nt_dgelu, py::arg("A"), py::arg("B"), py::arg("pre"), py::arg("dbias") = py::none());
+  m.def("gemm_nt_dgelu", &gemm_nt_dgelu, py::arg("A"), py::arg("B"), py::arg("pre"), py::arg("dbias") = py::none(),
+        py::arg("deriv") = false);
   m.def("gemm_nt", &gemm_nt, py::arg("A"), py::arg("B"), py::arg("bias") = py::none(), py::arg("gelu") = false,
-        py::arg("gelu_only") = false);
+        py::arg("gelu_only") = false, py::arg("gelu_deriv") = false);
   m.def("attn_set_tr", &jm_attn_set_tr);
   m.def("ln_set_bwd_la", &jm_ln_set_bwd_la);
   m.def("attn_set_fwd_hpw", &jm_attn_set_fwd_hpw);

@@ -40,17 +40,29 @@ template <> JM_DEVICE uint16_t from_f<uint16_t>(float v) { return f2bf(v); }
 // saturates correctly at +-inf, absolute error ~1e-7
 JM_DEVICE float jm_tanh(float u) { return 1.f - 2.f * __builtin_amdgcn_rcpf(1.f + __expf(2.f * u)); }
 
-// flax nn.gelu(approximate=True): 0.5 x (1 + tanh(sqrt(2/pi) (x + 0.044715 x^3)))
-JM_DEVICE float gelu_tanh_f(float x) {
-  const float u = 0.7978845608028654f * (x + 0.044715f * x * x * x);
-  return 0.5f * x * (1.f + jm_tanh(u));
+// flax nn.gelu(approximate=True): 0.5 x (1 + tanh(sqrt(2/pi) (x + 0.044715 x^3))).  With
+// p = 0.5 (1 + tanh u) = sigmoid(2u) = 1 / (1 + exp(-2u)) this is x * p -- one v_exp_f32 and one
+// reciprocal -- and the derivative is p + x p (1 - p) 2c (1 + 3a x^2); both saturate cleanly
+// (exp -> inf gives p = 0, exp -> 0 gives p = 1).
+JM_DEVICE float gelu_p_f(float x) {
+  const float m2u = x * (-1.5957691216057308f - 0.07135481627260025f * x * x);  // -2u
+  return __builtin_amdgcn_rcpf(1.f + __expf(m2u));
 }
+
+JM_DEVICE float gelu_tanh_f(float x) { return x * gelu_p_f(x); }
 
 // d/dx of gelu_tanh_f
 JM_DEVICE float gelu_grad_f(float x) {
-  const float c = 0.7978845608028654f, a = 0.044715f;
-  const float t = jm_tanh(c * (x + a * x * x * x));
-  return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * c * (1.f + 3.f * a * x * x);
+  const float p = gelu_p_f(x);
+  return __builtin_fmaf(x * p * (1.f - p), __builtin_fmaf(0.21406444881780076f, x * x, 1.5957691216057308f), p);
+}
+
+// gelu_tanh_f and its derivative sharing one exp / reciprocal (the forward epilogue that saves
+// gelu' for the backward instead of the pre-activation)
+JM_DEVICE void gelu_and_grad_f(float x, float& g, float& d) {
+  const float p = gelu_p_f(x);
+  g = x * p;
+  d = __builtin_fmaf(g * (1.f - p), __builtin_fmaf(0.21406444881780076f, x * x, 1.5957691216057308f), p);
 }
 
 // DPP lane moves (VALU, no LDS round trip like __shfl_xor's ds_bpermute)

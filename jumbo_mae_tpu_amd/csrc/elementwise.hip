@@ -54,6 +54,7 @@ JM_DEVICE ColPlan col_plan(int N) {
 
 // MODE 0: colsum(dy)          -> acc
 // MODE 1: gelu_bwd(h, da)     -> out (bf16), acc += colsum(out)
+// MODE 3: as MODE 1 with in0 = the saved gelu'(h) (a multiply instead of the derivative)
 // MODE 2: residual_bwd        -> out = m*s*dout (bf16, dout fp32), acc += colsum(m*dout*y),
 //                                acc2 += colsum(out)  (bias gradient of the Dense that produced y)
 template <int MODE>
@@ -105,7 +106,7 @@ __global__ __launch_bounds__(256) void rowcol_kernel(const void* __restrict__ in
             const long off = (long)r * N + col;
             if (MODE == 0) {
               load8((const uint16_t*)in0 + off, a[u]);
-            } else if (MODE == 1) {
+            } else if (MODE == 1 || MODE == 3) {
               load8((const uint16_t*)in0 + off, a[u]);
               load8(in1 + off, b[u]);
             } else {  // dout is a [B, T, D] view with strides (sB, sT, 1)
@@ -122,11 +123,11 @@ __global__ __launch_bounds__(256) void rowcol_kernel(const void* __restrict__ in
           if (MODE == 0) {
 #pragma unroll
             for (int j = 0; j < 8; ++j) s[j] += a[u][j];
-          } else if (MODE == 1) {
+          } else if (MODE == 1 || MODE == 3) {
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
               // round dh to bf16 first so the bias grad equals the colsum of what the GEMMs consume
-              b[u][j] = bf2f(f2bf(b[u][j] * gelu_grad(a[u][j])));
+              b[u][j] = bf2f(f2bf(b[u][j] * (MODE == 3 ? a[u][j] : gelu_grad(a[u][j]))));
               s[j] += b[u][j];
             }
             store8(out + off, b[u]);
@@ -231,9 +232,12 @@ int jm_gelu_fwd(const uint16_t* h, uint16_t* a, long n, hipStream_t st) {
 }
 
 int jm_gelu_bwd(const uint16_t* h, const uint16_t* da, uint16_t* dh, float* bias_grad, int M, int N,
-                hipStream_t st) {
+                hipStream_t st, int deriv) {
   if (N % 8) return -1;
-  launch_rowcol<1>(h, da, dh, bias_grad, nullptr, nullptr, M, N, 1, st);
+  if (deriv)
+    launch_rowcol<3>(h, da, dh, bias_grad, nullptr, nullptr, M, N, 1, st);
+  else
+    launch_rowcol<1>(h, da, dh, bias_grad, nullptr, nullptr, M, N, 1, st);
   return 0;
 }
 

@@ -73,7 +73,11 @@ struct Frags {
 // EPI_GELU_ONLY: out = gelu(bf16(acc + bias)) alone -- inference (no backward needs the
 // pre-activation), half the epilogue bytes of EPI_GELU.
 // EPI_TAIL: split-K partial tile of a tail-split launch, stored compact in ep.tail (see GemmEpi).
-enum { EPI_STORE = 0, EPI_GELU = 1, EPI_DGELU = 2, EPI_PARTIAL = 3, EPI_GELU_ONLY = 4, EPI_TAIL = 5 };
+// EPI_GELU_D: out = gelu'(h), out2 = gelu(h) for h = bf16(acc + bias): the FF1 forward saves the GELU
+// derivative for the backward instead of h (one shared tanh here, no tanh in the backward epilogue).
+// EPI_DMUL: out = bf16(acc) * aux with aux = the saved gelu'(h), + column partials as EPI_DGELU.
+enum { EPI_STORE = 0, EPI_GELU = 1, EPI_DGELU = 2, EPI_PARTIAL = 3, EPI_GELU_ONLY = 4, EPI_TAIL = 5, EPI_GELU_D = 6,
+       EPI_DMUL = 7 };
 
 namespace {
 
@@ -97,6 +101,14 @@ JM_DEVICE void epilogue(const f32x4_t (&acc)[8][NTW], const GemmEpi& ep, int M, 
       if (EPI == EPI_GELU_ONLY) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) v[i] = gelu_tanh_f(bf2f(f2bf(v[i])));
+      }
+      if (EPI == EPI_GELU_D) {
+        float gv[4], dv[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) gelu_and_grad_f(bf2f(f2bf(v[i])), gv[i], dv[i]);
+        store4(ep.out + (long)m * ep.ldo + n, dv);
+        store4(ep.out2 + (long)m * ep.ldo + n, gv);
+        continue;
       }
       store4(ep.out + (long)m * ep.ldo + n, v);
       if (EPI == EPI_GELU) {
@@ -207,16 +219,23 @@ JM_DEVICE void epilogue_lds(const f32x4_t (&acc)[8][NTW], const GemmEpi& ep, uin
     const int m = m0 + r;
     const uint4 v = *reinterpret_cast<const uint4*>(cs + r * RB + ((c ^ (r & 15)) << 3));
     if (m < M && col_ok) {
-      if (EPI == EPI_DGELU) {
+      if (EPI == EPI_DGELU || EPI == EPI_DMUL) {
         float f[8], hp[8];
         const uint16_t* dg = reinterpret_cast<const uint16_t*>(&v);
         load8(ep.aux + (long)m * ep.ldo + n0 + c * 8, hp);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          f[j] = bf2f(f2bf(bf2f(dg[j]) * gelu_grad_f(hp[j])));
+          f[j] = bf2f(f2bf(bf2f(dg[j]) * (EPI == EPI_DMUL ? hp[j] : gelu_grad_f(hp[j]))));
           csum[j] += f[j];
         }
         st16(ep.out + (long)m * ep.ldo + n0 + c * 8, pack8(f), NTS);
+      } else if (EPI == EPI_GELU_D) {
+        float fg[8], fd[8];
+        const uint16_t* h = reinterpret_cast<const uint16_t*>(&v);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) gelu_and_grad_f(bf2f(h[j]), fg[j], fd[j]);
+        st16(ep.out + (long)m * ep.ldo + n0 + c * 8, pack8(fd), NTS);
+        st16(ep.out2 + (long)m * ep.ldo + n0 + c * 8, pack8(fg), NTS);
       } else if (EPI == EPI_GELU_ONLY) {
         float f[8];
         const uint16_t* h = reinterpret_cast<const uint16_t*>(&v);
@@ -235,7 +254,7 @@ JM_DEVICE void epilogue_lds(const f32x4_t (&acc)[8][NTW], const GemmEpi& ep, uin
       }
     }
   }
-  if (EPI == EPI_DGELU && ep.colpart != nullptr) {
+  if ((EPI == EPI_DGELU || EPI == EPI_DMUL) && ep.colpart != nullptr) {
     // column sums of this row tile: RPP threads share a column chunk -> reduce through LDS
     float* red = reinterpret_cast<float*>(cs);
     __syncthreads();
@@ -1244,6 +1263,10 @@ int jm_gemm_nt(const uint16_t* A, long lda, const uint16_t* B, long ldb, int M, 
     launch_epi<EPI_GELU_ONLY>(A, lda, B, ldb, M, N, K, ep, nwg, st);
   else if (epi == EPI_DGELU && N % 8 == 0)
     launch_epi<EPI_DGELU>(A, lda, B, ldb, M, N, K, ep, nwg, st);
+  else if (epi == EPI_GELU_D)  // default kernel only (no A/B variants for the saved-derivative pair)
+    launch_nt64<EPI_GELU_D, 4>(A, lda, B, ldb, M, N, K, ep, nwg, st);
+  else if (epi == EPI_DMUL && N % 8 == 0)
+    launch_nt64<EPI_DMUL, 4>(A, lda, B, ldb, M, N, K, ep, nwg, st);
   else
     return -3;
   return 0;

@@ -91,14 +91,15 @@ def _attn_bwd(attn, da, h1, qkv, o, lse, B, S, wo_bias_done=False):
 
 
 def _ff_fwd(ff, h, train=True):
-    pre, g = P.linear_gelu_fwd(h, ff.w1.k, ff.w1.b, need_pre=train)
+    """(saved, gelu, y, deriv): ``saved`` is gelu'(pre) when ``deriv`` (fused MFMA forward), else pre."""
+    pre, g, deriv = P.linear_gelu_fwd_saved(h, ff.w1.k, ff.w1.b, need_pre=train)
     y = P.linear_fwd(g, ff.w2.k, ff.w2.b)
-    return pre, g, y
+    return pre, g, y, deriv
 
 
-def _ff_bwd(ff, dy, h, pre, g, w2_bias_done=False, dx_add=None):
+def _ff_bwd(ff, dy, h, pre, g, w2_bias_done=False, dx_add=None, deriv=False):
     hb1 = ff.w1.b if ff.w1.k.segs[0].trainable else None
-    dpre, bias_done = P.linear_gelu_bwd(dy, g, pre, ff.w2.k, ff.w2.b, hb1, w2_bias_done)
+    dpre, bias_done = P.linear_gelu_bwd(dy, g, pre, ff.w2.k, ff.w2.b, hb1, w2_bias_done, deriv)
     return P.linear_bwd(dpre, h, ff.w1.k, ff.w1.b, bias_done=bias_done, dx_add=dx_add)
 
 
@@ -131,10 +132,10 @@ class JumboBlockFn(torch.autograd.Function):
         cls_in = x1[:, :C].reshape(B, 1, J)
         # fp32 hc for the residual and its compute-dtype copy for the jumbo MLP, one pass
         hc, muc, rsc, hcb = P.ln_fwd(cls_in, layer.norm3.g, layer.norm3.b, torch.float32, dt)
-        jpre, jg, jy = _ff_fwd(layer.jumbo_mlp, hcb, train)
+        jpre, jg, jy, jd = _ff_fwd(layer.jumbo_mlp, hcb, train)
         # patch branch
         pin = x1[:, C:]
-        fpre, fg, fy = _ff_fwd(layer.ff, hp, train)
+        fpre, fg, fy, fd = _ff_fwd(layer.ff, hp, train)
         x2 = torch.empty_like(x1)
         P.residual_fwd(hc.view(B, 1, J), jy, layer.scale3, m3, out=x2[:, :C].reshape(B, 1, J))
         nl = link_out.ln1 if link_out is not None else None
@@ -147,6 +148,7 @@ class JumboBlockFn(torch.autograd.Function):
                               hp, mup, rsp, fpre, fg, fy, m1, m2, m3)
         ctx.layer = layer
         ctx.link_in, ctx.link_out = link_in, link_out
+        ctx.gelu_deriv = (jd, fd)  # FF1 saved gelu'(h) instead of h (jumbo MLP, patch FF)
         if link_out is not None:
             link_out.spec = P.ResSpec(fy, layer.scale2, m2, layer.ff.w2.b, C)
         return x2
@@ -169,7 +171,8 @@ class JumboBlockFn(torch.autograd.Function):
         dcls = dx2[:, :C].reshape(B, 1, J)
         djy, bd = P.residual_bwd(dcls, jy, layer.scale3, m3, dt, layer.jumbo_mlp.w2.b)
         # d hc = dcls + JumboMLP'(...) in fp32, the add fused into the jumbo dgrad's split-K reduce
-        dhc = _ff_bwd(layer.jumbo_mlp, djy, hcb, jpre, jg, bd, dx_add=dcls.reshape(B, J))
+        dhc = _ff_bwd(layer.jumbo_mlp, djy, hcb, jpre, jg, bd, dx_add=dcls.reshape(B, J),
+                      deriv=ctx.gelu_deriv[0])
         P.ln_bwd(dhc, x1[:, :C].reshape(B, 1, J), muc, rsc, layer.norm3.g, layer.norm3.b,
                  out=dx1[:, :C].reshape(B, 1, J))
         # attention-residual backward of the CLS rows (the patch rows ride on LN2' below, which
@@ -182,7 +185,7 @@ class JumboBlockFn(torch.autograd.Function):
             dfy, bd = fused
         else:
             dfy, bd = P.residual_bwd(dx2[:, C:], fy, layer.scale2, m2, dt, layer.ff.w2.b)
-        dhp = _ff_bwd(layer.ff, dfy, hp, fpre, fg, bd)
+        dhp = _ff_bwd(layer.ff, dfy, hp, fpre, fg, bd, deriv=ctx.gelu_deriv[1])
         # ... and the attention-residual backward of those rows in the same pass
         _, _, bd = P.ln_bwd(dhp, x1[:, C:], mup, rsp, layer.norm2.g, layer.norm2.b, dres=dx2[:, C:],
                             out=dx1[:, C:],
@@ -229,7 +232,7 @@ class ViTBlockFn(torch.autograd.Function):
         h1, mu1, rs1 = _ln1_fwd(x, layer, link_in, dt)
         qkv, o, lse, a = _attn_fwd(layer.attn, h1, B, S)
         x1, h2, mu2, rs2 = P.residual_ln_fwd(x, a, layer.scale1, m1, layer.norm2.g, layer.norm2.b, 0)
-        fpre, fg, fy = _ff_fwd(layer.ff, h2, train)
+        fpre, fg, fy, fd = _ff_fwd(layer.ff, h2, train)
         nl = link_out.ln1 if link_out is not None else None
         if nl is not None:  # last residual + the upper block's LN1, one pass
             x2, h1n, mun, rsn = P.residual_ln_fwd(x1, fy, layer.scale2, m2, nl[0], nl[1], 0)
@@ -239,6 +242,7 @@ class ViTBlockFn(torch.autograd.Function):
         ctx.save_for_backward(x, mu1, rs1, h1, qkv, o, lse, a, x1, mu2, rs2, h2, fpre, fg, fy, m1, m2)
         ctx.layer = layer
         ctx.link_in, ctx.link_out = link_in, link_out
+        ctx.gelu_deriv = (False, fd)
         if link_out is not None:
             link_out.spec = P.ResSpec(fy, layer.scale2, m2, layer.ff.w2.b, 0)
         return x2
@@ -255,7 +259,7 @@ class ViTBlockFn(torch.autograd.Function):
             dfy, bd = fused
         else:
             dfy, bd = P.residual_bwd(dx2, fy, layer.scale2, m2, dt, layer.ff.w2.b)
-        dh2 = _ff_bwd(layer.ff, dfy, h2, fpre, fg, bd)
+        dh2 = _ff_bwd(layer.ff, dfy, h2, fpre, fg, bd, deriv=ctx.gelu_deriv[1])
         # LN2' with the attention-residual backward of its dx fused in (never write autograd's dx2)
         dx1, da, bd = P.ln_bwd(dh2, x1, mu2, rs2, layer.norm2.g, layer.norm2.b, dres=dx2,
                                res=P.ResSpec(a, layer.scale1, m1, layer.attn.wo_b))

@@ -164,6 +164,24 @@ def linear_gelu_fwd(x2: torch.Tensor, hw: Handle, hb: Handle | None, need_pre: b
     return pre, gelu_fwd(pre)
 
 
+# save gelu'(h) instead of h for the backward when the fused MFMA forward runs (A/B switch)
+_GELU_DERIV = os.environ.get("JMAE_GELU_DERIV", "1") == "1"
+
+
+def linear_gelu_fwd_saved(x2: torch.Tensor, hw: Handle, hb: Handle | None, need_pre: bool = True):
+    """Like ``linear_gelu_fwd`` but returns (saved, gelu(h), deriv): on the fused MFMA path the
+    epilogue computes gelu(h) and gelu'(h) from one tanh and ``saved`` is gelu'(h) (deriv True),
+    so the backward's data-gradient epilogue multiplies instead of re-deriving it from h;
+    otherwise ``saved`` is h (deriv False)."""
+    w = hw.weight()
+    if (_GELU_DERIV and need_pre and hip(x2) and x2.dtype == torch.bfloat16
+            and use_our_gemm(x2.shape[0], w.shape[0], x2.shape[1], True)):
+        gp, g = _ext.load().gemm_nt(x2, w, hb.master if hb is not None else None, True, False, True)
+        return gp, g, True
+    pre, g = linear_gelu_fwd(x2, hw, hb, need_pre)
+    return pre, g, False
+
+
 # ------------------------------------------------------------------ weight-gradient stream
 # The weight-gradient GEMMs are off the backward critical path (nothing in the backward reads
 # them), so they run on a second HIP stream: hipBLASLt's 4-wave, <=256-VGPR workgroups leave
@@ -332,22 +350,23 @@ def linear_bwd(dy: torch.Tensor, x2: torch.Tensor, hw: Handle, hb: Handle | None
 
 
 def linear_gelu_bwd(dy: torch.Tensor, g: torch.Tensor, pre: torch.Tensor, hw2: Handle, hb2: Handle | None,
-                    hb1: Handle | None, bias2_done: bool = False):
+                    hb1: Handle | None, bias2_done: bool = False, deriv: bool = False):
     """Backward of ``y = Dense2(gelu(pre))`` down to d pre: returns (dpre, bias1_done).
 
     Fused path: one MFMA GEMM dy . W2 whose epilogue multiplies by gelu'(pre) and emits the
     column sums of dpre (= the gradient of Dense1's bias ``hb1``), so the GEMM output dg never
-    makes an HBM round trip.  W2's own gradients (wgrad, bias) are queued as usual."""
+    makes an HBM round trip.  W2's own gradients (wgrad, bias) are queued as usual.  ``deriv``:
+    ``pre`` is the saved gelu'(h) (``linear_gelu_fwd_saved``), not h."""
     w2 = hw2.weight()
     M, N, K = dy.shape[0], w2.shape[1], w2.shape[0]
     if (_DGRAD_OURS and hip(dy) and dy.dtype == torch.bfloat16 and N % 8 == 0
             and use_our_gemm(M, N, K, fused_gelu=True, kind="dgrad")):
         bg = hb1.grad if _trainable(hb1) else None
-        dpre = _ext.load().gemm_nt_dgelu(dy.contiguous(), hw2.weight_t(), pre.contiguous(), bg)
+        dpre = _ext.load().gemm_nt_dgelu(dy.contiguous(), hw2.weight_t(), pre.contiguous(), bg, deriv)
         linear_bwd(dy, g, hw2, hb2, need_dx=False, bias_done=bias2_done)
         return dpre, bg is not None
     dg = linear_bwd(dy, g, hw2, hb2, bias_done=bias2_done)
-    return gelu_bwd(pre, dg, hb1)
+    return gelu_bwd(pre, dg, hb1, deriv)
 
 
 # ------------------------------------------------------------------------------ gelu
@@ -357,12 +376,15 @@ def gelu_fwd(h: torch.Tensor) -> torch.Tensor:
     return F.gelu(h, approximate="tanh")
 
 
-def gelu_bwd(h: torch.Tensor, da: torch.Tensor, hb: Handle | None = None) -> tuple[torch.Tensor, bool]:
-    """dh = da * gelu'(h); when ``hb`` is given its bias gradient (colsum dh) is fused in.
-    Returns (dh, bias_done)."""
+def gelu_bwd(h: torch.Tensor, da: torch.Tensor, hb: Handle | None = None,
+             deriv: bool = False) -> tuple[torch.Tensor, bool]:
+    """dh = da * gelu'(h) (``deriv``: h already holds gelu'); when ``hb`` is given its bias gradient
+    (colsum dh) is fused in.  Returns (dh, bias_done)."""
     if hip(h):
         bg = hb.grad if _trainable(hb) else None
-        return _ext.load().gelu_bwd(h, da.contiguous(), bg), bg is not None
+        return _ext.load().gelu_bwd(h, da.contiguous(), bg, deriv), bg is not None
+    if deriv:
+        return (da.float() * h.float()).to(h.dtype), False
     hf = h.float()
     u = _GELU_C * (hf + 0.044715 * hf ** 3)
     t = torch.tanh(u)

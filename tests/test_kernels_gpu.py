@@ -445,3 +445,31 @@ def test_gemm_splitk_fused_fp32_add(ext):
     assert rel(out_b, ref + bias + add) < 2e-3
     # bf16 path unchanged
     assert rel(ext.gemm_nt_splitk(A, B, None, 10), ref) < 1e-2
+
+
+@pytest.mark.parametrize("M,N,K", [(1000, 512, 256), (600, 1000, 128)])
+def test_gemm_gelu_saved_derivative(ext, M, N, K):
+    """FF1 forward saving gelu'(h) (EPI_GELU_D) and the FF2 data gradient multiplying by it
+    (EPI_DMUL) == the h-saving pair (EPI_GELU / EPI_DGELU); the unfused gelu_bwd(deriv) too."""
+    torch.manual_seed(0)
+    x = (torch.randn(M, K, device="cuda") * 0.5).bfloat16()
+    w = (torch.randn(N, K, device="cuda") * 0.1).bfloat16()
+    b = torch.randn(N, device="cuda") * 0.1
+    h, g = ext.gemm_nt(x, w, b, True)
+    gp, g2 = ext.gemm_nt(x, w, b, True, False, True)
+    assert torch.equal(g, g2)
+    hf = h.float()
+    t = torch.tanh(0.7978845608028654 * (hf + 0.044715 * hf ** 3))
+    dref = 0.5 * (1 + t) + 0.5 * hf * (1 - t * t) * 0.7978845608028654 * (1 + 3 * 0.044715 * hf * hf)
+    assert (gp.float() - dref).abs().max().item() < 1e-2
+    dy = (torch.randn(M, 384, device="cuda") * 0.5).bfloat16()
+    w2t = (torch.randn(N, 384, device="cuda") * 0.05).bfloat16()
+    db1, db2 = torch.zeros(N, device="cuda"), torch.zeros(N, device="cuda")
+    d1 = ext.gemm_nt_dgelu(dy, w2t, h, db1)
+    d2 = ext.gemm_nt_dgelu(dy, w2t, gp, db2, True)
+    assert rel(d2, d1) < 1e-2 and rel(db2, db1) < 1e-2
+    da = (torch.randn(M, N, device="cuda")).bfloat16()
+    bg1, bg2 = torch.zeros(N, device="cuda"), torch.zeros(N, device="cuda")
+    e1 = ext.gelu_bwd(h, da, bg1)
+    e2 = ext.gelu_bwd(gp, da, bg2, True)
+    assert rel(e2, e1) < 1e-2 and rel(bg2, bg1) < 1e-2

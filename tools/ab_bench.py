@@ -48,6 +48,8 @@ def apply(P, cfg: str):
         elif k == "ATTN_TR":
             from jumbo_mae_tpu_amd.ops import _ext
             _ext.load(True).attn_set_tr(int(v))
+        elif k == "JMAE_GELU_DERIV":
+            P._GELU_DERIV = v == "1"
         elif k == "JMAE_FWD_LINKS":
             from jumbo_mae_tpu_amd.ops import blocks
             blocks.FWD_LINKS = v == "1"
