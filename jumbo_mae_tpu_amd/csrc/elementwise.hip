@@ -14,19 +14,9 @@
 
 namespace {
 
-constexpr float GELU_C = 0.7978845608028654f;  // sqrt(2/pi)
-constexpr float GELU_A = 0.044715f;
-
-JM_DEVICE float gelu_f(float h) {
-  const float u = GELU_C * (h + GELU_A * h * h * h);
-  return 0.5f * h * (1.f + jm_tanh(u));
-}
-
-JM_DEVICE float gelu_grad(float h) {
-  const float u = GELU_C * (h + GELU_A * h * h * h);
-  const float t = jm_tanh(u);
-  return 0.5f * (1.f + t) + 0.5f * h * (1.f - t * t) * GELU_C * (1.f + 3.f * GELU_A * h * h);
-}
+// one GELU implementation for every kernel (common.h, sigmoid form)
+JM_DEVICE float gelu_f(float h) { return gelu_tanh_f(h); }
+JM_DEVICE float gelu_grad(float h) { return gelu_grad_f(h); }
 
 __global__ __launch_bounds__(256) void gelu_fwd_kernel(const uint16_t* __restrict__ h, uint16_t* __restrict__ a,
                                                        long n8) {
