@@ -71,6 +71,8 @@ int jm_gemm_nt_tail_plan(int M, int N, int K, int epi, int* tail_r, long* ws_flo
 int jm_gemm_tn_plan(int M, int N, int K, int* S_out);
 int jm_gemm_tn(const uint16_t* A, long lda, const uint16_t* B, long ldb, int M, int N, int K, int sps, int S,
                float* G, long ldo, float* partial, hipStream_t st);
+int jm_gemm_tn_acc0();
+void jm_gemm_tn_set_acc0(int v);
 struct TnSegs {
   const uint16_t* a[32];
   const uint16_t* b[32];
@@ -688,11 +690,12 @@ int64_t gemm_tn_wgrad(torch::Tensor dy, torch::Tensor x, torch::Tensor g) {
   int S = 1;
   const int sps = jm_gemm_tn_plan(M, N, K, &S);
   torch::Tensor part;
-  if (S > 1) part = torch::empty({S, (long)N * K}, g.options());
+  const int SP = S - jm_gemm_tn_acc0();  // partial slices (split 0 may accumulate into g directly)
+  if (S > 1) part = torch::empty({SP, (long)N * K}, g.options());
   check_rc(jm_gemm_tn(bf(dy), dy.stride(0), bf(x), x.stride(0), M, N, K, sps, S, g.data_ptr<float>(), K,
                       S > 1 ? part.data_ptr<float>() : nullptr, stream()),
            "gemm_tn_wgrad");
-  if (S > 1) check_rc(jm_splitk_reduce_add(part.data_ptr<float>(), g.data_ptr<float>(), (long)N * K, S, stream()),
+  if (S > 1) check_rc(jm_splitk_reduce_add(part.data_ptr<float>(), g.data_ptr<float>(), (long)N * K, SP, stream()),
                       "gemm_tn_wgrad reduce");
   return S;
 }
@@ -724,11 +727,12 @@ int64_t gemm_tn_wgrad_seg(std::vector<torch::Tensor> dys, std::vector<torch::Ten
   int S = 1;
   const int sps = jm_gemm_tn_plan(M, N, K, &S);
   torch::Tensor part;
-  if (S > 1) part = torch::empty({S, (long)N * K}, g.options());
+  const int SP = S - jm_gemm_tn_acc0();
+  if (S > 1) part = torch::empty({SP, (long)N * K}, g.options());
   check_rc(jm_gemm_tn_seg(segs, d0.stride(0), x0.stride(0), N, K, sps, S, g.data_ptr<float>(), K,
                           S > 1 ? part.data_ptr<float>() : nullptr, stream()),
            "gemm_tn_wgrad_seg");
-  if (S > 1) check_rc(jm_splitk_reduce_add(part.data_ptr<float>(), g.data_ptr<float>(), (long)N * K, S, stream()),
+  if (S > 1) check_rc(jm_splitk_reduce_add(part.data_ptr<float>(), g.data_ptr<float>(), (long)N * K, SP, stream()),
                       "gemm_tn_wgrad_seg reduce");
   return S;
 }
@@ -815,6 +819,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_tn_wgrad_seg", &gemm_tn_wgrad_seg);
   m.def("gemm_set_variant", &jm_gemm_set_variant, py::arg("wn"), py::arg("group") = 8);
   m.def("gemm_set_tail", &jm_gemm_set_tail);
+  m.def("gemm_tn_set_acc0", &jm_gemm_tn_set_acc0);
   m.def("gemm_nt_splitk", &gemm_nt_splitk, py::arg("A"), py::arg("B"), py::arg("bias") = py::none(),
         py::arg("splits") = 8, py::arg("add") = py::none());
   m.def("gemm_nt_dgelu", &gemm_nt_dgelu, py::arg("A"), py::arg("B"), py::arg("pre"), py::arg("dbias") = py::none(),

@@ -85,11 +85,15 @@ struct TnSegs {
 
 namespace {
 
-template <int ACC, bool SEG = false>  // ACC = 1: G += tile (S == 1), 0: store the fp32 partial tile
+// ACC = 1: G += tile (S == 1), 0: store the fp32 partial tile.  With ACC = 0 and g0 set, split 0
+// adds its tile straight into G (g0, ldg0) and split s >= 1 stores partial slice s - 1: the
+// reduction then reads S - 1 slices, and one slice is never written nor read back.
+template <int ACC, bool SEG = false>
 __global__ __launch_bounds__(NTH, 1) void gemm_tn_kernel(const uint16_t* __restrict__ A, long lda,
                                                          const uint16_t* __restrict__ B, long ldb, int M, int N,
                                                          int K, int steps_per_split, float* __restrict__ out,
-                                                         long ldo, long split_stride, TnSegs segs = {}) {
+                                                         long ldo, long split_stride, TnSegs segs = {},
+                                                         float* __restrict__ g0 = nullptr, long ldg0 = 0) {
   JM_DGUARD(blockDim.x == NTH && steps_per_split >= 1 && M > 0);
   extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
   const int tid = threadIdx.x;
@@ -228,15 +232,17 @@ __global__ __launch_bounds__(NTH, 1) void gemm_tn_kernel(const uint16_t* __restr
   step(K0{}, t + 1, f1, f0);
 
   // ---- epilogue: acc[mt][nt][i] = G[n0 + wr*128 + mt*16 + l16][k0 + wc*64 + nt*16 + 4g + i]
-  float* dst = out + (ACC ? 0 : (long)split * split_stride);
+  const bool to_g = !ACC && g0 != nullptr && split == 0;  // workgroup-uniform
+  float* dst = ACC ? out : to_g ? g0 : out + (long)(g0 != nullptr ? split - 1 : split) * split_stride;
+  const long ld = to_g ? ldg0 : ldo;
 #pragma unroll
   for (int mt = 0; mt < 8; ++mt) {
     const int n = n0 + wr * 128 + mt * 16 + l16;
-    float* row = dst + (long)n * ldo + k0 + wc * 64 + 4 * g;
+    float* row = dst + (long)n * ld + k0 + wc * 64 + 4 * g;
 #pragma unroll
     for (int nt = 0; nt < 4; ++nt) {
       float v[4] = {acc[mt][nt][0], acc[mt][nt][1], acc[mt][nt][2], acc[mt][nt][3]};
-      if (ACC) {
+      if (ACC || to_g) {
         float o[4];
         load4(row + nt * 16, o);
 #pragma unroll
@@ -280,6 +286,14 @@ int jm_gemm_tn_plan(int M, int N, int K, int* S_out) {
 }
 
 // G[N][K] (ldo) += A[M][N]^T . B[M][K]; partial: [S][N][K] fp32 workspace when S > 1 (else null)
+// split 0 accumulates into G (partial then holds S - 1 slices).  A/B switch, off: the in-kernel
+// read-modify-write of G exposes a load latency in every split-0 epilogue and measured slower than
+// writing the extra slice (ViT-L step 97.80 -> 98.76 ms, profiles/r1_ab_tn_acc0.txt)
+int g_tn_acc0 = 0;
+int jm_gemm_tn_acc0() { return g_tn_acc0; }
+void jm_gemm_tn_set_acc0(int v) { g_tn_acc0 = v; }
+
+// partial: [S][N][K] fp32 (or [S - 1][N][K] when jm_gemm_tn_acc0())
 int jm_gemm_tn(const uint16_t* A, long lda, const uint16_t* B, long ldb, int M, int N, int K, int sps, int S,
                float* G, long ldo, float* partial, hipStream_t st) {
   if (N % TN_ || K % TK_ || M <= 0) return -1;
@@ -300,7 +314,8 @@ int jm_gemm_tn(const uint16_t* A, long lda, const uint16_t* B, long ldb, int M, 
       (void)hipFuncSetAttribute((const void*)gemm_tn_kernel<0>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
       attr = true;
     }
-    gemm_tn_kernel<0><<<tiles * S, NTH, sm, st>>>(A, lda, B, ldb, M, N, K, sps, partial, K, (long)N * K);
+    gemm_tn_kernel<0><<<tiles * S, NTH, sm, st>>>(A, lda, B, ldb, M, N, K, sps, partial, K, (long)N * K, TnSegs{},
+                                                  g_tn_acc0 ? G : nullptr, ldo);
   }
   return 0;
 }
@@ -330,7 +345,7 @@ int jm_gemm_tn_seg(const TnSegs& segs, long lda, long ldb, int N, int K, int sps
       attr = true;
     }
     gemm_tn_kernel<0, true><<<tiles * S, NTH, sm, st>>>(nullptr, lda, nullptr, ldb, M, N, K, sps, partial, K,
-                                                        (long)N * K, segs);
+                                                        (long)N * K, segs, g_tn_acc0 ? G : nullptr, ldo);
   }
   return 0;
 }

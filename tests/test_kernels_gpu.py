@@ -21,6 +21,7 @@ def _reset_gemm_variant(request):
         request.getfixturevalue("ext").gemm_set_variant(12, 8)
         request.getfixturevalue("ext").ln_set_bwd_la(2)
         request.getfixturevalue("ext").attn_set_bwd_ppw(0)
+        request.getfixturevalue("ext").gemm_tn_set_acc0(0)
 
 
 def rel(a, b):
@@ -265,16 +266,20 @@ def test_transpose_bf16(ext, R, C):
     assert torch.equal(y, x.t())
 
 
+@pytest.mark.parametrize("acc0", [1, 0])
 @pytest.mark.parametrize("M,N,K", [(4096, 256, 512), (3000, 512, 256), (512, 768, 1024), (26624, 1024, 256)])
-def test_gemm_tn_wgrad(ext, M, N, K):
-    """Weight-gradient TN MFMA GEMM (csrc/gemm_tn.hip): G += dy^T x, split over M, ragged M."""
+def test_gemm_tn_wgrad(ext, M, N, K, acc0):
+    """Weight-gradient TN MFMA GEMM (csrc/gemm_tn.hip): G += dy^T x, split over M, ragged M; acc0:
+    split 0 accumulates straight into G (S - 1 partial slices) or every split stores a partial."""
+    ext.gemm_tn_set_acc0(acc0)
     torch.manual_seed(0)
     dy = (torch.rand(M, N, device="cuda") * 2 - 1).bfloat16()
     x = (torch.rand(M, K, device="cuda") * 2 - 1).bfloat16()
     g = torch.randn(N, K, device="cuda")
     ref = g.double() + dy.double().t() @ x.double()
     S = ext.gemm_tn_wgrad(dy, x, g)
-    assert S >= 1
+    ext.gemm_tn_set_acc0(0)
+    assert S >= 1 and (S > 1 or M < 8192)
     assert rel(g, ref) < 1e-4
 
 
