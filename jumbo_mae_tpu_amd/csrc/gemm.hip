@@ -192,6 +192,28 @@ JM_DEVICE void epilogue_lds(const f32x4_t (&acc)[8][NTW], const GemmEpi& ep, uin
                             int n0, int wr, int wc, int l16, int g) {
   constexpr int RB = BNT;  // elements per LDS image row
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  constexpr int LPR = BNT / 8;        // lanes per row (16 B each)
+  constexpr int RPP = NTH / LPR;      // rows per pass
+  const int tid = threadIdx.x;
+  const int c = tid % LPR;
+  const bool col_ok = n0 + c * 8 < N;
+  // EPI_DGELU / EPI_DMUL: the first PF of this thread's aux rows are loaded before the accumulators
+  // are staged through LDS (their latency hides behind the staging) and each row pass then issues
+  // the load PF passes ahead -- a register ring instead of one exposed load per pass
+  constexpr bool PRE = EPI == EPI_DGELU || EPI == EPI_DMUL;
+  constexpr int NPASS = PRE ? BM / RPP : 1;
+  constexpr int PF = NPASS < 8 ? NPASS : 8;
+  uint4 auxv[PF];
+  auto aux_load = [&](int i) {
+    const int m = m0 + tid / LPR + i * RPP;
+    uint4 a = make_uint4(0, 0, 0, 0);
+    if (m < M && col_ok) a = *reinterpret_cast<const uint4*>(ep.aux + (long)m * ep.ldo + n0 + c * 8);
+    return a;
+  };
+  if constexpr (PRE) {
+#pragma unroll
+    for (int i = 0; i < PF; ++i) auxv[i] = aux_load(i);
+  }
 #pragma unroll
   for (int nt = 0; nt < NTW; ++nt) {
     const int nl = wc * NTW * 16 + nt * 16 + 4 * g;  // tile-local column
@@ -208,21 +230,18 @@ JM_DEVICE void epilogue_lds(const f32x4_t (&acc)[8][NTW], const GemmEpi& ep, uin
     }
   }
   __syncthreads();
-  constexpr int LPR = BNT / 8;        // lanes per row (16 B each)
-  constexpr int RPP = NTH / LPR;      // rows per pass
-  const int tid = threadIdx.x;
-  const int c = tid % LPR;
-  const bool col_ok = n0 + c * 8 < N;
   float csum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-#pragma unroll 4
-  for (int r = tid / LPR; r < BM; r += RPP) {
+  // one row pass: row r of the tile; av = the prefetched aux row (PRE epilogues)
+  auto pass = [&](int r, const uint4& av) {
     const int m = m0 + r;
     const uint4 v = *reinterpret_cast<const uint4*>(cs + r * RB + ((c ^ (r & 15)) << 3));
     if (m < M && col_ok) {
       if (EPI == EPI_DGELU || EPI == EPI_DMUL) {
         float f[8], hp[8];
         const uint16_t* dg = reinterpret_cast<const uint16_t*>(&v);
-        load8(ep.aux + (long)m * ep.ldo + n0 + c * 8, hp);
+        const uint16_t* ah = reinterpret_cast<const uint16_t*>(&av);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) hp[j] = bf2f(ah[j]);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           f[j] = bf2f(f2bf(bf2f(dg[j]) * (EPI == EPI_DMUL ? hp[j] : gelu_grad_f(hp[j]))));
@@ -253,6 +272,16 @@ JM_DEVICE void epilogue_lds(const f32x4_t (&acc)[8][NTW], const GemmEpi& ep, uin
         st16(ep.out2 + (long)m * ep.ldo + n0 + c * 8, pack8(f), NTS);
       }
     }
+  };
+  if constexpr (PRE) {
+#pragma unroll
+    for (int i = 0; i < NPASS; ++i) {
+      pass(tid / LPR + i * RPP, auxv[i % PF]);
+      if (i + PF < NPASS) auxv[i % PF] = aux_load(i + PF);
+    }
+  } else {
+#pragma unroll 4
+    for (int r = tid / LPR; r < BM; r += RPP) pass(r, auxv[0]);
   }
   if ((EPI == EPI_DGELU || EPI == EPI_DMUL) && ep.colpart != nullptr) {
     // column sums of this row tile: RPP threads share a column chunk -> reduce through LDS
