@@ -33,8 +33,11 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--variant", type=int, default=0, help="NT GEMM variant (ext.gemm_set_variant), 0 = default")
     a = ap.parse_args()
     ext = _ext.load()
+    if a.variant:
+        ext.gemm_set_variant(a.variant, 8)
     for name, (M, N, K) in SHAPES.items():
         x = (torch.randn(M, K, device="cuda") * 0.5).bfloat16()
         w1 = (torch.randn(N, K, device="cuda") * 0.03).bfloat16()
