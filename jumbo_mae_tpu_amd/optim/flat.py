@@ -83,6 +83,9 @@ class FlatOptimizer:
         self.gnorm_sq = torch.zeros(1, dtype=torch.float32, device=dev)
         self._tmp = None
         self._torch_meta = None
+        self._ranges = None      # (lo, hi) -> chunk-table rows (split updates, plan_ranges)
+        self._rest = None        # chunk-table rows outside every planned range
+        self._gn_ready = False   # gnorm_sq flag written for this step (split updates)
 
     # ---------------------------------------------------------------- helpers
     def _elem_meta(self):
@@ -133,6 +136,59 @@ class FlatOptimizer:
         else:
             self._step_torch(*self._cur)
 
+    # Split updates: the elementwise optimizers (AdamW, SGD without global-norm clipping) update
+    # each data-parallel bucket as soon as its all-reduce has completed (GradReducer.finish
+    # callback), so the update of the early buckets overlaps the reduction of the last ones.
+    def can_split(self) -> bool:
+        return self.kind in ("adamw", "sgd") and self.clip_grad <= 0
+
+    def plan_ranges(self, ranges: list[tuple[int, int]]) -> None:
+        starts = self.chunks[:, 0].long().cpu()
+        covered = torch.zeros(len(starts), dtype=torch.bool)
+        self._ranges = {}
+        for lo, hi in ranges:
+            m = (starts >= lo) & (starts < hi)
+            covered |= m
+            self._ranges[(lo, hi)] = self._rows(m)
+        self._rest = self._rows(~covered)
+
+    def _rows(self, mask: torch.Tensor):
+        idx = torch.nonzero(mask).flatten()
+        if idx.numel() == 0:
+            return None
+        if int(idx[-1]) - int(idx[0]) + 1 == idx.numel():  # contiguous rows: a view
+            return self.chunks[int(idx[0]):int(idx[-1]) + 1]
+        return self.chunks.index_select(0, idx.to(self.chunks.device))
+
+    def launch_range(self, lo: int, hi: int) -> None:
+        """Update the parameters of flat range [lo, hi) (a planned bucket)."""
+        rows = self._ranges[(lo, hi)]
+        if rows is not None:
+            self._launch_rows(rows, lo, hi)
+
+    def launch_rest(self) -> None:
+        """Update everything no planned range covers; ends a split step."""
+        if self._rest is not None:
+            self._launch_rows(self._rest, None, None)
+        self._gn_ready = False
+
+    def _launch_rows(self, rows, lo, hi) -> None:
+        s = self.store
+        if s.master.is_cuda and _ext.use_hip(s.master):
+            ext = _ext.load()
+            if not self._gn_ready:
+                self.gnorm_sq.fill_(-1.0)  # no clipping on the split path
+                self._gn_ready = True
+            shadow = s.shadow if s.shadow is not s.master else None
+            if self.kind == "adamw":
+                ext.opt_adamw(s.master, s.grad, self.mu, self.nu, shadow, rows, self.meta, self.hyper, self.gnorm_sq)
+            else:
+                ext.opt_sgd(s.master, s.grad, self.trace, shadow, rows, self.meta, self.hyper, self.gnorm_sq,
+                            self.momentum)
+        else:
+            for r0, n, _ in rows.tolist():
+                self._step_torch(*self._cur, lo=r0, hi=r0 + n)
+
     def finish(self) -> float:
         lr = self._cur[0]
         self.count += 1
@@ -147,8 +203,24 @@ class FlatOptimizer:
         return torch.where(gn < self.clip_grad, torch.ones_like(gn), self.clip_grad / gn)
 
     @torch.no_grad()
-    def _step_torch(self, lr, bc1, bc2):
+    def _step_torch(self, lr, bc1, bc2, lo: int | None = None, hi: int | None = None):
         s = self.store
+        if lo is not None:  # elementwise optimizers on one chunk of the flat buffer (split step)
+            sl = slice(lo, hi)
+            seg_id, valid, decay, llrd, trust_m, trainable = (t[sl] for t in self._elem_meta())
+            p, g = s.master[sl], s.grad[sl]
+            if self.kind == "adamw":
+                self.mu[sl].mul_(self.b1).add_((1 - self.b1) * g)
+                self.nu[sl].mul_(self.b2).add_((1 - self.b2) * g * g)
+                u = (self.mu[sl] / bc1) / (torch.sqrt(self.nu[sl] / bc2) + self.eps)
+                upd = -lr * (u + self.weight_decay * decay * p) * llrd
+            else:  # sgd
+                self.trace[sl].mul_(self.momentum).add_(g)
+                upd = -lr * self.trace[sl] * llrd
+            p.add_(torch.where(trainable & valid, upd, torch.zeros_like(upd)))
+            if s.shadow is not s.master:
+                s.shadow[sl].copy_(p)
+            return
         p, g = s.master, s.grad
         seg_id, valid, decay, llrd, trust_m, trainable = self._elem_meta()
         g = g * self._clip_scale_torch(g)

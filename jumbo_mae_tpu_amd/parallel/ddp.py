@@ -158,8 +158,16 @@ class GradReducer:
         w = dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
         return (w, t)
 
-    def finish(self) -> None:
-        """Launch any bucket not yet reduced (unused segments / no overlap) and wait for all."""
+    def bucket_ranges(self) -> list[tuple[int, int]]:
+        return [(lo, hi) for lo, hi, _ in self.buckets]
+
+    def finish(self, on_bucket_done=None) -> None:
+        """Launch any bucket not yet reduced (unused segments / no overlap) and wait for all.
+
+        ``on_bucket_done(lo, hi)`` is called as soon as the last reduction of a bucket has been
+        waited for (on RCCL: a stream wait, the host does not block), so the caller can queue
+        the optimizer update of that range behind it while later buckets -- the jumbo-MLP tail
+        -- are still being reduced."""
         from ..ops.prims import join_wgrad_stream
         join_wgrad_stream()
         if not self.enabled or not self.sync:
@@ -167,6 +175,9 @@ class GradReducer:
         for b in range(len(self.buckets)):
             if not self.launched[b]:
                 self._launch(b)
+        left = [0] * len(self.buckets)
+        for b, _ in self.works:
+            left[b] += 1
         for b, w in self.works:
             if isinstance(w, tuple):
                 w[0].wait()
@@ -176,6 +187,10 @@ class GradReducer:
             if b in self._compressed:
                 lo, hi, _ = self.buckets[b]
                 self.store.grad[lo:hi].copy_(self._compressed.pop(b))
+            left[b] -= 1
+            if on_bucket_done is not None and left[b] == 0:
+                lo, hi, _ = self.buckets[b]
+                on_bucket_done(lo, hi)
         self.works = []
 
     def stats(self) -> dict:

@@ -10,6 +10,8 @@ reference pmean's them every step, CC3, which is a blocking host round trip we a
 
 from __future__ import annotations
 
+import os
+
 import torch
 
 from ..ops.prims import join_wgrad_stream
@@ -29,6 +31,9 @@ class Trainer:
         self.reducer = reducer
         self.rngs = rngs
         self.grad_accum = grad_accum
+        # update each DP bucket right after its all-reduce (optimizer / reduction-tail overlap)
+        self.overlap_optimizer = os.environ.get("JMAE_OVERLAP_OPT", "1") == "1"
+        self._planned = False
 
     @property
     def store(self):
@@ -76,10 +81,15 @@ class Trainer:
             m = {k: v.detach().float() for k, v in out.items()}
             metrics_acc = m if metrics_acc is None else {k: metrics_acc[k] + m[k] for k in m}
         join_wgrad_stream()  # weight-gradient GEMMs run on a side stream (ops/prims.py)
+        split = (self.overlap_optimizer and self.reducer is not None and self.reducer.enabled
+                 and self.opt.can_split() and not self.skip_nonfinite)
+        if split and not self._planned:
+            self.opt.plan_ranges(self.reducer.bucket_ranges())
+            self._planned = True
         if self.reducer is not None:
             with trace_range("allreduce_wait"):
                 self.reducer.set_sync(True)
-                self.reducer.finish()
+                self.reducer.finish(self.opt.launch_range if split else None)
         metrics = {k: v / n for k, v in metrics_acc.items()}
         if self.skip_nonfinite:
             # opt-in guard (one host sync per step): drop the update of a step whose loss is
@@ -90,7 +100,10 @@ class Trainer:
                 self._skipped = metrics
                 return None
         with trace_range("optimizer"):
-            self.opt.launch()
+            if split:
+                self.opt.launch_rest()
+            else:
+                self.opt.launch()
         return metrics
 
     def host_finish(self) -> float:

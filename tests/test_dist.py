@@ -189,3 +189,48 @@ def test_allreduce_bench_gloo(tmp_path):
         assert row["world"] == 2
         assert row["allreduce_busbw_GBs"] > 0 and row["reduce_scatter_busbw_GBs"] > 0 and row["all_gather_busbw_GBs"] > 0
     assert res["model"]["vit_l_grad_allreduce_ms"] > res["model"]["vit_l_jumbo_tail_ms"] > 0
+
+
+def _overlap_worker(rank, world, port, out, kind):
+    _init(rank, world, port)
+    from jumbo_mae_tpu_amd.models.mae import PretrainModel
+    from jumbo_mae_tpu_amd.optim.flat import FlatOptimizer
+    from jumbo_mae_tpu_amd.optim.schedule import warmup_cosine_decay_schedule
+    from jumbo_mae_tpu_amd.parallel.ddp import GradReducer
+    from jumbo_mae_tpu_amd.train.engine import Trainer
+    vc, dc = _cfgs()
+    g = torch.Generator().manual_seed(0)
+    imgs = torch.randint(0, 256, (8, 3, 32, 32), dtype=torch.uint8, generator=g)
+    res = {}
+    for overlap in (False, True):
+        torch.manual_seed(100 + rank)  # same masking noise in both runs
+        m = PretrainModel(vc, dc).to("cpu", seed=0)
+        dist.broadcast(m.store.master, 0)
+        opt = FlatOptimizer(m.store, kind, warmup_cosine_decay_schedule(1e-6, 1e-2, 1, 10, 1e-5), b2=0.95,
+                            weight_decay=0.05, num_layers=vc.layers)
+        red = GradReducer(m.store, bucket_mb=0.01)
+        tr = Trainer(m, opt, red, None)
+        tr.overlap_optimizer = overlap
+        calls = []
+        real = opt.launch_range
+        opt.launch_range = lambda lo, hi: (calls.append((lo, hi)), real(lo, hi))
+        for step in range(3):
+            tr.train_step([(imgs[rank * 4:(rank + 1) * 4],)])
+        res[overlap] = (m.store.master.clone(), len(calls), len(red.buckets))
+    if rank == 0:
+        torch.save({"off": res[False][0], "on": res[True][0], "calls_on": res[True][1], "calls_off": res[False][1],
+                    "nb": res[True][2]}, out)
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("kind", ["adamw", "sgd"])
+def test_optimizer_overlaps_reduction_tail(kind):
+    """Split optimizer step (each DP bucket updated as soon as its all-reduce is waited for, the
+    rest at the end) == the monolithic step after the last reduction, bit for bit."""
+    port = _free_port()
+    with tempfile.TemporaryDirectory() as d:
+        out = os.path.join(d, "r.pt")
+        mp.spawn(_overlap_worker, args=(2, port, out, kind), nprocs=2, join=True)
+        res = torch.load(out, weights_only=True)
+    assert res["calls_off"] == 0 and res["calls_on"] == 3 * res["nb"] and res["nb"] > 3
+    assert torch.equal(res["on"], res["off"])
