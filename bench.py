@@ -127,6 +127,7 @@ def main():
     elapsed = time.perf_counter() - t_start
     elapsed = pdist.all_reduce_max_scalar(elapsed, dev)
     final_loss = float(m["loss"].item())
+    comm_ms = trainer.comm_ms()
 
     if args.profile_steps > 0 and info.is_main:
         from torch.profiler import ProfilerActivity, profile
@@ -152,6 +153,9 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "mfu_bf16_dense": round(mfu(value, pretrain_fwd_flops_per_image(vc, dc), world), 4),
+            # GPU time of the last step behind the DP reduction wait (exposed comm + overlapped
+            # bucket updates); null on one GPU
+            "exposed_comm_ms_last_step": None if comm_ms is None else round(comm_ms, 3),
             "dtype": "bf16",
             "data": "synthetic uint8 224x224 images on GPU, random-init weights",
             "config": {

@@ -34,6 +34,7 @@ class Trainer:
         # update each DP bucket right after its all-reduce (optimizer / reduction-tail overlap)
         self.overlap_optimizer = os.environ.get("JMAE_OVERLAP_OPT", "1") == "1"
         self._planned = False
+        self._comm_events = None  # (start, end) around the last step's reduction wait
 
     @property
     def store(self):
@@ -88,8 +89,15 @@ class Trainer:
             self._planned = True
         if self.reducer is not None:
             with trace_range("allreduce_wait"):
+                timed = self.reducer.enabled and self.store.grad.is_cuda and not torch.cuda.is_current_stream_capturing()
+                if timed:
+                    ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                    ev[0].record()
                 self.reducer.set_sync(True)
                 self.reducer.finish(self.opt.launch_range if split else None)
+                if timed:
+                    ev[1].record()
+                    self._comm_events = ev
         metrics = {k: v / n for k, v in metrics_acc.items()}
         if self.skip_nonfinite:
             # opt-in guard (one host sync per step): drop the update of a step whose loss is
@@ -108,6 +116,16 @@ class Trainer:
 
     def host_finish(self) -> float:
         return self.opt.finish()
+
+    def comm_ms(self) -> float | None:
+        """GPU time the last step spent behind the data-parallel reduction after its backward was
+        queued (the exposed communication, including overlapped bucket updates); None without a
+        reducer.  Synchronises on that step's end event: call it at log intervals only."""
+        if self._comm_events is None:
+            return None
+        e0, e1 = self._comm_events
+        e1.synchronize()
+        return e0.elapsed_time(e1)
 
     @torch.no_grad()
     def eval_step(self, args) -> dict:

@@ -106,6 +106,9 @@ def main(args) -> dict:
             summ = meter.summary("train/")
             summ["processed_samples"] = step * args.train_batch_size
             summ.update(perf.summary(step))
+            comm = trainer.comm_ms()
+            if comm is not None:
+                summ["perf/comm_ms"] = comm
             C.check_finite(summ, step)
             if info.is_main:
                 logger.log(summ, step)

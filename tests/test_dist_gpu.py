@@ -129,6 +129,8 @@ def _overlap_worker(rank, world, port, out):
         for _ in range(2):
             tr.train_step([(mine,)])
         torch.cuda.synchronize()
+        comm = tr.comm_ms()
+        assert comm is not None and comm >= 0.0  # perf/comm_ms: GPU-timed reduction wait
         res[overlap] = (m.store.master.cpu(), m.store.shadow.float().cpu())
     if rank == 0:
         torch.save({"off": res[False], "on": res[True]}, out)
