@@ -1279,6 +1279,321 @@ int dispatch_sp(bool fwd, const uint16_t* qkv, const uint16_t* o, const uint16_t
   return -2;
 }
 
+// ------------------------------------------------------ long sequences (S > 224): tile-streamed
+// Past 224 tokens one (b, h) no longer fits a workgroup's register/LDS budget (finetuning at
+// 448 px: S = 787), so 64-row tiles stream through LDS instead.  The MFMA
+// orientations are the ones of the fused kernels above:
+//   attn_fwd_long_kernel  WG = 64 queries of one (b, h) (one 16-query tile per wave, query on the
+//                         lane); online softmax over 64-key tiles; O^T = V^T P^T with P^T straight
+//                         from the S^T accumulators.
+//   attn_bwd_dq_kernel    WG = 64 queries; P^T recomputed from lse; dQ^T = K^T dS^T; also writes
+//                         delta = rowsum(dO * O) for the next kernel.
+//   attn_bwd_dkv_kernel   WG = 64 keys (key on the lane, K / V fragments kept in registers);
+//                         sweeps 64-query tiles: dV^T += dO^T P, dK^T += Q^T dS.
+// Every output element has one writer: no atomics, deterministic.  Grid x = (b, h) major, tile
+// minor, so the WGs sharing one (b, h)'s K / V (or Q / dO) rows are dispatched together.
+constexpr int LT = 64;
+
+template <int HD>
+JM_DEVICE void load_tile(uint16_t* dst, const uint16_t* src, long rs, int r0, int S) {
+  constexpr int CPR = HD / 8, KS = HD + 8;
+  for (int i = threadIdx.x; i < LT * CPR; i += 256) {
+    const int r = i / CPR, c = (i % CPR) * 8;
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (r0 + r < S) v = *reinterpret_cast<const uint4*>(src + (long)(r0 + r) * rs + c);
+    *reinterpret_cast<uint4*>(dst + r * KS + c) = v;
+  }
+}
+
+// A operand of X^T (d on the lane) for a 32-row chunk of a row-major LDS tile, rows permuted
+// like the packed P^T / dS^T fragments (rows 4g..4g+3, then 16+4g..16+4g+3)
+template <int HD>
+JM_DEVICE bf16x8_t tr_frag(const uint16_t* t, int s, int dt, int l16, int g) {
+  constexpr int KS = HD + 8;
+  const uint16_t* p = t + (32 * s + 4 * g + (l16 >> 2)) * KS + dt * 16 + 4 * (l16 & 3);
+  return cat44(tr4(p), tr4(p + 16 * KS));
+}
+
+template <int HD>
+__global__ __launch_bounds__(256) void attn_fwd_long_kernel(const uint16_t* __restrict__ qkv,
+                                                            uint16_t* __restrict__ o, float* __restrict__ lse,
+                                                            int S, int H, float scale) {
+  constexpr int KS = HD + 8, KK = HD / 32, DT = HD / 16;
+  __shared__ __attribute__((aligned(16))) uint16_t Ks[LT * KS];
+  __shared__ __attribute__((aligned(16))) uint16_t Vs[LT * KS];
+  const int nq = (S + LT - 1) / LT;
+  const int bh = blockIdx.x / nq, qb = blockIdx.x - bh * nq;
+  const int b = bh / H, h = bh - b * H;
+  const long ts = 3L * H * HD;
+  const uint16_t* base = qkv + (long)b * S * ts;
+  const uint16_t* Kg = base + (H + h) * HD;
+  const uint16_t* Vg = base + (2 * H + h) * HD;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, l16 = lane & 15, g = lane >> 4;
+  const int q = qb * LT + wave * 16 + l16;
+  const float sl2 = scale * LOG2E;
+
+  bf16x8_t qf[KK];
+#pragma unroll
+  for (int kk = 0; kk < KK; ++kk) {
+    s16x8_t z = {0, 0, 0, 0, 0, 0, 0, 0};
+    qf[kk] = q < S ? ld8(base + (long)q * ts + h * HD + 32 * kk + 8 * g) : __builtin_bit_cast(bf16x8_t, z);
+  }
+  f32x4_t oacc[DT];
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt) oacc[dt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  float m = -INFINITY, l = 0.f;
+
+  for (int k0 = 0; k0 < S; k0 += LT) {
+    __syncthreads();
+    load_tile<HD>(Ks, Kg, ts, k0, S);
+    load_tile<HD>(Vs, Vg, ts, k0, S);
+    __syncthreads();
+    f32x4_t sc[4];
+    float mt = -INFINITY;
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt) {
+      f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kk = 0; kk < KK; ++kk) acc = mfma(ld8(Ks + (kt * 16 + l16) * KS + 32 * kk + 8 * g), qf[kk], acc);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float v = k0 + kt * 16 + 4 * g + i < S ? acc[i] * sl2 : -INFINITY;
+        sc[kt][i] = v;
+        mt = fmaxf(mt, v);
+      }
+    }
+    mt = fmaxf(mt, __shfl_xor(mt, 16, WAVE));
+    mt = fmaxf(mt, __shfl_xor(mt, 32, WAVE));
+    const float mn = fmaxf(m, mt);  // finite: every tile holds at least one valid key
+    const float alpha = __builtin_amdgcn_exp2f(m - mn);
+    m = mn;
+    l *= alpha;
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) oacc[dt] *= alpha;
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float p = __builtin_amdgcn_exp2f(sc[kt][i] - m);
+        sc[kt][i] = p;
+        l += p;
+      }
+    }
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      float pf[8] = {sc[2 * s][0], sc[2 * s][1], sc[2 * s][2], sc[2 * s][3],
+                     sc[2 * s + 1][0], sc[2 * s + 1][1], sc[2 * s + 1][2], sc[2 * s + 1][3]};
+      const bf16x8_t pb = pack8(pf);
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt) oacc[dt] = mfma(tr_frag<HD>(Vs, s, dt, l16, g), pb, oacc[dt]);
+    }
+  }
+  l += __shfl_xor(l, 16, WAVE);
+  l += __shfl_xor(l, 32, WAVE);
+  if (q < S) {
+    const float inv = 1.f / l;
+    uint16_t* orow = o + ((long)b * S + q) * H * HD + h * HD;
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) {
+      float v[4] = {oacc[dt][0] * inv, oacc[dt][1] * inv, oacc[dt][2] * inv, oacc[dt][3] * inv};
+      store4(orow + dt * 16 + 4 * g, v);
+    }
+    if (g == 0) lse[((long)b * H + h) * S + q] = (m + log2f(l)) * LN2;
+  }
+}
+
+template <int HD>
+__global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const uint16_t* __restrict__ qkv,
+                                                          const uint16_t* __restrict__ o,
+                                                          const uint16_t* __restrict__ dO,
+                                                          const float* __restrict__ lse,
+                                                          uint16_t* __restrict__ dqkv, float* __restrict__ delta,
+                                                          int S, int H, float scale) {
+  constexpr int KS = HD + 8, KK = HD / 32, DT = HD / 16;
+  __shared__ __attribute__((aligned(16))) uint16_t Ks[LT * KS];
+  __shared__ __attribute__((aligned(16))) uint16_t Vs[LT * KS];
+  const int nq = (S + LT - 1) / LT;
+  const int bh = blockIdx.x / nq, qb = blockIdx.x - bh * nq;
+  const int b = bh / H, h = bh - b * H;
+  const long ts = 3L * H * HD;
+  const uint16_t* base = qkv + (long)b * S * ts;
+  const uint16_t* Kg = base + (H + h) * HD;
+  const uint16_t* Vg = base + (2 * H + h) * HD;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, l16 = lane & 15, g = lane >> 4;
+  const int q = qb * LT + wave * 16 + l16;
+  const float sl2 = scale * LOG2E;
+
+  bf16x8_t qf[KK], df[KK];
+  float dl = 0.f;
+#pragma unroll
+  for (int kk = 0; kk < KK; ++kk) {
+    s16x8_t z = {0, 0, 0, 0, 0, 0, 0, 0};
+    qf[kk] = df[kk] = __builtin_bit_cast(bf16x8_t, z);
+    if (q < S) {
+      const long orow = ((long)b * S + q) * H * HD + h * HD + 32 * kk + 8 * g;
+      qf[kk] = ld8(base + (long)q * ts + h * HD + 32 * kk + 8 * g);
+      df[kk] = ld8(dO + orow);
+      const s16x8_t dv = __builtin_bit_cast(s16x8_t, df[kk]);
+      const s16x8_t ov = __builtin_bit_cast(s16x8_t, ld8(o + orow));
+#pragma unroll
+      for (int j = 0; j < 8; ++j) dl += bf2f((uint16_t)dv[j]) * bf2f((uint16_t)ov[j]);
+    }
+  }
+  dl += __shfl_xor(dl, 16, WAVE);
+  dl += __shfl_xor(dl, 32, WAVE);
+  const long lrow = ((long)b * H + h) * S;
+  const float l2 = q < S ? lse[lrow + q] * LOG2E : INFINITY;
+  if (q < S && g == 0) delta[lrow + q] = dl;
+
+  f32x4_t dq[DT];
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt) dq[dt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  for (int k0 = 0; k0 < S; k0 += LT) {
+    __syncthreads();
+    load_tile<HD>(Ks, Kg, ts, k0, S);
+    load_tile<HD>(Vs, Vg, ts, k0, S);
+    __syncthreads();
+    float ds[4][4];
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt) {
+      f32x4_t sa = {0.f, 0.f, 0.f, 0.f}, pa = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kk = 0; kk < KK; ++kk) {
+        sa = mfma(ld8(Ks + (kt * 16 + l16) * KS + 32 * kk + 8 * g), qf[kk], sa);
+        pa = mfma(ld8(Vs + (kt * 16 + l16) * KS + 32 * kk + 8 * g), df[kk], pa);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float p = k0 + kt * 16 + 4 * g + i < S ? __builtin_amdgcn_exp2f(sa[i] * sl2 - l2) : 0.f;
+        ds[kt][i] = p * (pa[i] - dl);
+      }
+    }
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      float f[8] = {ds[2 * s][0], ds[2 * s][1], ds[2 * s][2], ds[2 * s][3],
+                    ds[2 * s + 1][0], ds[2 * s + 1][1], ds[2 * s + 1][2], ds[2 * s + 1][3]};
+      const bf16x8_t db = pack8(f);
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt) dq[dt] = mfma(tr_frag<HD>(Ks, s, dt, l16, g), db, dq[dt]);
+    }
+  }
+  if (q < S) {
+    uint16_t* row = dqkv + ((long)b * S + q) * ts + h * HD;
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) {
+      float v[4] = {dq[dt][0] * scale, dq[dt][1] * scale, dq[dt][2] * scale, dq[dt][3] * scale};
+      store4(row + dt * 16 + 4 * g, v);
+    }
+  }
+}
+
+template <int HD>
+__global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(const uint16_t* __restrict__ qkv,
+                                                           const uint16_t* __restrict__ dO,
+                                                           const float* __restrict__ lse,
+                                                           const float* __restrict__ delta,
+                                                           uint16_t* __restrict__ dqkv, int S, int H, float scale) {
+  constexpr int KS = HD + 8, KK = HD / 32, DT = HD / 16;
+  __shared__ __attribute__((aligned(16))) uint16_t Qs[LT * KS];
+  __shared__ __attribute__((aligned(16))) uint16_t Ds[LT * KS];
+  __shared__ float Ls[LT], Dl[LT];
+  const int nk = (S + LT - 1) / LT;
+  const int bh = blockIdx.x / nk, kb = blockIdx.x - bh * nk;
+  const int b = bh / H, h = bh - b * H;
+  const long ts = 3L * H * HD;
+  const uint16_t* base = qkv + (long)b * S * ts;
+  const uint16_t* Qg = base + h * HD;
+  const uint16_t* dOg = dO + (long)b * S * H * HD + h * HD;
+  const long lrow = ((long)b * H + h) * S;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, l16 = lane & 15, g = lane >> 4;
+  const int key = kb * LT + wave * 16 + l16;
+  const bool kv = key < S;
+  const float sl2 = scale * LOG2E;
+
+  bf16x8_t kf[KK], vf[KK];
+#pragma unroll
+  for (int kk = 0; kk < KK; ++kk) {
+    s16x8_t z = {0, 0, 0, 0, 0, 0, 0, 0};
+    kf[kk] = vf[kk] = __builtin_bit_cast(bf16x8_t, z);
+    if (kv) {
+      kf[kk] = ld8(base + (long)key * ts + (H + h) * HD + 32 * kk + 8 * g);
+      vf[kk] = ld8(base + (long)key * ts + (2 * H + h) * HD + 32 * kk + 8 * g);
+    }
+  }
+  f32x4_t dk[DT], dv[DT];
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt) dk[dt] = dv[dt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  for (int q0 = 0; q0 < S; q0 += LT) {
+    __syncthreads();
+    load_tile<HD>(Qs, Qg, ts, q0, S);
+    load_tile<HD>(Ds, dOg, (long)H * HD, q0, S);
+    if (threadIdx.x < LT) {
+      const int r = q0 + threadIdx.x;
+      Ls[threadIdx.x] = r < S ? lse[lrow + r] * LOG2E : INFINITY;
+      Dl[threadIdx.x] = r < S ? delta[lrow + r] : 0.f;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      float pf[8], df[8];
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const int qt = 2 * s + t;
+        f32x4_t sa = {0.f, 0.f, 0.f, 0.f}, pa = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int kk = 0; kk < KK; ++kk) {
+          sa = mfma(ld8(Qs + (qt * 16 + l16) * KS + 32 * kk + 8 * g), kf[kk], sa);
+          pa = mfma(ld8(Ds + (qt * 16 + l16) * KS + 32 * kk + 8 * g), vf[kk], pa);
+        }
+        // sa[i] = S[query = qt*16 + 4g + i][key = l16]
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int qq = qt * 16 + 4 * g + i;
+          const float p = kv ? __builtin_amdgcn_exp2f(sa[i] * sl2 - Ls[qq]) : 0.f;
+          pf[4 * t + i] = p;
+          df[4 * t + i] = p * (pa[i] - Dl[qq]);
+        }
+      }
+      const bf16x8_t pb = pack8(pf), db = pack8(df);
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt) {
+        dv[dt] = mfma(tr_frag<HD>(Ds, s, dt, l16, g), pb, dv[dt]);
+        dk[dt] = mfma(tr_frag<HD>(Qs, s, dt, l16, g), db, dk[dt]);
+      }
+    }
+  }
+  // dk[dt][i] = dK^T[d = dt*16 + 4g + i][key]
+  if (kv) {
+    uint16_t* row = dqkv + ((long)b * S + key) * ts;
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) {
+      float a[4] = {dk[dt][0] * scale, dk[dt][1] * scale, dk[dt][2] * scale, dk[dt][3] * scale};
+      float c[4] = {dv[dt][0], dv[dt][1], dv[dt][2], dv[dt][3]};
+      store4(row + (H + h) * HD + dt * 16 + 4 * g, a);
+      store4(row + (2 * H + h) * HD + dt * 16 + 4 * g, c);
+    }
+  }
+}
+
+template <int HD>
+int run_long_fwd(const uint16_t* qkv, uint16_t* o, float* lse, int B, int S, int H, float scale, hipStream_t st) {
+  const long grid = (long)B * H * ((S + LT - 1) / LT);
+  if (grid > 0x7fffffffL) return -5;
+  attn_fwd_long_kernel<HD><<<dim3((unsigned)grid), 256, 0, st>>>(qkv, o, lse, S, H, scale);
+  return 0;
+}
+
+template <int HD>
+int run_long_bwd(const uint16_t* qkv, const uint16_t* o, const uint16_t* dO, const float* lse, uint16_t* dqkv,
+                 float* delta, int B, int S, int H, float scale, hipStream_t st) {
+  const long grid = (long)B * H * ((S + LT - 1) / LT);
+  if (grid > 0x7fffffffL) return -5;
+  attn_bwd_dq_kernel<HD><<<dim3((unsigned)grid), 256, 0, st>>>(qkv, o, dO, lse, dqkv, delta, S, H, scale);
+  attn_bwd_dkv_kernel<HD><<<dim3((unsigned)grid), 256, 0, st>>>(qkv, dO, lse, delta, dqkv, S, H, scale);
+  return 0;
+}
+
 }  // namespace
 
 int jm_attn_max_seq() { return 224; }
@@ -1301,6 +1616,11 @@ int jm_attn_bwd_part_rows(int B, int S, int hd) {
 
 int jm_attn_fwd(const uint16_t* qkv, uint16_t* o, float* lse, int B, int S, int H, int hd, hipStream_t st) {
   const float scale = 1.f / sqrtf((float)hd);
+  if (S > jm_attn_max_seq()) {
+    if (hd == 32) return run_long_fwd<32>(qkv, o, lse, B, S, H, scale, st);
+    if (hd == 64) return run_long_fwd<64>(qkv, o, lse, B, S, H, scale, st);
+    return -1;
+  }
   if (hd == 32) return dispatch_sp<32>(true, qkv, nullptr, nullptr, nullptr, o, lse, B, S, H, scale, st);
   if (hd == 64) return dispatch_sp<64>(true, qkv, nullptr, nullptr, nullptr, o, lse, B, S, H, scale, st);
   return -1;
@@ -1312,6 +1632,16 @@ int jm_attn_bwd(const uint16_t* qkv, const uint16_t* o, const uint16_t* dO, cons
   const float scale = 1.f / sqrtf((float)hd);
   if (hd == 32) return dispatch_sp<32>(false, qkv, o, dO, lse, dqkv, dbias_part, B, S, H, scale, st);
   if (hd == 64) return dispatch_sp<64>(false, qkv, o, dO, lse, dqkv, dbias_part, B, S, H, scale, st);
+  return -1;
+}
+
+// S > jm_attn_max_seq(): tile-streamed backward; delta = fp32 [B][H][S] workspace.  No fused
+// bias colsum on this path (the caller takes colsum(dqkv)).
+int jm_attn_bwd_long(const uint16_t* qkv, const uint16_t* o, const uint16_t* dO, const float* lse, uint16_t* dqkv,
+                     float* delta, int B, int S, int H, int hd, hipStream_t st) {
+  const float scale = 1.f / sqrtf((float)hd);
+  if (hd == 32) return run_long_bwd<32>(qkv, o, dO, lse, dqkv, delta, B, S, H, scale, st);
+  if (hd == 64) return run_long_bwd<64>(qkv, o, dO, lse, dqkv, delta, B, S, H, scale, st);
   return -1;
 }
 

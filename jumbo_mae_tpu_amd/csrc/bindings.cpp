@@ -48,6 +48,8 @@ void jm_attn_set_tr(int v);
 void jm_attn_set_fwd_hpw(int v);
 void jm_attn_set_bwd_ppw(int v);
 int jm_attn_bwd_part_rows(int B, int S, int hd);
+int jm_attn_bwd_long(const uint16_t* qkv, const uint16_t* o, const uint16_t* dO, const float* lse, uint16_t* dqkv,
+                     float* delta, int B, int S, int H, int hd, hipStream_t st);
 void jm_opt_sumsq(const float* x, const int* chunks, int nchunks, float* out, hipStream_t st);
 void jm_opt_adamw(float* p, const float* g, float* mu, float* nu, uint16_t* shadow, const int* chunks, int nchunks,
                   const float* meta, const float* hyper, const float* gnorm_sq, hipStream_t st);
@@ -341,6 +343,14 @@ torch::Tensor attn_bwd(torch::Tensor dO, torch::Tensor qkv, torch::Tensor o, tor
   const int B = qkv.size(0), S = qkv.size(1), D3 = qkv.size(2);
   const int D = D3 / 3, hd = D / heads;
   auto dqkv = torch::empty_like(qkv);
+  if (S > jm_attn_max_seq()) {  // tile-streamed kernels; the caller reduces the bias gradient
+    TORCH_CHECK(!dbias, "attn_bwd: no fused bias gradient for S > ", jm_attn_max_seq());
+    auto delta = torch::empty({B, (long)heads, S}, qkv.options().dtype(torch::kFloat32));
+    check_rc(jm_attn_bwd_long(bf(qkv), bf(o), bf(dO), lse.data_ptr<float>(), bfm(dqkv), delta.data_ptr<float>(), B,
+                              S, heads, hd, stream()),
+             "attn_bwd (long)");
+    return dqkv;
+  }
   torch::Tensor part;
   const int rows = jm_attn_bwd_part_rows(B, S, hd);
   if (dbias) {

@@ -545,14 +545,14 @@ def residual_bwd(dout3: torch.Tensor, y2: torch.Tensor | None, hs: Handle | None
 
 # ------------------------------------------------------------------------------ attention
 def _attn_hip(qkv: torch.Tensor, heads: int) -> bool:
-    """The fused whole-sequence-in-LDS kernels cover S <= attn_max_seq() (224: every flagship
-    shape) and head dims 32 / 64; longer sequences (e.g. finetuning at 448 px,
-    S = 787) take the PyTorch composition below (fp32 softmax, same numerics)."""
+    """HIP attention covers head dims 32 / 64 at any length: the fused whole-sequence-in-LDS
+    kernels up to S = attn_max_seq() (224: every flagship shape), tile-streamed online-softmax
+    kernels beyond (e.g. finetuning at 448 px, S = 787).  Other head dims take
+    the PyTorch composition below (fp32 softmax, same numerics)."""
     if not hip(qkv):
         return False
-    B, S, three_d = qkv.shape
-    hd = three_d // 3 // heads
-    return S <= _ext.load().attn_max_seq() and hd in (32, 64)
+    hd = qkv.shape[2] // 3 // heads
+    return hd in (32, 64)
 
 
 def attn_fwd(qkv: torch.Tensor, heads: int):
@@ -579,8 +579,9 @@ def attn_bwd(do: torch.Tensor, qkv: torch.Tensor, o: torch.Tensor, lse: torch.Te
     hd = D // heads
     do = do.contiguous().view(B, S, D)
     if _attn_hip(qkv, heads):
-        bg = hbias.grad if _trainable(hbias) else None
-        return _ext.load().attn_bwd(do, qkv, o, lse, heads, bg), bg is not None
+        ext = _ext.load()
+        bg = hbias.grad if _trainable(hbias) and S <= ext.attn_max_seq() else None
+        return ext.attn_bwd(do, qkv, o, lse, heads, bg), bg is not None
     q, k, v = qkv.float().view(B, S, 3, heads, hd).unbind(2)
     dof = do.float().view(B, S, heads, hd)
     sc = 1.0 / math.sqrt(hd)
