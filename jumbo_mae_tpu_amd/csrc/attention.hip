@@ -1294,14 +1294,30 @@ int dispatch_sp(bool fwd, const uint16_t* qkv, const uint16_t* o, const uint16_t
 // minor, so the WGs sharing one (b, h)'s K / V (or Q / dO) rows are dispatched together.
 constexpr int LT = 64;
 
+// a 64 x HD bf16 tile moves HBM -> registers (issued one tile ahead, so its latency hides behind
+// the current tile's MFMA work) -> LDS (row stride HD + 8); rows past S are zero
 template <int HD>
-JM_DEVICE void load_tile(uint16_t* dst, const uint16_t* src, long rs, int r0, int S) {
+struct TileRegs {
+  uint4 v[HD / 32];
+};
+
+template <int HD>
+JM_DEVICE void tile_fetch(TileRegs<HD>& t, const uint16_t* src, long rs, int r0, int S) {
+  constexpr int CPR = HD / 8;
+#pragma unroll
+  for (int j = 0; j < HD / 32; ++j) {
+    const int i = threadIdx.x + 256 * j, r = i / CPR, c = (i % CPR) * 8;
+    t.v[j] = r0 + r < S ? *reinterpret_cast<const uint4*>(src + (long)(r0 + r) * rs + c) : make_uint4(0, 0, 0, 0);
+  }
+}
+
+template <int HD>
+JM_DEVICE void tile_store(uint16_t* dst, const TileRegs<HD>& t) {
   constexpr int CPR = HD / 8, KS = HD + 8;
-  for (int i = threadIdx.x; i < LT * CPR; i += 256) {
-    const int r = i / CPR, c = (i % CPR) * 8;
-    uint4 v = make_uint4(0, 0, 0, 0);
-    if (r0 + r < S) v = *reinterpret_cast<const uint4*>(src + (long)(r0 + r) * rs + c);
-    *reinterpret_cast<uint4*>(dst + r * KS + c) = v;
+#pragma unroll
+  for (int j = 0; j < HD / 32; ++j) {
+    const int i = threadIdx.x + 256 * j, r = i / CPR, c = (i % CPR) * 8;
+    *reinterpret_cast<uint4*>(dst + r * KS + c) = t.v[j];
   }
 }
 
@@ -1343,11 +1359,18 @@ __global__ __launch_bounds__(256) void attn_fwd_long_kernel(const uint16_t* __re
   for (int dt = 0; dt < DT; ++dt) oacc[dt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
   float m = -INFINITY, l = 0.f;
 
+  TileRegs<HD> kr, vr;
+  tile_fetch<HD>(kr, Kg, ts, 0, S);
+  tile_fetch<HD>(vr, Vg, ts, 0, S);
   for (int k0 = 0; k0 < S; k0 += LT) {
     __syncthreads();
-    load_tile<HD>(Ks, Kg, ts, k0, S);
-    load_tile<HD>(Vs, Vg, ts, k0, S);
+    tile_store<HD>(Ks, kr);
+    tile_store<HD>(Vs, vr);
     __syncthreads();
+    if (k0 + LT < S) {
+      tile_fetch<HD>(kr, Kg, ts, k0 + LT, S);
+      tile_fetch<HD>(vr, Vg, ts, k0 + LT, S);
+    }
     f32x4_t sc[4];
     float mt = -INFINITY;
 #pragma unroll
@@ -1448,11 +1471,18 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const uint16_t* __rest
   f32x4_t dq[DT];
 #pragma unroll
   for (int dt = 0; dt < DT; ++dt) dq[dt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  TileRegs<HD> kr, vr;
+  tile_fetch<HD>(kr, Kg, ts, 0, S);
+  tile_fetch<HD>(vr, Vg, ts, 0, S);
   for (int k0 = 0; k0 < S; k0 += LT) {
     __syncthreads();
-    load_tile<HD>(Ks, Kg, ts, k0, S);
-    load_tile<HD>(Vs, Vg, ts, k0, S);
+    tile_store<HD>(Ks, kr);
+    tile_store<HD>(Vs, vr);
     __syncthreads();
+    if (k0 + LT < S) {
+      tile_fetch<HD>(kr, Kg, ts, k0 + LT, S);
+      tile_fetch<HD>(vr, Vg, ts, k0 + LT, S);
+    }
     float ds[4][4];
 #pragma unroll
     for (int kt = 0; kt < 4; ++kt) {
@@ -1524,16 +1554,31 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(const uint16_t* __res
 #pragma unroll
   for (int dt = 0; dt < DT; ++dt) dk[dt] = dv[dt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
+  TileRegs<HD> qr, dr;
+  float lr = INFINITY, dlr = 0.f;
+  auto fetch = [&](int r0) {
+    tile_fetch<HD>(qr, Qg, ts, r0, S);
+    tile_fetch<HD>(dr, dOg, (long)H * HD, r0, S);
+    const int r = r0 + threadIdx.x;
+    if (threadIdx.x < LT && r < S) {
+      lr = lse[lrow + r] * LOG2E;
+      dlr = delta[lrow + r];
+    } else {
+      lr = INFINITY;
+      dlr = 0.f;
+    }
+  };
+  fetch(0);
   for (int q0 = 0; q0 < S; q0 += LT) {
     __syncthreads();
-    load_tile<HD>(Qs, Qg, ts, q0, S);
-    load_tile<HD>(Ds, dOg, (long)H * HD, q0, S);
+    tile_store<HD>(Qs, qr);
+    tile_store<HD>(Ds, dr);
     if (threadIdx.x < LT) {
-      const int r = q0 + threadIdx.x;
-      Ls[threadIdx.x] = r < S ? lse[lrow + r] * LOG2E : INFINITY;
-      Dl[threadIdx.x] = r < S ? delta[lrow + r] : 0.f;
+      Ls[threadIdx.x] = lr;
+      Dl[threadIdx.x] = dlr;
     }
     __syncthreads();
+    if (q0 + LT < S) fetch(q0 + LT);
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       float pf[8], df[8];
