@@ -45,6 +45,8 @@ def main():
     ap.add_argument("--batch-per-gpu", type=int, default=512)
     ap.add_argument("--grad-accum", type=int, default=1)
     ap.add_argument("--bucket-mb", type=float, default=64.0)
+    ap.add_argument("--reduce-dtype", default="fp32", choices=["fp32", "bf16"],
+                    help="gradient all-reduce dtype (fp32 master weights either way)")
     ap.add_argument("--no-overlap", action="store_true")
     ap.add_argument("--profile-steps", type=int, default=0, help="extra steps under torch.profiler (debug)")
     ap.add_argument("--task", default="pretrain", choices=["pretrain", "finetune", "linear"])
@@ -83,7 +85,9 @@ def main():
     sched = warmup_cosine_decay_schedule(1e-6, 1.5e-4 * 4096 / 256, 1281167 * 40 // 4096, steps_total, 1e-5)
     opt = FlatOptimizer(store, "adamw", sched, b1=0.9, b2=0.95, eps=1e-8, weight_decay=0.05,
                         num_layers=vc.layers)
-    reducer = GradReducer(store, bucket_mb=args.bucket_mb, overlap=not args.no_overlap) if world > 1 else None
+    rdt = torch.bfloat16 if args.reduce_dtype == "bf16" else torch.float32
+    reducer = (GradReducer(store, bucket_mb=args.bucket_mb, overlap=not args.no_overlap, reduce_dtype=rdt)
+               if world > 1 else None)
     rngs = RngStreams({"noise": 0, "dropout": 0, "mixup": 0}, info.rank, dev)
     trainer = Trainer(model, opt, reducer, rngs, grad_accum=args.grad_accum)
     from jumbo_mae_tpu_amd.runtime.graph import StepRunner
@@ -207,7 +211,8 @@ def bench_classifier(args):
                  "--weight-decay", "0.0", "--warmup-steps", str(N * 10 // 16384),
                  "--training-steps", str(N * 90 // 16384)]
         model_name, recipe = "vit_large_patch16 jumbo (3 CLS) linear probe", "lars syncbn-head"
-    fargs = finetune_parser().parse_args(flags + ["--train-batch-size", str(gb), "--bucket-mb", str(args.bucket_mb)])
+    fargs = finetune_parser().parse_args(flags + ["--train-batch-size", str(gb), "--bucket-mb", str(args.bucket_mb),
+                                                "--reduce-dtype", args.reduce_dtype])
     model = build_model(fargs, dev, torch.bfloat16, info.rank)
     pdist.broadcast_(model.store.master)
     model.store.sync_shadow()

@@ -28,7 +28,9 @@ def _t(a):
     return np.ascontiguousarray(np.asarray(a, dtype=np.float32))
 
 
-def flax_to_torch(params: dict, exclude_heads: bool = False, num_cls: int = 3) -> dict:
+def flax_to_torch(params: dict, exclude_heads: bool = False, num_cls: int = 3, image_size: int = 224) -> dict:
+    """``image_size`` sets the patch grid of a sincos model (no learnable table in the tree): the
+    exported ``pos_embed`` is the fixed table of an ``image_size`` input."""
     m = params["model"] if "model" in params else params
     emb = m["embed"]
     D = emb["wte"]["bias"].shape[0]
@@ -41,8 +43,7 @@ def flax_to_torch(params: dict, exclude_heads: bool = False, num_cls: int = 3) -
         g = pos.shape[0]
     else:
         k = emb["wte"]["kernel"]
-        # infer the grid from a conventional 224 input when sincos (no learnable table)
-        g = 224 // k.shape[0]
+        g = image_size // k.shape[0]  # HWIO kernel: k.shape[0] is the patch size
         pos = _sincos2d_np(g, g, D)
     pos = pos.reshape(1, -1, D)
     sd["pos_embed"] = np.concatenate([np.zeros((1, cls.shape[1], D), np.float32), pos], 1)

@@ -64,31 +64,45 @@ def collate_and_pad(batch, batch_size: int = 1):
     return _stack(list(batch) + [pad] * (batch_size - len(batch)))
 
 
+def sample_seed(seed: int, rank: int, wid: int, index: int) -> int:
+    """Seed of the augmentation draws of one training sample: sample ``index`` of worker ``wid``'s
+    post-repeat stream on ``rank``.  Seeding per sample (not once per worker) makes a sample's
+    augmentation independent of how many samples came before it, so a resumed run that skips the
+    consumed samples without decoding them reproduces the uninterrupted stream exactly."""
+    h = (seed * 1_000_003 + rank * 92_821 + wid * 7_919) & 0xFFFFFFFF
+    return (h * 2_654_435_761 + index * 40_503 + 0x9E3779B9) % (2 ** 32)
+
+
+def worker_skip(batches: int, wid: int, nw: int) -> int:
+    """Batches that worker ``wid`` of ``nw`` delivered among the first ``batches`` of a DataLoader
+    (the loader takes batches from its workers round-robin)."""
+    return (batches - wid + nw - 1) // nw if batches > wid else 0
+
+
 class ShardDataset(IterableDataset):
     def __init__(self, spec, mode: str, transform, train: bool, repeats: int = 1, seed: int = 0,
-                 rank: int = 0, world: int = 1, shuffle_buffer: int = 2000, image_size: int = 224):
+                 rank: int = 0, world: int = 1, shuffle_buffer: int = 2000, image_size: int = 224,
+                 skip_batches: int = 0, batch_size: int = 1):
         self.spec, self.mode, self.transform, self.train = spec, mode, transform, train
         self.repeats, self.seed, self.rank, self.world = repeats, seed, rank, world
         self.shuffle_buffer = shuffle_buffer
         self.image_size = image_size
+        # resume: the first ``skip_batches`` DataLoader batches (of ``batch_size``) were consumed by
+        # the interrupted run; each worker skips its share of them without decoding
+        self.skip_batches, self.batch_size = skip_batches, batch_size
         # validation batches always carry a label so that padded rows (-1) can be masked out
         self.with_label = mode in ("finetune", "linear") or not train
         self.synthetic = isinstance(spec, str) and spec.startswith("synthetic:")
         self.urls = [] if self.synthetic else S.shard_list(spec)
 
-    # raw (decoded) samples of this rank/worker, one epoch
-    def _raw(self, epoch: int, wid: int, nw: int):
+    # raw (undecoded) records of this rank/worker, one epoch
+    def _records(self, epoch: int, wid: int, nw: int):
         if self.synthetic:
             parts = self.spec.split(":")
             n = int(parts[1])
-            ncls = int(parts[2]) if len(parts) > 2 else 1000
-            idx = range(n)
-            idx = itertools.islice(idx, self.rank * nw + wid, None, self.world * nw)
+            idx = itertools.islice(range(n), self.rank * nw + wid, None, self.world * nw)
             for i in idx:
-                rs = np.random.default_rng(i + (epoch * 7919 if self.train else 0))
-                arr = rs.integers(0, 256, (self.image_size + 32, self.image_size + 32, 3), dtype=np.uint8)
-                from PIL import Image
-                yield {"jpg": Image.fromarray(arr), "cls": int(rs.integers(0, ncls))}
+                yield {"synthetic": i + (epoch * 7919 if self.train else 0)}
             return
         urls = S.epoch_shards(self.urls, self.seed, epoch, shuffle=self.train)
         total = self.world * nw
@@ -104,45 +118,82 @@ class ShardDataset(IterableDataset):
             it = itertools.islice(it, sample_filter[0], None, sample_filter[1])
         if self.train:
             it = S.detshuffle(it, self.shuffle_buffer, self.seed * 7 + epoch * 131 + self.rank * 17 + wid)
-        for s in it:
-            try:
-                out = {"jpg": S.decode_pil(s["jpg"])}
-                if self.with_label:
-                    out["cls"] = S.decode_cls(s["cls"]) if "cls" in s else 0
-                yield out
-            except Exception:
-                if not self.train:
-                    raise
-                continue
+        yield from it
+
+    def _decode(self, rec):
+        """Decoded sample dict of a record, or None (train: a corrupt record is skipped)."""
+        if "synthetic" in rec:
+            parts = self.spec.split(":")
+            ncls = int(parts[2]) if len(parts) > 2 else 1000
+            rs = np.random.default_rng(rec["synthetic"])
+            arr = rs.integers(0, 256, (self.image_size + 32, self.image_size + 32, 3), dtype=np.uint8)
+            from PIL import Image
+            return {"jpg": Image.fromarray(arr), "cls": int(rs.integers(0, ncls))}
+        try:
+            out = {"jpg": S.decode_pil(rec["jpg"])}
+            if self.with_label:
+                out["cls"] = S.decode_cls(rec["cls"]) if "cls" in rec else 0
+            return out
+        except Exception:
+            if not self.train:
+                raise
+            return None
+
+    # kept for callers of the one-epoch decoded view
+    def _raw(self, epoch: int, wid: int, nw: int):
+        for rec in self._records(epoch, wid, nw):
+            s = self._decode(rec)
+            if s is not None:
+                yield s
 
     def __iter__(self):
         info = get_worker_info()
         wid, nw = (info.id, info.num_workers) if info is not None else (0, 1)
         random.seed(self.seed * 1000 + self.rank * 97 + wid)
         np.random.seed((self.seed * 1000 + self.rank * 97 + wid) % (2 ** 32))
-        epoch = 0
-        while True:
-            raw = self._raw(epoch, wid, nw)
-            if self.train and self.repeats > 1:
-                raw = repeat_samples(raw, self.repeats)
-            for s in raw:
+        if not self.train:
+            for s in self._raw(0, wid, nw):
                 img = self.transform(s["jpg"])
                 yield (img, s["cls"]) if self.with_label else img
-            if not self.train:
-                return
+            return
+        r = max(self.repeats, 1)
+        skip = worker_skip(self.skip_batches, wid, nw) * self.batch_size  # post-repeat samples
+        index = 0  # position in this worker's post-repeat sample stream
+        epoch = 0
+        while True:
+            for rec in self._records(epoch, wid, nw):
+                if skip >= r:  # the whole record (all its repeats) was consumed before the resume
+                    skip -= r
+                    index += r
+                    continue
+                s = self._decode(rec)
+                if s is None:
+                    continue
+                first, skip = skip, 0
+                index += first
+                for k in range(first, r):
+                    # repeated augmentation: deep copies of one decoded sample, own draws each
+                    seed = sample_seed(self.seed, self.rank, wid, index)
+                    random.seed(seed)
+                    np.random.seed(seed)
+                    img = self.transform(copy.deepcopy(s["jpg"]) if r > 1 else s["jpg"])
+                    index += 1
+                    yield (img, s["cls"]) if self.with_label else img
             epoch += 1
 
 
-def create_dataloaders(args, rank: int = 0, world: int = 1):
-    """Returns (train_loader | None, valid_loader | None) like dataset.py:100-161."""
+def create_dataloaders(args, rank: int = 0, world: int = 1, start_batches: int = 0):
+    """Returns (train_loader | None, valid_loader | None) like dataset.py:100-161.  ``start_batches``
+    (resume): train batches already consumed on this rank -- the stream continues after them."""
     train_t, valid_t = create_transforms(args.random_crop, args.image_size, args.auto_augment, args.color_jitter,
                                          args.random_erasing, args.test_crop_ratio)
     train_dl = valid_dl = None
     pin = torch.cuda.is_available()
     if getattr(args, "train_dataset_shards", None):
-        ds = ShardDataset(args.train_dataset_shards, args.mode, train_t, True, args.augment_repeats,
-                          args.shuffle_seed, rank, world, image_size=args.image_size)
         bs = args.train_batch_size // world // args.grad_accum
+        ds = ShardDataset(args.train_dataset_shards, args.mode, train_t, True, args.augment_repeats,
+                          args.shuffle_seed, rank, world, image_size=args.image_size,
+                          skip_batches=start_batches, batch_size=bs)
         nw = args.train_loader_workers
         train_dl = DataLoader(ds, batch_size=bs, num_workers=nw,
                               collate_fn=partial(collate_and_shuffle, repeats=args.augment_repeats),

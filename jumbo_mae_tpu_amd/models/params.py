@@ -21,6 +21,8 @@ checkpoint time.  Segments are padded to 64 elements (256 B) so vector kernels n
 
 from __future__ import annotations
 
+import contextlib
+
 import math
 from dataclasses import dataclass, field
 from typing import Callable, Iterable
@@ -133,7 +135,7 @@ class Handle:
 
     def note_use(self) -> None:
         """Record one differentiable forward use (the reducer expects one ``ready`` per use)."""
-        if self.store.use_hooks and self.segs[0].trainable and torch.is_grad_enabled():
+        if self.store.use_hooks and self.store.count_uses and self.segs[0].trainable and torch.is_grad_enabled():
             for fn in self.store.use_hooks:
                 fn(self)
 
@@ -154,7 +156,17 @@ class ParamStore:
         # gradient are final (the DP reducer may start reducing that slice early)
         self.partial_hooks: list[Callable[[Handle, int, int], None]] = []
         self._handles: list[Handle] = []
+        self.count_uses = True  # off while an activation-checkpoint recompute re-runs a forward
         self.version = 0  # bumped whenever the shadow changes (optimizer step, sync, load)
+
+    @contextlib.contextmanager
+    def uses_suppressed(self):
+        """Forward re-runs (activation-checkpoint recompute) record no parameter uses."""
+        prev, self.count_uses = self.count_uses, False
+        try:
+            yield
+        finally:
+            self.count_uses = prev
 
     # ---------------------------------------------------------------- building
     def add(self, path: Iterable[str], shape: tuple[int, ...], init, flax_shape=None,

@@ -295,7 +295,7 @@ def _run_layers(layers, x, rng, det, grad_ckpt):
     under activation checkpointing, whose recompute would re-run forwards out of order)."""
     if grad_ckpt and torch.is_grad_enabled():
         for layer in layers:
-            x = torch.utils.checkpoint.checkpoint(layer, x, rng, det, use_reentrant=False)
+            x = _checkpointed(layer, x, rng, det)
         return x
     link = None
     for i, layer in enumerate(layers):
@@ -308,6 +308,34 @@ def _run_layers(layers, x, rng, det, grad_ckpt):
         x = layer(x, rng, det, link_in=link, link_out=nxt)
         link = nxt
     return x
+
+
+def _checkpointed(layer, x, rng, det):
+    """One layer under activation checkpointing (reference ``nn.remat``, modeling.py:232,280).
+
+    The recompute in backward must see exactly the forward's random draws: droppath / dropout
+    masks come from the explicit ``rng`` generator, which ``torch.utils.checkpoint`` does not
+    restore.  So the generator state at the layer's entry is snapshotted; the first call runs on
+    the shared generator (advancing it as an un-checkpointed run would) and the recompute runs on
+    a private generator restored to the snapshot.  The recompute also re-records no parameter
+    uses: the data-parallel reducer expects one ``ready`` per FORWARD use, and backward runs once.
+    """
+    store = layer.norm1.g.store
+    state = rng.get_state() if rng is not None else None
+    calls = [0]
+
+    def run(inp):
+        calls[0] += 1
+        if calls[0] == 1:
+            return layer(inp, rng, det)
+        g = None
+        if rng is not None:
+            g = torch.Generator(device=rng.device)
+            g.set_state(state)
+        with store.uses_suppressed():
+            return layer(inp, g, det)
+
+    return torch.utils.checkpoint.checkpoint(run, x, use_reentrant=False)
 
 
 class MAEDecoder:

@@ -106,6 +106,11 @@ class GradReducer:
         self.partial_done[b] += hi - lo
 
     def _on_use(self, h: Handle) -> None:
+        # only the synchronising micro-step's uses are matched by counted backward writes
+        # (``_on_ready`` ignores no-sync micro-steps); counting the others would keep
+        # ``pending_uses`` above 0 and push every bucket to ``finish()`` (no overlap)
+        if not self.sync:
+            return
         for s in h.segs:
             i = self.seg_index.get(id(s))
             if i is not None:

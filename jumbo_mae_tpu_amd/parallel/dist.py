@@ -111,6 +111,15 @@ def all_reduce_max_scalar(x: float, device) -> float:
     return float(t.item())
 
 
+def all_gather_object(obj) -> list:
+    """Every rank's ``obj`` (picklable), in rank order, on every rank."""
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        out = [None] * dist.get_world_size()
+        dist.all_gather_object(out, obj)
+        return out
+    return [obj]
+
+
 def cleanup():
     if dist.is_available() and dist.is_initialized():
         dist.destroy_process_group()

@@ -79,7 +79,14 @@ def _extensions(p: argparse.ArgumentParser):
                    help="'auto' or a path prefix {output_dir}/{name}-last: resume params + optimizer + step")
     g.add_argument("--save-interval", type=int, default=0, help="also save 'last' every N steps (0: at eval)")
     g.add_argument("--compute-dtype", default="auto", choices=["auto", "bf16", "fp32"])
-    g.add_argument("--bucket-mb", type=float, default=64.0)
+    g.add_argument("--bucket-mb", type=float, default=64.0,
+                   help="data-parallel all-reduce bucket size (tools/allreduce_bench.py recommends one)")
+    g.add_argument("--reduce-dtype", default="fp32", choices=["fp32", "bf16"],
+                   help="gradient all-reduce dtype (bf16 halves the bytes on xGMI; master weights, "
+                        "optimizer state and the local gradient stay fp32)")
+    g.add_argument("--stop-after-steps", type=int, default=0,
+                   help="end this invocation after N steps, writing 'last' (time-sliced / preemptible "
+                        "jobs: continue with --resume auto); 0 = run to --training-steps")
     g.add_argument("--device", default=None, help="cuda|cpu (default: cuda if available)")
     g.add_argument("--log-file-only", action="store_true", help="never use wandb even if installed")
     g.add_argument("--trace-ranges", action="store_true", help="roctx ranges per step phase (rocprofv3 --marker-trace)")

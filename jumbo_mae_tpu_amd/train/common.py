@@ -47,7 +47,8 @@ def make_optimizer(args, store, peak_lr: float, end_value: float) -> FlatOptimiz
 
 def make_reducer(args, store):
     if pdist.info().world_size > 1:
-        return GradReducer(store, bucket_mb=args.bucket_mb)
+        dt = torch.bfloat16 if getattr(args, "reduce_dtype", "fp32") == "bf16" else torch.float32
+        return GradReducer(store, bucket_mb=args.bucket_mb, reduce_dtype=dt)
     return None
 
 
@@ -96,43 +97,99 @@ class DevicePrefetcher:
         return b
 
 
-def save_last(args, model, opt, step, rngs, extra_state=None, postfix="last"):
-    """Rank 0: params msgpack (Flax tree) + resume sidecar, both written in the background."""
+def rank_states(rngs, model) -> list:
+    """COLLECTIVE (every rank calls it at the same step): each rank's random state -- its device
+    streams (mixup / dropout / noise) and the host Mixup generator -- gathered in rank order.
+    Saved in the resume sidecar so that after ``--resume`` every rank continues its OWN streams
+    (the reference's per-device ``shard_prng_key`` independence), not rank 0's."""
+    mine = {"rngs": rngs.state_dict() if rngs is not None else {}}
+    mix = getattr(model, "mixup", None)
+    if mix is not None and getattr(mix, "rs", None) is not None:
+        mine["mixup_host"] = mix.rs.bit_generator.state
+    return pdist.all_gather_object(mine)
+
+
+def save_last(args, model, opt, step, rngs, extra_state=None, postfix="last", per_rank=None, best=None):
+    """Rank 0: params msgpack (Flax tree) + resume sidecar, both written in the background.
+
+    The sidecar holds the optimizer state, every rank's random state (``per_rank`` from
+    ``rank_states``), the data position (train batches consumed per rank) and the best
+    validation metric so far."""
     if not pdist.info().is_main:
         return None
     tree = model.flax_params()
-    if hasattr(model, "batch_stats") and model.batch_stats() is not None:
-        pass  # batch_stats live in the sidecar (reference does not save them at all)
     url = save_params(args.output_dir, args.name or "run", tree, postfix)
     state = {"step": step, "optimizer": opt.state_dict(), "rngs": rngs.state_dict() if rngs else {},
-             "time": time.time()}
+             "time": time.time(), "world_size": pdist.info().world_size,
+             "data": {"batches_per_rank": step * getattr(args, "grad_accum", 1)}}
+    if per_rank is not None:
+        state["rngs_per_rank"] = per_rank
+    if best is not None:
+        state["best"] = dict(best)
     if extra_state:
         state.update(extra_state)
     save_resume_state(ckpt_path(args.output_dir, args.name or "run", postfix, "state.pt"), state)
     return url
 
 
-def maybe_resume(args, model, opt, rngs, log=print):
-    """--resume auto|<prefix>: restore params, optimizer moments/count, RNG streams; returns step."""
+class Resumed(dict):
+    """What ``maybe_resume`` restored: step, data position and best metrics (empty = fresh run)."""
+
+    @property
+    def step(self) -> int:
+        return int(self.get("step", 0))
+
+    @property
+    def batches(self) -> int:
+        return int(self.get("data", {}).get("batches_per_rank", 0))
+
+    def best(self, key: str, default: float) -> float:
+        return float(self.get("best", {}).get(key, default))
+
+
+def maybe_resume(args, model, opt, rngs, log=print) -> Resumed:
+    """--resume auto|<prefix>: restore params, optimizer moments/count, this rank's RNG streams and
+    host Mixup generator; returns the step, data position and best metrics (``Resumed``)."""
     if not args.resume:
-        return 0
+        return Resumed()
     prefix = os.path.join(args.output_dir, f"{args.name or 'run'}-last") if args.resume == "auto" else args.resume
     pfile, sfile = prefix + ".msgpack", prefix + ".state.pt"
     if not (os.path.exists(pfile) and os.path.exists(sfile)):
         log(f"[resume] nothing to resume at {prefix}")
-        return 0
+        return Resumed()
     model.store.load_flax_tree(load_params(pfile), strict=True)
     st = load_resume_state(sfile)
     opt.load_state_dict(st["optimizer"])
-    if rngs is not None and st.get("rngs"):
-        rngs.load_state_dict(st["rngs"])
+    info = pdist.info()
+    per_rank = st.get("rngs_per_rank")
+    if per_rank is not None and len(per_rank) == info.world_size:
+        mine = per_rank[info.rank]
+        if rngs is not None and mine.get("rngs"):
+            rngs.load_state_dict(mine["rngs"])
+        mix = getattr(model, "mixup", None)
+        if mine.get("mixup_host") is not None and mix is not None and getattr(mix, "rs", None) is not None:
+            mix.rs.bit_generator.state = mine["mixup_host"]
+    elif rngs is not None:
+        # saved with another world size (or by an older version): fresh per-rank streams keyed by
+        # the step, so ranks stay independent and do not replay the first steps' draws
+        rngs.reseed(int(st["step"]))
+        log("[resume] world size changed or no per-rank RNG state: streams re-derived from (seed, rank, step)")
     if "batch_stats" in st and hasattr(model, "head") and getattr(model.head, "running_mean", None) is not None:
         model.head.running_mean.copy_(st["batch_stats"]["mean"])
         model.head.running_var.copy_(st["batch_stats"]["var"])
     pdist.broadcast_(model.store.master)
     model.store.sync_shadow()
     log(f"[resume] restored step {st['step']} from {prefix}")
-    return int(st["step"])
+    out = Resumed(step=int(st["step"]), best=st.get("best", {}))
+    if "data" in st and st.get("world_size", info.world_size) == info.world_size:
+        out["data"] = st["data"]
+    return out
+
+
+def stop_here(args, step: int, start: int) -> bool:
+    """--stop-after-steps: this invocation has run its share of steps."""
+    n = getattr(args, "stop_after_steps", 0)
+    return n > 0 and step - start >= n and step < args.training_steps
 
 
 def flush_checkpoints():

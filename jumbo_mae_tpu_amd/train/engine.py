@@ -101,8 +101,10 @@ class Trainer:
         metrics = {k: v / n for k, v in metrics_acc.items()}
         if self.skip_nonfinite:
             # opt-in guard (one host sync per step): drop the update of a step whose loss is
-            # not finite instead of poisoning the weights / optimizer moments
-            if not bool(torch.isfinite(metrics_acc["loss"]).item()):
+            # not finite instead of poisoning the weights / optimizer moments.
+            # The decision is GLOBAL: a NaN on one rank has already reached every rank through the
+            # gradient all-reduce, so every rank must skip together (a MAX over the ranks' flags)
+            if self.nonfinite_anywhere(metrics_acc["loss"]):
                 self.skipped_steps += 1
                 metrics["learning_rate"] = self.opt.last_lr if hasattr(self.opt, "last_lr") else 0.0
                 self._skipped = metrics
@@ -113,6 +115,15 @@ class Trainer:
             else:
                 self.opt.launch()
         return metrics
+
+    def nonfinite_anywhere(self, loss: torch.Tensor) -> bool:
+        """True when the loss is not finite on ANY rank of the data-parallel group."""
+        bad = (~torch.isfinite(loss.detach().float())).float().reshape(1)
+        r = self.reducer
+        if r is not None and r.enabled:
+            import torch.distributed as dist
+            dist.all_reduce(bad, op=dist.ReduceOp.MAX, group=r.group)
+        return bool(bad.item() > 0)
 
     def host_finish(self) -> float:
         return self.opt.finish()

@@ -78,14 +78,16 @@ def main(args) -> dict:
                       info.rank, device)
     trainer = Trainer(model, opt, reducer, rngs, args.grad_accum, skip_nonfinite=args.skip_nonfinite)
     run_step = StepRunner(trainer, hip_graph=args.hip_graph and device.type == "cuda" and info.world_size == 1)
-    start = C.maybe_resume(args, model, opt, rngs, log)
+    resumed = C.maybe_resume(args, model, opt, rngs, log)
+    start = resumed.step
 
     def extra():
         if not model.cfg.batch_norm:
             return None
         return {"batch_stats": {"mean": model.head.running_mean.cpu(), "var": model.head.running_var.cpu()}}
 
-    train_loader, valid_loader = create_dataloaders(args, info.rank, info.world_size)
+    # a resumed run continues the data stream after the batches the interrupted run consumed
+    train_loader, valid_loader = create_dataloaders(args, info.rank, info.world_size, resumed.batches)
     result = {}
     logger = Logger(args.output_dir, args.name, args.project, vars(args), enabled=info.is_main,
                     use_wandb=False if args.log_file_only else None)
@@ -94,10 +96,11 @@ def main(args) -> dict:
         logger.log(dict(result), start)
         log(f"[eval] step {start} {result}")
     meter = AverageMeter(use_latest=["learning_rate"])
-    max_acc1 = 0.0
+    max_acc1 = resumed.best("val/acc1", 0.0)
     it = C.DevicePrefetcher(train_loader, device) if train_loader is not None else None
     t0 = time.time()
     perf = C.PerfClock(start, args.train_batch_size, finetune_fwd_flops_per_image(model.cfg), info.world_size)
+    step = start
     for step in range(start + 1, args.training_steps + 1):
         micro = [tuple(next(it)) for _ in range(args.grad_accum)]
         metrics = run_step(micro)
@@ -114,21 +117,31 @@ def main(args) -> dict:
                 logger.log(summ, step)
                 log(f"[train] step {step} " + " ".join(f"{k}={v:.5g}" for k, v in summ.items()))
         do_eval = args.eval_interval > 0 and (step % args.eval_interval == 0 or step == args.training_steps)
-        if do_eval or (args.save_interval > 0 and step % args.save_interval == 0):
-            C.save_last(args, model, opt, step, rngs, extra())
+        stop = C.stop_here(args, step, start)
+        do_save = do_eval or stop or (args.save_interval > 0 and step % args.save_interval == 0)
+        # every rank's random state (collective), then rank 0 writes; "last" is written after the
+        # evaluation so that its sidecar carries the updated best metric
+        per_rank = C.rank_states(rngs, model) if do_save else None
         if do_eval and valid_loader is not None:
             res = evaluate(model, valid_loader, rngs, device)
+            if res["val/acc1"] > max_acc1:  # identical on every rank (all-reduced)
+                max_acc1 = res["val/acc1"]
+                C.save_last(args, model, opt, step, rngs, extra(), postfix="best", per_rank=per_rank,
+                            best={"val/acc1": max_acc1})
             if info.is_main:
-                if res["val/acc1"] > max_acc1:
-                    max_acc1 = res["val/acc1"]
-                    C.save_last(args, model, opt, step, rngs, extra(), postfix="best")
                 res["val/acc1/best"] = max_acc1
                 res["processed_samples"] = step * args.train_batch_size
                 logger.log(res, step)
                 log(f"[eval] step {step} {res}")
             result.update(res)
+        if do_save:
+            C.save_last(args, model, opt, step, rngs, extra(), per_rank=per_rank, best={"val/acc1": max_acc1})
+        if stop:
+            log(f"[train] --stop-after-steps: stopping at step {step}")
+            break
     C.flush_checkpoints()
     result["train_time_s"] = time.time() - t0
+    result["final_step"] = step
     logger.close()
     return result
 

@@ -6,8 +6,9 @@ Parity: /root/reference/src/main_pretrain.py:37-94 and create_train_state
   * "SANITATION CHECK" validation before training (skipped when there is no validation set, Q8);
   * metrics averaged over log_interval with the latest learning_rate, keys train/loss,
     train/learning_rate, processed_samples, val/loss, val/loss/best;
-  * at eval_interval (and the last step): rank 0 saves ``{name}-last.msgpack``, then evaluates and
-    saves ``{name}-best.msgpack`` on a new minimum validation loss.
+  * at eval_interval (and the last step): evaluates, saves ``{name}-best.msgpack`` on a new minimum
+    validation loss and ``{name}-last.msgpack`` (the reference writes "last" before the evaluation;
+    here it follows it so that its resume sidecar carries the updated best metric).
 Launch: ``torchrun --nproc-per-node 8 src/main_pretrain.py <reference flags>``.
 """
 
@@ -73,9 +74,11 @@ def main(args) -> dict:
                       info.rank, device)
     trainer = Trainer(model, opt, reducer, rngs, args.grad_accum, skip_nonfinite=args.skip_nonfinite)
     run_step = StepRunner(trainer, hip_graph=args.hip_graph and device.type == "cuda" and info.world_size == 1)
-    start = C.maybe_resume(args, model, opt, rngs, log)
+    resumed = C.maybe_resume(args, model, opt, rngs, log)
+    start = resumed.step
 
-    train_loader, valid_loader = create_dataloaders(args, info.rank, info.world_size)
+    # a resumed run continues the data stream after the batches the interrupted run consumed
+    train_loader, valid_loader = create_dataloaders(args, info.rank, info.world_size, resumed.batches)
     result = {}
     logger = Logger(args.output_dir, args.name, args.project, vars(args), enabled=info.is_main,
                     use_wandb=False if args.log_file_only else None)
@@ -84,11 +87,12 @@ def main(args) -> dict:
         logger.log(dict(result), start)
         log(f"[eval] step {start} {result}")
     meter = AverageMeter(use_latest=["learning_rate"])
-    min_val_loss = 1e9
+    min_val_loss = resumed.best("val/loss", 1e9)
     it = C.DevicePrefetcher(train_loader, device) if train_loader is not None else None
     t0 = time.time()
     perf = C.PerfClock(start, args.train_batch_size, pretrain_fwd_flops_per_image(model.cfg, model.dec_cfg),
                        info.world_size)
+    step = start
     for step in range(start + 1, args.training_steps + 1):
         micro = []
         for _ in range(args.grad_accum):
@@ -108,23 +112,31 @@ def main(args) -> dict:
                 logger.log(summ, step)
                 log(f"[train] step {step} " + " ".join(f"{k}={v:.5g}" for k, v in summ.items()))
         do_eval = args.eval_interval > 0 and (step % args.eval_interval == 0 or step == args.training_steps)
-        do_save = do_eval or (args.save_interval > 0 and step % args.save_interval == 0)
-        if do_save:
-            C.save_last(args, model, opt, step, rngs)
+        stop = C.stop_here(args, step, start)
+        do_save = do_eval or stop or (args.save_interval > 0 and step % args.save_interval == 0)
+        # every rank's random state (collective), then rank 0 writes; "last" is written after the
+        # evaluation so that its sidecar carries the updated best metric
+        per_rank = C.rank_states(rngs, model) if do_save else None
         if do_eval and valid_loader is not None:
             res = evaluate(model, valid_loader, rngs, device)
+            if res["val/loss"] < min_val_loss:  # identical on every rank (all-reduced)
+                min_val_loss = res["val/loss"]
+                C.save_last(args, model, opt, step, rngs, postfix="best", per_rank=per_rank,
+                            best={"val/loss": min_val_loss})
             if info.is_main:
-                if res["val/loss"] < min_val_loss:
-                    min_val_loss = res["val/loss"]
-                    C.save_last(args, model, opt, step, rngs, postfix="best")
                 res["val/loss/best"] = min_val_loss
                 res["processed_samples"] = step * args.train_batch_size
                 logger.log(res, step)
                 log(f"[eval] step {step} {res}")
             result.update(res)
+        if do_save:
+            C.save_last(args, model, opt, step, rngs, per_rank=per_rank, best={"val/loss": min_val_loss})
+        if stop:
+            log(f"[train] --stop-after-steps: stopping at step {step}")
+            break
     C.flush_checkpoints()
     result["train_time_s"] = time.time() - t0
-    result["final_step"] = args.training_steps
+    result["final_step"] = step
     logger.close()
     return result
 

@@ -43,6 +43,12 @@ class RngStreams:
     def state_dict(self) -> dict:
         return {k: g.get_state() for k, g in self.gens.items()}
 
+    def reseed(self, step: int) -> None:
+        """Streams keyed by (seed, stream, rank, step): used on a resume whose saved per-rank
+        states do not match this world size."""
+        for name, g in self.gens.items():
+            g.manual_seed(derive_seed(self.seeds.get(name, 0) * 1_000_003 + step, name, self.rank))
+
     def load_state_dict(self, d: dict) -> None:
         for k, s in d.items():
             if k in self.gens:

@@ -20,8 +20,10 @@ def main(argv=None):
     ap.add_argument("checkpoint")
     ap.add_argument("--exclude-heads", action="store_true", default=False)
     ap.add_argument("--output", default=None)
+    ap.add_argument("--image-size", type=int, default=224,
+                    help="input resolution of a sincos-posemb model (sets the exported pos_embed grid)")
     a = ap.parse_args(argv)
-    sd = flax_to_torch(load_params(a.checkpoint), exclude_heads=a.exclude_heads)
+    sd = flax_to_torch(load_params(a.checkpoint), exclude_heads=a.exclude_heads, image_size=a.image_size)
     out = a.output or a.checkpoint.replace(".msgpack", ".pth")
     torch.save({k: torch.from_numpy(v) for k, v in sd.items()}, out)
     print(f"wrote {len(sd)} tensors to {out}")

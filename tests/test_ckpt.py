@@ -88,6 +88,25 @@ def test_converters_roundtrip():
         np.testing.assert_allclose(fl_a[k], fl_b[k], atol=1e-6, err_msg=str(k))
 
 
+@pytest.mark.parametrize("image_size", [224, 448])
+def test_converter_sincos_grid_follows_image_size(image_size):
+    """A sincos model has no wpe leaf: the exported pos_embed grid comes from --image-size."""
+    from jumbo_mae_tpu_amd.utils.posemb import _sincos2d_np
+    vc = ViTConfig(layers=1, dim=32, heads=4, labels=10, image_size=image_size, patch_size=16, posemb="sincos2d",
+                   image_mask_ratio=None)
+    m = FinetuneModel(vc).to("cpu")
+    tree = m.flax_params()
+    sd = flax_to_torch(tree, image_size=image_size)
+    g = image_size // 16
+    assert sd["pos_embed"].shape == (1, 3 + g * g, 32)
+    np.testing.assert_allclose(sd["pos_embed"][0, 3:], _sincos2d_np(g, g, 32).reshape(g * g, 32), atol=1e-6)
+    back = torch_to_flax(sd, num_heads=4, learnable_posemb=False)
+    fl_a, fl_b = M.flatten_tree(tree), M.flatten_tree(back)
+    assert set(fl_a) == set(fl_b)
+    for k in fl_a:
+        np.testing.assert_allclose(fl_a[k], fl_b[k], atol=1e-6, err_msg=str(k))
+
+
 def test_load_pretrained_into_finetune(tmp_path):
     pre = _pre()
     pre.store.master.normal_()
