@@ -645,6 +645,263 @@ __global__ __launch_bounds__(512, 1) void gemm_nt64_kernel(const uint16_t* __res
     nt64_body<EPI, false, false, (SCHED & 4) != 0>(A, lda, B, ldb, M, N, K, ep, GROUP_M, smem);
 }
 
+// ------------------------------------------------------------------ 4-phase counted-vmcnt variant
+// Same 256 x 256 tile, 8 waves (2 x 4, 128 x 64 each) and epilogues as nt64_body; the K loop is
+// cut into half-tile LDS slots so that loads stay in flight ACROSS barriers (counted vmcnt, never
+// 0 in steady state) instead of draining every stage:
+//   * a K-tile (64 deep) is 4 slots of 128 rows x 128 B: a0 / a1 = the A rows of the waves' upper
+//     / lower 64-row halves (rows wr*128 + mh*64 + [0,64) for both wr), b0 / b1 = the B rows of the
+//     waves' left / right 32-column halves (wc*64 + nh*32 + [0,32) for all wc);
+//   * 8 slots = two K-tiles in LDS (128 KB); each wave runs 4 phases per K-tile, one 64 x 32
+//     quadrant (mh, nh) x K = 64 = 16 MFMAs each, in the order (0,0) (0,1) (1,1) (1,0), so a
+//     phase needs at most one new operand half;
+//   * fragments are read one phase ahead of their MFMAs (registers: A_X/A_Y, two B sets whose
+//     roles swap every K-tile -- hence 2 K-tiles per loop trip): q4 reads a0,b0 of the next
+//     tile, q1 reads b1, q2 reads a1, q3 reads nothing;
+//   * every phase starts with [vmcnt(N) lgkmcnt(0) s_barrier] and then issues ONE slot load (2
+//     glds per thread) for the tile after next: q1 a0, q2 b1, q3 a1, q4 b0 -- each slot is
+//     refilled the phase after its last read, A slots 7 phases and b0 (weights, L2-resident) 4
+//     phases before they are read;
+//   * N per phase start (loads issued after the one that must have landed): q1 12, q2 12, q3 none,
+//     q4 6; the last two K-tiles issue nothing and count down (12 10 - 0 | 4 2 - -).
+// Slot rows are 128 B; 16-B chunks XOR-swizzled by swz64(slot row) on the per-lane global source
+// and on the ds_read address (conflict-free ds_read_b128, the nt64 image).
+// SCHED (A/B bits): 1 = s_setprio 1 around each phase's MFMA cluster; 2 = the phase's two glds
+// issued inside the MFMA stream (after MFMAs 1 and 5) instead of right after the barrier; 4 = waves
+// 4-7 run at priority 1 throughout (static young-half priority).  Diagnostics only (wrong results
+// by design, tools/gemm_nt_bench.py): 8 = no loads after the prologue, 16 = no vmcnt waits,
+// 32 = no barriers.
+template <int EPI, int SCHED>
+__attribute__((always_inline)) JM_DEVICE void p4_body(const uint16_t* __restrict__ A, long lda,
+                                                      const uint16_t* __restrict__ B, long ldb, int M, int N, int K,
+                                                      const GemmEpi& ep, int GROUP_M, uint16_t* smem) {
+  constexpr int NTW = 4, BK2 = 64, SLOT = 128 * BK2;  // elements per slot (16 KB)
+  const int tid = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+  const int l16 = lane & 15, g = lane >> 4;
+  const int wr = wave >> 2, wc = wave & 3;
+
+  int m0, n0, split = 0;
+  tile_of(M, N, GROUP_M, m0, n0, EPI == EPI_PARTIAL ? ep.splits : 1, EPI == EPI_PARTIAL ? &split : nullptr);
+  int k_begin = 0;
+  if (EPI == EPI_PARTIAL) {
+    const int ku = K / 128;  // splits take whole 128-deep units (even tile count per split)
+    const int ku0 = split * ku / ep.splits, ku1 = (split + 1) * ku / ep.splits;
+    k_begin = ku0 * 128;
+    K = (ku1 - ku0) * 128;
+  }
+  const __amdgpu_buffer_rsrc_t ra = make_rsrc(A + (long)m0 * lda + k_begin, (long)(M - m0) * lda * 2 - 2L * k_begin);
+  const __amdgpu_buffer_rsrc_t rb = make_rsrc(B + (long)n0 * ldb + k_begin, (long)(N - n0) * ldb * 2 - 2L * k_begin);
+  // glds pieces: slot rows q*8 + (lane >> 3), q = 2 * wave + r; slot row -> tile row / column
+  uint32_t a_src[2][2], b_src[2][2];  // [half][r] byte offsets
+#pragma unroll
+  for (int r = 0; r < 2; ++r) {
+    const int srow = (2 * wave + r) * 8 + (lane >> 3);
+    const int c = (lane & 7) ^ swz64(srow);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int arow = (srow >> 6) * 128 + h * 64 + (srow & 63);
+      const int bcol = (srow >> 5) * 64 + h * 32 + (srow & 31);
+      a_src[h][r] = (uint32_t)((arow * lda + c * 8) * 2);
+      b_src[h][r] = (uint32_t)((bcol * ldb + c * 8) * 2);
+    }
+  }
+  // slot index within a K-tile set: 0 = a0, 1 = a1, 2 = b0, 3 = b1
+  auto issue = [&](int t, auto slot) {
+    constexpr int S = decltype(slot)::value;
+    if constexpr ((SCHED & 8) != 0) {
+      if (t >= 2) return;  // ablation: no loads after the prologue
+    }
+    const uint32_t k0b = t * BK2 * 2;
+    uint16_t* l = smem + ((t & 1) * 4 + S) * SLOT + (2 * wave) * 8 * BK2;
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      if constexpr (S < 2) blds16(ra, a_src[S][r], k0b, l + r * 8 * BK2);
+      else blds16(rb, b_src[S - 2][r], k0b, l + r * 8 * BK2);
+    }
+  };
+  const int ch0 = ((0 * 4 + g) ^ swz64(l16)) * 8, ch1 = ((1 * 4 + g) ^ swz64(l16)) * 8;
+  const int a_row = (wr * 64 + l16) * BK2, b_row = (wc * 32 + l16) * BK2;
+  typedef bf16x8_t AF[4][2];  // [mt within the half][k32 step]
+  typedef bf16x8_t BF[2][2];  // [nt within the half][k32 step]
+  auto read_a = [&](int t, auto half, AF& f) {
+    const uint16_t* base = smem + ((t & 1) * 4 + decltype(half)::value) * SLOT + a_row;
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) {
+      f[mt][0] = lds8(base + mt * 16 * BK2 + ch0);
+      f[mt][1] = lds8(base + mt * 16 * BK2 + ch1);
+    }
+  };
+  auto read_b = [&](int t, auto half, BF& f) {
+    const uint16_t* base = smem + ((t & 1) * 4 + 2 + decltype(half)::value) * SLOT + b_row;
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt) {
+      f[nt][0] = lds8(base + nt * 16 * BK2 + ch0);
+      f[nt][1] = lds8(base + nt * 16 * BK2 + ch1);
+    }
+  };
+  f32x4_t acc[8][NTW];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < NTW; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  auto mfma_q = [&](auto mh, auto nh, const AF& a, const BF& b) {
+    constexpr int MH = decltype(mh)::value, NH = decltype(nh)::value;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt)
+          acc[MH * 4 + mt][NH * 2 + nt] = mfma16(b[nt][kk], a[mt][kk], acc[MH * 4 + mt][NH * 2 + nt]);
+  };
+  auto sync = [&](auto n) {  // vmcnt(n) lgkmcnt(0) s_barrier; n < 0: no vmcnt wait
+    constexpr int V = (SCHED & 16) ? -1 : decltype(n)::value;
+    if constexpr ((SCHED & 32) != 0) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    else if constexpr (V == 12) asm volatile("s_waitcnt vmcnt(12) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    else if constexpr (V == 10) asm volatile("s_waitcnt vmcnt(10) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    else if constexpr (V == 6) asm volatile("s_waitcnt vmcnt(6) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    else if constexpr (V == 4) asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    else if constexpr (V == 2) asm volatile("s_waitcnt vmcnt(2) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    else if constexpr (V == 0) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    else asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  // the phase's instruction order: its ds_reads spread over the 16 MFMAs (one after each of the
+  // first NR MFMAs when NR > 8, else one every 16 / NR), with SCHED & 2 the glds after MFMAs 1, 5
+  auto interleave = [&](auto nreads, auto nglds) {
+    constexpr int NR = decltype(nreads)::value, NG = (SCHED & 2) ? decltype(nglds)::value : 0;
+    constexpr int PER = NR > 8 ? 1 : 16 / (NR > 0 ? NR : 1);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      if (i % PER == 0 && i / PER < NR) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      if (NG > 0 && (i == 1 || i == 5)) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  auto prio = [&](auto p) {
+    if constexpr ((SCHED & 1) != 0) __builtin_amdgcn_s_setprio(decltype(p)::value);
+  };
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  using I2 = std::integral_constant<int, 2>;
+  using I3 = std::integral_constant<int, 3>;
+  using I4 = std::integral_constant<int, 4>;
+  using I6 = std::integral_constant<int, 6>;
+  using I8 = std::integral_constant<int, 8>;
+  using I10 = std::integral_constant<int, 10>;
+  using I12 = std::integral_constant<int, 12>;
+  using I16 = std::integral_constant<int, 16>;
+  using IN = std::integral_constant<int, -1>;
+  using IX = std::integral_constant<int, -2>;  // no barrier at all
+
+  AF ax, ay;
+  BF bp, bq;
+  // one K-tile: b0 holds its b0 fragments (read during the previous tile's q4), b1 receives b1 and
+  // then the next tile's b0.  KIND 2 = steady (issues tile t + 2), 1 = next-to-last, 0 = last.
+  auto tile = [&](auto kind, int t, BF& b0, BF& b1) {
+    constexpr int KIND = decltype(kind)::value;
+    using G = std::integral_constant<int, KIND == 2 ? 2 : 0>;
+    // q1 (0,0): read b1(t)
+    sync(std::conditional_t<KIND == 0, I4, I12>{});
+    prio(I1{});
+    if constexpr (KIND == 2) issue(t + 2, I0{});
+    read_b(t, I1{}, b1);
+    mfma_q(I0{}, I0{}, ax, b0);
+    interleave(I4{}, G{});
+    prio(I0{});
+    // q2 (0,1): read a1(t)
+    sync(std::conditional_t<KIND == 0, I2, std::conditional_t<KIND == 1, I10, I12>>{});
+    prio(I1{});
+    if constexpr (KIND == 2) issue(t + 2, I3{});
+    read_a(t, I1{}, ay);
+    mfma_q(I0{}, I1{}, ax, b1);
+    interleave(I8{}, G{});
+    prio(I0{});
+    // q3 (1,1): no reads
+    sync(IN{});
+    prio(I1{});
+    if constexpr (KIND == 2) issue(t + 2, I1{});
+    mfma_q(I1{}, I1{}, ay, b1);
+    interleave(I0{}, G{});
+    prio(I0{});
+    // q4 (1,0): read a0(t+1), b0(t+1) (into b1, free after q3)
+    if constexpr (KIND > 0) {
+      sync(std::conditional_t<KIND == 1, I0, I6>{});
+      prio(I1{});
+      if constexpr (KIND == 2) issue(t + 2, I2{});
+      read_a(t + 1, I0{}, ax);
+      read_b(t + 1, I0{}, b1);
+      mfma_q(I1{}, I0{}, ay, b0);
+      interleave(I12{}, G{});
+      prio(I0{});
+    } else {
+      mfma_q(I1{}, I0{}, ay, b0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+  using K2 = std::integral_constant<int, 2>;
+  using K1 = std::integral_constant<int, 1>;
+  using K0 = std::integral_constant<int, 0>;
+
+  const int nk = K / BK2;  // even, >= 2
+  // prologue: tiles 0 and 1 in the steady-state issue order (a0 b1 a1 | b0), so the counted
+  // waits of the first tiles hold unchanged
+  issue(0, I0{});
+  issue(0, I3{});
+  issue(0, I1{});
+  issue(0, I2{});
+  issue(1, I0{});
+  issue(1, I3{});
+  issue(1, I1{});
+  sync(I6{});
+  issue(1, I2{});
+  read_a(0, I0{}, ax);
+  read_b(0, I0{}, bp);
+  int t = 0;
+  for (; t + 4 <= nk; t += 2) {  // tiles t, t+1 with t + 3 < nk: both steady
+    tile(K2{}, t, bp, bq);
+    tile(K2{}, t + 1, bq, bp);
+  }
+  // nk - t == 2: the last two tiles (nk - 2 -> KIND 1, nk - 1 -> KIND 0)
+  tile(K1{}, t, bp, bq);
+  tile(K0{}, t + 1, bq, bp);
+  (void)IX{};
+  (void)I16{};
+
+  if (EPI == EPI_PARTIAL) {
+    float* dst = ep.part + (long)split * M * N;
+#pragma unroll
+    for (int mt = 0; mt < 8; ++mt) {
+      const int m = m0 + wr * 128 + mt * 16 + l16;
+      if (m >= M) continue;
+#pragma unroll
+      for (int nt = 0; nt < NTW; ++nt) {
+        const int n = n0 + wc * NTW * 16 + nt * 16 + 4 * g;
+        if (n >= N) continue;
+        float v[4] = {acc[mt][nt][0], acc[mt][nt][1], acc[mt][nt][2], acc[mt][nt][3]};
+        store4(dst + (long)m * N + n, v);
+      }
+    }
+  } else if (N % 8 == 0)
+    epilogue_lds<EPI, NTW, 512, BN, true>(acc, ep, smem, M, N, m0, n0, wr, wc, l16, g);
+  else
+    epilogue<EPI, NTW>(acc, ep, M, N, m0 + wr * 128, n0 + wc * NTW * 16, l16, g);
+}
+
+template <int EPI, int SCHED>
+__global__ __launch_bounds__(512, 1) void gemm_p4_kernel(const uint16_t* __restrict__ A, long lda,
+                                                         const uint16_t* __restrict__ B, long ldb, int M, int N,
+                                                         int K, GemmEpi ep, int GROUP_M) {
+  JM_DGUARD(blockDim.x == 512 && K % 128 == 0 && M > 0 && N > 0);
+  extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
+  if constexpr ((SCHED & 4) != 0) {
+    if (__builtin_amdgcn_readfirstlane(threadIdx.x) >= 256) __builtin_amdgcn_s_setprio(1);
+  }
+  p4_body<EPI, SCHED & ~4>(A, lda, B, ldb, M, N, K, ep, GROUP_M, smem);
+}
+
 // ------------------------------------------------------------------ half-width, 2 WGs per CU
 // 256 x 128 output tile, 4 waves (2 x 2, each the usual 128 x 64 sub-tile, 128 accumulator VGPRs),
 // 32-deep K steps through a 3-stage ring of 24 KB stages (72 KB): two workgroups fit on one CU
@@ -1102,7 +1359,9 @@ __global__ __launch_bounds__(256) void tail_finish_kernel(GemmEpi ep, int M, int
 size_t jm_gemm_smem() { return (size_t)NST * STAGE * sizeof(uint16_t); }
 
 // returns 0 on success, <0 on unsupported shape
-int g_gemm_wn = 12;    // runtime switches for A/B (jm_gemm_set_variant): 12 = 64-deep stages + nontemporal
+int g_gemm_wn = 20;    // runtime switches for A/B (jm_gemm_set_variant): 20-83 = the 4-phase counted-vmcnt
+                       // kernel + SCHED bits (default 24: static young-half priority;
+                       // profiles/r2_gemm_p4.txt), 12 = 64-deep stages + nontemporal
                        // epilogue stores (default; profiles/r1_gemm_nt_stores.txt), 6 = 64-deep stages,
                        // 10/11 = 256x128 tiles, 2 WGs per CU (no stagger / stagger),
                        // 4 = 32-deep ring, 2 = 4 waves, 5 = persistent, 4x = ablations
@@ -1158,6 +1417,39 @@ void launch_nt64(const uint16_t* A, long lda, const uint16_t* B, long ldb, int M
   gemm_nt64_kernel<EPI, SCHED><<<nwg, 512, sm, st>>>(A, lda, B, ldb, M, N, K, ep, g_gemm_group);
 }
 
+template <int EPI, int SCHED>
+void launch_p4s(const uint16_t* A, long lda, const uint16_t* B, long ldb, int M, int N, int K, const GemmEpi& ep,
+                int nwg, hipStream_t st) {
+  static bool attr = false;
+  const size_t sm = jm_gemm_smem();  // 8 x 16 KB slots
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)gemm_p4_kernel<EPI, SCHED>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)sm);
+    attr = true;
+  }
+  gemm_p4_kernel<EPI, SCHED><<<nwg, 512, sm, st>>>(A, lda, B, ldb, M, N, K, ep, g_gemm_group);
+}
+
+int g_p4_sched = 4;  // A/B: variant 20 + SCHED bits (variants 21..83 = 20 + bits)
+
+template <int EPI>
+void launch_p4(const uint16_t* A, long lda, const uint16_t* B, long ldb, int M, int N, int K, const GemmEpi& ep,
+               int nwg, hipStream_t st) {
+  switch (g_p4_sched) {
+    default: break;
+    case 1: return launch_p4s<EPI, 1>(A, lda, B, ldb, M, N, K, ep, nwg, st);
+    case 2: return launch_p4s<EPI, 2>(A, lda, B, ldb, M, N, K, ep, nwg, st);
+    case 3: return launch_p4s<EPI, 3>(A, lda, B, ldb, M, N, K, ep, nwg, st);
+    case 4: return launch_p4s<EPI, 4>(A, lda, B, ldb, M, N, K, ep, nwg, st);
+    case 6: return launch_p4s<EPI, 6>(A, lda, B, ldb, M, N, K, ep, nwg, st);
+    case 12: if constexpr (EPI == EPI_STORE) return launch_p4s<EPI, 12>(A, lda, B, ldb, M, N, K, ep, nwg, st); break;
+    case 20: if constexpr (EPI == EPI_STORE) return launch_p4s<EPI, 20>(A, lda, B, ldb, M, N, K, ep, nwg, st); break;
+    case 52: if constexpr (EPI == EPI_STORE) return launch_p4s<EPI, 52>(A, lda, B, ldb, M, N, K, ep, nwg, st); break;
+    case 60: if constexpr (EPI == EPI_STORE) return launch_p4s<EPI, 60>(A, lda, B, ldb, M, N, K, ep, nwg, st); break;
+  }
+  return launch_p4s<EPI, 0>(A, lda, B, ldb, M, N, K, ep, nwg, st);
+}
+
 template <int EPI, bool STAGGER>
 void launch_nth(const uint16_t* A, long lda, const uint16_t* B, long ldb, int M, int N, int K, const GemmEpi& ep,
                 hipStream_t st) {
@@ -1175,6 +1467,11 @@ void launch_nth(const uint16_t* A, long lda, const uint16_t* B, long ldb, int M,
 template <int EPI>
 void launch_epi(const uint16_t* A, long lda, const uint16_t* B, long ldb, int M, int N, int K, const GemmEpi& ep,
                 int nwg, hipStream_t st) {
+  if (g_gemm_wn == 20) {  // K in 128-deep units (split-K: per split); else the 64-deep kernel
+    if (K % 128 == 0 && (EPI != EPI_PARTIAL || K / 128 >= ep.splits))
+      return launch_p4<EPI>(A, lda, B, ldb, M, N, K, ep, nwg, st);
+    return launch_nt64<EPI, 4>(A, lda, B, ldb, M, N, K, ep, nwg, st);
+  }
   if (g_gemm_wn == 6) return launch_nt64<EPI, 0>(A, lda, B, ldb, M, N, K, ep, nwg, st);
   if (g_gemm_wn == 12) return launch_nt64<EPI, 4>(A, lda, B, ldb, M, N, K, ep, nwg, st);
   if (g_gemm_wn == 10) return launch_nth<EPI, false>(A, lda, B, ldb, M, N, K, ep, st);
@@ -1236,6 +1533,10 @@ void launch_tail(const uint16_t* A, long lda, const uint16_t* B, long ldb, int M
 }  // namespace
 
 void jm_gemm_set_variant(int wn, int group) {
+  if (wn >= 20 && wn < 84) {  // 4-phase kernel + SCHED bits
+    g_p4_sched = wn - 20;
+    wn = 20;
+  }
   g_gemm_wn = wn;
   g_gemm_group = group;
 }
@@ -1292,8 +1593,12 @@ int jm_gemm_nt(const uint16_t* A, long lda, const uint16_t* B, long ldb, int M, 
     launch_epi<EPI_GELU_ONLY>(A, lda, B, ldb, M, N, K, ep, nwg, st);
   else if (epi == EPI_DGELU && N % 8 == 0)
     launch_epi<EPI_DGELU>(A, lda, B, ldb, M, N, K, ep, nwg, st);
+  else if (epi == EPI_GELU_D && g_gemm_wn == 20 && K % 128 == 0)
+    launch_p4<EPI_GELU_D>(A, lda, B, ldb, M, N, K, ep, nwg, st);
   else if (epi == EPI_GELU_D)  // default kernel only (no A/B variants for the saved-derivative pair)
     launch_nt64<EPI_GELU_D, 4>(A, lda, B, ldb, M, N, K, ep, nwg, st);
+  else if (epi == EPI_DMUL && N % 8 == 0 && g_gemm_wn == 20 && K % 128 == 0)
+    launch_p4<EPI_DMUL>(A, lda, B, ldb, M, N, K, ep, nwg, st);
   else if (epi == EPI_DMUL && N % 8 == 0)
     launch_nt64<EPI_DMUL, 4>(A, lda, B, ldb, M, N, K, ep, nwg, st);
   else

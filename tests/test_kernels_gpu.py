@@ -18,7 +18,7 @@ def ext():
 def _reset_gemm_variant(request):
     yield
     if "ext" in request.fixturenames:
-        request.getfixturevalue("ext").gemm_set_variant(12, 8)
+        request.getfixturevalue("ext").gemm_set_variant(24, 8)
         request.getfixturevalue("ext").ln_set_bwd_la(2)
         request.getfixturevalue("ext").attn_set_bwd_ppw(0)
         request.getfixturevalue("ext").gemm_tn_set_acc0(0)
@@ -200,7 +200,7 @@ def test_optimizer_hip_matches_torch(kind, clip):
     assert rel(res[0], res[1]) < 1e-5
 
 
-@pytest.mark.parametrize("variant", [4, 2, 5, 6, 7, 8, 10, 11, 12])
+@pytest.mark.parametrize("variant", [4, 2, 5, 6, 7, 8, 10, 11, 12, 20, 21, 22, 24])
 @pytest.mark.parametrize("M,N,K,gelu", [(512, 256, 64, False), (300, 196, 128, True), (1000, 1536, 512, False),
                                         (257, 260, 192, True), (16100, 2048, 128, True), (40000, 520, 64, False)])
 def test_gemm_nt(ext, M, N, K, gelu, variant):
@@ -216,7 +216,7 @@ def test_gemm_nt(ext, M, N, K, gelu, variant):
     if gelu:
         g_ref = torch.nn.functional.gelu(outs[0].float(), approximate="tanh")
         assert rel(outs[1], g_ref) < 1e-2
-    ext.gemm_set_variant(12, 8)
+    ext.gemm_set_variant(24, 8)
 
 
 @pytest.mark.parametrize("B,S,H,hd", [(2, 300, 4, 64), (1, 787, 3, 64), (2, 225, 2, 32), (1, 787, 2, 32)])
@@ -246,7 +246,7 @@ def test_attention_long_sequence_path(ext, B, S, H, hd):
     assert torch.equal(dqkv, dqkv2)  # one writer per element: deterministic
 
 
-@pytest.mark.parametrize("variant", [4, 6, 10, 11, 12])
+@pytest.mark.parametrize("variant", [4, 6, 10, 11, 12, 24])
 @pytest.mark.parametrize("M,N,K", [(512, 256, 64), (1000, 1536, 512), (300, 512, 128)])
 def test_gemm_nt_dgelu(ext, M, N, K, variant):
     """FF2 data gradient through the GELU with the FF1 bias gradient (csrc/gemm.hip EPI_DGELU)."""
@@ -336,7 +336,7 @@ def test_residual_ln_fwd_partial_rows(ext, D):
     assert torch.allclose(mu, mur, atol=1e-6) and torch.allclose(rs, rsr, rtol=1e-5)
 
 
-@pytest.mark.parametrize("variant", [4, 6, 10, 11, 12])
+@pytest.mark.parametrize("variant", [4, 6, 10, 11, 12, 24])
 @pytest.mark.parametrize("M,N,K,S", [(512, 3072, 12288, 10), (300, 512, 4096, 3), (512, 256, 1024, 16)])
 def test_gemm_nt_splitk(ext, M, N, K, S, variant):
     """Split-K MFMA GEMM (fp32 partial tiles + bf16 reduce with bias), ragged M."""
@@ -460,8 +460,9 @@ def test_gemm_splitk_fused_fp32_add(ext):
     assert rel(ext.gemm_nt_splitk(A, B, None, 10), ref) < 1e-2
 
 
+@pytest.mark.parametrize("variant", [12, 24])
 @pytest.mark.parametrize("M,N,K", [(1000, 512, 256), (600, 1000, 128)])
-def test_gemm_gelu_saved_derivative(ext, M, N, K):
+def test_gemm_gelu_saved_derivative(ext, M, N, K, variant):
     """FF1 forward saving gelu'(h) (EPI_GELU_D) and the FF2 data gradient multiplying by it
     (EPI_DMUL) == the h-saving pair (EPI_GELU / EPI_DGELU); the unfused gelu_bwd(deriv) too."""
     torch.manual_seed(0)

@@ -41,13 +41,15 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--only", default="")
     ap.add_argument("--kinds", default="fwd,fwd_gelu,dgrad")
-    ap.add_argument("--variant", type=int, default=6, help="kernel variant (see jm_gemm_set_variant)")
+    ap.add_argument("--variant", default="12", help="kernel variant(s), comma separated (jm_gemm_set_variant); "
+                    "several = interleaved A/B in this process")
     ap.add_argument("--group", type=int, default=8, help="row tiles per column sweep")
     ap.add_argument("--tail", type=int, default=0, help="tail split of the last partial wave (1 = on)")
     a = ap.parse_args()
     ext = _ext.load()
     ext.gemm_set_tail(a.tail)
-    ext.gemm_set_variant(a.variant, a.group)
+    variants = [int(v) for v in a.variant.split(",")]
+    ext.gemm_set_variant(variants[0], a.group)
     names = [n for n in FWD if not a.only or n in a.only.split(",")]
     tot = {"ours": 0.0, "blas": 0.0}
     for kind in a.kinds.split(","):
@@ -87,6 +89,13 @@ def main():
             else:
                 ours = lambda: ext.gemm_nt(x, w, b, False)  # noqa: E731
                 blas = lambda: torch.addmm(bb, x, w.t())  # noqa: E731
+            errs = []
+            for v in variants:
+                ext.gemm_set_variant(v, a.group)
+                o = ours()
+                r0 = torch.addmm(b, x.float(), w.float().t()) if kind != "dgrad_gelu" else o[0].float()
+                errs.append(((o[0].float() - r0).abs().max() / r0.abs().max()).item())
+            ext.gemm_set_variant(variants[0], a.group)
             out = ours()
             ref = torch.addmm(b, x.float(), w.float().t()) if kind != "dgrad_gelu" else out[0].float()
             err = ((out[0].float() - ref).abs().max() / ref.abs().max()).item()
@@ -95,11 +104,19 @@ def main():
                 err = max(err, ((out[1].float() - g_ref).abs().max() / g_ref.abs().max()).item())
             blas()
             torch.cuda.synchronize()
-            to, tb = [], []
+            tv = {v: [] for v in variants}
+            tb = []
             for _ in range(a.rounds):
-                to.append(timeit(ours, a.iters))
+                for v in variants:
+                    ext.gemm_set_variant(v, a.group)
+                    tv[v].append(timeit(ours, a.iters))
                 tb.append(timeit(blas, a.iters))
-            to, tb = min(to), min(tb)
+            ext.gemm_set_variant(variants[0], a.group)
+            to, tb = min(tv[variants[0]]), min(tb)
+            if len(variants) > 1:
+                fl = 2.0 * M * N * K
+                print("   " + "  ".join(f"v{v}: {min(tv[v]):7.1f} us {fl / min(tv[v]) / 1e6:5.0f} TF err {e:.1e}"
+                                        for v, e in zip(variants, errs)), flush=True)
             fl = 2.0 * M * N * K
             tot["ours"] += to
             tot["blas"] += tb

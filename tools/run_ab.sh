@@ -1,6 +1,6 @@
+# step-level interleaved A/B: tools/run_ab.sh <outdir> <config>...
 set -o pipefail
 export TMPDIR=/tmp
-R=$GRAFT_REPO_ROOT
-cd $R
-timeout -k 10 300 python -m jumbo_mae_tpu_amd.csrc.build > gpurun_out/build.log 2>&1 || { echo BUILD FAIL; tail -20 gpurun_out/build.log; exit 1; }
-timeout -k 10 400 python -m pytest -q -x tests/test_dist_gpu.py > gpurun_out/dg.txt 2>&1; rc=$?; tail -15 gpurun_out/dg.txt; exit $rc
+R=$GRAFT_REPO_ROOT; cd $R; O=gpurun_out/$1; shift; mkdir -p $O
+timeout -k 10 500 python -u tools/ab_bench.py --configs "$@" --rounds 4 --steps 6 > $O/ab.txt 2>&1 || { tail -20 $O/ab.txt; exit 1; }
+tail -8 $O/ab.txt
