@@ -194,7 +194,8 @@ JM_DEVICE void epilogue_lds(const f32x4_t (&acc)[8][NTW], const GemmEpi& ep, uin
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
   constexpr int LPR = BNT / 8;        // lanes per row (16 B each)
   constexpr int RPP = NTH / LPR;      // rows per pass
-  const int tid = threadIdx.x;
+  int tid = threadIdx.x;
+  asm volatile("" : "+v"(tid));  // not hoisted out of a persistent kernel's item loop
   const int c = tid % LPR;
   const bool col_ok = n0 + c * 8 < N;
   // EPI_DGELU / EPI_DMUL: the first PF of this thread's aux rows are loaded before the accumulators
@@ -671,25 +672,22 @@ __global__ __launch_bounds__(512, 1) void gemm_nt64_kernel(const uint16_t* __res
 // 4-7 run at priority 1 throughout (static young-half priority).  Diagnostics only (wrong results
 // by design, tools/gemm_nt_bench.py): 8 = no loads after the prologue, 16 = no vmcnt waits,
 // 32 = no barriers.
-template <int EPI, int SCHED>
-__attribute__((always_inline)) JM_DEVICE void p4_body(const uint16_t* __restrict__ A, long lda,
-                                                      const uint16_t* __restrict__ B, long ldb, int M, int N, int K,
-                                                      const GemmEpi& ep, int GROUP_M, uint16_t* smem) {
+// acc = A[m0:m0+256, k_begin:k_begin+K] . B[n0:n0+256, same]^T  (K % 128 == 0, K > 0); every LDS
+// slot is free on entry (caller's barrier) and the ring is drained on exit except for the reads
+// of the last K-tile's MFMAs (caller's epilogue barriers before reusing LDS).
+template <int SCHED>
+__attribute__((always_inline)) JM_DEVICE void p4_mainloop(const uint16_t* __restrict__ A, long lda,
+                                                          const uint16_t* __restrict__ B, long ldb, int M, int N,
+                                                          int m0, int n0, int k_begin, int K, f32x4_t (&acc)[8][4],
+                                                          uint16_t* smem) {
   constexpr int NTW = 4, BK2 = 64, SLOT = 128 * BK2;  // elements per slot (16 KB)
-  const int tid = threadIdx.x;
+  int tid = threadIdx.x;
+  // opaque copy: in the persistent kernel the per-lane offsets below are then recomputed per work
+  // item instead of being hoisted out of its item loop (they would stay live across the K loop)
+  asm volatile("" : "+v"(tid));
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
   const int l16 = lane & 15, g = lane >> 4;
   const int wr = wave >> 2, wc = wave & 3;
-
-  int m0, n0, split = 0;
-  tile_of(M, N, GROUP_M, m0, n0, EPI == EPI_PARTIAL ? ep.splits : 1, EPI == EPI_PARTIAL ? &split : nullptr);
-  int k_begin = 0;
-  if (EPI == EPI_PARTIAL) {
-    const int ku = K / 128;  // splits take whole 128-deep units (even tile count per split)
-    const int ku0 = split * ku / ep.splits, ku1 = (split + 1) * ku / ep.splits;
-    k_begin = ku0 * 128;
-    K = (ku1 - ku0) * 128;
-  }
   const __amdgpu_buffer_rsrc_t ra = make_rsrc(A + (long)m0 * lda + k_begin, (long)(M - m0) * lda * 2 - 2L * k_begin);
   const __amdgpu_buffer_rsrc_t rb = make_rsrc(B + (long)n0 * ldb + k_begin, (long)(N - n0) * ldb * 2 - 2L * k_begin);
   // glds pieces: slot rows q*8 + (lane >> 3), q = 2 * wave + r; slot row -> tile row / column
@@ -740,7 +738,6 @@ __attribute__((always_inline)) JM_DEVICE void p4_body(const uint16_t* __restrict
       f[nt][1] = lds8(base + nt * 16 * BK2 + ch1);
     }
   };
-  f32x4_t acc[8][NTW];
 #pragma unroll
   for (int i = 0; i < 8; ++i)
 #pragma unroll
@@ -869,7 +866,17 @@ __attribute__((always_inline)) JM_DEVICE void p4_body(const uint16_t* __restrict
   tile(K0{}, t + 1, bq, bp);
   (void)IX{};
   (void)I16{};
+}
 
+// the 256 x 256 tile's epilogue from the p4 accumulators (EPI_PARTIAL: fp32 split slice)
+template <int EPI>
+__attribute__((always_inline)) JM_DEVICE void p4_epilogue(const f32x4_t (&acc)[8][4], const GemmEpi& ep, int M, int N,
+                                                          int m0, int n0, int split, uint16_t* smem) {
+  constexpr int NTW = 4;
+  const int tid = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+  const int l16 = lane & 15, g = lane >> 4;
+  const int wr = wave >> 2, wc = wave & 3;
   if (EPI == EPI_PARTIAL) {
     float* dst = ep.part + (long)split * M * N;
 #pragma unroll
@@ -899,7 +906,127 @@ __global__ __launch_bounds__(512, 1) void gemm_p4_kernel(const uint16_t* __restr
   if constexpr ((SCHED & 4) != 0) {
     if (__builtin_amdgcn_readfirstlane(threadIdx.x) >= 256) __builtin_amdgcn_s_setprio(1);
   }
-  p4_body<EPI, SCHED & ~4>(A, lda, B, ldb, M, N, K, ep, GROUP_M, smem);
+  int m0, n0, split = 0;
+  tile_of(M, N, GROUP_M, m0, n0, EPI == EPI_PARTIAL ? ep.splits : 1, EPI == EPI_PARTIAL ? &split : nullptr);
+  int k_begin = 0;
+  if (EPI == EPI_PARTIAL) {
+    const int ku = K / 128;  // splits take whole 128-deep units (even tile count per split)
+    const int ku0 = split * ku / ep.splits, ku1 = (split + 1) * ku / ep.splits;
+    k_begin = ku0 * 128;
+    K = (ku1 - ku0) * 128;
+  }
+  f32x4_t acc[8][4];
+  p4_mainloop<SCHED & ~4>(A, lda, B, ldb, M, N, m0, n0, k_begin, K, acc, smem);
+  p4_epilogue<EPI>(acc, ep, M, N, m0, n0, split, smem);
+}
+
+// ------------------------------------------------------------------ persistent DP + stream-K
+// One workgroup per CU.  Workgroups are grouped in S-wide squads (S | column tiles, same XCD) that
+// share the A row tile: a squad works on a MACRO tile = one 256-row tile x S column tiles, lane j
+// of the squad on column tile j, all lanes over the same K range at the same time (so the A panel
+// is fetched once per squad through the XCD's L2, as in the tiled launch).  A squad walks
+// (1) whole macro tiles data-parallel, macro q + r*Q in round r, for the first dp macro tiles,
+// then (2) a contiguous range of 128-deep K units of the remaining macro tiles (stream-K: the
+// last, partly filled round(s) spread evenly over all Q squads).  A range that starts inside a
+// macro tile makes the squad a CONTRIBUTOR of it (at most once): every lane stores its fp32
+// partial to ws[w] and raises flags[w] (agent-scope release).  The squad holding a tile's first
+// unit OWNS it and reaches it at the END of its range, so its contributors (higher squads, which
+// start with it) are long done: it acquires their flags, adds their partials, resets the flags to
+// 0 and runs the epilogue.  Waits only ever point at higher squads (no cycle; grid <= CUs, one
+// workgroup per CU); every spin is bounded.  ws / flags are per device and serial per launch
+// stream (the NT GEMMs run on the compute stream only).
+typedef __attribute__((ext_vector_type(4))) unsigned int u32x4_v;
+
+struct SkPlan {
+  int S;          // workgroups per squad (column tiles of a macro tile)
+  int nu;         // 128-deep K units per tile
+  int dp;         // macro tiles [0, dp): whole, data-parallel
+  int L, extra;   // stream-K units [dp*nu, macros*nu): squad q has L (+1 for q < extra) units
+  float* ws;      // [G][256*256] fp32 contributor partials (register-layout order, coalesced)
+  int* flags;     // [G]
+};
+
+JM_DEVICE int sk_u0(const SkPlan& p, int q) { return q * p.L + min(q, p.extra); }
+
+template <int EPI, int SCHED>
+__global__ __launch_bounds__(512, 1) void gemm_sk_kernel(const uint16_t* __restrict__ A, long lda,
+                                                         const uint16_t* __restrict__ B, long ldb, int M, int N,
+                                                         int K, GemmEpi ep, int GROUP_M, SkPlan p) {
+  JM_DGUARD(blockDim.x == 512 && K % 128 == 0 && M > 0 && N > 0 && gridDim.x % 8 == 0);
+  extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
+  if constexpr ((SCHED & 4) != 0) {
+    if (__builtin_amdgcn_readfirstlane(threadIdx.x) >= 256) __builtin_amdgcn_s_setprio(1);
+  }
+  const int G = gridDim.x;
+  const int w = (blockIdx.x & 7) * (G >> 3) + (blockIdx.x >> 3);  // same-XCD workgroups: consecutive w
+  const int q = w / p.S, j = w - q * p.S, Q = G / p.S;
+  const int nM = (M + BM - 1) / BM;
+  const int tid = threadIdx.x;
+  const int U0 = p.dp * p.nu;
+  int T = q, u = U0 + sk_u0(p, q);
+  const int u1 = U0 + sk_u0(p, q + 1);
+  for (;;) {
+    int mac, kb, ke;
+    if (T < p.dp) {
+      mac = T;
+      kb = 0;
+      ke = p.nu;
+      T += Q;
+    } else if (u < u1) {
+      mac = u / p.nu;
+      kb = u - mac * p.nu;
+      ke = min(p.nu, kb + (u1 - u));
+      u += ke - kb;
+    } else {
+      break;
+    }
+    // macro tiles: row tile fastest (consecutive squads of an XCD share the B column block)
+    const int m0 = (mac % nM) * BM, n0 = ((mac / nM) * p.S + j) * BN;
+    __syncthreads();  // the previous item's epilogue is done with LDS
+    f32x4_t acc[8][4];
+    p4_mainloop<SCHED & ~4>(A, lda, B, ldb, M, N, m0, n0, kb * 128, (ke - kb) * 128, acc, smem);
+    // partial tiles through buffer ops: one VGPR offset (16 * tid) + per-i SGPR offsets, so no
+    // 64-bit address per i stays live (they would be hoisted out of the item loop and spilled)
+    int vo = tid * 16;
+    asm volatile("" : "+v"(vo));
+    if (kb > 0) {  // contributor: publish the partial
+      const __amdgpu_buffer_rsrc_t rw =
+          __builtin_amdgcn_make_buffer_rsrc(p.ws + (long)w * (BM * BN), (short)0, BM * BN * 4, 0x00020000);
+#pragma unroll
+      for (int i = 0; i < 32; ++i)
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_v, acc[i >> 2][i & 3]), rw, vo, i * 8192, 0);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_store(p.flags + w, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      continue;
+    }
+    if (ke < p.nu) {  // owner of a split tile: add the contributors' partials
+      const int end = (mac + 1) * p.nu;
+      for (int q2 = q + 1; q2 < Q && U0 + sk_u0(p, q2) < end; ++q2) {
+        const int w2 = q2 * p.S + j;
+        if (tid == 0) {
+          for (int it = 0; it < (1 << 24); ++it) {
+            if (__hip_atomic_load(p.flags + w2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) break;
+            __builtin_amdgcn_s_sleep(2);
+          }
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          __hip_atomic_store(p.flags + w2, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        __syncthreads();
+        const __amdgpu_buffer_rsrc_t rr =
+            __builtin_amdgcn_make_buffer_rsrc(p.ws + (long)w2 * (BM * BN), (short)0, BM * BN * 4, 0x00020000);
+#pragma unroll
+        for (int i = 0; i < 32; ++i)
+          acc[i >> 2][i & 3] += __builtin_bit_cast(f32x4_t, __builtin_amdgcn_raw_buffer_load_b128(rr, vo, i * 8192, 0));
+      }
+    }
+    p4_epilogue<EPI>(acc, ep, M, N, m0, n0, 0, smem);
+  }
 }
 
 // ------------------------------------------------------------------ half-width, 2 WGs per CU
@@ -1431,10 +1558,77 @@ void launch_p4s(const uint16_t* A, long lda, const uint16_t* B, long ldb, int M,
 }
 
 int g_p4_sched = 4;  // A/B: variant 20 + SCHED bits (variants 21..83 = 20 + bits)
+int g_sk = 0;        // A/B: persistent DP + stream-K launches where the plan says they pay (jm_gemm_set_sk); off:
+                     // measured slower on every planned shape (fp32 partial traffic; profiles/r2_gemm_stream_k.txt)
+int num_cus();
+
+// stream-K plan for an NT launch (0 = plain tiled launch).  Squad width S = the largest power of 2
+// <= 8 dividing the column-tile count; macro tiles = row tiles x column blocks.  Cost model in
+// 128-deep K units of one tile on one CU: tiled = ceil(tiles / G) * nu; DP + stream-K = the whole
+// rounds of macro tiles but the last, the rest spread evenly over the squads, + ~1 unit per
+// partial an owner has to add.
+int sk_plan(int M, int N, int K, SkPlan* pl) {
+  if (!g_sk || K % 128) return 0;
+  const int G = num_cus() / 8 * 8;
+  const int nM = (M + BM - 1) / BM, nN = (N + BN - 1) / BN;
+  const int tiles = nM * nN;
+  const int nu = K / 128;
+  if (G < 8 || tiles % G == 0) return 0;
+  int S = 8;
+  while (nN % S) S >>= 1;
+  const int Q = G / S, macros = nM * (nN / S);
+  const int rounds = macros / Q;
+  const int dp = rounds > 0 ? (rounds - 1) * Q : 0;
+  const long U = (long)(macros - dp) * nu;
+  const int L = (int)(U / Q);
+  if (L < 1) return 0;
+  const int parts = (nu + L - 1) / L;  // squads a macro tile spans (about)
+  if (parts > 4) return 0;             // owner would add too many partials: split-K / tiled instead
+  const double tiled = (double)((tiles + G - 1) / G) * nu;
+  const double sk = (double)(dp / Q) * nu + (double)((U + Q - 1) / Q) + (parts > 1 ? parts : 0);
+  if (sk > 0.95 * tiled) return 0;
+  pl->S = S;
+  pl->nu = nu;
+  pl->dp = dp;
+  pl->L = L;
+  pl->extra = (int)(U - (long)L * Q);
+  return G;
+}
+
+float* g_sk_ws = nullptr;
+int* g_sk_flags = nullptr;
+
+template <int EPI, int SCHED>
+void launch_sk(const uint16_t* A, long lda, const uint16_t* B, long ldb, int M, int N, int K, const GemmEpi& ep,
+               int G, SkPlan pl, hipStream_t st) {
+  static bool attr = false;
+  const size_t sm = jm_gemm_smem();
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)gemm_sk_kernel<EPI, SCHED>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)sm);
+    attr = true;
+  }
+  if (g_sk_ws == nullptr) {  // once per process (outside any graph capture: the first call is eager)
+    (void)hipMalloc((void**)&g_sk_ws, (size_t)1024 * BM * BN * sizeof(float));
+    (void)hipMalloc((void**)&g_sk_flags, 1024 * sizeof(int));
+    (void)hipMemset(g_sk_flags, 0, 1024 * sizeof(int));
+  }
+  pl.ws = g_sk_ws;
+  pl.flags = g_sk_flags;
+  gemm_sk_kernel<EPI, SCHED><<<G, 512, sm, st>>>(A, lda, B, ldb, M, N, K, ep, g_gemm_group, pl);
+}
 
 template <int EPI>
 void launch_p4(const uint16_t* A, long lda, const uint16_t* B, long ldb, int M, int N, int K, const GemmEpi& ep,
                int nwg, hipStream_t st) {
+  if constexpr (EPI != EPI_PARTIAL && EPI != EPI_TAIL) {
+    SkPlan pl;
+    const int G = (g_p4_sched == 4 || g_p4_sched == 0) ? sk_plan(M, N, K, &pl) : 0;
+    if (G > 0) {
+      if (g_p4_sched == 4) return launch_sk<EPI, 4>(A, lda, B, ldb, M, N, K, ep, G, pl, st);
+      return launch_sk<EPI, 0>(A, lda, B, ldb, M, N, K, ep, G, pl, st);
+    }
+  }
   switch (g_p4_sched) {
     default: break;
     case 1: return launch_p4s<EPI, 1>(A, lda, B, ldb, M, N, K, ep, nwg, st);
@@ -1542,6 +1736,8 @@ void jm_gemm_set_variant(int wn, int group) {
 }
 
 void jm_gemm_set_tail(int on) { g_gemm_tail = on; }
+
+void jm_gemm_set_sk(int on) { g_sk = on; }
 
 // Tail split plan for an NT launch: the last wave of output tiles (tiles % CUs of them) fills only
 // part of the chip; when it is at most a quarter wave, those tiles run split-K S ways (compact fp32

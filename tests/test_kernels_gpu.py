@@ -487,3 +487,36 @@ def test_gemm_gelu_saved_derivative(ext, M, N, K, variant):
     e1 = ext.gelu_bwd(h, da, bg1)
     e2 = ext.gelu_bwd(gp, da, bg2, True)
     assert rel(e2, e1) < 1e-2 and rel(bg2, bg1) < 1e-2
+
+
+@pytest.mark.parametrize("kind", ["store", "gelu", "gelu_d", "dgelu", "dmul"])
+@pytest.mark.parametrize("M,N,K", [(8192, 1024, 4096), (5000, 1000, 1280), (26624, 1024, 1024), (25088, 4096, 1024)])
+def test_gemm_nt_stream_k(ext, kind, M, N, K):
+    """Persistent DP + stream-K launch (split tiles: contributor partials + owner fix-up through
+    flags) == the plain tiled launch == the fp32 reference, every epilogue kind; shapes where the
+    plan picks stream-K (tiles not a multiple of the CU count), ragged M / N and a DP part included."""
+    torch.manual_seed(3)
+    A = (torch.rand(M, K, device="cuda") * 2 - 1).bfloat16()
+    W = ((torch.rand(N, K, device="cuda") * 2 - 1) * 0.05).bfloat16()
+    b = torch.randn(N, device="cuda") * 0.1
+    aux = (torch.randn(M, N, device="cuda") * 2).bfloat16()
+    outs = []
+    for sk in (0, 1):
+        ext.gemm_set_sk(sk)
+        for _ in range(2):  # twice: the flags must come back clean
+            if kind in ("dgelu", "dmul"):
+                db = torch.zeros(N, device="cuda")
+                o = (ext.gemm_nt_dgelu(A, W, aux, db, kind == "dmul"), db)
+            elif kind == "gelu_d":
+                o = tuple(ext.gemm_nt(A, W, b, True, False, True))
+            else:
+                o = tuple(ext.gemm_nt(A, W, b, kind == "gelu"))
+        outs.append(o)
+    ext.gemm_set_sk(0)
+    ref = A.float() @ W.float().t()
+    for o0, o1 in zip(outs[0], outs[1]):
+        assert rel(o1, o0) < 2e-3
+    if kind in ("store", "gelu"):
+        assert rel(outs[1][0], ref + b) < 1e-2
+    if kind == "dmul":
+        assert rel(outs[1][0], (ref.bfloat16().float() * aux.float())) < 1e-2

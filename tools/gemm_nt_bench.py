@@ -48,8 +48,13 @@ def main():
     a = ap.parse_args()
     ext = _ext.load()
     ext.gemm_set_tail(a.tail)
-    variants = [int(v) for v in a.variant.split(",")]
-    ext.gemm_set_variant(variants[0], a.group)
+    variants = a.variant.split(",")  # "24" = variant 24 (stream-K where planned), "24n" = no stream-K
+
+    def setv(v):
+        ext.gemm_set_sk(0 if v.endswith("n") else 1)
+        ext.gemm_set_variant(int(v.rstrip("n")), a.group)
+
+    setv(variants[0])
     names = [n for n in FWD if not a.only or n in a.only.split(",")]
     tot = {"ours": 0.0, "blas": 0.0}
     for kind in a.kinds.split(","):
@@ -91,11 +96,11 @@ def main():
                 blas = lambda: torch.addmm(bb, x, w.t())  # noqa: E731
             errs = []
             for v in variants:
-                ext.gemm_set_variant(v, a.group)
+                setv(v)
                 o = ours()
                 r0 = torch.addmm(b, x.float(), w.float().t()) if kind != "dgrad_gelu" else o[0].float()
                 errs.append(((o[0].float() - r0).abs().max() / r0.abs().max()).item())
-            ext.gemm_set_variant(variants[0], a.group)
+            setv(variants[0])
             out = ours()
             ref = torch.addmm(b, x.float(), w.float().t()) if kind != "dgrad_gelu" else out[0].float()
             err = ((out[0].float() - ref).abs().max() / ref.abs().max()).item()
@@ -108,10 +113,10 @@ def main():
             tb = []
             for _ in range(a.rounds):
                 for v in variants:
-                    ext.gemm_set_variant(v, a.group)
+                    setv(v)
                     tv[v].append(timeit(ours, a.iters))
                 tb.append(timeit(blas, a.iters))
-            ext.gemm_set_variant(variants[0], a.group)
+            setv(variants[0])
             to, tb = min(tv[variants[0]]), min(tb)
             if len(variants) > 1:
                 fl = 2.0 * M * N * K
