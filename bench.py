@@ -52,6 +52,9 @@ def main():
     ap.add_argument("--task", default="pretrain", choices=["pretrain", "finetune", "linear"])
     ap.add_argument("--hip-graph", action="store_true",
                     help="replay the captured train step from a HIP graph (single process; runtime/graph.py)")
+    ap.add_argument("--cpu", action="store_true",
+                    help="tests only: run the same flow on the CPU (gloo when distributed, fp32 PyTorch path)")
+    ap.add_argument("--image-size", type=int, default=224, help=argparse.SUPPRESS)  # tests: smaller images
     args = ap.parse_args()
     if args.task != "pretrain":
         return bench_classifier(args)
@@ -66,17 +69,19 @@ def main():
     from jumbo_mae_tpu_amd.utils.flops import mfu, pretrain_fwd_flops_per_image
     from jumbo_mae_tpu_amd.utils.rng import RngStreams
 
-    info = pdist.init_distributed()
+    info = pdist.init_distributed("cpu" if args.cpu else None)
     dev = info.device
     world = info.world_size
+    cdt = torch.float32 if args.cpu else torch.bfloat16
     if world != args.gpus and info.is_main:
         log(f"[bench] warning: --gpus {args.gpus} but WORLD_SIZE={world}; reporting WORLD_SIZE")
     B = args.batch_per_gpu
     global_batch = B * world
 
-    vc = vit_config(args.model, labels=0, posemb="sincos2d", image_mask_ratio=0.75, droppath=0.0, dropout=0.0)
-    dc = decoder_config(dec_droppath=0.0)
-    model = PretrainModel(vc, dc).to(dev, torch.bfloat16, seed=0)
+    vc = vit_config(args.model, labels=0, posemb="sincos2d", image_mask_ratio=0.75, droppath=0.0, dropout=0.0,
+                    image_size=args.image_size)
+    dc = decoder_config(dec_droppath=0.0, image_size=args.image_size)
+    model = PretrainModel(vc, dc).to(dev, cdt, seed=0)
     store = model.store
     pdist.broadcast_(store.master)  # CC6: identical init on every rank
     store.sync_shadow()
@@ -95,8 +100,8 @@ def main():
 
     gen = torch.Generator(device=dev).manual_seed(1234 + info.rank)
     mb = B // args.grad_accum
-    pool = [torch.randint(0, 256, (mb, 3, 224, 224), dtype=torch.uint8, device=dev, generator=gen)
-            for _ in range(2)]
+    S = args.image_size
+    pool = [torch.randint(0, 256, (mb, 3, S, S), dtype=torch.uint8, device=dev, generator=gen) for _ in range(2)]
 
     if info.is_main:
         log(f"[bench] {args.model} jumbo-MAE params={store.num_params()/1e6:.1f}M world={world} "
@@ -112,33 +117,41 @@ def main():
         it += 1
         return runner(micro)
 
+    def sync():
+        if dev.type == "cuda":
+            torch.cuda.synchronize()
+
     t0 = time.time()
     for i in range(args.warmup):
         m = step()
         if info.is_main:
-            torch.cuda.synchronize()
+            sync()
             log(f"[bench] warmup {i + 1}/{args.warmup} loss={m['loss'].item():.4f} lr={m['learning_rate']:.3e} "
                 f"t={time.time() - t0:.1f}s")
     pdist.barrier()
-    torch.cuda.synchronize()
+    sync()
     t_start = time.perf_counter()
     for i in range(args.steps):
         m = step()
         if info.is_main and (i + 1) % max(1, args.steps // 4) == 0:
             log(f"[bench] step {i + 1}/{args.steps} t={time.perf_counter() - t_start:.2f}s")
     pdist.barrier()
-    torch.cuda.synchronize()
+    sync()
     elapsed = time.perf_counter() - t_start
     elapsed = pdist.all_reduce_max_scalar(elapsed, dev)
     final_loss = float(m["loss"].item())
     comm_ms = trainer.comm_ms()
+    # data-parallel replicas must hold identical weights after the timed steps (outside the timed
+    # region): spread of a weight checksum over the ranks, 0.0 when in sync
+    spread = pdist.all_reduce_max_scalar(float(store.master.double().abs().sum()), dev) - \
+        -pdist.all_reduce_max_scalar(-float(store.master.double().abs().sum()), dev) if world > 1 else 0.0
 
     if args.profile_steps > 0 and info.is_main:
         from torch.profiler import ProfilerActivity, profile
         with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA]) as prof:
             for _ in range(args.profile_steps):
                 step()
-            torch.cuda.synchronize()
+            sync()
         log(prof.key_averages().table(sort_by="cuda_time_total", row_limit=40))
 
     ms = elapsed / args.steps * 1000.0
@@ -160,8 +173,9 @@ def main():
             # GPU time of the last step behind the DP reduction wait (exposed comm + overlapped
             # bucket updates); null on one GPU
             "exposed_comm_ms_last_step": None if comm_ms is None else round(comm_ms, 3),
-            "dtype": "bf16",
-            "data": "synthetic uint8 224x224 images on GPU, random-init weights",
+            "replica_weight_checksum_spread": spread,
+            "dtype": "fp32" if args.cpu else "bf16",
+            "data": f"synthetic uint8 {S}x{S} images on {'CPU' if args.cpu else 'GPU'}, random-init weights",
             "config": {
                 "model": f"{args.model} jumbo-MAE (3 CLS, shared jumbo MLP) + decoder 8x512x16h",
                 "global_batch": global_batch,

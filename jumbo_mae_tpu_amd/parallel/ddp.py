@@ -26,6 +26,8 @@ MI355X design:
 
 from __future__ import annotations
 
+import contextlib
+
 import torch
 import torch.distributed as dist
 
@@ -149,19 +151,21 @@ class GradReducer:
         self.works.append((b, w))
 
     def _allreduce(self, t: torch.Tensor):
-        if dist.get_backend(self.group) == "nccl":
-            # issue from the weight-gradient stream (ops/prims.py) after it has caught up with
-            # the main stream: RCCL then waits for the GEMM that wrote the bucket's last kernel
-            # gradient without stalling the backward chain on the main stream
-            from ..ops.prims import wgrad_stream
-            side = wgrad_stream() if t.is_cuda else None
-            if side is not None:
-                side.wait_stream(torch.cuda.current_stream())
-                with torch.cuda.stream(side):
-                    return dist.all_reduce(t, op=dist.ReduceOp.AVG, group=self.group, async_op=True)
-            return dist.all_reduce(t, op=dist.ReduceOp.AVG, group=self.group, async_op=True)
-        w = dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
-        return (w, t)
+        """Async all-reduce-average of ``t`` -> (work, tensor to divide by world or None).  One code
+        path for every backend: only the reduction op differs (RCCL averages inside the
+        collective, gloo has no AVG and is divided after the wait).  On a GPU the collective is
+        issued from the weight-gradient stream (ops/prims.py) when that stream is enabled, after
+        it has caught up with the main stream: RCCL then waits for the GEMM that wrote the
+        bucket's last kernel gradient without stalling the backward chain on the main stream."""
+        from ..ops.prims import wgrad_stream
+        native_avg = dist.get_backend(self.group) == "nccl"
+        op = dist.ReduceOp.AVG if native_avg else dist.ReduceOp.SUM
+        side = wgrad_stream() if t.is_cuda else None
+        if side is not None:
+            side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side) if side is not None else contextlib.nullcontext():
+            w = dist.all_reduce(t, op=op, group=self.group, async_op=True)
+        return w, (None if native_avg else t)
 
     def bucket_ranges(self) -> list[tuple[int, int]]:
         return [(lo, hi) for lo, hi, _ in self.buckets]
@@ -183,12 +187,10 @@ class GradReducer:
         left = [0] * len(self.buckets)
         for b, _ in self.works:
             left[b] += 1
-        for b, w in self.works:
-            if isinstance(w, tuple):
-                w[0].wait()
-                w[1].div_(self.world)
-            else:
-                w.wait()
+        for b, (w, to_div) in self.works:
+            w.wait()
+            if to_div is not None:
+                to_div.div_(self.world)
             if b in self._compressed:
                 lo, hi, _ = self.buckets[b]
                 self.store.grad[lo:hi].copy_(self._compressed.pop(b))

@@ -189,6 +189,7 @@ def test_allreduce_bench_gloo(tmp_path):
         assert row["world"] == 2
         assert row["allreduce_busbw_GBs"] > 0 and row["reduce_scatter_busbw_GBs"] > 0 and row["all_gather_busbw_GBs"] > 0
     assert res["model"]["vit_l_grad_allreduce_ms"] > res["model"]["vit_l_jumbo_tail_ms"] > 0
+    assert res["model"]["recommended_bucket_mb"] in [row["size_mb"] for row in res["collective_sweep"]]
 
 
 def _overlap_worker(rank, world, port, out, kind):

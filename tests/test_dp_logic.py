@@ -56,7 +56,7 @@ def test_reducer_buckets_partition_and_launch_in_readiness_order():
     red.enabled = red.overlap = True
     m.store.hooks.append(red._on_ready)
     m.store.use_hooks.append(red._on_use)
-    red._allreduce = lambda t: (launched.append(t.data_ptr()), _FakeWork())[1]
+    red._allreduce = lambda t: (launched.append(t.data_ptr()), (_FakeWork(), None))[1]
     red.world = 2
     m.store.zero_grad()
     red.begin_step()

@@ -16,7 +16,15 @@ curve; the sweep also reports the modelled exposed time of the ViT-L gradient al
 (1.62 GB fp32, of which the 302 MB shared jumbo-MLP gradient is the tail that cannot overlap).
 
 Rank 0 prints a table and one JSON line (``{"collective_sweep": [...]}``); times are the max over
-ranks of the per-iteration mean.
+ranks of the per-iteration mean.  ``model.recommended_bucket_mb`` is the smallest swept size that
+reaches 90 % of the best all-reduce bus bandwidth: pass it as ``--bucket-mb`` (bench.py / the
+training CLI) -- larger buckets only delay the first reduction behind the backward pass.
+
+RCCL knobs worth sweeping with this tool (environment, one run per setting; the defaults are what
+bench.py uses): ``NCCL_MIN_NCHANNELS`` / ``NCCL_MAX_NCHANNELS`` (channels = rings in flight; on
+8 fully connected xGMI GPUs enough channels are needed to drive all 7 links of a GPU),
+``NCCL_PROTO`` (``Simple`` for large buckets, ``LL128`` / ``LL`` for small ones), ``NCCL_ALGO``
+(``Ring`` / ``Tree``).  Keep ``HSA_ENABLE_IPC_MODE_LEGACY=0`` exported (dmabuf IPC).
 """
 
 from __future__ import annotations
@@ -96,7 +104,10 @@ def model_exposed(rows: list[dict]) -> dict:
     best = max(ar, key=lambda r: r["allreduce_busbw_GBs"])
     n = best["world"]
     bw = best["allreduce_busbw_GBs"] * 1e9 / (2 * (n - 1) / n) if n > 1 else float("inf")
+    rec = min((r for r in ar if r["allreduce_busbw_GBs"] >= 0.9 * best["allreduce_busbw_GBs"]),
+              key=lambda r: r["size_mb"])
     return {"best_busbw_GBs": best["allreduce_busbw_GBs"], "best_size_mb": best["size_mb"],
+            "recommended_bucket_mb": rec["size_mb"],
             "vit_l_grad_allreduce_ms": VIT_L_GRAD_BYTES / bw * 1e3,
             "vit_l_jumbo_tail_ms": VIT_L_JUMBO_TAIL_BYTES / bw * 1e3}
 
