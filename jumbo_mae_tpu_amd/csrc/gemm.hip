@@ -1577,6 +1577,18 @@ int sk_plan(int M, int N, int K, SkPlan* pl) {
   int S = 8;
   while (nN % S) S >>= 1;
   const int Q = G / S, macros = nM * (nN / S);
+  if (g_sk == 2) {  // A/B: whole tiles only, on the fewest squads that keep the round count
+    const int rounds = (macros + Q - 1) / Q;
+    int q = (macros + rounds - 1) / rounds;
+    while ((q * S) % 8) ++q;
+    if (q >= Q) return 0;
+    pl->S = S;
+    pl->nu = nu;
+    pl->dp = macros;
+    pl->L = 0;
+    pl->extra = 0;
+    return q * S;
+  }
   const int rounds = macros / Q;
   const int dp = rounds > 0 ? (rounds - 1) * Q : 0;
   const long U = (long)(macros - dp) * nu;

@@ -48,11 +48,13 @@ def main():
     a = ap.parse_args()
     ext = _ext.load()
     ext.gemm_set_tail(a.tail)
-    variants = a.variant.split(",")  # "24" = variant 24 (stream-K where planned), "24n" = no stream-K
+    # "24" = variant 24 as launched by default; suffix "s" = persistent DP + stream-K where planned,
+    # "d" = persistent whole tiles on the fewest CUs that keep the round count (gemm_set_sk 1 / 2)
+    variants = a.variant.split(",")
 
     def setv(v):
-        ext.gemm_set_sk(0 if v.endswith("n") else 1)
-        ext.gemm_set_variant(int(v.rstrip("n")), a.group)
+        ext.gemm_set_sk({"s": 1, "d": 2}.get(v[-1], 0))
+        ext.gemm_set_variant(int(v.rstrip("sd")), a.group)
 
     setv(variants[0])
     names = [n for n in FWD if not a.only or n in a.only.split(",")]
