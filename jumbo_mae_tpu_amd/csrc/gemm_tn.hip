@@ -48,6 +48,28 @@ JM_DEVICE s16x4_t tr4(const uint16_t* p) {
   return r;
 }
 
+// tr4 of (addr ^ X) + OFF: the XOR in the same asm block, so no per-block address stays live
+template <int X, int OFF>
+JM_DEVICE s16x4_t tr4x(uint32_t a) {
+  s16x4_t r;
+  if constexpr (X == 0) {
+    asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(r) : "v"(a), "i"(OFF));
+  } else {
+    uint32_t tmp;
+    asm volatile("v_xor_b32 %1, %3, %2\n\tds_read_b64_tr_b16 %0, %1 offset:%4"
+                 : "=v"(r), "=&v"(tmp) : "v"(a), "i"(X), "i"(OFF));
+  }
+  return r;
+}
+
+template <int N, int I = 0, typename F>
+JM_DEVICE void static_for(F&& f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>{});
+    static_for<N, I + 1>(f);
+  }
+}
+
 JM_DEVICE void wait_lds() {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_sched_barrier(0);
@@ -253,6 +275,231 @@ __global__ __launch_bounds__(NTH, 1) void gemm_tn_kernel(const uint16_t* __restr
   }
 }
 
+// ------------------------------------------------------------------ 4-phase variant (default)
+// The NT kernel's 4-phase counted-vmcnt pipeline (gemm.hip gemm_p4_kernel) on the TN layout:
+// 64-row (M) K-tiles cut into half-tile slots of 64 rows x 128 columns (256 B rows, 16 KB):
+// a0 / a1 = the dY columns of the waves' upper / lower 64-row output halves (wr*128 + mh*64 +
+// [0,64) for both wr), b0 / b1 = the X columns of the waves' left / right 32-column halves (wc*64
+// + nh*32 + [0,32) for all wc).  8 slots = 2 K-tiles (128 KB); 4 phases per K-tile, one 64 x 32
+// quadrant (16 MFMAs) each, in the order (0,0) (0,1) (1,1) (1,0); fragments one phase ahead;
+// each phase starts with [vmcnt(N) lgkmcnt(0) s_barrier] and issues one slot of the tile after
+// next (q1 a0, q2 b1, q3 a1, q4 b0).  Fragments are COLUMNS of the slot images (8 consecutive M
+// per lane): two ds_read_b64_tr_b16 each.  16-byte chunks XOR-swizzled by tswz(row) (bits 1-3):
+// the 8 rows of a transposing read's 32-lane half then cover 8 distinct 32-byte bank slots, and
+// the swizzle only permutes a fragment's 4 (A) / 2 (B) column blocks, so each lane keeps one
+// address per block (+ immediates for the k offsets).  Waves 4-7 at static priority 1.
+constexpr int SLOT4 = 64 * 128;  // elements per slot
+
+template <int ACC, bool SEG>
+__global__ __launch_bounds__(NTH, 1) void gemm_tn4_kernel(const uint16_t* __restrict__ A, long lda,
+                                                          const uint16_t* __restrict__ B, long ldb, int M, int N,
+                                                          int K, int steps_per_split, float* __restrict__ out,
+                                                          long ldo, long split_stride, TnSegs segs = {},
+                                                          float* __restrict__ g0 = nullptr, long ldg0 = 0) {
+  JM_DGUARD(blockDim.x == NTH && steps_per_split >= 4 && steps_per_split % 4 == 0 && M > 0);
+  extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
+  const int tid = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+  const int l16 = lane & 15, g = lane >> 4;
+  const int wr = wave >> 2, wc = wave & 3;
+  if (__builtin_amdgcn_readfirstlane(tid) >= 256) __builtin_amdgcn_s_setprio(1);
+
+  const int nK = K / TK_;
+  const int tiles = (N / TN_) * nK;
+  const int nwg = gridDim.x;
+  const int orig = blockIdx.x;
+  const int xcd = orig & 7, q = nwg >> 3, r = nwg & 7;
+  const int wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+  const int split = wg / tiles, tile = wg - split * tiles;
+  const int n0 = (tile / nK) * TN_, k0 = (tile % nK) * TK_;
+  const int m_begin = split * steps_per_split * BS;
+  const int rows = min(M - m_begin, steps_per_split * BS);  // > 0 (host guarantees)
+  int nk = (rows + 63) / 64;
+  nk += nk & 1;  // even (pairs of K-tiles); rows past the split read zeros
+
+  const __amdgpu_buffer_rsrc_t ra = make_rsrc(SEG ? segs.a[0] : A + (long)m_begin * lda + n0, SEG ? 0 : (long)rows * lda * 2);
+  const __amdgpu_buffer_rsrc_t rb = make_rsrc(SEG ? segs.b[0] : B + (long)m_begin * ldb + k0, SEG ? 0 : (long)rows * ldb * 2);
+  // glds pieces: 4 rows x 256 B; slot rows pr = (2 wave + rr) * 4 + (lane >> 4); LDS chunk lane & 15
+  // holds logical chunk c = (lane & 15) ^ tswz(pr) -> column of the half's segment
+  uint32_t a_src[2][2], b_src[2][2];  // [half][rr] byte offsets
+#pragma unroll
+  for (int rr = 0; rr < 2; ++rr) {
+    const int pr = (2 * wave + rr) * 4 + (lane >> 4);
+    const int c = (lane & 15) ^ tswz(pr);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      a_src[h][rr] = (uint32_t)((pr * lda + (c >> 3) * 128 + h * 64 + (c & 7) * 8) * 2);
+      b_src[h][rr] = (uint32_t)((pr * ldb + (c >> 2) * 64 + h * 32 + (c & 3) * 8) * 2);
+    }
+  }
+  auto issue = [&](int t, auto slot) {
+    constexpr int S = decltype(slot)::value;
+    uint16_t* l = smem + ((t & 1) * 4 + S) * SLOT4 + (2 * wave) * 4 * 128;
+    if constexpr (SEG) {  // this K-tile's 64 rows lie in one block (segs.rows % 64 == 0)
+      const int row = m_begin + t * 64;
+      const int sg = min(row / segs.rows, segs.n - 1);
+      const int loc = row - sg * segs.rows;
+      const int left = row < m_begin + rows ? min(segs.rows - loc, m_begin + rows - row) : 0;
+      if constexpr (S < 2) {
+        const __amdgpu_buffer_rsrc_t sra = make_rsrc(segs.a[sg] + (long)loc * lda + n0, (long)left * lda * 2);
+#pragma unroll
+        for (int rr = 0; rr < 2; ++rr) blds16(sra, a_src[S][rr], 0, l + rr * 4 * 128);
+      } else {
+        const __amdgpu_buffer_rsrc_t srb = make_rsrc(segs.b[sg] + (long)loc * ldb + k0, (long)left * ldb * 2);
+#pragma unroll
+        for (int rr = 0; rr < 2; ++rr) blds16(srb, b_src[S - 2][rr], 0, l + rr * 4 * 128);
+      }
+    } else {
+#pragma unroll
+      for (int rr = 0; rr < 2; ++rr) {
+        if constexpr (S < 2) blds16(ra, a_src[S][rr], (uint32_t)(t * 64 * lda * 2), l + rr * 4 * 128);
+        else blds16(rb, b_src[S - 2][rr], (uint32_t)(t * 64 * ldb * 2), l + rr * 4 * 128);
+      }
+    }
+  };
+  // transposing fragment reads: lane 4q + p of a 16-lane group -> slot row 8g + q (+4), columns
+  // 4p..4p+3 of the fragment's 16-column block; the block's swizzled chunk differs per lane only
+  // through bits 1-2 of the chunk index (A: the 4 blocks mt, B: bit 1 = nt), i.e. address bits 5-6
+  // Byte address of block 0 per operand and slot set; block j (A: mt, B: nt) is at
+  // addr ^ (j << 5) (the swizzle only permutes address bits 5-6), the slot within the set, the
+  // k step and the second 4 rows are immediates (<= 58 KB): 4 address VGPRs in all.
+  const int qrow = 8 * g + (l16 >> 2), pp = l16 & 3;
+  const int sw = tswz(qrow);  // == tswz(qrow + 4 + 32 kk): rows differ in bits 2 and 5 only
+  const uint32_t lds0 = (uint32_t)(size_t)((const __attribute__((address_space(3))) uint16_t*)smem);
+  const uint32_t a_lo = 2 * (qrow * 128 + (((wr * 8 + (pp >> 1)) ^ sw) << 3) + (pp & 1) * 4);
+  const uint32_t b_lo = 2 * (qrow * 128 + (((wc * 4 + (pp >> 1)) ^ sw) << 3) + (pp & 1) * 4);
+  const uint32_t a_addr[2] = {lds0 + a_lo, lds0 + 4 * SLOT4 * 2 + a_lo};
+  const uint32_t b_addr[2] = {lds0 + b_lo, lds0 + 4 * SLOT4 * 2 + b_lo};
+  typedef bf16x8_t AF[4][2];
+  typedef bf16x8_t BF[2][2];
+  // fragment i of a half: A (mt, kk) = (i % 4, i / 4), B (nt, kk) = (i % 2, i / 2); slot-in-set SL
+  auto read_a1 = [&](int t, auto sl, AF& f, auto ic) {
+    constexpr int SL = decltype(sl)::value, I = decltype(ic)::value;
+    constexpr int OFF = SL * SLOT4 * 2 + (I / 4) * 32 * 256;
+    f[I % 4][I / 4] = cat44(tr4x<(I % 4) << 5, OFF>(a_addr[t & 1]), tr4x<(I % 4) << 5, OFF + 1024>(a_addr[t & 1]));
+  };
+  auto read_b1 = [&](int t, auto sl, BF& f, auto ic) {
+    constexpr int SL = decltype(sl)::value, I = decltype(ic)::value;
+    constexpr int OFF = SL * SLOT4 * 2 + (I / 2) * 32 * 256;
+    f[I % 2][I / 2] = cat44(tr4x<(I % 2) << 5, OFF>(b_addr[t & 1]), tr4x<(I % 2) << 5, OFF + 1024>(b_addr[t & 1]));
+  };
+  f32x4_t acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  // one phase: the quadrant's 16 MFMAs (kk-major), fragment read r of the next phase issued just
+  // before MFMA r (r < NR), each pair fenced (inline-asm reads are invisible to the scheduler's
+  // instruction groups)
+  auto phase = [&](auto mh, auto nh, const AF& a, const BF& b, auto nreads, auto&& rd) {
+    constexpr int MH = decltype(mh)::value, NH = decltype(nh)::value, NR = decltype(nreads)::value;
+    static_for<16>([&](auto ic) {
+      constexpr int i = decltype(ic)::value;
+      if constexpr (i < NR) rd(ic);
+      constexpr int kk = i / 8, mt = (i % 8) / 2, nt = i % 2;
+      acc[MH * 4 + mt][NH * 2 + nt] = mfma16(b[nt][kk], a[mt][kk], acc[MH * 4 + mt][NH * 2 + nt]);
+      __builtin_amdgcn_sched_barrier(0);
+    });
+  };
+  // the transposing reads are inline asm (hipcc would drain the LDS-DMA ring before builtin ones),
+  // so the waits for their results are explicit: lgkmcnt(0) + barrier at every phase start, where
+  // the previous phase's reads are exactly the ones this phase's MFMAs consume
+  auto sync = [&](auto n) {
+    constexpr int V = decltype(n)::value;
+    if constexpr (V == 12) asm volatile("s_waitcnt vmcnt(12) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    else if constexpr (V == 10) asm volatile("s_waitcnt vmcnt(10) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    else if constexpr (V == 6) asm volatile("s_waitcnt vmcnt(6) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    else if constexpr (V == 4) asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    else if constexpr (V == 2) asm volatile("s_waitcnt vmcnt(2) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    else if constexpr (V == 0) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    else asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  using I2 = std::integral_constant<int, 2>;
+  using I3 = std::integral_constant<int, 3>;
+  using I4 = std::integral_constant<int, 4>;
+  using I6 = std::integral_constant<int, 6>;
+  using I8 = std::integral_constant<int, 8>;
+  using I10 = std::integral_constant<int, 10>;
+  using I12 = std::integral_constant<int, 12>;
+  using IN = std::integral_constant<int, -1>;
+
+  AF ax, ay;
+  BF bp, bq;
+  auto ktile = [&](auto kind, int t, BF& b0, BF& b1) {
+    constexpr int KIND = decltype(kind)::value;
+    // q1 (0,0): read b1(t)
+    sync(std::conditional_t<KIND == 0, I4, I12>{});
+    if constexpr (KIND == 2) issue(t + 2, I0{});
+    phase(I0{}, I0{}, ax, b0, I4{}, [&](auto i) { read_b1(t, I3{}, b1, i); });
+    // q2 (0,1): read a1(t)
+    sync(std::conditional_t<KIND == 0, I2, std::conditional_t<KIND == 1, I10, I12>>{});
+    if constexpr (KIND == 2) issue(t + 2, I3{});
+    phase(I0{}, I1{}, ax, b1, I8{}, [&](auto i) { read_a1(t, I1{}, ay, i); });
+    // q3 (1,1): no reads
+    sync(IN{});
+    if constexpr (KIND == 2) issue(t + 2, I1{});
+    phase(I1{}, I1{}, ay, b1, I0{}, [&](auto) {});
+    // q4 (1,0): read a0(t+1), b0(t+1) (into b1, free after q3)
+    if constexpr (KIND > 0) {
+      sync(std::conditional_t<KIND == 1, I0, I6>{});
+      if constexpr (KIND == 2) issue(t + 2, I2{});
+      phase(I1{}, I0{}, ay, b0, I12{}, [&](auto i) {
+        constexpr int I = decltype(i)::value;
+        if constexpr (I < 8) read_a1(t + 1, I0{}, ax, i);
+        else read_b1(t + 1, I2{}, b1, std::integral_constant<int, I - 8>{});
+      });
+    } else {
+      phase(I1{}, I0{}, ay, b0, I0{}, [&](auto) {});
+    }
+  };
+  using K2 = std::integral_constant<int, 2>;
+  using K1 = std::integral_constant<int, 1>;
+  using K0 = std::integral_constant<int, 0>;
+
+  issue(0, I0{});
+  issue(0, I3{});
+  issue(0, I1{});
+  issue(0, I2{});
+  issue(1, I0{});
+  issue(1, I3{});
+  issue(1, I1{});
+  sync(I6{});
+  issue(1, I2{});
+  static_for<8>([&](auto i) { read_a1(0, I0{}, ax, i); });
+  static_for<4>([&](auto i) { read_b1(0, I2{}, bp, i); });
+  int t = 0;
+  for (; t + 4 <= nk; t += 2) {
+    ktile(K2{}, t, bp, bq);
+    ktile(K2{}, t + 1, bq, bp);
+  }
+  ktile(K1{}, t, bp, bq);
+  ktile(K0{}, t + 1, bq, bp);
+
+  // ---- epilogue: acc[mt][nt][i] = G[n0 + wr*128 + mt*16 + l16][k0 + wc*64 + nt*16 + 4g + i]
+  const bool to_g = !ACC && g0 != nullptr && split == 0;  // workgroup-uniform
+  float* dst = ACC ? out : to_g ? g0 : out + (long)(g0 != nullptr ? split - 1 : split) * split_stride;
+  const long ld = to_g ? ldg0 : ldo;
+#pragma unroll
+  for (int mt = 0; mt < 8; ++mt) {
+    const int n = n0 + wr * 128 + mt * 16 + l16;
+    float* row = dst + (long)n * ld + k0 + wc * 64 + 4 * g;
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+      float v[4] = {acc[mt][nt][0], acc[mt][nt][1], acc[mt][nt][2], acc[mt][nt][3]};
+      if (ACC || to_g) {
+        float o[4];
+        load4(row + nt * 16, o);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[i] += o[i];
+      }
+      store4(row + nt * 16, v);
+    }
+  }
+}
+
 }  // namespace
 
 size_t jm_gemm_tn_smem() { return (size_t)NST * STAGE * sizeof(uint16_t); }
@@ -260,14 +507,18 @@ size_t jm_gemm_tn_smem() { return (size_t)NST * STAGE * sizeof(uint16_t); }
 // Split of the M range: returns steps (of 32 rows) per split; *S_out = number of splits.
 // Picks the split count that minimises an estimate of (waves of 256 CUs) x (steps per split +
 // epilogue) + the fp32 partial-tile traffic of the reduction.
+int g_tn4 = 1;  // A/B: 4-phase TN kernel (default) vs the r1 32-row-step kernel (jm_gemm_tn_set_variant)
+void jm_gemm_tn_set_variant(int v) { g_tn4 = v == 4; }
+
 int jm_gemm_tn_plan(int M, int N, int K, int* S_out) {
   const int tiles = (N / TN_) * (K / TK_);
   const int steps = (M + BS - 1) / BS;
+  const int unit = g_tn4 ? 4 : 2;  // steps per split: whole 128-row (4-phase) / 64-row pairs
   double best = 1e30;
-  int best_sps = steps + (steps & 1), best_S = 1;
+  int best_sps = (steps + unit - 1) / unit * unit, best_S = 1;
   for (int S = 1; S <= 128; ++S) {
     int sps = (steps + S - 1) / S;
-    sps += sps & 1;
+    sps = (sps + unit - 1) / unit * unit;
     if (sps < 4 && S > 1) break;
     const int s_eff = (steps + sps - 1) / sps;
     const long wgs = (long)tiles * s_eff;
@@ -300,6 +551,28 @@ int jm_gemm_tn(const uint16_t* A, long lda, const uint16_t* B, long ldb, int M, 
   if ((long)M * lda * 2 >= (1L << 32) || (long)M * ldb * 2 >= (1L << 32)) return -2;
   const int tiles = (N / TN_) * (K / TK_);
   const size_t sm = jm_gemm_tn_smem();
+  if (g_tn4 && sps % 4 == 0) {
+    if (S == 1) {
+      static bool attr = false;
+      if (!attr) {
+        (void)hipFuncSetAttribute((const void*)gemm_tn4_kernel<1, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)sm);
+        attr = true;
+      }
+      gemm_tn4_kernel<1, false><<<tiles, NTH, sm, st>>>(A, lda, B, ldb, M, N, K, sps, G, ldo, 0);
+    } else {
+      if (partial == nullptr) return -3;
+      static bool attr = false;
+      if (!attr) {
+        (void)hipFuncSetAttribute((const void*)gemm_tn4_kernel<0, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)sm);
+        attr = true;
+      }
+      gemm_tn4_kernel<0, false><<<tiles * S, NTH, sm, st>>>(A, lda, B, ldb, M, N, K, sps, partial, K, (long)N * K,
+                                                            TnSegs{}, g_tn_acc0 ? G : nullptr, ldo);
+    }
+    return 0;
+  }
   if (S == 1) {
     static bool attr = false;
     if (!attr) {
@@ -328,6 +601,28 @@ int jm_gemm_tn_seg(const TnSegs& segs, long lda, long ldb, int N, int K, int sps
   const int M = segs.rows * segs.n;
   const int tiles = (N / TN_) * (K / TK_);
   const size_t sm = jm_gemm_tn_smem();
+  if (g_tn4 && sps % 4 == 0 && segs.rows % 64 == 0) {
+    if (S == 1) {
+      static bool attr = false;
+      if (!attr) {
+        (void)hipFuncSetAttribute((const void*)gemm_tn4_kernel<1, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)sm);
+        attr = true;
+      }
+      gemm_tn4_kernel<1, true><<<tiles, NTH, sm, st>>>(nullptr, lda, nullptr, ldb, M, N, K, sps, G, ldo, 0, segs);
+    } else {
+      if (partial == nullptr) return -3;
+      static bool attr = false;
+      if (!attr) {
+        (void)hipFuncSetAttribute((const void*)gemm_tn4_kernel<0, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)sm);
+        attr = true;
+      }
+      gemm_tn4_kernel<0, true><<<tiles * S, NTH, sm, st>>>(nullptr, lda, nullptr, ldb, M, N, K, sps, partial, K,
+                                                           (long)N * K, segs, g_tn_acc0 ? G : nullptr, ldo);
+    }
+    return 0;
+  }
   if (S == 1) {
     static bool attr = false;
     if (!attr) {

@@ -22,6 +22,7 @@ def _reset_gemm_variant(request):
         request.getfixturevalue("ext").ln_set_bwd_la(2)
         request.getfixturevalue("ext").attn_set_bwd_ppw(0)
         request.getfixturevalue("ext").gemm_tn_set_acc0(0)
+        request.getfixturevalue("ext").gemm_tn_set_variant(4)
 
 
 def rel(a, b):
@@ -274,11 +275,15 @@ def test_transpose_bf16(ext, R, C):
     assert torch.equal(y, x.t())
 
 
+@pytest.mark.parametrize("variant", [4, 0])
 @pytest.mark.parametrize("acc0", [1, 0])
-@pytest.mark.parametrize("M,N,K", [(4096, 256, 512), (3000, 512, 256), (512, 768, 1024), (26624, 1024, 256)])
-def test_gemm_tn_wgrad(ext, M, N, K, acc0):
+@pytest.mark.parametrize("M,N,K", [(4096, 256, 512), (3000, 512, 256), (512, 768, 1024), (26624, 1024, 256),
+                                   (101888, 512, 512), (200, 256, 256)])
+def test_gemm_tn_wgrad(ext, M, N, K, acc0, variant):
     """Weight-gradient TN MFMA GEMM (csrc/gemm_tn.hip): G += dy^T x, split over M, ragged M; acc0:
-    split 0 accumulates straight into G (S - 1 partial slices) or every split stores a partial."""
+    split 0 accumulates straight into G (S - 1 partial slices) or every split stores a partial;
+    variant 4 = the 4-phase kernel (default), 0 = the r1 32-row-step kernel."""
+    ext.gemm_tn_set_variant(variant)
     ext.gemm_tn_set_acc0(acc0)
     torch.manual_seed(0)
     dy = (torch.rand(M, N, device="cuda") * 2 - 1).bfloat16()
@@ -287,6 +292,7 @@ def test_gemm_tn_wgrad(ext, M, N, K, acc0):
     ref = g.double() + dy.double().t() @ x.double()
     S = ext.gemm_tn_wgrad(dy, x, g)
     ext.gemm_tn_set_acc0(0)
+    ext.gemm_tn_set_variant(4)
     assert S >= 1 and (S > 1 or M < 8192)
     assert rel(g, ref) < 1e-4
 

@@ -40,22 +40,37 @@ def timeit(fn, iters=10):
 
 
 def main():
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--variants", default="4,0", help="TN kernel variants (gemm_tn_set_variant), first = 'ours'")
+    ap.add_argument("--only", default="")
+    a = ap.parse_args()
+    vs = [int(v) for v in a.variants.split(",")]
     ext = _ext.load()
     to_t = tb_t = 0.0
     for name, (M, N, K) in SHAPES.items():
+        if a.only and name not in a.only.split(","):
+            continue
         dy = (torch.rand(M, N, device="cuda") * 2 - 1).bfloat16()
         x = (torch.rand(M, K, device="cuda") * 2 - 1).bfloat16()
         g0 = torch.zeros(N, K, device="cuda")
         g1 = torch.zeros(N, K, device="cuda")
+        ext.gemm_tn_set_variant(vs[0])
         S = ext.gemm_tn_wgrad(dy, x, g0)
         blas(dy, x, g1)
         err = ((g0 - g1).abs().max() / g1.abs().max()).item()
-        tos, tbs = [], []
+        tv = {v: [] for v in vs}
+        tbs = []
         for _ in range(3):
-            tos.append(timeit(lambda: ext.gemm_tn_wgrad(dy, x, g0)))
+            for v in vs:
+                ext.gemm_tn_set_variant(v)
+                tv[v].append(timeit(lambda: ext.gemm_tn_wgrad(dy, x, g0)))
             tbs.append(timeit(lambda: blas(dy, x, g1)))
-        to, tb = min(tos), min(tbs)
+        ext.gemm_tn_set_variant(vs[0])
+        to, tb = min(tv[vs[0]]), min(tbs)
         fl = 2.0 * M * N * K
+        if len(vs) > 1:
+            print("   " + "  ".join(f"v{v}: {min(tv[v]):7.1f} us {fl / min(tv[v]) / 1e6:5.0f} TF" for v in vs), flush=True)
         to_t += to
         tb_t += tb
         print(f"{name:8s} M={M:6d} N={N:5d} K={K:5d} S={S:3d}  ours {to:8.1f} us {fl / to / 1e6:6.0f} TF | "
