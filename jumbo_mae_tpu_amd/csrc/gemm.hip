@@ -675,31 +675,38 @@ __global__ __launch_bounds__(512, 1) void gemm_nt64_kernel(const uint16_t* __res
 // acc = A[m0:m0+256, k_begin:k_begin+K] . B[n0:n0+256, same]^T  (K % 128 == 0, K > 0); every LDS
 // slot is free on entry (caller's barrier) and the ring is drained on exit except for the reads
 // of the last K-tile's MFMAs (caller's epilogue barriers before reusing LDS).
-template <int SCHED>
+template <int SCHED, int NW = 8>
 __attribute__((always_inline)) JM_DEVICE void p4_mainloop(const uint16_t* __restrict__ A, long lda,
                                                           const uint16_t* __restrict__ B, long ldb, int M, int N,
-                                                          int m0, int n0, int k_begin, int K, f32x4_t (&acc)[8][4],
-                                                          uint16_t* smem) {
-  constexpr int NTW = 4, BK2 = 64, SLOT = 128 * BK2;  // elements per slot (16 KB)
+                                                          int m0, int n0, int k_begin, int K,
+                                                          f32x4_t (&acc)[8][16 / NW * 2], uint16_t* smem) {
+  // NW = 8: 2 x 4 waves of 128 x 64 (2 waves / SIMD); NW = 4: 2 x 2 waves of 128 x 128 (one wave
+  // per SIMD, 256 accumulator registers)
+  constexpr int WN = NW / 2;          // waves along N
+  constexpr int QC = 128 / WN;        // columns of a wave's quadrant (32 / 64)
+  constexpr int NTQ = QC / 16;        // 16-wide n tiles per quadrant (2 / 4)
+  constexpr int NTW = 2 * NTQ;        // per wave (4 / 8)
+  constexpr int P = 16 / NW;          // glds pieces per wave and slot (2 / 4)
+  constexpr int BK2 = 64, SLOT = 128 * BK2;  // elements per slot (16 KB)
   int tid = threadIdx.x;
   // opaque copy: in the persistent kernel the per-lane offsets below are then recomputed per work
   // item instead of being hoisted out of its item loop (they would stay live across the K loop)
   asm volatile("" : "+v"(tid));
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
   const int l16 = lane & 15, g = lane >> 4;
-  const int wr = wave >> 2, wc = wave & 3;
+  const int wr = wave / WN, wc = wave % WN;
   const __amdgpu_buffer_rsrc_t ra = make_rsrc(A + (long)m0 * lda + k_begin, (long)(M - m0) * lda * 2 - 2L * k_begin);
   const __amdgpu_buffer_rsrc_t rb = make_rsrc(B + (long)n0 * ldb + k_begin, (long)(N - n0) * ldb * 2 - 2L * k_begin);
-  // glds pieces: slot rows q*8 + (lane >> 3), q = 2 * wave + r; slot row -> tile row / column
-  uint32_t a_src[2][2], b_src[2][2];  // [half][r] byte offsets
+  // glds pieces: slot rows q*8 + (lane >> 3), q = P * wave + r; slot row -> tile row / column
+  uint32_t a_src[2][P], b_src[2][P];  // [half][r] byte offsets
 #pragma unroll
-  for (int r = 0; r < 2; ++r) {
-    const int srow = (2 * wave + r) * 8 + (lane >> 3);
+  for (int r = 0; r < P; ++r) {
+    const int srow = (P * wave + r) * 8 + (lane >> 3);
     const int c = (lane & 7) ^ swz64(srow);
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const int arow = (srow >> 6) * 128 + h * 64 + (srow & 63);
-      const int bcol = (srow >> 5) * 64 + h * 32 + (srow & 31);
+      const int bcol = (srow / QC) * (2 * QC) + h * QC + (srow % QC);
       a_src[h][r] = (uint32_t)((arow * lda + c * 8) * 2);
       b_src[h][r] = (uint32_t)((bcol * ldb + c * 8) * 2);
     }
@@ -711,17 +718,17 @@ __attribute__((always_inline)) JM_DEVICE void p4_mainloop(const uint16_t* __rest
       if (t >= 2) return;  // ablation: no loads after the prologue
     }
     const uint32_t k0b = t * BK2 * 2;
-    uint16_t* l = smem + ((t & 1) * 4 + S) * SLOT + (2 * wave) * 8 * BK2;
+    uint16_t* l = smem + ((t & 1) * 4 + S) * SLOT + (P * wave) * 8 * BK2;
 #pragma unroll
-    for (int r = 0; r < 2; ++r) {
+    for (int r = 0; r < P; ++r) {
       if constexpr (S < 2) blds16(ra, a_src[S][r], k0b, l + r * 8 * BK2);
       else blds16(rb, b_src[S - 2][r], k0b, l + r * 8 * BK2);
     }
   };
   const int ch0 = ((0 * 4 + g) ^ swz64(l16)) * 8, ch1 = ((1 * 4 + g) ^ swz64(l16)) * 8;
-  const int a_row = (wr * 64 + l16) * BK2, b_row = (wc * 32 + l16) * BK2;
-  typedef bf16x8_t AF[4][2];  // [mt within the half][k32 step]
-  typedef bf16x8_t BF[2][2];  // [nt within the half][k32 step]
+  const int a_row = (wr * 64 + l16) * BK2, b_row = (wc * QC + l16) * BK2;
+  typedef bf16x8_t AF[4][2];    // [mt within the half][k32 step]
+  typedef bf16x8_t BF[NTQ][2];  // [nt within the half][k32 step]
   auto read_a = [&](int t, auto half, AF& f) {
     const uint16_t* base = smem + ((t & 1) * 4 + decltype(half)::value) * SLOT + a_row;
 #pragma unroll
@@ -733,7 +740,7 @@ __attribute__((always_inline)) JM_DEVICE void p4_mainloop(const uint16_t* __rest
   auto read_b = [&](int t, auto half, BF& f) {
     const uint16_t* base = smem + ((t & 1) * 4 + 2 + decltype(half)::value) * SLOT + b_row;
 #pragma unroll
-    for (int nt = 0; nt < 2; ++nt) {
+    for (int nt = 0; nt < NTQ; ++nt) {
       f[nt][0] = lds8(base + nt * 16 * BK2 + ch0);
       f[nt][1] = lds8(base + nt * 16 * BK2 + ch1);
     }
@@ -749,28 +756,25 @@ __attribute__((always_inline)) JM_DEVICE void p4_mainloop(const uint16_t* __rest
 #pragma unroll
       for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
-        for (int nt = 0; nt < 2; ++nt)
-          acc[MH * 4 + mt][NH * 2 + nt] = mfma16(b[nt][kk], a[mt][kk], acc[MH * 4 + mt][NH * 2 + nt]);
+        for (int nt = 0; nt < NTQ; ++nt)
+          acc[MH * 4 + mt][NH * NTQ + nt] = mfma16(b[nt][kk], a[mt][kk], acc[MH * 4 + mt][NH * NTQ + nt]);
   };
-  auto sync = [&](auto n) {  // vmcnt(n) lgkmcnt(0) s_barrier; n < 0: no vmcnt wait
-    constexpr int V = (SCHED & 16) ? -1 : decltype(n)::value;
+  // vmcnt(n * P) lgkmcnt(0) s_barrier (n in phase units of P glds); n < 0: no vmcnt wait
+  auto sync = [&](auto n) {
+    constexpr int V = (SCHED & 16) ? -1 : decltype(n)::value * P;
     if constexpr ((SCHED & 32) != 0) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    else if constexpr (V == 12) asm volatile("s_waitcnt vmcnt(12) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    else if constexpr (V == 10) asm volatile("s_waitcnt vmcnt(10) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    else if constexpr (V == 6) asm volatile("s_waitcnt vmcnt(6) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    else if constexpr (V == 4) asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    else if constexpr (V == 2) asm volatile("s_waitcnt vmcnt(2) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    else if constexpr (V == 0) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    else if constexpr (V >= 0) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"i"(V) : "memory");
     else asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
   };
-  // the phase's instruction order: its ds_reads spread over the 16 MFMAs (one after each of the
-  // first NR MFMAs when NR > 8, else one every 16 / NR), with SCHED & 2 the glds after MFMAs 1, 5
+  // the phase's instruction order: its NR ds_reads spread evenly over its NM MFMAs, with SCHED & 2
+  // the glds after MFMAs 1, 5
   auto interleave = [&](auto nreads, auto nglds) {
+    constexpr int NM = 8 * NTQ;
     constexpr int NR = decltype(nreads)::value, NG = (SCHED & 2) ? decltype(nglds)::value : 0;
-    constexpr int PER = NR > 8 ? 1 : 16 / (NR > 0 ? NR : 1);
+    constexpr int PER = NR >= NM ? 1 : NM / (NR > 0 ? NR : 1);
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
+    for (int i = 0; i < NM; ++i) {
       __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
       if (i % PER == 0 && i / PER < NR) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
       if (NG > 0 && (i == 1 || i == 5)) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
@@ -784,32 +788,32 @@ __attribute__((always_inline)) JM_DEVICE void p4_mainloop(const uint16_t* __rest
   using I1 = std::integral_constant<int, 1>;
   using I2 = std::integral_constant<int, 2>;
   using I3 = std::integral_constant<int, 3>;
-  using I4 = std::integral_constant<int, 4>;
+  using I5 = std::integral_constant<int, 5>;
   using I6 = std::integral_constant<int, 6>;
   using I8 = std::integral_constant<int, 8>;
-  using I10 = std::integral_constant<int, 10>;
-  using I12 = std::integral_constant<int, 12>;
-  using I16 = std::integral_constant<int, 16>;
   using IN = std::integral_constant<int, -1>;
-  using IX = std::integral_constant<int, -2>;  // no barrier at all
+  using RB = std::integral_constant<int, 2 * NTQ>;      // fragment reads of a B half
+  using RQ4 = std::integral_constant<int, 8 + 2 * NTQ>;  // q4: a0 + b0 of the next tile
 
   AF ax, ay;
   BF bp, bq;
   // one K-tile: b0 holds its b0 fragments (read during the previous tile's q4), b1 receives b1 and
   // then the next tile's b0.  KIND 2 = steady (issues tile t + 2), 1 = next-to-last, 0 = last.
+  // Counted waits (phases of P glds issued after the one that must have landed): q1 6, q2 6,
+  // q3 none, q4 3; next-to-last 6 5 - 0; last 2 1 - -.
   auto tile = [&](auto kind, int t, BF& b0, BF& b1) {
     constexpr int KIND = decltype(kind)::value;
     using G = std::integral_constant<int, KIND == 2 ? 2 : 0>;
     // q1 (0,0): read b1(t)
-    sync(std::conditional_t<KIND == 0, I4, I12>{});
+    sync(std::conditional_t<KIND == 0, I2, I6>{});
     prio(I1{});
     if constexpr (KIND == 2) issue(t + 2, I0{});
     read_b(t, I1{}, b1);
     mfma_q(I0{}, I0{}, ax, b0);
-    interleave(I4{}, G{});
+    interleave(RB{}, G{});
     prio(I0{});
     // q2 (0,1): read a1(t)
-    sync(std::conditional_t<KIND == 0, I2, std::conditional_t<KIND == 1, I10, I12>>{});
+    sync(std::conditional_t<KIND == 0, I1, std::conditional_t<KIND == 1, I5, I6>>{});
     prio(I1{});
     if constexpr (KIND == 2) issue(t + 2, I3{});
     read_a(t, I1{}, ay);
@@ -825,13 +829,13 @@ __attribute__((always_inline)) JM_DEVICE void p4_mainloop(const uint16_t* __rest
     prio(I0{});
     // q4 (1,0): read a0(t+1), b0(t+1) (into b1, free after q3)
     if constexpr (KIND > 0) {
-      sync(std::conditional_t<KIND == 1, I0, I6>{});
+      sync(std::conditional_t<KIND == 1, I0, I3>{});
       prio(I1{});
       if constexpr (KIND == 2) issue(t + 2, I2{});
       read_a(t + 1, I0{}, ax);
       read_b(t + 1, I0{}, b1);
       mfma_q(I1{}, I0{}, ay, b0);
-      interleave(I12{}, G{});
+      interleave(RQ4{}, G{});
       prio(I0{});
     } else {
       mfma_q(I1{}, I0{}, ay, b0);
@@ -852,7 +856,7 @@ __attribute__((always_inline)) JM_DEVICE void p4_mainloop(const uint16_t* __rest
   issue(1, I0{});
   issue(1, I3{});
   issue(1, I1{});
-  sync(I6{});
+  sync(I3{});
   issue(1, I2{});
   read_a(0, I0{}, ax);
   read_b(0, I0{}, bp);
@@ -864,19 +868,17 @@ __attribute__((always_inline)) JM_DEVICE void p4_mainloop(const uint16_t* __rest
   // nk - t == 2: the last two tiles (nk - 2 -> KIND 1, nk - 1 -> KIND 0)
   tile(K1{}, t, bp, bq);
   tile(K0{}, t + 1, bq, bp);
-  (void)IX{};
-  (void)I16{};
 }
 
 // the 256 x 256 tile's epilogue from the p4 accumulators (EPI_PARTIAL: fp32 split slice)
-template <int EPI>
-__attribute__((always_inline)) JM_DEVICE void p4_epilogue(const f32x4_t (&acc)[8][4], const GemmEpi& ep, int M, int N,
-                                                          int m0, int n0, int split, uint16_t* smem) {
-  constexpr int NTW = 4;
+template <int EPI, int NW = 8>
+__attribute__((always_inline)) JM_DEVICE void p4_epilogue(const f32x4_t (&acc)[8][16 / NW * 2], const GemmEpi& ep,
+                                                          int M, int N, int m0, int n0, int split, uint16_t* smem) {
+  constexpr int NTW = 16 / NW * 2, WN = NW / 2;
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
   const int l16 = lane & 15, g = lane >> 4;
-  const int wr = wave >> 2, wc = wave & 3;
+  const int wr = wave / WN, wc = wave % WN;
   if (EPI == EPI_PARTIAL) {
     float* dst = ep.part + (long)split * M * N;
 #pragma unroll
@@ -892,18 +894,21 @@ __attribute__((always_inline)) JM_DEVICE void p4_epilogue(const f32x4_t (&acc)[8
       }
     }
   } else if (N % 8 == 0)
-    epilogue_lds<EPI, NTW, 512, BN, true>(acc, ep, smem, M, N, m0, n0, wr, wc, l16, g);
+    epilogue_lds<EPI, NTW, 64 * NW, BN, true>(acc, ep, smem, M, N, m0, n0, wr, wc, l16, g);
   else
     epilogue<EPI, NTW>(acc, ep, M, N, m0 + wr * 128, n0 + wc * NTW * 16, l16, g);
 }
 
+// SCHED bit 64: 4 waves (2 x 2, 128 x 128 each, one wave per SIMD) instead of 8
 template <int EPI, int SCHED>
-__global__ __launch_bounds__(512, 1) void gemm_p4_kernel(const uint16_t* __restrict__ A, long lda,
-                                                         const uint16_t* __restrict__ B, long ldb, int M, int N,
-                                                         int K, GemmEpi ep, int GROUP_M) {
-  JM_DGUARD(blockDim.x == 512 && K % 128 == 0 && M > 0 && N > 0);
+__global__ __launch_bounds__((SCHED & 64) ? 256 : 512, 1) void gemm_p4_kernel(const uint16_t* __restrict__ A, long lda,
+                                                                             const uint16_t* __restrict__ B, long ldb,
+                                                                             int M, int N, int K, GemmEpi ep,
+                                                                             int GROUP_M) {
+  constexpr int NW = (SCHED & 64) ? 4 : 8;
+  JM_DGUARD(blockDim.x == 64 * NW && K % 128 == 0 && M > 0 && N > 0);
   extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
-  if constexpr ((SCHED & 4) != 0) {
+  if constexpr ((SCHED & 4) != 0 && NW == 8) {
     if (__builtin_amdgcn_readfirstlane(threadIdx.x) >= 256) __builtin_amdgcn_s_setprio(1);
   }
   int m0, n0, split = 0;
@@ -915,9 +920,9 @@ __global__ __launch_bounds__(512, 1) void gemm_p4_kernel(const uint16_t* __restr
     k_begin = ku0 * 128;
     K = (ku1 - ku0) * 128;
   }
-  f32x4_t acc[8][4];
-  p4_mainloop<SCHED & ~4>(A, lda, B, ldb, M, N, m0, n0, k_begin, K, acc, smem);
-  p4_epilogue<EPI>(acc, ep, M, N, m0, n0, split, smem);
+  f32x4_t acc[8][16 / NW * 2];
+  p4_mainloop<SCHED & ~(4 | 64), NW>(A, lda, B, ldb, M, N, m0, n0, k_begin, K, acc, smem);
+  p4_epilogue<EPI, NW>(acc, ep, M, N, m0, n0, split, smem);
 }
 
 // ------------------------------------------------------------------ persistent DP + stream-K
@@ -1554,7 +1559,7 @@ void launch_p4s(const uint16_t* A, long lda, const uint16_t* B, long ldb, int M,
                               (int)sm);
     attr = true;
   }
-  gemm_p4_kernel<EPI, SCHED><<<nwg, 512, sm, st>>>(A, lda, B, ldb, M, N, K, ep, g_gemm_group);
+  gemm_p4_kernel<EPI, SCHED><<<nwg, (SCHED & 64) ? 256 : 512, sm, st>>>(A, lda, B, ldb, M, N, K, ep, g_gemm_group);
 }
 
 int g_p4_sched = 4;  // A/B: variant 20 + SCHED bits (variants 21..83 = 20 + bits)
@@ -1648,6 +1653,7 @@ void launch_p4(const uint16_t* A, long lda, const uint16_t* B, long ldb, int M, 
     case 3: return launch_p4s<EPI, 3>(A, lda, B, ldb, M, N, K, ep, nwg, st);
     case 4: return launch_p4s<EPI, 4>(A, lda, B, ldb, M, N, K, ep, nwg, st);
     case 6: return launch_p4s<EPI, 6>(A, lda, B, ldb, M, N, K, ep, nwg, st);
+    case 64: return launch_p4s<EPI, 64>(A, lda, B, ldb, M, N, K, ep, nwg, st);
     case 12: if constexpr (EPI == EPI_STORE) return launch_p4s<EPI, 12>(A, lda, B, ldb, M, N, K, ep, nwg, st); break;
     case 20: if constexpr (EPI == EPI_STORE) return launch_p4s<EPI, 20>(A, lda, B, ldb, M, N, K, ep, nwg, st); break;
     case 52: if constexpr (EPI == EPI_STORE) return launch_p4s<EPI, 52>(A, lda, B, ldb, M, N, K, ep, nwg, st); break;
@@ -1739,7 +1745,7 @@ void launch_tail(const uint16_t* A, long lda, const uint16_t* B, long ldb, int M
 }  // namespace
 
 void jm_gemm_set_variant(int wn, int group) {
-  if (wn >= 20 && wn < 84) {  // 4-phase kernel + SCHED bits
+  if (wn >= 20 && wn < 148) {  // 4-phase kernel + SCHED bits
     g_p4_sched = wn - 20;
     wn = 20;
   }

@@ -201,7 +201,7 @@ def test_optimizer_hip_matches_torch(kind, clip):
     assert rel(res[0], res[1]) < 1e-5
 
 
-@pytest.mark.parametrize("variant", [4, 2, 5, 6, 7, 8, 10, 11, 12, 20, 21, 22, 24])
+@pytest.mark.parametrize("variant", [4, 2, 5, 6, 7, 8, 10, 11, 12, 20, 21, 22, 24, 84])
 @pytest.mark.parametrize("M,N,K,gelu", [(512, 256, 64, False), (300, 196, 128, True), (1000, 1536, 512, False),
                                         (257, 260, 192, True), (16100, 2048, 128, True), (40000, 520, 64, False)])
 def test_gemm_nt(ext, M, N, K, gelu, variant):
@@ -247,7 +247,7 @@ def test_attention_long_sequence_path(ext, B, S, H, hd):
     assert torch.equal(dqkv, dqkv2)  # one writer per element: deterministic
 
 
-@pytest.mark.parametrize("variant", [4, 6, 10, 11, 12, 24])
+@pytest.mark.parametrize("variant", [4, 6, 10, 11, 12, 24, 84])
 @pytest.mark.parametrize("M,N,K", [(512, 256, 64), (1000, 1536, 512), (300, 512, 128)])
 def test_gemm_nt_dgelu(ext, M, N, K, variant):
     """FF2 data gradient through the GELU with the FF1 bias gradient (csrc/gemm.hip EPI_DGELU)."""
@@ -342,7 +342,7 @@ def test_residual_ln_fwd_partial_rows(ext, D):
     assert torch.allclose(mu, mur, atol=1e-6) and torch.allclose(rs, rsr, rtol=1e-5)
 
 
-@pytest.mark.parametrize("variant", [4, 6, 10, 11, 12, 24])
+@pytest.mark.parametrize("variant", [4, 6, 10, 11, 12, 24, 84])
 @pytest.mark.parametrize("M,N,K,S", [(512, 3072, 12288, 10), (300, 512, 4096, 3), (512, 256, 1024, 16)])
 def test_gemm_nt_splitk(ext, M, N, K, S, variant):
     """Split-K MFMA GEMM (fp32 partial tiles + bf16 reduce with bias), ragged M."""
@@ -466,7 +466,7 @@ def test_gemm_splitk_fused_fp32_add(ext):
     assert rel(ext.gemm_nt_splitk(A, B, None, 10), ref) < 1e-2
 
 
-@pytest.mark.parametrize("variant", [12, 24])
+@pytest.mark.parametrize("variant", [12, 24, 84])
 @pytest.mark.parametrize("M,N,K", [(1000, 512, 256), (600, 1000, 128)])
 def test_gemm_gelu_saved_derivative(ext, M, N, K, variant):
     """FF1 forward saving gelu'(h) (EPI_GELU_D) and the FF2 data gradient multiplying by it
