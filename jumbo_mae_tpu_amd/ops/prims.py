@@ -91,39 +91,15 @@ _GEMM_MODE = os.environ.get("JMAE_GEMM", "auto")  # auto | blas | ours (forward 
 _DGRAD_OURS = os.environ.get("JMAE_DGRAD", "1") == "1"  # data-gradient GEMMs on the MFMA kernel
 
 
-# flagship shapes the rule below would reject but where the MFMA kernel measured faster
-# (tools/gemm_nt_bench.py, profiles/r1_gemm_nt_vs_hipblaslt_v2.txt): ViT-L encoder QKV / Wo and
-# MAE-decoder Wo data gradients (1.05x, 1.08x, 1.11x), decoder Wo forward (1.02x)
-_OURS_MEASURED = {"dgrad": {(26624, 1024, 3072), (26624, 1024, 1024), (101888, 512, 512), (26624, 768, 768)},
-                  "fwd": {(101888, 512, 512), (26624, 768, 768)}}
-# ... and shapes the rule would accept where hipBLASLt measured faster (ViT-B encoder QKV forward,
-# 105 vs 98 us; profiles/r1_gemm_vitb_shapes.txt)
-_BLAS_MEASURED = {"fwd": {(26624, 2304, 768)}, "dgrad": set()}
-
-
 def use_our_gemm(M: int, N: int, K: int, fused_gelu: bool = False, kind: str = "fwd") -> bool:
-    """Pick the hand-written MFMA GEMM (csrc/gemm.hip) over hipBLASLt for a forward Dense.
-
-    Measured on MI355X (profiles/r1_gemm_nt_vs_hipblaslt.txt): with its LDS-staged epilogue the
-    256x256-tile kernel wins on short-K shapes whose tile count fills the last wave of 256 CUs
-    (decoder QKV 1.48x, decoder FF1+GELU 1.42x, encoder QKV 1.05x) and loses where one partial
-    wave dominates (it has no stream-K) or K is long.  A fused GELU epilogue also saves a full
-    read+write pass, which makes the FF1 shapes worth it at parity."""
+    """Every forward / data-gradient Dense with at least 4096 rows runs on the hand-written MFMA
+    GEMM (csrc/gemm.hip, 4-phase counted-vmcnt kernel): measured on MI355X it matches or beats
+    hipBLASLt on the ViT-L step as a whole (in-process A/B 92.52 vs 92.50 ms,
+    profiles/r2_gemm_routing.txt; per shape profiles/r2_gemm_p4.txt).  Skinny-M GEMMs (the
+    512-row shared jumbo MLP) take the split-K MFMA path (``splitk_plan``) or hipBLASLt."""
     if _GEMM_MODE == "blas":
         return False
-    if K % 64 or N % 8 or M < 4096:
-        return False
-    if _GEMM_MODE == "ours":
-        return True
-    if (M, N, K) in _OURS_MEASURED.get(kind, ()):
-        return True
-    if (M, N, K) in _BLAS_MEASURED.get(kind, ()) and not fused_gelu:
-        return False
-    if K > 1024:
-        return False
-    tiles = -(-M // 256) * -(-N // 256)
-    fill = tiles / (-(-tiles // 256) * 256)
-    return fused_gelu or fill >= 0.9
+    return K % 64 == 0 and N % 8 == 0 and M >= 4096
 
 
 def splitk_plan(M: int, N: int, K: int) -> int:
