@@ -55,10 +55,23 @@ JM_DEVICE f32x4_t mfma(bf16x8_t a, bf16x8_t b, f32x4_t c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
 
+// Workgroup -> (b, h) order: the dispatcher deals consecutive workgroups round-robin over the 8
+// XCDs, so heads h and h + 1 of one token row -- the two halves of a 128-B line at hd = 32 --
+// would be read (and written) through two different L2s.  With remap the grid is relabelled
+// bijectively so that consecutive (b, h) share an XCD (the GEMM tile remap); placement only
+// changes speed, never results.
+JM_DEVICE int xcd_bid(int remap) {
+  const int orig = blockIdx.x, nwg = gridDim.x;
+  if (!(remap & 1)) return orig;
+  const int xcd = orig & 7, q = nwg >> 3, r = nwg & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+}
+
 // --------------------------------------------------------------------------------- forward
 template <int HD, int SP, bool TR>
 __global__ __launch_bounds__(256) void attn_fwd_kernel(const uint16_t* __restrict__ qkv, uint16_t* __restrict__ o,
-                                                       float* __restrict__ lse, int S, int H, float scale) {
+                                                       float* __restrict__ lse, int S, int H, float scale,
+                                                       int remap) {
   JM_DGUARD(S >= 1 && S <= SP && blockDim.x == 256);
   constexpr int KS = HD + 8;  // K row stride (elements), 16-B aligned, breaks bank aliasing
   constexpr int VS = SP + 8;  // V^T row stride
@@ -69,7 +82,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const uint16_t* __restric
   uint16_t* Ks = smem;
   uint16_t* Vt = smem + SP * KS;  // TR: row-major V [SP][KS]; else V^T [HD][VS]
 
-  const int bh = blockIdx.x;
+  const int bh = xcd_bid(remap);
   const int b = bh / H, h = bh - (bh / H) * H;
   const long ts = 3L * H * HD;  // token stride in qkv
   const uint16_t* base = qkv + (long)b * S * ts;
@@ -77,35 +90,79 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const uint16_t* __restric
   const uint16_t* Kg = base + (H + h) * HD;
   const uint16_t* Vg = base + (2 * H + h) * HD;
 
-  constexpr int CPR = HD / 8;
-  for (int i = threadIdx.x; i < SP * CPR; i += 256) {
-    const int r = i / CPR, c = (i % CPR) * 8;
-    uint4 kv = make_uint4(0, 0, 0, 0), vv = make_uint4(0, 0, 0, 0);
-    if (r < S) {
-      kv = *reinterpret_cast<const uint4*>(Kg + r * ts + c);
-      vv = *reinterpret_cast<const uint4*>(Vg + r * ts + c);
-    }
-    *reinterpret_cast<uint4*>(Ks + r * KS + c) = kv;
-    if (TR) {
-      *reinterpret_cast<uint4*>(Vt + r * KS + c) = vv;
-    } else {
-      const uint16_t* vh = reinterpret_cast<const uint16_t*>(&vv);
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int l16 = lane & 15, g = lane >> 4;
+  // the Q fragments of every query tile of this wave, loaded up front so their latency overlaps
+  // the K / V staging instead of stalling each tile (remap bit 1; A/B switch)
+  constexpr int NQW = (SP / 16 + 3) / 4;
+  bf16x8_t qpre[NQW][HD / 32];
+  const bool qp = (remap & 2) != 0;
+  if (qp) {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) Vt[(c + j) * VS + r] = vh[j];
+    for (int i = 0; i < NQW; ++i) {
+      const int q = (wave + 4 * i) * 16 + l16;
+#pragma unroll
+      for (int kk = 0; kk < HD / 32; ++kk) {
+        s16x8_t z = {0, 0, 0, 0, 0, 0, 0, 0};
+        qpre[i][kk] = q < S ? ld8(Qg + (long)q * ts + 32 * kk + 8 * g) : __builtin_bit_cast(bf16x8_t, z);
+      }
+    }
+  }
+  constexpr int CPR = HD / 8;
+  if (TR && (remap & 2)) {
+    // all of this thread's K / V chunks in flight at once (one HBM round trip, not one per chunk)
+    constexpr int NIT = (SP * CPR + 255) / 256;
+    uint4 kv[NIT], vv[NIT];
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+      const int i = it * 256 + threadIdx.x, r = i / CPR, c = (i % CPR) * 8;
+      kv[it] = vv[it] = make_uint4(0, 0, 0, 0);
+      if (i < SP * CPR && r < S) {
+        kv[it] = *reinterpret_cast<const uint4*>(Kg + r * ts + c);
+        vv[it] = *reinterpret_cast<const uint4*>(Vg + r * ts + c);
+      }
+    }
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+      const int i = it * 256 + threadIdx.x, r = i / CPR, c = (i % CPR) * 8;
+      if (i < SP * CPR) {
+        *reinterpret_cast<uint4*>(Ks + r * KS + c) = kv[it];
+        *reinterpret_cast<uint4*>(Vt + r * KS + c) = vv[it];
+      }
+    }
+  } else {
+    for (int i = threadIdx.x; i < SP * CPR; i += 256) {
+      const int r = i / CPR, c = (i % CPR) * 8;
+      uint4 kv = make_uint4(0, 0, 0, 0), vv = make_uint4(0, 0, 0, 0);
+      if (r < S) {
+        kv = *reinterpret_cast<const uint4*>(Kg + r * ts + c);
+        vv = *reinterpret_cast<const uint4*>(Vg + r * ts + c);
+      }
+      *reinterpret_cast<uint4*>(Ks + r * KS + c) = kv;
+      if (TR) {
+        *reinterpret_cast<uint4*>(Vt + r * KS + c) = vv;
+      } else {
+        const uint16_t* vh = reinterpret_cast<const uint16_t*>(&vv);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) Vt[(c + j) * VS + r] = vh[j];
+      }
     }
   }
   __syncthreads();
 
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int l16 = lane & 15, g = lane >> 4;
   const float sl2 = scale * LOG2E;
 
-  for (int qt = wave; qt < NT; qt += 4) {
+#pragma unroll
+  for (int it = 0; it < NQW; ++it) {
+    const int qt = wave + 4 * it;
+    if (qt >= NT) break;
     const int q = qt * 16 + l16;
     bf16x8_t qf[KK];
 #pragma unroll
     for (int kk = 0; kk < KK; ++kk) {
-      if (q < S) {
+      if (qp) {
+        qf[kk] = qpre[it][kk];
+      } else if (q < S) {
         qf[kk] = ld8(Qg + (long)q * ts + 32 * kk + 8 * g);
       } else {
         s16x8_t z = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -191,7 +248,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const uint16_t* __restric
 template <int HD, int SP>
 __global__ __launch_bounds__(256) void attn_fwd_ml_kernel(const uint16_t* __restrict__ qkv, uint16_t* __restrict__ o,
                                                           float* __restrict__ lse, int S, int H, int BH, int hpw,
-                                                          float scale) {
+                                                          float scale, int remap) {
   JM_DGUARD(S >= 1 && S <= SP && hpw >= 1 && blockDim.x == 256);
   constexpr int KS = HD + 8;
   constexpr int NT = SP / 16;
@@ -247,7 +304,7 @@ __global__ __launch_bounds__(256) void attn_fwd_ml_kernel(const uint16_t* __rest
     }
   };
 
-  const int bh0 = blockIdx.x * hpw;
+  const int bh0 = xcd_bid(remap) * hpw;
   load(bh0);
   for (int j = 0; j < hpw; ++j) {
     const int bh = bh0 + j;
@@ -612,7 +669,7 @@ __global__ __launch_bounds__(256) void attn_bwd2_kernel(const uint16_t* __restri
                                                         const uint16_t* __restrict__ dO,
                                                         const float* __restrict__ lse,
                                                         uint16_t* __restrict__ dqkv, int S, int H, float scale,
-                                                        float* __restrict__ dbp, int B, int ppw) {
+                                                        float* __restrict__ dbp, int B, int ppw, int remap) {
   JM_DGUARD(S >= 1 && S <= SP && blockDim.x == 256 && ppw >= 1);
   constexpr int NW = 4, NTH = 256, QC = 64;
   constexpr int NT = SP / 16, KK = HD / 32, DT = HD / 16;
@@ -629,7 +686,8 @@ __global__ __launch_bounds__(256) void attn_bwd2_kernel(const uint16_t* __restri
 
   // one workgroup walks ``ppw`` batch elements of ONE head (blockIdx = bg * H + h): the QKV bias
   // gradient partials stay in registers across them and are reduced across lanes once
-  const int h = blockIdx.x % H, bg = blockIdx.x / H;
+  const int bid = xcd_bid(remap);
+  const int h = bid % H, bg = bid / H;
   const long ts = 3L * H * HD;
   const long os = (long)H * HD;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -666,51 +724,66 @@ __global__ __launch_bounds__(256) void attn_bwd2_kernel(const uint16_t* __restri
   if (dbp != nullptr)
     for (int i = threadIdx.x; i < 3 * HD; i += NTH) bsum[i] = 0.f;
 
+  constexpr int NIT = (SP * NCH + NTH - 1) / NTH;
+  uint4 qv[NIT], kv[NIT], dv[NIT], ov[NIT];
+  bf16x8_t vf[NKW][KK], vfn[NKW][KK];  // vfn: as loaded, vf: the element being computed
+  float lsen = 0.f;
+  // every global load of batch element b into registers in one burst -- V fragments of this
+  // wave's key tiles (the B operand of dP = dO V^T), the Q / K / dO / O rows of the staging and
+  // this thread's lse -- one exposed round trip per element instead of two (enc bwd 132 -> 112 us,
+  // profiles/r2_attn_remap.txt); prefetching the NEXT element's burst during this element's MFMAs
+  // measured slower (occupancy step: 118 us enc, 401 vs 247 us at S = 199)
+  auto load_regs = [&](int b) {
+    const uint16_t* base = qkv + (long)b * S * ts;
+    const uint16_t* Qg = base + h * HD;
+    const uint16_t* Kg = base + (H + h) * HD;
+    const uint16_t* Vg = base + (2 * H + h) * HD;
+    const uint16_t* Og = o + (long)b * S * os + h * HD;
+    const uint16_t* dOg = dO + (long)b * S * os + h * HD;
+#pragma unroll
+    for (int w = 0; w < NKW; ++w) {
+      const int key = (wave + NW * w) * 16 + l16;
+#pragma unroll
+      for (int kk = 0; kk < KK; ++kk) {
+        s16x8_t z = {0, 0, 0, 0, 0, 0, 0, 0};
+        vfn[w][kk] = __builtin_bit_cast(bf16x8_t, z);
+        if (key < S) vfn[w][kk] = ld8(Vg + (long)key * ts + 32 * kk + 8 * g);
+      }
+    }
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+      const int i = it * NTH + threadIdx.x;
+      const int r = i / NCH, c = (i % NCH) * 8;
+      qv[it] = kv[it] = dv[it] = ov[it] = make_uint4(0, 0, 0, 0);
+      if (i < SP * NCH && r < S) {
+        qv[it] = *reinterpret_cast<const uint4*>(Qg + r * ts + c);
+        kv[it] = *reinterpret_cast<const uint4*>(Kg + r * ts + c);
+        dv[it] = *reinterpret_cast<const uint4*>(dOg + r * os + c);
+        ov[it] = *reinterpret_cast<const uint4*>(Og + r * os + c);
+      }
+    }
+    const int i = threadIdx.x;
+    lsen = (i < SP && i < S) ? lse[((long)b * H + h) * S + i] * LOG2E : INFINITY;
+  };
+
   for (int pj = 0; pj < ppw; ++pj) {
   const int b = bg * ppw + pj;
   if (b >= B) break;  // workgroup-uniform
-  const uint16_t* base = qkv + (long)b * S * ts;
-  const uint16_t* Qg = base + h * HD;
-  const uint16_t* Kg = base + (H + h) * HD;
-  const uint16_t* Vg = base + (2 * H + h) * HD;
-  const uint16_t* Og = o + (long)b * S * os + h * HD;
-  const uint16_t* dOg = dO + (long)b * S * os + h * HD;
   uint16_t* dQg = dqkv + (long)b * S * ts + h * HD;
   uint16_t* dKg = dqkv + (long)b * S * ts + (H + h) * HD;
   uint16_t* dVg = dqkv + (long)b * S * ts + (2 * H + h) * HD;
 
-  // V fragments of this wave's key tiles straight from global (B operand of dP = dO V^T)
-  bf16x8_t vf[NKW][KK];
+  load_regs(b);
 #pragma unroll
-  for (int w = 0; w < NKW; ++w) {
-    const int key = (wave + NW * w) * 16 + l16;
+  for (int w = 0; w < NKW; ++w)
 #pragma unroll
-    for (int kk = 0; kk < KK; ++kk) {
-      s16x8_t z = {0, 0, 0, 0, 0, 0, 0, 0};
-      vf[w][kk] = __builtin_bit_cast(bf16x8_t, z);
-      if (key < S) vf[w][kk] = ld8(Vg + (long)key * ts + 32 * kk + 8 * g);
-    }
-  }
-  for (int i = threadIdx.x; i < SP; i += NTH) {
-    delta_s[i] = 0.f;
-    lse_s[i] = i < S ? lse[((long)b * H + h) * S + i] * LOG2E : INFINITY;
+    for (int kk = 0; kk < KK; ++kk) vf[w][kk] = vfn[w][kk];
+  if (threadIdx.x < SP) {
+    delta_s[threadIdx.x] = 0.f;
+    lse_s[threadIdx.x] = lsen;
   }
   __syncthreads();
-  // staging: all global loads of the thread first (one latency), then LDS writes; delta = O . dO
-  constexpr int NIT = (SP * NCH + NTH - 1) / NTH;
-  uint4 qv[NIT], kv[NIT], dv[NIT], ov[NIT];
-#pragma unroll
-  for (int it = 0; it < NIT; ++it) {
-    const int i = it * NTH + threadIdx.x;
-    const int r = i / NCH, c = (i % NCH) * 8;
-    qv[it] = kv[it] = dv[it] = ov[it] = make_uint4(0, 0, 0, 0);
-    if (i < SP * NCH && r < S) {
-      qv[it] = *reinterpret_cast<const uint4*>(Qg + r * ts + c);
-      kv[it] = *reinterpret_cast<const uint4*>(Kg + r * ts + c);
-      dv[it] = *reinterpret_cast<const uint4*>(dOg + r * os + c);
-      ov[it] = *reinterpret_cast<const uint4*>(Og + r * os + c);
-    }
-  }
+  // LDS images from the registers; delta = O . dO
 #pragma unroll
   for (int it = 0; it < NIT; ++it) {
     const int i = it * NTH + threadIdx.x;
@@ -895,7 +968,7 @@ __global__ __launch_bounds__(256) void attn_bwd3_kernel(const uint16_t* __restri
                                                         const uint16_t* __restrict__ dO,
                                                         const float* __restrict__ lse,
                                                         uint16_t* __restrict__ dqkv, int S, int H, float scale,
-                                                        float* __restrict__ dbp) {
+                                                        float* __restrict__ dbp, int remap) {
   JM_DGUARD(S >= 1 && S <= SP && blockDim.x == 256);
   constexpr int NW = 4, NTH = 256, QC = 64;
   constexpr int NT = SP / 16, KK = HD / 32, DT = HD / 16;
@@ -910,7 +983,7 @@ __global__ __launch_bounds__(256) void attn_bwd3_kernel(const uint16_t* __restri
   float* delta_s = lse_s + SP;
   float* bsum = delta_s + SP;
 
-  const int bh = blockIdx.x;
+  const int bh = xcd_bid(remap);
   const int b = bh / H, h = bh - (bh / H) * H;
   const long ts = 3L * H * HD;
   const long os = (long)H * HD;
@@ -940,12 +1013,10 @@ __global__ __launch_bounds__(256) void attn_bwd3_kernel(const uint16_t* __restri
       if (key < S) vf[w][kk] = ld8(Vg + (long)key * ts + 32 * kk + 8 * g);
     }
   }
-  for (int i = threadIdx.x; i < 3 * HD; i += NTH) bsum[i] = 0.f;
-  for (int i = threadIdx.x; i < SP; i += NTH) {
-    delta_s[i] = 0.f;
-    lse_s[i] = i < S ? lse[((long)b * H + h) * S + i] * LOG2E : INFINITY;
-  }
-  __syncthreads();
+  // every global load in one burst (V fragments above, lse, the staging rows): one exposed round
+  // trip instead of two
+  static_assert(SP <= NTH, "one lse per thread");
+  const float lsev = (int)threadIdx.x < S ? lse[((long)b * H + h) * S + threadIdx.x] * LOG2E : INFINITY;
   constexpr int NIT = (SP * NCH + NTH - 1) / NTH;
   uint4 qv[NIT], kv[NIT], dv[NIT], ov[NIT];
 #pragma unroll
@@ -960,6 +1031,12 @@ __global__ __launch_bounds__(256) void attn_bwd3_kernel(const uint16_t* __restri
       ov[it] = *reinterpret_cast<const uint4*>(Og + r * os + c);
     }
   }
+  for (int i = threadIdx.x; i < 3 * HD; i += NTH) bsum[i] = 0.f;
+  if ((int)threadIdx.x < SP) {
+    delta_s[threadIdx.x] = 0.f;
+    lse_s[threadIdx.x] = lsev;
+  }
+  __syncthreads();
 #pragma unroll
   for (int it = 0; it < NIT; ++it) {
     const int i = it * NTH + threadIdx.x;
@@ -1175,6 +1252,9 @@ size_t bwd_smem() {
          (2 * SP + 3 * HD) * sizeof(float);
 }
 
+int g_attn_remap = 3;  // runtime switch: bit 0 XCD-aware workgroup -> (b, h) order (xcd_bid), bit 1 forward
+                       // Q prefetch + batched K / V staging; dec fwd 175 -> 163 us, bwd 361 -> 340 us
+                       // (profiles/r2_attn_remap.txt)
 int g_use_tr = 3;  // runtime switch: 3 = batched backward (bwd3) for hd 32, 2 = compact backward (bwd2) + TR
                    // forward, 1 = TR, 0 = transposed images
 
@@ -1191,7 +1271,7 @@ int run_t(bool fwd, const uint16_t* qkv, const uint16_t* o, const uint16_t* dO, 
     attr_set[fwd ? 0 : 1] = true;
   }
   if (fwd)
-    attn_fwd_kernel<HD, SP, TR><<<grid, 256, sm, st>>>(qkv, out, lse_out, S, H, scale);
+    attn_fwd_kernel<HD, SP, TR><<<grid, 256, sm, st>>>(qkv, out, lse_out, S, H, scale, g_attn_remap);
   else
     attn_bwd_kernel<HD, SP, TR><<<grid, 64 * bwd_waves<HD, SP>(), sm, st>>>(qkv, o, dO, lse_in, out, S, H, scale,
                                                                           lse_out);
@@ -1226,14 +1306,15 @@ int run_bwd2(const uint16_t* qkv, const uint16_t* o, const uint16_t* dO, const f
                                 (int)sm);
       attr3 = true;
     }
-    attn_bwd3_kernel<HD, SP><<<dim3(B * H), 256, sm, st>>>(qkv, o, dO, lse_in, out, S, H, scale, dbias_part);
+    attn_bwd3_kernel<HD, SP><<<dim3(B * H), 256, sm, st>>>(qkv, o, dO, lse_in, out, S, H, scale, dbias_part,
+                                                           g_attn_remap);
     return 0;
   }
 bwd2:
   {
     const int ppw = bwd_ppw<HD, SP>();
     attn_bwd2_kernel<HD, SP><<<dim3(((B + ppw - 1) / ppw) * H), 256, sm, st>>>(qkv, o, dO, lse_in, out, S, H, scale,
-                                                                              dbias_part, B, ppw);
+                                                                              dbias_part, B, ppw, g_attn_remap);
   }
   return 0;
 }
@@ -1255,7 +1336,7 @@ int run_fwd_ml(const uint16_t* qkv, uint16_t* out, float* lse_out, int B, int S,
   const int BH = B * H;
   const int hpw = g_fwd_hpw > 0 ? g_fwd_hpw : 4;
   const int grid = (BH + hpw - 1) / hpw;
-  attn_fwd_ml_kernel<HD, SP><<<grid, 256, sm, st>>>(qkv, out, lse_out, S, H, BH, hpw, scale);
+  attn_fwd_ml_kernel<HD, SP><<<grid, 256, sm, st>>>(qkv, out, lse_out, S, H, BH, hpw, scale, g_attn_remap);
   return 0;
 }
 
@@ -1643,6 +1724,7 @@ int run_long_bwd(const uint16_t* qkv, const uint16_t* o, const uint16_t* dO, con
 
 int jm_attn_max_seq() { return 224; }
 void jm_attn_set_tr(int v) { g_use_tr = v; }
+void jm_attn_set_remap(int v) { g_attn_remap = v; }
 void jm_attn_set_fwd_hpw(int v) { g_fwd_hpw = v < 0 ? 0 : v; }
 void jm_attn_set_bwd_ppw(int v) { g_bwd_ppw = v < 0 ? 0 : v; }
 

@@ -45,6 +45,7 @@ int jm_attn_bwd(const uint16_t* qkv, const uint16_t* o, const uint16_t* dO, cons
                 int S, int H, int hd, float* dbias_part, hipStream_t st);
 int jm_attn_max_seq();
 void jm_attn_set_tr(int v);
+void jm_attn_set_remap(int v);
 void jm_attn_set_fwd_hpw(int v);
 void jm_attn_set_bwd_ppw(int v);
 int jm_attn_bwd_part_rows(int B, int S, int hd);
@@ -841,6 +842,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_nt", &gemm_nt, py::arg("A"), py::arg("B"), py::arg("bias") = py::none(), py::arg("gelu") = false,
         py::arg("gelu_only") = false, py::arg("gelu_deriv") = false);
   m.def("attn_set_tr", &jm_attn_set_tr);
+  m.def("attn_set_remap", &jm_attn_set_remap, "attention grid: bit 0 XCD-aware (b, h) order, bit 1 forward Q prefetch");
   m.def("ln_set_bwd_la", &jm_ln_set_bwd_la);
   m.def("attn_set_fwd_hpw", &jm_attn_set_fwd_hpw);
   m.def("attn_set_bwd_ppw", &jm_attn_set_bwd_ppw);

@@ -25,8 +25,10 @@ def main():
     ap.add_argument("--tr", type=int, default=-1, help="kernel variant (ext.attn_set_tr), -1 = default")
     ap.add_argument("--hpw", type=int, default=0, help="forward (b, h) pairs per workgroup, 0 = default")
     ap.add_argument("--ppw", type=int, default=0, help="backward batch elements per workgroup (bwd2), 0 = default")
+    ap.add_argument("--remap", default="", help="comma list of attn_set_remap values to A/B (interleaved)")
     a = ap.parse_args()
     ext = _ext.load()
+    remaps = [int(v) for v in a.remap.split(",")] if a.remap else [None]
     if a.ppw > 0:
         ext.attn_set_bwd_ppw(a.ppw)
     if a.hpw > 0:
@@ -43,17 +45,26 @@ def main():
         fl_f = 4.0 * B * H * S * S * hd
         for label, fn, fl in (("fwd", lambda: ext.attn_fwd(qkv, H), fl_f),
                               ("bwd", lambda: ext.attn_bwd(do, qkv, o, lse, H, db), 2.5 * fl_f)):
+            res = {r: [] for r in remaps}
             for _ in range(3):
-                fn()
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            torch.cuda.synchronize()
-            e0.record()
-            for _ in range(a.iters):
-                fn()
-            e1.record()
-            torch.cuda.synchronize()
-            us = e0.elapsed_time(e1) * 1e3 / a.iters
-            print(f"{name} {label} B={B} S={S} H={H} hd={hd}: {us:8.1f} us  {fl / us / 1e6:7.1f} TF/s", flush=True)
+                for r in remaps:
+                    if r is not None:
+                        ext.attn_set_remap(r)
+                    for _ in range(3):
+                        fn()
+                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    torch.cuda.synchronize()
+                    e0.record()
+                    for _ in range(a.iters):
+                        fn()
+                    e1.record()
+                    torch.cuda.synchronize()
+                    res[r].append(e0.elapsed_time(e1) * 1e3 / a.iters)
+            for r in remaps:
+                us = min(res[r])
+                tag = "" if r is None else f" remap={r}"
+                print(f"{name} {label} B={B} S={S} H={H} hd={hd}{tag}: {us:8.1f} us  {fl / us / 1e6:7.1f} TF/s",
+                      flush=True)
 
 
 if __name__ == "__main__":
