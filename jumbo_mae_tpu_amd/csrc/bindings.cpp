@@ -71,6 +71,7 @@ int jm_gemm_nt(const uint16_t* A, long lda, const uint16_t* B, long ldb, int M, 
 void jm_gemm_set_variant(int wn, int group);
 void jm_gemm_set_tail(int on);
 void jm_gemm_set_sk(int on);
+void jm_gemm_set_pp(int on);
 int jm_gemm_nt_tail_plan(int M, int N, int K, int epi, int* tail_r, long* ws_floats);
 int jm_gemm_tn_plan(int M, int N, int K, int* S_out);
 int jm_gemm_tn(const uint16_t* A, long lda, const uint16_t* B, long ldb, int M, int N, int K, int sps, int S,
@@ -832,6 +833,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_tn_wgrad_seg", &gemm_tn_wgrad_seg);
   m.def("gemm_set_variant", &jm_gemm_set_variant, py::arg("wn"), py::arg("group") = 8);
   m.def("gemm_set_tail", &jm_gemm_set_tail);
+  m.def("gemm_set_pp", &jm_gemm_set_pp, "persistent overlapped NT launch for multi-round grids (1, default) or tiled (0)");
   m.def("gemm_set_sk", &jm_gemm_set_sk, "persistent DP + stream-K NT launches where they pay (1, default) or never (0)");
   m.def("gemm_tn_set_acc0", &jm_gemm_tn_set_acc0);
   m.def("gemm_tn_set_variant", &jm_gemm_tn_set_variant, "TN wgrad kernel: 4 = 4-phase (default), 0 = r1 32-row steps");

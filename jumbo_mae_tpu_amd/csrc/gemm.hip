@@ -675,7 +675,9 @@ __global__ __launch_bounds__(512, 1) void gemm_nt64_kernel(const uint16_t* __res
 // acc = A[m0:m0+256, k_begin:k_begin+K] . B[n0:n0+256, same]^T  (K % 128 == 0, K > 0); every LDS
 // slot is free on entry (caller's barrier) and the ring is drained on exit except for the reads
 // of the last K-tile's MFMAs (caller's epilogue barriers before reusing LDS).
-template <int SCHED, int NW = 8>
+// MODE 0: the whole K loop; 1: K-tile 0 was already issued (p4_mainloop<.., 2> of the same tile,
+// e.g. behind the previous tile's epilogue in the persistent kernel); 2: only issue K-tile 0.
+template <int SCHED, int NW = 8, int MODE = 0>
 __attribute__((always_inline)) JM_DEVICE void p4_mainloop(const uint16_t* __restrict__ A, long lda,
                                                           const uint16_t* __restrict__ B, long ldb, int M, int N,
                                                           int m0, int n0, int k_begin, int K,
@@ -745,10 +747,12 @@ __attribute__((always_inline)) JM_DEVICE void p4_mainloop(const uint16_t* __rest
       f[nt][1] = lds8(base + nt * 16 * BK2 + ch1);
     }
   };
+  if constexpr (MODE != 2) {
 #pragma unroll
-  for (int i = 0; i < 8; ++i)
+    for (int i = 0; i < 8; ++i)
 #pragma unroll
-    for (int j = 0; j < NTW; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+      for (int j = 0; j < NTW; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  }
   auto mfma_q = [&](auto mh, auto nh, const AF& a, const BF& b) {
     constexpr int MH = decltype(mh)::value, NH = decltype(nh)::value;
 #pragma unroll
@@ -849,10 +853,13 @@ __attribute__((always_inline)) JM_DEVICE void p4_mainloop(const uint16_t* __rest
   const int nk = K / BK2;  // even, >= 2
   // prologue: tiles 0 and 1 in the steady-state issue order (a0 b1 a1 | b0), so the counted
   // waits of the first tiles hold unchanged
-  issue(0, I0{});
-  issue(0, I3{});
-  issue(0, I1{});
-  issue(0, I2{});
+  if constexpr (MODE != 1) {
+    issue(0, I0{});
+    issue(0, I3{});
+    issue(0, I1{});
+    issue(0, I2{});
+  }
+  if constexpr (MODE == 2) return;
   issue(1, I0{});
   issue(1, I3{});
   issue(1, I1{});
@@ -1416,6 +1423,142 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_persist_kernel(const uint16_t*
   finish_tile(u + 2);
 }
 
+// ------------------------------------------------------------------ persistent, overlapped (p4)
+// One workgroup per CU walks tiles w, w + G, ... of the grouped order on the 4-phase main loop,
+// and hides each tile's start behind the previous tile's end: as soon as a tile's K loop is done
+// (set 0 of the LDS slots is free, its loads all landed) the NEXT tile's K-tile 0 is issued into
+// set 0, and only then the epilogue runs -- staged through set 1 (64 KB) in two 128-row halves
+// with inline-asm LDS accesses and the bias from an LDS copy (a compiler-visible LDS access or
+// global load would make hipcc drain the in-flight DMA with vmcnt(0)).  The next K loop then
+// starts with its first K-tile landed (MODE 1).  The epilogue's stores count in vmcnt and are
+// simply waited for by the first counted wait of the next tile.  Epilogues without aux input.
+template <int EPI>
+JM_DEVICE void epilogue_set1(const f32x4_t (&acc)[8][4], const GemmEpi& ep, const float* bias_lds, uint16_t* cs,
+                             int M, int N, int m0, int n0) {
+  constexpr int LPR = BN / 8, RPP = 512 / LPR;  // 32 lanes per 512-B row, 16 rows per sweep
+  int tid = threadIdx.x;
+  asm volatile("" : "+v"(tid));  // recomputed per tile, not hoisted out of the tile loop
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+  const int l16 = lane & 15, g = lane >> 4;
+  const int wr = wave >> 2, wc = wave & 3;
+  const int c = tid % LPR;
+  const bool col_ok = n0 + c * 8 < N;
+  const uint32_t csa = lds_addr(cs);
+  const uint32_t ba = bias_lds ? lds_addr(bias_lds) : 0u;
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {  // rows [128 p, 128 p + 128) = the accumulators of the waves with wr == p
+    if (wr == p) {
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) {
+        const int nl = wc * 64 + nt * 16 + 4 * g;
+        float bv[4] = {0.f, 0.f, 0.f, 0.f};
+        if (bias_lds) {
+          const uint4 r = ds_r128(ba + 4 * min(n0 + nl, N - 4));
+          wait_lgkm();
+          if (n0 + nl < N) {
+            bv[0] = __uint_as_float(r.x);
+            bv[1] = __uint_as_float(r.y);
+            bv[2] = __uint_as_float(r.z);
+            bv[3] = __uint_as_float(r.w);
+          }
+        }
+#pragma unroll
+        for (int mt = 0; mt < 8; ++mt) {
+          const int rl = mt * 16 + l16;
+          uint2 pk;
+          pk.x = pack_bf2(acc[mt][nt][0] + bv[0], acc[mt][nt][1] + bv[1]);
+          pk.y = pack_bf2(acc[mt][nt][2] + bv[2], acc[mt][nt][3] + bv[3]);
+          ds_w64(csa + 2 * (rl * BN + (((nl >> 3) ^ (rl & 15)) << 3) + (nl & 7)), pk);
+        }
+      }
+    }
+    bar_lds();
+    uint4 v[128 / RPP];
+#pragma unroll
+    for (int k = 0; k < 128 / RPP; ++k) {
+      const int rl = tid / LPR + k * RPP;
+      v[k] = ds_r128(csa + 2 * (rl * BN + ((c ^ (rl & 15)) << 3)));
+    }
+    wait_lgkm();
+#pragma unroll
+    for (int k = 0; k < 128 / RPP; ++k) {
+      const int m = m0 + p * 128 + tid / LPR + k * RPP;
+      if (m < M && col_ok) {
+        uint16_t* o = ep.out + (long)m * ep.ldo + n0 + c * 8;
+        const uint16_t* h = reinterpret_cast<const uint16_t*>(&v[k]);
+        if (EPI == EPI_STORE || EPI == EPI_GELU) st16(o, v[k], true);
+        if (EPI == EPI_GELU || EPI == EPI_GELU_ONLY) {
+          float f[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) f[j] = gelu_tanh_f(bf2f(h[j]));
+          st16(EPI == EPI_GELU ? ep.out2 + (long)m * ep.ldo + n0 + c * 8 : o, pack8(f), true);
+        }
+        if (EPI == EPI_GELU_D) {
+          float fg[8], fd[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) gelu_and_grad_f(bf2f(h[j]), fg[j], fd[j]);
+          st16(o, pack8(fd), true);
+          st16(ep.out2 + (long)m * ep.ldo + n0 + c * 8, pack8(fg), true);
+        }
+      }
+    }
+    bar_lds();
+  }
+}
+
+template <int EPI>
+__global__ __launch_bounds__(512, 1) void gemm_pp_kernel(const uint16_t* __restrict__ A, long lda,
+                                                         const uint16_t* __restrict__ B, long ldb, int M, int N,
+                                                         int K, GemmEpi ep, int GROUP_M) {
+  JM_DGUARD(blockDim.x == 512 && K % 128 == 0 && M > 0 && N > 0 && gridDim.x % 8 == 0);
+  extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
+  constexpr int SLOT = 128 * 64;
+  if (__builtin_amdgcn_readfirstlane(threadIdx.x) >= 256) __builtin_amdgcn_s_setprio(1);
+  const int G = gridDim.x;
+  const int tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
+  // round r covers tiles [r G, r G + R); each XCD label x (blockIdx % 8) takes a contiguous
+  // chunk of about R / 8 of them (neighbouring tiles share A / B panels through that XCD's L2)
+  // and a partial last round is spread over all eight XCDs, not packed onto the first few
+  const int xcd = blockIdx.x & 7, loc = blockIdx.x >> 3;
+  auto tile_of_round = [&](int r) {
+    const int R = min(G, tiles - r * G);
+    const int q = R >> 3, rem = R & 7;
+    if (loc >= q + (xcd < rem ? 1 : 0)) return -1;
+    return r * G + xcd * q + min(xcd, rem) + loc;
+  };
+  float* bias_lds = nullptr;
+  if (ep.bias) {  // whole bias behind the 8 slots, before any DMA is in flight
+    bias_lds = reinterpret_cast<float*>(smem + 8 * SLOT);
+    for (int i = threadIdx.x; i < N; i += 512) bias_lds[i] = ep.bias[i];
+    __syncthreads();
+  }
+  int r = 0;
+  int T = tile_of_round(0);
+  if (T < 0) return;  // workgroup-uniform (grid <= tiles on the host)
+  int m0, n0;
+  tile_coords(T, M, N, GROUP_M, m0, n0);
+  f32x4_t acc[8][4];
+  p4_mainloop<0, 8, 2>(A, lda, B, ldb, M, N, m0, n0, 0, K, acc, smem);
+  for (;;) {
+    p4_mainloop<0, 8, 1>(A, lda, B, ldb, M, N, m0, n0, 0, K, acc, smem);
+    const int T2 = r * G + G < tiles ? tile_of_round(r + 1) : -1;
+    const bool more = T2 >= 0;  // workgroup-uniform
+    int m1 = 0, n1 = 0;
+    // all waves are past their last reads of set 0 (the final K-tiles' barriers), so the next
+    // tile's K-tile 0 can stream in underneath this tile's epilogue
+    if (more) {
+      tile_coords(T2, M, N, GROUP_M, m1, n1);
+      p4_mainloop<0, 8, 2>(A, lda, B, ldb, M, N, m1, n1, 0, K, acc, smem);
+    }
+    // set 1 is free once every wave passed the last K-tile's q3 barrier (its reads were in q1 / q2)
+    epilogue_set1<EPI>(acc, ep, bias_lds, smem + 4 * SLOT, M, N, m0, n0);
+    if (!more) break;
+    ++r;
+    m0 = m1;
+    n0 = n1;
+  }
+}
+
 // ------------------------------------------------------------------ tail split finish
 // Sums the tail_S compact fp32 partials of the tail tiles and applies the launch's epilogue
 // (same rounding points as epilogue_lds).  Block = 32 rows of one tail tile; thread = 4 rows x 8
@@ -1635,9 +1778,29 @@ void launch_sk(const uint16_t* A, long lda, const uint16_t* B, long ldb, int M, 
   gemm_sk_kernel<EPI, SCHED><<<G, 512, sm, st>>>(A, lda, B, ldb, M, N, K, ep, g_gemm_group, pl);
 }
 
+int g_pp = 0;  // A/B: persistent overlapped launch (gemm_pp_kernel) for multi-round grids (jm_gemm_set_pp);
+               // off: within +-4 % of the tiled launch, slower on the GELU epilogue (profiles/r2_gemm_persistent.txt)
+
+template <int EPI>
+void launch_pp(const uint16_t* A, long lda, const uint16_t* B, long ldb, int M, int N, int K, const GemmEpi& ep,
+               int G, hipStream_t st) {
+  const size_t sm = jm_gemm_smem() + (ep.bias ? (size_t)N * sizeof(float) : 0);
+  static size_t attr = 0;
+  if (attr < sm) {
+    (void)hipFuncSetAttribute((const void*)gemm_pp_kernel<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
+    attr = sm;
+  }
+  gemm_pp_kernel<EPI><<<G, 512, sm, st>>>(A, lda, B, ldb, M, N, K, ep, g_gemm_group);
+}
+
 template <int EPI>
 void launch_p4(const uint16_t* A, long lda, const uint16_t* B, long ldb, int M, int N, int K, const GemmEpi& ep,
                int nwg, hipStream_t st) {
+  if constexpr (EPI == EPI_STORE || EPI == EPI_GELU || EPI == EPI_GELU_ONLY || EPI == EPI_GELU_D) {
+    const int G = num_cus() / 8 * 8;
+    if (g_pp && g_p4_sched == 4 && nwg > G && N % 8 == 0 && N <= 8192 && ep.t_count == 0)
+      return launch_pp<EPI>(A, lda, B, ldb, M, N, K, ep, G, st);
+  }
   if constexpr (EPI != EPI_PARTIAL && EPI != EPI_TAIL) {
     SkPlan pl;
     const int G = (g_p4_sched == 4 || g_p4_sched == 0) ? sk_plan(M, N, K, &pl) : 0;
@@ -1756,6 +1919,8 @@ void jm_gemm_set_variant(int wn, int group) {
 void jm_gemm_set_tail(int on) { g_gemm_tail = on; }
 
 void jm_gemm_set_sk(int on) { g_sk = on; }
+
+void jm_gemm_set_pp(int on) { g_pp = on; }
 
 // Tail split plan for an NT launch: the last wave of output tiles (tiles % CUs of them) fills only
 // part of the chip; when it is at most a quarter wave, those tiles run split-K S ways (compact fp32

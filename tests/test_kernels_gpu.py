@@ -526,3 +526,25 @@ def test_gemm_nt_stream_k(ext, kind, M, N, K):
         assert rel(outs[1][0], ref + b) < 1e-2
     if kind == "dmul":
         assert rel(outs[1][0], (ref.bfloat16().float() * aux.float())) < 1e-2
+
+
+@pytest.mark.parametrize("kind", ["store", "gelu", "gelu_only", "gelu_d"])
+@pytest.mark.parametrize("M,N,K", [(16100, 2048, 256), (9000, 1000, 512), (70000, 512, 128), (26624, 1024, 1024)])
+def test_gemm_nt_persistent_overlapped(ext, kind, M, N, K):
+    """Persistent launch (next tile's first K-tile streamed in under the epilogue, epilogue through
+    half the LDS with a bias copy in LDS) == the tiled launch, bit for bit: same main loop, same
+    rounding points; ragged M / N, several tiles per workgroup."""
+    torch.manual_seed(7)
+    A = (torch.rand(M, K, device="cuda") * 2 - 1).bfloat16()
+    W = ((torch.rand(N, K, device="cuda") * 2 - 1) * 0.05).bfloat16()
+    b = torch.randn(N, device="cuda") * 0.1
+    outs = []
+    for pp in (0, 1):
+        ext.gemm_set_pp(pp)
+        outs.append(tuple(ext.gemm_nt(A, W, b, kind != "store", kind == "gelu_only", kind == "gelu_d")))
+        outs.append(tuple(ext.gemm_nt(A, W, None, kind != "store", kind == "gelu_only", kind == "gelu_d")))
+    ext.gemm_set_pp(0)
+    for o0, o1 in zip(outs[0] + outs[1], outs[2] + outs[3]):
+        assert torch.equal(o0, o1)
+    if kind == "store":
+        assert rel(outs[2][0], A.float() @ W.float().t() + b) < 1e-2

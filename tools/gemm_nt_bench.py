@@ -52,9 +52,10 @@ def main():
     # "d" = persistent whole tiles on the fewest CUs that keep the round count (gemm_set_sk 1 / 2)
     variants = a.variant.split(",")
 
-    def setv(v):
-        ext.gemm_set_sk({"s": 1, "d": 2}.get(v[-1], 0))
-        ext.gemm_set_variant(int(v.rstrip("sd")), a.group)
+    def setv(v):  # suffixes: s / d = persistent stream-K / fewer-CU whole tiles, p = persistent overlapped
+        ext.gemm_set_sk(2 if "d" in v else 1 if "s" in v else 0)
+        ext.gemm_set_pp(1 if "p" in v else 0)
+        ext.gemm_set_variant(int(v.rstrip("sdp")), a.group)
 
     setv(variants[0])
     names = [n for n in FWD if not a.only or n in a.only.split(",")]

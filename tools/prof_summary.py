@@ -6,7 +6,7 @@ cat = {}
 for r in rows:
     n = r["Name"]; t = float(r["TotalDurationNs"]) / 1e6 / steps
     if n.startswith("Cijk") or n.startswith("Custom_Cijk"): k = "GEMM(hipBLASLt)"
-    elif "gemm_nt" in n or "gemm_tn" in n or "gemm_persist" in n: k = "GEMM (ours, MFMA)"
+    elif "gemm_" in n: k = "GEMM (ours, MFMA)"
     elif "attn" in n: k = "attention"
     elif any(x in n for x in ("patch", "unshuffle", "embed_finish")): k = "mae glue (ours)"
     elif "ln_" in n: k = "layernorm"
