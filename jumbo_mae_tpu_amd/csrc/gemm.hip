@@ -906,7 +906,7 @@ __attribute__((always_inline)) JM_DEVICE void p4_epilogue(const f32x4_t (&acc)[8
     epilogue<EPI, NTW>(acc, ep, M, N, m0 + wr * 128, n0 + wc * NTW * 16, l16, g);
 }
 
-// SCHED bit 64: 4 waves (2 x 2, 128 x 128 each, one wave per SIMD) instead of 8
+// SCHED bit 64: 4 waves (2 x 2, 128 x 128 each, one wave per SIMD) instead of 8.
 template <int EPI, int SCHED>
 __global__ __launch_bounds__((SCHED & 64) ? 256 : 512, 1) void gemm_p4_kernel(const uint16_t* __restrict__ A, long lda,
                                                                              const uint16_t* __restrict__ B, long ldb,
