@@ -90,7 +90,8 @@ def _enh_level(lvl):
 
 
 def _enh_inc_level(lvl):
-    return max(0.0, 1.0 + _neg(lvl / _MAX * 0.9))
+    # "no change" is 1.0; range [0.1, 1.9] for levels <= 10, floored at 0.1 above that
+    return max(0.1, 1.0 + _neg(lvl / _MAX * 0.9))
 
 
 def color(img, lvl, hp):
@@ -228,21 +229,45 @@ def rand_augment_transform(spec: str, hparams: dict) -> RandAugment:
 
 
 class AugMix:
+    """AugMix (Hendrycks et al. 2020) as timm composes it: ``width`` chains of ``depth`` (or 1-3)
+    ops mixed with Dirichlet(alpha) weights, then blended with the original by m ~ Beta(alpha,
+    alpha).  ``blended`` mode instead alpha-blends each chain into the running image with weights
+    rescaled so the final composite has the same mixing proportions."""
+
     def __init__(self, ops, alpha=1.0, width=3, depth=-1, blended=False):
         self.ops, self.alpha, self.width, self.depth, self.blended = ops, alpha, width, depth, blended
 
+    def _chain(self, img):
+        d = self.depth if self.depth > 0 else random.randint(1, 3)
+        for op in random.choices(self.ops, k=d):
+            img = op(img)
+        return img
+
+    @staticmethod
+    def blended_weights(ws, m):
+        """Per-step blend alphas a_k (applied last-to-first) such that sequential
+        ``img = (1-a_k) img + a_k chain_k`` leaves weight m*w_k on chain k."""
+        ws = np.asarray(ws, np.float64) * m
+        rest, out = 1.0, []
+        for w in ws[::-1]:
+            a = w / rest
+            rest *= 1.0 - a
+            out.append(a)
+        return np.asarray(out[::-1], np.float32)
+
     def __call__(self, img):
         ws = np.random.dirichlet([self.alpha] * self.width).astype(np.float32)
-        m = np.float32(np.random.beta(self.alpha, self.alpha))
+        m = float(np.float32(np.random.beta(self.alpha, self.alpha)))
+        if self.blended:
+            orig = img
+            for a in self.blended_weights(ws, m):
+                img = Image.blend(img, self._chain(orig), float(a))
+            return img
         mixed = np.zeros(np.asarray(img).shape, dtype=np.float32)
         for w in ws:
-            d = self.depth if self.depth > 0 else random.randint(1, 3)
-            aug = img
-            for op in random.choices(self.ops, k=d):
-                aug = op(aug)
-            mixed += w * np.asarray(aug, dtype=np.float32)
-        out = (1 - m) * np.asarray(img, dtype=np.float32) + m * mixed
-        return Image.fromarray(np.clip(out, 0, 255).astype(np.uint8))
+            mixed += w * np.asarray(self._chain(img), dtype=np.float32)
+        mixed = Image.fromarray(np.clip(mixed, 0, 255).astype(np.uint8))
+        return Image.blend(img, mixed, m)
 
 
 def augmix_transform(spec: str, hparams: dict) -> AugMix:
@@ -291,6 +316,34 @@ POLICY_ORIGINAL = [
 ]
 
 
+# ImageNet "v0" policy of the EfficientNet TPU reference implementation (timm ``v0``)
+POLICY_V0 = [
+    [("Equalize", 0.8, 1), ("ShearY", 0.8, 4)], [("Color", 0.4, 9), ("Equalize", 0.6, 3)],
+    [("Color", 0.4, 1), ("Rotate", 0.6, 8)], [("Solarize", 0.8, 3), ("Equalize", 0.4, 7)],
+    [("Solarize", 0.4, 2), ("Solarize", 0.6, 2)], [("Color", 0.2, 0), ("Equalize", 0.8, 8)],
+    [("Equalize", 0.4, 8), ("SolarizeAdd", 0.8, 3)], [("ShearX", 0.2, 9), ("Rotate", 0.6, 8)],
+    [("Color", 0.6, 1), ("Equalize", 1.0, 2)], [("Invert", 0.4, 9), ("Rotate", 0.6, 0)],
+    [("Equalize", 1.0, 9), ("ShearY", 0.6, 3)], [("Color", 0.4, 7), ("Equalize", 0.6, 0)],
+    [("Posterize", 0.4, 6), ("AutoContrast", 0.4, 7)], [("Solarize", 0.6, 8), ("Color", 0.6, 9)],
+    [("Solarize", 0.2, 4), ("Rotate", 0.8, 9)], [("Rotate", 1.0, 7), ("TranslateYRel", 0.8, 9)],
+    [("ShearX", 0.0, 0), ("Solarize", 0.8, 4)], [("ShearY", 0.8, 0), ("Color", 0.6, 4)],
+    [("Color", 1.0, 0), ("Rotate", 0.6, 2)], [("Equalize", 0.8, 4), ("Equalize", 0.0, 8)],
+    [("Equalize", 1.0, 4), ("AutoContrast", 0.6, 2)], [("ShearY", 0.4, 7), ("SolarizeAdd", 0.6, 7)],
+    [("Posterize", 0.8, 2), ("Solarize", 0.6, 10)], [("Solarize", 0.6, 8), ("Equalize", 0.6, 1)],
+    [("Color", 0.8, 6), ("Rotate", 0.4, 5)],
+]
+
+
+def _r_variant(policy):
+    """The ``...r`` policies: Posterize replaced by the increasing-severity PosterizeIncreasing."""
+    sub = {"Posterize": "PosterizeIncreasing", "PosterizeOriginal": "PosterizeIncreasing"}
+    return [[(sub.get(n, n), p, m) for n, p, m in sp] for sp in policy]
+
+
+POLICIES = {"original": POLICY_ORIGINAL, "originalr": _r_variant(POLICY_ORIGINAL),
+            "v0": POLICY_V0, "v0r": _r_variant(POLICY_V0)}
+
+
 class AutoAugment:
     def __init__(self, policy):
         self.policy = policy
@@ -307,7 +360,6 @@ def auto_augment_transform(spec: str, hparams: dict) -> AutoAugment:
     for a in args:
         if a.startswith("mstd"):
             hp["magnitude_std"] = float(a[4:])
-    if name not in ("original", "originalr", "v0", "v0r"):
+    if name not in POLICIES:
         raise ValueError(f"unknown AutoAugment policy {spec}")
-    policy = [[AugmentOp(n, p, m, hp) for n, p, m in sp] for sp in POLICY_ORIGINAL]
-    return AutoAugment(policy)
+    return AutoAugment([[AugmentOp(n, p, m, hp) for n, p, m in sp] for sp in POLICIES[name]])

@@ -113,7 +113,8 @@ class ShardDataset(IterableDataset):
             mine = urls
             sample_filter = (self.rank * nw + wid, total)
         handler = S.ignore_and_continue if self.train else None
-        it = S.iter_samples(mine, handler)
+        # validation shards are cached locally on the first pass (webdataset cached_tarfile_to_samples)
+        it = S.iter_samples(mine, handler) if self.train else S.cached_samples(mine, handler)
         if sample_filter is not None:
             it = itertools.islice(it, sample_filter[0], None, sample_filter[1])
         if self.train:

@@ -54,13 +54,105 @@ def shard_list(spec: str | list[str]) -> list[str]:
     return urls
 
 
+class PipeStream(io.RawIOBase):
+    """stdout of a ``pipe:`` command; ``close`` reaps the command and raises ``IOError`` when it
+    failed, so a truncated download is an error rather than a silently short shard.  A command
+    killed by SIGPIPE because the reader stopped early is not an error."""
+
+    def __init__(self, cmd: str):
+        self.cmd = cmd
+        self.proc = subprocess.Popen(cmd, shell=True, stdout=subprocess.PIPE)
+        self._eof = False
+
+    def readable(self):
+        return True
+
+    def readinto(self, b):
+        n = self.proc.stdout.readinto(b)
+        if not n:
+            self._eof = True
+        return n
+
+    def close(self):
+        if self.closed:
+            return
+        self.proc.stdout.close()
+        rc = self.proc.wait()
+        super().close()
+        if rc != 0 and not (not self._eof and rc in (-13, 141)):
+            raise IOError(f"pipe command failed with exit status {rc}: {self.cmd}")
+
+
 def open_stream(url: str):
     if url.startswith("pipe:"):
-        p = subprocess.Popen(url[5:], shell=True, stdout=subprocess.PIPE)
-        return p.stdout
+        return io.BufferedReader(PipeStream(url[5:]), 1 << 20)
     if url.startswith("file://"):
         url = url[7:]
     return open(url, "rb")
+
+
+def cache_dir() -> str:
+    """Shard cache directory: ``$WDS_CACHE`` or ``./_cache`` (webdataset's defaults)."""
+    return os.environ.get("WDS_CACHE", "./_cache")
+
+
+def cache_name(url: str) -> str:
+    """File name of a cached shard: the basename of the last word of the URL (the object a
+    ``pipe:gsutil cat gs://bucket/val-0003.tar`` command streams) behind a short hash of the whole
+    URL, so equal basenames from different buckets do not collide."""
+    import hashlib
+
+    target = url[5:].split()[-1] if url.startswith("pipe:") else url
+    base = re.sub(r"[^\w.\-]", "_", target.rstrip("/").rsplit("/", 1)[-1]) or "shard"
+    return hashlib.sha1(url.encode()).hexdigest()[:10] + "-" + base
+
+
+def cached_path(url: str, directory: str | None = None) -> str:
+    """Local path of ``url``, streaming a remote/``pipe:`` shard into the cache once.
+
+    Equivalent of webdataset's ``cached_tarfile_to_samples`` download step used by the reference
+    validation pipeline (/root/reference/src/dataset.py:139-150): the first pass over the
+    validation set streams each shard to ``<cache>/<name>`` (written to a temporary file and
+    renamed into place, so a concurrent worker or an interrupted download never leaves a partial
+    shard under the final name; the command's exit status is checked), later passes read the
+    local copy.  Local files are read in place."""
+    local = _local_path(url)
+    if local is not None:
+        return local
+    directory = directory or cache_dir()
+    os.makedirs(directory, exist_ok=True)
+    dest = os.path.join(directory, cache_name(url))
+    if os.path.exists(dest):
+        return dest
+    tmp = f"{dest}.{os.getpid()}.tmp"
+    try:
+        with open_stream(url) as src, open(tmp, "wb") as out:
+            while True:
+                buf = src.read(1 << 22)
+                if not buf:
+                    break
+                out.write(buf)
+        os.replace(tmp, dest)
+    finally:
+        if os.path.exists(tmp):
+            os.unlink(tmp)
+    return dest
+
+
+def cached_samples(urls: list[str], handler=None, directory: str | None = None) -> Iterator[dict]:
+    """``iter_samples`` over the cached copies of ``urls``; each shard is fetched when the stream
+    reaches it (a failed fetch goes to ``handler`` like a read error)."""
+    for u in urls:
+        try:
+            p = cached_path(u, directory)
+        except Exception as e:
+            if handler is None:
+                raise
+            handler(e)
+            continue
+        for smp in iter_samples([p], handler):
+            smp["__url__"] = u
+            yield smp
 
 
 def _split_key(name: str) -> tuple[str, str]:

@@ -143,9 +143,21 @@ class PILToArray:
         return np.ascontiguousarray(np.asarray(img.convert("RGB"), dtype=np.uint8).transpose(2, 0, 1))
 
 
+def erase_fill(noise: np.ndarray) -> np.ndarray:
+    """float noise -> uint8 the way ``uint8_tensor[...] = float_tensor`` stores it (truncate, wrap)."""
+    return (np.trunc(noise).astype(np.int64) & 255).astype(np.uint8)
+
+
 class RandomErasing:
-    """torchvision RandomErasing(p, scale=(0.02, 0.33), ratio=(0.3, 3.3), value="random") on a
-    uint8 CHW array (random values are uniform uint8)."""
+    """torchvision v2 RandomErasing(p, scale=(0.02, 0.33), ratio=(0.3, 3.3), value="random") on a
+    uint8 CHW array (/root/reference/src/dataset.py:74).
+
+    ``value="random"`` in torchvision v2 draws the patch as float32 standard-normal noise and
+    assigns it into the uint8 image, i.e. each value is truncated toward zero and wrapped modulo
+    256 (-1.3 -> 255, 0.9 -> 0, 2.2 -> 2): the erased patch is near-black with a sprinkle of
+    near-white pixels.  That effective fill is reproduced here (``erase_fill``).  torchvision is
+    not installed in this image, so the match is pinned to torch's own float->uint8 assignment in
+    tests/test_data.py, not to torchvision itself (parity unpinned at the library level)."""
 
     def __init__(self, p=0.5, scale=(0.02, 0.33), ratio=(0.3, 3.3)):
         self.p, self.scale, self.ratio = p, scale, ratio
@@ -165,7 +177,7 @@ class RandomErasing:
                 i = random.randint(0, h - eh)
                 j = random.randint(0, w - ew)
                 a = a.copy()
-                a[:, i:i + eh, j:j + ew] = np.random.randint(0, 256, (c, eh, ew), dtype=np.uint8)
+                a[:, i:i + eh, j:j + ew] = erase_fill(np.random.standard_normal((c, eh, ew)).astype(np.float32))
                 return a
         return a
 

@@ -95,22 +95,24 @@ def masking_ids(noise: torch.Tensor, keep_len: int):
     ids_shuffle = torch.argsort(noise, dim=-1)
     ids_restore = torch.argsort(ids_shuffle, dim=-1)
     ids_keep = ids_shuffle[..., :keep_len]
-    length = noise.shape[-1]
     base = torch.ones(noise.shape, device=noise.device, dtype=torch.float32)
     base[..., :keep_len] = 0.0
     if noise.dim() == 1:
         mask = base[ids_restore]
     else:
         mask = torch.gather(base, -1, ids_restore)
-    del length
     return ids_shuffle, ids_restore, ids_keep, mask
 
 
 def random_masking(x: torch.Tensor, generator: torch.Generator | None, keep_len: int,
-                   mode: str = "shared", noise: torch.Tensor | None = None):
+                   mode: str = "shared", noise: torch.Tensor | None = None,
+                   padding_mask: torch.Tensor | None = None):
     """Returns (kept, mask[B,N], ids_restore) like utils_mae.py:88-102.
 
     ``mode="shared"`` (reference semantics): one noise vector per call/rank.
+    With ``padding_mask`` ([B,N], 1 = real token) the kept rows of it are
+    returned as a 4th element, matching the reference's optional
+    ``padding_mask`` argument (src/utils_mae.py:88-102).
     """
     b, n, _ = x.shape
     if noise is None:
@@ -121,4 +123,6 @@ def random_masking(x: torch.Tensor, generator: torch.Generator | None, keep_len:
     kept = index_sequence(x, ids_keep)
     if mask.dim() == 1:
         mask = mask.unsqueeze(0).expand(b, n)
+    if padding_mask is not None:
+        return kept, mask, ids_restore, index_sequence(padding_mask, ids_keep)
     return kept, mask, ids_restore

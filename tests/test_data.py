@@ -120,3 +120,162 @@ def test_loader_synthetic_workers():
     assert x.shape == (8, 3, 32, 32) and x.dtype == torch.uint8 and y.shape == (8,)
     batches = list(vl)
     assert sum(int((b[1] != -1).sum()) for b in batches) == 10
+
+
+# ---- RandAugment op fixtures: level -> argument values of timm's level mappings, applied through
+# PIL directly and compared with our op (sign and resample draws pinned).
+def _pinned(monkeypatch, negate):
+    import jumbo_mae_tpu_amd.data.autoaugment as A
+    monkeypatch.setattr(A.random, "random", lambda: 0.9 if negate else 0.1)
+    monkeypatch.setattr(A.random, "choice", lambda seq: seq[0])
+    return A
+
+
+def _img(seed=0, size=(48, 40)):
+    return Image.fromarray(np.random.RandomState(seed).randint(0, 256, (size[1], size[0], 3), np.uint8))
+
+
+@pytest.mark.parametrize("negate", [False, True])
+def test_randaugment_geometric_fixtures(monkeypatch, negate):
+    from PIL import Image as I
+    A = _pinned(monkeypatch, negate)
+    img, hp, sgn = _img(), {"translate_const": 100, "img_mean": (1, 2, 3)}, -1 if negate else 1
+    bil = I.BILINEAR
+    cases = {  # (op, level): expected PIL call; arguments are the timm formula values at level 9
+        "Rotate": lambda: img.rotate(27.0 * sgn, resample=bil, fillcolor=(1, 2, 3)),
+        "ShearX": lambda: img.transform(img.size, I.AFFINE, (1, 0.27 * sgn, 0, 0, 1, 0), resample=bil,
+                                        fillcolor=(1, 2, 3)),
+        "ShearY": lambda: img.transform(img.size, I.AFFINE, (1, 0, 0, 0.27 * sgn, 1, 0), resample=bil,
+                                        fillcolor=(1, 2, 3)),
+        "TranslateX": lambda: img.transform(img.size, I.AFFINE, (1, 0, 90.0 * sgn, 0, 1, 0), resample=bil,
+                                            fillcolor=(1, 2, 3)),
+        "TranslateYRel": lambda: img.transform(img.size, I.AFFINE, (1, 0, 0, 0, 1, 0.405 * 40 * sgn),
+                                               resample=bil, fillcolor=(1, 2, 3)),
+    }
+    for name, ref in cases.items():
+        out = A.NAME_TO_OP[name](img, 9.0, hp)
+        assert np.array_equal(np.asarray(out), np.asarray(ref())), name
+
+
+def test_randaugment_pixel_fixtures(monkeypatch):
+    from PIL import ImageEnhance, ImageOps
+    A = _pinned(monkeypatch, negate=True)
+    img, a = _img(1), np.asarray(_img(1)).astype(np.int32)
+    expect = {
+        "Posterize": ImageOps.posterize(img, 3), "PosterizeIncreasing": ImageOps.posterize(img, 1),
+        "PosterizeOriginal": ImageOps.posterize(img, 7),
+        "Solarize": ImageOps.solarize(img, 230), "SolarizeIncreasing": ImageOps.solarize(img, 26),
+        "SolarizeAdd": Image.fromarray(np.where(a < 128, np.minimum(a + 99, 255), a).astype(np.uint8)),
+        "Color": ImageEnhance.Color(img).enhance(1.72), "Contrast": ImageEnhance.Contrast(img).enhance(1.72),
+        "Brightness": ImageEnhance.Brightness(img).enhance(1.72),
+        "Sharpness": ImageEnhance.Sharpness(img).enhance(1.72),
+        "ColorIncreasing": ImageEnhance.Color(img).enhance(1.0 - 0.81),
+        "BrightnessIncreasing": ImageEnhance.Brightness(img).enhance(1.0 - 0.81),
+        "AutoContrast": ImageOps.autocontrast(img), "Equalize": ImageOps.equalize(img),
+        "Invert": ImageOps.invert(img),
+    }
+    for name, ref in expect.items():
+        out = A.NAME_TO_OP[name](img, 9.0, {})
+        assert np.array_equal(np.asarray(out), np.asarray(ref)), name
+    # posterize at >= 8 bits is the identity; enhance-increasing is floored at 0.1 beyond level 10
+    assert A.NAME_TO_OP["PosterizeOriginal"](img, 10.0, {}) is img
+    assert A._enh_inc_level(20.0) == pytest.approx(0.1)
+
+
+def test_augment_magnitude_noise(monkeypatch):
+    from jumbo_mae_tpu_amd.data.autoaugment import AugmentOp
+    seen = []
+    op = AugmentOp("Rotate", prob=1.0, magnitude=9, hparams={"magnitude_std": 0.5, "magnitude_max": 10})
+    op.fn = lambda img, m, hp: seen.append(m) or img
+    import random as R
+    R.seed(0)
+    for _ in range(200):
+        op(None)
+    assert all(0.0 <= m <= 10.0 for m in seen) and abs(np.mean(seen) - 9.0) < 0.2
+    op.mstd = float("inf")  # uniform in [0, m]
+    seen.clear()
+    for _ in range(200):
+        op(None)
+    assert 0.0 <= min(seen) and max(seen) <= 9.0 and abs(np.mean(seen) - 4.5) < 0.6
+
+
+def test_augmix_blended_weights():
+    from jumbo_mae_tpu_amd.data.autoaugment import AugMix
+    ws, m = np.array([0.2, 0.5, 0.3]), 0.6
+    a = AugMix.blended_weights(ws, m)
+    # sequential blends img = (1 - a_k) img + a_k chain_k leave weight m*w_k on chain k
+    eff, orig = [], 1.0
+    for k in range(3):
+        eff.append(a[k] * np.prod([1 - a[j] for j in range(k + 1, 3)]))
+        orig *= 1 - a[k]
+    np.testing.assert_allclose(eff, m * ws, rtol=1e-5)
+    assert orig == pytest.approx(1 - m, rel=1e-5)
+
+
+@pytest.mark.parametrize("spec", ["augmix-m3-w3-d2-b1", "v0", "v0r", "originalr"])
+def test_augment_variants_run(spec):
+    img = _img(2, (32, 32))
+    t = augmix_transform(spec, {}) if spec.startswith("augmix") else auto_augment_transform(spec, {})
+    for _ in range(4):
+        assert t(img).size == (32, 32)
+    if spec == "v0r":
+        names = {op.name for sp in t.policy for op in sp}
+        assert "PosterizeIncreasing" in names and "Posterize" not in names
+
+
+def test_random_erasing_fill_matches_uint8_assignment():
+    from jumbo_mae_tpu_amd.data.transforms import RandomErasing, erase_fill
+    v = np.random.RandomState(0).standard_normal((3, 8, 8)).astype(np.float32)
+    t = torch.zeros(3, 8, 8, dtype=torch.uint8)
+    t[:] = torch.from_numpy(v)  # what torchvision v2 erase does with value="random"
+    assert np.array_equal(erase_fill(v), t.numpy())
+    a = np.full((3, 32, 32), 77, np.uint8)
+    out = RandomErasing(p=1.0)(a)
+    changed = out != 77
+    assert changed.any() and set(np.unique(out[changed])) <= set(range(0, 6)) | set(range(250, 256))
+
+
+# ---- validation shard cache (webdataset cached_tarfile_to_samples)
+def test_cached_path_pipe(tmp_path):
+    src = tmp_path / "val-0001.tar"
+    _make_tar(str(src), 3)
+    cache = tmp_path / "cache"
+    url = f"pipe:cat {src}"
+    p = S.cached_path(url, str(cache))
+    assert p.startswith(str(cache)) and p.endswith("val-0001.tar")
+    assert open(p, "rb").read() == src.read_bytes()
+    src.unlink()  # the second pass reads the cached copy only
+    assert S.cached_path(url, str(cache)) == p
+    assert [s["__url__"] for s in S.cached_samples([url], directory=str(cache))] == [url] * 3
+    assert S.cached_path(str(tmp_path / "x.tar"), str(cache)) == str(tmp_path / "x.tar")  # local: in place
+
+
+def test_cached_path_failed_pipe(tmp_path):
+    cache = tmp_path / "cache"
+    with pytest.raises(IOError):
+        S.cached_path(f"pipe:cat {tmp_path}/missing.tar", str(cache))
+    assert list(cache.iterdir()) == []  # no partial shard left behind
+    got = []
+    assert list(S.cached_samples([f"pipe:cat {tmp_path}/missing.tar"], handler=got.append,
+                                 directory=str(cache))) == []
+    assert len(got) == 1
+
+
+def test_pipe_exit_status_checked(tmp_path):
+    src = tmp_path / "s.tar"
+    _make_tar(str(src), 2)
+    assert len(list(S.tar_samples(f"pipe:cat {src}"))) == 2
+    with pytest.raises(IOError):
+        list(S.tar_samples(f"pipe:cat {src}; exit 3"))
+
+
+def test_valid_dataset_uses_cache(tmp_path, monkeypatch):
+    for k in range(2):
+        _make_tar(str(tmp_path / f"v-{k}.tar"), 4, start=k * 4)
+    monkeypatch.setenv("WDS_CACHE", str(tmp_path / "wc"))
+    _, va = create_transforms("none", 16, "none", 0.0, 0.0, 1.0)
+    spec = f"pipe:cat {tmp_path}/v-{{0..1}}.tar"
+    ds = ShardDataset(spec, "finetune", va, train=False, image_size=16)
+    assert len(list(ds)) == 8
+    assert len(list((tmp_path / "wc").iterdir())) == 2
+    assert len(list(ds)) == 8  # second pass from the cache

@@ -21,6 +21,21 @@ def test_masking_invariants_shared():
     assert torch.equal(m[0], m[3])
 
 
+def test_masking_padding_mask():
+    noise = torch.rand(16)
+    x = torch.randn(2, 16, 3)
+    pad = (torch.arange(16) < 11).float().expand(2, 16).clone()
+    pad[1, 5:] = 0
+    kept, m, restore, pad_kept = U.random_masking(x, None, 4, noise=noise, padding_mask=pad)
+    ids = torch.argsort(noise)[:4]
+    assert torch.equal(pad_kept, pad[:, ids]) and torch.equal(kept, x[:, ids])
+    # per-sample ids gather per row
+    noise2 = torch.rand(2, 16)
+    *_, pad_kept2 = U.random_masking(x, None, 4, mode="per-sample", noise=noise2, padding_mask=pad)
+    for b in range(2):
+        assert torch.equal(pad_kept2[b], pad[b, torch.argsort(noise2[b])[:4]])
+
+
 def test_masking_per_sample():
     noise = torch.rand(3, 16)
     x = torch.randn(3, 16, 2)
