@@ -67,8 +67,74 @@ JM_DEVICE int xcd_bid(int remap) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
 }
 
+// ---------------------------------------------------------------- forward softmax (fast form)
+// The forward is VALU-bound (PMC: ~80 % of SIMD cycles in VALU at S = 199, hd = 32, ~10 VALU
+// instructions per score), so per score it now issues only an fma (scale and max subtraction in
+// one), the exp2, half a max3 and half a bf16 pack:
+//  * padded keys are masked through the QK^T accumulator init (-1e30 for keys >= S, only in the
+//    key tiles that straddle S) instead of a compare + select per score;
+//  * the max is taken over raw scores and the scale folded into the exp2 argument;
+//  * the row sum comes out of the MFMA: an all-ones A operand next to V^T sums the same bf16 P
+//    the P.V product uses (7 extra MFMAs per query tile instead of one add per score);
+//  * query tiles past S (fully padded) are skipped.
+// remap bit 2 selects the previous per-score form (A/B switch).
+JM_DEVICE f32x4_t key_init(int kt, int g, int S) {
+  f32x4_t a = {0.f, 0.f, 0.f, 0.f};
+  if (kt * 16 + 16 > S) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) a[i] = kt * 16 + 4 * g + i < S ? 0.f : -1e30f;
+  }
+  return a;
+}
+
+JM_DEVICE bf16x8_t bf16_ones() {
+  s16x8_t s;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) s[j] = (short)0x3F80;
+  return __builtin_bit_cast(bf16x8_t, s);
+}
+
+// sc: raw S^T tiles (key on the lane group) of one query tile, NTv of them real; va(s, dt): the
+// V^T A operand of key pair s, d tile dt.  Returns O^T (unnormalised), ms = scaled row max (log2
+// domain) and l = row sum of the bf16 P.
+template <int NT, int DT, class VA>
+JM_DEVICE void softmax_pv(const f32x4_t (&sc)[NT], float sl2, VA&& va, f32x4_t (&oacc)[DT], float& ms, float& l) {
+  float m = -INFINITY;
+#pragma unroll
+  for (int kt = 0; kt < NT; ++kt) m = fmaxf(fmaxf(m, fmaxf(sc[kt][0], sc[kt][1])), fmaxf(sc[kt][2], sc[kt][3]));
+  m = fmaxf(m, __shfl_xor(m, 16, WAVE));
+  m = fmaxf(m, __shfl_xor(m, 32, WAVE));
+  ms = m * sl2;
+  const bf16x8_t ones = bf16_ones();
+  f32x4_t lacc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt) oacc[dt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int s = 0; s < NT / 2; ++s) {
+    float pf[8];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      pf[i] = __builtin_amdgcn_exp2f(fmaf(sc[2 * s][i], sl2, -ms));
+      pf[4 + i] = __builtin_amdgcn_exp2f(fmaf(sc[2 * s + 1][i], sl2, -ms));
+    }
+    const bf16x8_t pb = pack8(pf);
+    lacc = mfma(ones, pb, lacc);
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) oacc[dt] = mfma(va(s, dt), pb, oacc[dt]);
+  }
+  l = lacc[0];
+}
+
+// QK^T tile init: keys >= S get -1e30 (P = 0).  EX (S > SP - 32): only the last two key tiles
+// can hold padded keys, so every other tile starts from zero with no per-score work.
+template <int NT, bool EX>
+JM_DEVICE f32x4_t qk_init(int kt, int g, int S) {
+  if (EX && kt < NT - 2) return f32x4_t{0.f, 0.f, 0.f, 0.f};
+  return key_init(kt, g, S);
+}
+
 // --------------------------------------------------------------------------------- forward
-template <int HD, int SP, bool TR>
+template <int HD, int SP, bool TR, bool EX = false>
 __global__ __launch_bounds__(256) void attn_fwd_kernel(const uint16_t* __restrict__ qkv, uint16_t* __restrict__ o,
                                                        float* __restrict__ lse, int S, int H, float scale,
                                                        int remap) {
@@ -151,6 +217,59 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const uint16_t* __restric
   __syncthreads();
 
   const float sl2 = scale * LOG2E;
+
+  if (!(remap & 4)) {
+    const int NTv = (S + 15) >> 4;
+#pragma unroll
+    for (int it = 0; it < NQW; ++it) {
+      const int qt = wave + 4 * it;
+      if (qt >= NTv) break;
+      const int q = qt * 16 + l16;
+      bf16x8_t qf[KK];
+#pragma unroll
+      for (int kk = 0; kk < KK; ++kk) {
+        if (qp) {
+          qf[kk] = qpre[it][kk];
+        } else if (q < S) {
+          qf[kk] = ld8(Qg + (long)q * ts + 32 * kk + 8 * g);
+        } else {
+          s16x8_t z = {0, 0, 0, 0, 0, 0, 0, 0};
+          qf[kk] = __builtin_bit_cast(bf16x8_t, z);
+        }
+      }
+      f32x4_t sc[NT];
+#pragma unroll
+      for (int kt = 0; kt < NT; ++kt) {
+        f32x4_t acc = qk_init<NT, EX>(kt, g, S);
+#pragma unroll
+        for (int kk = 0; kk < KK; ++kk) acc = mfma(ld8(Ks + (kt * 16 + l16) * KS + 32 * kk + 8 * g), qf[kk], acc);
+        sc[kt] = acc;
+      }
+      f32x4_t oacc[DT];
+      float ms, l;
+      softmax_pv(sc, sl2,
+                 [&](int s, int dt) {
+                   if (TR) {
+                     const uint16_t* vr = Vt + (32 * s + 4 * g + (l16 >> 2)) * KS + dt * 16 + 4 * (l16 & 3);
+                     return cat44(tr4(vr), tr4(vr + 16 * KS));
+                   }
+                   const uint16_t* vr = Vt + (dt * 16 + l16) * VS + 32 * s + 4 * g;
+                   return cat44(ld4(vr), ld4(vr + 16));
+                 },
+                 oacc, ms, l);
+      if (q < S) {
+        const float inv = 1.f / l;
+        uint16_t* orow = o + ((long)b * S + q) * H * HD + h * HD;
+#pragma unroll
+        for (int dt = 0; dt < DT; ++dt) {
+          float v[4] = {oacc[dt][0] * inv, oacc[dt][1] * inv, oacc[dt][2] * inv, oacc[dt][3] * inv};
+          store4(orow + dt * 16 + 4 * g, v);
+        }
+        if (g == 0) lse[((long)b * H + h) * S + q] = (ms + log2f(l)) * LN2;
+      }
+    }
+    return;
+  }
 
 #pragma unroll
   for (int it = 0; it < NQW; ++it) {
@@ -245,7 +364,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const uint16_t* __restric
 // the current pair's images are in LDS, so their HBM latency hides behind the current pair's
 // MFMA / softmax work (the one-pair kernel stalls on every load phase); Q fragments of the next
 // query tile are prefetched the same way.
-template <int HD, int SP>
+template <int HD, int SP, bool EX = false>
 __global__ __launch_bounds__(256) void attn_fwd_ml_kernel(const uint16_t* __restrict__ qkv, uint16_t* __restrict__ o,
                                                           float* __restrict__ lse, int S, int H, int BH, int hpw,
                                                           float scale, int remap) {
@@ -324,6 +443,34 @@ __global__ __launch_bounds__(256) void attn_fwd_ml_kernel(const uint16_t* __rest
       for (int kk = 0; kk < KK; ++kk) qf[kk] = qn[kk];
       if (qt + 4 < NT) load_q(Qg, qt + 4, qn);
       f32x4_t sc[NT];
+      if (!(remap & 4)) {
+#pragma unroll
+        for (int kt = 0; kt < NT; ++kt) {
+          f32x4_t acc = qk_init<NT, EX>(kt, g, S);
+#pragma unroll
+          for (int kk = 0; kk < KK; ++kk) acc = mfma(ld8(Ks + (kt * 16 + l16) * KS + 32 * kk + 8 * g), qf[kk], acc);
+          sc[kt] = acc;
+        }
+        f32x4_t oacc[DT];
+        float ms, l;
+        softmax_pv(sc, sl2,
+                   [&](int s, int dt) {
+                     const uint16_t* vr2 = Vt + (32 * s + 4 * g + (l16 >> 2)) * KS + dt * 16 + 4 * (l16 & 3);
+                     return cat44(tr4(vr2), tr4(vr2 + 16 * KS));
+                   },
+                   oacc, ms, l);
+        if (q < S) {
+          const float inv = 1.f / l;
+          uint16_t* orow = o + ((long)b * S + q) * H * HD + h * HD;
+#pragma unroll
+          for (int dt = 0; dt < DT; ++dt) {
+            float v[4] = {oacc[dt][0] * inv, oacc[dt][1] * inv, oacc[dt][2] * inv, oacc[dt][3] * inv};
+            store4(orow + dt * 16 + 4 * g, v);
+          }
+          if (g == 0) lse[((long)b * H + h) * S + q] = (ms + log2f(l)) * LN2;
+        }
+        continue;
+      }
 #pragma unroll
       for (int kt = 0; kt < NT; ++kt) {
         f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
@@ -1270,7 +1417,15 @@ int run_t(bool fwd, const uint16_t* qkv, const uint16_t* o, const uint16_t* dO, 
     hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
     attr_set[fwd ? 0 : 1] = true;
   }
-  if (fwd)
+  if (fwd && S > SP - 32) {
+    static bool attr_ex = false;
+    if (sm > 64 * 1024 && !attr_ex) {
+      (void)hipFuncSetAttribute((const void*)attn_fwd_kernel<HD, SP, TR, true>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
+      attr_ex = true;
+    }
+    attn_fwd_kernel<HD, SP, TR, true><<<grid, 256, sm, st>>>(qkv, out, lse_out, S, H, scale, g_attn_remap);
+  } else if (fwd)
     attn_fwd_kernel<HD, SP, TR><<<grid, 256, sm, st>>>(qkv, out, lse_out, S, H, scale, g_attn_remap);
   else
     attn_bwd_kernel<HD, SP, TR><<<grid, 64 * bwd_waves<HD, SP>(), sm, st>>>(qkv, o, dO, lse_in, out, S, H, scale,
@@ -1327,16 +1482,20 @@ int g_fwd_hpw = 0;
 template <int HD, int SP>
 int run_fwd_ml(const uint16_t* qkv, uint16_t* out, float* lse_out, int B, int S, int H, float scale, hipStream_t st) {
   const size_t sm = fwd_smem<HD, SP, true>();
-  static bool attr_set = false;
-  if (sm > 64 * 1024 && !attr_set) {
-    (void)hipFuncSetAttribute((const void*)attn_fwd_ml_kernel<HD, SP>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)sm);
-    attr_set = true;
+  static bool attr_set[2] = {false, false};
+  const bool ex = S > SP - 32;
+  const void* fn = ex ? (const void*)attn_fwd_ml_kernel<HD, SP, true> : (const void*)attn_fwd_ml_kernel<HD, SP>;
+  if (sm > 64 * 1024 && !attr_set[ex]) {
+    (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
+    attr_set[ex] = true;
   }
   const int BH = B * H;
   const int hpw = g_fwd_hpw > 0 ? g_fwd_hpw : 4;
   const int grid = (BH + hpw - 1) / hpw;
-  attn_fwd_ml_kernel<HD, SP><<<grid, 256, sm, st>>>(qkv, out, lse_out, S, H, BH, hpw, scale, g_attn_remap);
+  if (ex)
+    attn_fwd_ml_kernel<HD, SP, true><<<grid, 256, sm, st>>>(qkv, out, lse_out, S, H, BH, hpw, scale, g_attn_remap);
+  else
+    attn_fwd_ml_kernel<HD, SP><<<grid, 256, sm, st>>>(qkv, out, lse_out, S, H, BH, hpw, scale, g_attn_remap);
   return 0;
 }
 

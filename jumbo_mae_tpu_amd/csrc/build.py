@@ -99,6 +99,13 @@ def build_io(verbose: bool = True) -> Path:
     return out
 
 
+# per-file code-generation flags.  attention.hip: MFMA results in arch VGPRs instead of AGPRs --
+# the attention kernels run VALU work (softmax) on every accumulator, and with the default AGPR
+# form each score costs a v_accvgpr_read plus a larger register footprint (forward S=199, hd=32:
+# 160 VGPR + 56 AGPR -> 109 VGPR, one occupancy step up; backward 296 -> 217).
+FILE_FLAGS = {"attention.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form"]}
+
+
 def build(jobs: int = 8, verbose: bool = True, clean: bool = False, variant: str = "release") -> Path:
     if clean and BUILD.exists():
         shutil.rmtree(BUILD)
@@ -129,9 +136,10 @@ def build(jobs: int = 8, verbose: bool = True, clean: bool = False, variant: str
         src = HERE / k
         if not src.exists():
             continue
-        dig = _digest([src] + hdrs, kflags)
+        fl = kflags + FILE_FLAGS.get(k, [])
+        dig = _digest([src] + hdrs, fl)
         obj = BUILD / f"{src.stem}.{dig}.o"
-        jobs_list.append((obj, [HIPCC] + kflags + ["-c", str(src), "-o", str(obj)]))
+        jobs_list.append((obj, [HIPCC] + fl + ["-c", str(src), "-o", str(obj)]))
     bsrc = HERE / "bindings.cpp"
     dig = _digest([bsrc], cflags)
     bobj = BUILD / f"bindings.{dig}.o"
