@@ -101,7 +101,10 @@ template <int NT, int DT, class VA>
 JM_DEVICE void softmax_pv(const f32x4_t (&sc)[NT], float sl2, VA&& va, f32x4_t (&oacc)[DT], float& ms, float& l) {
   float m = -INFINITY;
 #pragma unroll
-  for (int kt = 0; kt < NT; ++kt) m = fmaxf(fmaxf(m, fmaxf(sc[kt][0], sc[kt][1])), fmaxf(sc[kt][2], sc[kt][3]));
+  for (int kt = 0; kt < NT; ++kt) {  // two v_max3 per tile
+    m = fmaxf(fmaxf(m, sc[kt][0]), sc[kt][1]);
+    m = fmaxf(fmaxf(m, sc[kt][2]), sc[kt][3]);
+  }
   m = fmaxf(m, __shfl_xor(m, 16, WAVE));
   m = fmaxf(m, __shfl_xor(m, 32, WAVE));
   ms = m * sl2;

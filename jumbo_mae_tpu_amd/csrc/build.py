@@ -103,7 +103,9 @@ def build_io(verbose: bool = True) -> Path:
 # the attention kernels run VALU work (softmax) on every accumulator, and with the default AGPR
 # form each score costs a v_accvgpr_read plus a larger register footprint (forward S=199, hd=32:
 # 160 VGPR + 56 AGPR -> 109 VGPR, one occupancy step up; backward 296 -> 217).
-FILE_FLAGS = {"attention.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form"]}
+# -fno-honor-nans: fmaxf without the NaN-quieting v_max_f32 x, x on each MFMA result (the softmax
+# max is then one v_max3 per two scores).
+FILE_FLAGS = {"attention.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form", "-fno-honor-nans"]}
 
 
 def build(jobs: int = 8, verbose: bool = True, clean: bool = False, variant: str = "release") -> Path:
