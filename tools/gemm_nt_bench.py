@@ -63,7 +63,7 @@ def main():
     for kind in a.kinds.split(","):
         for name in names:
             M, N, K = FWD[name]
-            if kind == "fwd_gelu" and name not in ("enc_ff1", "dec_ff1", "jumbo1", "b_ff1"):
+            if kind.startswith("fwd_gelu") and name not in ("enc_ff1", "dec_ff1", "jumbo1", "b_ff1"):
                 continue
             if kind == "dgrad_gelu" and name not in ("enc_ff2", "dec_ff2", "b_ff2"):
                 continue
@@ -91,6 +91,12 @@ def main():
                 wm = w.t().contiguous()  # W as the model stores it: [N_fwd, K_fwd] = w^T
                 ours = lambda: ext.gemm_nt(x, w, None, False)  # noqa: E731
                 blas = lambda: x @ wm  # noqa: E731
+            elif kind == "fwd_gelu_only":  # one output, gelu(h): the GELU VALU without the second store
+                ours = lambda: ext.gemm_nt(x, w, b, True, True)  # noqa: E731
+                blas = lambda: torch.nn.functional.gelu(torch.addmm(bb, x, w.t()), approximate="tanh")  # noqa: E731
+            elif kind == "fwd_gelu_d":  # two outputs, gelu'(h) and gelu(h) (the training forward)
+                ours = lambda: ext.gemm_nt(x, w, b, True, False, True)  # noqa: E731
+                blas = lambda: torch.nn.functional.gelu(torch.addmm(bb, x, w.t()), approximate="tanh")  # noqa: E731
             elif gelu:
                 ours = lambda: ext.gemm_nt(x, w, b, True)  # noqa: E731
                 blas = lambda: torch.nn.functional.gelu(torch.addmm(bb, x, w.t()), approximate="tanh")  # noqa: E731
@@ -102,10 +108,20 @@ def main():
                 setv(v)
                 o = ours()
                 r0 = torch.addmm(b, x.float(), w.float().t()) if kind != "dgrad_gelu" else o[0].float()
+                if kind == "fwd_gelu_only":
+                    r0 = torch.nn.functional.gelu(r0.bfloat16().float(), approximate="tanh")
+                elif kind == "fwd_gelu_d":
+                    r0 = torch.nn.functional.gelu(r0.bfloat16().float(), approximate="tanh")
+                    o = o[1:]
                 errs.append(((o[0].float() - r0).abs().max() / r0.abs().max()).item())
             setv(variants[0])
             out = ours()
             ref = torch.addmm(b, x.float(), w.float().t()) if kind != "dgrad_gelu" else out[0].float()
+            if kind == "fwd_gelu_only":
+                ref = torch.nn.functional.gelu(ref.bfloat16().float(), approximate="tanh")
+            elif kind == "fwd_gelu_d":
+                ref = torch.nn.functional.gelu(ref.bfloat16().float(), approximate="tanh")
+                out = out[1:]
             err = ((out[0].float() - ref).abs().max() / ref.abs().max()).item()
             if gelu:
                 g_ref = torch.nn.functional.gelu(out[0].float(), approximate="tanh")
