@@ -1438,6 +1438,14 @@ int run_t(bool fwd, const uint16_t* qkv, const uint16_t* o, const uint16_t* dO, 
 
 // runtime switch: batch elements per bwd2 workgroup (one head each); 0 = auto (bwd_ppw)
 int g_bwd_ppw = 0;
+// runtime switch: the batched backward (bwd3) also for head dim 64 at S > 64 (finetune S = 199)
+int g_bwd3_hd64 = 1;  // finetune S=199 hd=64 backward 249 -> 177 us (profiles/r2_attn_ft_bwd.txt)
+// the backward that jm_attn_bwd runs is the batched bwd3 kernel (B dbias partial rows) -- the
+// single source of that choice for run_bwd2 and jm_attn_bwd_part_rows
+bool uses_bwd3(int S, int hd) {
+  return g_use_tr == 3 && (hd == 32 || (hd == 64 && S > 64 && g_bwd3_hd64));
+}
+
 
 template <int HD, int SP>
 int bwd_ppw() {
@@ -1456,8 +1464,8 @@ int run_bwd2(const uint16_t* qkv, const uint16_t* o, const uint16_t* dO, const f
                               (int)sm);
     attr_set = true;
   }
-  if constexpr (HD == 32) {
-    if (g_use_tr != 3) goto bwd2;
+  if constexpr (HD == 32 || (HD == 64 && SP > 64)) {
+    if (!uses_bwd3(S, HD)) goto bwd2;
     static bool attr3 = false;
     if (sm > 64 * 1024 && !attr3) {
       (void)hipFuncSetAttribute((const void*)attn_bwd3_kernel<HD, SP>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -1884,16 +1892,22 @@ int run_long_bwd(const uint16_t* qkv, const uint16_t* o, const uint16_t* dO, con
 
 }  // namespace
 
-int jm_attn_max_seq() { return 224; }
+// longest sequence on the whole-sequence-in-LDS kernels (runtime switch; the tile-streamed
+// kernels take longer ones)
+int g_attn_max_seq = 224;
+int jm_attn_max_seq() { return g_attn_max_seq; }
+void jm_attn_set_max_seq(int v) { g_attn_max_seq = v < 32 ? 32 : (v > 224 ? 224 : v); }
 void jm_attn_set_tr(int v) { g_use_tr = v; }
 void jm_attn_set_remap(int v) { g_attn_remap = v; }
 void jm_attn_set_fwd_hpw(int v) { g_fwd_hpw = v < 0 ? 0 : v; }
 void jm_attn_set_bwd_ppw(int v) { g_bwd_ppw = v < 0 ? 0 : v; }
+void jm_attn_set_bwd3_hd64(int v) { g_bwd3_hd64 = v; }
 
 // rows of the dbias_part workspace that jm_attn_bwd writes: the bwd2 kernel folds ``ppw`` batch
-// elements into one row, every other backward writes one row per batch element
+// elements into one row, every other backward writes one row per batch element.  Must mirror the
+// kernel choice of run_bwd2 exactly (bwd3 writes B rows).
 int jm_attn_bwd_part_rows(int B, int S, int hd) {
-  const bool bwd2 = g_use_tr >= 2 && !(hd == 32 && g_use_tr == 3);
+  const bool bwd2 = g_use_tr >= 2 && !uses_bwd3(S, hd);
   if (!bwd2 || S > 224 || (hd != 32 && hd != 64)) return B;
   int ppw;
   if (hd == 64)

@@ -44,10 +44,12 @@ int jm_attn_fwd(const uint16_t* qkv, uint16_t* o, float* lse, int B, int S, int 
 int jm_attn_bwd(const uint16_t* qkv, const uint16_t* o, const uint16_t* dO, const float* lse, uint16_t* dqkv, int B,
                 int S, int H, int hd, float* dbias_part, hipStream_t st);
 int jm_attn_max_seq();
+void jm_attn_set_max_seq(int v);
 void jm_attn_set_tr(int v);
 void jm_attn_set_remap(int v);
 void jm_attn_set_fwd_hpw(int v);
 void jm_attn_set_bwd_ppw(int v);
+void jm_attn_set_bwd3_hd64(int v);
 int jm_attn_bwd_part_rows(int B, int S, int hd);
 int jm_attn_bwd_long(const uint16_t* qkv, const uint16_t* o, const uint16_t* dO, const float* lse, uint16_t* dqkv,
                      float* delta, int B, int S, int H, int hd, hipStream_t st);
@@ -829,6 +831,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("attn_bwd", &attn_bwd, py::arg("dO"), py::arg("qkv"), py::arg("o"), py::arg("lse"), py::arg("heads"),
         py::arg("dbias") = py::none());
   m.def("attn_max_seq", &jm_attn_max_seq);
+  m.def("attn_set_max_seq", &jm_attn_set_max_seq);
   m.def("gemm_tn_wgrad", &gemm_tn_wgrad);
   m.def("gemm_tn_wgrad_seg", &gemm_tn_wgrad_seg);
   m.def("gemm_set_variant", &jm_gemm_set_variant, py::arg("wn"), py::arg("group") = 8);
@@ -848,6 +851,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("ln_set_bwd_la", &jm_ln_set_bwd_la);
   m.def("attn_set_fwd_hpw", &jm_attn_set_fwd_hpw);
   m.def("attn_set_bwd_ppw", &jm_attn_set_bwd_ppw);
+  m.def("attn_set_bwd3_hd64", &jm_attn_set_bwd3_hd64);
   m.def("opt_sumsq", &opt_sumsq);
   m.def("opt_adamw", &opt_adamw);
   m.def("opt_lamb_phase1", &opt_lamb_phase1);

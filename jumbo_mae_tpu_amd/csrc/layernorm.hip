@@ -340,6 +340,145 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const TI* __restrict__ dy, 
   }
 }
 
+// ln_bwd_kernel<..., ER> with a one-row software pipeline: the x / dy / dres (/ y) loads of the
+// wave's NEXT row are issued before the current row's reduction, math and stores, so every wave
+// keeps a row of loads in flight while it computes (the kernel is HBM-bound at 2 waves / SIMD:
+// ~190 VGPRs, most of them the per-column parameter partials).
+template <int V, typename TI, bool RES>
+__global__ __launch_bounds__(256) void ln_bwd_pf_kernel(const TI* __restrict__ dy, const float* __restrict__ x,
+                                                        long sB, long sT, int T, int rows, int D,
+                                                        const float* __restrict__ mean, const float* __restrict__ rstd,
+                                                        const float* __restrict__ gamma, LnBwdIO io, LnResIO rio,
+                                                        float* __restrict__ ws, int accum_params) {
+  JM_DGUARD(blockDim.x == 256 && D % 4 == 0 && D <= V * 256);
+  constexpr int NP = RES ? 4 : 2;
+  extern __shared__ __attribute__((aligned(16))) float red[];  // [NP*D]
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const bool partials = accum_params || RES;
+  float acc[NP][V][4], gg[V][4], sc[V][4];
+#pragma unroll
+  for (int i = 0; i < V; ++i) {
+    const int col = (i * 64 + lane) * 4;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+#pragma unroll
+      for (int k = 0; k < NP; ++k) acc[k][i][j] = 0.f;
+      sc[i][j] = 1.f;
+    }
+    if (col < D) {
+      load4(gamma + col, gg[i]);
+      if (RES && rio.scale) load4(rio.scale + col, sc[i]);
+    }
+  }
+  const bool use_y = RES && rio.scale;
+  float xv[V][4], dv[V][4], rv[V][4], yv[V][4];
+  auto load_row = [&](int row) {
+    const int b = row / T, t = row - b * T;
+    const float* xr = x + b * sB + t * sT;
+    const TI* dyr = dy + (long)row * D;
+    const float* rr = io.dres ? io.dres + b * io.rB + t * io.rT : nullptr;
+    const bool rrow = RES && t >= rio.T0;
+    const long yoff = RES ? b * rio.yB + (long)(t - rio.T0) * rio.yT : 0;
+#pragma unroll
+    for (int i = 0; i < V; ++i) {
+      const int col = (i * 64 + lane) * 4;
+      if (col < D) {
+        load4(xr + col, xv[i]);
+        load4(dyr + col, dv[i]);
+        if (use_y && rrow) load4(rio.y + yoff + col, yv[i]);
+        if (rr) load4(rr + col, rv[i]);
+        else rv[i][0] = rv[i][1] = rv[i][2] = rv[i][3] = 0.f;
+      }
+    }
+  };
+  int row = blockIdx.x * 4 + wave;
+  const int step = gridDim.x * 4;
+  if (row < rows) load_row(row);
+  for (; row < rows; row += step) {
+    const int b = row / T, t = row - b * T;
+    const float mu = mean[row], rs = rstd[row];
+    const bool rrow = RES && t >= rio.T0;
+    const long yoff = RES ? b * rio.yB + (long)(t - rio.T0) * rio.yT : 0;
+    float xh[V][4], g[V][4], r[V][4], y[V][4];
+    float sg = 0.f, sgx = 0.f;
+#pragma unroll
+    for (int i = 0; i < V; ++i) {
+      const int col = (i * 64 + lane) * 4;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        r[i][j] = rv[i][j];
+        y[i][j] = yv[i][j];
+      }
+      if (col < D) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          xh[i][j] = (xv[i][j] - mu) * rs;
+          g[i][j] = dv[i][j] * gg[i][j];
+          sg += g[i][j];
+          sgx += g[i][j] * xh[i][j];
+          acc[0][i][j] += dv[i][j] * xh[i][j];
+          acc[1][i][j] += dv[i][j];
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) xh[i][j] = g[i][j] = 0.f;
+      }
+    }
+    // the next row's loads fly while this row reduces, computes and stores
+    if (row + step < rows) load_row(row + step);
+    sg = wave_sum(sg) / D;
+    sgx = wave_sum(sgx) / D;
+    float* dxr = io.dx + b * io.oB + t * io.oT;
+    const float m = (RES && rio.mask) ? rio.mask[b] : 1.f;
+#pragma unroll
+    for (int i = 0; i < V; ++i) {
+      const int col = (i * 64 + lane) * 4;
+      if (col < D) {
+        float o[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) o[j] = rs * (g[i][j] - sg - xh[i][j] * sgx) + r[i][j];
+        store4(dxr + col, o);
+        if (RES && rrow) {
+          float d[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const float md = m * o[j];
+            d[j] = md * sc[i][j];
+            if (use_y) acc[2 % NP][i][j] += md * y[i][j];
+            acc[3 % NP][i][j] += bf2f(f2bf(d[j]));  // colsum of the bf16 values the GEMMs consume
+          }
+          store4(rio.dy + yoff + col, d);
+        }
+      }
+    }
+  }
+  if (!partials) return;
+  for (int w = 0; w < 4; ++w) {
+    if (wave == w) {
+#pragma unroll
+      for (int i = 0; i < V; ++i) {
+        const int col = (i * 64 + lane) * 4;
+        if (col < D) {
+#pragma unroll
+          for (int k = 0; k < NP; ++k) {
+            float a[4] = {0.f, 0.f, 0.f, 0.f};
+            if (w > 0) load4(red + k * D + col, a);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) a[j] += acc[k][i][j];
+            store4(red + k * D + col, a);
+          }
+        }
+      }
+    }
+    __syncthreads();
+  }
+  for (int i = threadIdx.x * 4; i < NP * D; i += 256 * 4) {
+    float a[4];
+    load4(red + i, a);
+    store4(ws + (long)blockIdx.x * NP * D + i, a);
+  }
+}
+
 // out_k[c] += sum_b ws[b][k*D + c] for the NP partial vectors (null outputs skipped); grid.y
 // splits the partial rows.
 struct ParamOuts {
@@ -533,7 +672,8 @@ bool use_wide(int rows, int D) { return D > 1024 && rows <= LN_WIDE_MAX_ROWS && 
 // runtime switch (A/B): 0 = register partials, dres loaded after the row reduction; 1 = LDS-accumulated
 // parameter partials + early dres load (the ds_add_f32 accumulation made the ViT-L step 97.8 ->
 // 122.2 ms despite the doubled occupancy, profiles/r1_ab_ln_bwd_lds_acc.txt); 2 (default) = register
-// partials + early dres load: 97.96 -> 97.75 ms/step (profiles/r1_ab_ln_bwd_early_dres.txt)
+// partials + early dres load: 97.96 -> 97.75 ms/step (profiles/r1_ab_ln_bwd_early_dres.txt);
+// 3 = 2 + the next row's loads issued before this row's math (ln_bwd_pf_kernel)
 int g_ln_bwd_la = 2;
 
 template <typename TI, bool RES>
@@ -545,6 +685,9 @@ void launch_bwd(int V, dim3 grid, size_t smem, hipStream_t st, const TI* dy, con
     if (g_ln_bwd_la == 1 && VV >= 2 && VV <= 4)                                                             \
       ln_bwd_kernel<VV, TI, RES, true><<<grid, 256, smem, st>>>(dy, x, sB, sT, T, rows, D, m, r, g, dx, rio, ws, \
                                                                  acc);                                     \
+    else if (g_ln_bwd_la == 3 && VV >= 2 && VV <= 4)                                                        \
+      ln_bwd_pf_kernel<VV, TI, RES><<<grid, 256, smem, st>>>(dy, x, sB, sT, T, rows, D, m, r, g, dx, rio, ws,   \
+                                                             acc);                                          \
     else if (g_ln_bwd_la == 2 && VV >= 2 && VV <= 4)                                                        \
       ln_bwd_kernel<VV, TI, RES, false, true><<<grid, 256, smem, st>>>(dy, x, sB, sT, T, rows, D, m, r, g, dx, \
                                                                         rio, ws, acc);                      \

@@ -31,7 +31,7 @@ def rel(a, b):
 
 @pytest.mark.parametrize("D", [32, 512, 768, 1024, 2304, 3072])
 @pytest.mark.parametrize("out_dtype", [torch.bfloat16, torch.float32])
-@pytest.mark.parametrize("la", [2, 1, 0])
+@pytest.mark.parametrize("la", [3, 2, 1, 0])
 def test_layernorm(ext, D, out_dtype, la):
     ext.ln_set_bwd_la(la)
     torch.manual_seed(0)
@@ -358,7 +358,7 @@ def test_gemm_nt_splitk(ext, M, N, K, S, variant):
 
 @pytest.mark.parametrize("T0,view_y,with_scale", [(0, False, True), (3, False, True), (0, True, True),
                                                   (3, True, False)])
-@pytest.mark.parametrize("la", [2, 1, 0])
+@pytest.mark.parametrize("la", [3, 2, 1, 0])
 def test_layernorm_bwd_fused_residual(ext, T0, view_y, with_scale, la):
     ext.ln_set_bwd_la(la)
     """LN backward with the consumer's residual backward fused in == layernorm_bwd followed by

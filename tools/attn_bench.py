@@ -15,7 +15,7 @@ sys.path.insert(0, os.environ.get("JMAE_ROOT") or os.path.dirname(os.path.dirnam
 
 from jumbo_mae_tpu_amd.ops import _ext  # noqa: E402
 
-SHAPES = {"dec": (512, 199, 16, 32), "enc": (512, 52, 16, 64), "ft": (128, 199, 16, 64)}
+SHAPES = {"dec": (512, 199, 16, 32), "enc": (512, 52, 16, 64), "ft": (128, 199, 16, 64), "ft12": (128, 199, 12, 64)}
 
 
 def main():
@@ -26,6 +26,8 @@ def main():
     ap.add_argument("--hpw", type=int, default=0, help="forward (b, h) pairs per workgroup, 0 = default")
     ap.add_argument("--ppw", type=int, default=0, help="backward batch elements per workgroup (bwd2), 0 = default")
     ap.add_argument("--remap", default="", help="comma list of attn_set_remap values to A/B (interleaved)")
+    ap.add_argument("--max-seq", type=int, default=0, help="attn_set_max_seq (longer S -> tile-streamed kernels)")
+    ap.add_argument("--bwd3-hd64", type=int, default=-1, help="attn_set_bwd3_hd64 (batched backward at hd 64)")
     a = ap.parse_args()
     ext = _ext.load()
     remaps = [int(v) for v in a.remap.split(",")] if a.remap else [None]
@@ -35,12 +37,16 @@ def main():
         ext.attn_set_fwd_hpw(a.hpw)
     if a.tr >= 0:
         ext.attn_set_tr(a.tr)
+    if a.max_seq > 0:
+        ext.attn_set_max_seq(a.max_seq)
+    if a.bwd3_hd64 >= 0:
+        ext.attn_set_bwd3_hd64(a.bwd3_hd64)
     for name in a.shapes.split(","):
         B, S, H, hd = SHAPES[name]
         D = H * hd
         qkv = (torch.randn(B, S, 3 * D, device="cuda") * 1.5).bfloat16()
         do = torch.randn(B, S, D, device="cuda").bfloat16()
-        db = torch.zeros(3 * D, device="cuda")
+        db = torch.zeros(3 * D, device="cuda") if S <= ext.attn_max_seq() else None
         o, lse = ext.attn_fwd(qkv, H)
         fl_f = 4.0 * B * H * S * S * hd
         for label, fn, fl in (("fwd", lambda: ext.attn_fwd(qkv, H), fl_f),

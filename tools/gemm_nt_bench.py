@@ -22,6 +22,8 @@ FWD = {
     # ViT-B/16 encoder (D = 768, J = 2304)
     "b_qkv": (26624, 2304, 768), "b_wo": (26624, 768, 768), "b_ff1": (25088, 3072, 768),
     "b_ff2": (25088, 768, 3072), "b_jumbo1": (512, 9216, 2304), "b_jumbo2": (512, 2304, 9216),
+    # ViT-B/16 finetune (128 images x 199 tokens; the FF runs on the 196 patch rows = b_ff1/b_ff2)
+    "ft_qkv": (25472, 2304, 768), "ft_wo": (25472, 768, 768),
 }
 
 
