@@ -919,7 +919,12 @@ __global__ __launch_bounds__((SCHED & 64) ? 256 : 512, 1) void gemm_p4_kernel(co
     if (__builtin_amdgcn_readfirstlane(threadIdx.x) >= 256) __builtin_amdgcn_s_setprio(1);
   }
   int m0, n0, split = 0;
-  tile_of(M, N, GROUP_M, m0, n0, EPI == EPI_PARTIAL ? ep.splits : 1, EPI == EPI_PARTIAL ? &split : nullptr);
+  if (EPI != EPI_PARTIAL && ep.t_count > 0) {  // main part of a tail-split launch: tiles [t_begin, +t_count)
+    int tg;
+    tile_of_range(M, N, GROUP_M, ep.t_begin, ep.t_count, 1, m0, n0, split, tg);
+  } else {
+    tile_of(M, N, GROUP_M, m0, n0, EPI == EPI_PARTIAL ? ep.splits : 1, EPI == EPI_PARTIAL ? &split : nullptr);
+  }
   int k_begin = 0;
   if (EPI == EPI_PARTIAL) {
     const int ku = K / 128;  // splits take whole 128-deep units (even tile count per split)
@@ -1803,7 +1808,7 @@ void launch_p4(const uint16_t* A, long lda, const uint16_t* B, long ldb, int M, 
   }
   if constexpr (EPI != EPI_PARTIAL && EPI != EPI_TAIL) {
     SkPlan pl;
-    const int G = (g_p4_sched == 4 || g_p4_sched == 0) ? sk_plan(M, N, K, &pl) : 0;
+    const int G = (g_p4_sched == 4 || g_p4_sched == 0) && ep.t_count == 0 ? sk_plan(M, N, K, &pl) : 0;
     if (G > 0) {
       if (g_p4_sched == 4) return launch_sk<EPI, 4>(A, lda, B, ldb, M, N, K, ep, G, pl, st);
       return launch_sk<EPI, 0>(A, lda, B, ldb, M, N, K, ep, G, pl, st);
@@ -1875,7 +1880,7 @@ void launch_epi(const uint16_t* A, long lda, const uint16_t* B, long ldb, int M,
 // tail split of the last partial wave (A/B switch).  Off: measured slower on every shape it applies
 // to (enc FF1 199 -> 215 us, decoder Wo 70 -> 81 us; ViT-L step +0.9 ms, profiles/r1_gemm_tail_split.txt)
 // -- the last, sparsely filled wave already runs faster per tile than a full one
-int g_gemm_tail = 0;
+int g_gemm_tail = 1;  // tail split of the last partial wave (K >= 1024): ViT-B FF2 fwd 127 -> 109 us (profiles/r2_gemm_tail_p4.txt)
 
 int num_cus() {
   if (g_num_cus == 0) {
@@ -1929,7 +1934,7 @@ void jm_gemm_set_pp(int on) { g_pp = on; }
 int jm_gemm_nt_tail_plan(int M, int N, int K, int epi, int* tail_r, long* ws_floats) {
   *tail_r = 0;
   *ws_floats = 0;
-  if (!g_gemm_tail || (g_gemm_wn != 12 && g_gemm_wn != 6)) return 0;
+  if (!g_gemm_tail || (g_gemm_wn != 12 && g_gemm_wn != 6 && g_gemm_wn != 20)) return 0;
   if (!(epi == EPI_STORE || epi == EPI_GELU || epi == EPI_DGELU || epi == EPI_GELU_ONLY) || N % 8 || K % 128) return 0;
   const int ncu = num_cus();
   const int tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
@@ -1937,7 +1942,9 @@ int jm_gemm_nt_tail_plan(int M, int N, int K, int epi, int* tail_r, long* ws_flo
   const int r = tiles % ncu;
   if (r == 0 || r > ncu / 4) return 0;
   int S = ncu / r;
-  if (S > K / 64) S = K / 64;
+  // every split keeps >= 8 64-deep K steps (r1: splits of 1-2 steps lost to the partial round trip,
+  // profiles/r1_gemm_tail_split.txt)
+  if (S > K / 512) S = K / 512;
   if (S > 8) S = 8;
   if (S < 2) return 0;
   *tail_r = r;

@@ -23,6 +23,7 @@ def _reset_gemm_variant(request):
         request.getfixturevalue("ext").attn_set_bwd_ppw(0)
         request.getfixturevalue("ext").gemm_tn_set_acc0(0)
         request.getfixturevalue("ext").gemm_tn_set_variant(4)
+        request.getfixturevalue("ext").gemm_set_tail(1)
 
 
 def rel(a, b):
@@ -407,7 +408,7 @@ def test_layernorm_bwd_fused_residual(ext, T0, view_y, with_scale, la):
 
 
 @pytest.mark.parametrize("kind", ["store", "gelu", "gelu_only", "dgelu"])
-@pytest.mark.parametrize("M,N,K", [(4352, 4096, 1024), (4200, 4096, 512)])
+@pytest.mark.parametrize("M,N,K", [(4352, 4096, 1024), (4200, 4096, 512), (25472, 768, 3072)])
 def test_gemm_nt_tail_split(ext, kind, M, N, K):
     """Last partial wave of tiles computed split-K + finish kernel == the plain launch."""
     torch.manual_seed(5)
@@ -423,7 +424,7 @@ def test_gemm_nt_tail_split(ext, kind, M, N, K):
             outs.append((ext.gemm_nt_dgelu(A, W, pre, db), db))
         else:
             outs.append(tuple(ext.gemm_nt(A, W, b, kind != "store", kind == "gelu_only")))
-    ext.gemm_set_tail(0)
+    ext.gemm_set_tail(1)
     ref = A.float() @ W.float().t()
     for o0, o1 in zip(outs[0], outs[1]):
         assert o0.shape == o1.shape

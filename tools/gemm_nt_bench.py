@@ -54,10 +54,12 @@ def main():
     # "d" = persistent whole tiles on the fewest CUs that keep the round count (gemm_set_sk 1 / 2)
     variants = a.variant.split(",")
 
-    def setv(v):  # suffixes: s / d = persistent stream-K / fewer-CU whole tiles, p = persistent overlapped
+    def setv(v):  # suffixes: s / d = persistent stream-K / fewer-CU whole tiles, p = persistent overlapped,
+        # t = tail split (last partial wave split-K + finish kernel)
         ext.gemm_set_sk(2 if "d" in v else 1 if "s" in v else 0)
         ext.gemm_set_pp(1 if "p" in v else 0)
-        ext.gemm_set_variant(int(v.rstrip("sdp")), a.group)
+        ext.gemm_set_tail(1 if "t" in v else 0)
+        ext.gemm_set_variant(int(v.rstrip("sdpt")), a.group)
 
     setv(variants[0])
     names = [n for n in FWD if not a.only or n in a.only.split(",")]
