@@ -16,6 +16,7 @@ int jm_layernorm_bwd(const void* dy, int dy_bf16, const float* x, long sB, long 
                      const float* dres, long rB, long rT, float* dgamma, float* dbeta, int accum_params, float* ws,
                      const JmLnRes* res, hipStream_t st);
 int jm_layernorm_bwd_blocks(int rows, int D);
+void jm_ln_set_bwd_blocks(int v);
 void jm_ln_set_bwd_la(int v);
 // debug build (-DJM_DEBUG): first failing soft-check line per kernel translation unit (0 = none;
 // reading clears it); always 0 in the release build
@@ -836,6 +837,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_tn_wgrad_seg", &gemm_tn_wgrad_seg);
   m.def("gemm_set_variant", &jm_gemm_set_variant, py::arg("wn"), py::arg("group") = 8);
   m.def("gemm_set_tail", &jm_gemm_set_tail);
+  m.def("ln_set_bwd_blocks", &jm_ln_set_bwd_blocks);
   m.def("gemm_set_pp", &jm_gemm_set_pp, "persistent overlapped NT launch for multi-round grids (1, default) or tiled (0)");
   m.def("gemm_set_sk", &jm_gemm_set_sk, "persistent DP + stream-K NT launches where they pay (1, default) or never (0)");
   m.def("gemm_tn_set_acc0", &jm_gemm_tn_set_acc0);

@@ -763,13 +763,17 @@ int jm_residual_ln_fwd(const float* x, long sB, long sT, const uint16_t* y, cons
 
 void jm_ln_set_bwd_la(int v) { g_ln_bwd_la = v; }
 
+// runtime switch: most row-loop blocks of the (non-wide) LN backward
+int g_ln_bwd_blocks = 512;  // = 2 resident blocks per CU (2 waves / SIMD): one round, half the partials of 1024 (-0.3 ms/step, profiles/r2_ln_bwd_blocks.txt)
+void jm_ln_set_bwd_blocks(int v) { g_ln_bwd_blocks = v < 64 ? 64 : v; }
+
 int jm_layernorm_bwd_blocks(int rows, int D) {
   // wide rows: one workgroup per row (at most 1024 workgroups, grid-stride beyond)
   if (use_wide(rows, D)) return rows > 1024 ? 1024 : rows;
-  // grid-stride over rows: 1024 blocks x 4 waves = 4 waves per SIMD streaming; each block writes
-  // one [2*D] partial (no atomics in the hot kernel)
+  // grid-stride over rows, 4 waves per block; each block writes one [NP*D] partial (no atomics in
+  // the hot kernel)
   int nb = (rows + 3) / 4;
-  return nb > 1024 ? 1024 : nb;
+  return nb > g_ln_bwd_blocks ? g_ln_bwd_blocks : nb;
 }
 
 int jm_layernorm_bwd(const void* dy, int dy_bf16, const float* x, long sB, long sT, int B, int T, int D,
