@@ -1438,12 +1438,13 @@ int run_t(bool fwd, const uint16_t* qkv, const uint16_t* o, const uint16_t* dO, 
 
 // runtime switch: batch elements per bwd2 workgroup (one head each); 0 = auto (bwd_ppw)
 int g_bwd_ppw = 0;
-// runtime switch: the batched backward (bwd3) also for head dim 64 at S > 64 (finetune S = 199)
+// runtime switch: the batched backward (bwd3) also for head dim 64 at S > 64 (finetune S = 199);
+// 2: also at S <= 64 (the encoder, A/B)
 int g_bwd3_hd64 = 1;  // finetune S=199 hd=64 backward 249 -> 177 us (profiles/r2_attn_ft_bwd.txt)
 // the backward that jm_attn_bwd runs is the batched bwd3 kernel (B dbias partial rows) -- the
 // single source of that choice for run_bwd2 and jm_attn_bwd_part_rows
 bool uses_bwd3(int S, int hd) {
-  return g_use_tr == 3 && (hd == 32 || (hd == 64 && S > 64 && g_bwd3_hd64));
+  return g_use_tr == 3 && (hd == 32 || (hd == 64 && (S > 64 ? g_bwd3_hd64 : g_bwd3_hd64 == 2)));
 }
 
 
@@ -1464,7 +1465,7 @@ int run_bwd2(const uint16_t* qkv, const uint16_t* o, const uint16_t* dO, const f
                               (int)sm);
     attr_set = true;
   }
-  if constexpr (HD == 32 || (HD == 64 && SP > 64)) {
+  if constexpr (HD == 32 || HD == 64) {
     if (!uses_bwd3(S, HD)) goto bwd2;
     static bool attr3 = false;
     if (sm > 64 * 1024 && !attr3) {
