@@ -102,13 +102,19 @@ def use_our_gemm(M: int, N: int, K: int, fused_gelu: bool = False, kind: str = "
     return K % 64 == 0 and N % 8 == 0 and M >= 4096
 
 
+_SPLITK_MIN_K = int(os.environ.get("JMAE_SPLITK_MIN_K", "4096"))
+
+
 def splitk_plan(M: int, N: int, K: int) -> int:
-    """Split-K factor for a small-M, long-K GEMM on the MFMA kernel (0 = not this path): the
-    jumbo MLP's 512-row GEMMs with K = 12288 have only 24 output tiles for 256 CUs."""
-    if _GEMM_MODE == "blas" or M > 2048 or K < 4096 or K % 64 or N % 8:
+    """Split-K factor for a small-M GEMM on the MFMA kernel (0 = not this path): the jumbo MLP's
+    512-row GEMMs have 24 (K = 12288) or 96 (K = 3072: W1 forward, W2 data gradient) output tiles
+    for 256 CUs.  Every split keeps >= 512 of K.  K >= 4096 by default: routing the K = 3072 pair
+    here too (JMAE_SPLITK_MIN_K=2048, S = 2) measured 93.95 vs 93.57 ms/step with hipBLASLt's
+    192x128 tiles (profiles/r2_jumbo_splitk.txt), so those two stay on the library."""
+    if _GEMM_MODE == "blas" or M > 2048 or K < _SPLITK_MIN_K or K % 128 or N % 8:
         return 0
     tiles = -(-M // 256) * -(-N // 256)
-    if tiles > 64:
+    if tiles > 128:
         return 0
     return max(2, min(256 // tiles, K // 512, 32))
 

@@ -36,6 +36,8 @@ def apply(P, cfg: str):
         elif k == "GEMM_TAIL":
             from jumbo_mae_tpu_amd.ops import _ext
             _ext.load(True).gemm_set_tail(int(v))
+        elif k == "SPLITK_MIN_K":
+            P._SPLITK_MIN_K = int(v)
         elif k == "LN_BWD_BLOCKS":
             from jumbo_mae_tpu_amd.ops import _ext
             _ext.load(True).ln_set_bwd_blocks(int(v))

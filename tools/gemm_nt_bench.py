@@ -69,11 +69,11 @@ def main():
             M, N, K = FWD[name]
             if kind.startswith("fwd_gelu") and name not in ("enc_ff1", "dec_ff1", "jumbo1", "b_ff1"):
                 continue
-            if kind == "dgrad_gelu" and name not in ("enc_ff2", "dec_ff2", "b_ff2"):
+            if kind.startswith("dgrad_") and name not in ("enc_ff2", "dec_ff2", "b_ff2"):
                 continue
             if kind == "splitk" and name not in ("jumbo1", "jumbo2"):
                 continue
-            if kind in ("dgrad", "dgrad_gelu"):  # dX[M,K] = dy[M,N] @ W[N,K]  ->  NT with B = W^T [K, N]
+            if kind.startswith("dgrad"):  # dX[M,K] = dy[M,N] @ W[N,K]  ->  NT with B = W^T [K, N]
                 M, N, K = M, K, N
             x = (torch.rand(M, K, device="cuda") * 2 - 1).bfloat16()
             w = ((torch.rand(N, K, device="cuda") * 2 - 1) * 0.05).bfloat16()
@@ -91,6 +91,12 @@ def main():
                 dbg = torch.zeros(N, device="cuda")
                 ours = lambda: (ext.gemm_nt_dgelu(x, w, pre, dbg),)  # noqa: E731
                 blas = lambda: ext.gelu_bwd(pre, x @ wm, dbg)  # noqa: E731
+            elif kind in ("dgrad_dmul", "dgrad_dmul_nob"):  # x saved gelu'(h) (training path), +- FF1 bias grad
+                wm = w.t().contiguous()
+                pre = (torch.rand(M, N, device="cuda") * 1.1).bfloat16()
+                dbg = torch.zeros(N, device="cuda") if kind == "dgrad_dmul" else None
+                ours = lambda: (ext.gemm_nt_dgelu(x, w, pre, dbg, True),)  # noqa: E731
+                blas = lambda: (x @ wm) * pre  # noqa: E731
             elif kind == "dgrad":
                 wm = w.t().contiguous()  # W as the model stores it: [N_fwd, K_fwd] = w^T
                 ours = lambda: ext.gemm_nt(x, w, None, False)  # noqa: E731
@@ -111,7 +117,7 @@ def main():
             for v in variants:
                 setv(v)
                 o = ours()
-                r0 = torch.addmm(b, x.float(), w.float().t()) if kind != "dgrad_gelu" else o[0].float()
+                r0 = torch.addmm(b, x.float(), w.float().t()) if not kind.startswith("dgrad_") else o[0].float()
                 if kind == "fwd_gelu_only":
                     r0 = torch.nn.functional.gelu(r0.bfloat16().float(), approximate="tanh")
                 elif kind == "fwd_gelu_d":
@@ -120,7 +126,7 @@ def main():
                 errs.append(((o[0].float() - r0).abs().max() / r0.abs().max()).item())
             setv(variants[0])
             out = ours()
-            ref = torch.addmm(b, x.float(), w.float().t()) if kind != "dgrad_gelu" else out[0].float()
+            ref = torch.addmm(b, x.float(), w.float().t()) if not kind.startswith("dgrad_") else out[0].float()
             if kind == "fwd_gelu_only":
                 ref = torch.nn.functional.gelu(ref.bfloat16().float(), approximate="tanh")
             elif kind == "fwd_gelu_d":
