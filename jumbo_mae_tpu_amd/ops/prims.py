@@ -171,8 +171,10 @@ def linear_gelu_fwd_saved(x2: torch.Tensor, hw: Handle, hb: Handle | None, need_
 # data-gradient chain, which then execute underneath them instead of after them.  The chain's
 # tensors are pinned for the side stream with record_stream; the DP reducer launches its
 # all-reduces from this stream and the trainer joins it before the optimizer.
-# Off by default: measured on MI355X it gains 1-2 % on most runs but some runs collapse to
-# 0.4-0.6x (the two queues' kernels interfere), which is not acceptable for a benchmark path.
+# Off by default.  Round 1 (hipBLASLt wgrads): +1-2 % on most runs, some runs collapsed to
+# 0.4-0.6x.  Round 2 (TN MFMA wgrads): no collapse in 6 processes, +0.3-0.8 %, and ~0.5 ms/step of
+# cross-queue hand-off gaps in the trace (profiles/r2_wgrad_side_stream.txt); kept off so the DP
+# reducer's collectives stay on the compute stream in multi-GPU runs.
 _side = {"stream": None, "enabled": os.environ.get("JMAE_WGRAD_STREAM", "0") == "1", "cb": False}
 
 
