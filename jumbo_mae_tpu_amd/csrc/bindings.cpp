@@ -37,6 +37,7 @@ int jm_gelu_bwd(const uint16_t* h, const uint16_t* da, uint16_t* dh, float* bias
 int jm_colsum_bf16(const uint16_t* x, float* acc, int M, int N, hipStream_t st);
 int jm_splitk_reduce_add(const float* part, float* g, long n, int S, hipStream_t st);
 int jm_transpose_bf16(const uint16_t* src, uint16_t* dst, int R, int C, hipStream_t st);
+int jm_transpose_bf16_batch(const long long* desc, int n, int tiles, hipStream_t st);
 int jm_residual_fwd(const float* x, long sB, long sT, int B, int T, int D, const uint16_t* y, const float* scale,
                     const float* mask, float* out, long oB, long oT, hipStream_t st);
 int jm_residual_bwd(const float* dout, long dB, long dT, const uint16_t* y, const float* scale, const float* mask,
@@ -695,6 +696,17 @@ void transpose_bf16(torch::Tensor src, torch::Tensor dst) {
   check_rc(jm_transpose_bf16(bf(src), bfm(dst), src.size(0), src.size(1), stream()), "transpose_bf16");
 }
 
+// all transposed weight copies of a step in one launch: desc int64 [n, 6] on the device
+// ({src, dst, R, C, first tile, tiles along C}, built by ParamStore.refresh_transposes)
+void transpose_bf16_batch(torch::Tensor desc, int64_t tiles) {
+  CHECK_CONTIG(desc);
+  TORCH_CHECK(desc.is_cuda() && desc.scalar_type() == torch::kInt64 && desc.dim() == 2 && desc.size(1) == 6,
+              "transpose_bf16_batch: desc int64 [n, 6] on the device");
+  check_rc(jm_transpose_bf16_batch(reinterpret_cast<const long long*>(desc.data_ptr<int64_t>()), (int)desc.size(0),
+                                   (int)tiles, stream()),
+           "transpose_bf16_batch");
+}
+
 // weight gradient G[N, K] += dy[M, N]^T . x[M, K] on the TN MFMA kernel (split over M, fp32
 // partial tiles reduced into G); returns the number of M splits used
 int64_t gemm_tn_wgrad(torch::Tensor dy, torch::Tensor x, torch::Tensor g) {
@@ -837,6 +849,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_tn_wgrad_seg", &gemm_tn_wgrad_seg);
   m.def("gemm_set_variant", &jm_gemm_set_variant, py::arg("wn"), py::arg("group") = 8);
   m.def("gemm_set_tail", &jm_gemm_set_tail);
+  m.def("transpose_bf16_batch", &transpose_bf16_batch);
   m.def("ln_set_bwd_blocks", &jm_ln_set_bwd_blocks);
   m.def("gemm_set_pp", &jm_gemm_set_pp, "persistent overlapped NT launch for multi-round grids (1, default) or tiled (0)");
   m.def("gemm_set_sk", &jm_gemm_set_sk, "persistent DP + stream-K NT launches where they pay (1, default) or never (0)");

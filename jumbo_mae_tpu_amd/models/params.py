@@ -24,6 +24,7 @@ from __future__ import annotations
 import contextlib
 
 import math
+import os
 from dataclasses import dataclass, field
 from typing import Callable, Iterable
 
@@ -61,6 +62,10 @@ class Segment:
 
 def identity(a: np.ndarray) -> np.ndarray:
     return a
+
+
+# Handle.weight_t copies refreshed in one batched launch (A/B switch, JMAE_WT_BATCH=0 disables)
+BATCH_TRANSPOSES = os.environ.get("JMAE_WT_BATCH", "1") == "1"
 
 
 class Handle:
@@ -114,10 +119,14 @@ class Handle:
         once per shadow update (``ParamStore.version``)."""
         if self._wt is None or self._wt_version != self.store.version:
             w = self.weight()
-            if self._wt is None:
+            first = self._wt is None
+            if first:
                 self._wt = torch.empty((w.shape[1], w.shape[0]), dtype=w.dtype, device=w.device)
             from ..ops import _ext  # noqa: PLC0415 (models must import without the extension)
-            if _ext.use_hip(w) and w.dtype == torch.bfloat16 and w.shape[0] % 8 == 0 and w.shape[1] % 8 == 0:
+            hip_ok = _ext.use_hip(w) and w.dtype == torch.bfloat16 and w.shape[0] % 8 == 0 and w.shape[1] % 8 == 0
+            if hip_ok and not first and self.store.refresh_transposes():
+                return self._wt  # refreshed together with every other stale transposed copy
+            if hip_ok:
                 _ext.load().transpose_bf16(w, self._wt)
             else:
                 self._wt.copy_(w.t())
@@ -158,6 +167,34 @@ class ParamStore:
         self._handles: list[Handle] = []
         self.count_uses = True  # off while an activation-checkpoint recompute re-runs a forward
         self.version = 0  # bumped whenever the shadow changes (optimizer step, sync, load)
+        # batched refresh of the transposed weight copies (Handle.weight_t): device descriptor
+        # table, cached per set of copies
+        self._wt_batch: tuple | None = None
+
+    def refresh_transposes(self) -> bool:
+        """Rewrite every existing transposed weight copy from the current bf16 shadow in ONE
+        launch (the first ``weight_t`` call after a shadow update triggers it; the backward then
+        finds all copies fresh).  Returns False when batching is off / not applicable."""
+        if not BATCH_TRANSPOSES:
+            return False
+        hs = [h for h in self._handles if h._wt is not None and h._wt.dtype == torch.bfloat16 and h._wt.is_cuda]
+        if not hs:
+            return False
+        key = tuple((h._wt.data_ptr(), h.shadow.data_ptr()) for h in hs)
+        if self._wt_batch is None or self._wt_batch[0] != key:
+            rows, tiles = [], 0
+            for h in hs:
+                R, C = h.shape
+                ntc = -(-C // 64)
+                rows.append([h.shadow.data_ptr(), h._wt.data_ptr(), R, C, tiles, ntc])
+                tiles += ntc * -(-R // 64)
+            desc = torch.tensor(rows, dtype=torch.int64).to(hs[0]._wt.device)
+            self._wt_batch = (key, desc, tiles)
+        from ..ops import _ext  # noqa: PLC0415
+        _ext.load().transpose_bf16_batch(self._wt_batch[1], self._wt_batch[2])
+        for h in hs:
+            h._wt_version = self.version
+        return True
 
     @contextlib.contextmanager
     def uses_suppressed(self):

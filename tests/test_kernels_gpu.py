@@ -549,3 +549,36 @@ def test_gemm_nt_persistent_overlapped(ext, kind, M, N, K):
         assert torch.equal(o0, o1)
     if kind == "store":
         assert rel(outs[2][0], A.float() @ W.float().t() + b) < 1e-2
+
+
+def test_transpose_bf16_batch(ext):
+    """All transposed weight copies in one launch == per-matrix transposes (ragged 64-tiles)."""
+    shapes = [(3072, 1024), (1024, 1024), (520, 136), (64, 4096)]
+    srcs = [torch.randn(r, c, device="cuda").bfloat16() for r, c in shapes]
+    dsts = [torch.empty(c, r, device="cuda", dtype=torch.bfloat16) for r, c in shapes]
+    rows, tiles = [], 0
+    for s_, d_ in zip(srcs, dsts):
+        R, C = s_.shape
+        ntc = -(-C // 64)
+        rows.append([s_.data_ptr(), d_.data_ptr(), R, C, tiles, ntc])
+        tiles += ntc * -(-R // 64)
+    ext.transpose_bf16_batch(torch.tensor(rows, dtype=torch.int64).cuda(), tiles)
+    for s_, d_ in zip(srcs, dsts):
+        assert torch.equal(d_, s_.t())
+
+
+def test_weight_t_batched_refresh():
+    """ParamStore refreshes every transposed copy in one batch after a shadow update."""
+    from jumbo_mae_tpu_amd.config import ViTConfig
+    from jumbo_mae_tpu_amd.models.classifier import FinetuneModel
+    vc = ViTConfig(layers=2, dim=128, heads=4, labels=10, image_size=32, patch_size=16, posemb="sincos2d")
+    m = FinetuneModel(vc).to("cuda", torch.bfloat16, seed=0)
+    hs = [h for h in m.store._handles if len(h.shape) == 2 and h.shape[0] % 8 == 0 and h.shape[1] % 8 == 0]
+    for h in hs:
+        h.weight_t()
+    m.store.master.mul_(1.5)
+    m.store.sync_shadow()
+    assert torch.equal(hs[0].weight_t(), hs[0].weight().t())  # triggers the batched refresh
+    for h in hs:
+        assert h._wt_version == m.store.version
+        assert torch.equal(h._wt, h.weight().t())

@@ -36,6 +36,9 @@ def apply(P, cfg: str):
         elif k == "GEMM_TAIL":
             from jumbo_mae_tpu_amd.ops import _ext
             _ext.load(True).gemm_set_tail(int(v))
+        elif k == "JMAE_WT_BATCH":
+            import jumbo_mae_tpu_amd.models.params as PM
+            PM.BATCH_TRANSPOSES = v == "1"
         elif k == "SPLITK_MIN_K":
             P._SPLITK_MIN_K = int(v)
         elif k == "LN_BWD_BLOCKS":
