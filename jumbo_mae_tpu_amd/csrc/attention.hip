@@ -51,6 +51,62 @@ JM_DEVICE s16x4_t tr4(const uint16_t* p) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4_t*)(p));
 }
 
+// workgroup barrier; LDSONLY: LDS traffic only (s_waitcnt lgkmcnt(0) + s_barrier) -- unlike
+// __syncthreads it does not wait for outstanding global loads / LDS-DMA (vmcnt), so a prefetch
+// stays in flight across it
+template <int V>
+struct IC {
+  static constexpr int value = V;
+};
+
+// two static LDS image sets for the double-buffered backward: distinct LDS objects, so alias
+// analysis proves that reads of one set never touch the DMA in flight into the other (with one
+// dynamic array the compiler inserts a vmcnt wait for that DMA before every LDS read)
+template <int N, int TAG>
+JM_DEVICE uint16_t* lds_images() {
+  __shared__ __attribute__((aligned(16))) uint16_t buf[N];
+  return buf;
+}
+
+template <bool LDSONLY>
+JM_DEVICE void wg_bar() {
+  if constexpr (LDSONLY) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  else __syncthreads();
+}
+
+typedef __attribute__((address_space(3))) void lds_void_t;
+
+// buffer resource over [base, base + bytes): loads past the end read zero (padded rows)
+JM_DEVICE __amdgpu_buffer_rsrc_t make_rsrc(const uint16_t* base, long bytes) {
+  const int n = bytes >= 0xffffffffL ? -1 : (int)bytes;
+  return __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, n, 0x00020000);
+}
+
+// buffer_load_dwordx4 ... lds: 16 B per lane into LDS at (wave-uniform l) + 16 * lane
+JM_DEVICE void blds16(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff, uint16_t* l) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void_t*)(l), 16, voff, soff, 0, 0);
+}
+
+// The same load as inline asm: the compiler does not see it as an LDS DMA, so it adds no vmcnt
+// wait for it before later LDS reads (the double-buffered backward reads one image set while
+// the DMA into the other is in flight; the kernel waits for its DMA with explicit counted waits)
+typedef int i32x4_t __attribute__((ext_vector_type(4)));
+JM_DEVICE i32x4_t rsrc4(const uint16_t* base, long bytes) {
+  const unsigned long a = (unsigned long)base;
+  i32x4_t r;
+  r.x = (int)(unsigned)a;
+  r.y = (int)((unsigned)(a >> 32) & 0xffffu);
+  r.z = bytes >= 0xffffffffL ? -1 : (int)bytes;
+  r.w = 0x00020000;
+  return r;
+}
+JM_DEVICE void blds16_asm(i32x4_t rsrc, uint32_t voff, uint16_t* l) {
+  const uint32_t m0v =
+      __builtin_amdgcn_readfirstlane((uint32_t)(unsigned long)(__attribute__((address_space(3))) uint16_t*)l);
+  asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds" ::"s"(m0v), "v"(voff), "s"(rsrc)
+               : "memory", "m0");
+}
+
 JM_DEVICE f32x4_t mfma(bf16x8_t a, bf16x8_t b, f32x4_t c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
@@ -808,12 +864,20 @@ JM_DEVICE int swo(int row, int col) {
   return row * (NCH * 8) + ((((col >> 3) ^ aswz(row)) & (NCH - 1)) << 3) + (col & 7);
 }
 
-template <int HD, int SP>
-constexpr size_t bwd2_smem() {
-  return (size_t)(3 * SP * HD + SP * 64) * 2 + (2 * SP + 3 * HD) * sizeof(float);
+template <int HD, int SP, bool DB = false>
+constexpr size_t bwd2_smem() {  // dynamic part (DB: + 2 x 4 static images)
+  return (size_t)((DB ? 0 : 3) * SP * HD + SP * 64) * 2 + (2 * SP + 3 * HD) * sizeof(float);
 }
 
-template <int HD, int SP>
+// DB (double-buffered, SP = HD = 64: the encoder): the Q / dO / K / O images of the NEXT batch
+// element are DMA'd global -> LDS (buffer_load ... lds, 16 B per lane, the chunk swizzle applied
+// on the global side) into the second image set while this element computes, instead of a
+// register burst whose latency is exposed once per element; V fragments and lse of the next
+// element are prefetched into registers.  delta = O . dO is then taken from the LDS images.
+template <int HD, int SP, bool DB>
+constexpr int bwd2_imgs() { return DB ? 0 : 3; }  // DB: the image sets are static LDS arrays
+
+template <int HD, int SP, bool DB = false>
 __global__ __launch_bounds__(256) void attn_bwd2_kernel(const uint16_t* __restrict__ qkv,
                                                         const uint16_t* __restrict__ o,
                                                         const uint16_t* __restrict__ dO,
@@ -821,15 +885,22 @@ __global__ __launch_bounds__(256) void attn_bwd2_kernel(const uint16_t* __restri
                                                         uint16_t* __restrict__ dqkv, int S, int H, float scale,
                                                         float* __restrict__ dbp, int B, int ppw, int remap) {
   JM_DGUARD(S >= 1 && S <= SP && blockDim.x == 256 && ppw >= 1);
+  static_assert(!DB || (SP == 64 && HD == 64), "double-buffered backward: S <= 64, hd 64");
   constexpr int NW = 4, NTH = 256, QC = 64;
   constexpr int NT = SP / 16, KK = HD / 32, DT = HD / 16;
   constexpr int NKW = (NT + NW - 1) / NW;
   constexpr int NCH = HD / 8;  // 16-byte chunks per Q / dO / K row
+  constexpr int IMG = SP * HD;
   extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
   uint16_t* Qs = smem;
-  uint16_t* dOs = Qs + SP * HD;
-  uint16_t* Ks = dOs + SP * HD;
-  uint16_t* dSt = Ks + SP * HD;  // [SP][QC], 8 chunks per row
+  uint16_t* dOs = Qs + IMG;
+  uint16_t* Ks = dOs + IMG;
+  uint16_t* dSt = smem + bwd2_imgs<HD, SP, DB>() * IMG;  // [SP][QC], 8 chunks per row
+  uint16_t* img[2] = {nullptr, nullptr};
+  if constexpr (DB) {
+    img[0] = lds_images<4 * IMG, 0>();
+    img[1] = lds_images<4 * IMG, 1>();
+  }
   float* lse_s = reinterpret_cast<float*>(dSt + SP * QC);
   float* delta_s = lse_s + SP;
   float* bsum = delta_s + SP;
@@ -916,13 +987,115 @@ __global__ __launch_bounds__(256) void attn_bwd2_kernel(const uint16_t* __restri
     lsen = (i < SP && i < S) ? lse[((long)b * H + h) * S + i] * LOG2E : INFINITY;
   };
 
-  for (int pj = 0; pj < ppw; ++pj) {
+  // DB: the Q / dO / K / O images of element b DMA'd into image set k (16-row slabs per wave,
+  // 8 rows x 8 chunks per instruction; rows >= S read as zero through the buffer range)
+  auto issue_glds = [&](int b, uint16_t* dst) {
+    const uint16_t* base = qkv + (long)b * S * ts;
+    const i32x4_t rs[4] = {rsrc4(base + h * HD, (S - 1) * ts * 2 + HD * 2),
+                           rsrc4(dO + (long)b * S * os + h * HD, (S - 1) * os * 2 + HD * 2),
+                           rsrc4(base + (H + h) * HD, (S - 1) * ts * 2 + HD * 2),
+                           rsrc4(o + (long)b * S * os + h * HD, (S - 1) * os * 2 + HD * 2)};
+    const long strides[4] = {ts, os, ts, os};
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int row0 = 16 * wave + 8 * u, row = row0 + (lane >> 3);
+        const int c = (lane & 7) ^ aswz(row);
+        blds16_asm(rs[t], (uint32_t)(row * strides[t] * 2 + c * 16), dst + t * IMG + row0 * HD);
+      }
+  };
+  // V fragments and lse of element b into the prefetch registers: unconditional loads (clamped
+  // rows, masked after) so every wave issues the same number of vector-memory instructions
+  // (inline-asm loads: the compiler neither waits for them nor counts them -- the explicit counted
+  // wait at the top of the next element, tied to these registers, does; the padded-key zeroing and
+  // the lse select happen when the registers are consumed)
+  float lse_raw = 0.f;
+  static_assert(!DB || (NKW == 1 && KK == 2), "DB prefetch registers: one key tile, two V fragments");
+  auto load_vl = [&](int b) {
+    const uint16_t* Vg = qkv + (long)b * S * ts + (2 * H + h) * HD;
+#pragma unroll
+    for (int w = 0; w < NKW; ++w) {
+      const int key = (wave + NW * w) * 16 + l16;
+      const int kc = key < S ? key : S - 1;
+#pragma unroll
+      for (int kk = 0; kk < KK; ++kk) {
+        const uint16_t* pv = Vg + (long)kc * ts + 32 * kk + 8 * g;
+        asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(vfn[w][kk]) : "v"(pv) : "memory");
+      }
+    }
+    const int i = threadIdx.x;
+    const float* pl = lse + ((long)b * H + h) * S + (i < S ? i : S - 1);
+    asm volatile("global_load_dword %0, %1, off" : "=v"(lse_raw) : "v"(pl) : "memory");
+  };
+  if constexpr (DB) {
+    if (bg * ppw < B) {
+      issue_glds(bg * ppw, img[0]);
+      load_vl(bg * ppw);
+    }
+  }
+
+  // one batch element; BUF = its image set (DB: compile-time, so the LDS reads of this set and
+  // the DMA into the other one are provably disjoint and the compiler adds no vmcnt wait between)
+  auto pair = [&](const int pj, auto bufc) -> bool {
+  constexpr int BUF = decltype(bufc)::value;
   const int b = bg * ppw + pj;
-  if (b >= B) break;  // workgroup-uniform
+  if (b >= B) return false;  // workgroup-uniform
   uint16_t* dQg = dqkv + (long)b * S * ts + h * HD;
   uint16_t* dKg = dqkv + (long)b * S * ts + (H + h) * HD;
   uint16_t* dVg = dqkv + (long)b * S * ts + (2 * H + h) * HD;
 
+  if constexpr (DB) {
+    Qs = img[BUF];
+    dOs = Qs + IMG;
+    Ks = dOs + IMG;
+    const uint16_t* Os = Ks + IMG;
+    // next element's images DMA'd now (they land while this one computes), then this element's
+    // V fragments / lse leave the prefetch registers, then the next element's are loaded
+    // issued unconditionally (the last element re-fetches itself into the idle image set) so
+    // every path has the same outstanding-load count for the counted wait below
+    const bool nxt = pj + 1 < ppw && b + 1 < B;
+    const int bn = nxt ? b + 1 : b;
+    issue_glds(bn, img[1 - BUF]);
+    // this element's DMA and V / lse loads (older than the 8 DMA just issued) have landed
+    asm volatile("s_waitcnt vmcnt(8)" : "+v"(vfn[0][0]), "+v"(vfn[0][1]), "+v"(lse_raw) : : "memory");
+#pragma unroll
+    for (int w = 0; w < NKW; ++w) {
+      const bool kin = (wave + NW * w) * 16 + l16 < S;
+#pragma unroll
+      for (int kk = 0; kk < KK; ++kk) {
+        s16x8_t z = {0, 0, 0, 0, 0, 0, 0, 0};
+        vf[w][kk] = kin ? vfn[w][kk] : __builtin_bit_cast(bf16x8_t, z);
+      }
+    }
+    const float lcur = ((int)threadIdx.x < S) ? lse_raw * LOG2E : INFINITY;
+    load_vl(bn);
+    if (threadIdx.x < SP) {
+      delta_s[threadIdx.x] = 0.f;
+      lse_s[threadIdx.x] = lcur;
+    }
+    wg_bar<DB>();
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+      const int i = it * NTH + threadIdx.x;
+      const int r = i / NCH, c = (i % NCH) * 8;
+      if (i < SP * NCH && r < S) {
+        const int off = swo<NCH>(r, c);
+        const uint4 ovv = *reinterpret_cast<const uint4*>(Os + off);
+        const uint4 dvv = *reinterpret_cast<const uint4*>(dOs + off);
+        const uint32_t* ow = reinterpret_cast<const uint32_t*>(&ovv);
+        const uint32_t* dw = reinterpret_cast<const uint32_t*>(&dvv);
+        float dsum = 0.f;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          dsum += __uint_as_float(ow[j] << 16) * __uint_as_float(dw[j] << 16);
+          dsum += __uint_as_float(ow[j] & 0xffff0000u) * __uint_as_float(dw[j] & 0xffff0000u);
+        }
+        atomicAdd(&delta_s[r], dsum);
+      }
+    }
+    wg_bar<DB>();
+  } else {
   load_regs(b);
 #pragma unroll
   for (int w = 0; w < NKW; ++w)
@@ -957,6 +1130,7 @@ __global__ __launch_bounds__(256) void attn_bwd2_kernel(const uint16_t* __restri
     }
   }
   __syncthreads();
+  }  // !DB staging
 
   bf16x8_t kf[NKW][KK];
   f32x4_t dvacc[NKW][DT], dkacc[NKW][DT];
@@ -1022,7 +1196,7 @@ __global__ __launch_bounds__(256) void attn_bwd2_kernel(const uint16_t* __restri
         }
       }
     }
-    __syncthreads();
+    wg_bar<DB>();
     // dQ^T[d][q] = sum_key K^T[d][key] dS^T[key][q] for this wave's 16 queries of the chunk
     {
       const int qt = qc * (QC / 16) + wave;
@@ -1055,7 +1229,7 @@ __global__ __launch_bounds__(256) void attn_bwd2_kernel(const uint16_t* __restri
         }
       }
     }
-    __syncthreads();
+    wg_bar<DB>();
   }
 #pragma unroll
   for (int w = 0; w < NKW; ++w) {
@@ -1081,7 +1255,19 @@ __global__ __launch_bounds__(256) void attn_bwd2_kernel(const uint16_t* __restri
         kb[dt][i] += dkacc[w][dt][i];
         vb[dt][i] += dvacc[w][dt][i];
       }
-  }  // batch elements
+  return true;
+  };  // batch element
+  if constexpr (DB) {
+    for (int pj = 0; pj < ppw; pj += 2) {
+      if (!pair(pj, IC<0>{})) break;
+      if (pj + 1 >= ppw || !pair(pj + 1, IC<1>{})) break;
+    }
+    // the last element's (dummy) DMA must land before the workgroup's LDS is released
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  } else {
+    for (int pj = 0; pj < ppw; ++pj)
+      if (!pair(pj, IC<0>{})) break;
+  }
   if (dbp != nullptr) {
 #pragma unroll
     for (int dt = 0; dt < DT; ++dt)
@@ -1438,6 +1624,8 @@ int run_t(bool fwd, const uint16_t* qkv, const uint16_t* o, const uint16_t* dO, 
 
 // runtime switch: batch elements per bwd2 workgroup (one head each); 0 = auto (bwd_ppw)
 int g_bwd_ppw = 0;
+// runtime switch: double-buffered (LDS-DMA prefetch of the next element) bwd2 at S <= 64, hd 64
+int g_bwd2_db = 0;
 // runtime switch: the batched backward (bwd3) also for head dim 64 at S > 64 (finetune S = 199);
 // 2: also at S <= 64 (the encoder, A/B)
 int g_bwd3_hd64 = 1;  // finetune S=199 hd=64 backward 249 -> 177 us (profiles/r2_attn_ft_bwd.txt)
@@ -1480,6 +1668,20 @@ int run_bwd2(const uint16_t* qkv, const uint16_t* o, const uint16_t* dO, const f
 bwd2:
   {
     const int ppw = bwd_ppw<HD, SP>();
+    if constexpr (HD == 64 && SP == 64) {
+      if (g_bwd2_db) {  // double-buffered LDS-DMA variant (the encoder)
+        constexpr size_t smd = bwd2_smem<HD, SP, true>();
+        static bool attr_db = false;
+        if (!attr_db) {
+          (void)hipFuncSetAttribute((const void*)attn_bwd2_kernel<HD, SP, true>,
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)smd);
+          attr_db = true;
+        }
+        attn_bwd2_kernel<HD, SP, true><<<dim3(((B + ppw - 1) / ppw) * H), 256, smd, st>>>(
+            qkv, o, dO, lse_in, out, S, H, scale, dbias_part, B, ppw, g_attn_remap);
+        return 0;
+      }
+    }
     attn_bwd2_kernel<HD, SP><<<dim3(((B + ppw - 1) / ppw) * H), 256, sm, st>>>(qkv, o, dO, lse_in, out, S, H, scale,
                                                                               dbias_part, B, ppw, g_attn_remap);
   }
@@ -1903,6 +2105,7 @@ void jm_attn_set_remap(int v) { g_attn_remap = v; }
 void jm_attn_set_fwd_hpw(int v) { g_fwd_hpw = v < 0 ? 0 : v; }
 void jm_attn_set_bwd_ppw(int v) { g_bwd_ppw = v < 0 ? 0 : v; }
 void jm_attn_set_bwd3_hd64(int v) { g_bwd3_hd64 = v; }
+void jm_attn_set_bwd2_db(int v) { g_bwd2_db = v; }
 
 // rows of the dbias_part workspace that jm_attn_bwd writes: the bwd2 kernel folds ``ppw`` batch
 // elements into one row, every other backward writes one row per batch element.  Must mirror the

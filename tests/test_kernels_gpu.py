@@ -24,6 +24,7 @@ def _reset_gemm_variant(request):
         request.getfixturevalue("ext").gemm_tn_set_acc0(0)
         request.getfixturevalue("ext").gemm_tn_set_variant(4)
         request.getfixturevalue("ext").gemm_set_tail(1)
+        request.getfixturevalue("ext").attn_set_bwd2_db(0)
 
 
 def rel(a, b):
@@ -582,3 +583,25 @@ def test_weight_t_batched_refresh():
     for h in hs:
         assert h._wt_version == m.store.version
         assert torch.equal(h._wt, h.weight().t())
+
+
+@pytest.mark.parametrize("B,S,H", [(3, 52, 16), (2, 64, 4), (5, 33, 2), (16, 52, 3)])
+@pytest.mark.parametrize("ppw", [1, 2, 3, 8])
+def test_attention_bwd2_double_buffered(ext, B, S, H, ppw):
+    """Encoder backward with the next element's images DMA'd global -> LDS while the current one
+    computes (attn_set_bwd2_db) == the register-staged backward, incl. the fused QKV bias sums."""
+    torch.manual_seed(1)
+    D = H * 64
+    qkv = (torch.randn(B, S, 3 * D, device="cuda") * 1.5).bfloat16()
+    o, lse = ext.attn_fwd(qkv, H)
+    do = torch.randn(B, S, D, device="cuda").bfloat16()
+    outs = []
+    ext.attn_set_bwd_ppw(ppw)
+    for db in (0, 1):
+        ext.attn_set_bwd2_db(db)
+        dbias = torch.zeros(3 * D, device="cuda")
+        outs.append((ext.attn_bwd(do, qkv, o, lse, H, dbias), dbias))
+    ext.attn_set_bwd2_db(0)
+    ext.attn_set_bwd_ppw(0)
+    assert torch.equal(outs[0][0], outs[1][0])
+    assert (outs[0][1] - outs[1][1]).abs().max().item() <= 1e-3 * outs[0][1].abs().max().item() + 1e-4
