@@ -152,7 +152,7 @@ def main():
             for _ in range(args.profile_steps):
                 step()
             sync()
-        log(prof.key_averages().table(sort_by="cuda_time_total", row_limit=40))
+        log(prof.key_averages().table(sort_by="cuda_time_total", row_limit=150))
 
     ms = elapsed / args.steps * 1000.0
     value = global_batch * args.steps / elapsed

@@ -142,6 +142,44 @@ def droppath_mask(rate: float, batch: int, rng, device, det: bool):
     return m
 
 
+def droppath_masks(layers, batch: int, rng, device, det: bool):
+    """Every droppath mask of a layer stack in one draw (three kernels instead of three or four
+    per mask: 36 masks per ViT-B finetune step), sliced per layer in draw order; None entries
+    for layers without droppath.  Also what activation checkpointing hands to the recompute."""
+    counts = [(layer.droppath_rate, layer.n_droppath) for layer in layers]
+    total = sum(n for r, n in counts if r > 0.0)
+    if det or total == 0:
+        return [None] * len(layers)
+    u = torch.rand((total, batch), generator=rng, device=device)
+    # runs of equal rate get one select each (Python-scalar keep: no host->device copy, so
+    # the draw is legal inside a captured graph); a uniform rate is a single kernel
+    runs, i = [], 0
+    for r, n in counts:
+        if r > 0.0:
+            if runs and runs[-1][0] == r:
+                runs[-1][2] += n
+            else:
+                runs.append([r, i, n])
+            i += n
+    parts = [torch.where(u[a:a + n] < 1.0 - r, 1.0 / (1.0 - r), 0.0) for r, a, n in runs]
+    pool = parts[0] if len(parts) == 1 else torch.cat(parts)
+    out, i = [], 0
+    for r, n in counts:
+        if r > 0.0:
+            out.append(pool[i:i + n])
+            i += n
+        else:
+            out.append(None)
+    return out
+
+
+def _mask(masks, k, rate, batch, rng, device, det):
+    """k-th pooled mask of a layer, or a fresh draw when the layer was called without a pool."""
+    if masks is not None:
+        return masks[k]
+    return droppath_mask(rate, batch, rng, device, det)
+
+
 # ---------------------------------------------------------------------------------- blocks
 class JumboLayer:
     """Encoder block (modeling.py:169-206)."""
@@ -162,30 +200,36 @@ class JumboLayer:
             self.scale2 = store.handle(store.add(path + ("scale2",), (D,), const_(1e-4), trainable=trainable))
             self.scale3 = store.handle(store.add(path + ("scale3",), (J,), const_(1e-4), trainable=trainable))
 
-    def __call__(self, x, rng=None, det=True, link_in=None, link_out=None):
+    n_droppath = 3  # masks per call, draw order: attention, jumbo, patch FF residual
+
+    @property
+    def droppath_rate(self):
+        return self.cfg.droppath
+
+    def __call__(self, x, rng=None, det=True, link_in=None, link_out=None, masks=None):
         B, S, D = x.shape
         C = self.C
         p = self.cfg.droppath
         if use_fused_blocks() and (self.cfg.dropout <= 0.0 or det):
-            m1 = droppath_mask(p, B, rng, x.device, det)
-            m3 = droppath_mask(p, B, rng, x.device, det)
-            m2 = droppath_mask(p, B, rng, x.device, det)
+            m1 = _mask(masks, 0, p, B, rng, x.device, det)
+            m3 = _mask(masks, 1, p, B, rng, x.device, det)
+            m2 = _mask(masks, 2, p, B, rng, x.device, det)
             return blocks.jumbo_block(self, x, m1, m2, m3, link_in, link_out)
         h = self.norm1(x)
         a = self.attn(h, B, S, rng, det)
-        x = Fn.residual(x, a, self.scale1, droppath_mask(p, B, rng, x.device, det))
+        x = Fn.residual(x, a, self.scale1, _mask(masks, 0, p, B, rng, x.device, det))
 
         # NB: the jumbo residual is added to the *normalized* CLS token (modeling.py:197-199),
         # so the CLS stream is re-normalized by norm3 in every layer.
         cls = x[:, :C].reshape(B, 1, C * D)
         hc = self.norm3(cls, out_dtype=torch.float32)  # [B, J] fp32 residual base
         yc = self.jumbo_mlp(hc.to(self.norm3.g.store.compute_dtype), rng, det)
-        xc = Fn.residual(hc.view(B, 1, C * D), yc, self.scale3, droppath_mask(p, B, rng, x.device, det))
+        xc = Fn.residual(hc.view(B, 1, C * D), yc, self.scale3, _mask(masks, 1, p, B, rng, x.device, det))
 
         pt = x[:, C:]
         hp = self.norm2(pt)
         yp = self.ff(hp, rng, det)
-        xp = Fn.residual(pt, yp, self.scale2, droppath_mask(p, B, rng, x.device, det))
+        xp = Fn.residual(pt, yp, self.scale2, _mask(masks, 2, p, B, rng, x.device, det))
         return torch.cat([xc.view(B, C, D), xp], 1)
 
 
@@ -203,18 +247,25 @@ class ViTLayer:
             self.scale1 = store.handle(store.add(path + ("scale1",), (dim,), const_(1e-4), trainable=trainable))
             self.scale2 = store.handle(store.add(path + ("scale2",), (dim,), const_(1e-4), trainable=trainable))
 
-    def __call__(self, x, rng=None, det=True, link_in=None, link_out=None):
+    n_droppath = 2  # masks per call, draw order: attention, FF residual
+
+    @property
+    def droppath_rate(self):
+        return self.droppath
+
+    def __call__(self, x, rng=None, det=True, link_in=None, link_out=None, masks=None):
         B, S, D = x.shape
+        p = self.droppath
         if use_fused_blocks() and (self.attn.dropout <= 0.0 or det):
-            m1 = droppath_mask(self.droppath, B, rng, x.device, det)
-            m2 = droppath_mask(self.droppath, B, rng, x.device, det)
+            m1 = _mask(masks, 0, p, B, rng, x.device, det)
+            m2 = _mask(masks, 1, p, B, rng, x.device, det)
             return blocks.vit_block(self, x, m1, m2, link_in, link_out)
         h = self.norm1(x)
         a = self.attn(h, B, S, rng, det)
-        x = Fn.residual(x, a, self.scale1, droppath_mask(self.droppath, B, rng, x.device, det))
+        x = Fn.residual(x, a, self.scale1, _mask(masks, 0, p, B, rng, x.device, det))
         h = self.norm2(x)
         f = self.ff(h, rng, det)
-        return Fn.residual(x, f, self.scale2, droppath_mask(self.droppath, B, rng, x.device, det))
+        return Fn.residual(x, f, self.scale2, _mask(masks, 1, p, B, rng, x.device, det))
 
 
 # ------------------------------------------------------------------------------ encoder
@@ -293,9 +344,10 @@ class JumboViT:
 def _run_layers(layers, x, rng, det, grad_ckpt):
     """The layer loop; consecutive fused blocks are chained by ``blocks.Link`` hand-offs (not
     under activation checkpointing, whose recompute would re-run forwards out of order)."""
+    masks = droppath_masks(layers, x.shape[0], rng, x.device, det)
     if grad_ckpt and torch.is_grad_enabled():
-        for layer in layers:
-            x = _checkpointed(layer, x, rng, det)
+        for layer, m in zip(layers, masks):
+            x = _checkpointed(layer, x, rng, det, m)
         return x
     link = None
     for i, layer in enumerate(layers):
@@ -305,12 +357,12 @@ def _run_layers(layers, x, rng, det, grad_ckpt):
             # the upper block's LN1 rides on this block's last residual pass (forward hand-off)
             ln1 = (up.norm1.g, up.norm1.b) if up is not None and blocks.FWD_LINKS else None
             nxt = blocks.Link(ln1)
-        x = layer(x, rng, det, link_in=link, link_out=nxt)
+        x = layer(x, rng, det, link_in=link, link_out=nxt, masks=masks[i])
         link = nxt
     return x
 
 
-def _checkpointed(layer, x, rng, det):
+def _checkpointed(layer, x, rng, det, masks=None):
     """One layer under activation checkpointing (reference ``nn.remat``, modeling.py:232,280).
 
     The recompute in backward must see exactly the forward's random draws: droppath / dropout
@@ -327,13 +379,13 @@ def _checkpointed(layer, x, rng, det):
     def run(inp):
         calls[0] += 1
         if calls[0] == 1:
-            return layer(inp, rng, det)
+            return layer(inp, rng, det, masks=masks)
         g = None
         if rng is not None:
             g = torch.Generator(device=rng.device)
             g.set_state(state)
         with store.uses_suppressed():
-            return layer(inp, g, det)
+            return layer(inp, g, det, masks=masks)
 
     return torch.utils.checkpoint.checkpoint(run, x, use_reentrant=False)
 
