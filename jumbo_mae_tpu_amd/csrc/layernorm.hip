@@ -188,6 +188,11 @@ struct LnResIO {
   int T0;
 };
 
+// parameter-gradient outputs (null entries skipped): dgamma, dbeta, dscale, dbias
+struct ParamOuts {
+  float* p[4];
+};
+
 // partial rows in ws: [dgamma | dbeta] (NP = 2) or [dgamma | dbeta | dscale | dbias] (NP = 4)
 // LA (LDS accumulation): the per-column parameter partials are added into the block's LDS row
 // with ds_add_f32 instead of living in registers across the row loop (64 fewer VGPRs at D=1024:
@@ -200,7 +205,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const TI* __restrict__ dy, 
                                                      long sB, long sT, int T, int rows, int D,
                                                      const float* __restrict__ mean, const float* __restrict__ rstd,
                                                      const float* __restrict__ gamma, LnBwdIO io, LnResIO rio,
-                                                     float* __restrict__ ws, int accum_params) {
+                                                     float* __restrict__ ws, int accum_params, ParamOuts outs) {
   JM_DGUARD(blockDim.x == 256 && D % 4 == 0 && D <= V * 256);
   constexpr int NP = RES ? 4 : 2;
   constexpr int NA = LA ? 1 : NP;  // register accumulators kept (dummy when LA)
@@ -303,8 +308,17 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const TI* __restrict__ dy, 
     }
   }
   if (!partials) return;
+  // ws == null: the block's sums go straight into the outputs with float atomics, one 256-B row
+  // segment per wave-instruction (no workspace round trip, no ln_param_reduce launch)
+  auto direct = [&]() {
+    for (int i = threadIdx.x; i < NP * D; i += 256) {
+      float* dst = outs.p[i / D];
+      if (dst != nullptr) atomicAdd(&dst[i - (i / D) * D], red[i]);
+    }
+  };
   if constexpr (LA) {
     __syncthreads();
+    if (ws == nullptr) return direct();
     for (int i = threadIdx.x * 4; i < NP * D; i += 256 * 4) {
       float a[4];
       load4(red + i, a);
@@ -333,6 +347,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const TI* __restrict__ dy, 
     }
     __syncthreads();
   }
+  if (ws == nullptr) return direct();
   for (int i = threadIdx.x * 4; i < NP * D; i += 256 * 4) {
     float a[4];
     load4(red + i, a);
@@ -481,31 +496,59 @@ __global__ __launch_bounds__(256) void ln_bwd_pf_kernel(const TI* __restrict__ d
 
 // out_k[c] += sum_b ws[b][k*D + c] for the NP partial vectors (null outputs skipped); grid.y
 // splits the partial rows.
-struct ParamOuts {
-  float* p[4];
-};
 
 __global__ __launch_bounds__(256) void ln_param_reduce_kernel(const float* __restrict__ ws, int nb, int D, int NP,
                                                               ParamOuts outs) {
-  const int i = blockIdx.x * 256 + threadIdx.x;
-  if (i >= NP * D) return;
-  float* dst = outs.p[i / D];
-  if (dst == nullptr) return;
+  // one float4 of columns per thread while loading (the whole 4-8 MB workspace in flight at once:
+  // the r1 one-float-per-thread form ran at ~1 TB/s, 8.7 us per call, 90 calls per ViT-L step);
+  // the sums are transposed through LDS so each atomic wave-instruction covers 256 contiguous
+  // bytes (a 16-B lane stride made the adds 4x the requests and the kernel slower than r1's)
+  __shared__ float red[1024];
+  const int i4 = blockIdx.x * 256 + threadIdx.x;
   const long ld = (long)NP * D;
   const int per = (nb + gridDim.y - 1) / gridDim.y;
   const int b0 = blockIdx.y * per;
   int b1 = b0 + per;
   if (b1 > nb) b1 = nb;
-  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
-  int b = b0;
-  for (; b + 3 < b1; b += 4) {
-    s0 += ws[(long)b * ld + i];
-    s1 += ws[(long)(b + 1) * ld + i];
-    s2 += ws[(long)(b + 2) * ld + i];
-    s3 += ws[(long)(b + 3) * ld + i];
+  float s[2][4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+  if (i4 * 4 < NP * D) {
+    int b = b0;
+    for (; b + 1 < b1; b += 2) {
+      float a[4], c[4];
+      load4(ws + (long)b * ld + i4 * 4, a);
+      load4(ws + (long)(b + 1) * ld + i4 * 4, c);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        s[0][j] += a[j];
+        s[1][j] += c[j];
+      }
+    }
+    if (b < b1) {
+      float a[4];
+      load4(ws + (long)b * ld + i4 * 4, a);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) s[0][j] += a[j];
+    }
   }
-  for (; b < b1; ++b) s0 += ws[(long)b * ld + i];
-  atomicAdd(&dst[i % D], (s0 + s1) + (s2 + s3));
+  float o[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) o[j] = s[0][j] + s[1][j];
+  store4(red + threadIdx.x * 4, o);
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int col = blockIdx.x * 1024 + j * 256 + threadIdx.x;
+    if (col >= NP * D) continue;
+    float* dst = outs.p[col / D];
+    if (dst != nullptr) atomicAdd(&dst[col % D], red[j * 256 + threadIdx.x]);
+  }
+}
+
+// grid for ln_param_reduce_kernel over nb partial rows of NP * D floats: ~8 rows per thread
+dim3 param_reduce_grid(int nb, int D, int NP) {
+  int ys = (nb + 7) / 8;
+  if (ys < 1) ys = 1;
+  return dim3((NP * D / 4 + 255) / 256, ys);
 }
 
 template <typename TO>
@@ -675,24 +718,30 @@ bool use_wide(int rows, int D) { return D > 1024 && rows <= LN_WIDE_MAX_ROWS && 
 // partials + early dres load: 97.96 -> 97.75 ms/step (profiles/r1_ab_ln_bwd_early_dres.txt);
 // 3 = 2 + the next row's loads issued before this row's math (ln_bwd_pf_kernel)
 int g_ln_bwd_la = 2;
+// LN backward parameter partials: 1 = float atomics from each block straight into the outputs,
+// 0 = per-block workspace rows + ln_param_reduce_kernel (default: the direct form measured the
+// same step time, ViT-L 94.05 vs 93.90 ms in one process -- 512 adders per address cost what the
+// reduce launch did; profiles/r2_ln_param_reduce.txt)
+int g_ln_direct = 0;
 
 template <typename TI, bool RES>
 void launch_bwd(int V, dim3 grid, size_t smem, hipStream_t st, const TI* dy, const float* x, long sB, long sT,
                 int T, int rows, int D, const float* m, const float* r, const float* g, LnBwdIO dx, LnResIO rio,
-                float* ws, int acc) {
+                float* ws, int acc, ParamOuts outs) {
 #define JM_LNB(VV)                                                                                          \
   case VV:                                                                                                  \
     if (g_ln_bwd_la == 1 && VV >= 2 && VV <= 4)                                                             \
       ln_bwd_kernel<VV, TI, RES, true><<<grid, 256, smem, st>>>(dy, x, sB, sT, T, rows, D, m, r, g, dx, rio, ws, \
-                                                                 acc);                                     \
+                                                                 acc, outs);                                   \
     else if (g_ln_bwd_la == 3 && VV >= 2 && VV <= 4)                                                        \
       ln_bwd_pf_kernel<VV, TI, RES><<<grid, 256, smem, st>>>(dy, x, sB, sT, T, rows, D, m, r, g, dx, rio, ws,   \
                                                              acc);                                          \
     else if (g_ln_bwd_la == 2 && VV >= 2 && VV <= 4)                                                        \
       ln_bwd_kernel<VV, TI, RES, false, true><<<grid, 256, smem, st>>>(dy, x, sB, sT, T, rows, D, m, r, g, dx, \
-                                                                        rio, ws, acc);                      \
+                                                                        rio, ws, acc, outs);                \
     else                                                                                                    \
-      ln_bwd_kernel<VV, TI, RES><<<grid, 256, smem, st>>>(dy, x, sB, sT, T, rows, D, m, r, g, dx, rio, ws, acc); \
+      ln_bwd_kernel<VV, TI, RES><<<grid, 256, smem, st>>>(dy, x, sB, sT, T, rows, D, m, r, g, dx, rio, ws, acc, \
+                                                          outs);                                             \
     break;
   switch (V) {
     JM_LNB(1) JM_LNB(2) JM_LNB(3) JM_LNB(4) JM_LNB(6) JM_LNB(8) JM_LNB(9) JM_LNB(12) JM_LNB(16)
@@ -762,6 +811,7 @@ int jm_residual_ln_fwd(const float* x, long sB, long sT, const uint16_t* y, cons
 }
 
 void jm_ln_set_bwd_la(int v) { g_ln_bwd_la = v; }
+void jm_ln_set_direct(int v) { g_ln_direct = v; }
 
 // runtime switch: most row-loop blocks of the (non-wide) LN backward
 int g_ln_bwd_blocks = 512;  // = 2 resident blocks per CU (2 waves / SIMD): one round, half the partials of 1024 (-0.3 ms/step, profiles/r2_ln_bwd_blocks.txt)
@@ -803,35 +853,35 @@ int jm_layernorm_bwd(const void* dy, int dy_bf16, const float* x, long sB, long 
 #undef JM_LNBW
     if (accum_params) {
       ParamOuts outs{{dgamma, dbeta, nullptr, nullptr}};
-      const int ysplit = nb >= 64 ? 16 : 1;
-      ln_param_reduce_kernel<<<dim3((2 * D + 255) / 256, ysplit), 256, 0, st>>>(ws, nb, D, 2, outs);
+      ln_param_reduce_kernel<<<param_reduce_grid(nb, D, 2), 256, 0, st>>>(ws, nb, D, 2, outs);
     }
     return 0;
   }
   const size_t smem = partials ? NP * D * sizeof(float) : 0;
+  const ParamOuts outs{{accum_params ? dgamma : nullptr, accum_params ? dbeta : nullptr,
+                        res ? res->dscale : nullptr, res ? res->dbias : nullptr}};
+  // direct atomics (the prefetch variant keeps the workspace + reduce form)
+  const bool direct = g_ln_direct && g_ln_bwd_la != 3;
+  float* wsk = direct ? nullptr : ws;
   LnResIO rio{nullptr, nullptr, 0, 0, nullptr, nullptr, 0};
   if (res) rio = LnResIO{res->y, res->dy, res->yB, res->yT, res->scale, res->mask, res->T0};
   if (dy_bf16) {
     if (res)
       launch_bwd<uint16_t, true>(V, grid, smem, st, (const uint16_t*)dy, x, sB, sT, T, rows, D, mean, rstd, gamma,
-                                 dx, rio, ws, accum_params);
+                                 dx, rio, wsk, accum_params, outs);
     else
       launch_bwd<uint16_t, false>(V, grid, smem, st, (const uint16_t*)dy, x, sB, sT, T, rows, D, mean, rstd, gamma,
-                                  dx, rio, ws, accum_params);
+                                  dx, rio, wsk, accum_params, outs);
   } else {
     if (res)
       launch_bwd<float, true>(V, grid, smem, st, (const float*)dy, x, sB, sT, T, rows, D, mean, rstd, gamma, dx, rio,
-                              ws, accum_params);
+                              wsk, accum_params, outs);
     else
       launch_bwd<float, false>(V, grid, smem, st, (const float*)dy, x, sB, sT, T, rows, D, mean, rstd, gamma, dx, rio,
-                               ws, accum_params);
+                               wsk, accum_params, outs);
   }
-  if (partials) {
-    ParamOuts outs{{accum_params ? dgamma : nullptr, accum_params ? dbeta : nullptr,
-                    res ? res->dscale : nullptr, res ? res->dbias : nullptr}};
-    const int ysplit = nb >= 64 ? 16 : 1;
-    ln_param_reduce_kernel<<<dim3((NP * D + 255) / 256, ysplit), 256, 0, st>>>(ws, nb, D, NP, outs);
-  }
+  if (partials && !direct)
+    ln_param_reduce_kernel<<<param_reduce_grid(nb, D, NP), 256, 0, st>>>(ws, nb, D, NP, outs);
   return 0;
 }
 

@@ -25,6 +25,7 @@ def _reset_gemm_variant(request):
         request.getfixturevalue("ext").gemm_tn_set_variant(4)
         request.getfixturevalue("ext").gemm_set_tail(1)
         request.getfixturevalue("ext").attn_set_bwd2_db(0)
+        request.getfixturevalue("ext").ln_set_direct(0)
 
 
 def rel(a, b):
@@ -361,10 +362,13 @@ def test_gemm_nt_splitk(ext, M, N, K, S, variant):
 @pytest.mark.parametrize("T0,view_y,with_scale", [(0, False, True), (3, False, True), (0, True, True),
                                                   (3, True, False)])
 @pytest.mark.parametrize("la", [3, 2, 1, 0])
-def test_layernorm_bwd_fused_residual(ext, T0, view_y, with_scale, la):
-    ext.ln_set_bwd_la(la)
+@pytest.mark.parametrize("direct", [1, 0])
+def test_layernorm_bwd_fused_residual(ext, T0, view_y, with_scale, la, direct):
     """LN backward with the consumer's residual backward fused in == layernorm_bwd followed by
-    residual_bwd on the rows t >= T0 (y as a contiguous slab or a strided view into a buffer)."""
+    residual_bwd on the rows t >= T0 (y as a contiguous slab or a strided view into a buffer);
+    direct = parameter partials as float atomics from each block (1) or workspace + reduce (0)."""
+    ext.ln_set_bwd_la(la)
+    ext.ln_set_direct(direct)
     torch.manual_seed(0)
     B, T, D = 6, 52, 1024
     x = torch.randn(B, T, D, device="cuda") * 2
