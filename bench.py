@@ -148,11 +148,16 @@ def main():
 
     if args.profile_steps > 0 and info.is_main:
         from torch.profiler import ProfilerActivity, profile
-        with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA]) as prof:
+        stacks = os.environ.get("JMAE_PROF_STACK", "")  # e.g. "aten::copy_,aten::cat": where they come from
+        with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], with_stack=bool(stacks)) as prof:
             for _ in range(args.profile_steps):
                 step()
             sync()
         log(prof.key_averages().table(sort_by="cuda_time_total", row_limit=150))
+        if stacks:
+            for ev in prof.key_averages(group_by_stack_n=6):
+                if ev.key in stacks.split(","):
+                    log(f"{ev.key} x{ev.count} {ev.device_time_total:.0f}us <- " + " | ".join(ev.stack[:6]))
 
     ms = elapsed / args.steps * 1000.0
     value = global_batch * args.steps / elapsed
