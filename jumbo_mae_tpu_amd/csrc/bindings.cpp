@@ -22,6 +22,13 @@ void jm_ln_set_direct(int v);
 // debug build (-DJM_DEBUG): first failing soft-check line per kernel translation unit (0 = none;
 // reading clears it); always 0 in the release build
 int jm_debug_line_attention();
+int jm_debug_line_dropout();
+int jm_dropout_apply(const void* x, void* y, long n, int bf16, const int64_t* seed, uint32_t thr, float scale,
+                     hipStream_t st);
+int jm_softmax_dropout_fwd(const float* z, float* p, float* pd, long rows, int S, const int64_t* seed, uint32_t thr,
+                           float scale, hipStream_t st);
+int jm_softmax_dropout_bwd(const float* dpd, const float* p, float* dz, long rows, int S, const int64_t* seed,
+                           uint32_t thr, float scale, hipStream_t st);
 int jm_debug_line_elementwise();
 int jm_debug_line_gemm();
 int jm_debug_line_gemm_tn();
@@ -687,6 +694,64 @@ torch::Tensor gemm_nt_dgelu(torch::Tensor A, torch::Tensor B, torch::Tensor pre,
   return out;
 }
 
+// ---------------------------------------------------------------- dropout (csrc/dropout.hip)
+// keep threshold on the top 24 hash bits and the 1/keep scale of a drop rate in [0, 1)
+static std::pair<uint32_t, float> keep_params(double rate) {
+  TORCH_CHECK(rate >= 0.0 && rate < 1.0, "dropout rate must be in [0, 1)");
+  const double keep = 1.0 - rate;
+  return {(uint32_t)std::llround(keep * 16777216.0), (float)(1.0 / keep)};
+}
+
+static void check_seed(const torch::Tensor& seed, const torch::Tensor& like) {
+  TORCH_CHECK(seed.scalar_type() == torch::kInt64 && seed.numel() == 1 && seed.device() == like.device(),
+              "dropout seed: int64 [1] on the data's device");
+}
+
+// y = x * keep(seed, i) / keep  (bf16 or fp32, contiguous, numel % 8 == 0); also its own backward
+torch::Tensor dropout_apply(torch::Tensor x, torch::Tensor seed, double rate) {
+  CHECK_CONTIG(x);
+  check_seed(seed, x);
+  TORCH_CHECK(x.scalar_type() == torch::kBFloat16 || x.scalar_type() == torch::kFloat32, "dropout: bf16 / fp32");
+  TORCH_CHECK(x.numel() % 8 == 0, "dropout: numel % 8");
+  auto [thr, scale] = keep_params(rate);
+  auto y = torch::empty_like(x);
+  check_rc(jm_dropout_apply(x.data_ptr(), y.data_ptr(), x.numel(), x.scalar_type() == torch::kBFloat16,
+                            seed.data_ptr<int64_t>(), thr, scale, stream()),
+           "dropout_apply");
+  return y;
+}
+
+// rows of fp32 logits [..., S] -> (softmax p (saved for the backward), dropped p * mask / keep)
+std::vector<torch::Tensor> softmax_dropout_fwd(torch::Tensor z, torch::Tensor seed, double rate) {
+  CHECK_CONTIG(z);
+  CHECK_DT(z, torch::kFloat32);
+  check_seed(seed, z);
+  auto [thr, scale] = keep_params(rate);
+  const int S = z.size(-1);
+  auto p = torch::empty_like(z);
+  auto pd = torch::empty_like(z);
+  check_rc(jm_softmax_dropout_fwd(z.data_ptr<float>(), p.data_ptr<float>(), pd.data_ptr<float>(), z.numel() / S, S,
+                                  seed.data_ptr<int64_t>(), thr, scale, stream()),
+           "softmax_dropout_fwd");
+  return {p, pd};
+}
+
+torch::Tensor softmax_dropout_bwd(torch::Tensor dpd, torch::Tensor p, torch::Tensor seed, double rate) {
+  CHECK_CONTIG(dpd);
+  CHECK_CONTIG(p);
+  CHECK_DT(dpd, torch::kFloat32);
+  CHECK_DT(p, torch::kFloat32);
+  TORCH_CHECK(dpd.sizes() == p.sizes(), "softmax_dropout_bwd shapes");
+  check_seed(seed, p);
+  auto [thr, scale] = keep_params(rate);
+  const int S = p.size(-1);
+  auto dz = torch::empty_like(p);
+  check_rc(jm_softmax_dropout_bwd(dpd.data_ptr<float>(), p.data_ptr<float>(), dz.data_ptr<float>(), p.numel() / S, S,
+                                  seed.data_ptr<int64_t>(), thr, scale, stream()),
+           "softmax_dropout_bwd");
+  return dz;
+}
+
 // dst [C, R] = src [R, C]^T (bf16, both contiguous)
 void transpose_bf16(torch::Tensor src, torch::Tensor dst) {
   CHECK_CONTIG(src);
@@ -807,7 +872,8 @@ std::vector<torch::Tensor> residual_ln_fwd(torch::Tensor x, torch::Tensor y, c10
 py::dict debug_lines() {
   py::dict d;
   const std::pair<const char*, int (*)()> tus[] = {
-      {"attention", jm_debug_line_attention}, {"elementwise", jm_debug_line_elementwise},
+      {"attention", jm_debug_line_attention}, {"dropout", jm_debug_line_dropout},
+      {"elementwise", jm_debug_line_elementwise},
       {"gemm", jm_debug_line_gemm},           {"gemm_tn", jm_debug_line_gemm_tn},
       {"layernorm", jm_debug_line_layernorm}, {"mae", jm_debug_line_mae},
       {"optim", jm_debug_line_optim}};
@@ -830,6 +896,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("res_mask") = py::none(), py::arg("res_dscale") = py::none(), py::arg("res_dbias") = py::none(),
         py::arg("res_T0") = 0, py::arg("res_out") = py::none());
   m.def("gelu_fwd", &gelu_fwd);
+  m.def("dropout_apply", &dropout_apply);
+  m.def("softmax_dropout_fwd", &softmax_dropout_fwd);
+  m.def("softmax_dropout_bwd", &softmax_dropout_bwd);
   m.def("gelu_bwd", &gelu_bwd, py::arg("h"), py::arg("da"), py::arg("bias_grad") = py::none(),
         py::arg("deriv") = false);
   m.def("colsum", &colsum);

@@ -26,6 +26,7 @@ import torch
 
 from ..config import DecoderConfig, ViTConfig
 from ..ops import blocks
+from ..ops import dropout as Dr
 from ..ops import functional as Fn
 from ..ops import mae as mae_ops
 from ..utils.posemb import fixed_sincos2d_embeddings
@@ -115,21 +116,22 @@ class Attention:
 
 
 def _dropout(x, rate, rng, det):
+    """Flax nn.Dropout (train mode): hash-mask HIP kernel, mask regenerated in backward (ops/dropout.py)."""
     if rate <= 0.0 or det:
         return x
-    keep = 1.0 - rate
-    m = torch.rand(x.shape, generator=rng, device=x.device) < keep
-    return torch.where(m, x / keep, torch.zeros_like(x))
+    return Dr.dropout(x, rate, rng)
 
 
 def _attention_with_dropout(qkv, heads, rate, rng):
-    """Rare path (all presets use dropout 0): unfused attention with dropout on the probs."""
+    """Attention with dropout on the probabilities (all presets use dropout 0): the two batched
+    products on the BLAS library in fp32, softmax + dropout (and its backward) as one fused HIP
+    row kernel each way -- the whole-sequence attention kernels never materialise P."""
     B, S, three_d = qkv.shape
     D = three_d // 3
     hd = D // heads
     q, k, v = qkv.view(B, S, 3, heads, hd).unbind(2)
     z = torch.einsum("bqhd,bkhd->bhqk", q.float() / math.sqrt(hd), k.float())
-    p = _dropout(torch.softmax(z, -1), rate, rng, False)
+    p = Dr.softmax_dropout(z, rate, rng)
     return torch.einsum("bhqk,bkhd->bqhd", p, v.float()).reshape(B, S, D).to(qkv.dtype)
 
 
