@@ -202,6 +202,15 @@ void launch_rowcol(const void* in0, const uint16_t* in1, uint16_t* out, float* a
   const int rps = 256 / tpr;
   int rows_per_block = rps * 16;
   int nb = (M + rows_per_block - 1) / rows_per_block;
+  // few rows (the jumbo residual / GELU backward: 512 x 3072 / 512 x 12288, the CLS-row residual:
+  // 1536 x 1024): spread over >= 256 blocks in total, one per CU -- 16 rows per slot gave 48-192
+  // blocks and a latency-bound 16-20 us per call
+  const int want = (256 + ncol - 1) / ncol;
+  if (nb < want) {
+    rows_per_block = (M + want - 1) / want;
+    if (rows_per_block < rps) rows_per_block = rps;
+    nb = (M + rows_per_block - 1) / rows_per_block;
+  }
   const int cap = 2048 / ncol > 1 ? 2048 / ncol : 1;
   if (nb > cap) {
     nb = cap;
