@@ -65,6 +65,7 @@ int jm_attn_bwd_part_rows(int B, int S, int hd);
 int jm_attn_bwd_long(const uint16_t* qkv, const uint16_t* o, const uint16_t* dO, const float* lse, uint16_t* dqkv,
                      float* delta, int B, int S, int H, int hd, hipStream_t st);
 void jm_opt_sumsq(const float* x, const int* chunks, int nchunks, float* out, hipStream_t st);
+void jm_opt_set_adamw_vec(int v);
 void jm_opt_adamw(float* p, const float* g, float* mu, float* nu, uint16_t* shadow, const int* chunks, int nchunks,
                   const float* meta, const float* hyper, const float* gnorm_sq, hipStream_t st);
 void jm_opt_lamb_phase1(const float* p, const float* g, float* mu, float* nu, float* u, const int* chunks, int nchunks,
@@ -942,6 +943,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("attn_set_bwd2_db", &jm_attn_set_bwd2_db);
   m.def("opt_sumsq", &opt_sumsq);
   m.def("opt_adamw", &opt_adamw);
+  m.def("opt_set_adamw_vec", &jm_opt_set_adamw_vec);
   m.def("opt_lamb_phase1", &opt_lamb_phase1);
   m.def("opt_lars_norms", &opt_lars_norms);
   m.def("opt_apply_trust", &opt_apply_trust);

@@ -44,6 +44,9 @@ def apply(P, cfg: str):
         elif k == "LN_BWD_BLOCKS":
             from jumbo_mae_tpu_amd.ops import _ext
             _ext.load(True).ln_set_bwd_blocks(int(v))
+        elif k == "ADAMW_VEC":
+            from jumbo_mae_tpu_amd.ops import _ext
+            _ext.load(True).opt_set_adamw_vec(int(v))
         elif k == "LN_DIRECT":
             from jumbo_mae_tpu_amd.ops import _ext
             _ext.load(True).ln_set_direct(int(v))
