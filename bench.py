@@ -92,7 +92,7 @@ def main():
                         num_layers=vc.layers)
     rdt = torch.bfloat16 if args.reduce_dtype == "bf16" else torch.float32
     reducer = (GradReducer(store, bucket_mb=args.bucket_mb, overlap=not args.no_overlap, reduce_dtype=rdt)
-               if world > 1 else None)
+               if world > 1 or pdist.forced_group() else None)
     rngs = RngStreams({"noise": 0, "dropout": 0, "mixup": 0}, info.rank, dev)
     trainer = Trainer(model, opt, reducer, rngs, grad_accum=args.grad_accum)
     from jumbo_mae_tpu_amd.runtime.graph import StepRunner
@@ -145,6 +145,7 @@ def main():
     # region): spread of a weight checksum over the ranks, 0.0 when in sync
     spread = pdist.all_reduce_max_scalar(float(store.master.double().abs().sum()), dev) - \
         -pdist.all_reduce_max_scalar(-float(store.master.double().abs().sum()), dev) if world > 1 else 0.0
+    weight_checksum = float(store.master.double().abs().sum())
 
     if args.profile_steps > 0 and info.is_main:
         from torch.profiler import ProfilerActivity, profile
@@ -178,7 +179,8 @@ def main():
             # GPU time of the last step behind the DP reduction wait (exposed comm + overlapped
             # bucket updates); null on one GPU
             "exposed_comm_ms_last_step": None if comm_ms is None else round(comm_ms, 3),
-            "replica_weight_checksum_spread": spread,
+            "replica_weight_checksum_spread": spread, "weight_checksum": weight_checksum,
+            "reducer": reducer.stats() if reducer is not None else None,
             "dtype": "fp32" if args.cpu else "bf16",
             "data": f"synthetic uint8 {S}x{S} images on {'CPU' if args.cpu else 'GPU'}, random-init weights",
             "config": {

@@ -92,6 +92,8 @@ int jm_gemm_tn(const uint16_t* A, long lda, const uint16_t* B, long ldb, int M, 
                float* G, long ldo, float* partial, hipStream_t st);
 int jm_gemm_tn_acc0();
 void jm_gemm_tn_set_acc0(int v);
+int jm_gemm_tn_atomic();
+void jm_gemm_tn_set_atomic(int v);
 void jm_gemm_tn_set_variant(int v);
 struct TnSegs {
   const uint16_t* a[32];
@@ -787,12 +789,13 @@ int64_t gemm_tn_wgrad(torch::Tensor dy, torch::Tensor x, torch::Tensor g) {
   int S = 1;
   const int sps = jm_gemm_tn_plan(M, N, K, &S);
   torch::Tensor part;
-  const int SP = S - jm_gemm_tn_acc0();  // partial slices (split 0 may accumulate into g directly)
-  if (S > 1) part = torch::empty({SP, (long)N * K}, g.options());
+  // partial slices (split 0 may accumulate into g directly; none when the splits add atomically)
+  const int SP = jm_gemm_tn_atomic() ? 0 : S - jm_gemm_tn_acc0();
+  if (S > 1 && SP > 0) part = torch::empty({SP, (long)N * K}, g.options());
   check_rc(jm_gemm_tn(bf(dy), dy.stride(0), bf(x), x.stride(0), M, N, K, sps, S, g.data_ptr<float>(), K,
-                      S > 1 ? part.data_ptr<float>() : nullptr, stream()),
+                      S > 1 && SP > 0 ? part.data_ptr<float>() : nullptr, stream()),
            "gemm_tn_wgrad");
-  if (S > 1) check_rc(jm_splitk_reduce_add(part.data_ptr<float>(), g.data_ptr<float>(), (long)N * K, SP, stream()),
+  if (S > 1 && SP > 0) check_rc(jm_splitk_reduce_add(part.data_ptr<float>(), g.data_ptr<float>(), (long)N * K, SP, stream()),
                       "gemm_tn_wgrad reduce");
   return S;
 }
@@ -824,12 +827,12 @@ int64_t gemm_tn_wgrad_seg(std::vector<torch::Tensor> dys, std::vector<torch::Ten
   int S = 1;
   const int sps = jm_gemm_tn_plan(M, N, K, &S);
   torch::Tensor part;
-  const int SP = S - jm_gemm_tn_acc0();
-  if (S > 1) part = torch::empty({SP, (long)N * K}, g.options());
+  const int SP = (jm_gemm_tn_atomic() && rows % 64 == 0) ? 0 : S - jm_gemm_tn_acc0();
+  if (S > 1 && SP > 0) part = torch::empty({SP, (long)N * K}, g.options());
   check_rc(jm_gemm_tn_seg(segs, d0.stride(0), x0.stride(0), N, K, sps, S, g.data_ptr<float>(), K,
-                          S > 1 ? part.data_ptr<float>() : nullptr, stream()),
+                          S > 1 && SP > 0 ? part.data_ptr<float>() : nullptr, stream()),
            "gemm_tn_wgrad_seg");
-  if (S > 1) check_rc(jm_splitk_reduce_add(part.data_ptr<float>(), g.data_ptr<float>(), (long)N * K, SP, stream()),
+  if (S > 1 && SP > 0) check_rc(jm_splitk_reduce_add(part.data_ptr<float>(), g.data_ptr<float>(), (long)N * K, SP, stream()),
                       "gemm_tn_wgrad_seg reduce");
   return S;
 }
@@ -926,6 +929,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_set_pp", &jm_gemm_set_pp, "persistent overlapped NT launch for multi-round grids (1, default) or tiled (0)");
   m.def("gemm_set_sk", &jm_gemm_set_sk, "persistent DP + stream-K NT launches where they pay (1, default) or never (0)");
   m.def("gemm_tn_set_acc0", &jm_gemm_tn_set_acc0);
+  m.def("gemm_tn_set_atomic", &jm_gemm_tn_set_atomic);
   m.def("gemm_tn_set_variant", &jm_gemm_tn_set_variant, "TN wgrad kernel: 4 = 4-phase (default), 0 = r1 32-row steps");
   m.def("gemm_nt_splitk", &gemm_nt_splitk, py::arg("A"), py::arg("B"), py::arg("bias") = py::none(),
         py::arg("splits") = 8, py::arg("add") = py::none());

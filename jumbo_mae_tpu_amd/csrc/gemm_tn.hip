@@ -479,6 +479,41 @@ __global__ __launch_bounds__(NTH, 1) void gemm_tn4_kernel(const uint16_t* __rest
   ktile(K0{}, t + 1, bq, bp);
 
   // ---- epilogue: acc[mt][nt][i] = G[n0 + wr*128 + mt*16 + l16][k0 + wc*64 + nt*16 + 4g + i]
+  if constexpr (ACC == 2) {
+    // atomic split reduction (jm_gemm_tn_set_atomic): every split adds its tile into G (out, ldo)
+    // with float atomics -- no fp32 partial slices, no reduce pass.  The tile is restaged through
+    // the (drained) ring in two 128-row halves, [128][256] fp32 = 128 KB, 16-byte chunks XOR-
+    // swizzled by (row & 15), so each wave-wide atomic covers 64 consecutive floats (256 B) of one
+    // G row instead of 16 rows x 4 scattered floats.
+    float* cs = reinterpret_cast<float*>(smem);
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      __syncthreads();
+      if (wr == h) {
+#pragma unroll
+        for (int mt = 0; mt < 8; ++mt) {
+          const int r = mt * 16 + l16;
+#pragma unroll
+          for (int nt = 0; nt < 4; ++nt) {
+            const int chunk = ((wc * 64 + nt * 16) >> 2) + g;
+            float v[4] = {acc[mt][nt][0], acc[mt][nt][1], acc[mt][nt][2], acc[mt][nt][3]};
+            store4(cs + r * 256 + ((chunk ^ (r & 15)) << 2), v);
+          }
+        }
+      }
+      __syncthreads();
+      for (int r = wave; r < 128; r += 8) {
+        float* grow = out + (long)(n0 + h * 128 + r) * ldo + k0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int col = j * 64 + lane;
+          unsafeAtomicAdd(grow + col, cs[r * 256 + ((((col >> 2) ^ (r & 15))) << 2) + (col & 3)]);
+        }
+      }
+    }
+    return;
+  }
   const bool to_g = !ACC && g0 != nullptr && split == 0;  // workgroup-uniform
   float* dst = ACC ? out : to_g ? g0 : out + (long)(g0 != nullptr ? split - 1 : split) * split_stride;
   const long ld = to_g ? ldg0 : ldo;
@@ -507,6 +542,7 @@ size_t jm_gemm_tn_smem() { return (size_t)NST * STAGE * sizeof(uint16_t); }
 // Split of the M range: returns steps (of 32 rows) per split; *S_out = number of splits.
 // Picks the split count that minimises an estimate of (waves of 256 CUs) x (steps per split +
 // epilogue) + the fp32 partial-tile traffic of the reduction.
+int g_tn_atomic = 0;
 int g_tn4 = 1;  // A/B: 4-phase TN kernel (default) vs the r1 32-row-step kernel (jm_gemm_tn_set_variant)
 void jm_gemm_tn_set_variant(int v) { g_tn4 = v == 4; }
 
@@ -524,7 +560,8 @@ int jm_gemm_tn_plan(int M, int N, int K, int* S_out) {
     const long wgs = (long)tiles * s_eff;
     const long waves = (wgs + 255) / 256;
     const double t_steps = (double)waves * (sps + 12);                       // ~1 us per step
-    const double t_red = s_eff > 1 ? (double)s_eff * N * K * 8.0 / 5.0e12 * 1e6 : 0.0;  // us
+    double t_red = s_eff > 1 ? (double)s_eff * N * K * 8.0 / 5.0e12 * 1e6 : 0.0;  // us
+    if (g_tn_atomic >= 2) t_red /= (double)(1 << (g_tn_atomic - 1));  // A/B: atomics priced lower
     const double est = t_steps + t_red;
     if (est < best) {
       best = est;
@@ -544,6 +581,12 @@ int g_tn_acc0 = 0;
 int jm_gemm_tn_acc0() { return g_tn_acc0; }
 void jm_gemm_tn_set_acc0(int v) { g_tn_acc0 = v; }
 
+// A/B: split reduction by float atomics into G from the 4-phase kernel's epilogue (ACC = 2) instead
+// of fp32 partial slices + jm_splitk_reduce_add.  Summation order then varies from run to run.
+// Values >= 2 also price the split reduction 2^(v-1) x cheaper in jm_gemm_tn_plan (more splits).
+int jm_gemm_tn_atomic() { return g_tn_atomic && g_tn4; }
+void jm_gemm_tn_set_atomic(int v) { g_tn_atomic = v; }
+
 // partial: [S][N][K] fp32 (or [S - 1][N][K] when jm_gemm_tn_acc0())
 int jm_gemm_tn(const uint16_t* A, long lda, const uint16_t* B, long ldb, int M, int N, int K, int sps, int S,
                float* G, long ldo, float* partial, hipStream_t st) {
@@ -560,6 +603,14 @@ int jm_gemm_tn(const uint16_t* A, long lda, const uint16_t* B, long ldb, int M, 
         attr = true;
       }
       gemm_tn4_kernel<1, false><<<tiles, NTH, sm, st>>>(A, lda, B, ldb, M, N, K, sps, G, ldo, 0);
+    } else if (g_tn_atomic && partial == nullptr) {
+      static bool attr = false;
+      if (!attr) {
+        (void)hipFuncSetAttribute((const void*)gemm_tn4_kernel<2, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)sm);
+        attr = true;
+      }
+      gemm_tn4_kernel<2, false><<<tiles * S, NTH, sm, st>>>(A, lda, B, ldb, M, N, K, sps, G, ldo, 0);
     } else {
       if (partial == nullptr) return -3;
       static bool attr = false;
@@ -610,6 +661,14 @@ int jm_gemm_tn_seg(const TnSegs& segs, long lda, long ldb, int N, int K, int sps
         attr = true;
       }
       gemm_tn4_kernel<1, true><<<tiles, NTH, sm, st>>>(nullptr, lda, nullptr, ldb, M, N, K, sps, G, ldo, 0, segs);
+    } else if (g_tn_atomic && partial == nullptr) {
+      static bool attr = false;
+      if (!attr) {
+        (void)hipFuncSetAttribute((const void*)gemm_tn4_kernel<2, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)sm);
+        attr = true;
+      }
+      gemm_tn4_kernel<2, true><<<tiles * S, NTH, sm, st>>>(nullptr, lda, nullptr, ldb, M, N, K, sps, G, ldo, 0, segs);
     } else {
       if (partial == nullptr) return -3;
       static bool attr = false;

@@ -41,7 +41,9 @@ class GradReducer:
         self.store = store
         self.group = group
         self.world = dist.get_world_size(group) if (dist.is_available() and dist.is_initialized()) else 1
-        self.enabled = self.world > 1
+        from .dist import forced_group
+
+        self.enabled = self.world > 1 or (forced_group() and dist.is_available() and dist.is_initialized())
         self.overlap = overlap and self.enabled
         self.sync = True
         self.reduce_dtype = reduce_dtype

@@ -53,7 +53,7 @@ def init_distributed(device: str | None = None, timeout_s: int = 1800) -> DistIn
     else:
         dev = torch.device("cpu")
     backend = None
-    if world > 1 and not dist.is_initialized():
+    if (world > 1 or forced_group()) and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29500")
         backend = "nccl" if use_gpu else "gloo"
@@ -65,6 +65,15 @@ def init_distributed(device: str | None = None, timeout_s: int = 1800) -> DistIn
         backend = dist.get_backend()
     _INFO = DistInfo(rank, world, local, dev, backend)
     return _INFO
+
+
+def forced_group() -> bool:
+    """``JMAE_FORCE_PG=1``: create the process group (and the gradient reducer) even at world size
+    1.  Test/diagnostic switch: a 1-rank RCCL communicator runs every line of the data-parallel path
+    (bucketed async all-reduce from the weight-gradient stream, per-bucket optimizer overlap,
+    device barriers) on a one-GPU box, and AVG over one rank is the identity, so the step must equal
+    the non-distributed step bit for bit (tests/test_rccl_gpu.py)."""
+    return os.environ.get("JMAE_FORCE_PG", "0") == "1"
 
 
 def info() -> DistInfo:

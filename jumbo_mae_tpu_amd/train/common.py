@@ -46,7 +46,7 @@ def make_optimizer(args, store, peak_lr: float, end_value: float) -> FlatOptimiz
 
 
 def make_reducer(args, store):
-    if pdist.info().world_size > 1:
+    if pdist.info().world_size > 1 or pdist.forced_group():
         dt = torch.bfloat16 if getattr(args, "reduce_dtype", "fp32") == "bf16" else torch.float32
         return GradReducer(store, bucket_mb=args.bucket_mb, reduce_dtype=dt)
     return None

@@ -22,6 +22,7 @@ def _reset_gemm_variant(request):
         request.getfixturevalue("ext").ln_set_bwd_la(2)
         request.getfixturevalue("ext").attn_set_bwd_ppw(0)
         request.getfixturevalue("ext").gemm_tn_set_acc0(0)
+        request.getfixturevalue("ext").gemm_tn_set_atomic(0)
         request.getfixturevalue("ext").gemm_tn_set_variant(4)
         request.getfixturevalue("ext").gemm_set_tail(1)
         request.getfixturevalue("ext").attn_set_bwd2_db(0)
@@ -298,6 +299,33 @@ def test_gemm_tn_wgrad(ext, M, N, K, acc0, variant):
     ext.gemm_tn_set_variant(4)
     assert S >= 1 and (S > 1 or M < 8192)
     assert rel(g, ref) < 1e-4
+
+
+@pytest.mark.parametrize("mode", [1, 3])
+@pytest.mark.parametrize("M,N,K", [(4096, 256, 512), (3000, 512, 256), (26624, 1024, 256), (101888, 512, 512),
+                                   (25088, 3072, 1024)])
+def test_gemm_tn_wgrad_atomic(ext, M, N, K, mode):
+    """Atomic split reduction (ACC = 2 epilogue, LDS-restaged 256-B atomic rows): every split adds
+    its tile into G, no partial slices; mode 3 also plans more splits.  Plain and segmented."""
+    ext.gemm_tn_set_atomic(mode)
+    torch.manual_seed(0)
+    dy = (torch.rand(M, N, device="cuda") * 2 - 1).bfloat16()
+    x = (torch.rand(M, K, device="cuda") * 2 - 1).bfloat16()
+    g = torch.randn(N, K, device="cuda")
+    ref = g.double() + dy.double().t() @ x.double()
+    S = ext.gemm_tn_wgrad(dy, x, g)
+    assert S >= 1 and (S > 1 or M < 8192)
+    err = rel(g, ref)
+    if M % 128 == 0:
+        g2 = ref.float().clone()
+        n = 4 if (M // 4) % 64 == 0 else 1
+        rows = M // n
+        ref2 = ref + dy.double().t() @ x.double()
+        ext.gemm_tn_wgrad_seg([dy[i * rows:(i + 1) * rows] for i in range(n)],
+                              [x[i * rows:(i + 1) * rows] for i in range(n)], g2)
+        assert rel(g2, ref2) < 1e-4
+    ext.gemm_tn_set_atomic(0)
+    assert err < 1e-4
 
 
 @pytest.mark.parametrize("T0", [0, 3])

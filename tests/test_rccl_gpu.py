@@ -1,0 +1,80 @@
+"""The data-parallel path on a real RCCL communicator, on a one-GPU box.
+
+``JMAE_FORCE_PG=1`` makes bench.py create the process group and the bucketed ``GradReducer`` even
+at world size 1 (parallel/dist.py ``forced_group``).  Under torchrun with one rank that runs every
+RCCL line the driver's multi-GPU scaling run executes -- ``init_process_group("nccl",
+device_id=...)``, async ``all_reduce(AVG)`` per bucket issued during the backward, the per-bucket
+optimizer ranges queued behind each reduction, device barriers, the max-over-ranks timing -- and
+since AVG over one rank is the identity, the result must equal the plain single-process step bit
+for bit.  The CPU twin (gloo, ``--cpu``) runs in the default suite.
+Reference: the pmap/pmean step of /root/reference/src/pretraining.py:125-159."""
+
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _run(args, torchrun: bool, force: bool, timeout: int = 300):
+    bench = [os.path.join(ROOT, "bench.py")] + args
+    if torchrun:
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+               "--master-addr", "127.0.0.1", "--master-port", str(_port())] + bench
+    else:
+        cmd = [sys.executable] + bench
+    env = dict(os.environ, OMP_NUM_THREADS="2", JMAE_FORCE_PG="1" if force else "0")
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, cwd="/tmp", env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    return json.loads(lines[0])
+
+
+def _check_equal(args):
+    plain = _run(args, torchrun=False, force=False)
+    dp = _run(args, torchrun=True, force=True)
+    assert plain.get("reducer") is None
+    if "reducer" in dp:
+        assert dp["reducer"] is not None and dp["reducer"]["buckets"] >= 2, dp
+    assert dp["config"]["final_loss"] == plain["config"]["final_loss"], (dp, plain)
+    if "weight_checksum" in plain:
+        # a few GPU reductions (LayerNorm / bias parameter partials) add with float atomics, so two
+        # runs may differ in the last bit of a weight: ~1 ulp of the fp64 checksum, not more
+        assert abs(dp["weight_checksum"] - plain["weight_checksum"]) <= 1e-12 * plain["weight_checksum"], (dp, plain)
+    return plain, dp
+
+
+PRETRAIN = ["--gpus", "1", "--steps", "2", "--warmup", "1", "--model", "vit_tiny_patch16",
+            "--batch-per-gpu", "32", "--bucket-mb", "0.5"]
+
+
+def test_forced_group_matches_plain_cpu():
+    _check_equal(PRETRAIN[:-4] + ["--batch-per-gpu", "4", "--image-size", "64", "--bucket-mb", "0.5", "--cpu"])
+
+
+@pytest.mark.gpu
+def test_rccl_pretrain_matches_plain():
+    _check_equal(PRETRAIN)
+
+
+@pytest.mark.gpu
+def test_rccl_pretrain_bf16_reduce_and_accum():
+    out = _run(PRETRAIN + ["--reduce-dtype", "bf16", "--grad-accum", "2"], torchrun=True, force=True)
+    assert out["config"]["final_loss"] == out["config"]["final_loss"] and out["reducer"] is not None
+
+
+@pytest.mark.gpu
+def test_rccl_finetune_matches_plain():
+    _check_equal(["--task", "finetune", "--gpus", "1", "--steps", "2", "--warmup", "1", "--model",
+                  "vit_tiny_patch16", "--batch-per-gpu", "32", "--bucket-mb", "0.5"])

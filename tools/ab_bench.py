@@ -62,6 +62,9 @@ def apply(P, cfg: str):
         elif k == "ATTN_TR":
             from jumbo_mae_tpu_amd.ops import _ext
             _ext.load(True).attn_set_tr(int(v))
+        elif k == "GEMM_TN_ATOMIC":
+            from jumbo_mae_tpu_amd.ops import _ext
+            _ext.load(True).gemm_tn_set_atomic(int(v))
         elif k == "GEMM_TN_ACC0":
             from jumbo_mae_tpu_amd.ops import _ext
             _ext.load(True).gemm_tn_set_acc0(int(v))
