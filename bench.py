@@ -232,6 +232,9 @@ def bench_classifier(args):
                  "--weight-decay", "0.0", "--warmup-steps", str(N * 10 // 16384),
                  "--training-steps", str(N * 90 // 16384)]
         model_name, recipe = "vit_large_patch16 jumbo (3 CLS) linear probe", "lars syncbn-head"
+    # fixed seeds (the CLI defaults them to random.randint, as the reference does): reproducible runs
+    for k in ("init", "mixup", "dropout", "shuffle", "noise"):
+        flags += [f"--{k}-seed", "0"]
     fargs = finetune_parser().parse_args(flags + ["--train-batch-size", str(gb), "--bucket-mb", str(args.bucket_mb),
                                                 "--reduce-dtype", args.reduce_dtype])
     model = build_model(fargs, dev, torch.bfloat16, info.rank)

@@ -583,6 +583,7 @@ void jm_gemm_tn_set_acc0(int v) { g_tn_acc0 = v; }
 
 // A/B: split reduction by float atomics into G from the 4-phase kernel's epilogue (ACC = 2) instead
 // of fp32 partial slices + jm_splitk_reduce_add.  Summation order then varies from run to run.
+// Off: measured 2 ms/step slower on the ViT-L step (95.3 -> 97.3 ms, profiles/r2_tn_atomic.txt).
 // Values >= 2 also price the split reduction 2^(v-1) x cheaper in jm_gemm_tn_plan (more splits).
 int jm_gemm_tn_atomic() { return g_tn_atomic && g_tn4; }
 void jm_gemm_tn_set_atomic(int v) { g_tn_atomic = v; }

@@ -27,6 +27,7 @@ MI355X design:
 from __future__ import annotations
 
 import contextlib
+import os
 
 import torch
 import torch.distributed as dist
@@ -44,7 +45,8 @@ class GradReducer:
         from .dist import forced_group
 
         self.enabled = self.world > 1 or (forced_group() and dist.is_available() and dist.is_initialized())
-        self.overlap = overlap and self.enabled
+        # JMAE_REDUCER_OVERLAP=0: every bucket is launched from finish() (diagnostics / A/B)
+        self.overlap = overlap and self.enabled and os.environ.get("JMAE_REDUCER_OVERLAP", "1") == "1"
         self.sync = True
         self.reduce_dtype = reduce_dtype
         segs = [s for s in store.segments if s.trainable and (seg_filter is None or seg_filter(s))]
