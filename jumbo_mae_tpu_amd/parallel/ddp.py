@@ -174,10 +174,27 @@ class GradReducer:
     def bucket_ranges(self) -> list[tuple[int, int]]:
         return [(lo, hi) for lo, hi, _ in self.buckets]
 
+    def optimizer_groups(self) -> list[list[int]]:
+        """Consecutive bucket indices whose optimizer update is issued as ONE launch once all of
+        them are reduced (``JMAE_OPT_GROUPS``, default 4; 0 = one launch per bucket).  Buckets are
+        contiguous flat ranges in launch order, so a group is one contiguous range.  Measured at one
+        rank on RCCL: 30 per-bucket AdamW launches cost 0.4 ms/step more than one
+        (profiles/r2_dp_overhead_1rank.txt); a few groups keep the update of the early buckets
+        overlapped with the reduction of the last ones."""
+        nb = len(self.buckets)
+        g = int(os.environ.get("JMAE_OPT_GROUPS", "4"))
+        g = nb if g <= 0 else max(1, min(g, nb))
+        return [list(range(nb * i // g, nb * (i + 1) // g)) for i in range(g)]
+
+    def optimizer_ranges(self) -> list[tuple[int, int]]:
+        return [(min(self.buckets[b][0] for b in grp), max(self.buckets[b][1] for b in grp))
+                for grp in self.optimizer_groups()]
+
     def finish(self, on_bucket_done=None) -> None:
         """Launch any bucket not yet reduced (unused segments / no overlap) and wait for all.
 
-        ``on_bucket_done(lo, hi)`` is called as soon as the last reduction of a bucket has been
+        ``on_bucket_done(lo, hi)`` is called as soon as the last reduction of an optimizer group
+        (``optimizer_ranges``, consecutive buckets) has been
         waited for (on RCCL: a stream wait, the host does not block), so the caller can queue
         the optimizer update of that range behind it while later buckets -- the jumbo-MLP tail
         -- are still being reduced."""
@@ -188,9 +205,12 @@ class GradReducer:
         for b in range(len(self.buckets)):
             if not self.launched[b]:
                 self._launch(b)
-        left = [0] * len(self.buckets)
+        groups = self.optimizer_groups()
+        ranges = self.optimizer_ranges()
+        gid = {b: i for i, grp in enumerate(groups) for b in grp}
+        left = [0] * len(groups)  # outstanding reductions per optimizer group
         for b, _ in self.works:
-            left[b] += 1
+            left[gid[b]] += 1
         for b, (w, to_div) in self.works:
             w.wait()
             if to_div is not None:
@@ -198,10 +218,13 @@ class GradReducer:
             if b in self._compressed:
                 lo, hi, _ = self.buckets[b]
                 self.store.grad[lo:hi].copy_(self._compressed.pop(b))
-            left[b] -= 1
-            if on_bucket_done is not None and left[b] == 0:
-                lo, hi, _ = self.buckets[b]
-                on_bucket_done(lo, hi)
+            left[gid[b]] -= 1
+            if on_bucket_done is not None and left[gid[b]] == 0:
+                on_bucket_done(*ranges[gid[b]])
+        if on_bucket_done is not None:  # a group without any reduction of its own (none today)
+            for i, grp in enumerate(groups):
+                if not any(gid[b] == i for b, _ in self.works):
+                    on_bucket_done(*ranges[i])
         self.works = []
 
     def stats(self) -> dict:

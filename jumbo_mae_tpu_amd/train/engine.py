@@ -85,7 +85,7 @@ class Trainer:
         split = (self.overlap_optimizer and self.reducer is not None and self.reducer.enabled
                  and self.opt.can_split() and not self.skip_nonfinite)
         if split and not self._planned:
-            self.opt.plan_ranges(self.reducer.bucket_ranges())
+            self.opt.plan_ranges(self.reducer.optimizer_ranges())
             self._planned = True
         if self.reducer is not None:
             with trace_range("allreduce_wait"):
