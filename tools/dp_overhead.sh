@@ -9,9 +9,8 @@ TR="python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 
 run() { local n=$1; local a=$2; shift 2; (cd /tmp && timeout -k 10 240 env "$@" $R/bench.py --steps 20 --warmup 5 $a > $O/$n.json 2> $O/$n.err) \
   || { tail -20 $O/$n.err; exit 1; }; python -c "import json; d=[json.loads(l) for l in open('$O/$n.json') if l.startswith('{')][-1]; print('$n', d['ms_per_step'], d['value'], d.get('exposed_comm_ms_last_step'), d.get('reducer'), d['config']['final_loss'])"; }
 run plain "" JMAE_FORCE_PG=0 python
-run dp64 "" JMAE_FORCE_PG=1 $TR
-run dp64_g0 "" JMAE_FORCE_PG=1 JMAE_OPT_GROUPS=0 $TR
-run dp64_g1 "" JMAE_FORCE_PG=1 JMAE_OPT_GROUPS=1 $TR
-run dp64_nosplit "" JMAE_FORCE_PG=1 JMAE_OVERLAP_OPT=0 $TR
-run dp256 "--bucket-mb 256" JMAE_FORCE_PG=1 $TR
-run dp16 "--bucket-mb 16" JMAE_FORCE_PG=1 $TR
+run dp64 "" JMAE_FORCE_PG=1 JMAE_RCCL_HIPRI=0 $TR
+run dp64_hipri "" JMAE_FORCE_PG=1 JMAE_RCCL_HIPRI=1 $TR
+run dp64_g1 "" JMAE_FORCE_PG=1 JMAE_OPT_GROUPS=1 JMAE_RCCL_HIPRI=0 $TR
+run dp64_g1_hipri "" JMAE_FORCE_PG=1 JMAE_OPT_GROUPS=1 JMAE_RCCL_HIPRI=1 $TR
+run dp16_hipri "--bucket-mb 16" JMAE_FORCE_PG=1 JMAE_RCCL_HIPRI=1 $TR
