@@ -33,6 +33,9 @@ def apply(P, cfg: str):
         elif k == "GEMM_VARIANT":
             from jumbo_mae_tpu_amd.ops import _ext
             _ext.load(True).gemm_set_variant(int(v), 8)
+        elif k == "GEMM_GROUP":  # row tiles per column sweep of the default (4-phase, variant 24) kernel
+            from jumbo_mae_tpu_amd.ops import _ext
+            _ext.load(True).gemm_set_variant(24, int(v))
         elif k == "GEMM_TAIL":
             from jumbo_mae_tpu_amd.ops import _ext
             _ext.load(True).gemm_set_tail(int(v))
