@@ -94,6 +94,7 @@ int jm_gemm_tn_acc0();
 void jm_gemm_tn_set_acc0(int v);
 int jm_gemm_tn_atomic();
 void jm_gemm_tn_set_atomic(int v);
+void jm_gemm_tn_set_red_scale(double v);
 void jm_gemm_tn_set_variant(int v);
 struct TnSegs {
   const uint16_t* a[32];
@@ -930,6 +931,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_set_sk", &jm_gemm_set_sk, "persistent DP + stream-K NT launches where they pay (1, default) or never (0)");
   m.def("gemm_tn_set_acc0", &jm_gemm_tn_set_acc0);
   m.def("gemm_tn_set_atomic", &jm_gemm_tn_set_atomic);
+  m.def("gemm_tn_set_red_scale", &jm_gemm_tn_set_red_scale);
   m.def("gemm_tn_set_variant", &jm_gemm_tn_set_variant, "TN wgrad kernel: 4 = 4-phase (default), 0 = r1 32-row steps");
   m.def("gemm_nt_splitk", &gemm_nt_splitk, py::arg("A"), py::arg("B"), py::arg("bias") = py::none(),
         py::arg("splits") = 8, py::arg("add") = py::none());

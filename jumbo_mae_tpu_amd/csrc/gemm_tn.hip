@@ -543,6 +543,8 @@ size_t jm_gemm_tn_smem() { return (size_t)NST * STAGE * sizeof(uint16_t); }
 // Picks the split count that minimises an estimate of (waves of 256 CUs) x (steps per split +
 // epilogue) + the fp32 partial-tile traffic of the reduction.
 int g_tn_atomic = 0;
+double g_tn_red_scale = 1.0;  // A/B: weight of the partial-slice traffic in the split plan
+void jm_gemm_tn_set_red_scale(double v) { g_tn_red_scale = v; }
 int g_tn4 = 1;  // A/B: 4-phase TN kernel (default) vs the r1 32-row-step kernel (jm_gemm_tn_set_variant)
 void jm_gemm_tn_set_variant(int v) { g_tn4 = v == 4; }
 
@@ -562,6 +564,7 @@ int jm_gemm_tn_plan(int M, int N, int K, int* S_out) {
     const double t_steps = (double)waves * (sps + 12);                       // ~1 us per step
     double t_red = s_eff > 1 ? (double)s_eff * N * K * 8.0 / 5.0e12 * 1e6 : 0.0;  // us
     if (g_tn_atomic >= 2) t_red /= (double)(1 << (g_tn_atomic - 1));  // A/B: atomics priced lower
+    t_red *= g_tn_red_scale;
     const double est = t_steps + t_red;
     if (est < best) {
       best = est;

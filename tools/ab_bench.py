@@ -65,6 +65,9 @@ def apply(P, cfg: str):
         elif k == "ATTN_TR":
             from jumbo_mae_tpu_amd.ops import _ext
             _ext.load(True).attn_set_tr(int(v))
+        elif k == "TN_RED_SCALE":  # weight of the partial traffic in the TN split plan
+            from jumbo_mae_tpu_amd.ops import _ext
+            _ext.load(True).gemm_tn_set_red_scale(float(v))
         elif k == "GEMM_TN_ATOMIC":
             from jumbo_mae_tpu_amd.ops import _ext
             _ext.load(True).gemm_tn_set_atomic(int(v))
