@@ -1,14 +1,21 @@
 #!/usr/bin/env bash
 # Shared launcher: one process per MI355X over RCCL/xGMI via torchrun.
 #   NGPU (default: all visible GPUs), NNODES/NODE_RANK/MASTER_ADDR/MASTER_PORT for multi-node.
-#   DATA_DIR: directory holding imagenet-1k-wds shards (replaces the reference's $GCS_DATASET_DIR,
-#   which may also be a "pipe:gsutil cat gs://..." prefix), CKPT_DIR: output dir,
-#   PRETRAINED: checkpoint for finetune / linear probe (replaces $GCS_MODEL_PATH).
+#   DATA_DIR: directory or URL holding imagenet-1k-wds shards (the reference's $GCS_DATASET_DIR:
+#   a local path, gs://bucket/..., s3://..., http(s)://..., or a "pipe:<cmd> " prefix such as
+#   "pipe:gsutil cat gs://bucket"), CKPT_DIR: output dir or URL (default $DATA_DIR/CKPT; for a
+#   pipe: prefix, the URL that ends the prefix + /CKPT), PRETRAINED: checkpoint path or URL for
+#   finetune / linear probe (the reference's $GCS_MODEL_PATH).
 set -euo pipefail
 REPO="$(cd "$(dirname "${BASH_SOURCE[0]}")/.." && pwd)"
 NGPU="${NGPU:-$(python3 -c 'import torch; print(max(torch.cuda.device_count(), 1))')}"
 DATA_DIR="${DATA_DIR:-${GCS_DATASET_DIR:-$REPO/data}}"
-CKPT_DIR="${CKPT_DIR:-$DATA_DIR/CKPT}"
+if [[ "$DATA_DIR" == pipe:* ]]; then
+  # a pipe: prefix is a READ command; checkpoints go to the URL it reads from (its last word)
+  CKPT_DIR="${CKPT_DIR:-${DATA_DIR##* }/CKPT}"
+else
+  CKPT_DIR="${CKPT_DIR:-$DATA_DIR/CKPT}"
+fi
 PRETRAINED="${PRETRAINED:-${GCS_MODEL_PATH:-}}"
 TRAIN_SHARDS="${TRAIN_SHARDS:-$DATA_DIR/imagenet-1k-wds/imagenet1k-train-{0000..1023}.tar}"
 VALID_SHARDS="${VALID_SHARDS:-$DATA_DIR/imagenet-1k-wds/imagenet1k-validation-{00..63}.tar}"

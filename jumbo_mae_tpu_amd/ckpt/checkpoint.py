@@ -2,7 +2,8 @@
 
 Reference:
   save_checkpoint_in_background ... /root/reference/src/utils.py:55-63 (a bare thread per save,
-                                    writing ``{output_dir}/{name}-{postfix}.msgpack`` via gopen)
+                                    writing ``{output_dir}/{name}-{postfix}.msgpack`` via gopen:
+                                    local, gs://, s3://, pipe: -- utils/gopen.py here)
   load_pretrained_params .......... /root/reference/src/utils.py:150-202
   save sites ...................... main_pretrain.py:77-90 (``last`` every eval, ``best`` on
                                     improvement)
@@ -18,42 +19,19 @@ Changes by design:
 
 from __future__ import annotations
 
-import os
 import queue
-import subprocess
 import threading
 
 import numpy as np
 
+from ..utils import gopen
 from .msgpack_flax import msgpack_restore, msgpack_serialize
 
 
 # ------------------------------------------------------------------------------ gopen
-def read_bytes(url: str) -> bytes:
-    """Local path, ``file://``, or ``pipe:<cmd>`` (stdout of a shell command, e.g. gsutil cat)."""
-    if url.startswith("pipe:"):
-        return subprocess.run(url[5:], shell=True, check=True, capture_output=True).stdout
-    if url.startswith("file://"):
-        url = url[7:]
-    with open(url, "rb") as f:
-        return f.read()
-
-
-def write_bytes(url: str, data: bytes) -> None:
-    if url.startswith("pipe:"):
-        subprocess.run(url[5:], shell=True, check=True, input=data)
-        return
-    if url.startswith("file://"):
-        url = url[7:]
-    d = os.path.dirname(url)
-    if d:
-        os.makedirs(d, exist_ok=True)
-    tmp = f"{url}.tmp.{os.getpid()}"
-    with open(tmp, "wb") as f:
-        f.write(data)
-        f.flush()
-        os.fsync(f.fileno())
-    os.replace(tmp, url)
+# local paths, file://, pipe:<cmd>, gs://, s3://, http(s):// (read) -- utils/gopen.py
+read_bytes = gopen.read_bytes
+write_bytes = gopen.write_bytes
 
 
 # ------------------------------------------------------------------------------ writer
@@ -106,7 +84,7 @@ def writer() -> AsyncCheckpointWriter:
 
 
 def ckpt_path(output_dir: str, name: str, postfix: str, ext: str = "msgpack") -> str:
-    return os.path.join(output_dir, f"{name}-{postfix}.{ext}")
+    return gopen.join(output_dir, f"{name}-{postfix}.{ext}")
 
 
 def save_checkpoint_in_background(output_dir: str, name: str, params_bytes: bytes, postfix: str = "last") -> str:

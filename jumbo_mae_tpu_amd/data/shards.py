@@ -6,7 +6,8 @@ Reference pipeline (/root/reference/src/dataset.py:107-116,139-150):
 Implemented here with the stdlib ``tarfile`` in streaming mode: brace-expanded shard lists,
 deterministic per-epoch shard shuffles, rank/worker splitting, sample grouping by key
 (``{key}.jpg`` + ``{key}.cls`` -> one sample), a deterministic shuffle buffer, and
-``pipe:`` URLs (e.g. ``pipe:gsutil cat gs://...``) next to local files.
+``pipe:`` / ``gs://`` / ``s3://`` / ``http(s)://`` URLs next to local files (utils/gopen.py; the
+reference's presets read ``$GCS_DATASET_DIR`` = ``gs://...`` through webdataset's gopen).
 
 Local shards are read by the native module ``jumbo_mae_tpu_amd._io`` when it is built
 (csrc/io/tario.cpp: tar parsing and file I/O on a pool of C++ threads with ordered read-ahead, the
@@ -23,6 +24,8 @@ import re
 import subprocess
 import tarfile
 from typing import Iterable, Iterator
+
+from ..utils import gopen
 
 
 def brace_expand(pattern: str) -> list[str]:
@@ -84,11 +87,12 @@ class PipeStream(io.RawIOBase):
 
 
 def open_stream(url: str):
-    if url.startswith("pipe:"):
-        return io.BufferedReader(PipeStream(url[5:]), 1 << 20)
-    if url.startswith("file://"):
-        url = url[7:]
-    return open(url, "rb")
+    """Byte stream of a shard: local file, or the stdout of the scheme's read command (``pipe:``,
+    ``gs://`` via gsutil, ``s3://``, ``http(s)://`` via curl -- utils/gopen.py)."""
+    local = gopen.local_path(url)
+    if local is not None:
+        return open(local, "rb")
+    return io.BufferedReader(PipeStream(gopen.command(url, "read")), 1 << 20)
 
 
 def cache_dir() -> str:
@@ -102,7 +106,7 @@ def cache_name(url: str) -> str:
     URL, so equal basenames from different buckets do not collide."""
     import hashlib
 
-    target = url[5:].split()[-1] if url.startswith("pipe:") else url
+    target = url[5:].split()[-1] if url.startswith("pipe:") else url.split("?", 1)[0]
     base = re.sub(r"[^\w.\-]", "_", target.rstrip("/").rsplit("/", 1)[-1]) or "shard"
     return hashlib.sha1(url.encode()).hexdigest()[:10] + "-" + base
 
@@ -198,10 +202,7 @@ def _native():
     return _io
 
 
-def _local_path(url: str) -> str | None:
-    if url.startswith("pipe:"):
-        return None
-    return url[7:] if url.startswith("file://") else url
+_local_path = gopen.local_path
 
 
 def iter_samples(urls: list[str], handler=None, threads: int = 4) -> Iterator[dict]:

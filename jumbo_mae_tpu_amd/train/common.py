@@ -12,6 +12,7 @@ from ..optim.flat import FlatOptimizer
 from ..optim.schedule import warmup_cosine_decay_schedule
 from ..parallel import dist as pdist
 from ..parallel.ddp import GradReducer
+from ..utils import gopen
 
 
 def pick_device(args) -> torch.device:
@@ -152,9 +153,9 @@ def maybe_resume(args, model, opt, rngs, log=print) -> Resumed:
     host Mixup generator; returns the step, data position and best metrics (``Resumed``)."""
     if not args.resume:
         return Resumed()
-    prefix = os.path.join(args.output_dir, f"{args.name or 'run'}-last") if args.resume == "auto" else args.resume
+    prefix = gopen.join(args.output_dir, f"{args.name or 'run'}-last") if args.resume == "auto" else args.resume
     pfile, sfile = prefix + ".msgpack", prefix + ".state.pt"
-    if not (os.path.exists(pfile) and os.path.exists(sfile)):
+    if not (gopen.exists(pfile) and gopen.exists(sfile)):
         log(f"[resume] nothing to resume at {prefix}")
         return Resumed()
     model.store.load_flax_tree(load_params(pfile), strict=True)

@@ -43,6 +43,7 @@ def build_model(args, device, dtype, rank: int = 0) -> FinetuneModel:
 
 
 def evaluate(model, loader, rngs, device) -> dict:
+    rngs = rngs.fork()  # validation never advances the training streams
     sums = None
     for images, labels in C.DevicePrefetcher(loader, device):
         m = model.evaluate(images, labels, rngs.as_dict())

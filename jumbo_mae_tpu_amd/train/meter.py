@@ -20,6 +20,8 @@ import numpy as np
 import torch
 import torch.distributed as dist
 
+from ..utils import gopen
+
 
 class AverageMeter:
     def __init__(self, use_latest: list[str] | None = None, group=None):
@@ -67,8 +69,12 @@ class Logger:
         self.wandb = None
         if not enabled:
             return
-        os.makedirs(output_dir or ".", exist_ok=True)
-        self.path = os.path.join(output_dir or ".", f"{name or 'run'}-metrics.jsonl")
+        # a remote --output-dir (gs://...) keeps the metrics log in the working directory
+        log_dir = output_dir or "."
+        if not gopen.is_local(log_dir):
+            log_dir = "."
+        os.makedirs(log_dir, exist_ok=True)
+        self.path = os.path.join(log_dir, f"{name or 'run'}-metrics.jsonl")
         self.f = open(self.path, "a")
         if use_wandb is None:
             use_wandb = os.environ.get("WANDB_MODE", "") not in ("", "disabled") or bool(os.environ.get("WANDB_API_KEY"))

@@ -46,6 +46,7 @@ def build_model(args, device, dtype) -> PretrainModel:
 
 
 def evaluate(model, loader, rngs, device) -> dict:
+    rngs = rngs.fork()  # validation never advances the training streams
     sums = None
     for batch in C.DevicePrefetcher(loader, device):
         images, labels = batch if isinstance(batch, (list, tuple)) else (batch, None)

@@ -49,6 +49,20 @@ class RngStreams:
         for name, g in self.gens.items():
             g.manual_seed(derive_seed(self.seeds.get(name, 0) * 1_000_003 + step, name, self.rank))
 
+    def fork(self) -> "RngStreams":
+        """Streams that start at this object's current states and never advance it.  Validation
+        draws from a fork: the reference's validation_step splits the state's keys and drops the
+        update (/root/reference/src/pretraining.py:162-167), so evaluating never moves the training
+        streams -- and an interrupted run resumes exactly whether or not its save step evaluated."""
+        new = RngStreams.__new__(RngStreams)
+        new.seeds, new.rank, new.device = dict(self.seeds), self.rank, self.device
+        new.gens = {}
+        for k, g in self.gens.items():
+            ng = torch.Generator(device=self.device)
+            ng.set_state(g.get_state())
+            new.gens[k] = ng
+        return new
+
     def load_state_dict(self, d: dict) -> None:
         for k, s in d.items():
             if k in self.gens:

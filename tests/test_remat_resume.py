@@ -228,16 +228,19 @@ def test_loader_resume_continues_stream(workers):
         assert torch.equal(b[0], ref[k][0]) and torch.equal(b[1], ref[k][1]), k
 
 
-def test_interrupted_run_resumes_exactly(tmp_path):
-    """6 steps uninterrupted == 4 steps (--stop-after-steps) + --resume auto to 6: same weights."""
+@pytest.mark.parametrize("stop", [4, 3])
+def test_interrupted_run_resumes_exactly(tmp_path, stop):
+    """6 steps uninterrupted == ``stop`` steps (--stop-after-steps) + --resume auto to 6: same weights.
+    stop=3 saves at a step without an evaluation (eval interval 2): validation must not advance the
+    training RNG streams, or the resumed run's streams diverge."""
     from jumbo_mae_tpu_amd.ckpt.checkpoint import load_params
     from tests.test_e2e import _pretrain
     a, b = str(tmp_path / "a"), str(tmp_path / "b")
     extra = ["--eval-interval", "2", "--augment-repeats", "2"]
     _pretrain(a, 6, extra)
-    _pretrain(b, 6, extra + ["--stop-after-steps", "4"])
+    _pretrain(b, 6, extra + ["--stop-after-steps", str(stop)])
     rows = [json.loads(line) for line in open(os.path.join(b, "p-metrics.jsonl"))]
-    assert max(r["step"] for r in rows) == 4
+    assert max(r["step"] for r in rows) <= stop
     res = _pretrain(b, 6, extra + ["--resume", "auto"])
     assert res["final_step"] == 6
     pa, pb = load_params(os.path.join(a, "p-last.msgpack")), load_params(os.path.join(b, "p-last.msgpack"))
