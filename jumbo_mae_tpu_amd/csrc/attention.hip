@@ -51,62 +51,6 @@ JM_DEVICE s16x4_t tr4(const uint16_t* p) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4_t*)(p));
 }
 
-// workgroup barrier; LDSONLY: LDS traffic only (s_waitcnt lgkmcnt(0) + s_barrier) -- unlike
-// __syncthreads it does not wait for outstanding global loads / LDS-DMA (vmcnt), so a prefetch
-// stays in flight across it
-template <int V>
-struct IC {
-  static constexpr int value = V;
-};
-
-// two static LDS image sets for the double-buffered backward: distinct LDS objects, so alias
-// analysis proves that reads of one set never touch the DMA in flight into the other (with one
-// dynamic array the compiler inserts a vmcnt wait for that DMA before every LDS read)
-template <int N, int TAG>
-JM_DEVICE uint16_t* lds_images() {
-  __shared__ __attribute__((aligned(16))) uint16_t buf[N];
-  return buf;
-}
-
-template <bool LDSONLY>
-JM_DEVICE void wg_bar() {
-  if constexpr (LDSONLY) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-  else __syncthreads();
-}
-
-typedef __attribute__((address_space(3))) void lds_void_t;
-
-// buffer resource over [base, base + bytes): loads past the end read zero (padded rows)
-JM_DEVICE __amdgpu_buffer_rsrc_t make_rsrc(const uint16_t* base, long bytes) {
-  const int n = bytes >= 0xffffffffL ? -1 : (int)bytes;
-  return __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, n, 0x00020000);
-}
-
-// buffer_load_dwordx4 ... lds: 16 B per lane into LDS at (wave-uniform l) + 16 * lane
-JM_DEVICE void blds16(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff, uint16_t* l) {
-  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void_t*)(l), 16, voff, soff, 0, 0);
-}
-
-// The same load as inline asm: the compiler does not see it as an LDS DMA, so it adds no vmcnt
-// wait for it before later LDS reads (the double-buffered backward reads one image set while
-// the DMA into the other is in flight; the kernel waits for its DMA with explicit counted waits)
-typedef int i32x4_t __attribute__((ext_vector_type(4)));
-JM_DEVICE i32x4_t rsrc4(const uint16_t* base, long bytes) {
-  const unsigned long a = (unsigned long)base;
-  i32x4_t r;
-  r.x = (int)(unsigned)a;
-  r.y = (int)((unsigned)(a >> 32) & 0xffffu);
-  r.z = bytes >= 0xffffffffL ? -1 : (int)bytes;
-  r.w = 0x00020000;
-  return r;
-}
-JM_DEVICE void blds16_asm(i32x4_t rsrc, uint32_t voff, uint16_t* l) {
-  const uint32_t m0v =
-      __builtin_amdgcn_readfirstlane((uint32_t)(unsigned long)(__attribute__((address_space(3))) uint16_t*)l);
-  asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds" ::"s"(m0v), "v"(voff), "s"(rsrc)
-               : "memory", "m0");
-}
-
 JM_DEVICE f32x4_t mfma(bf16x8_t a, bf16x8_t b, f32x4_t c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
@@ -591,261 +535,11 @@ __global__ __launch_bounds__(256) void attn_fwd_ml_kernel(const uint16_t* __rest
 }
 
 // -------------------------------------------------------------------------------- backward
-// waves per backward workgroup: 8 when the LDS budget allows (decoder, hd 32), else 4
-template <int HD, int SP>
-constexpr int bwd_waves() { return (SP >= 128 && HD == 32) ? 8 : 4; }
-
-template <int HD, int SP, bool TR>
-__global__ __launch_bounds__((64 * bwd_waves<HD, SP>())) void attn_bwd_kernel(const uint16_t* __restrict__ qkv,
-                                                       const uint16_t* __restrict__ o,
-                                                       const uint16_t* __restrict__ dO,
-                                                       const float* __restrict__ lse,
-                                                       uint16_t* __restrict__ dqkv, int S, int H, float scale,
-                                                       float* __restrict__ dbp) {
-  JM_DGUARD(S >= 1 && S <= SP);
-  // dbp (optional): per-sample partial column sums of dqkv, [B][3*H*HD] fp32 -- the QKV Dense
-  // bias gradient fused in (summed over b by jm_splitk_reduce_add), taken from the fp32 MFMA
-  // accumulators so dqkv is never re-read.
-  constexpr int RS = HD + 8;  // row-major image stride
-  constexpr int TS = SP + 8;  // transposed image stride
-  constexpr int NT = SP / 16;
-  constexpr int KK = HD / 32;
-  constexpr int DT = HD / 16;
-  constexpr int NW = bwd_waves<HD, SP>();
-  constexpr int NTH = 64 * NW;
-  constexpr int QC = 16 * NW;             // query rows per dS chunk: one q tile per wave for dQ
-  constexpr int NKW = (NT + NW - 1) / NW;  // key tiles per wave
-  extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
-  uint16_t* Qs = smem;
-  uint16_t* Ks = Qs + SP * RS;
-  uint16_t* Vs = Ks + SP * RS;
-  uint16_t* dOs = Vs + SP * RS;
-  // TR: transposed operands come from the row-major images through ds_read_b64_tr_b16
-  uint16_t* Qt = dOs + SP * RS;
-  uint16_t* dOt = Qt + (TR ? 0 : HD * TS);
-  uint16_t* Kt = dOt + (TR ? 0 : HD * TS);
-  uint16_t* dSs = Kt + (TR ? 0 : HD * TS);
-  float* lse_s = reinterpret_cast<float*>(dSs + QC * TS);
-  float* delta_s = lse_s + SP;
-  float* bsum = delta_s + SP;  // [3 * HD] block column sums of dQ | dK | dV
-
-  const int bh = blockIdx.x;
-  const int b = bh / H, h = bh - (bh / H) * H;
-  const long ts = 3L * H * HD;
-  const long os = (long)H * HD;
-  const uint16_t* base = qkv + (long)b * S * ts;
-  const uint16_t* Qg = base + h * HD;
-  const uint16_t* Kg = base + (H + h) * HD;
-  const uint16_t* Vg = base + (2 * H + h) * HD;
-  const uint16_t* Og = o + (long)b * S * os + h * HD;
-  const uint16_t* dOg = dO + (long)b * S * os + h * HD;
-  uint16_t* dQg = dqkv + (long)b * S * ts + h * HD;
-  uint16_t* dKg = dqkv + (long)b * S * ts + (H + h) * HD;
-  uint16_t* dVg = dqkv + (long)b * S * ts + (2 * H + h) * HD;
-
-  for (int i = threadIdx.x; i < 3 * HD; i += NTH) bsum[i] = 0.f;
-  for (int i = threadIdx.x; i < SP; i += NTH) {
-    delta_s[i] = 0.f;
-    lse_s[i] = i < S ? lse[((long)b * H + h) * S + i] * LOG2E : INFINITY;
-  }
-  __syncthreads();
-  constexpr int CPR = HD / 8;
-  for (int i = threadIdx.x; i < SP * CPR; i += NTH) {
-    const int r = i / CPR, c = (i % CPR) * 8;
-    uint4 qv = make_uint4(0, 0, 0, 0), kv = qv, vv = qv, dv = qv;
-    float dsum = 0.f;
-    if (r < S) {
-      qv = *reinterpret_cast<const uint4*>(Qg + r * ts + c);
-      kv = *reinterpret_cast<const uint4*>(Kg + r * ts + c);
-      vv = *reinterpret_cast<const uint4*>(Vg + r * ts + c);
-      dv = *reinterpret_cast<const uint4*>(dOg + r * os + c);
-      float of[8], df[8];
-      load8(Og + r * os + c, of);
-      load8(dOg + r * os + c, df);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) dsum += of[j] * df[j];
-    }
-    *reinterpret_cast<uint4*>(Qs + r * RS + c) = qv;
-    *reinterpret_cast<uint4*>(Ks + r * RS + c) = kv;
-    *reinterpret_cast<uint4*>(Vs + r * RS + c) = vv;
-    *reinterpret_cast<uint4*>(dOs + r * RS + c) = dv;
-    if (!TR) {
-      const uint16_t* qh = reinterpret_cast<const uint16_t*>(&qv);
-      const uint16_t* kh = reinterpret_cast<const uint16_t*>(&kv);
-      const uint16_t* dh = reinterpret_cast<const uint16_t*>(&dv);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        Qt[(c + j) * TS + r] = qh[j];
-        Kt[(c + j) * TS + r] = kh[j];
-        dOt[(c + j) * TS + r] = dh[j];
-      }
-    }
-    if (r < S) atomicAdd(&delta_s[r], dsum);
-  }
-  __syncthreads();
-
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int l16 = lane & 15, g = lane >> 4;
-  const float sl2 = scale * LOG2E;
-
-  f32x4_t dvacc[NKW][DT], dkacc[NKW][DT];
-#pragma unroll
-  for (int w = 0; w < NKW; ++w)
-#pragma unroll
-    for (int dt = 0; dt < DT; ++dt) {
-      dvacc[w][dt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-      dkacc[w][dt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-    }
-
-  for (int qc = 0; qc * QC < SP; ++qc) {
-#pragma unroll
-    for (int w = 0; w < NKW; ++w) {
-      const int kt = wave + NW * w;
-      if (kt < NT) {
-        bf16x8_t kf[KK], vf[KK];
-#pragma unroll
-        for (int kk = 0; kk < KK; ++kk) {
-          kf[kk] = ld8(Ks + (kt * 16 + l16) * RS + 32 * kk + 8 * g);
-          vf[kk] = ld8(Vs + (kt * 16 + l16) * RS + 32 * kk + 8 * g);
-        }
-        const int key = kt * 16 + l16;
-#pragma unroll
-        for (int r = 0; r < QC / 32; ++r) {
-          const int qbase = qc * QC + 32 * r;
-          if (qbase < SP) {
-            float pf[8], df[8];
-#pragma unroll
-            for (int half = 0; half < 2; ++half) {
-              const int q0 = qbase + 16 * half;
-              f32x4_t s = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-              for (int kk = 0; kk < KK; ++kk) {
-                s = mfma(ld8(Qs + (q0 + l16) * RS + 32 * kk + 8 * g), kf[kk], s);
-                dp = mfma(ld8(dOs + (q0 + l16) * RS + 32 * kk + 8 * g), vf[kk], dp);
-              }
-              // s[i] = S[q = q0 + 4g + i][key]
-#pragma unroll
-              for (int i = 0; i < 4; ++i) {
-                const int q = q0 + 4 * g + i;
-                const float p = key < S ? __builtin_amdgcn_exp2f(s[i] * sl2 - lse_s[q]) : 0.f;
-                const float ds = p * (dp[i] - delta_s[q]);
-                pf[4 * half + i] = p;
-                df[4 * half + i] = ds;
-                dSs[(q - qc * QC) * TS + key] = f2bf(ds);
-              }
-            }
-            const bf16x8_t pb = pack8(pf);
-            const bf16x8_t dsb = pack8(df);
-#pragma unroll
-            for (int dt = 0; dt < DT; ++dt) {
-              bf16x8_t a_do, a_q;
-              if (TR) {
-                const int off = (qbase + 4 * g + (l16 >> 2)) * RS + dt * 16 + 4 * (l16 & 3);
-                a_do = cat44(tr4(dOs + off), tr4(dOs + off + 16 * RS));
-                a_q = cat44(tr4(Qs + off), tr4(Qs + off + 16 * RS));
-              } else {
-                const int d = dt * 16 + l16;
-                const uint16_t* dor = dOt + d * TS + qbase + 4 * g;
-                const uint16_t* qr = Qt + d * TS + qbase + 4 * g;
-                a_do = cat44(ld4(dor), ld4(dor + 16));
-                a_q = cat44(ld4(qr), ld4(qr + 16));
-              }
-              dvacc[w][dt] = mfma(a_do, pb, dvacc[w][dt]);
-              dkacc[w][dt] = mfma(a_q, dsb, dkacc[w][dt]);
-            }
-          }
-        }
-      }
-    }
-    __syncthreads();
-    // dQ^T[d][q] = sum_key K^T[d][key] dS^T[key][q] for the query tile of this wave
-    {
-      const int qt = qc * (QC / 16) + wave;
-      if (qt < NT) {
-        f32x4_t dq[DT];
-#pragma unroll
-        for (int dt = 0; dt < DT; ++dt) dq[dt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int s = 0; s < SP / 32; ++s) {
-          const bf16x8_t bop = ld8(dSs + (wave * 16 + l16) * TS + 32 * s + 8 * g);
-#pragma unroll
-          for (int dt = 0; dt < DT; ++dt) {
-            bf16x8_t ka;
-            if (TR) {
-              const uint16_t* kr = Ks + (32 * s + 8 * g + (l16 >> 2)) * RS + dt * 16 + 4 * (l16 & 3);
-              ka = cat44(tr4(kr), tr4(kr + 4 * RS));
-            } else {
-              ka = ld8(Kt + (dt * 16 + l16) * TS + 32 * s + 8 * g);
-            }
-            dq[dt] = mfma(ka, bop, dq[dt]);
-          }
-        }
-        if (dbp != nullptr) {  // column sums of this dQ tile (padded query rows are 0)
-#pragma unroll
-          for (int dt = 0; dt < DT; ++dt)
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-              const float v = row16_sum(dq[dt][i]);
-              if (l16 == 0) atomicAdd(&bsum[dt * 16 + 4 * g + i], v * scale);
-            }
-        }
-        const int q = qt * 16 + l16;
-        if (q < S) {
-#pragma unroll
-          for (int dt = 0; dt < DT; ++dt) {
-            float v[4] = {dq[dt][0] * scale, dq[dt][1] * scale, dq[dt][2] * scale, dq[dt][3] * scale};
-            store4(dQg + (long)q * ts + dt * 16 + 4 * g, v);
-          }
-        }
-      }
-    }
-    __syncthreads();
-  }
-  // write dK, dV of this wave's key tiles: acc[dt][i] = X^T[d = dt*16+4g+i][key = kt*16+l16]
-#pragma unroll
-  for (int w = 0; w < NKW; ++w) {
-    const int kt = wave + NW * w;
-    const int key = kt * 16 + l16;
-    if (kt < NT && key < S) {
-#pragma unroll
-      for (int dt = 0; dt < DT; ++dt) {
-        float kv[4] = {dkacc[w][dt][0] * scale, dkacc[w][dt][1] * scale, dkacc[w][dt][2] * scale,
-                       dkacc[w][dt][3] * scale};
-        float vv[4] = {dvacc[w][dt][0], dvacc[w][dt][1], dvacc[w][dt][2], dvacc[w][dt][3]};
-        store4(dKg + (long)key * ts + dt * 16 + 4 * g, kv);
-        store4(dVg + (long)key * ts + dt * 16 + 4 * g, vv);
-      }
-    }
-  }
-  if (dbp != nullptr) {
-    // lane (l16, g) holds column d = dt*16 + 4g + i of 16 keys: sum the key tiles, the 16 lanes
-    // of the DPP row, then the waves through LDS
-#pragma unroll
-    for (int dt = 0; dt < DT; ++dt)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        float sk = 0.f, sv = 0.f;
-#pragma unroll
-        for (int w = 0; w < NKW; ++w) {
-          sk += dkacc[w][dt][i];
-          sv += dvacc[w][dt][i];
-        }
-        sk = row16_sum(sk);
-        sv = row16_sum(sv);
-        if (l16 == 0) {
-          const int d = dt * 16 + 4 * g + i;
-          atomicAdd(&bsum[HD + d], sk * scale);
-          atomicAdd(&bsum[2 * HD + d], sv);
-        }
-      }
-    __syncthreads();
-    float* dst = dbp + (long)b * ts + h * HD;
-    for (int i = threadIdx.x; i < 3 * HD; i += NTH) dst[(i / HD) * H * HD + (i % HD)] = bsum[i];
-  }
-}
-
+// (the r1 one-workgroup-per-(b, h) backward with padded LDS images was replaced by the compact and
+// batched kernels below: profiles/r1_attn_bench_v3.txt, r1_attn_bwd3.txt; removed)
 // ------------------------------------------------------------------ backward, compact variant
-// Same math and MFMA orientation as attn_bwd_kernel, re-laid out so two or more workgroups fit a
+// S = softmax(Q K^T) recomputed from the saved lse, dV = P^T dO, dS = P (dP - delta), dK = dS^T Q,
+// dQ = dS K; laid out so that two or more workgroups fit a
 // CU (their barriers and staging then overlap each other's MFMA work):
 //  * Q, dO, K images are unpadded [SP][HD] rows with the 16-byte chunks XOR-swizzled by aswz(row)
 //    (a GF(2) map found by exhaustive search: conflict-free for the ds_read_b128 fragment reads AND
@@ -864,20 +558,13 @@ JM_DEVICE int swo(int row, int col) {
   return row * (NCH * 8) + ((((col >> 3) ^ aswz(row)) & (NCH - 1)) << 3) + (col & 7);
 }
 
-template <int HD, int SP, bool DB = false>
-constexpr size_t bwd2_smem() {  // dynamic part (DB: + 2 x 4 static images)
-  return (size_t)((DB ? 0 : 3) * SP * HD + SP * 64) * 2 + (2 * SP + 3 * HD) * sizeof(float);
+template <int HD, int SP>
+constexpr size_t bwd2_smem() {
+  return (size_t)(3 * SP * HD + SP * 64) * 2 + (2 * SP + 3 * HD) * sizeof(float);
 }
 
-// DB (double-buffered, SP = HD = 64: the encoder): the Q / dO / K / O images of the NEXT batch
-// element are DMA'd global -> LDS (buffer_load ... lds, 16 B per lane, the chunk swizzle applied
-// on the global side) into the second image set while this element computes, instead of a
-// register burst whose latency is exposed once per element; V fragments and lse of the next
-// element are prefetched into registers.  delta = O . dO is then taken from the LDS images.
-template <int HD, int SP, bool DB>
-constexpr int bwd2_imgs() { return DB ? 0 : 3; }  // DB: the image sets are static LDS arrays
 
-template <int HD, int SP, bool DB = false>
+template <int HD, int SP>
 __global__ __launch_bounds__(256) void attn_bwd2_kernel(const uint16_t* __restrict__ qkv,
                                                         const uint16_t* __restrict__ o,
                                                         const uint16_t* __restrict__ dO,
@@ -885,7 +572,6 @@ __global__ __launch_bounds__(256) void attn_bwd2_kernel(const uint16_t* __restri
                                                         uint16_t* __restrict__ dqkv, int S, int H, float scale,
                                                         float* __restrict__ dbp, int B, int ppw, int remap) {
   JM_DGUARD(S >= 1 && S <= SP && blockDim.x == 256 && ppw >= 1);
-  static_assert(!DB || (SP == 64 && HD == 64), "double-buffered backward: S <= 64, hd 64");
   constexpr int NW = 4, NTH = 256, QC = 64;
   constexpr int NT = SP / 16, KK = HD / 32, DT = HD / 16;
   constexpr int NKW = (NT + NW - 1) / NW;
@@ -895,12 +581,7 @@ __global__ __launch_bounds__(256) void attn_bwd2_kernel(const uint16_t* __restri
   uint16_t* Qs = smem;
   uint16_t* dOs = Qs + IMG;
   uint16_t* Ks = dOs + IMG;
-  uint16_t* dSt = smem + bwd2_imgs<HD, SP, DB>() * IMG;  // [SP][QC], 8 chunks per row
-  uint16_t* img[2] = {nullptr, nullptr};
-  if constexpr (DB) {
-    img[0] = lds_images<4 * IMG, 0>();
-    img[1] = lds_images<4 * IMG, 1>();
-  }
+  uint16_t* dSt = smem + 3 * IMG;  // [SP][QC], 8 chunks per row
   float* lse_s = reinterpret_cast<float*>(dSt + SP * QC);
   float* delta_s = lse_s + SP;
   float* bsum = delta_s + SP;
@@ -987,115 +668,14 @@ __global__ __launch_bounds__(256) void attn_bwd2_kernel(const uint16_t* __restri
     lsen = (i < SP && i < S) ? lse[((long)b * H + h) * S + i] * LOG2E : INFINITY;
   };
 
-  // DB: the Q / dO / K / O images of element b DMA'd into image set k (16-row slabs per wave,
-  // 8 rows x 8 chunks per instruction; rows >= S read as zero through the buffer range)
-  auto issue_glds = [&](int b, uint16_t* dst) {
-    const uint16_t* base = qkv + (long)b * S * ts;
-    const i32x4_t rs[4] = {rsrc4(base + h * HD, (S - 1) * ts * 2 + HD * 2),
-                           rsrc4(dO + (long)b * S * os + h * HD, (S - 1) * os * 2 + HD * 2),
-                           rsrc4(base + (H + h) * HD, (S - 1) * ts * 2 + HD * 2),
-                           rsrc4(o + (long)b * S * os + h * HD, (S - 1) * os * 2 + HD * 2)};
-    const long strides[4] = {ts, os, ts, os};
-#pragma unroll
-    for (int t = 0; t < 4; ++t)
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        const int row0 = 16 * wave + 8 * u, row = row0 + (lane >> 3);
-        const int c = (lane & 7) ^ aswz(row);
-        blds16_asm(rs[t], (uint32_t)(row * strides[t] * 2 + c * 16), dst + t * IMG + row0 * HD);
-      }
-  };
-  // V fragments and lse of element b into the prefetch registers: unconditional loads (clamped
-  // rows, masked after) so every wave issues the same number of vector-memory instructions
-  // (inline-asm loads: the compiler neither waits for them nor counts them -- the explicit counted
-  // wait at the top of the next element, tied to these registers, does; the padded-key zeroing and
-  // the lse select happen when the registers are consumed)
-  float lse_raw = 0.f;
-  static_assert(!DB || (NKW == 1 && KK == 2), "DB prefetch registers: one key tile, two V fragments");
-  auto load_vl = [&](int b) {
-    const uint16_t* Vg = qkv + (long)b * S * ts + (2 * H + h) * HD;
-#pragma unroll
-    for (int w = 0; w < NKW; ++w) {
-      const int key = (wave + NW * w) * 16 + l16;
-      const int kc = key < S ? key : S - 1;
-#pragma unroll
-      for (int kk = 0; kk < KK; ++kk) {
-        const uint16_t* pv = Vg + (long)kc * ts + 32 * kk + 8 * g;
-        asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(vfn[w][kk]) : "v"(pv) : "memory");
-      }
-    }
-    const int i = threadIdx.x;
-    const float* pl = lse + ((long)b * H + h) * S + (i < S ? i : S - 1);
-    asm volatile("global_load_dword %0, %1, off" : "=v"(lse_raw) : "v"(pl) : "memory");
-  };
-  if constexpr (DB) {
-    if (bg * ppw < B) {
-      issue_glds(bg * ppw, img[0]);
-      load_vl(bg * ppw);
-    }
-  }
-
-  // one batch element; BUF = its image set (DB: compile-time, so the LDS reads of this set and
-  // the DMA into the other one are provably disjoint and the compiler adds no vmcnt wait between)
-  auto pair = [&](const int pj, auto bufc) -> bool {
-  constexpr int BUF = decltype(bufc)::value;
+  // one batch element
+  auto pair = [&](const int pj) -> bool {
   const int b = bg * ppw + pj;
   if (b >= B) return false;  // workgroup-uniform
   uint16_t* dQg = dqkv + (long)b * S * ts + h * HD;
   uint16_t* dKg = dqkv + (long)b * S * ts + (H + h) * HD;
   uint16_t* dVg = dqkv + (long)b * S * ts + (2 * H + h) * HD;
 
-  if constexpr (DB) {
-    Qs = img[BUF];
-    dOs = Qs + IMG;
-    Ks = dOs + IMG;
-    const uint16_t* Os = Ks + IMG;
-    // next element's images DMA'd now (they land while this one computes), then this element's
-    // V fragments / lse leave the prefetch registers, then the next element's are loaded
-    // issued unconditionally (the last element re-fetches itself into the idle image set) so
-    // every path has the same outstanding-load count for the counted wait below
-    const bool nxt = pj + 1 < ppw && b + 1 < B;
-    const int bn = nxt ? b + 1 : b;
-    issue_glds(bn, img[1 - BUF]);
-    // this element's DMA and V / lse loads (older than the 8 DMA just issued) have landed
-    asm volatile("s_waitcnt vmcnt(8)" : "+v"(vfn[0][0]), "+v"(vfn[0][1]), "+v"(lse_raw) : : "memory");
-#pragma unroll
-    for (int w = 0; w < NKW; ++w) {
-      const bool kin = (wave + NW * w) * 16 + l16 < S;
-#pragma unroll
-      for (int kk = 0; kk < KK; ++kk) {
-        s16x8_t z = {0, 0, 0, 0, 0, 0, 0, 0};
-        vf[w][kk] = kin ? vfn[w][kk] : __builtin_bit_cast(bf16x8_t, z);
-      }
-    }
-    const float lcur = ((int)threadIdx.x < S) ? lse_raw * LOG2E : INFINITY;
-    load_vl(bn);
-    if (threadIdx.x < SP) {
-      delta_s[threadIdx.x] = 0.f;
-      lse_s[threadIdx.x] = lcur;
-    }
-    wg_bar<DB>();
-#pragma unroll
-    for (int it = 0; it < NIT; ++it) {
-      const int i = it * NTH + threadIdx.x;
-      const int r = i / NCH, c = (i % NCH) * 8;
-      if (i < SP * NCH && r < S) {
-        const int off = swo<NCH>(r, c);
-        const uint4 ovv = *reinterpret_cast<const uint4*>(Os + off);
-        const uint4 dvv = *reinterpret_cast<const uint4*>(dOs + off);
-        const uint32_t* ow = reinterpret_cast<const uint32_t*>(&ovv);
-        const uint32_t* dw = reinterpret_cast<const uint32_t*>(&dvv);
-        float dsum = 0.f;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          dsum += __uint_as_float(ow[j] << 16) * __uint_as_float(dw[j] << 16);
-          dsum += __uint_as_float(ow[j] & 0xffff0000u) * __uint_as_float(dw[j] & 0xffff0000u);
-        }
-        atomicAdd(&delta_s[r], dsum);
-      }
-    }
-    wg_bar<DB>();
-  } else {
   load_regs(b);
 #pragma unroll
   for (int w = 0; w < NKW; ++w)
@@ -1130,7 +710,6 @@ __global__ __launch_bounds__(256) void attn_bwd2_kernel(const uint16_t* __restri
     }
   }
   __syncthreads();
-  }  // !DB staging
 
   bf16x8_t kf[NKW][KK];
   f32x4_t dvacc[NKW][DT], dkacc[NKW][DT];
@@ -1196,7 +775,7 @@ __global__ __launch_bounds__(256) void attn_bwd2_kernel(const uint16_t* __restri
         }
       }
     }
-    wg_bar<DB>();
+    __syncthreads();
     // dQ^T[d][q] = sum_key K^T[d][key] dS^T[key][q] for this wave's 16 queries of the chunk
     {
       const int qt = qc * (QC / 16) + wave;
@@ -1229,7 +808,7 @@ __global__ __launch_bounds__(256) void attn_bwd2_kernel(const uint16_t* __restri
         }
       }
     }
-    wg_bar<DB>();
+    __syncthreads();
   }
 #pragma unroll
   for (int w = 0; w < NKW; ++w) {
@@ -1257,17 +836,8 @@ __global__ __launch_bounds__(256) void attn_bwd2_kernel(const uint16_t* __restri
       }
   return true;
   };  // batch element
-  if constexpr (DB) {
-    for (int pj = 0; pj < ppw; pj += 2) {
-      if (!pair(pj, IC<0>{})) break;
-      if (pj + 1 >= ppw || !pair(pj + 1, IC<1>{})) break;
-    }
-    // the last element's (dummy) DMA must land before the workgroup's LDS is released
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  } else {
-    for (int pj = 0; pj < ppw; ++pj)
-      if (!pair(pj, IC<0>{})) break;
-  }
+  for (int pj = 0; pj < ppw; ++pj)
+    if (!pair(pj)) break;
   if (dbp != nullptr) {
 #pragma unroll
     for (int dt = 0; dt < DT; ++dt)
@@ -1580,52 +1150,43 @@ __global__ __launch_bounds__(256) void attn_bwd3_kernel(const uint16_t* __restri
   }
 }
 
-template <int HD, int SP, bool TR>
-size_t fwd_smem() { return (size_t)(SP * (HD + 8) + (TR ? SP * (HD + 8) : HD * (SP + 8))) * 2; }
-template <int HD, int SP, bool TR>
-size_t bwd_smem() {
-  return (size_t)(4 * SP * (HD + 8) + (TR ? 0 : 3 * HD * (SP + 8)) + 16 * bwd_waves<HD, SP>() * (SP + 8)) * 2 +
-         (2 * SP + 3 * HD) * sizeof(float);
-}
+// forward images: row-major Q and V (V^T operands through ds_read_b64_tr_b16)
+template <int HD, int SP>
+size_t fwd_smem() { return (size_t)(2 * SP * (HD + 8)) * 2; }
 
 int g_attn_remap = 3;  // runtime switch: bit 0 XCD-aware workgroup -> (b, h) order (xcd_bid), bit 1 forward
                        // Q prefetch + batched K / V staging; dec fwd 175 -> 163 us, bwd 361 -> 340 us
                        // (profiles/r2_attn_remap.txt)
-int g_use_tr = 3;  // runtime switch: 3 = batched backward (bwd3) for hd 32, 2 = compact backward (bwd2) + TR
-                   // forward, 1 = TR, 0 = transposed images
+int g_use_tr = 3;  // runtime switch: 3 = batched backward (bwd3) for hd 32, 2 = compact backward (bwd2)
 
-template <int HD, int SP, bool TR>
-int run_t(bool fwd, const uint16_t* qkv, const uint16_t* o, const uint16_t* dO, const float* lse_in, uint16_t* out,
-          float* lse_out, int B, int S, int H, float scale, hipStream_t st) {
+// one (b, h) per workgroup (S > 64; the short encoder sequences take the multi-pair kernel)
+template <int HD, int SP>
+int run_fwd(const uint16_t* qkv, uint16_t* out, float* lse_out, int B, int S, int H, float scale, hipStream_t st) {
   dim3 grid(B * H);
-  const size_t sm = fwd ? fwd_smem<HD, SP, TR>() : bwd_smem<HD, SP, TR>();
+  const size_t sm = fwd_smem<HD, SP>();
   if (sm > 160 * 1024) return -3;
-  const void* fn = fwd ? (const void*)attn_fwd_kernel<HD, SP, TR> : (const void*)attn_bwd_kernel<HD, SP, TR>;
-  static bool attr_set[2] = {false, false};
-  if (sm > 64 * 1024 && !attr_set[fwd ? 0 : 1]) {
-    hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
-    attr_set[fwd ? 0 : 1] = true;
-  }
-  if (fwd && S > SP - 32) {
+  if (S > SP - 32) {
     static bool attr_ex = false;
     if (sm > 64 * 1024 && !attr_ex) {
-      (void)hipFuncSetAttribute((const void*)attn_fwd_kernel<HD, SP, TR, true>,
+      (void)hipFuncSetAttribute((const void*)attn_fwd_kernel<HD, SP, true, true>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
       attr_ex = true;
     }
-    attn_fwd_kernel<HD, SP, TR, true><<<grid, 256, sm, st>>>(qkv, out, lse_out, S, H, scale, g_attn_remap);
-  } else if (fwd)
-    attn_fwd_kernel<HD, SP, TR><<<grid, 256, sm, st>>>(qkv, out, lse_out, S, H, scale, g_attn_remap);
-  else
-    attn_bwd_kernel<HD, SP, TR><<<grid, 64 * bwd_waves<HD, SP>(), sm, st>>>(qkv, o, dO, lse_in, out, S, H, scale,
-                                                                          lse_out);
+    attn_fwd_kernel<HD, SP, true, true><<<grid, 256, sm, st>>>(qkv, out, lse_out, S, H, scale, g_attn_remap);
+  } else {
+    static bool attr = false;
+    if (sm > 64 * 1024 && !attr) {
+      (void)hipFuncSetAttribute((const void*)attn_fwd_kernel<HD, SP, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)sm);
+      attr = true;
+    }
+    attn_fwd_kernel<HD, SP, true><<<grid, 256, sm, st>>>(qkv, out, lse_out, S, H, scale, g_attn_remap);
+  }
   return 0;
 }
 
 // runtime switch: batch elements per bwd2 workgroup (one head each); 0 = auto (bwd_ppw)
 int g_bwd_ppw = 0;
-// runtime switch: double-buffered (LDS-DMA prefetch of the next element) bwd2 at S <= 64, hd 64
-int g_bwd2_db = 0;
 // runtime switch: the batched backward (bwd3) also for head dim 64 at S > 64 (finetune S = 199);
 // 2: also at S <= 64 (the encoder, A/B)
 int g_bwd3_hd64 = 1;  // finetune S=199 hd=64 backward 249 -> 177 us (profiles/r2_attn_ft_bwd.txt)
@@ -1668,20 +1229,6 @@ int run_bwd2(const uint16_t* qkv, const uint16_t* o, const uint16_t* dO, const f
 bwd2:
   {
     const int ppw = bwd_ppw<HD, SP>();
-    if constexpr (HD == 64 && SP == 64) {
-      if (g_bwd2_db) {  // double-buffered LDS-DMA variant (the encoder)
-        constexpr size_t smd = bwd2_smem<HD, SP, true>();
-        static bool attr_db = false;
-        if (!attr_db) {
-          (void)hipFuncSetAttribute((const void*)attn_bwd2_kernel<HD, SP, true>,
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)smd);
-          attr_db = true;
-        }
-        attn_bwd2_kernel<HD, SP, true><<<dim3(((B + ppw - 1) / ppw) * H), 256, smd, st>>>(
-            qkv, o, dO, lse_in, out, S, H, scale, dbias_part, B, ppw, g_attn_remap);
-        return 0;
-      }
-    }
     attn_bwd2_kernel<HD, SP><<<dim3(((B + ppw - 1) / ppw) * H), 256, sm, st>>>(qkv, o, dO, lse_in, out, S, H, scale,
                                                                               dbias_part, B, ppw, g_attn_remap);
   }
@@ -1695,7 +1242,7 @@ int g_fwd_hpw = 0;
 
 template <int HD, int SP>
 int run_fwd_ml(const uint16_t* qkv, uint16_t* out, float* lse_out, int B, int S, int H, float scale, hipStream_t st) {
-  const size_t sm = fwd_smem<HD, SP, true>();
+  const size_t sm = fwd_smem<HD, SP>();
   static bool attr_set[2] = {false, false};
   const bool ex = S > SP - 32;
   const void* fn = ex ? (const void*)attn_fwd_ml_kernel<HD, SP, true> : (const void*)attn_fwd_ml_kernel<HD, SP>;
@@ -1716,11 +1263,10 @@ int run_fwd_ml(const uint16_t* qkv, uint16_t* out, float* lse_out, int B, int S,
 template <int HD, int SP>
 int run(bool fwd, const uint16_t* qkv, const uint16_t* o, const uint16_t* dO, const float* lse_in, uint16_t* out,
         float* lse_out, int B, int S, int H, float scale, hipStream_t st) {
-  if (fwd && g_use_tr && (g_fwd_hpw > 1 || (g_fwd_hpw == 0 && SP <= 64)))
+  if (fwd && (g_fwd_hpw > 1 || (g_fwd_hpw == 0 && SP <= 64)))
     return run_fwd_ml<HD, SP>(qkv, out, lse_out, B, S, H, scale, st);
-  if (g_use_tr >= 2 && !fwd) return run_bwd2<HD, SP>(qkv, o, dO, lse_in, out, lse_out, B, S, H, scale, st);
-  if (g_use_tr) return run_t<HD, SP, true>(fwd, qkv, o, dO, lse_in, out, lse_out, B, S, H, scale, st);
-  return run_t<HD, SP, false>(fwd, qkv, o, dO, lse_in, out, lse_out, B, S, H, scale, st);
+  if (!fwd) return run_bwd2<HD, SP>(qkv, o, dO, lse_in, out, lse_out, B, S, H, scale, st);
+  return run_fwd<HD, SP>(qkv, out, lse_out, B, S, H, scale, st);
 }
 
 template <int HD>
@@ -2100,12 +1646,11 @@ int run_long_bwd(const uint16_t* qkv, const uint16_t* o, const uint16_t* dO, con
 int g_attn_max_seq = 224;
 int jm_attn_max_seq() { return g_attn_max_seq; }
 void jm_attn_set_max_seq(int v) { g_attn_max_seq = v < 32 ? 32 : (v > 224 ? 224 : v); }
-void jm_attn_set_tr(int v) { g_use_tr = v; }
+void jm_attn_set_tr(int v) { g_use_tr = v >= 3 ? 3 : 2; }
 void jm_attn_set_remap(int v) { g_attn_remap = v; }
 void jm_attn_set_fwd_hpw(int v) { g_fwd_hpw = v < 0 ? 0 : v; }
 void jm_attn_set_bwd_ppw(int v) { g_bwd_ppw = v < 0 ? 0 : v; }
 void jm_attn_set_bwd3_hd64(int v) { g_bwd3_hd64 = v; }
-void jm_attn_set_bwd2_db(int v) { g_bwd2_db = v; }
 
 // rows of the dbias_part workspace that jm_attn_bwd writes: the bwd2 kernel folds ``ppw`` batch
 // elements into one row, every other backward writes one row per batch element.  Must mirror the

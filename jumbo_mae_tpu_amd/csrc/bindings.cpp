@@ -17,7 +17,6 @@ int jm_layernorm_bwd(const void* dy, int dy_bf16, const float* x, long sB, long 
                      const JmLnRes* res, hipStream_t st);
 int jm_layernorm_bwd_blocks(int rows, int D);
 void jm_ln_set_bwd_blocks(int v);
-void jm_ln_set_bwd_la(int v);
 void jm_ln_set_direct(int v);
 // debug build (-DJM_DEBUG): first failing soft-check line per kernel translation unit (0 = none;
 // reading clears it); always 0 in the release build
@@ -60,7 +59,6 @@ void jm_attn_set_remap(int v);
 void jm_attn_set_fwd_hpw(int v);
 void jm_attn_set_bwd_ppw(int v);
 void jm_attn_set_bwd3_hd64(int v);
-void jm_attn_set_bwd2_db(int v);
 int jm_attn_bwd_part_rows(int B, int S, int hd);
 int jm_attn_bwd_long(const uint16_t* qkv, const uint16_t* o, const uint16_t* dO, const float* lse, uint16_t* dqkv,
                      float* delta, int B, int S, int H, int hd, hipStream_t st);
@@ -84,18 +82,10 @@ int jm_gemm_nt(const uint16_t* A, long lda, const uint16_t* B, long ldb, int M, 
                const GemmEpi& ep, hipStream_t st);
 void jm_gemm_set_variant(int wn, int group);
 void jm_gemm_set_tail(int on);
-void jm_gemm_set_sk(int on);
-void jm_gemm_set_pp(int on);
 int jm_gemm_nt_tail_plan(int M, int N, int K, int epi, int* tail_r, long* ws_floats);
 int jm_gemm_tn_plan(int M, int N, int K, int* S_out);
 int jm_gemm_tn(const uint16_t* A, long lda, const uint16_t* B, long ldb, int M, int N, int K, int sps, int S,
                float* G, long ldo, float* partial, hipStream_t st);
-int jm_gemm_tn_acc0();
-void jm_gemm_tn_set_acc0(int v);
-int jm_gemm_tn_atomic();
-void jm_gemm_tn_set_atomic(int v);
-void jm_gemm_tn_set_red_scale(double v);
-void jm_gemm_tn_set_variant(int v);
 struct TnSegs {
   const uint16_t* a[32];
   const uint16_t* b[32];
@@ -790,13 +780,12 @@ int64_t gemm_tn_wgrad(torch::Tensor dy, torch::Tensor x, torch::Tensor g) {
   int S = 1;
   const int sps = jm_gemm_tn_plan(M, N, K, &S);
   torch::Tensor part;
-  // partial slices (split 0 may accumulate into g directly; none when the splits add atomically)
-  const int SP = jm_gemm_tn_atomic() ? 0 : S - jm_gemm_tn_acc0();
-  if (S > 1 && SP > 0) part = torch::empty({SP, (long)N * K}, g.options());
+  const int SP = S;  // fp32 partial slices, reduced into g
+  if (S > 1) part = torch::empty({SP, (long)N * K}, g.options());
   check_rc(jm_gemm_tn(bf(dy), dy.stride(0), bf(x), x.stride(0), M, N, K, sps, S, g.data_ptr<float>(), K,
-                      S > 1 && SP > 0 ? part.data_ptr<float>() : nullptr, stream()),
+                      S > 1 ? part.data_ptr<float>() : nullptr, stream()),
            "gemm_tn_wgrad");
-  if (S > 1 && SP > 0) check_rc(jm_splitk_reduce_add(part.data_ptr<float>(), g.data_ptr<float>(), (long)N * K, SP, stream()),
+  if (S > 1) check_rc(jm_splitk_reduce_add(part.data_ptr<float>(), g.data_ptr<float>(), (long)N * K, SP, stream()),
                       "gemm_tn_wgrad reduce");
   return S;
 }
@@ -828,12 +817,12 @@ int64_t gemm_tn_wgrad_seg(std::vector<torch::Tensor> dys, std::vector<torch::Ten
   int S = 1;
   const int sps = jm_gemm_tn_plan(M, N, K, &S);
   torch::Tensor part;
-  const int SP = (jm_gemm_tn_atomic() && rows % 64 == 0) ? 0 : S - jm_gemm_tn_acc0();
-  if (S > 1 && SP > 0) part = torch::empty({SP, (long)N * K}, g.options());
+  const int SP = S;
+  if (S > 1) part = torch::empty({SP, (long)N * K}, g.options());
   check_rc(jm_gemm_tn_seg(segs, d0.stride(0), x0.stride(0), N, K, sps, S, g.data_ptr<float>(), K,
-                          S > 1 && SP > 0 ? part.data_ptr<float>() : nullptr, stream()),
+                          S > 1 ? part.data_ptr<float>() : nullptr, stream()),
            "gemm_tn_wgrad_seg");
-  if (S > 1 && SP > 0) check_rc(jm_splitk_reduce_add(part.data_ptr<float>(), g.data_ptr<float>(), (long)N * K, SP, stream()),
+  if (S > 1) check_rc(jm_splitk_reduce_add(part.data_ptr<float>(), g.data_ptr<float>(), (long)N * K, SP, stream()),
                       "gemm_tn_wgrad_seg reduce");
   return S;
 }
@@ -923,16 +912,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("attn_set_max_seq", &jm_attn_set_max_seq);
   m.def("gemm_tn_wgrad", &gemm_tn_wgrad);
   m.def("gemm_tn_wgrad_seg", &gemm_tn_wgrad_seg);
-  m.def("gemm_set_variant", &jm_gemm_set_variant, py::arg("wn"), py::arg("group") = 8);
+  m.def("gemm_set_variant", &jm_gemm_set_variant, py::arg("nt64"), py::arg("group") = 8,
+        "nt64 = 1: every NT launch on the 64-deep main loop (tests); group: row tiles per column sweep");
   m.def("gemm_set_tail", &jm_gemm_set_tail);
   m.def("transpose_bf16_batch", &transpose_bf16_batch);
   m.def("ln_set_bwd_blocks", &jm_ln_set_bwd_blocks);
-  m.def("gemm_set_pp", &jm_gemm_set_pp, "persistent overlapped NT launch for multi-round grids (1, default) or tiled (0)");
-  m.def("gemm_set_sk", &jm_gemm_set_sk, "persistent DP + stream-K NT launches where they pay (1, default) or never (0)");
-  m.def("gemm_tn_set_acc0", &jm_gemm_tn_set_acc0);
-  m.def("gemm_tn_set_atomic", &jm_gemm_tn_set_atomic);
-  m.def("gemm_tn_set_red_scale", &jm_gemm_tn_set_red_scale);
-  m.def("gemm_tn_set_variant", &jm_gemm_tn_set_variant, "TN wgrad kernel: 4 = 4-phase (default), 0 = r1 32-row steps");
   m.def("gemm_nt_splitk", &gemm_nt_splitk, py::arg("A"), py::arg("B"), py::arg("bias") = py::none(),
         py::arg("splits") = 8, py::arg("add") = py::none());
   m.def("gemm_nt_dgelu", &gemm_nt_dgelu, py::arg("A"), py::arg("B"), py::arg("pre"), py::arg("dbias") = py::none(),
@@ -941,12 +925,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("gelu_only") = false, py::arg("gelu_deriv") = false);
   m.def("attn_set_tr", &jm_attn_set_tr);
   m.def("attn_set_remap", &jm_attn_set_remap, "attention grid: bit 0 XCD-aware (b, h) order, bit 1 forward Q prefetch");
-  m.def("ln_set_bwd_la", &jm_ln_set_bwd_la);
   m.def("ln_set_direct", &jm_ln_set_direct);
   m.def("attn_set_fwd_hpw", &jm_attn_set_fwd_hpw);
   m.def("attn_set_bwd_ppw", &jm_attn_set_bwd_ppw);
   m.def("attn_set_bwd3_hd64", &jm_attn_set_bwd3_hd64);
-  m.def("attn_set_bwd2_db", &jm_attn_set_bwd2_db);
   m.def("opt_sumsq", &opt_sumsq);
   m.def("opt_adamw", &opt_adamw);
   m.def("opt_set_adamw_vec", &jm_opt_set_adamw_vec);

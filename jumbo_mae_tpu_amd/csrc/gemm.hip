@@ -6,24 +6,22 @@
 //
 // Tiling (CDNA4, 64-wide waves): one 512-thread workgroup (8 waves, 2 along M x 4 along N) owns a
 // 256 x 256 output tile; each wave a 128 x 64 sub-tile = 8 x 4 v_mfma_f32_16x16x32_bf16 tiles
-// (128 accumulator VGPRs).  K is consumed in 32-deep steps staged global -> LDS with
-// global_load_lds_dwordx4 (no VGPR round trip) through a 4-stage ring of 32 KB stages, issued 3
-// steps ahead.  One barrier per step, placed in the MIDDLE of the step: a wave issues the first
-// half of its MFMAs, then waits (counted vmcnt) for its own loads of step t+1 and joins the
-// barrier -- its MFMAs keep the matrix pipe busy meanwhile -- and then reads step t+1's fragments
-// interleaved with the second half of step t's MFMAs (fragments double-buffered in registers).
-//
-// LDS image: row-major [256][32] bf16 per operand (64 B rows), 16-byte chunks XOR-swizzled by
-// 2 * ((row >> 2) & 1) -- applied to the per-lane GLOBAL source address (glds writes lane-linear)
-// and to the ds_read address; with ds_read_b128's lane groups ({0-3,12-15,20-27}, ...) every
-// fragment read is conflict-free.
-//
+// (128 accumulator VGPRs).  Operands are staged global -> LDS with buffer_load_dwordx4 ... lds (no
+// VGPR round trip).  Two main loops:
+//   * p4 (K % 128 == 0, the default): 64-deep K-tiles cut into half-tile LDS slots whose loads stay
+//     in flight ACROSS barriers (counted vmcnt), four phases per K-tile (see p4_mainloop);
+//   * nt64 (K % 128 == 64, tail-split partial tiles): 64-deep stages through two 64 KB slots.
 // MFMA orientation: the B fragment is the MFMA "A" operand, so each lane's accumulator holds four
 // consecutive output COLUMNS of one row -- bias / activation / residual epilogues work on float4
-// runs.
+// runs.  Epilogues stage the bf16 tile through LDS and stream full 128-byte rows out.
 //
 // Workgroup -> tile map: bijective XCD remap (consecutive tile ids share an XCD and its L2), then
 // groups of 8 row-tiles sweep the column tiles.
+//
+// Measured and removed (records in profiles/, code in git history): the r1 32-deep ring kernel,
+// 4-wave (one wave per SIMD) tiles, 256 x 128 tiles at 2 workgroups per CU (with and without a
+// staggered start), persistent launches with the next tile's loads under the epilogue, persistent
+// data-parallel + stream-K with in-kernel fix-up, per-phase priority / in-stream glds schedules.
 #include <type_traits>
 
 #include "common.h"
@@ -31,8 +29,8 @@
 
 namespace {
 
-constexpr int BM = 256, BN = 256, BK = 32, NST = 4;
-constexpr int STAGE = (BM + BN) * BK;  // elements per ring stage (A then B): 32 KB
+constexpr int BM = 256, BN = 256;
+constexpr size_t GEMM_SMEM = 128 * 1024;  // p4: 8 x 16 KB slots; nt64: 2 x 64 KB slots
 
 typedef __attribute__((address_space(3))) void lds_void_t;
 
@@ -53,8 +51,6 @@ JM_DEVICE bf16x8_t lds8(const uint16_t* p) { return *reinterpret_cast<const bf16
 JM_DEVICE f32x4_t mfma16(bf16x8_t a, bf16x8_t b, f32x4_t c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
-
-JM_DEVICE int swz(int row) { return ((row >> 2) & 1) << 1; }
 
 template <int NTW>
 struct Frags {
@@ -301,157 +297,6 @@ JM_DEVICE void epilogue_lds(const f32x4_t (&acc)[8][NTW], const GemmEpi& ep, uin
   }
 }
 
-// ABL (diagnostics only, tools/gemm_nt_bench.py --variant 41/42/44): 1 = no in-loop staging
-// loads, 2 = no barrier / vmcnt wait, 4 = no fragment re-reads.  Outputs are wrong by design.
-template <int EPI, int WN, int ABL = 0>
-__global__ __launch_bounds__(128 * WN, 1) void gemm_nt_kernel(const uint16_t* __restrict__ A, long lda,
-                                                              const uint16_t* __restrict__ B, long ldb, int M,
-                                                              int N, int K, GemmEpi ep, int GROUP_M) {
-  JM_DGUARD(blockDim.x == 128 * WN && K % 64 == 0 && M > 0 && N > 0);
-  constexpr int NW = 2 * WN;          // waves
-  constexpr int NTW = BN / WN / 16;   // 16-wide column tiles per wave
-  constexpr int RND = 16 / NW;        // glds rounds per operand and stage
-  extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
-  const int tid = threadIdx.x;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
-  const int l16 = lane & 15, g = lane >> 4;
-  const int wr = wave / WN, wc = wave % WN;
-
-  int m0, n0, split = 0;
-  tile_of(M, N, GROUP_M, m0, n0, EPI == EPI_PARTIAL ? ep.splits : 1, EPI == EPI_PARTIAL ? &split : nullptr);
-  int k_begin = 0;
-  if (EPI == EPI_PARTIAL) {  // this split's K range, in units of 64
-    const int ku = K / 64;
-    const int ku0 = split * ku / ep.splits, ku1 = (split + 1) * ku / ep.splits;
-    k_begin = ku0 * 64;
-    K = (ku1 - ku0) * 64;
-  }
-
-  // ---- per-lane swizzled source offsets: RND rounds x NW waves x 16 rows per operand and stage
-  const __amdgpu_buffer_rsrc_t ra = make_rsrc(A + (long)m0 * lda + k_begin, (long)(M - m0) * lda * 2 - 2L * k_begin);
-  const __amdgpu_buffer_rsrc_t rb = make_rsrc(B + (long)n0 * ldb + k_begin, (long)(N - n0) * ldb * 2 - 2L * k_begin);
-  uint32_t a_src[RND], b_src[RND];  // byte offsets
-#pragma unroll
-  for (int rr = 0; rr < RND; ++rr) {
-    const int row = rr * 16 * NW + wave * 16 + (lane >> 2);
-    const int c = (lane & 3) ^ swz(row);
-    a_src[rr] = (uint32_t)((row * lda + c * 8) * 2);
-    b_src[rr] = (uint32_t)((row * ldb + c * 8) * 2);
-  }
-  auto issue = [&](int t) {
-    const uint32_t k0b = t * BK * 2;
-    uint16_t* la = smem + (t % NST) * STAGE;
-    uint16_t* lb = la + BM * BK;
-#pragma unroll
-    for (int rr = 0; rr < RND; ++rr) {
-      blds16(ra, a_src[rr], k0b, la + (rr * 16 * NW + wave * 16) * BK);
-      blds16(rb, b_src[rr], k0b, lb + (rr * 16 * NW + wave * 16) * BK);
-    }
-  };
-  // fragment reads: row * 32 + swizzled chunk * 8; swz(row) == swz(l16) for these rows
-  const int ch = (g ^ swz(l16)) * 8;
-  const int a_off = (wr * 128 + l16) * BK + ch;
-  const int b_off = BM * BK + (wc * NTW * 16 + l16) * BK + ch;
-  auto read = [&](int t, Frags<NTW>& f) {
-    const uint16_t* base = smem + (t % NST) * STAGE;
-#pragma unroll
-    for (int nt = 0; nt < NTW; ++nt) f.b[nt] = lds8(base + b_off + nt * 16 * BK);
-#pragma unroll
-    for (int mt = 0; mt < 8; ++mt) f.a[mt] = lds8(base + a_off + mt * 16 * BK);
-  };
-
-  f32x4_t acc[8][NTW];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < NTW; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-
-  // one K step: MFMAs of cur (rows 0-3 | barrier for step t+1 | rows 4-7 beside the reads of
-  // nxt).  KIND: 3 = steady (issue t+3, 2 stages left in flight), 2 / 1 = ring draining,
-  // 0 = last step.  Compile-time so each step is one basic block the scheduler can interleave.
-  auto wait_bar = [&](auto outstanding_stages) {  // vmcnt counts this thread's glds (2 * RND per stage)
-    constexpr int N = decltype(outstanding_stages)::value * 2 * RND;
-    if constexpr (N == 16) asm volatile("s_waitcnt vmcnt(16) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-  };
-  auto step = [&](auto kind, int t, Frags<NTW>& cur, Frags<NTW>& nxt) {
-    constexpr int KIND = decltype(kind)::value;
-    if constexpr (KIND == 3 && !(ABL & 1)) issue(t + 3);
-#pragma unroll
-    for (int mt = 0; mt < 4; ++mt)
-#pragma unroll
-      for (int nt = 0; nt < NTW; ++nt) acc[mt][nt] = mfma16(cur.b[nt], cur.a[mt], acc[mt][nt]);
-    __builtin_amdgcn_sched_barrier(0);
-    if constexpr (KIND > 0 && !(ABL & 2)) wait_bar(std::integral_constant<int, (ABL & 1) ? 0 : KIND - 1>{});
-    __builtin_amdgcn_sched_barrier(0);
-    if constexpr (KIND > 0 && !(ABL & 4)) read(t + 1, nxt);
-    if constexpr (KIND > 0 && (ABL & 4)) nxt = cur;
-#pragma unroll
-    for (int mt = 4; mt < 8; ++mt)
-#pragma unroll
-      for (int nt = 0; nt < NTW; ++nt) acc[mt][nt] = mfma16(cur.b[nt], cur.a[mt], acc[mt][nt]);
-    if constexpr (KIND > 0) {
-      constexpr int NR = NTW + 8, NM = 4 * NTW, PER = NM / NR;  // reads, MFMAs, MFMAs per read
-#pragma unroll
-      for (int i = 0; i < NR; ++i) {
-        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);    // 1 ds_read of the next step
-        __builtin_amdgcn_sched_group_barrier(0x008, PER, 0);  // MFMAs
-      }
-      __builtin_amdgcn_sched_group_barrier(0x008, NM - PER * NR, 0);
-    }
-    __builtin_amdgcn_sched_barrier(0);
-  };
-  using K3 = std::integral_constant<int, 3>;
-  using K2 = std::integral_constant<int, 2>;
-  using K1 = std::integral_constant<int, 1>;
-  using K0 = std::integral_constant<int, 0>;
-
-  const int nk = K / BK;  // even, >= 2 (host checks K % 64 == 0)
-  issue(0);
-  issue(1);
-  if (nk > 2) {
-    issue(2);
-    wait_bar(std::integral_constant<int, 2>{});
-  } else {
-    wait_bar(std::integral_constant<int, 1>{});
-  }
-  __builtin_amdgcn_sched_barrier(0);
-  Frags<NTW> f0, f1;
-  read(0, f0);
-  int t = 0;
-  for (; t + 4 < nk; t += 2) {
-    step(K3{}, t, f0, f1);
-    step(K3{}, t + 1, f1, f0);
-  }
-  if (nk - t == 4) {
-    step(K3{}, t, f0, f1);
-    step(K2{}, t + 1, f1, f0);
-    t += 2;
-  }
-  step(K1{}, t, f0, f1);
-  step(K0{}, t + 1, f1, f0);
-
-  if (EPI == EPI_PARTIAL) {
-    float* dst = ep.part + (long)split * M * N;
-#pragma unroll
-    for (int mt = 0; mt < 8; ++mt) {
-      const int m = m0 + wr * 128 + mt * 16 + l16;
-      if (m >= M) continue;
-#pragma unroll
-      for (int nt = 0; nt < NTW; ++nt) {
-        const int n = n0 + wc * NTW * 16 + nt * 16 + 4 * g;
-        if (n >= N) continue;
-        float v[4] = {acc[mt][nt][0], acc[mt][nt][1], acc[mt][nt][2], acc[mt][nt][3]};
-        store4(dst + (long)m * N + n, v);
-      }
-    }
-  } else if (N % 8 == 0)
-    epilogue_lds<EPI, NTW, 128 * WN>(acc, ep, smem, M, N, m0, n0, wr, wc, l16, g);
-  else
-    epilogue<EPI, NTW>(acc, ep, M, N, m0 + wr * 128, n0 + wc * NTW * 16, l16, g);
-}
 
 // ------------------------------------------------------------------ 128-byte-row variant
 // Same tile, waves and epilogues as gemm_nt_kernel, but K is staged 64 deep: every operand row of
@@ -465,7 +310,7 @@ __global__ __launch_bounds__(128 * WN, 1) void gemm_nt_kernel(const uint16_t* __
 // halves (brute-forced over the four lane groups).
 JM_DEVICE int swz64(int row) { return (row >> 1) & 7; }
 
-template <int EPI, bool LATE, bool PRIO, bool NTS = false>
+template <int EPI, bool NTS>
 __attribute__((always_inline)) JM_DEVICE void nt64_body(const uint16_t* __restrict__ A, long lda,
                                                         const uint16_t* __restrict__ B, long ldb, int M, int N,
                                                         int K, const GemmEpi& ep, int GROUP_M, uint16_t* smem) {
@@ -556,14 +401,7 @@ __attribute__((always_inline)) JM_DEVICE void nt64_body(const uint16_t* __restri
     __builtin_amdgcn_sched_barrier(0);
     mfma_rows(R0{}, f1);
     __builtin_amdgcn_sched_barrier(0);
-    if constexpr (KIND > 0 && LATE) {
-      mfma_rows(R4{}, f1);
-      __builtin_amdgcn_sched_barrier(0);
-      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-      __builtin_amdgcn_sched_barrier(0);
-      if constexpr (KIND == 2) issue(u + 2);
-      read(u + 1, H0{}, f0);
-    } else if constexpr (KIND > 0) {
+    if constexpr (KIND > 0) {
       asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);
       if constexpr (KIND == 2) issue(u + 2);
@@ -580,7 +418,6 @@ __attribute__((always_inline)) JM_DEVICE void nt64_body(const uint16_t* __restri
   using K0 = std::integral_constant<int, 0>;
 
   const int nst = K / BK2;  // >= 1 (host checks K % 64 == 0)
-  if (PRIO) __builtin_amdgcn_s_setprio(1);
   issue(0);
   if (nst > 1) {
     issue(1);
@@ -595,7 +432,6 @@ __attribute__((always_inline)) JM_DEVICE void nt64_body(const uint16_t* __restri
   for (; u + 2 < nst; ++u) stage(K2{}, u, f0, f1);
   if (u + 1 < nst) stage(K1{}, u++, f0, f1);
   stage(K0{}, u, f0, f1);
-  if (PRIO) __builtin_amdgcn_s_setprio(0);
 
   if (EPI == EPI_TAIL) {  // compact fp32 partial tile: tail[split][tg][256][256] (rows past M unused)
     float* dst = ep.tail + ((long)split * ep.t_count + tg) * (BM * BN);
@@ -629,21 +465,13 @@ __attribute__((always_inline)) JM_DEVICE void nt64_body(const uint16_t* __restri
     epilogue<EPI, NTW>(acc, ep, M, N, m0 + wr * 128, n0 + wc * NTW * 16, l16, g);
 }
 
-// SCHED (A/B): bit 0 = stagger -- waves 4-7 (the SIMD partners of waves 0-3) issue ALL their
-// half-B MFMAs before the barrier and read the next stage after it, so one wave of each SIMD pair
-// has matrix work queued while the other waits; bit 1 = s_setprio 1 for waves 4-7.  The two
-// halves run separately inlined bodies (no live ranges shared across the branch).
-template <int EPI, int SCHED = 0>
+template <int EPI, bool NTS>
 __global__ __launch_bounds__(512, 1) void gemm_nt64_kernel(const uint16_t* __restrict__ A, long lda,
                                                            const uint16_t* __restrict__ B, long ldb, int M, int N,
                                                            int K, GemmEpi ep, int GROUP_M) {
   JM_DGUARD(blockDim.x == 512 && K % 64 == 0 && M > 0 && N > 0);
   extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
-  constexpr bool ST = SCHED & 1, PR = (SCHED & 2) != 0;
-  if ((SCHED & 3) != 0 && __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) >= 4)
-    nt64_body<EPI, ST, PR>(A, lda, B, ldb, M, N, K, ep, GROUP_M, smem);
-  else
-    nt64_body<EPI, false, false, (SCHED & 4) != 0>(A, lda, B, ldb, M, N, K, ep, GROUP_M, smem);
+  nt64_body<EPI, NTS>(A, lda, B, ldb, M, N, K, ep, GROUP_M, smem);
 }
 
 // ------------------------------------------------------------------ 4-phase counted-vmcnt variant
@@ -667,33 +495,23 @@ __global__ __launch_bounds__(512, 1) void gemm_nt64_kernel(const uint16_t* __res
 //     q4 6; the last two K-tiles issue nothing and count down (12 10 - 0 | 4 2 - -).
 // Slot rows are 128 B; 16-B chunks XOR-swizzled by swz64(slot row) on the per-lane global source
 // and on the ds_read address (conflict-free ds_read_b128, the nt64 image).
-// SCHED (A/B bits): 1 = s_setprio 1 around each phase's MFMA cluster; 2 = the phase's two glds
-// issued inside the MFMA stream (after MFMAs 1 and 5) instead of right after the barrier; 4 = waves
-// 4-7 run at priority 1 throughout (static young-half priority).  Diagnostics only (wrong results
-// by design, tools/gemm_nt_bench.py): 8 = no loads after the prologue, 16 = no vmcnt waits,
-// 32 = no barriers.
+// Waves 4-7 (the younger half, SIMD partners of waves 0-3) run at priority 1 throughout (static
+// young-half priority, MI355X_MICROARCH.md "Two waves per SIMD" item 4; profiles/r2_gemm_p4.txt).
 // acc = A[m0:m0+256, k_begin:k_begin+K] . B[n0:n0+256, same]^T  (K % 128 == 0, K > 0); every LDS
 // slot is free on entry (caller's barrier) and the ring is drained on exit except for the reads
 // of the last K-tile's MFMAs (caller's epilogue barriers before reusing LDS).
-// MODE 0: the whole K loop; 1: K-tile 0 was already issued (p4_mainloop<.., 2> of the same tile,
-// e.g. behind the previous tile's epilogue in the persistent kernel); 2: only issue K-tile 0.
-template <int SCHED, int NW = 8, int MODE = 0>
 __attribute__((always_inline)) JM_DEVICE void p4_mainloop(const uint16_t* __restrict__ A, long lda,
                                                           const uint16_t* __restrict__ B, long ldb, int M, int N,
                                                           int m0, int n0, int k_begin, int K,
-                                                          f32x4_t (&acc)[8][16 / NW * 2], uint16_t* smem) {
-  // NW = 8: 2 x 4 waves of 128 x 64 (2 waves / SIMD); NW = 4: 2 x 2 waves of 128 x 128 (one wave
-  // per SIMD, 256 accumulator registers)
-  constexpr int WN = NW / 2;          // waves along N
-  constexpr int QC = 128 / WN;        // columns of a wave's quadrant (32 / 64)
-  constexpr int NTQ = QC / 16;        // 16-wide n tiles per quadrant (2 / 4)
-  constexpr int NTW = 2 * NTQ;        // per wave (4 / 8)
-  constexpr int P = 16 / NW;          // glds pieces per wave and slot (2 / 4)
+                                                          f32x4_t (&acc)[8][4], uint16_t* smem) {
+  // 2 x 4 waves of 128 x 64 (2 waves / SIMD)
+  constexpr int WN = 4;               // waves along N
+  constexpr int QC = 128 / WN;        // columns of a wave's quadrant (32)
+  constexpr int NTQ = QC / 16;        // 16-wide n tiles per quadrant (2)
+  constexpr int NTW = 2 * NTQ;        // per wave (4)
+  constexpr int P = 2;                // glds pieces per wave and slot
   constexpr int BK2 = 64, SLOT = 128 * BK2;  // elements per slot (16 KB)
-  int tid = threadIdx.x;
-  // opaque copy: in the persistent kernel the per-lane offsets below are then recomputed per work
-  // item instead of being hoisted out of its item loop (they would stay live across the K loop)
-  asm volatile("" : "+v"(tid));
+  const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
   const int l16 = lane & 15, g = lane >> 4;
   const int wr = wave / WN, wc = wave % WN;
@@ -716,9 +534,6 @@ __attribute__((always_inline)) JM_DEVICE void p4_mainloop(const uint16_t* __rest
   // slot index within a K-tile set: 0 = a0, 1 = a1, 2 = b0, 3 = b1
   auto issue = [&](int t, auto slot) {
     constexpr int S = decltype(slot)::value;
-    if constexpr ((SCHED & 8) != 0) {
-      if (t >= 2) return;  // ablation: no loads after the prologue
-    }
     const uint32_t k0b = t * BK2 * 2;
     uint16_t* l = smem + ((t & 1) * 4 + S) * SLOT + (P * wave) * 8 * BK2;
 #pragma unroll
@@ -747,12 +562,10 @@ __attribute__((always_inline)) JM_DEVICE void p4_mainloop(const uint16_t* __rest
       f[nt][1] = lds8(base + nt * 16 * BK2 + ch1);
     }
   };
-  if constexpr (MODE != 2) {
 #pragma unroll
-    for (int i = 0; i < 8; ++i)
+  for (int i = 0; i < 8; ++i)
 #pragma unroll
-      for (int j = 0; j < NTW; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-  }
+    for (int j = 0; j < NTW; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
   auto mfma_q = [&](auto mh, auto nh, const AF& a, const BF& b) {
     constexpr int MH = decltype(mh)::value, NH = decltype(nh)::value;
 #pragma unroll
@@ -765,28 +578,22 @@ __attribute__((always_inline)) JM_DEVICE void p4_mainloop(const uint16_t* __rest
   };
   // vmcnt(n * P) lgkmcnt(0) s_barrier (n in phase units of P glds); n < 0: no vmcnt wait
   auto sync = [&](auto n) {
-    constexpr int V = (SCHED & 16) ? -1 : decltype(n)::value * P;
-    if constexpr ((SCHED & 32) != 0) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    else if constexpr (V >= 0) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"i"(V) : "memory");
+    constexpr int V = decltype(n)::value * P;
+    if constexpr (V >= 0) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"i"(V) : "memory");
     else asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
   };
-  // the phase's instruction order: its NR ds_reads spread evenly over its NM MFMAs, with SCHED & 2
-  // the glds after MFMAs 1, 5
-  auto interleave = [&](auto nreads, auto nglds) {
+  // the phase's instruction order: its NR ds_reads spread evenly over its NM MFMAs
+  auto interleave = [&](auto nreads) {
     constexpr int NM = 8 * NTQ;
-    constexpr int NR = decltype(nreads)::value, NG = (SCHED & 2) ? decltype(nglds)::value : 0;
+    constexpr int NR = decltype(nreads)::value;
     constexpr int PER = NR >= NM ? 1 : NM / (NR > 0 ? NR : 1);
 #pragma unroll
     for (int i = 0; i < NM; ++i) {
       __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
       if (i % PER == 0 && i / PER < NR) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-      if (NG > 0 && (i == 1 || i == 5)) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
     }
     __builtin_amdgcn_sched_barrier(0);
-  };
-  auto prio = [&](auto p) {
-    if constexpr ((SCHED & 1) != 0) __builtin_amdgcn_s_setprio(decltype(p)::value);
   };
   using I0 = std::integral_constant<int, 0>;
   using I1 = std::integral_constant<int, 1>;
@@ -807,41 +614,32 @@ __attribute__((always_inline)) JM_DEVICE void p4_mainloop(const uint16_t* __rest
   // q3 none, q4 3; next-to-last 6 5 - 0; last 2 1 - -.
   auto tile = [&](auto kind, int t, BF& b0, BF& b1) {
     constexpr int KIND = decltype(kind)::value;
-    using G = std::integral_constant<int, KIND == 2 ? 2 : 0>;
     // q1 (0,0): read b1(t)
     sync(std::conditional_t<KIND == 0, I2, I6>{});
-    prio(I1{});
     if constexpr (KIND == 2) issue(t + 2, I0{});
     read_b(t, I1{}, b1);
     mfma_q(I0{}, I0{}, ax, b0);
-    interleave(RB{}, G{});
-    prio(I0{});
+    interleave(RB{});
     // q2 (0,1): read a1(t)
     sync(std::conditional_t<KIND == 0, I1, std::conditional_t<KIND == 1, I5, I6>>{});
-    prio(I1{});
     if constexpr (KIND == 2) issue(t + 2, I3{});
     read_a(t, I1{}, ay);
     mfma_q(I0{}, I1{}, ax, b1);
-    interleave(I8{}, G{});
-    prio(I0{});
+    interleave(I8{});
     // q3 (1,1): no reads
     sync(IN{});
-    prio(I1{});
     if constexpr (KIND == 2) issue(t + 2, I1{});
     mfma_q(I1{}, I1{}, ay, b1);
-    interleave(I0{}, G{});
-    prio(I0{});
+    interleave(I0{});
     // q4 (1,0): read a0(t+1), b0(t+1) (into b1, free after q3)
     if constexpr (KIND > 0) {
       sync(std::conditional_t<KIND == 1, I0, I3>{});
-      prio(I1{});
-      if constexpr (KIND == 2) issue(t + 2, I2{});
+        if constexpr (KIND == 2) issue(t + 2, I2{});
       read_a(t + 1, I0{}, ax);
       read_b(t + 1, I0{}, b1);
       mfma_q(I1{}, I0{}, ay, b0);
-      interleave(RQ4{}, G{});
-      prio(I0{});
-    } else {
+      interleave(RQ4{});
+      } else {
       mfma_q(I1{}, I0{}, ay, b0);
       __builtin_amdgcn_sched_barrier(0);
     }
@@ -853,13 +651,10 @@ __attribute__((always_inline)) JM_DEVICE void p4_mainloop(const uint16_t* __rest
   const int nk = K / BK2;  // even, >= 2
   // prologue: tiles 0 and 1 in the steady-state issue order (a0 b1 a1 | b0), so the counted
   // waits of the first tiles hold unchanged
-  if constexpr (MODE != 1) {
-    issue(0, I0{});
-    issue(0, I3{});
-    issue(0, I1{});
-    issue(0, I2{});
-  }
-  if constexpr (MODE == 2) return;
+  issue(0, I0{});
+  issue(0, I3{});
+  issue(0, I1{});
+  issue(0, I2{});
   issue(1, I0{});
   issue(1, I3{});
   issue(1, I1{});
@@ -878,10 +673,10 @@ __attribute__((always_inline)) JM_DEVICE void p4_mainloop(const uint16_t* __rest
 }
 
 // the 256 x 256 tile's epilogue from the p4 accumulators (EPI_PARTIAL: fp32 split slice)
-template <int EPI, int NW = 8>
-__attribute__((always_inline)) JM_DEVICE void p4_epilogue(const f32x4_t (&acc)[8][16 / NW * 2], const GemmEpi& ep,
-                                                          int M, int N, int m0, int n0, int split, uint16_t* smem) {
-  constexpr int NTW = 16 / NW * 2, WN = NW / 2;
+template <int EPI>
+__attribute__((always_inline)) JM_DEVICE void p4_epilogue(const f32x4_t (&acc)[8][4], const GemmEpi& ep, int M,
+                                                          int N, int m0, int n0, int split, uint16_t* smem) {
+  constexpr int NTW = 4, WN = 4;
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
   const int l16 = lane & 15, g = lane >> 4;
@@ -901,23 +696,18 @@ __attribute__((always_inline)) JM_DEVICE void p4_epilogue(const f32x4_t (&acc)[8
       }
     }
   } else if (N % 8 == 0)
-    epilogue_lds<EPI, NTW, 64 * NW, BN, true>(acc, ep, smem, M, N, m0, n0, wr, wc, l16, g);
+    epilogue_lds<EPI, NTW, 512, BN, true>(acc, ep, smem, M, N, m0, n0, wr, wc, l16, g);
   else
     epilogue<EPI, NTW>(acc, ep, M, N, m0 + wr * 128, n0 + wc * NTW * 16, l16, g);
 }
 
-// SCHED bit 64: 4 waves (2 x 2, 128 x 128 each, one wave per SIMD) instead of 8.
-template <int EPI, int SCHED>
-__global__ __launch_bounds__((SCHED & 64) ? 256 : 512, 1) void gemm_p4_kernel(const uint16_t* __restrict__ A, long lda,
-                                                                             const uint16_t* __restrict__ B, long ldb,
-                                                                             int M, int N, int K, GemmEpi ep,
-                                                                             int GROUP_M) {
-  constexpr int NW = (SCHED & 64) ? 4 : 8;
-  JM_DGUARD(blockDim.x == 64 * NW && K % 128 == 0 && M > 0 && N > 0);
+template <int EPI>
+__global__ __launch_bounds__(512, 1) void gemm_p4_kernel(const uint16_t* __restrict__ A, long lda,
+                                                         const uint16_t* __restrict__ B, long ldb, int M, int N,
+                                                         int K, GemmEpi ep, int GROUP_M) {
+  JM_DGUARD(blockDim.x == 512 && K % 128 == 0 && M > 0 && N > 0);
   extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
-  if constexpr ((SCHED & 4) != 0 && NW == 8) {
-    if (__builtin_amdgcn_readfirstlane(threadIdx.x) >= 256) __builtin_amdgcn_s_setprio(1);
-  }
+  if (__builtin_amdgcn_readfirstlane(threadIdx.x) >= 256) __builtin_amdgcn_s_setprio(1);  // young half
   int m0, n0, split = 0;
   if (EPI != EPI_PARTIAL && ep.t_count > 0) {  // main part of a tail-split launch: tiles [t_begin, +t_count)
     int tg;
@@ -932,636 +722,9 @@ __global__ __launch_bounds__((SCHED & 64) ? 256 : 512, 1) void gemm_p4_kernel(co
     k_begin = ku0 * 128;
     K = (ku1 - ku0) * 128;
   }
-  f32x4_t acc[8][16 / NW * 2];
-  p4_mainloop<SCHED & ~(4 | 64), NW>(A, lda, B, ldb, M, N, m0, n0, k_begin, K, acc, smem);
-  p4_epilogue<EPI, NW>(acc, ep, M, N, m0, n0, split, smem);
-}
-
-// ------------------------------------------------------------------ persistent DP + stream-K
-// One workgroup per CU.  Workgroups are grouped in S-wide squads (S | column tiles, same XCD) that
-// share the A row tile: a squad works on a MACRO tile = one 256-row tile x S column tiles, lane j
-// of the squad on column tile j, all lanes over the same K range at the same time (so the A panel
-// is fetched once per squad through the XCD's L2, as in the tiled launch).  A squad walks
-// (1) whole macro tiles data-parallel, macro q + r*Q in round r, for the first dp macro tiles,
-// then (2) a contiguous range of 128-deep K units of the remaining macro tiles (stream-K: the
-// last, partly filled round(s) spread evenly over all Q squads).  A range that starts inside a
-// macro tile makes the squad a CONTRIBUTOR of it (at most once): every lane stores its fp32
-// partial to ws[w] and raises flags[w] (agent-scope release).  The squad holding a tile's first
-// unit OWNS it and reaches it at the END of its range, so its contributors (higher squads, which
-// start with it) are long done: it acquires their flags, adds their partials, resets the flags to
-// 0 and runs the epilogue.  Waits only ever point at higher squads (no cycle; grid <= CUs, one
-// workgroup per CU); every spin is bounded.  ws / flags are per device and serial per launch
-// stream (the NT GEMMs run on the compute stream only).
-typedef __attribute__((ext_vector_type(4))) unsigned int u32x4_v;
-
-struct SkPlan {
-  int S;          // workgroups per squad (column tiles of a macro tile)
-  int nu;         // 128-deep K units per tile
-  int dp;         // macro tiles [0, dp): whole, data-parallel
-  int L, extra;   // stream-K units [dp*nu, macros*nu): squad q has L (+1 for q < extra) units
-  float* ws;      // [G][256*256] fp32 contributor partials (register-layout order, coalesced)
-  int* flags;     // [G]
-};
-
-JM_DEVICE int sk_u0(const SkPlan& p, int q) { return q * p.L + min(q, p.extra); }
-
-template <int EPI, int SCHED>
-__global__ __launch_bounds__(512, 1) void gemm_sk_kernel(const uint16_t* __restrict__ A, long lda,
-                                                         const uint16_t* __restrict__ B, long ldb, int M, int N,
-                                                         int K, GemmEpi ep, int GROUP_M, SkPlan p) {
-  JM_DGUARD(blockDim.x == 512 && K % 128 == 0 && M > 0 && N > 0 && gridDim.x % 8 == 0);
-  extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
-  if constexpr ((SCHED & 4) != 0) {
-    if (__builtin_amdgcn_readfirstlane(threadIdx.x) >= 256) __builtin_amdgcn_s_setprio(1);
-  }
-  const int G = gridDim.x;
-  const int w = (blockIdx.x & 7) * (G >> 3) + (blockIdx.x >> 3);  // same-XCD workgroups: consecutive w
-  const int q = w / p.S, j = w - q * p.S, Q = G / p.S;
-  const int nM = (M + BM - 1) / BM;
-  const int tid = threadIdx.x;
-  const int U0 = p.dp * p.nu;
-  int T = q, u = U0 + sk_u0(p, q);
-  const int u1 = U0 + sk_u0(p, q + 1);
-  for (;;) {
-    int mac, kb, ke;
-    if (T < p.dp) {
-      mac = T;
-      kb = 0;
-      ke = p.nu;
-      T += Q;
-    } else if (u < u1) {
-      mac = u / p.nu;
-      kb = u - mac * p.nu;
-      ke = min(p.nu, kb + (u1 - u));
-      u += ke - kb;
-    } else {
-      break;
-    }
-    // macro tiles: row tile fastest (consecutive squads of an XCD share the B column block)
-    const int m0 = (mac % nM) * BM, n0 = ((mac / nM) * p.S + j) * BN;
-    __syncthreads();  // the previous item's epilogue is done with LDS
-    f32x4_t acc[8][4];
-    p4_mainloop<SCHED & ~4>(A, lda, B, ldb, M, N, m0, n0, kb * 128, (ke - kb) * 128, acc, smem);
-    // partial tiles through buffer ops: one VGPR offset (16 * tid) + per-i SGPR offsets, so no
-    // 64-bit address per i stays live (they would be hoisted out of the item loop and spilled)
-    int vo = tid * 16;
-    asm volatile("" : "+v"(vo));
-    if (kb > 0) {  // contributor: publish the partial
-      const __amdgpu_buffer_rsrc_t rw =
-          __builtin_amdgcn_make_buffer_rsrc(p.ws + (long)w * (BM * BN), (short)0, BM * BN * 4, 0x00020000);
-#pragma unroll
-      for (int i = 0; i < 32; ++i)
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_v, acc[i >> 2][i & 3]), rw, vo, i * 8192, 0);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      if (tid == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __hip_atomic_store(p.flags + w, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-      continue;
-    }
-    if (ke < p.nu) {  // owner of a split tile: add the contributors' partials
-      const int end = (mac + 1) * p.nu;
-      for (int q2 = q + 1; q2 < Q && U0 + sk_u0(p, q2) < end; ++q2) {
-        const int w2 = q2 * p.S + j;
-        if (tid == 0) {
-          for (int it = 0; it < (1 << 24); ++it) {
-            if (__hip_atomic_load(p.flags + w2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) break;
-            __builtin_amdgcn_s_sleep(2);
-          }
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-          __hip_atomic_store(p.flags + w2, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        __syncthreads();
-        const __amdgpu_buffer_rsrc_t rr =
-            __builtin_amdgcn_make_buffer_rsrc(p.ws + (long)w2 * (BM * BN), (short)0, BM * BN * 4, 0x00020000);
-#pragma unroll
-        for (int i = 0; i < 32; ++i)
-          acc[i >> 2][i & 3] += __builtin_bit_cast(f32x4_t, __builtin_amdgcn_raw_buffer_load_b128(rr, vo, i * 8192, 0));
-      }
-    }
-    p4_epilogue<EPI>(acc, ep, M, N, m0, n0, 0, smem);
-  }
-}
-
-// ------------------------------------------------------------------ half-width, 2 WGs per CU
-// 256 x 128 output tile, 4 waves (2 x 2, each the usual 128 x 64 sub-tile, 128 accumulator VGPRs),
-// 32-deep K steps through a 3-stage ring of 24 KB stages (72 KB): two workgroups fit on one CU
-// (2 x 72 KB LDS, 2 waves per SIMD).  While one workgroup runs its epilogue (VALU + a burst of
-// HBM stores that the whole chip issues at once with one workgroup per CU) the other keeps the
-// matrix pipe busy.  STAGGER delays the second resident set of workgroups by about half a tile so
-// that the two never reach their epilogues together; freed slots are refilled immediately, so
-// the offset persists for the rest of the launch.
-constexpr int BNH = 128, NSTH = 3, STAGEH = (BM + BNH) * BK;
-
-size_t jm_gemm_smem_half() { return (size_t)NSTH * STAGEH * sizeof(uint16_t); }
-
-template <int EPI, bool STAGGER>
-__global__ __launch_bounds__(256, 2) void gemm_nth_kernel(const uint16_t* __restrict__ A, long lda,
-                                                          const uint16_t* __restrict__ B, long ldb, int M, int N,
-                                                          int K, GemmEpi ep, int GROUP_M) {
-  JM_DGUARD(blockDim.x == 256 && K % 64 == 0 && M > 0 && N > 0);
-  constexpr int NW = 4, NTW = 4;
-  constexpr int RNDA = BM / 16 / NW, RNDB = BNH / 16 / NW;  // glds pieces (16 rows x 64 B) per wave
-  constexpr int PER_STAGE = RNDA + RNDB;                      // vmcnt units per stage
-  extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
-  const int tid = threadIdx.x;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
-  const int l16 = lane & 15, g = lane >> 4;
-  const int wr = wave >> 1, wc = wave & 1;
-
-  if (STAGGER && blockIdx.x >= 256 && blockIdx.x < 512) {
-    for (int i = 0; i < K / 512; ++i) __builtin_amdgcn_s_sleep(127);
-  }
-  int m0, n0, split = 0;
-  tile_of<BNH>(M, N, GROUP_M, m0, n0, EPI == EPI_PARTIAL ? ep.splits : 1, EPI == EPI_PARTIAL ? &split : nullptr);
-  int k_begin = 0;
-  if (EPI == EPI_PARTIAL) {
-    const int ku = K / 64;
-    const int ku0 = split * ku / ep.splits, ku1 = (split + 1) * ku / ep.splits;
-    k_begin = ku0 * 64;
-    K = (ku1 - ku0) * 64;
-  }
-  const __amdgpu_buffer_rsrc_t ra = make_rsrc(A + (long)m0 * lda + k_begin, (long)(M - m0) * lda * 2 - 2L * k_begin);
-  const __amdgpu_buffer_rsrc_t rb = make_rsrc(B + (long)n0 * ldb + k_begin, (long)(N - n0) * ldb * 2 - 2L * k_begin);
-  uint32_t a_src[RNDA], b_src[RNDB];
-#pragma unroll
-  for (int rr = 0; rr < RNDA; ++rr) {
-    const int row = rr * 16 * NW + wave * 16 + (lane >> 2);
-    a_src[rr] = (uint32_t)((row * lda + ((lane & 3) ^ swz(row)) * 8) * 2);
-  }
-#pragma unroll
-  for (int rr = 0; rr < RNDB; ++rr) {
-    const int row = rr * 16 * NW + wave * 16 + (lane >> 2);
-    b_src[rr] = (uint32_t)((row * ldb + ((lane & 3) ^ swz(row)) * 8) * 2);
-  }
-  auto issue = [&](int t) {
-    const uint32_t k0b = t * BK * 2;
-    uint16_t* la = smem + (t % NSTH) * STAGEH;
-    uint16_t* lb = la + BM * BK;
-#pragma unroll
-    for (int rr = 0; rr < RNDA; ++rr) blds16(ra, a_src[rr], k0b, la + (rr * 16 * NW + wave * 16) * BK);
-#pragma unroll
-    for (int rr = 0; rr < RNDB; ++rr) blds16(rb, b_src[rr], k0b, lb + (rr * 16 * NW + wave * 16) * BK);
-  };
-  const int ch = (g ^ swz(l16)) * 8;
-  const int a_off = (wr * 128 + l16) * BK + ch;
-  const int b_off = BM * BK + (wc * NTW * 16 + l16) * BK + ch;
-  auto read = [&](int t, Frags<NTW>& f) {
-    const uint16_t* base = smem + (t % NSTH) * STAGEH;
-#pragma unroll
-    for (int nt = 0; nt < NTW; ++nt) f.b[nt] = lds8(base + b_off + nt * 16 * BK);
-#pragma unroll
-    for (int mt = 0; mt < 8; ++mt) f.a[mt] = lds8(base + a_off + mt * 16 * BK);
-  };
-  f32x4_t acc[8][NTW];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < NTW; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-  auto wait_bar = [&](auto outstanding_stages) {
-    constexpr int W = decltype(outstanding_stages)::value * PER_STAGE;
-    if constexpr (W == 6) asm volatile("s_waitcnt vmcnt(6) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    if constexpr (W == 0) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    static_assert(W == 6 || W == 0, "vmcnt table");
-  };
-  // KIND 2: steady (issue t + 2, one stage in flight after t + 1 lands), 1: drain, 0: last step
-  auto step = [&](auto kind, int t, Frags<NTW>& cur, Frags<NTW>& nxt) {
-    constexpr int KIND = decltype(kind)::value;
-    if constexpr (KIND == 2) issue(t + 2);
-#pragma unroll
-    for (int mt = 0; mt < 4; ++mt)
-#pragma unroll
-      for (int nt = 0; nt < NTW; ++nt) acc[mt][nt] = mfma16(cur.b[nt], cur.a[mt], acc[mt][nt]);
-    __builtin_amdgcn_sched_barrier(0);
-    if constexpr (KIND > 0) wait_bar(std::integral_constant<int, KIND - 1>{});
-    __builtin_amdgcn_sched_barrier(0);
-    if constexpr (KIND > 0) read(t + 1, nxt);
-#pragma unroll
-    for (int mt = 4; mt < 8; ++mt)
-#pragma unroll
-      for (int nt = 0; nt < NTW; ++nt) acc[mt][nt] = mfma16(cur.b[nt], cur.a[mt], acc[mt][nt]);
-    if constexpr (KIND > 0) {
-#pragma unroll
-      for (int i = 0; i < 12; ++i) {
-        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-      }
-      __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
-    }
-    __builtin_amdgcn_sched_barrier(0);
-  };
-  using K2 = std::integral_constant<int, 2>;
-  using K1 = std::integral_constant<int, 1>;
-  using K0 = std::integral_constant<int, 0>;
-
-  const int nk = K / BK;  // even, >= 2
-  issue(0);
-  issue(1);
-  wait_bar(std::integral_constant<int, 1>{});
-  __builtin_amdgcn_sched_barrier(0);
-  Frags<NTW> f0, f1;
-  read(0, f0);
-  int t = 0;
-  for (; t + 3 < nk; t += 2) {
-    step(K2{}, t, f0, f1);
-    step(K2{}, t + 1, f1, f0);
-  }
-  step(K1{}, t, f0, f1);
-  step(K0{}, t + 1, f1, f0);
-
-  if (EPI == EPI_PARTIAL) {
-    float* dst = ep.part + (long)split * M * N;
-#pragma unroll
-    for (int mt = 0; mt < 8; ++mt) {
-      const int m = m0 + wr * 128 + mt * 16 + l16;
-      if (m >= M) continue;
-#pragma unroll
-      for (int nt = 0; nt < NTW; ++nt) {
-        const int n = n0 + wc * NTW * 16 + nt * 16 + 4 * g;
-        if (n >= N) continue;
-        float v[4] = {acc[mt][nt][0], acc[mt][nt][1], acc[mt][nt][2], acc[mt][nt][3]};
-        store4(dst + (long)m * N + n, v);
-      }
-    }
-  } else if (N % 8 == 0)
-    epilogue_lds<EPI, NTW, 256, BNH>(acc, ep, smem, M, N, m0, n0, wr, wc, l16, g);
-  else
-    epilogue<EPI, NTW>(acc, ep, M, N, m0 + wr * 128, n0 + wc * NTW * 16, l16, g);
-}
-
-// ------------------------------------------------------------------ persistent variant
-// One workgroup per CU walks its tiles (bid, bid + G, ...) as ONE stream of K steps: the ring's
-// look-ahead loads run straight into the next tile, so a tile's prologue latency is hidden behind
-// the previous tile's last steps and its epilogue.  The epilogue stages C through the single ring
-// slot that is free at a tile boundary (the other three hold the next tile's first stages), in
-// four passes of 64 rows; raw s_barrier + lgkmcnt waits keep the in-flight prefetch alive.
-JM_DEVICE void bar_lds() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
-
-// LDS traffic of the persistent epilogue goes through inline asm: hipcc cannot tell the staging
-// slot from the ring slots the next tile's DMA is filling, and would put vmcnt(0) (= drain the
-// whole prefetch) in front of every compiler-visible LDS access.  Same for global loads, hence
-// the bias is staged in LDS once at kernel start.
-JM_DEVICE uint32_t lds_addr(const void* p) {
-  return (uint32_t)(size_t)((const __attribute__((address_space(3))) char*)p);
-}
-JM_DEVICE void ds_w64(uint32_t a, uint2 v) { asm volatile("ds_write_b64 %0, %1" ::"v"(a), "v"(v) : "memory"); }
-JM_DEVICE uint4 ds_r128(uint32_t a) {
-  uint4 r;
-  asm volatile("ds_read_b128 %0, %1" : "=v"(r) : "v"(a));
-  return r;
-}
-JM_DEVICE void wait_lgkm() {
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_sched_barrier(0);
-}
-
-template <int EPI>
-JM_DEVICE void epilogue_chunked(const f32x4_t (&acc)[8][4], const GemmEpi& ep, const float* bias_lds,
-                                uint16_t* cs, int M, int N, int m0, int n0, int wr, int wc, int l16, int g) {
-  static_assert(EPI == EPI_STORE || EPI == EPI_GELU, "persistent epilogue: store / gelu only");
-  constexpr int NTH = 512, LPR = BN / 8, RPP = NTH / LPR;  // 32 lanes per 512 B row, 16 rows per sweep
-  const int tid = threadIdx.x;
-  const int c = tid % LPR;
-  const bool col_ok = n0 + c * 8 < N;
-  const uint32_t csa = lds_addr(cs);
-  const uint32_t ba = bias_lds ? lds_addr(bias_lds) : 0u;
-#pragma unroll
-  for (int p = 0; p < 4; ++p) {  // rows [64 p, 64 p + 64): waves with wr == p / 2, mt in 4 (p % 2) + 0..3
-    if (wr == (p >> 1)) {
-#pragma unroll
-      for (int nt = 0; nt < 4; ++nt) {
-        const int nl = wc * 64 + nt * 16 + 4 * g;
-        float bv[4] = {0.f, 0.f, 0.f, 0.f};
-        if (bias_lds) {  // re-read per pass: keeps 16 VGPRs free for the next tile's fragments
-          const uint4 r = ds_r128(ba + 4 * min(n0 + nl, N - 4));
-          wait_lgkm();
-          if (n0 + nl < N) {
-            bv[0] = __uint_as_float(r.x);
-            bv[1] = __uint_as_float(r.y);
-            bv[2] = __uint_as_float(r.z);
-            bv[3] = __uint_as_float(r.w);
-          }
-        }
-#pragma unroll
-        for (int mm = 0; mm < 4; ++mm) {
-          const int mt = (p & 1) * 4 + mm;
-          const int rl = mm * 16 + l16;
-          uint2 pk;
-          pk.x = pack_bf2(acc[mt][nt][0] + bv[0], acc[mt][nt][1] + bv[1]);
-          pk.y = pack_bf2(acc[mt][nt][2] + bv[2], acc[mt][nt][3] + bv[3]);
-          ds_w64(csa + 2 * (rl * BN + (((nl >> 3) ^ (rl & 15)) << 3) + (nl & 7)), pk);
-        }
-      }
-    }
-    bar_lds();
-    uint4 v[64 / RPP];
-#pragma unroll
-    for (int k = 0; k < 64 / RPP; ++k) {
-      const int rl = tid / LPR + k * RPP;
-      v[k] = ds_r128(csa + 2 * (rl * BN + ((c ^ (rl & 15)) << 3)));
-    }
-    wait_lgkm();
-#pragma unroll
-    for (int k = 0; k < 64 / RPP; ++k) {
-      const int m = m0 + p * 64 + tid / LPR + k * RPP;
-      if (m < M && col_ok) {
-        *reinterpret_cast<uint4*>(ep.out + (long)m * ep.ldo + n0 + c * 8) = v[k];
-        if (EPI == EPI_GELU) {
-          float f[8];
-          const uint16_t* h = reinterpret_cast<const uint16_t*>(&v[k]);
-#pragma unroll
-          for (int j = 0; j < 8; ++j) f[j] = gelu_tanh_f(bf2f(h[j]));
-          store8(ep.out2 + (long)m * ep.ldo + n0 + c * 8, f);
-        }
-      }
-    }
-    bar_lds();
-  }
-}
-
-template <int EPI>
-__global__ __launch_bounds__(512, 1) void gemm_nt_persist_kernel(const uint16_t* __restrict__ A, long lda,
-                                                                 const uint16_t* __restrict__ B, long ldb, int M,
-                                                                 int N, int K, GemmEpi ep, int GROUP_M) {
-  constexpr int NW = 8, NTW = 4, RND = 2;
-  extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
-  const int tid = threadIdx.x;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
-  const int l16 = lane & 15, g = lane >> 4;
-  const int wr = wave >> 2, wc = wave & 3;
-  const int nM = (M + BM - 1) / BM, nN = (N + BN - 1) / BN, tiles = nM * nN;
-  const int G = gridDim.x;  // multiple of 8
-  // workgroups of one XCD (bid % 8) take consecutive slots -> tiles in flight together are
-  // neighbours in the grouped order
-  const int slot = (blockIdx.x & 7) * (G >> 3) + (blockIdx.x >> 3);
-  const int my_tiles = slot < tiles ? (tiles - slot + G - 1) / G : 0;
-  const int nk = K / BK;
-  const int total = my_tiles * nk;
-  if (total == 0) return;
-  float* bias_lds = nullptr;
-  if (ep.bias) {  // whole bias into LDS behind the ring, before any DMA is in flight
-    bias_lds = reinterpret_cast<float*>(smem + NST * STAGE);
-    for (int i = tid; i < N; i += 512) bias_lds[i] = ep.bias[i];
-    __syncthreads();
-  }
-  auto tile_coords = [&](int j, int& m0, int& n0) {
-    const int wg = slot + j * G;
-    const int per_group = GROUP_M * nN;
-    const int first_m = (wg / per_group) * GROUP_M;
-    const int gsz = min(nM - first_m, GROUP_M);
-    m0 = (first_m + (wg % per_group) % gsz) * BM;
-    n0 = ((wg % per_group) / gsz) * BN;
-  };
-  uint32_t a_src[RND], b_src[RND];
-#pragma unroll
-  for (int rr = 0; rr < RND; ++rr) {
-    const int row = rr * 16 * NW + wave * 16 + (lane >> 2);
-    const int c = (lane & 3) ^ swz(row);
-    a_src[rr] = (uint32_t)((row * lda + c * 8) * 2);
-    b_src[rr] = (uint32_t)((row * ldb + c * 8) * 2);
-  }
-  auto issue = [&](int u) {  // stage u of this workgroup's stream
-    const int j = u / nk, t = u - j * nk;
-    int m0, n0;
-    tile_coords(j, m0, n0);
-    const __amdgpu_buffer_rsrc_t ra = make_rsrc(A + (long)m0 * lda, (long)(M - m0) * lda * 2);
-    const __amdgpu_buffer_rsrc_t rb = make_rsrc(B + (long)n0 * ldb, (long)(N - n0) * ldb * 2);
-    const uint32_t k0b = t * BK * 2;
-    uint16_t* la = smem + (u % NST) * STAGE;
-    uint16_t* lb = la + BM * BK;
-#pragma unroll
-    for (int rr = 0; rr < RND; ++rr) {
-      blds16(ra, a_src[rr], k0b, la + (rr * 16 * NW + wave * 16) * BK);
-      blds16(rb, b_src[rr], k0b, lb + (rr * 16 * NW + wave * 16) * BK);
-    }
-  };
-  const int ch = (g ^ swz(l16)) * 8;
-  const int a_off = (wr * 128 + l16) * BK + ch;
-  const int b_off = BM * BK + (wc * NTW * 16 + l16) * BK + ch;
-  auto read = [&](int u, Frags<NTW>& f) {
-    const uint16_t* base = smem + (u % NST) * STAGE;
-#pragma unroll
-    for (int nt = 0; nt < NTW; ++nt) f.b[nt] = lds8(base + b_off + nt * 16 * BK);
-#pragma unroll
-    for (int mt = 0; mt < 8; ++mt) f.a[mt] = lds8(base + a_off + mt * 16 * BK);
-  };
-  f32x4_t acc[8][NTW];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < NTW; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-  auto wait_bar = [&](auto outstanding_stages) {
-    constexpr int W = decltype(outstanding_stages)::value * 2 * RND;
-    if constexpr (W == 8) asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    if constexpr (W == 4) asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    if constexpr (W == 0) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-  };
-  auto step = [&](auto kind, int u, Frags<NTW>& cur, Frags<NTW>& nxt) {
-    constexpr int KIND = decltype(kind)::value;
-    if constexpr (KIND == 3) issue(u + 3);
-#pragma unroll
-    for (int mt = 0; mt < 4; ++mt)
-#pragma unroll
-      for (int nt = 0; nt < NTW; ++nt) acc[mt][nt] = mfma16(cur.b[nt], cur.a[mt], acc[mt][nt]);
-    __builtin_amdgcn_sched_barrier(0);
-    if constexpr (KIND > 0) wait_bar(std::integral_constant<int, KIND - 1>{});
-    __builtin_amdgcn_sched_barrier(0);
-    if constexpr (KIND > 0) read(u + 1, nxt);
-#pragma unroll
-    for (int mt = 4; mt < 8; ++mt)
-#pragma unroll
-      for (int nt = 0; nt < NTW; ++nt) acc[mt][nt] = mfma16(cur.b[nt], cur.a[mt], acc[mt][nt]);
-    if constexpr (KIND > 0) {
-#pragma unroll
-      for (int i = 0; i < 12; ++i) {
-        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-      }
-      __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
-    }
-    __builtin_amdgcn_sched_barrier(0);
-  };
-  auto finish_tile = [&](int u_next) {  // u_next = first step of the next tile
-    const int j = u_next / nk - 1;
-    int m0, n0;
-    tile_coords(j, m0, n0);
-    // the slot of the step just consumed is free: the others hold the next tile's stages
-    epilogue_chunked<EPI>(acc, ep, bias_lds, smem + ((u_next - 1) % NST) * STAGE, M, N, m0, n0, wr, wc, l16, g);
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-      for (int jj = 0; jj < NTW; ++jj) acc[i][jj] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-  };
-  using K3 = std::integral_constant<int, 3>;
-  using K2 = std::integral_constant<int, 2>;
-  using K1 = std::integral_constant<int, 1>;
-  using K0 = std::integral_constant<int, 0>;
-
-  issue(0);
-  issue(1);
-  if (total > 2) {
-    issue(2);
-    wait_bar(std::integral_constant<int, 2>{});
-  } else {
-    wait_bar(std::integral_constant<int, 1>{});
-  }
-  __builtin_amdgcn_sched_barrier(0);
-  Frags<NTW> f0, f1;
-  read(0, f0);
-  int u = 0;
-  for (; u + 4 < total; u += 2) {
-    step(K3{}, u, f0, f1);
-    step(K3{}, u + 1, f1, f0);
-    if ((u + 2) % nk == 0) finish_tile(u + 2);
-  }
-  if (total - u == 4) {
-    step(K3{}, u, f0, f1);
-    step(K2{}, u + 1, f1, f0);
-    u += 2;
-    if (u % nk == 0) finish_tile(u);
-  }
-  step(K1{}, u, f0, f1);
-  step(K0{}, u + 1, f1, f0);
-  finish_tile(u + 2);
-}
-
-// ------------------------------------------------------------------ persistent, overlapped (p4)
-// One workgroup per CU walks tiles w, w + G, ... of the grouped order on the 4-phase main loop,
-// and hides each tile's start behind the previous tile's end: as soon as a tile's K loop is done
-// (set 0 of the LDS slots is free, its loads all landed) the NEXT tile's K-tile 0 is issued into
-// set 0, and only then the epilogue runs -- staged through set 1 (64 KB) in two 128-row halves
-// with inline-asm LDS accesses and the bias from an LDS copy (a compiler-visible LDS access or
-// global load would make hipcc drain the in-flight DMA with vmcnt(0)).  The next K loop then
-// starts with its first K-tile landed (MODE 1).  The epilogue's stores count in vmcnt and are
-// simply waited for by the first counted wait of the next tile.  Epilogues without aux input.
-template <int EPI>
-JM_DEVICE void epilogue_set1(const f32x4_t (&acc)[8][4], const GemmEpi& ep, const float* bias_lds, uint16_t* cs,
-                             int M, int N, int m0, int n0) {
-  constexpr int LPR = BN / 8, RPP = 512 / LPR;  // 32 lanes per 512-B row, 16 rows per sweep
-  int tid = threadIdx.x;
-  asm volatile("" : "+v"(tid));  // recomputed per tile, not hoisted out of the tile loop
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
-  const int l16 = lane & 15, g = lane >> 4;
-  const int wr = wave >> 2, wc = wave & 3;
-  const int c = tid % LPR;
-  const bool col_ok = n0 + c * 8 < N;
-  const uint32_t csa = lds_addr(cs);
-  const uint32_t ba = bias_lds ? lds_addr(bias_lds) : 0u;
-#pragma unroll
-  for (int p = 0; p < 2; ++p) {  // rows [128 p, 128 p + 128) = the accumulators of the waves with wr == p
-    if (wr == p) {
-#pragma unroll
-      for (int nt = 0; nt < 4; ++nt) {
-        const int nl = wc * 64 + nt * 16 + 4 * g;
-        float bv[4] = {0.f, 0.f, 0.f, 0.f};
-        if (bias_lds) {
-          const uint4 r = ds_r128(ba + 4 * min(n0 + nl, N - 4));
-          wait_lgkm();
-          if (n0 + nl < N) {
-            bv[0] = __uint_as_float(r.x);
-            bv[1] = __uint_as_float(r.y);
-            bv[2] = __uint_as_float(r.z);
-            bv[3] = __uint_as_float(r.w);
-          }
-        }
-#pragma unroll
-        for (int mt = 0; mt < 8; ++mt) {
-          const int rl = mt * 16 + l16;
-          uint2 pk;
-          pk.x = pack_bf2(acc[mt][nt][0] + bv[0], acc[mt][nt][1] + bv[1]);
-          pk.y = pack_bf2(acc[mt][nt][2] + bv[2], acc[mt][nt][3] + bv[3]);
-          ds_w64(csa + 2 * (rl * BN + (((nl >> 3) ^ (rl & 15)) << 3) + (nl & 7)), pk);
-        }
-      }
-    }
-    bar_lds();
-    uint4 v[128 / RPP];
-#pragma unroll
-    for (int k = 0; k < 128 / RPP; ++k) {
-      const int rl = tid / LPR + k * RPP;
-      v[k] = ds_r128(csa + 2 * (rl * BN + ((c ^ (rl & 15)) << 3)));
-    }
-    wait_lgkm();
-#pragma unroll
-    for (int k = 0; k < 128 / RPP; ++k) {
-      const int m = m0 + p * 128 + tid / LPR + k * RPP;
-      if (m < M && col_ok) {
-        uint16_t* o = ep.out + (long)m * ep.ldo + n0 + c * 8;
-        const uint16_t* h = reinterpret_cast<const uint16_t*>(&v[k]);
-        if (EPI == EPI_STORE || EPI == EPI_GELU) st16(o, v[k], true);
-        if (EPI == EPI_GELU || EPI == EPI_GELU_ONLY) {
-          float f[8];
-#pragma unroll
-          for (int j = 0; j < 8; ++j) f[j] = gelu_tanh_f(bf2f(h[j]));
-          st16(EPI == EPI_GELU ? ep.out2 + (long)m * ep.ldo + n0 + c * 8 : o, pack8(f), true);
-        }
-        if (EPI == EPI_GELU_D) {
-          float fg[8], fd[8];
-#pragma unroll
-          for (int j = 0; j < 8; ++j) gelu_and_grad_f(bf2f(h[j]), fg[j], fd[j]);
-          st16(o, pack8(fd), true);
-          st16(ep.out2 + (long)m * ep.ldo + n0 + c * 8, pack8(fg), true);
-        }
-      }
-    }
-    bar_lds();
-  }
-}
-
-template <int EPI>
-__global__ __launch_bounds__(512, 1) void gemm_pp_kernel(const uint16_t* __restrict__ A, long lda,
-                                                         const uint16_t* __restrict__ B, long ldb, int M, int N,
-                                                         int K, GemmEpi ep, int GROUP_M) {
-  JM_DGUARD(blockDim.x == 512 && K % 128 == 0 && M > 0 && N > 0 && gridDim.x % 8 == 0);
-  extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
-  constexpr int SLOT = 128 * 64;
-  if (__builtin_amdgcn_readfirstlane(threadIdx.x) >= 256) __builtin_amdgcn_s_setprio(1);
-  const int G = gridDim.x;
-  const int tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
-  // round r covers tiles [r G, r G + R); each XCD label x (blockIdx % 8) takes a contiguous
-  // chunk of about R / 8 of them (neighbouring tiles share A / B panels through that XCD's L2)
-  // and a partial last round is spread over all eight XCDs, not packed onto the first few
-  const int xcd = blockIdx.x & 7, loc = blockIdx.x >> 3;
-  auto tile_of_round = [&](int r) {
-    const int R = min(G, tiles - r * G);
-    const int q = R >> 3, rem = R & 7;
-    if (loc >= q + (xcd < rem ? 1 : 0)) return -1;
-    return r * G + xcd * q + min(xcd, rem) + loc;
-  };
-  float* bias_lds = nullptr;
-  if (ep.bias) {  // whole bias behind the 8 slots, before any DMA is in flight
-    bias_lds = reinterpret_cast<float*>(smem + 8 * SLOT);
-    for (int i = threadIdx.x; i < N; i += 512) bias_lds[i] = ep.bias[i];
-    __syncthreads();
-  }
-  int r = 0;
-  int T = tile_of_round(0);
-  if (T < 0) return;  // workgroup-uniform (grid <= tiles on the host)
-  int m0, n0;
-  tile_coords(T, M, N, GROUP_M, m0, n0);
   f32x4_t acc[8][4];
-  p4_mainloop<0, 8, 2>(A, lda, B, ldb, M, N, m0, n0, 0, K, acc, smem);
-  for (;;) {
-    p4_mainloop<0, 8, 1>(A, lda, B, ldb, M, N, m0, n0, 0, K, acc, smem);
-    const int T2 = r * G + G < tiles ? tile_of_round(r + 1) : -1;
-    const bool more = T2 >= 0;  // workgroup-uniform
-    int m1 = 0, n1 = 0;
-    // all waves are past their last reads of set 0 (the final K-tiles' barriers), so the next
-    // tile's K-tile 0 can stream in underneath this tile's epilogue
-    if (more) {
-      tile_coords(T2, M, N, GROUP_M, m1, n1);
-      p4_mainloop<0, 8, 2>(A, lda, B, ldb, M, N, m1, n1, 0, K, acc, smem);
-    }
-    // set 1 is free once every wave passed the last K-tile's q3 barrier (its reads were in q1 / q2)
-    epilogue_set1<EPI>(acc, ep, bias_lds, smem + 4 * SLOT, M, N, m0, n0);
-    if (!more) break;
-    ++r;
-    m0 = m1;
-    n0 = n1;
-  }
+  p4_mainloop(A, lda, B, ldb, M, N, m0, n0, k_begin, K, acc, smem);
+  p4_epilogue<EPI>(acc, ep, M, N, m0, n0, split, smem);
 }
 
 // ------------------------------------------------------------------ tail split finish
@@ -1636,251 +799,10 @@ __global__ __launch_bounds__(256) void tail_finish_kernel(GemmEpi ep, int M, int
   }
 }
 
-size_t jm_gemm_smem() { return (size_t)NST * STAGE * sizeof(uint16_t); }
 
-// returns 0 on success, <0 on unsupported shape
-int g_gemm_wn = 20;    // runtime switches for A/B (jm_gemm_set_variant): 20-83 = the 4-phase counted-vmcnt
-                       // kernel + SCHED bits (default 24: static young-half priority;
-                       // profiles/r2_gemm_p4.txt), 12 = 64-deep stages + nontemporal
-                       // epilogue stores (default; profiles/r1_gemm_nt_stores.txt), 6 = 64-deep stages,
-                       // 10/11 = 256x128 tiles, 2 WGs per CU (no stagger / stagger),
-                       // 4 = 32-deep ring, 2 = 4 waves, 5 = persistent, 4x = ablations
-int g_gemm_group = 8;
-
-template <int EPI, int WN, int ABL = 0>
-void launch_nt(const uint16_t* A, long lda, const uint16_t* B, long ldb, int M, int N, int K, const GemmEpi& ep,
-               int nwg, hipStream_t st) {
-  static bool attr = false;
-  const size_t sm = jm_gemm_smem();
-  if (!attr) {
-    (void)hipFuncSetAttribute((const void*)gemm_nt_kernel<EPI, WN, ABL>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)sm);
-    attr = true;
-  }
-  gemm_nt_kernel<EPI, WN, ABL><<<nwg, 128 * WN, sm, st>>>(A, lda, B, ldb, M, N, K, ep, g_gemm_group);
-}
-
+int g_gemm_group = 8;  // row tiles per column sweep (profiles/r2_gemm_group.txt: 8 best)
+int g_gemm_nt64 = 0;   // test switch: every launch on the nt64 main loop (it otherwise runs K % 128 == 64)
 int g_num_cus = 0;
-
-template <int EPI>
-void launch_persist(const uint16_t* A, long lda, const uint16_t* B, long ldb, int M, int N, int K,
-                    const GemmEpi& ep, int tiles, hipStream_t st) {
-  const size_t sm = jm_gemm_smem() + (ep.bias ? (size_t)N * sizeof(float) : 0);
-  static size_t attr = 0;
-  if (attr < sm) {
-    (void)hipFuncSetAttribute((const void*)gemm_nt_persist_kernel<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)sm);
-    attr = sm;
-  }
-  if (g_num_cus == 0) {
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    hipDeviceProp_t prop;
-    (void)hipGetDeviceProperties(&prop, dev);
-    g_num_cus = prop.multiProcessorCount;
-  }
-  int grid = g_num_cus < tiles ? g_num_cus : tiles;
-  grid = (grid + 7) / 8 * 8;  // the XCD slot mapping assumes a multiple of 8
-  gemm_nt_persist_kernel<EPI><<<grid, 512, sm, st>>>(A, lda, B, ldb, M, N, K, ep, g_gemm_group);
-}
-
-template <int EPI, int SCHED>
-void launch_nt64(const uint16_t* A, long lda, const uint16_t* B, long ldb, int M, int N, int K, const GemmEpi& ep,
-                 int nwg, hipStream_t st) {
-  static bool attr = false;
-  const size_t sm = jm_gemm_smem();  // 2 x 64 KB slots == the 4 x 32 KB ring
-  if (!attr) {
-    (void)hipFuncSetAttribute((const void*)gemm_nt64_kernel<EPI, SCHED>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)sm);
-    attr = true;
-  }
-  gemm_nt64_kernel<EPI, SCHED><<<nwg, 512, sm, st>>>(A, lda, B, ldb, M, N, K, ep, g_gemm_group);
-}
-
-template <int EPI, int SCHED>
-void launch_p4s(const uint16_t* A, long lda, const uint16_t* B, long ldb, int M, int N, int K, const GemmEpi& ep,
-                int nwg, hipStream_t st) {
-  static bool attr = false;
-  const size_t sm = jm_gemm_smem();  // 8 x 16 KB slots
-  if (!attr) {
-    (void)hipFuncSetAttribute((const void*)gemm_p4_kernel<EPI, SCHED>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)sm);
-    attr = true;
-  }
-  gemm_p4_kernel<EPI, SCHED><<<nwg, (SCHED & 64) ? 256 : 512, sm, st>>>(A, lda, B, ldb, M, N, K, ep, g_gemm_group);
-}
-
-int g_p4_sched = 4;  // A/B: variant 20 + SCHED bits (variants 21..83 = 20 + bits)
-int g_sk = 0;        // A/B: persistent DP + stream-K launches where the plan says they pay (jm_gemm_set_sk); off:
-                     // measured slower on every planned shape (fp32 partial traffic; profiles/r2_gemm_stream_k.txt)
-int num_cus();
-
-// stream-K plan for an NT launch (0 = plain tiled launch).  Squad width S = the largest power of 2
-// <= 8 dividing the column-tile count; macro tiles = row tiles x column blocks.  Cost model in
-// 128-deep K units of one tile on one CU: tiled = ceil(tiles / G) * nu; DP + stream-K = the whole
-// rounds of macro tiles but the last, the rest spread evenly over the squads, + ~1 unit per
-// partial an owner has to add.
-int sk_plan(int M, int N, int K, SkPlan* pl) {
-  if (!g_sk || K % 128) return 0;
-  const int G = num_cus() / 8 * 8;
-  const int nM = (M + BM - 1) / BM, nN = (N + BN - 1) / BN;
-  const int tiles = nM * nN;
-  const int nu = K / 128;
-  if (G < 8 || tiles % G == 0) return 0;
-  int S = 8;
-  while (nN % S) S >>= 1;
-  const int Q = G / S, macros = nM * (nN / S);
-  if (g_sk == 2) {  // A/B: whole tiles only, on the fewest squads that keep the round count
-    const int rounds = (macros + Q - 1) / Q;
-    int q = (macros + rounds - 1) / rounds;
-    while ((q * S) % 8) ++q;
-    if (q >= Q) return 0;
-    pl->S = S;
-    pl->nu = nu;
-    pl->dp = macros;
-    pl->L = 0;
-    pl->extra = 0;
-    return q * S;
-  }
-  const int rounds = macros / Q;
-  const int dp = rounds > 0 ? (rounds - 1) * Q : 0;
-  const long U = (long)(macros - dp) * nu;
-  const int L = (int)(U / Q);
-  if (L < 1) return 0;
-  const int parts = (nu + L - 1) / L;  // squads a macro tile spans (about)
-  if (parts > 4) return 0;             // owner would add too many partials: split-K / tiled instead
-  const double tiled = (double)((tiles + G - 1) / G) * nu;
-  const double sk = (double)(dp / Q) * nu + (double)((U + Q - 1) / Q) + (parts > 1 ? parts : 0);
-  if (sk > 0.95 * tiled) return 0;
-  pl->S = S;
-  pl->nu = nu;
-  pl->dp = dp;
-  pl->L = L;
-  pl->extra = (int)(U - (long)L * Q);
-  return G;
-}
-
-float* g_sk_ws = nullptr;
-int* g_sk_flags = nullptr;
-
-template <int EPI, int SCHED>
-void launch_sk(const uint16_t* A, long lda, const uint16_t* B, long ldb, int M, int N, int K, const GemmEpi& ep,
-               int G, SkPlan pl, hipStream_t st) {
-  static bool attr = false;
-  const size_t sm = jm_gemm_smem();
-  if (!attr) {
-    (void)hipFuncSetAttribute((const void*)gemm_sk_kernel<EPI, SCHED>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)sm);
-    attr = true;
-  }
-  if (g_sk_ws == nullptr) {  // once per process (outside any graph capture: the first call is eager)
-    (void)hipMalloc((void**)&g_sk_ws, (size_t)1024 * BM * BN * sizeof(float));
-    (void)hipMalloc((void**)&g_sk_flags, 1024 * sizeof(int));
-    (void)hipMemset(g_sk_flags, 0, 1024 * sizeof(int));
-  }
-  pl.ws = g_sk_ws;
-  pl.flags = g_sk_flags;
-  gemm_sk_kernel<EPI, SCHED><<<G, 512, sm, st>>>(A, lda, B, ldb, M, N, K, ep, g_gemm_group, pl);
-}
-
-int g_pp = 0;  // A/B: persistent overlapped launch (gemm_pp_kernel) for multi-round grids (jm_gemm_set_pp);
-               // off: within +-4 % of the tiled launch, slower on the GELU epilogue (profiles/r2_gemm_persistent.txt)
-
-template <int EPI>
-void launch_pp(const uint16_t* A, long lda, const uint16_t* B, long ldb, int M, int N, int K, const GemmEpi& ep,
-               int G, hipStream_t st) {
-  const size_t sm = jm_gemm_smem() + (ep.bias ? (size_t)N * sizeof(float) : 0);
-  static size_t attr = 0;
-  if (attr < sm) {
-    (void)hipFuncSetAttribute((const void*)gemm_pp_kernel<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
-    attr = sm;
-  }
-  gemm_pp_kernel<EPI><<<G, 512, sm, st>>>(A, lda, B, ldb, M, N, K, ep, g_gemm_group);
-}
-
-template <int EPI>
-void launch_p4(const uint16_t* A, long lda, const uint16_t* B, long ldb, int M, int N, int K, const GemmEpi& ep,
-               int nwg, hipStream_t st) {
-  if constexpr (EPI == EPI_STORE || EPI == EPI_GELU || EPI == EPI_GELU_ONLY || EPI == EPI_GELU_D) {
-    const int G = num_cus() / 8 * 8;
-    if (g_pp && g_p4_sched == 4 && nwg > G && N % 8 == 0 && N <= 8192 && ep.t_count == 0)
-      return launch_pp<EPI>(A, lda, B, ldb, M, N, K, ep, G, st);
-  }
-  if constexpr (EPI != EPI_PARTIAL && EPI != EPI_TAIL) {
-    SkPlan pl;
-    const int G = (g_p4_sched == 4 || g_p4_sched == 0) && ep.t_count == 0 ? sk_plan(M, N, K, &pl) : 0;
-    if (G > 0) {
-      if (g_p4_sched == 4) return launch_sk<EPI, 4>(A, lda, B, ldb, M, N, K, ep, G, pl, st);
-      return launch_sk<EPI, 0>(A, lda, B, ldb, M, N, K, ep, G, pl, st);
-    }
-  }
-  switch (g_p4_sched) {
-    default: break;
-    case 1: return launch_p4s<EPI, 1>(A, lda, B, ldb, M, N, K, ep, nwg, st);
-    case 2: return launch_p4s<EPI, 2>(A, lda, B, ldb, M, N, K, ep, nwg, st);
-    case 3: return launch_p4s<EPI, 3>(A, lda, B, ldb, M, N, K, ep, nwg, st);
-    case 4: return launch_p4s<EPI, 4>(A, lda, B, ldb, M, N, K, ep, nwg, st);
-    case 6: return launch_p4s<EPI, 6>(A, lda, B, ldb, M, N, K, ep, nwg, st);
-    case 64: return launch_p4s<EPI, 64>(A, lda, B, ldb, M, N, K, ep, nwg, st);
-    case 12: if constexpr (EPI == EPI_STORE) return launch_p4s<EPI, 12>(A, lda, B, ldb, M, N, K, ep, nwg, st); break;
-    case 20: if constexpr (EPI == EPI_STORE) return launch_p4s<EPI, 20>(A, lda, B, ldb, M, N, K, ep, nwg, st); break;
-    case 52: if constexpr (EPI == EPI_STORE) return launch_p4s<EPI, 52>(A, lda, B, ldb, M, N, K, ep, nwg, st); break;
-    case 60: if constexpr (EPI == EPI_STORE) return launch_p4s<EPI, 60>(A, lda, B, ldb, M, N, K, ep, nwg, st); break;
-  }
-  return launch_p4s<EPI, 0>(A, lda, B, ldb, M, N, K, ep, nwg, st);
-}
-
-template <int EPI, bool STAGGER>
-void launch_nth(const uint16_t* A, long lda, const uint16_t* B, long ldb, int M, int N, int K, const GemmEpi& ep,
-                hipStream_t st) {
-  static bool attr = false;
-  const size_t sm = jm_gemm_smem_half();
-  if (!attr) {
-    (void)hipFuncSetAttribute((const void*)gemm_nth_kernel<EPI, STAGGER>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)sm);
-    attr = true;
-  }
-  const int nwg = ((M + BM - 1) / BM) * ((N + BNH - 1) / BNH) * (EPI == EPI_PARTIAL ? ep.splits : 1);
-  gemm_nth_kernel<EPI, STAGGER><<<nwg, 256, sm, st>>>(A, lda, B, ldb, M, N, K, ep, g_gemm_group);
-}
-
-template <int EPI>
-void launch_epi(const uint16_t* A, long lda, const uint16_t* B, long ldb, int M, int N, int K, const GemmEpi& ep,
-                int nwg, hipStream_t st) {
-  if (g_gemm_wn == 20) {  // K in 128-deep units (split-K: per split); else the 64-deep kernel
-    if (K % 128 == 0 && (EPI != EPI_PARTIAL || K / 128 >= ep.splits))
-      return launch_p4<EPI>(A, lda, B, ldb, M, N, K, ep, nwg, st);
-    return launch_nt64<EPI, 4>(A, lda, B, ldb, M, N, K, ep, nwg, st);
-  }
-  if (g_gemm_wn == 6) return launch_nt64<EPI, 0>(A, lda, B, ldb, M, N, K, ep, nwg, st);
-  if (g_gemm_wn == 12) return launch_nt64<EPI, 4>(A, lda, B, ldb, M, N, K, ep, nwg, st);
-  if (g_gemm_wn == 10) return launch_nth<EPI, false>(A, lda, B, ldb, M, N, K, ep, st);
-  if (g_gemm_wn == 11) return launch_nth<EPI, true>(A, lda, B, ldb, M, N, K, ep, st);
-  if (g_gemm_wn == 7) return launch_nt64<EPI, 1>(A, lda, B, ldb, M, N, K, ep, nwg, st);
-  if (g_gemm_wn == 8) return launch_nt64<EPI, 3>(A, lda, B, ldb, M, N, K, ep, nwg, st);
-  if (g_gemm_wn == 9) return launch_nt64<EPI, 2>(A, lda, B, ldb, M, N, K, ep, nwg, st);
-  if constexpr (EPI == EPI_STORE || EPI == EPI_GELU) {
-    if (g_gemm_wn == 5 && N % 8 == 0 && N <= 8192) return launch_persist<EPI>(A, lda, B, ldb, M, N, K, ep, nwg, st);
-  }
-  if (g_gemm_wn == 2)
-    launch_nt<EPI, 2>(A, lda, B, ldb, M, N, K, ep, nwg, st);
-  else if (EPI == EPI_STORE && g_gemm_wn == 41)
-    launch_nt<EPI, 4, 1>(A, lda, B, ldb, M, N, K, ep, nwg, st);
-  else if (EPI == EPI_STORE && g_gemm_wn == 42)
-    launch_nt<EPI, 4, 2>(A, lda, B, ldb, M, N, K, ep, nwg, st);
-  else if (EPI == EPI_STORE && g_gemm_wn == 44)
-    launch_nt<EPI, 4, 4>(A, lda, B, ldb, M, N, K, ep, nwg, st);
-  else if (EPI == EPI_STORE && g_gemm_wn == 47)
-    launch_nt<EPI, 4, 7>(A, lda, B, ldb, M, N, K, ep, nwg, st);
-  else  // 4, and 5 for the epilogues the persistent kernel does not cover
-    launch_nt<EPI, 4>(A, lda, B, ldb, M, N, K, ep, nwg, st);
-}
-
-
-// tail split of the last partial wave (A/B switch).  Off: measured slower on every shape it applies
-// to (enc FF1 199 -> 215 us, decoder Wo 70 -> 81 us; ViT-L step +0.9 ms, profiles/r1_gemm_tail_split.txt)
-// -- the last, sparsely filled wave already runs faster per tile than a full one
-int g_gemm_tail = 1;  // tail split of the last partial wave (K >= 1024): ViT-B FF2 fwd 127 -> 109 us (profiles/r2_gemm_tail_p4.txt)
 
 int num_cus() {
   if (g_num_cus == 0) {
@@ -1893,6 +815,41 @@ int num_cus() {
   return g_num_cus;
 }
 
+template <int EPI, bool NTS>
+void launch_nt64(const uint16_t* A, long lda, const uint16_t* B, long ldb, int M, int N, int K, const GemmEpi& ep,
+                 int nwg, hipStream_t st) {
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)gemm_nt64_kernel<EPI, NTS>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)GEMM_SMEM);
+    attr = true;
+  }
+  gemm_nt64_kernel<EPI, NTS><<<nwg, 512, GEMM_SMEM, st>>>(A, lda, B, ldb, M, N, K, ep, g_gemm_group);
+}
+
+template <int EPI>
+void launch_p4(const uint16_t* A, long lda, const uint16_t* B, long ldb, int M, int N, int K, const GemmEpi& ep,
+               int nwg, hipStream_t st) {
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)gemm_p4_kernel<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)GEMM_SMEM);
+    attr = true;
+  }
+  gemm_p4_kernel<EPI><<<nwg, 512, GEMM_SMEM, st>>>(A, lda, B, ldb, M, N, K, ep, g_gemm_group);
+}
+
+// K in 128-deep units (split-K: per split) -> p4, else the 64-deep kernel (nontemporal epilogue stores)
+template <int EPI>
+void launch_epi(const uint16_t* A, long lda, const uint16_t* B, long ldb, int M, int N, int K, const GemmEpi& ep,
+                int nwg, hipStream_t st) {
+  if (!g_gemm_nt64 && K % 128 == 0 && (EPI != EPI_PARTIAL || K / 128 >= ep.splits))
+    return launch_p4<EPI>(A, lda, B, ldb, M, N, K, ep, nwg, st);
+  return launch_nt64<EPI, true>(A, lda, B, ldb, M, N, K, ep, nwg, st);
+}
+
+int g_gemm_tail = 1;  // tail split of the last partial wave (K >= 1024): ViT-B FF2 fwd 127 -> 109 us (profiles/r2_gemm_tail_p4.txt)
+
 template <int EPI>
 void launch_tail(const uint16_t* A, long lda, const uint16_t* B, long ldb, int M, int N, int K, const GemmEpi& ep,
                  int tiles, hipStream_t st) {
@@ -1903,29 +860,19 @@ void launch_tail(const uint16_t* A, long lda, const uint16_t* B, long ldb, int M
   launch_epi<EPI>(A, lda, B, ldb, M, N, K, em, tiles - r, st);
   GemmEpi et = ep;
   et.t_begin = tiles - r;
-  if (g_gemm_wn == 12)
-    launch_nt64<EPI_TAIL, 4>(A, lda, B, ldb, M, N, K, et, r * ep.tail_S, st);
-  else
-    launch_nt64<EPI_TAIL, 0>(A, lda, B, ldb, M, N, K, et, r * ep.tail_S, st);
+  launch_nt64<EPI_TAIL, false>(A, lda, B, ldb, M, N, K, et, r * ep.tail_S, st);
   tail_finish_kernel<EPI><<<r * 8, 256, 0, st>>>(et, M, N, g_gemm_group);
 }
 
 }  // namespace
 
-void jm_gemm_set_variant(int wn, int group) {
-  if (wn >= 20 && wn < 148) {  // 4-phase kernel + SCHED bits
-    g_p4_sched = wn - 20;
-    wn = 20;
-  }
-  g_gemm_wn = wn;
+// nt64 = 1 forces the 64-deep main loop (tests); group = row tiles per column sweep
+void jm_gemm_set_variant(int nt64, int group) {
+  g_gemm_nt64 = nt64;
   g_gemm_group = group;
 }
 
 void jm_gemm_set_tail(int on) { g_gemm_tail = on; }
-
-void jm_gemm_set_sk(int on) { g_sk = on; }
-
-void jm_gemm_set_pp(int on) { g_pp = on; }
 
 // Tail split plan for an NT launch: the last wave of output tiles (tiles % CUs of them) fills only
 // part of the chip; when it is at most a quarter wave, those tiles run split-K S ways (compact fp32
@@ -1934,7 +881,7 @@ void jm_gemm_set_pp(int on) { g_pp = on; }
 int jm_gemm_nt_tail_plan(int M, int N, int K, int epi, int* tail_r, long* ws_floats) {
   *tail_r = 0;
   *ws_floats = 0;
-  if (!g_gemm_tail || (g_gemm_wn != 12 && g_gemm_wn != 6 && g_gemm_wn != 20)) return 0;
+  if (!g_gemm_tail) return 0;
   if (!(epi == EPI_STORE || epi == EPI_GELU || epi == EPI_DGELU || epi == EPI_GELU_ONLY) || N % 8 || K % 128) return 0;
   const int ncu = num_cus();
   const int tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
@@ -1952,11 +899,10 @@ int jm_gemm_nt_tail_plan(int M, int N, int K, int epi, int* tail_r, long* ws_flo
   return S;
 }
 
-
 // returns 0 on success, <0 on unsupported shape
 int jm_gemm_nt(const uint16_t* A, long lda, const uint16_t* B, long ldb, int M, int N, int K, int epi,
                const GemmEpi& ep, hipStream_t st) {
-  if (K % (2 * BK) || N % 4 || M <= 0 || N <= 0) return -1;
+  if (K % 64 || N % 4 || M <= 0 || N <= 0) return -1;
   if ((long)M * lda * 2 >= (1L << 32) || (long)N * ldb * 2 >= (1L << 32)) return -2;
   const int nwg = ((M + BM - 1) / BM) * ((N + BN - 1) / BN) * (epi == EPI_PARTIAL ? ep.splits : 1);
   if (epi == EPI_PARTIAL && (ep.splits < 1 || (K / 64) < ep.splits)) return -4;
@@ -1979,14 +925,10 @@ int jm_gemm_nt(const uint16_t* A, long lda, const uint16_t* B, long ldb, int M, 
     launch_epi<EPI_GELU_ONLY>(A, lda, B, ldb, M, N, K, ep, nwg, st);
   else if (epi == EPI_DGELU && N % 8 == 0)
     launch_epi<EPI_DGELU>(A, lda, B, ldb, M, N, K, ep, nwg, st);
-  else if (epi == EPI_GELU_D && g_gemm_wn == 20 && K % 128 == 0)
-    launch_p4<EPI_GELU_D>(A, lda, B, ldb, M, N, K, ep, nwg, st);
-  else if (epi == EPI_GELU_D)  // default kernel only (no A/B variants for the saved-derivative pair)
-    launch_nt64<EPI_GELU_D, 4>(A, lda, B, ldb, M, N, K, ep, nwg, st);
-  else if (epi == EPI_DMUL && N % 8 == 0 && g_gemm_wn == 20 && K % 128 == 0)
-    launch_p4<EPI_DMUL>(A, lda, B, ldb, M, N, K, ep, nwg, st);
+  else if (epi == EPI_GELU_D)
+    launch_epi<EPI_GELU_D>(A, lda, B, ldb, M, N, K, ep, nwg, st);
   else if (epi == EPI_DMUL && N % 8 == 0)
-    launch_nt64<EPI_DMUL, 4>(A, lda, B, ldb, M, N, K, ep, nwg, st);
+    launch_epi<EPI_DMUL>(A, lda, B, ldb, M, N, K, ep, nwg, st);
   else
     return -3;
   return 0;

@@ -107,15 +107,15 @@ struct TnSegs {
 
 namespace {
 
-// ACC = 1: G += tile (S == 1), 0: store the fp32 partial tile.  With ACC = 0 and g0 set, split 0
-// adds its tile straight into G (g0, ldg0) and split s >= 1 stores partial slice s - 1: the
-// reduction then reads S - 1 slices, and one slice is never written nor read back.
+// ACC = 1: G += tile (S == 1), 0: store the fp32 partial tile of split s into slice s.  (Split 0
+// adding straight into G measured slower -- the read-modify-write exposes a load latency in the
+// epilogue, profiles/r1_ab_tn_acc0.txt -- and so did float-atomic split reduction,
+// profiles/r2_tn_atomic.txt; both removed.)
 template <int ACC, bool SEG = false>
 __global__ __launch_bounds__(NTH, 1) void gemm_tn_kernel(const uint16_t* __restrict__ A, long lda,
                                                          const uint16_t* __restrict__ B, long ldb, int M, int N,
                                                          int K, int steps_per_split, float* __restrict__ out,
-                                                         long ldo, long split_stride, TnSegs segs = {},
-                                                         float* __restrict__ g0 = nullptr, long ldg0 = 0) {
+                                                         long ldo, long split_stride, TnSegs segs = {}) {
   JM_DGUARD(blockDim.x == NTH && steps_per_split >= 1 && M > 0);
   extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
   const int tid = threadIdx.x;
@@ -254,17 +254,15 @@ __global__ __launch_bounds__(NTH, 1) void gemm_tn_kernel(const uint16_t* __restr
   step(K0{}, t + 1, f1, f0);
 
   // ---- epilogue: acc[mt][nt][i] = G[n0 + wr*128 + mt*16 + l16][k0 + wc*64 + nt*16 + 4g + i]
-  const bool to_g = !ACC && g0 != nullptr && split == 0;  // workgroup-uniform
-  float* dst = ACC ? out : to_g ? g0 : out + (long)(g0 != nullptr ? split - 1 : split) * split_stride;
-  const long ld = to_g ? ldg0 : ldo;
+  float* dst = ACC ? out : out + (long)split * split_stride;
 #pragma unroll
   for (int mt = 0; mt < 8; ++mt) {
     const int n = n0 + wr * 128 + mt * 16 + l16;
-    float* row = dst + (long)n * ld + k0 + wc * 64 + 4 * g;
+    float* row = dst + (long)n * ldo + k0 + wc * 64 + 4 * g;
 #pragma unroll
     for (int nt = 0; nt < 4; ++nt) {
       float v[4] = {acc[mt][nt][0], acc[mt][nt][1], acc[mt][nt][2], acc[mt][nt][3]};
-      if (ACC || to_g) {
+      if (ACC) {
         float o[4];
         load4(row + nt * 16, o);
 #pragma unroll
@@ -294,8 +292,7 @@ template <int ACC, bool SEG>
 __global__ __launch_bounds__(NTH, 1) void gemm_tn4_kernel(const uint16_t* __restrict__ A, long lda,
                                                           const uint16_t* __restrict__ B, long ldb, int M, int N,
                                                           int K, int steps_per_split, float* __restrict__ out,
-                                                          long ldo, long split_stride, TnSegs segs = {},
-                                                          float* __restrict__ g0 = nullptr, long ldg0 = 0) {
+                                                          long ldo, long split_stride, TnSegs segs = {}) {
   JM_DGUARD(blockDim.x == NTH && steps_per_split >= 4 && steps_per_split % 4 == 0 && M > 0);
   extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
   const int tid = threadIdx.x;
@@ -479,52 +476,15 @@ __global__ __launch_bounds__(NTH, 1) void gemm_tn4_kernel(const uint16_t* __rest
   ktile(K0{}, t + 1, bq, bp);
 
   // ---- epilogue: acc[mt][nt][i] = G[n0 + wr*128 + mt*16 + l16][k0 + wc*64 + nt*16 + 4g + i]
-  if constexpr (ACC == 2) {
-    // atomic split reduction (jm_gemm_tn_set_atomic): every split adds its tile into G (out, ldo)
-    // with float atomics -- no fp32 partial slices, no reduce pass.  The tile is restaged through
-    // the (drained) ring in two 128-row halves, [128][256] fp32 = 128 KB, 16-byte chunks XOR-
-    // swizzled by (row & 15), so each wave-wide atomic covers 64 consecutive floats (256 B) of one
-    // G row instead of 16 rows x 4 scattered floats.
-    float* cs = reinterpret_cast<float*>(smem);
-    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      __syncthreads();
-      if (wr == h) {
-#pragma unroll
-        for (int mt = 0; mt < 8; ++mt) {
-          const int r = mt * 16 + l16;
-#pragma unroll
-          for (int nt = 0; nt < 4; ++nt) {
-            const int chunk = ((wc * 64 + nt * 16) >> 2) + g;
-            float v[4] = {acc[mt][nt][0], acc[mt][nt][1], acc[mt][nt][2], acc[mt][nt][3]};
-            store4(cs + r * 256 + ((chunk ^ (r & 15)) << 2), v);
-          }
-        }
-      }
-      __syncthreads();
-      for (int r = wave; r < 128; r += 8) {
-        float* grow = out + (long)(n0 + h * 128 + r) * ldo + k0;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int col = j * 64 + lane;
-          unsafeAtomicAdd(grow + col, cs[r * 256 + ((((col >> 2) ^ (r & 15))) << 2) + (col & 3)]);
-        }
-      }
-    }
-    return;
-  }
-  const bool to_g = !ACC && g0 != nullptr && split == 0;  // workgroup-uniform
-  float* dst = ACC ? out : to_g ? g0 : out + (long)(g0 != nullptr ? split - 1 : split) * split_stride;
-  const long ld = to_g ? ldg0 : ldo;
+  float* dst = ACC ? out : out + (long)split * split_stride;
 #pragma unroll
   for (int mt = 0; mt < 8; ++mt) {
     const int n = n0 + wr * 128 + mt * 16 + l16;
-    float* row = dst + (long)n * ld + k0 + wc * 64 + 4 * g;
+    float* row = dst + (long)n * ldo + k0 + wc * 64 + 4 * g;
 #pragma unroll
     for (int nt = 0; nt < 4; ++nt) {
       float v[4] = {acc[mt][nt][0], acc[mt][nt][1], acc[mt][nt][2], acc[mt][nt][3]};
-      if (ACC || to_g) {
+      if (ACC) {
         float o[4];
         load4(row + nt * 16, o);
 #pragma unroll
@@ -541,17 +501,11 @@ size_t jm_gemm_tn_smem() { return (size_t)NST * STAGE * sizeof(uint16_t); }
 
 // Split of the M range: returns steps (of 32 rows) per split; *S_out = number of splits.
 // Picks the split count that minimises an estimate of (waves of 256 CUs) x (steps per split +
-// epilogue) + the fp32 partial-tile traffic of the reduction.
-int g_tn_atomic = 0;
-double g_tn_red_scale = 1.0;  // A/B: weight of the partial-slice traffic in the split plan
-void jm_gemm_tn_set_red_scale(double v) { g_tn_red_scale = v; }
-int g_tn4 = 1;  // A/B: 4-phase TN kernel (default) vs the r1 32-row-step kernel (jm_gemm_tn_set_variant)
-void jm_gemm_tn_set_variant(int v) { g_tn4 = v == 4; }
-
+// epilogue) + the fp32 partial-tile traffic of the reduction (weight A/B: profiles/r2_tn_plan_scale.txt).
 int jm_gemm_tn_plan(int M, int N, int K, int* S_out) {
   const int tiles = (N / TN_) * (K / TK_);
   const int steps = (M + BS - 1) / BS;
-  const int unit = g_tn4 ? 4 : 2;  // steps per split: whole 128-row (4-phase) / 64-row pairs
+  const int unit = 4;  // steps per split: whole 128-row units of the 4-phase kernel
   double best = 1e30;
   int best_sps = (steps + unit - 1) / unit * unit, best_S = 1;
   for (int S = 1; S <= 128; ++S) {
@@ -562,9 +516,7 @@ int jm_gemm_tn_plan(int M, int N, int K, int* S_out) {
     const long wgs = (long)tiles * s_eff;
     const long waves = (wgs + 255) / 256;
     const double t_steps = (double)waves * (sps + 12);                       // ~1 us per step
-    double t_red = s_eff > 1 ? (double)s_eff * N * K * 8.0 / 5.0e12 * 1e6 : 0.0;  // us
-    if (g_tn_atomic >= 2) t_red /= (double)(1 << (g_tn_atomic - 1));  // A/B: atomics priced lower
-    t_red *= g_tn_red_scale;
+    const double t_red = s_eff > 1 ? (double)s_eff * N * K * 8.0 / 5.0e12 * 1e6 : 0.0;  // us
     const double est = t_steps + t_red;
     if (est < best) {
       best = est;
@@ -576,76 +528,52 @@ int jm_gemm_tn_plan(int M, int N, int K, int* S_out) {
   return best_sps;
 }
 
+namespace {
+template <typename KERN>
+void set_smem_once(KERN k, bool& done) {
+  if (!done) {
+    (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)jm_gemm_tn_smem());
+    done = true;
+  }
+}
+
+// the 4-phase kernel (whole 128-row units, 64-row segments) or the r1 32-row-step kernel
+template <bool SEG>
+int launch_tn(const uint16_t* A, long lda, const uint16_t* B, long ldb, int M, int N, int K, int sps, int S,
+              float* G, long ldo, float* partial, const TnSegs& segs, bool p4, hipStream_t st) {
+  const int tiles = (N / TN_) * (K / TK_);
+  const size_t sm = jm_gemm_tn_smem();
+  if (S > 1 && partial == nullptr) return -3;
+  if (p4) {
+    if (S == 1) {
+      static bool a = false;
+      set_smem_once(gemm_tn4_kernel<1, SEG>, a);
+      gemm_tn4_kernel<1, SEG><<<tiles, NTH, sm, st>>>(A, lda, B, ldb, M, N, K, sps, G, ldo, 0, segs);
+    } else {
+      static bool a = false;
+      set_smem_once(gemm_tn4_kernel<0, SEG>, a);
+      gemm_tn4_kernel<0, SEG><<<tiles * S, NTH, sm, st>>>(A, lda, B, ldb, M, N, K, sps, partial, K, (long)N * K,
+                                                          segs);
+    }
+  } else if (S == 1) {
+    static bool a = false;
+    set_smem_once(gemm_tn_kernel<1, SEG>, a);
+    gemm_tn_kernel<1, SEG><<<tiles, NTH, sm, st>>>(A, lda, B, ldb, M, N, K, sps, G, ldo, 0, segs);
+  } else {
+    static bool a = false;
+    set_smem_once(gemm_tn_kernel<0, SEG>, a);
+    gemm_tn_kernel<0, SEG><<<tiles * S, NTH, sm, st>>>(A, lda, B, ldb, M, N, K, sps, partial, K, (long)N * K, segs);
+  }
+  return 0;
+}
+}  // namespace
+
 // G[N][K] (ldo) += A[M][N]^T . B[M][K]; partial: [S][N][K] fp32 workspace when S > 1 (else null)
-// split 0 accumulates into G (partial then holds S - 1 slices).  A/B switch, off: the in-kernel
-// read-modify-write of G exposes a load latency in every split-0 epilogue and measured slower than
-// writing the extra slice (ViT-L step 97.80 -> 98.76 ms, profiles/r1_ab_tn_acc0.txt)
-int g_tn_acc0 = 0;
-int jm_gemm_tn_acc0() { return g_tn_acc0; }
-void jm_gemm_tn_set_acc0(int v) { g_tn_acc0 = v; }
-
-// A/B: split reduction by float atomics into G from the 4-phase kernel's epilogue (ACC = 2) instead
-// of fp32 partial slices + jm_splitk_reduce_add.  Summation order then varies from run to run.
-// Off: measured 2 ms/step slower on the ViT-L step (95.3 -> 97.3 ms, profiles/r2_tn_atomic.txt).
-// Values >= 2 also price the split reduction 2^(v-1) x cheaper in jm_gemm_tn_plan (more splits).
-int jm_gemm_tn_atomic() { return g_tn_atomic && g_tn4; }
-void jm_gemm_tn_set_atomic(int v) { g_tn_atomic = v; }
-
-// partial: [S][N][K] fp32 (or [S - 1][N][K] when jm_gemm_tn_acc0())
 int jm_gemm_tn(const uint16_t* A, long lda, const uint16_t* B, long ldb, int M, int N, int K, int sps, int S,
                float* G, long ldo, float* partial, hipStream_t st) {
   if (N % TN_ || K % TK_ || M <= 0) return -1;
   if ((long)M * lda * 2 >= (1L << 32) || (long)M * ldb * 2 >= (1L << 32)) return -2;
-  const int tiles = (N / TN_) * (K / TK_);
-  const size_t sm = jm_gemm_tn_smem();
-  if (g_tn4 && sps % 4 == 0) {
-    if (S == 1) {
-      static bool attr = false;
-      if (!attr) {
-        (void)hipFuncSetAttribute((const void*)gemm_tn4_kernel<1, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  (int)sm);
-        attr = true;
-      }
-      gemm_tn4_kernel<1, false><<<tiles, NTH, sm, st>>>(A, lda, B, ldb, M, N, K, sps, G, ldo, 0);
-    } else if (g_tn_atomic && partial == nullptr) {
-      static bool attr = false;
-      if (!attr) {
-        (void)hipFuncSetAttribute((const void*)gemm_tn4_kernel<2, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  (int)sm);
-        attr = true;
-      }
-      gemm_tn4_kernel<2, false><<<tiles * S, NTH, sm, st>>>(A, lda, B, ldb, M, N, K, sps, G, ldo, 0);
-    } else {
-      if (partial == nullptr) return -3;
-      static bool attr = false;
-      if (!attr) {
-        (void)hipFuncSetAttribute((const void*)gemm_tn4_kernel<0, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  (int)sm);
-        attr = true;
-      }
-      gemm_tn4_kernel<0, false><<<tiles * S, NTH, sm, st>>>(A, lda, B, ldb, M, N, K, sps, partial, K, (long)N * K,
-                                                            TnSegs{}, g_tn_acc0 ? G : nullptr, ldo);
-    }
-    return 0;
-  }
-  if (S == 1) {
-    static bool attr = false;
-    if (!attr) {
-      (void)hipFuncSetAttribute((const void*)gemm_tn_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
-      attr = true;
-    }
-    gemm_tn_kernel<1><<<tiles, NTH, sm, st>>>(A, lda, B, ldb, M, N, K, sps, G, ldo, 0);
-  } else {
-    if (partial == nullptr) return -3;
-    static bool attr = false;
-    if (!attr) {
-      (void)hipFuncSetAttribute((const void*)gemm_tn_kernel<0>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
-      attr = true;
-    }
-    gemm_tn_kernel<0><<<tiles * S, NTH, sm, st>>>(A, lda, B, ldb, M, N, K, sps, partial, K, (long)N * K, TnSegs{},
-                                                  g_tn_acc0 ? G : nullptr, ldo);
-  }
-  return 0;
+  return launch_tn<false>(A, lda, B, ldb, M, N, K, sps, S, G, ldo, partial, TnSegs{}, sps % 4 == 0, st);
 }
 
 // Segmented-M variant of jm_gemm_tn: A / B rows come from segs (n blocks of segs.rows rows).
@@ -654,58 +582,8 @@ int jm_gemm_tn_seg(const TnSegs& segs, long lda, long ldb, int N, int K, int sps
   if (N % TN_ || K % TK_ || segs.n < 1 || segs.n > 32 || segs.rows % BS) return -1;
   if ((long)segs.rows * lda * 2 >= (1L << 32) || (long)segs.rows * ldb * 2 >= (1L << 32)) return -2;
   const int M = segs.rows * segs.n;
-  const int tiles = (N / TN_) * (K / TK_);
-  const size_t sm = jm_gemm_tn_smem();
-  if (g_tn4 && sps % 4 == 0 && segs.rows % 64 == 0) {
-    if (S == 1) {
-      static bool attr = false;
-      if (!attr) {
-        (void)hipFuncSetAttribute((const void*)gemm_tn4_kernel<1, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  (int)sm);
-        attr = true;
-      }
-      gemm_tn4_kernel<1, true><<<tiles, NTH, sm, st>>>(nullptr, lda, nullptr, ldb, M, N, K, sps, G, ldo, 0, segs);
-    } else if (g_tn_atomic && partial == nullptr) {
-      static bool attr = false;
-      if (!attr) {
-        (void)hipFuncSetAttribute((const void*)gemm_tn4_kernel<2, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  (int)sm);
-        attr = true;
-      }
-      gemm_tn4_kernel<2, true><<<tiles * S, NTH, sm, st>>>(nullptr, lda, nullptr, ldb, M, N, K, sps, G, ldo, 0, segs);
-    } else {
-      if (partial == nullptr) return -3;
-      static bool attr = false;
-      if (!attr) {
-        (void)hipFuncSetAttribute((const void*)gemm_tn4_kernel<0, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  (int)sm);
-        attr = true;
-      }
-      gemm_tn4_kernel<0, true><<<tiles * S, NTH, sm, st>>>(nullptr, lda, nullptr, ldb, M, N, K, sps, partial, K,
-                                                           (long)N * K, segs, g_tn_acc0 ? G : nullptr, ldo);
-    }
-    return 0;
-  }
-  if (S == 1) {
-    static bool attr = false;
-    if (!attr) {
-      (void)hipFuncSetAttribute((const void*)gemm_tn_kernel<1, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)sm);
-      attr = true;
-    }
-    gemm_tn_kernel<1, true><<<tiles, NTH, sm, st>>>(nullptr, lda, nullptr, ldb, M, N, K, sps, G, ldo, 0, segs);
-  } else {
-    if (partial == nullptr) return -3;
-    static bool attr = false;
-    if (!attr) {
-      (void)hipFuncSetAttribute((const void*)gemm_tn_kernel<0, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)sm);
-      attr = true;
-    }
-    gemm_tn_kernel<0, true><<<tiles * S, NTH, sm, st>>>(nullptr, lda, nullptr, ldb, M, N, K, sps, partial, K,
-                                                        (long)N * K, segs, g_tn_acc0 ? G : nullptr, ldo);
-  }
-  return 0;
+  return launch_tn<true>(nullptr, lda, nullptr, ldb, M, N, K, sps, S, G, ldo, partial, segs,
+                         sps % 4 == 0 && segs.rows % 64 == 0, st);
 }
 
 JM_DEBUG_EXPORT(gemm_tn)

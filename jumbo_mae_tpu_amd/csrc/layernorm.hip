@@ -194,13 +194,9 @@ struct ParamOuts {
 };
 
 // partial rows in ws: [dgamma | dbeta] (NP = 2) or [dgamma | dbeta | dscale | dbias] (NP = 4)
-// LA (LDS accumulation): the per-column parameter partials are added into the block's LDS row
-// with ds_add_f32 instead of living in registers across the row loop (64 fewer VGPRs at D=1024:
-// twice the waves per SIMD for this memory-bound kernel), and the residual-gradient input is
-// loaded together with x / dy so each row costs one HBM round trip instead of two.
 // ER (early residual-gradient load): dres is loaded together with x / dy in the first pass (one
 // HBM round trip per row instead of two) while the parameter partials stay in registers.
-template <int V, typename TI, bool RES, bool LA = false, bool ER = false>
+template <int V, typename TI, bool RES, bool ER = false>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(const TI* __restrict__ dy, const float* __restrict__ x,
                                                      long sB, long sT, int T, int rows, int D,
                                                      const float* __restrict__ mean, const float* __restrict__ rstd,
@@ -208,29 +204,18 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const TI* __restrict__ dy, 
                                                      float* __restrict__ ws, int accum_params, ParamOuts outs) {
   JM_DGUARD(blockDim.x == 256 && D % 4 == 0 && D <= V * 256);
   constexpr int NP = RES ? 4 : 2;
-  constexpr int NA = LA ? 1 : NP;  // register accumulators kept (dummy when LA)
   extern __shared__ __attribute__((aligned(16))) float red[];  // [NP*D]
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const bool partials = accum_params || RES;
-  if (LA && partials) {
-    for (int i = threadIdx.x; i < NP * D; i += 256) red[i] = 0.f;
-    __syncthreads();
-  }
-  auto acc_add = [&](float (&acc)[NA][V][4], int k, int i, int j, float v) {
-    if constexpr (LA) {
-      atomicAdd(&red[k * D + (i * 64 + lane) * 4 + j], v);
-    } else {
-      acc[k % NA][i][j] += v;
-    }
-  };
-  float acc[NA][V][4], gg[V][4], sc[V][4];
+  auto acc_add = [&](float (&acc)[NP][V][4], int k, int i, int j, float v) { acc[k][i][j] += v; };
+  float acc[NP][V][4], gg[V][4], sc[V][4];
 #pragma unroll
   for (int i = 0; i < V; ++i) {
     const int col = (i * 64 + lane) * 4;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
 #pragma unroll
-      for (int k = 0; k < NA; ++k) acc[k][i][j] = 0.f;
+      for (int k = 0; k < NP; ++k) acc[k][i][j] = 0.f;
       sc[i][j] = 1.f;
     }
     if (col < D) {
@@ -246,7 +231,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const TI* __restrict__ dy, 
     const bool rrow = RES && t >= rio.T0;
     const long yoff = RES ? b * rio.yB + (long)(t - rio.T0) * rio.yT : 0;
     float xh[V][4], g[V][4], yv[V][4];
-    float rvp[(LA || ER) ? V : 1][4];
+    float rvp[ER ? V : 1][4];
     const float* rr = io.dres ? io.dres + b * io.rB + t * io.rT : nullptr;
     float sg = 0.f, sgx = 0.f;
 #pragma unroll
@@ -257,7 +242,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const TI* __restrict__ dy, 
         load4(xr + col, xv);
         load4(dyr + col, dv);
         if (RES && rrow && rio.scale) load4(rio.y + yoff + col, yv[i]);
-        if constexpr (LA || ER) {
+        if constexpr (ER) {
           if (rr) load4(rr + col, rvp[i]);
           else rvp[i][0] = rvp[i][1] = rvp[i][2] = rvp[i][3] = 0.f;
         }
@@ -284,7 +269,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const TI* __restrict__ dy, 
       const int col = (i * 64 + lane) * 4;
       if (col < D) {
         float o[4], rv[4] = {0.f, 0.f, 0.f, 0.f};
-        if constexpr (LA || ER) {
+        if constexpr (ER) {
 #pragma unroll
           for (int j = 0; j < 4; ++j) rv[j] = rvp[i][j];
         } else if (rr) {
@@ -316,158 +301,8 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const TI* __restrict__ dy, 
       if (dst != nullptr) atomicAdd(&dst[i - (i / D) * D], red[i]);
     }
   };
-  if constexpr (LA) {
-    __syncthreads();
-    if (ws == nullptr) return direct();
-    for (int i = threadIdx.x * 4; i < NP * D; i += 256 * 4) {
-      float a[4];
-      load4(red + i, a);
-      store4(ws + (long)blockIdx.x * NP * D + i, a);
-    }
-    return;
-  }
   // merge the 4 waves' partials through LDS in turn (float4, conflict-free, no atomics), then
   // one coalesced store of the block partial row into the workspace
-  for (int w = 0; w < 4; ++w) {
-    if (wave == w) {
-#pragma unroll
-      for (int i = 0; i < V; ++i) {
-        const int col = (i * 64 + lane) * 4;
-        if (col < D) {
-#pragma unroll
-          for (int k = 0; k < NP; ++k) {
-            float a[4] = {0.f, 0.f, 0.f, 0.f};
-            if (w > 0) load4(red + k * D + col, a);
-#pragma unroll
-            for (int j = 0; j < 4; ++j) a[j] += acc[k % NA][i][j];
-            store4(red + k * D + col, a);
-          }
-        }
-      }
-    }
-    __syncthreads();
-  }
-  if (ws == nullptr) return direct();
-  for (int i = threadIdx.x * 4; i < NP * D; i += 256 * 4) {
-    float a[4];
-    load4(red + i, a);
-    store4(ws + (long)blockIdx.x * NP * D + i, a);
-  }
-}
-
-// ln_bwd_kernel<..., ER> with a one-row software pipeline: the x / dy / dres (/ y) loads of the
-// wave's NEXT row are issued before the current row's reduction, math and stores, so every wave
-// keeps a row of loads in flight while it computes (the kernel is HBM-bound at 2 waves / SIMD:
-// ~190 VGPRs, most of them the per-column parameter partials).
-template <int V, typename TI, bool RES>
-__global__ __launch_bounds__(256) void ln_bwd_pf_kernel(const TI* __restrict__ dy, const float* __restrict__ x,
-                                                        long sB, long sT, int T, int rows, int D,
-                                                        const float* __restrict__ mean, const float* __restrict__ rstd,
-                                                        const float* __restrict__ gamma, LnBwdIO io, LnResIO rio,
-                                                        float* __restrict__ ws, int accum_params) {
-  JM_DGUARD(blockDim.x == 256 && D % 4 == 0 && D <= V * 256);
-  constexpr int NP = RES ? 4 : 2;
-  extern __shared__ __attribute__((aligned(16))) float red[];  // [NP*D]
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const bool partials = accum_params || RES;
-  float acc[NP][V][4], gg[V][4], sc[V][4];
-#pragma unroll
-  for (int i = 0; i < V; ++i) {
-    const int col = (i * 64 + lane) * 4;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-#pragma unroll
-      for (int k = 0; k < NP; ++k) acc[k][i][j] = 0.f;
-      sc[i][j] = 1.f;
-    }
-    if (col < D) {
-      load4(gamma + col, gg[i]);
-      if (RES && rio.scale) load4(rio.scale + col, sc[i]);
-    }
-  }
-  const bool use_y = RES && rio.scale;
-  float xv[V][4], dv[V][4], rv[V][4], yv[V][4];
-  auto load_row = [&](int row) {
-    const int b = row / T, t = row - b * T;
-    const float* xr = x + b * sB + t * sT;
-    const TI* dyr = dy + (long)row * D;
-    const float* rr = io.dres ? io.dres + b * io.rB + t * io.rT : nullptr;
-    const bool rrow = RES && t >= rio.T0;
-    const long yoff = RES ? b * rio.yB + (long)(t - rio.T0) * rio.yT : 0;
-#pragma unroll
-    for (int i = 0; i < V; ++i) {
-      const int col = (i * 64 + lane) * 4;
-      if (col < D) {
-        load4(xr + col, xv[i]);
-        load4(dyr + col, dv[i]);
-        if (use_y && rrow) load4(rio.y + yoff + col, yv[i]);
-        if (rr) load4(rr + col, rv[i]);
-        else rv[i][0] = rv[i][1] = rv[i][2] = rv[i][3] = 0.f;
-      }
-    }
-  };
-  int row = blockIdx.x * 4 + wave;
-  const int step = gridDim.x * 4;
-  if (row < rows) load_row(row);
-  for (; row < rows; row += step) {
-    const int b = row / T, t = row - b * T;
-    const float mu = mean[row], rs = rstd[row];
-    const bool rrow = RES && t >= rio.T0;
-    const long yoff = RES ? b * rio.yB + (long)(t - rio.T0) * rio.yT : 0;
-    float xh[V][4], g[V][4], r[V][4], y[V][4];
-    float sg = 0.f, sgx = 0.f;
-#pragma unroll
-    for (int i = 0; i < V; ++i) {
-      const int col = (i * 64 + lane) * 4;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        r[i][j] = rv[i][j];
-        y[i][j] = yv[i][j];
-      }
-      if (col < D) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          xh[i][j] = (xv[i][j] - mu) * rs;
-          g[i][j] = dv[i][j] * gg[i][j];
-          sg += g[i][j];
-          sgx += g[i][j] * xh[i][j];
-          acc[0][i][j] += dv[i][j] * xh[i][j];
-          acc[1][i][j] += dv[i][j];
-        }
-      } else {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) xh[i][j] = g[i][j] = 0.f;
-      }
-    }
-    // the next row's loads fly while this row reduces, computes and stores
-    if (row + step < rows) load_row(row + step);
-    sg = wave_sum(sg) / D;
-    sgx = wave_sum(sgx) / D;
-    float* dxr = io.dx + b * io.oB + t * io.oT;
-    const float m = (RES && rio.mask) ? rio.mask[b] : 1.f;
-#pragma unroll
-    for (int i = 0; i < V; ++i) {
-      const int col = (i * 64 + lane) * 4;
-      if (col < D) {
-        float o[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) o[j] = rs * (g[i][j] - sg - xh[i][j] * sgx) + r[i][j];
-        store4(dxr + col, o);
-        if (RES && rrow) {
-          float d[4];
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const float md = m * o[j];
-            d[j] = md * sc[i][j];
-            if (use_y) acc[2 % NP][i][j] += md * y[i][j];
-            acc[3 % NP][i][j] += bf2f(f2bf(d[j]));  // colsum of the bf16 values the GEMMs consume
-          }
-          store4(rio.dy + yoff + col, d);
-        }
-      }
-    }
-  }
-  if (!partials) return;
   for (int w = 0; w < 4; ++w) {
     if (wave == w) {
 #pragma unroll
@@ -487,6 +322,7 @@ __global__ __launch_bounds__(256) void ln_bwd_pf_kernel(const TI* __restrict__ d
     }
     __syncthreads();
   }
+  if (ws == nullptr) return direct();
   for (int i = threadIdx.x * 4; i < NP * D; i += 256 * 4) {
     float a[4];
     load4(red + i, a);
@@ -496,7 +332,6 @@ __global__ __launch_bounds__(256) void ln_bwd_pf_kernel(const TI* __restrict__ d
 
 // out_k[c] += sum_b ws[b][k*D + c] for the NP partial vectors (null outputs skipped); grid.y
 // splits the partial rows.
-
 __global__ __launch_bounds__(256) void ln_param_reduce_kernel(const float* __restrict__ ws, int nb, int D, int NP,
                                                               ParamOuts outs) {
   // one float4 of columns per thread while loading (the whole 4-8 MB workspace in flight at once:
@@ -712,36 +547,24 @@ constexpr int LN_WIDE_MAX_ROWS = 8192;
 int pick_vw(int D) { return D <= 2048 ? 2 : D <= 3072 ? 3 : D <= 4096 ? 4 : -1; }
 bool use_wide(int rows, int D) { return D > 1024 && rows <= LN_WIDE_MAX_ROWS && pick_vw(D) > 0; }
 
-// runtime switch (A/B): 0 = register partials, dres loaded after the row reduction; 1 = LDS-accumulated
-// parameter partials + early dres load (the ds_add_f32 accumulation made the ViT-L step 97.8 ->
-// 122.2 ms despite the doubled occupancy, profiles/r1_ab_ln_bwd_lds_acc.txt); 2 (default) = register
-// partials + early dres load: 97.96 -> 97.75 ms/step (profiles/r1_ab_ln_bwd_early_dres.txt);
-// 3 = 2 + the next row's loads issued before this row's math (ln_bwd_pf_kernel)
-int g_ln_bwd_la = 2;
 // LN backward parameter partials: 1 = float atomics from each block straight into the outputs,
 // 0 = per-block workspace rows + ln_param_reduce_kernel (default: the direct form measured the
 // same step time, ViT-L 94.05 vs 93.90 ms in one process -- 512 adders per address cost what the
 // reduce launch did; profiles/r2_ln_param_reduce.txt)
 int g_ln_direct = 0;
 
+// the residual-gradient input is loaded with x / dy (ER) where the registers allow it (V <= 4:
+// 97.96 -> 97.75 ms/step, profiles/r1_ab_ln_bwd_early_dres.txt).  Measured and removed: LDS-
+// accumulated parameter partials (r1_ab_ln_bwd_lds_acc.txt), a next-row prefetch variant
+// (r2_ln_bwd_prefetch.txt).
 template <typename TI, bool RES>
 void launch_bwd(int V, dim3 grid, size_t smem, hipStream_t st, const TI* dy, const float* x, long sB, long sT,
                 int T, int rows, int D, const float* m, const float* r, const float* g, LnBwdIO dx, LnResIO rio,
                 float* ws, int acc, ParamOuts outs) {
 #define JM_LNB(VV)                                                                                          \
   case VV:                                                                                                  \
-    if (g_ln_bwd_la == 1 && VV >= 2 && VV <= 4)                                                             \
-      ln_bwd_kernel<VV, TI, RES, true><<<grid, 256, smem, st>>>(dy, x, sB, sT, T, rows, D, m, r, g, dx, rio, ws, \
-                                                                 acc, outs);                                   \
-    else if (g_ln_bwd_la == 3 && VV >= 2 && VV <= 4)                                                        \
-      ln_bwd_pf_kernel<VV, TI, RES><<<grid, 256, smem, st>>>(dy, x, sB, sT, T, rows, D, m, r, g, dx, rio, ws,   \
-                                                             acc);                                          \
-    else if (g_ln_bwd_la == 2 && VV >= 2 && VV <= 4)                                                        \
-      ln_bwd_kernel<VV, TI, RES, false, true><<<grid, 256, smem, st>>>(dy, x, sB, sT, T, rows, D, m, r, g, dx, \
-                                                                        rio, ws, acc, outs);                \
-    else                                                                                                    \
-      ln_bwd_kernel<VV, TI, RES><<<grid, 256, smem, st>>>(dy, x, sB, sT, T, rows, D, m, r, g, dx, rio, ws, acc, \
-                                                          outs);                                             \
+    ln_bwd_kernel<VV, TI, RES, (VV >= 2 && VV <= 4)><<<grid, 256, smem, st>>>(dy, x, sB, sT, T, rows, D, m, r, \
+                                                                              g, dx, rio, ws, acc, outs);     \
     break;
   switch (V) {
     JM_LNB(1) JM_LNB(2) JM_LNB(3) JM_LNB(4) JM_LNB(6) JM_LNB(8) JM_LNB(9) JM_LNB(12) JM_LNB(16)
@@ -810,7 +633,6 @@ int jm_residual_ln_fwd(const float* x, long sB, long sT, const uint16_t* y, cons
   return 0;
 }
 
-void jm_ln_set_bwd_la(int v) { g_ln_bwd_la = v; }
 void jm_ln_set_direct(int v) { g_ln_direct = v; }
 
 // runtime switch: most row-loop blocks of the (non-wide) LN backward
@@ -860,8 +682,8 @@ int jm_layernorm_bwd(const void* dy, int dy_bf16, const float* x, long sB, long 
   const size_t smem = partials ? NP * D * sizeof(float) : 0;
   const ParamOuts outs{{accum_params ? dgamma : nullptr, accum_params ? dbeta : nullptr,
                         res ? res->dscale : nullptr, res ? res->dbias : nullptr}};
-  // direct atomics (the prefetch variant keeps the workspace + reduce form)
-  const bool direct = g_ln_direct && g_ln_bwd_la != 3;
+  // direct atomics or workspace + reduce
+  const bool direct = g_ln_direct;
   float* wsk = direct ? nullptr : ws;
   LnResIO rio{nullptr, nullptr, 0, 0, nullptr, nullptr, 0};
   if (res) rio = LnResIO{res->y, res->dy, res->yB, res->yT, res->scale, res->mask, res->T0};

@@ -169,6 +169,13 @@ class ShardDataset(IterableDataset):
                     continue
                 s = self._decode(rec)
                 if s is None:
+                    # a record that fails to decode still takes its r positions, so the per-sample
+                    # augmentation seeds of everything after it match a resumed run (whose skip
+                    # counts records without decoding them).  Exact resume assumes no corrupt
+                    # record BEFORE the resume point: the skip (samples consumed / r records) then
+                    # lands one record early per corrupt record and repeats its successor's samples.
+                    index += r - skip if skip else r
+                    skip = 0
                     continue
                 first, skip = skip, 0
                 index += first

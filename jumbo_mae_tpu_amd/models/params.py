@@ -177,7 +177,9 @@ class ParamStore:
         finds all copies fresh).  Returns False when batching is off / not applicable."""
         if not BATCH_TRANSPOSES:
             return False
-        hs = [h for h in self._handles if h._wt is not None and h._wt.dtype == torch.bfloat16 and h._wt.is_cuda]
+        # the batch kernel's 16-byte vector accesses need the single-transpose kernel's preconditions
+        hs = [h for h in self._handles if h._wt is not None and h._wt.dtype == torch.bfloat16 and h._wt.is_cuda
+              and len(h.shape) == 2 and h.shape[0] % 8 == 0 and h.shape[1] % 8 == 0]
         if not hs:
             return False
         key = tuple((h._wt.data_ptr(), h.shadow.data_ptr()) for h in hs)

@@ -30,12 +30,12 @@ def apply(P, cfg: str):
             P.set_wgrad_stream(v == "1")
         elif k == "JMAE_WGRAD":
             P._WGRAD_OURS = v == "1"
-        elif k == "GEMM_VARIANT":
+        elif k == "GEMM_NT64":  # 1: every NT launch on the 64-deep main loop
             from jumbo_mae_tpu_amd.ops import _ext
             _ext.load(True).gemm_set_variant(int(v), 8)
-        elif k == "GEMM_GROUP":  # row tiles per column sweep of the default (4-phase, variant 24) kernel
+        elif k == "GEMM_GROUP":  # row tiles per column sweep of the NT kernels
             from jumbo_mae_tpu_amd.ops import _ext
-            _ext.load(True).gemm_set_variant(24, int(v))
+            _ext.load(True).gemm_set_variant(0, int(v))
         elif k == "GEMM_TAIL":
             from jumbo_mae_tpu_amd.ops import _ext
             _ext.load(True).gemm_set_tail(int(v))
@@ -53,9 +53,6 @@ def apply(P, cfg: str):
         elif k == "LN_DIRECT":
             from jumbo_mae_tpu_amd.ops import _ext
             _ext.load(True).ln_set_direct(int(v))
-        elif k == "LN_BWD_LA":
-            from jumbo_mae_tpu_amd.ops import _ext
-            _ext.load(True).ln_set_bwd_la(int(v))
         elif k == "ATTN_HPW":
             from jumbo_mae_tpu_amd.ops import _ext
             _ext.load(True).attn_set_fwd_hpw(int(v))
@@ -65,15 +62,6 @@ def apply(P, cfg: str):
         elif k == "ATTN_TR":
             from jumbo_mae_tpu_amd.ops import _ext
             _ext.load(True).attn_set_tr(int(v))
-        elif k == "TN_RED_SCALE":  # weight of the partial traffic in the TN split plan
-            from jumbo_mae_tpu_amd.ops import _ext
-            _ext.load(True).gemm_tn_set_red_scale(float(v))
-        elif k == "GEMM_TN_ATOMIC":
-            from jumbo_mae_tpu_amd.ops import _ext
-            _ext.load(True).gemm_tn_set_atomic(int(v))
-        elif k == "GEMM_TN_ACC0":
-            from jumbo_mae_tpu_amd.ops import _ext
-            _ext.load(True).gemm_tn_set_acc0(int(v))
         elif k == "JMAE_GELU_DERIV":
             P._GELU_DERIV = v == "1"
         elif k == "JMAE_FWD_LINKS":

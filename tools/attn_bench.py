@@ -22,13 +22,12 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--shapes", default="dec,enc")
-    ap.add_argument("--tr", type=int, default=-1, help="kernel variant (ext.attn_set_tr), -1 = default")
+    ap.add_argument("--tr", type=int, default=-1, help="backward kernel (ext.attn_set_tr): 3 = batched bwd3 at hd 32, 2 = compact bwd2; -1 = default")
     ap.add_argument("--hpw", type=int, default=0, help="forward (b, h) pairs per workgroup, 0 = default")
     ap.add_argument("--ppw", type=int, default=0, help="backward batch elements per workgroup (bwd2), 0 = default")
     ap.add_argument("--remap", default="", help="comma list of attn_set_remap values to A/B (interleaved)")
     ap.add_argument("--max-seq", type=int, default=0, help="attn_set_max_seq (longer S -> tile-streamed kernels)")
     ap.add_argument("--bwd3-hd64", type=int, default=-1, help="attn_set_bwd3_hd64 (batched backward at hd 64)")
-    ap.add_argument("--db", type=int, default=-1, help="attn_set_bwd2_db (double-buffered encoder backward)")
     a = ap.parse_args()
     ext = _ext.load()
     remaps = [int(v) for v in a.remap.split(",")] if a.remap else [None]
@@ -42,8 +41,6 @@ def main():
         ext.attn_set_max_seq(a.max_seq)
     if a.bwd3_hd64 >= 0:
         ext.attn_set_bwd3_hd64(a.bwd3_hd64)
-    if a.db >= 0:
-        ext.attn_set_bwd2_db(a.db)
     for name in a.shapes.split(","):
         B, S, H, hd = SHAPES[name]
         D = H * hd

@@ -43,23 +43,18 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--only", default="")
     ap.add_argument("--kinds", default="fwd,fwd_gelu,dgrad")
-    ap.add_argument("--variant", default="12", help="kernel variant(s), comma separated (jm_gemm_set_variant); "
-                    "several = interleaved A/B in this process")
+    ap.add_argument("--variant", default="0", help="kernel variant(s), comma separated: 0 = default routing, "
+                    "1 = 64-deep main loop everywhere, suffix t = tail split; several = interleaved A/B")
     ap.add_argument("--group", type=int, default=8, help="row tiles per column sweep")
     ap.add_argument("--tail", type=int, default=0, help="tail split of the last partial wave (1 = on)")
     a = ap.parse_args()
     ext = _ext.load()
     ext.gemm_set_tail(a.tail)
-    # "24" = variant 24 as launched by default; suffix "s" = persistent DP + stream-K where planned,
-    # "d" = persistent whole tiles on the fewest CUs that keep the round count (gemm_set_sk 1 / 2)
     variants = a.variant.split(",")
 
-    def setv(v):  # suffixes: s / d = persistent stream-K / fewer-CU whole tiles, p = persistent overlapped,
-        # t = tail split (last partial wave split-K + finish kernel)
-        ext.gemm_set_sk(2 if "d" in v else 1 if "s" in v else 0)
-        ext.gemm_set_pp(1 if "p" in v else 0)
+    def setv(v):  # suffix t = tail split (last partial wave split-K + finish kernel)
         ext.gemm_set_tail(1 if "t" in v else 0)
-        ext.gemm_set_variant(int(v.rstrip("sdpt")), a.group)
+        ext.gemm_set_variant(int(v.rstrip("t")), a.group)
 
     setv(variants[0])
     names = [n for n in FWD if not a.only or n in a.only.split(",")]

@@ -42,10 +42,9 @@ def timeit(fn, iters=10):
 def main():
     import argparse
     ap = argparse.ArgumentParser()
-    ap.add_argument("--variants", default="4,0", help="TN kernel variants (gemm_tn_set_variant), first = 'ours'")
     ap.add_argument("--only", default="")
     a = ap.parse_args()
-    vs = [int(v) for v in a.variants.split(",")]
+    vs = [0]  # one TN kernel (the r1 / atomic / acc0 variants were removed; profiles/r1_*, r2_tn_*)
     ext = _ext.load()
     to_t = tb_t = 0.0
     for name, (M, N, K) in SHAPES.items():
@@ -55,7 +54,6 @@ def main():
         x = (torch.rand(M, K, device="cuda") * 2 - 1).bfloat16()
         g0 = torch.zeros(N, K, device="cuda")
         g1 = torch.zeros(N, K, device="cuda")
-        ext.gemm_tn_set_variant(vs[0])
         S = ext.gemm_tn_wgrad(dy, x, g0)
         blas(dy, x, g1)
         err = ((g0 - g1).abs().max() / g1.abs().max()).item()
@@ -63,10 +61,8 @@ def main():
         tbs = []
         for _ in range(3):
             for v in vs:
-                ext.gemm_tn_set_variant(v)
                 tv[v].append(timeit(lambda: ext.gemm_tn_wgrad(dy, x, g0)))
             tbs.append(timeit(lambda: blas(dy, x, g1)))
-        ext.gemm_tn_set_variant(vs[0])
         to, tb = min(tv[vs[0]]), min(tbs)
         fl = 2.0 * M * N * K
         if len(vs) > 1:
