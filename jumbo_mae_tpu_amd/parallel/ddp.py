@@ -22,18 +22,84 @@ MI355X design:
   (ops/prims.py flush_deferred_wgrads) and each chunk's slice is all-reduced as soon as it is
   written (``ParamStore.mark_partial_ready``), so only the last chunk's reduction is exposed
   instead of two 150 MB tensors (ViT-L).  Only single-segment buckets take partial launches.
+* Buckets are cut on layer boundaries (SURVEY.md §5.8 bucket plan): consecutive segments of one
+  encoder / decoder layer (or of the jumbo MLP, or of one top-level module) form a unit that is
+  never split across buckets unless the unit alone exceeds the bucket size; a segment larger
+  than the bucket size (the jumbo MLP kernels) is a bucket of its own, so it keeps its partial
+  launches.  At the 64 MiB default that is one ViT-L encoder layer (50 MB) per bucket, five
+  decoder layers, and one bucket per jumbo kernel.
+* ``reduce_dtype=bf16`` converts each bucket (or partial slice) into ONE preallocated bf16
+  staging buffer laid out like the flat gradient buffer -- no per-step allocation -- and copies
+  the averaged slice back after the collective; partial launches work the same way.
 """
 
 from __future__ import annotations
 
 import contextlib
 import os
+import re
 
 import torch
 import torch.distributed as dist
 
 from ..models.params import Handle, ParamStore
 from . import dist as pdist
+
+
+_LAYER = re.compile(r"(dec_)?layer_\d+")
+
+
+def unit_key(path: tuple[str, ...]) -> tuple[str, ...]:
+    """Bucketing unit of a parameter: its encoder / decoder layer, the shared jumbo MLP, or (for
+    everything else) its top-level module."""
+    for i, p in enumerate(path):
+        if p == "jumbo_mlp" or _LAYER.fullmatch(p):
+            return tuple(path[:i + 1])
+    return tuple(path[:2])
+
+
+def plan_buckets(sizes: list[int], keys: list[tuple], limit: int) -> list[list[int]]:
+    """Buckets (lists of segment indices, in launch order = from the END of the buffer) of at most
+    ``limit`` elements where possible: consecutive segments with one key form a unit that goes
+    into one bucket; a unit larger than ``limit`` is split greedily, and a segment larger than
+    ``limit`` is a bucket of its own."""
+    units: list[list[int]] = []
+    for i, k in enumerate(keys):
+        if units and keys[units[-1][0]] == k:
+            units[-1].append(i)
+        else:
+            units.append([i])
+    buckets: list[list[int]] = []
+    cur: list[int] = []
+    size = 0
+
+    def flush():
+        nonlocal cur, size
+        if cur:
+            buckets.append(cur)
+        cur, size = [], 0
+
+    for u in reversed(units):
+        usize = sum(sizes[i] for i in u)
+        if usize <= limit:
+            if cur and size + usize > limit:
+                flush()
+            cur.extend(reversed(u))
+            size += usize
+            continue
+        flush()
+        for i in reversed(u):
+            if sizes[i] > limit:
+                flush()
+                buckets.append([i])
+                continue
+            if cur and size + sizes[i] > limit:
+                flush()
+            cur.append(i)
+            size += sizes[i]
+        flush()
+    flush()
+    return buckets
 
 
 class GradReducer:
@@ -51,20 +117,9 @@ class GradReducer:
         self.reduce_dtype = reduce_dtype
         segs = [s for s in store.segments if s.trainable and (seg_filter is None or seg_filter(s))]
         self.seg_index = {id(s): i for i, s in enumerate(segs)}
-        # -------- buckets from the end of the flat buffer
-        limit = int(bucket_mb * 1024 * 1024 / 4)
-        buckets: list[list[int]] = []
-        cur: list[int] = []
-        size = 0
-        for i in range(len(segs) - 1, -1, -1):
-            s = segs[i]
-            if cur and size + s.numel > limit:
-                buckets.append(cur)
-                cur, size = [], 0
-            cur.append(i)
-            size += s.numel
-        if cur:
-            buckets.append(cur)
+        # -------- buckets from the end of the flat buffer, cut on unit (layer) boundaries
+        limit = max(int(bucket_mb * 1024 * 1024 / 4), 1)
+        buckets = plan_buckets([s.numel for s in segs], [unit_key(s.path) for s in segs], limit)
         self.segs = segs
         self.buckets = []
         self.seg_bucket = [0] * len(segs)
@@ -74,11 +129,13 @@ class GradReducer:
             self.buckets.append((lo, hi, idxs))
             for i in idxs:
                 self.seg_bucket[i] = bi
+        self._stage = None  # bf16 staging buffer over [stage_lo, stage_hi) of the flat buffer
+        self._stage_lo = min((lo for lo, _, _ in self.buckets), default=0)
+        self._stage_hi = max((hi for _, hi, _ in self.buckets), default=0)
         self.pending_uses = [0] * len(segs)
         self.bucket_left = [len(b[2]) for b in self.buckets]
         self.launched = [False] * len(self.buckets)
-        self.works = []
-        self._compressed = {}
+        self.works: list[tuple] = []  # (bucket, work, tensor to divide or None, lo, hi, staged, partial)
         self.partial_done = [0] * len(self.buckets)  # elements of a bucket already launched
         if self.enabled:
             store.hooks.append(self._on_ready)
@@ -105,10 +162,10 @@ class GradReducer:
             return
         b = self.seg_bucket[i]
         blo, bhi, idxs = self.buckets[b]
-        if len(idxs) != 1 or self.launched[b] or self.reduce_dtype != torch.float32:
+        if len(idxs) != 1 or self.launched[b]:
             return
         off = self.segs[i].offset
-        self.works.append((b, self._allreduce(self.store.grad[off + lo:off + hi])))
+        self._reduce_range(b, off + lo, off + hi, partial=True)
         self.partial_done[b] += hi - lo
 
     def _on_use(self, h: Handle) -> None:
@@ -145,14 +202,29 @@ class GradReducer:
             if self.partial_done[b] != hi - lo:
                 raise RuntimeError(f"bucket {b}: partial reductions cover {self.partial_done[b]} of {hi - lo}")
             return
+        self._reduce_range(b, lo, hi)
+
+    def staging(self) -> torch.Tensor | None:
+        """The bf16 staging buffer (allocated once, on the gradient buffer's device)."""
+        if self.reduce_dtype == torch.float32:
+            return None
+        if self._stage is None:
+            self._stage = torch.empty(self._stage_hi - self._stage_lo, dtype=self.reduce_dtype,
+                                      device=self.store.grad.device)
+        return self._stage
+
+    def _reduce_range(self, b: int, lo: int, hi: int, partial: bool = False) -> None:
+        """Launch the all-reduce of flat-buffer elements [lo, hi) (bucket ``b``)."""
         view = self.store.grad[lo:hi]
-        if self.reduce_dtype != torch.float32:
-            buf = view.to(self.reduce_dtype)
-            self._compressed[b] = buf
-            w = self._allreduce(buf)
+        st = self.staging()
+        if st is not None:
+            sv = st[lo - self._stage_lo:hi - self._stage_lo]
+            sv.copy_(view)
+            w, to_div = self._allreduce(sv)
+            self.works.append((b, w, to_div, lo, hi, sv, partial))
         else:
-            w = self._allreduce(view)
-        self.works.append((b, w))
+            w, to_div = self._allreduce(view)
+            self.works.append((b, w, to_div, lo, hi, None, partial))
 
     def _allreduce(self, t: torch.Tensor):
         """Async all-reduce-average of ``t`` -> (work, tensor to divide by world or None).  One code
@@ -209,21 +281,20 @@ class GradReducer:
         ranges = self.optimizer_ranges()
         gid = {b: i for i, grp in enumerate(groups) for b in grp}
         left = [0] * len(groups)  # outstanding reductions per optimizer group
-        for b, _ in self.works:
-            left[gid[b]] += 1
-        for b, (w, to_div) in self.works:
+        for wk in self.works:
+            left[gid[wk[0]]] += 1
+        for b, w, to_div, lo, hi, staged, _ in self.works:
             w.wait()
             if to_div is not None:
                 to_div.div_(self.world)
-            if b in self._compressed:
-                lo, hi, _ = self.buckets[b]
-                self.store.grad[lo:hi].copy_(self._compressed.pop(b))
+            if staged is not None:
+                self.store.grad[lo:hi].copy_(staged)
             left[gid[b]] -= 1
             if on_bucket_done is not None and left[gid[b]] == 0:
                 on_bucket_done(*ranges[gid[b]])
         if on_bucket_done is not None:  # a group without any reduction of its own (none today)
             for i, grp in enumerate(groups):
-                if not any(gid[b] == i for b, _ in self.works):
+                if not any(gid[wk[0]] == i for wk in self.works):
                     on_bucket_done(*ranges[i])
         self.works = []
 

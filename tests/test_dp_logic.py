@@ -110,3 +110,28 @@ def test_linear_probe_reducer_covers_head_only():
     J = 3 * 32
     assert total == 2 * J + J * 10 + 10  # BatchNorm scale/bias + Dense kernel/bias
     assert all(s.path[:2] == ("model", "head") for s in red.segs)
+
+
+def test_bucket_plan_layer_aligned():
+    """Buckets never split a layer unless the layer alone exceeds the size; an oversized segment
+    is a bucket of its own (keeps partial launches); launch order is from the end of the buffer."""
+    from jumbo_mae_tpu_amd.parallel.ddp import GradReducer, plan_buckets, unit_key
+
+    assert unit_key(("model", "layer_3", "attn", "wq", "kernel")) == ("model", "layer_3")
+    assert unit_key(("decoder_model", "dec_layer_0", "ff", "w1", "bias")) == ("decoder_model", "dec_layer_0")
+    assert unit_key(("model", "jumbo_mlp", "w1", "kernel")) == ("model", "jumbo_mlp")
+    assert unit_key(("decoder_proj", "kernel")) == ("decoder_proj", "kernel")
+    keys = [("a",), ("l0",), ("l0",), ("l1",), ("l1",), ("j",), ("j",), ("j",)]
+    sizes = [5, 4, 4, 4, 4, 30, 1, 2]
+    b = plan_buckets(sizes, keys, 10)
+    assert b == [[7, 6], [5], [4, 3], [2, 1], [0]]
+    # ViT-L-like: one encoder layer per 64 MiB bucket, the jumbo kernels alone
+    m = _pretrain_model()
+    red = GradReducer(m.store, bucket_mb=0.05)
+    for lo, hi, idxs in red.buckets:
+        units = {unit_key(red.segs[i].path) for i in idxs}
+        if len(units) > 1:  # several whole units
+            for u in units:
+                members = [i for i, s in enumerate(red.segs) if unit_key(s.path) == u]
+                assert set(members) <= set(idxs), u
+

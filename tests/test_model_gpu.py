@@ -88,3 +88,71 @@ def test_finetune_long_sequence_gpu_matches_cpu(heads):
         b = gg[s.offset:s.offset + s.numel]
         if a.norm() > 1e-3 * gc.norm() / len(cpu.store.segments) ** 0.5:
             assert _cos(a, b) > 0.95, s.key
+
+
+def _compare_leaves(cpu, gpu, lc, lg, strict=0.99, loose=0.95):
+    """Loss within 2 %; flat-gradient cosine > 0.99; every 2-D (GEMM weight) leaf > ``strict``, the
+    other leaves > ``loose`` (tiny gradients -- below 1e-3 of the per-leaf RMS norm -- are skipped)."""
+    assert abs(lc.item() - lg.item()) / abs(lc.item()) < 2e-2, (lc.item(), lg.item())
+    gc, gg = cpu.store.grad, gpu.store.grad.cpu()
+    assert _cos(gc, gg) > 0.99
+    bad = []
+    for s in cpu.store.segments:
+        a = gc[s.offset:s.offset + s.numel]
+        b = gg[s.offset:s.offset + s.numel]
+        if a.norm() <= 1e-3 * gc.norm() / len(cpu.store.segments) ** 0.5:
+            continue
+        c = _cos(a, b)
+        if c < (strict if len(s.shape) == 2 else loose):
+            bad.append((s.key, len(s.shape), round(c, 4)))
+    assert not bad, bad
+
+
+def test_pretrain_production_routing_matches_cpu():
+    """ViT-B-width Jumbo MAE (dim 768, 224 px, batch 96) so that every Dense takes the production
+    route: encoder rows 96 x 52 = 4992, patch-FF rows 4704 and decoder rows 96 x 199 >= 4096 run the
+    hand-written MFMA GEMMs (FF1 saving gelu', FF2 data gradient x gelu' (DMUL), data gradients on
+    the transposed weight shadows, TN weight gradients split over M, the deferred segmented jumbo
+    weight gradient over both layers' CLS rows).  bf16 HIP step vs the fp32 CPU step
+    (/root/reference/src/pretraining.py:87-122)."""
+    from jumbo_mae_tpu_amd.config import DecoderConfig, ViTConfig
+    from jumbo_mae_tpu_amd.models.mae import PretrainModel
+    vc = ViTConfig(layers=2, dim=768, heads=12, labels=0, image_size=224, patch_size=16, posemb="sincos2d",
+                   layerscale=True)
+    dc = DecoderConfig(dec_layers=2, dec_dim=512, dec_heads=16, image_size=224, patch_size=16, dec_layerscale=True)
+    cpu = PretrainModel(vc, dc).to("cpu", torch.float32, seed=0)
+    gpu = PretrainModel(vc, dc).to("cuda", torch.bfloat16, seed=0)
+    gpu.store.master.copy_(cpu.store.master)
+    gpu.store.sync_shadow()
+    g = torch.Generator().manual_seed(0)
+    imgs = torch.randint(0, 256, (96, 3, 224, 224), dtype=torch.uint8, generator=g)
+    noise = torch.rand(196, generator=g)
+    lc = cpu(imgs, noise=noise)["loss"]
+    lc.backward()
+    lg = gpu(imgs.cuda(), noise=noise.cuda())["loss"]
+    lg.backward()
+    torch.cuda.synchronize()
+    _compare_leaves(cpu, gpu, lc, lg)
+
+
+def test_finetune_production_routing_matches_cpu():
+    """Classifier at batch 32 x 199 tokens = 6368 encoder rows (>= 4096: MFMA GEMMs for every
+    Dense but the 32-row jumbo MLP and the head), dim 768; bf16 HIP vs fp32 CPU
+    (/root/reference/src/finetuning.py:84-106)."""
+    from jumbo_mae_tpu_amd.config import ViTConfig
+    from jumbo_mae_tpu_amd.models.classifier import FinetuneModel
+    vc = ViTConfig(layers=2, dim=768, heads=12, labels=1000, image_size=224, patch_size=16, posemb="learnable",
+                   layerscale=True)
+    cpu = FinetuneModel(vc).to("cpu", torch.float32, seed=0)
+    gpu = FinetuneModel(vc).to("cuda", torch.bfloat16, seed=0)
+    gpu.store.master.copy_(cpu.store.master)
+    gpu.store.sync_shadow()
+    g = torch.Generator().manual_seed(0)
+    imgs = torch.randint(0, 256, (32, 3, 224, 224), dtype=torch.uint8, generator=g)
+    labels = torch.randint(0, 1000, (32,), generator=g)
+    lc = cpu(imgs, labels)["loss"]
+    lc.backward()
+    lg = gpu(imgs.cuda(), labels.cuda())["loss"]
+    lg.backward()
+    torch.cuda.synchronize()
+    _compare_leaves(cpu, gpu, lc, lg)

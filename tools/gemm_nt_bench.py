@@ -37,6 +37,25 @@ def timeit(fn, iters):
     return e0.elapsed_time(e1) * 1e3 / iters
 
 
+def reference(kind, x, w, b, pre):
+    """fp32 reference of what ``ours`` computes for each kind (data-gradient kinds carry no bias;
+    the dGELU kinds multiply the bf16-rounded GEMM output, as the epilogue does)."""
+    base = x.float() @ w.float().t()
+    if kind == "dgrad":
+        return base
+    if kind == "dgrad_gelu":
+        h = pre.float()
+        t = torch.tanh(0.7978845608028654 * (h + 0.044715 * h ** 3))
+        d = 0.5 * (1 + t) + 0.5 * h * (1 - t * t) * 0.7978845608028654 * (1 + 3 * 0.044715 * h * h)
+        return base.bfloat16().float() * d
+    if kind in ("dgrad_dmul", "dgrad_dmul_nob"):
+        return base.bfloat16().float() * pre.float()
+    r = base + b
+    if kind in ("fwd_gelu_only", "fwd_gelu_d"):
+        return torch.nn.functional.gelu(r.bfloat16().float(), approximate="tanh")
+    return r
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=10)
@@ -75,6 +94,7 @@ def main():
             b = torch.randn(N, device="cuda") * 0.1
             bb = b.bfloat16()
             gelu = kind == "fwd_gelu"
+            pre = None
             if kind == "splitk":
                 from jumbo_mae_tpu_amd.ops.prims import splitk_plan
                 S = max(2, splitk_plan(M, N, K))
@@ -108,24 +128,17 @@ def main():
             else:
                 ours = lambda: ext.gemm_nt(x, w, b, False)  # noqa: E731
                 blas = lambda: torch.addmm(bb, x, w.t())  # noqa: E731
+            ref = reference(kind, x, w, b, pre)
             errs = []
             for v in variants:
                 setv(v)
                 o = ours()
-                r0 = torch.addmm(b, x.float(), w.float().t()) if not kind.startswith("dgrad_") else o[0].float()
-                if kind == "fwd_gelu_only":
-                    r0 = torch.nn.functional.gelu(r0.bfloat16().float(), approximate="tanh")
-                elif kind == "fwd_gelu_d":
-                    r0 = torch.nn.functional.gelu(r0.bfloat16().float(), approximate="tanh")
+                if kind == "fwd_gelu_d":
                     o = o[1:]
-                errs.append(((o[0].float() - r0).abs().max() / r0.abs().max()).item())
+                errs.append(((o[0].float() - ref).abs().max() / ref.abs().max()).item())
             setv(variants[0])
             out = ours()
-            ref = torch.addmm(b, x.float(), w.float().t()) if not kind.startswith("dgrad_") else out[0].float()
-            if kind == "fwd_gelu_only":
-                ref = torch.nn.functional.gelu(ref.bfloat16().float(), approximate="tanh")
-            elif kind == "fwd_gelu_d":
-                ref = torch.nn.functional.gelu(ref.bfloat16().float(), approximate="tanh")
+            if kind == "fwd_gelu_d":
                 out = out[1:]
             err = ((out[0].float() - ref).abs().max() / ref.abs().max()).item()
             if gelu:
