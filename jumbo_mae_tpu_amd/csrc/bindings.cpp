@@ -82,6 +82,9 @@ int jm_gemm_nt(const uint16_t* A, long lda, const uint16_t* B, long ldb, int M, 
                const GemmEpi& ep, hipStream_t st);
 void jm_gemm_set_variant(int wn, int group);
 void jm_gemm_set_tail(int on);
+void jm_gemm_set_narrow(int max_m);
+int jm_gemm_nt_tiles(int M, int N);
+int jm_gemm_nt_colpart_rows(int M, int N);
 int jm_gemm_nt_tail_plan(int M, int N, int K, int epi, int* tail_r, long* ws_floats);
 int jm_gemm_tn_plan(int M, int N, int K, int* S_out);
 int jm_gemm_tn(const uint16_t* A, long lda, const uint16_t* B, long ldb, int M, int N, int K, int sps, int S,
@@ -653,6 +656,20 @@ torch::Tensor gemm_nt_splitk(torch::Tensor A, torch::Tensor B, c10::optional<tor
   return out;
 }
 
+// C[M, N] = A[M, K] . B[N, K]^T in fp32 (EPI_PARTIAL with one split: the accumulators stored as
+// they are) -- short-reduction weight gradients in NT form (ops/prims.py wgrad)
+torch::Tensor gemm_nt_f32(torch::Tensor A, torch::Tensor B) {
+  CHECK_DT(A, torch::kBFloat16);
+  CHECK_DT(B, torch::kBFloat16);
+  TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && A.size(1) == B.size(1), "gemm_nt_f32: A [M,K], B [N,K]");
+  TORCH_CHECK(A.stride(1) == 1 && B.stride(1) == 1, "gemm_nt_f32: K must be contiguous");
+  const int M = A.size(0), N = B.size(0), K = A.size(1);
+  auto out = torch::empty({M, N}, A.options().dtype(torch::kFloat32));
+  GemmEpi ep{nullptr, nullptr, N, nullptr, nullptr, nullptr, out.data_ptr<float>(), 1};
+  check_rc(jm_gemm_nt(bf(A), A.stride(0), bf(B), B.stride(0), M, N, K, 3, ep, stream()), "gemm_nt_f32");
+  return out;
+}
+
 // dh[M, N] = (A[M, K] . B[N, K]^T) * gelu'(pre[M, N]) -- FF2 data gradient through the GELU,
 // B = W2^T; dbias (fp32 [N], optional) += column sums of dh (the FF1 bias gradient).
 // deriv: ``pre`` holds the saved gelu'(h) (EPI_GELU_D forward): the epilogue multiplies (EPI_DMUL)
@@ -671,7 +688,7 @@ torch::Tensor gemm_nt_dgelu(torch::Tensor A, torch::Tensor B, torch::Tensor pre,
   torch::Tensor ws;
   const int epi = deriv ? 7 : 2;
   const int r = attach_tail(ep, ws, M, N, K, epi, A);
-  int nM = (M + 255) / 256;
+  int nM = jm_gemm_nt_colpart_rows(M, N);
   if (dbias) {
     TORCH_CHECK(dbias->is_contiguous() && dbias->scalar_type() == torch::kFloat32 && dbias->numel() == N,
                 "gemm_nt_dgelu dbias");
@@ -915,12 +932,15 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_set_variant", &jm_gemm_set_variant, py::arg("nt64"), py::arg("group") = 8,
         "nt64 = 1: every NT launch on the 64-deep main loop (tests); group: row tiles per column sweep");
   m.def("gemm_set_tail", &jm_gemm_set_tail);
+  m.def("gemm_set_narrow", &jm_gemm_set_narrow, "M below which NT GEMMs take the 128 x 192 narrow tiles (0 = never)");
+  m.def("gemm_nt_tiles", &jm_gemm_nt_tiles, "output tiles (workgroups before split-K) of an NT launch");
   m.def("transpose_bf16_batch", &transpose_bf16_batch);
   m.def("ln_set_bwd_blocks", &jm_ln_set_bwd_blocks);
   m.def("gemm_nt_splitk", &gemm_nt_splitk, py::arg("A"), py::arg("B"), py::arg("bias") = py::none(),
         py::arg("splits") = 8, py::arg("add") = py::none());
   m.def("gemm_nt_dgelu", &gemm_nt_dgelu, py::arg("A"), py::arg("B"), py::arg("pre"), py::arg("dbias") = py::none(),
         py::arg("deriv") = false);
+  m.def("gemm_nt_f32", &gemm_nt_f32, py::arg("A"), py::arg("B"));
   m.def("gemm_nt", &gemm_nt, py::arg("A"), py::arg("B"), py::arg("bias") = py::none(), py::arg("gelu") = false,
         py::arg("gelu_only") = false, py::arg("gelu_deriv") = false);
   m.def("attn_set_tr", &jm_attn_set_tr);

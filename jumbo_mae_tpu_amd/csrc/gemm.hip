@@ -727,6 +727,240 @@ __global__ __launch_bounds__(512, 1) void gemm_p4_kernel(const uint16_t* __restr
   p4_epilogue<EPI>(acc, ep, M, N, m0, n0, split, smem);
 }
 
+// ------------------------------------------------------------------ narrow tiles (M < 4096)
+// Skinny-M GEMMs -- the shared jumbo MLP (512 rows per GPU in pretraining, 128 in finetuning),
+// the classifier head, small batches -- get too few 256 x 256 tiles to fill 256 CUs.  Here one
+// 512-thread workgroup owns a 128 x 192 tile: 8 waves, 2 along M x 4 along N, each 64 x 48 =
+// 4 x 3 v_mfma_f32_16x16x32_bf16 tiles (48 accumulator VGPRs).  M = 512, N = 12288 (the jumbo
+// W1 forward / W2 data gradient, K = 3072) is then exactly 4 x 64 = 256 tiles: one full wave.
+// K moves in 64-deep K-tiles (A 128 x 128 B + B 192 x 128 B = 40 KB) through a 3-slot LDS ring
+// by buffer_load ... lds with the nt64 chunk swizzle; one barrier per K-tile, the next-but-one
+// K-tile issued right after it (counted vmcnt keeps one K-tile in flight across the barrier).
+// Epilogues: the tile is staged as bf16 through a padded LDS image ([128][200]: conflict-free
+// 8-byte writes) and streamed out 16 B per lane by 384 threads (24 per row, 16 rows per pass),
+// each on fixed columns, so the DGELU / DMUL column sums stay in registers until one LDS reduce.
+// EPI_PARTIAL: split-K fp32 slices straight from the accumulators.
+constexpr int NBM = 128, NBN = 192, NKT = 64;
+constexpr int N_AEL = NBM * NKT, N_BEL = NBN * NKT, N_STAGE = N_AEL + N_BEL;  // elements (40 KB / K-tile)
+constexpr int N_RING = 3;
+constexpr int N_LD = NBN + 8;  // epilogue image row stride (elements)
+static_assert(N_RING * N_STAGE * 2 <= (int)GEMM_SMEM, "narrow ring exceeds the LDS budget");
+
+// bijective XCD remap, split-major, then GROUP_M row tiles sweep the column tiles
+JM_DEVICE void narrow_tile(int M, int N, int GROUP_M, int splits, int& m0, int& n0, int& split) {
+  const int nM = (M + NBM - 1) / NBM, nN = (N + NBN - 1) / NBN;
+  const int tiles = nM * nN, nwg = tiles * splits;
+  const int orig = blockIdx.x;
+  const int xcd = orig & 7, q = nwg >> 3, r = nwg & 7;
+  int wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+  split = wg / tiles;
+  wg -= split * tiles;
+  const int per_group = GROUP_M * nN;
+  const int first_m = (wg / per_group) * GROUP_M;
+  const int gsz = min(nM - first_m, GROUP_M);
+  m0 = (first_m + (wg % per_group) % gsz) * NBM;
+  n0 = ((wg % per_group) / gsz) * NBN;
+}
+
+template <int EPI>
+JM_DEVICE void narrow_epilogue(const f32x4_t (&acc)[4][3], const GemmEpi& ep, uint16_t* cs, int M, int N, int m0,
+                               int n0, int split, int wr, int wc, int l16, int g) {
+  if constexpr (EPI == EPI_PARTIAL) {
+    float* dst = ep.part + (long)split * M * N;
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) {
+      const int m = m0 + wr * 64 + mt * 16 + l16;
+      if (m >= M) continue;
+#pragma unroll
+      for (int nt = 0; nt < 3; ++nt) {
+        const int n = n0 + wc * 48 + nt * 16 + 4 * g;
+        if (n >= N) continue;
+        float v[4] = {acc[mt][nt][0], acc[mt][nt][1], acc[mt][nt][2], acc[mt][nt][3]};
+        store4(dst + (long)m * N + n, v);
+      }
+    }
+    return;
+  }
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");  // ring drained and free
+#pragma unroll
+  for (int nt = 0; nt < 3; ++nt) {
+    const int nl = wc * 48 + nt * 16 + 4 * g;
+    float bv[4] = {0.f, 0.f, 0.f, 0.f};
+    if (ep.bias && n0 + nl < N) load4(ep.bias + n0 + nl, bv);
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) {
+      const int r = wr * 64 + mt * 16 + l16;
+      uint2 pk;
+      pk.x = pack_bf2(acc[mt][nt][0] + bv[0], acc[mt][nt][1] + bv[1]);
+      pk.y = pack_bf2(acc[mt][nt][2] + bv[2], acc[mt][nt][3] + bv[3]);
+      *reinterpret_cast<uint2*>(cs + r * N_LD + nl) = pk;
+    }
+  }
+  __syncthreads();
+  const int tid = threadIdx.x;
+  constexpr bool PRE = EPI == EPI_DGELU || EPI == EPI_DMUL;
+  const bool active = tid < 384;
+  const int c = tid % 24, rr = tid / 24;  // column chunk, first row (active threads: rr < 16)
+  const int n = n0 + c * 8;
+  const bool col_ok = active && n < N;
+  uint4 auxv[8];
+  if constexpr (PRE) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int m = m0 + rr + 16 * i;
+      auxv[i] = make_uint4(0, 0, 0, 0);
+      if (col_ok && m < M) auxv[i] = *reinterpret_cast<const uint4*>(ep.aux + (long)m * ep.ldo + n);
+    }
+  }
+  float csum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (active) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int r = rr + 16 * i, m = m0 + r;
+      if (m >= M || !col_ok) continue;
+      const uint4 v = *reinterpret_cast<const uint4*>(cs + r * N_LD + c * 8);
+      uint16_t* o = ep.out + (long)m * ep.ldo + n;
+      const uint16_t* h = reinterpret_cast<const uint16_t*>(&v);
+      if constexpr (PRE) {
+        const uint16_t* ah = reinterpret_cast<const uint16_t*>(&auxv[i]);
+        float f[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float hp = bf2f(ah[j]);
+          f[j] = bf2f(f2bf(bf2f(h[j]) * (EPI == EPI_DMUL ? hp : gelu_grad_f(hp))));
+          csum[j] += f[j];
+        }
+        st16(o, pack8(f), false);
+      } else if constexpr (EPI == EPI_GELU_D) {
+        float fg[8], fd[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) gelu_and_grad_f(bf2f(h[j]), fg[j], fd[j]);
+        st16(o, pack8(fd), false);
+        st16(ep.out2 + (long)m * ep.ldo + n, pack8(fg), false);
+      } else if constexpr (EPI == EPI_GELU_ONLY) {
+        float f[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) f[j] = gelu_tanh_f(bf2f(h[j]));
+        st16(o, pack8(f), false);
+      } else {
+        st16(o, v, false);
+        if constexpr (EPI == EPI_GELU) {
+          float f[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) f[j] = gelu_tanh_f(bf2f(h[j]));
+          st16(ep.out2 + (long)m * ep.ldo + n, pack8(f), false);
+        }
+      }
+    }
+  }
+  if constexpr (PRE) {
+    if (ep.colpart != nullptr) {  // column sums of this row tile: 16 row threads per column chunk
+      float* red = reinterpret_cast<float*>(cs);
+      __syncthreads();
+      if (active) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) red[rr * NBN + c * 8 + j] = csum[j];
+      }
+      __syncthreads();
+      if (tid < NBN && n0 + tid < N) {
+        float a = 0.f;
+#pragma unroll
+        for (int q = 0; q < 16; ++q) a += red[q * NBN + tid];
+        ep.colpart[(long)(m0 / NBM) * N + n0 + tid] = a;
+      }
+    }
+  }
+}
+
+template <int EPI>
+__global__ __launch_bounds__(512, 1) void gemm_narrow_kernel(const uint16_t* __restrict__ A, long lda,
+                                                             const uint16_t* __restrict__ B, long ldb, int M, int N,
+                                                             int K, GemmEpi ep, int GROUP_M) {
+  JM_DGUARD(blockDim.x == 512 && K % 64 == 0 && M > 0 && N > 0 && N % 8 == 0);
+  extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
+  const int tid = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+  const int l16 = lane & 15, g = lane >> 4;
+  const int wr = wave >> 2, wc = wave & 3;
+  if (wave >= 4) __builtin_amdgcn_s_setprio(1);  // static young-half priority (as p4)
+  int m0, n0, split;
+  narrow_tile(M, N, GROUP_M, EPI == EPI_PARTIAL ? ep.splits : 1, m0, n0, split);
+  int k_begin = 0;
+  if (EPI == EPI_PARTIAL) {  // this split's K range, in units of 64
+    const int ku = K / 64;
+    const int ku0 = split * ku / ep.splits, ku1 = (split + 1) * ku / ep.splits;
+    k_begin = ku0 * 64;
+    K = (ku1 - ku0) * 64;
+  }
+  const __amdgpu_buffer_rsrc_t ra = make_rsrc(A + (long)m0 * lda + k_begin, (long)(M - m0) * lda * 2 - 2L * k_begin);
+  const __amdgpu_buffer_rsrc_t rb = make_rsrc(B + (long)n0 * ldb + k_begin, (long)(N - n0) * ldb * 2 - 2L * k_begin);
+  // glds pieces of 8 rows x 128 B: A rows (wave + 8 p) * 8 + lane / 8 (p < 2), B rows (p < 3)
+  uint32_t a_src[2], b_src[3];
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+    const int row = (wave + 8 * p) * 8 + (lane >> 3);
+    a_src[p] = (uint32_t)((row * lda + ((lane & 7) ^ swz64(row)) * 8) * 2);
+  }
+#pragma unroll
+  for (int p = 0; p < 3; ++p) {
+    const int row = (wave + 8 * p) * 8 + (lane >> 3);
+    b_src[p] = (uint32_t)((row * ldb + ((lane & 7) ^ swz64(row)) * 8) * 2);
+  }
+  auto issue = [&](int t) {
+    const uint32_t k0b = t * NKT * 2;
+    uint16_t* la = smem + (t % N_RING) * N_STAGE;
+    uint16_t* lb = la + N_AEL;
+#pragma unroll
+    for (int p = 0; p < 2; ++p) blds16(ra, a_src[p], k0b, la + (wave + 8 * p) * 8 * NKT);
+#pragma unroll
+    for (int p = 0; p < 3; ++p) blds16(rb, b_src[p], k0b, lb + (wave + 8 * p) * 8 * NKT);
+  };
+  const int ch0 = ((0 * 4 + g) ^ swz64(l16)) * 8, ch1 = ((1 * 4 + g) ^ swz64(l16)) * 8;
+  const int a_row = (wr * 64 + l16) * NKT, b_row = N_AEL + (wc * 48 + l16) * NKT;
+  f32x4_t acc[4][3];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = K / NKT;  // >= 1
+  issue(0);
+  if (nk > 1) issue(1);
+  for (int t = 0; t < nk; ++t) {
+    if (t + 1 < nk) asm volatile("s_waitcnt vmcnt(5) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    if (t + 2 < nk) issue(t + 2);  // slot (t + 2) % 3 was read in step t - 1: every wave is past it
+    const uint16_t* base = smem + (t % N_RING) * N_STAGE;
+    bf16x8_t a[4][2], b[3][2];
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int ch = kk ? ch1 : ch0;
+#pragma unroll
+      for (int nt = 0; nt < 3; ++nt) b[nt][kk] = lds8(base + b_row + nt * 16 * NKT + ch);
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) a[mt][kk] = lds8(base + a_row + mt * 16 * NKT + ch);
+    }
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < 3; ++nt) acc[mt][nt] = mfma16(b[nt][kk], a[mt][kk], acc[mt][nt]);
+    // 7 reads of k 0-31, then the 12 MFMAs of k 0-31 interleaved with the 7 reads of k 32-63
+    __builtin_amdgcn_sched_group_barrier(0x100, 7, 0);
+#pragma unroll
+    for (int i = 0; i < 7; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+    }
+    __builtin_amdgcn_sched_group_barrier(0x008, 17, 0);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  if (wave >= 4) __builtin_amdgcn_s_setprio(0);
+  narrow_epilogue<EPI>(acc, ep, smem, M, N, m0, n0, split, wr, wc, l16, g);
+}
+
 // ------------------------------------------------------------------ tail split finish
 // Sums the tail_S compact fp32 partials of the tail tiles and applies the launch's epilogue
 // (same rounding points as epilogue_lds).  Block = 32 rows of one tail tile; thread = 4 rows x 8
@@ -839,10 +1073,32 @@ void launch_p4(const uint16_t* A, long lda, const uint16_t* B, long ldb, int M, 
   gemm_p4_kernel<EPI><<<nwg, 512, GEMM_SMEM, st>>>(A, lda, B, ldb, M, N, K, ep, g_gemm_group);
 }
 
-// K in 128-deep units (split-K: per split) -> p4, else the 64-deep kernel (nontemporal epilogue stores)
+template <int EPI>
+void launch_narrow(const uint16_t* A, long lda, const uint16_t* B, long ldb, int M, int N, int K, const GemmEpi& ep,
+                   hipStream_t st) {
+  static bool attr = false;
+  constexpr size_t sm = (size_t)N_RING * N_STAGE * 2;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)gemm_narrow_kernel<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)sm);
+    attr = true;
+  }
+  const int nwg = ((M + NBM - 1) / NBM) * ((N + NBN - 1) / NBN) * (EPI == EPI_PARTIAL ? ep.splits : 1);
+  gemm_narrow_kernel<EPI><<<nwg, 512, sm, st>>>(A, lda, B, ldb, M, N, K, ep, g_gemm_group);
+}
+
+int g_narrow_max_m = 4096;  // M below this: 128 x 192 tiles (A/B switch: 0 = never)
+
+bool narrow(int M, int N) { return M < g_narrow_max_m && N % 8 == 0; }
+
+// narrow tiles for M < 4096; K in 128-deep units (split-K: per split) -> p4, else the 64-deep
+// kernel (nontemporal epilogue stores)
 template <int EPI>
 void launch_epi(const uint16_t* A, long lda, const uint16_t* B, long ldb, int M, int N, int K, const GemmEpi& ep,
                 int nwg, hipStream_t st) {
+  if constexpr (EPI != EPI_TAIL) {
+    if (narrow(M, N) && ep.t_count == 0) return launch_narrow<EPI>(A, lda, B, ldb, M, N, K, ep, st);
+  }
   if (!g_gemm_nt64 && K % 128 == 0 && (EPI != EPI_PARTIAL || K / 128 >= ep.splits))
     return launch_p4<EPI>(A, lda, B, ldb, M, N, K, ep, nwg, st);
   return launch_nt64<EPI, true>(A, lda, B, ldb, M, N, K, ep, nwg, st);
@@ -874,6 +1130,17 @@ void jm_gemm_set_variant(int nt64, int group) {
 
 void jm_gemm_set_tail(int on) { g_gemm_tail = on; }
 
+void jm_gemm_set_narrow(int max_m) { g_narrow_max_m = max_m; }
+
+// output tiles of an NT launch (the narrow kernel's 128 x 192 or the 256 x 256 kernels)
+int jm_gemm_nt_tiles(int M, int N) {
+  if (narrow(M, N)) return ((M + NBM - 1) / NBM) * ((N + NBN - 1) / NBN);
+  return ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
+}
+
+// rows of the EPI_DGELU / EPI_DMUL column-partial buffer (one per row tile, before tail rows)
+int jm_gemm_nt_colpart_rows(int M, int N) { return narrow(M, N) ? (M + NBM - 1) / NBM : (M + BM - 1) / BM; }
+
 // Tail split plan for an NT launch: the last wave of output tiles (tiles % CUs of them) fills only
 // part of the chip; when it is at most a quarter wave, those tiles run split-K S ways (compact fp32
 // partials, *ws_floats) and a finish kernel applies the epilogue.  Returns S (0 = no tail split);
@@ -883,6 +1150,7 @@ int jm_gemm_nt_tail_plan(int M, int N, int K, int epi, int* tail_r, long* ws_flo
   *ws_floats = 0;
   if (!g_gemm_tail) return 0;
   if (!(epi == EPI_STORE || epi == EPI_GELU || epi == EPI_DGELU || epi == EPI_GELU_ONLY) || N % 8 || K % 128) return 0;
+  if (narrow(M, N)) return 0;
   const int ncu = num_cus();
   const int tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
   if (tiles < ncu) return 0;

@@ -67,6 +67,12 @@ def wgrad(h: Handle, dy: torch.Tensor, x: torch.Tensor, rows: tuple[int, int] | 
                 and N % 256 == 0 and K % 256 == 0 and M >= 4096 and dy.stride(1) == 1 and x.stride(1) == 1):
             _ext.load().gemm_tn_wgrad(dy, x, g)
             return
+        if (_WGRAD_OURS and hip(dy) and dy.dtype == torch.bfloat16 and x.dtype == torch.bfloat16
+                and M < NARROW_MAX_M and K % 8 == 0):
+            # short reduction (the classifier head, small batches): G^T-free NT form on the narrow
+            # kernel, dW[N, K] = dy^T . x with the (zero-padded) token dim as the reduction
+            g.add_(_ext.load().gemm_nt_f32(_pad_cols(dy.t()), _pad_cols(x.t())))
+            return
         s = wgrad_split(M, N, K)
         if s > 1:
             part = torch.bmm(dy.view(s, M // s, N).transpose(1, 2), x.view(s, M // s, K), out_dtype=torch.float32)
@@ -91,32 +97,51 @@ _GEMM_MODE = os.environ.get("JMAE_GEMM", "auto")  # auto | blas | ours (forward 
 _DGRAD_OURS = os.environ.get("JMAE_DGRAD", "1") == "1"  # data-gradient GEMMs on the MFMA kernel
 
 
+NARROW_MAX_M = 4096  # csrc/gemm.hip g_narrow_max_m: below it the NT GEMMs take 128 x 192 tiles
+_NARROW_FUSED_MIN_TILES = 160  # a fused GELU epilogue needs the tiles alone to fill most CUs
+
+
+def nt_tiles(M: int, N: int) -> int:
+    """Output tiles of an NT launch (mirror of jm_gemm_nt_tiles)."""
+    if M < NARROW_MAX_M:
+        return -(-M // 128) * -(-N // 192)
+    return -(-M // 256) * -(-N // 256)
+
+
 def use_our_gemm(M: int, N: int, K: int, fused_gelu: bool = False, kind: str = "fwd") -> bool:
-    """Every forward / data-gradient Dense with at least 4096 rows runs on the hand-written MFMA
-    GEMM (csrc/gemm.hip, 4-phase counted-vmcnt kernel): measured on MI355X it matches or beats
-    hipBLASLt on the ViT-L step as a whole (in-process A/B 92.52 vs 92.50 ms,
-    profiles/r2_gemm_routing.txt; per shape profiles/r2_gemm_p4.txt).  Skinny-M GEMMs (the
-    512-row shared jumbo MLP) take the split-K MFMA path (``splitk_plan``) or hipBLASLt."""
-    if _GEMM_MODE == "blas":
+    """Every forward / data-gradient Dense runs on a hand-written MFMA GEMM (csrc/gemm.hip): M >=
+    4096 on the 256 x 256 4-phase kernel (it matches or beats hipBLASLt on the ViT-L step as a
+    whole, profiles/r2_gemm_routing.txt), smaller M on the 128 x 192 narrow kernel (the 512-row
+    jumbo MLP: one full wave of 256 tiles at N = 12288).  A fused GELU / dGELU epilogue is taken
+    only when the narrow tiles alone fill most of the chip; otherwise the GEMM goes split-K
+    (``splitk_plan``) and the GELU runs as its own kernel."""
+    if _GEMM_MODE == "blas" or K % 64 or N % 8:
         return False
-    return K % 64 == 0 and N % 8 == 0 and M >= 4096
-
-
-_SPLITK_MIN_K = int(os.environ.get("JMAE_SPLITK_MIN_K", "4096"))
+    if M >= NARROW_MAX_M:
+        return True
+    return not fused_gelu or nt_tiles(M, N) >= _NARROW_FUSED_MIN_TILES
 
 
 def splitk_plan(M: int, N: int, K: int) -> int:
-    """Split-K factor for a small-M GEMM on the MFMA kernel (0 = not this path): the jumbo MLP's
-    512-row GEMMs have 24 (K = 12288) or 96 (K = 3072: W1 forward, W2 data gradient) output tiles
-    for 256 CUs.  Every split keeps >= 512 of K.  K >= 4096 by default: routing the K = 3072 pair
-    here too (JMAE_SPLITK_MIN_K=2048, S = 2) measured 93.95 vs 93.57 ms/step with hipBLASLt's
-    192x128 tiles (profiles/r2_jumbo_splitk.txt), so those two stay on the library."""
-    if _GEMM_MODE == "blas" or M > 2048 or K < _SPLITK_MIN_K or K % 128 or N % 8:
+    """Split-K factor for a small-M GEMM on the narrow MFMA kernel (0 = not this path): the jumbo
+    MLP's K = 12288 GEMMs (W2 forward, W1 data gradient) have 64 narrow tiles at M = 512 -> 4
+    splits; the finetune jumbo MLP (M = 128) and the classifier head likewise.  Every split keeps
+    >= 512 of K; fp32 partial slices are summed by one reduce (+ bias, or + an fp32 addend)."""
+    if _GEMM_MODE == "blas" or M >= NARROW_MAX_M or K % 64 or N % 8:
         return 0
-    tiles = -(-M // 256) * -(-N // 256)
-    if tiles > 128:
+    tiles = nt_tiles(M, N)
+    if tiles >= _NARROW_FUSED_MIN_TILES:
         return 0
-    return max(2, min(256 // tiles, K // 512, 32))
+    s = min(256 // tiles, K // 512, 16)
+    return s if s >= 2 else 0
+
+
+def _pad_cols(t: torch.Tensor, mult: int = 64) -> torch.Tensor:
+    """[R, C] -> [R, ceil(C / mult) * mult] with zero columns (a reduction dim the MFMA kernels
+    need in 64-deep steps, e.g. the 1000-class head's data gradient)."""
+    c = t.shape[1]
+    pad = -c % mult
+    return F.pad(t, (0, pad)) if pad else t.contiguous()
 
 
 def linear_fwd(x2: torch.Tensor, hw: Handle, hb: Handle | None) -> torch.Tensor:
@@ -295,6 +320,10 @@ def linear_dgrad(dy: torch.Tensor, hw: Handle, add: torch.Tensor | None = None) 
     if (_DGRAD_OURS and hip(dy) and dy.dtype == torch.bfloat16
             and use_our_gemm(dy.shape[0], w.shape[1], w.shape[0], kind="dgrad")):
         return _ext.load().gemm_nt(dy.contiguous(), hw.weight_t(), None, False)[0]
+    if (_DGRAD_OURS and hip(dy) and dy.dtype == torch.bfloat16 and w.shape[0] % 64
+            and use_our_gemm(dy.shape[0], w.shape[1], -(-w.shape[0] // 64) * 64, kind="dgrad")):
+        # reduction dim (the Dense's output width, e.g. 1000 classes) zero-padded to 64-deep steps
+        return _ext.load().gemm_nt(_pad_cols(dy), _pad_cols(hw.weight_t()), None, False)[0]
     return dy @ w
 
 

@@ -21,6 +21,7 @@ def _reset_gemm_variant(request):
         request.getfixturevalue("ext").gemm_set_variant(0, 8)
         request.getfixturevalue("ext").attn_set_bwd_ppw(0)
         request.getfixturevalue("ext").gemm_set_tail(1)
+        request.getfixturevalue("ext").gemm_set_narrow(4096)
         request.getfixturevalue("ext").ln_set_direct(0)
 
 
@@ -196,13 +197,15 @@ def test_optimizer_hip_matches_torch(kind, clip):
     assert rel(res[0], res[1]) < 1e-5
 
 
-@pytest.mark.parametrize("nt64", [0, 1])
+@pytest.mark.parametrize("nt64,narrow", [(0, 4096), (1, 0), (0, 0)])
 @pytest.mark.parametrize("M,N,K,gelu", [(512, 256, 64, False), (300, 196, 128, True), (1000, 1536, 512, False),
                                         (257, 260, 192, True), (16100, 2048, 128, True), (40000, 520, 64, False)])
-def test_gemm_nt(ext, M, N, K, gelu, nt64):
-    """Hand-written MFMA GEMM (csrc/gemm.hip) vs an fp32 reference, ragged M / N included; nt64 = 1
-    forces the 64-deep main loop (it otherwise runs only at K % 128 == 64)."""
+def test_gemm_nt(ext, M, N, K, gelu, nt64, narrow):
+    """Hand-written MFMA GEMMs (csrc/gemm.hip) vs an fp32 reference, ragged M / N included: the
+    128 x 192 narrow kernel below M = 4096 (narrow = 4096), the 256 x 256 kernels otherwise (narrow
+    = 0: every M); nt64 = 1 forces the 64-deep main loop (it otherwise runs only at K % 128 == 64)."""
     ext.gemm_set_variant(nt64)
+    ext.gemm_set_narrow(narrow)
     torch.manual_seed(0)
     x = (torch.rand(M, K, device="cuda") * 2 - 1).bfloat16()
     w = ((torch.rand(N, K, device="cuda") * 2 - 1) * 0.1).bfloat16()
@@ -243,11 +246,12 @@ def test_attention_long_sequence_path(ext, B, S, H, hd):
     assert torch.equal(dqkv, dqkv2)  # one writer per element: deterministic
 
 
-@pytest.mark.parametrize("variant", [0, 1])
-@pytest.mark.parametrize("M,N,K", [(512, 256, 64), (1000, 1536, 512), (300, 512, 128)])
-def test_gemm_nt_dgelu(ext, M, N, K, variant):
+@pytest.mark.parametrize("variant,narrow", [(0, 4096), (0, 0), (1, 0)])
+@pytest.mark.parametrize("M,N,K", [(512, 256, 64), (1000, 1536, 512), (300, 512, 128), (5000, 776, 256)])
+def test_gemm_nt_dgelu(ext, M, N, K, variant, narrow):
     """FF2 data gradient through the GELU with the FF1 bias gradient (csrc/gemm.hip EPI_DGELU)."""
     ext.gemm_set_variant(variant, 8)
+    ext.gemm_set_narrow(narrow)
     torch.manual_seed(0)
     dy = (torch.rand(M, K, device="cuda") * 2 - 1).bfloat16()
     w2t = ((torch.rand(N, K, device="cuda") * 2 - 1) * 0.1).bfloat16()
@@ -341,11 +345,13 @@ def test_residual_ln_fwd_partial_rows(ext, D):
     assert torch.allclose(mu, mur, atol=1e-6) and torch.allclose(rs, rsr, rtol=1e-5)
 
 
-@pytest.mark.parametrize("variant", [0, 1])
-@pytest.mark.parametrize("M,N,K,S", [(512, 3072, 12288, 10), (300, 512, 4096, 3), (512, 256, 1024, 16)])
-def test_gemm_nt_splitk(ext, M, N, K, S, variant):
+@pytest.mark.parametrize("variant,narrow", [(0, 4096), (0, 0), (1, 0)])
+@pytest.mark.parametrize("M,N,K,S", [(512, 3072, 12288, 10), (300, 512, 4096, 3), (512, 256, 1024, 16),
+                                     (128, 2304, 9216, 16), (128, 1000, 2304, 4)])
+def test_gemm_nt_splitk(ext, M, N, K, S, variant, narrow):
     """Split-K MFMA GEMM (fp32 partial tiles + bf16 reduce with bias), ragged M."""
     ext.gemm_set_variant(variant, 8)
+    ext.gemm_set_narrow(narrow)
     torch.manual_seed(0)
     x = (torch.rand(M, K, device="cuda") * 2 - 1).bfloat16()
     w = ((torch.rand(N, K, device="cuda") * 2 - 1) * 0.05).bfloat16()
@@ -527,4 +533,69 @@ def test_weight_t_batched_refresh():
         assert h._wt_version == m.store.version
         assert torch.equal(h._wt, h.weight().t())
 
+
+@pytest.mark.parametrize("M,N,K", [(512, 12288, 3072), (128, 9216, 2304), (257, 200, 192), (3000, 776, 64),
+                                   (4095, 392, 320)])
+def test_gemm_narrow_epilogues(ext, M, N, K):
+    """The 128 x 192 narrow kernel (M < 4096: the jumbo MLP, heads, small batches) with every fused
+    epilogue -- bias store, GELU pair, GELU-only, gelu' + gelu (EPI_GELU_D), dGELU and multiply by
+    the saved gelu' with the bias-gradient column sums (EPI_DGELU / EPI_DMUL) -- and the fp32 form,
+    against fp32 references; ragged M and N (not multiples of 128 / 192)."""
+    torch.manual_seed(5)
+    x = (torch.rand(M, K, device="cuda") * 2 - 1).bfloat16()
+    w = ((torch.rand(N, K, device="cuda") * 2 - 1) * 0.1).bfloat16()
+    b = torch.randn(N, device="cuda") * 0.1
+    base = x.float() @ w.float().t()
+    h_ref = base + b
+    o = ext.gemm_nt(x, w, b, False)[0]
+    assert rel(o, h_ref) < 1e-2
+    h, gl = ext.gemm_nt(x, w, b, True)
+    assert rel(h, h_ref) < 1e-2
+    gref = torch.nn.functional.gelu(h.float(), approximate="tanh")
+    assert rel(gl, gref) < 1e-2
+    go = ext.gemm_nt(x, w, b, True, True)[0]
+    assert rel(go, gref) < 1e-2
+    gd, g2 = ext.gemm_nt(x, w, b, True, False, True)
+    hr = h.float()
+    t = torch.tanh(0.7978845608028654 * (hr + 0.044715 * hr ** 3))
+    d = 0.5 * (1 + t) + 0.5 * hr * (1 - t * t) * 0.7978845608028654 * (1 + 3 * 0.044715 * hr * hr)
+    assert rel(gd, d) < 1e-2 and rel(g2, gref) < 1e-2
+    f = ext.gemm_nt_f32(x, w)
+    assert f.dtype == torch.float32 and rel(f, base) < 1e-5
+    pre = (torch.randn(M, N, device="cuda") * 2).bfloat16()
+    for deriv in (False, True):
+        db = torch.full((N,), 0.5, device="cuda")
+        out = ext.gemm_nt_dgelu(x, w, pre, db, deriv)
+        p = pre.float()
+        if deriv:
+            mul = p
+        else:
+            tt = torch.tanh(0.7978845608028654 * (p + 0.044715 * p ** 3))
+            mul = 0.5 * (1 + tt) + 0.5 * p * (1 - tt * tt) * 0.7978845608028654 * (1 + 3 * 0.044715 * p * p)
+        ref = base.bfloat16().float() * mul
+        assert rel(out, ref) < 1e-2, deriv
+        assert rel(db - 0.5, ref.sum(0)) < 1e-2, deriv
+
+
+def test_small_m_routing_uses_mfma(ext):
+    """Below 4096 rows every Dense forward / data gradient / weight gradient of the prims takes a
+    hand-written kernel (no hipBLASLt): fused narrow GEMMs where 160+ tiles fill the chip, split-K
+    narrow GEMMs otherwise, a padded reduction for the 1000-class head's data gradient."""
+    from jumbo_mae_tpu_amd.ops import prims as P
+    assert P.use_our_gemm(512, 12288, 3072, fused_gelu=True) and P.splitk_plan(512, 12288, 3072) == 0
+    assert P.splitk_plan(512, 3072, 12288) == 4
+    assert not P.use_our_gemm(128, 9216, 2304, fused_gelu=True) and P.splitk_plan(128, 9216, 2304) >= 2
+    from jumbo_mae_tpu_amd.models.params import ParamStore, trunc_normal_t, zeros_
+    st = ParamStore()
+    hw = st.handle(st.add(("k",), (1000, 768), trunc_normal_t(0.02)))
+    hb = st.handle(st.add(("b",), (1000,), zeros_))
+    st.finalize("cuda", torch.bfloat16)
+    x = torch.randn(96, 768, device="cuda").bfloat16()
+    dy = torch.randn(96, 1000, device="cuda").bfloat16()
+    y = P.linear_fwd(x, hw, hb)
+    w = st.master[:1000 * 768].view(1000, 768)
+    assert rel(y, x.float() @ w.bfloat16().float().t()) < 1e-2
+    dx = P.linear_bwd(dy, x, hw, hb)
+    assert rel(dx, dy.float() @ w.bfloat16().float()) < 1e-2
+    assert rel(hw.grad, dy.float().t() @ x.float()) < 1e-2
 

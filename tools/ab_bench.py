@@ -42,8 +42,10 @@ def apply(P, cfg: str):
         elif k == "JMAE_WT_BATCH":
             import jumbo_mae_tpu_amd.models.params as PM
             PM.BATCH_TRANSPOSES = v == "1"
-        elif k == "SPLITK_MIN_K":
-            P._SPLITK_MIN_K = int(v)
+        elif k == "NARROW_MAX_M":  # NT GEMMs below this M on the 128 x 192 narrow kernel (0 = never)
+            from jumbo_mae_tpu_amd.ops import _ext
+            _ext.load(True).gemm_set_narrow(int(v))
+            P.NARROW_MAX_M = int(v)
         elif k == "LN_BWD_BLOCKS":
             from jumbo_mae_tpu_amd.ops import _ext
             _ext.load(True).ln_set_bwd_blocks(int(v))
