@@ -22,6 +22,7 @@ def _reset_gemm_variant(request):
         request.getfixturevalue("ext").attn_set_bwd_ppw(0)
         request.getfixturevalue("ext").gemm_set_tail(1)
         request.getfixturevalue("ext").gemm_set_narrow(4096)
+        request.getfixturevalue("ext").gemm_tn_set_fused(1)
         request.getfixturevalue("ext").ln_set_direct(0)
 
 
@@ -275,12 +276,15 @@ def test_transpose_bf16(ext, R, C):
     assert torch.equal(y, x.t())
 
 
+@pytest.mark.parametrize("fused", [1, 0])
 @pytest.mark.parametrize("M,N,K", [(4096, 256, 512), (3000, 512, 256), (512, 768, 1024), (26624, 1024, 256),
-                                   (101888, 512, 512), (200, 256, 256), (480, 256, 256)])
-def test_gemm_tn_wgrad(ext, M, N, K):
-    """Weight-gradient TN MFMA GEMM (csrc/gemm_tn.hip): G += dy^T x, split over M (fp32 partial
-    slices + reduce), ragged M; plain and segmented (the 4-phase kernel at 64-row segments, the
-    32-row-step kernel otherwise)."""
+                                   (101888, 512, 512), (200, 256, 256), (480, 256, 256), (25088, 1024, 4096)])
+def test_gemm_tn_wgrad(ext, M, N, K, fused):
+    """Weight-gradient TN MFMA GEMM (csrc/gemm_tn.hip): G += dy^T x, split over M, ragged M; the
+    split reduction in the kernel (fused: the last-arriving split of each tile adds the other fp32
+    slices, tickets re-armed -- checked by running twice) or by a reduce launch; plain and segmented
+    (the 4-phase kernel at 64-row segments, the 32-row-step kernel otherwise)."""
+    ext.gemm_tn_set_fused(fused)
     torch.manual_seed(0)
     dy = (torch.rand(M, N, device="cuda") * 2 - 1).bfloat16()
     x = (torch.rand(M, K, device="cuda") * 2 - 1).bfloat16()
@@ -289,6 +293,10 @@ def test_gemm_tn_wgrad(ext, M, N, K):
     S = ext.gemm_tn_wgrad(dy, x, g)
     assert S >= 1 and (S > 1 or M < 8192)
     assert rel(g, ref) < 1e-4
+    g3 = torch.zeros_like(g)
+    ext.gemm_tn_wgrad(dy, x, g3)
+    ext.gemm_tn_wgrad(dy, x, g3)
+    assert rel(g3, 2 * (dy.double().t() @ x.double())) < 1e-4
     for n in (4, 5):
         if M % n or (M // n) % 32:
             continue
@@ -298,6 +306,7 @@ def test_gemm_tn_wgrad(ext, M, N, K):
         ext.gemm_tn_wgrad_seg([dy[i * rows:(i + 1) * rows] for i in range(n)],
                               [x[i * rows:(i + 1) * rows] for i in range(n)], g2)
         assert rel(g2, ref2) < 1e-4, n
+    ext.gemm_tn_set_fused(1)
 
 
 @pytest.mark.parametrize("T0", [0, 3])

@@ -63,7 +63,8 @@ def main():
     ap.add_argument("--only", default="")
     ap.add_argument("--kinds", default="fwd,fwd_gelu,dgrad")
     ap.add_argument("--variant", default="0", help="kernel variant(s), comma separated: 0 = default routing, "
-                    "1 = 64-deep main loop everywhere, suffix t = tail split; several = interleaved A/B")
+                    "1 = 64-deep main loop everywhere; suffix t = tail split, n = narrow tiles at every M, w = never narrow; "
+                    "several = interleaved A/B")
     ap.add_argument("--group", type=int, default=8, help="row tiles per column sweep")
     ap.add_argument("--tail", type=int, default=0, help="tail split of the last partial wave (1 = on)")
     a = ap.parse_args()
@@ -71,9 +72,11 @@ def main():
     ext.gemm_set_tail(a.tail)
     variants = a.variant.split(",")
 
-    def setv(v):  # suffix t = tail split (last partial wave split-K + finish kernel)
+    def setv(v):  # suffix t = tail split (last partial wave split-K + finish kernel), n = narrow
+        # 128 x 192 tiles at every M, w = never narrow (256 x 256 tiles at every M)
         ext.gemm_set_tail(1 if "t" in v else 0)
-        ext.gemm_set_variant(int(v.rstrip("t")), a.group)
+        ext.gemm_set_narrow(1 << 30 if "n" in v else 0 if "w" in v else 4096)
+        ext.gemm_set_variant(int(v.rstrip("tnw")), a.group)
 
     setv(variants[0])
     names = [n for n in FWD if not a.only or n in a.only.split(",")]
