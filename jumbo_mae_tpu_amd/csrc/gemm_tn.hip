@@ -503,7 +503,9 @@ __global__ __launch_bounds__(NTH, 1) void gemm_tn4_kernel(const uint16_t* __rest
     }
   }
   if constexpr (ACC == 2) {
-    __shared__ int is_last;
+    // the flag lives in the (drained) dynamic LDS ring: a static __shared__ variable would move the
+    // ring's base, which the transposing-read asm addresses relative to an aligned origin
+    int& is_last = *reinterpret_cast<int*>(smem);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's slice stores are done
     __syncthreads();
     if (tid == 0) {
@@ -528,8 +530,16 @@ __global__ __launch_bounds__(NTH, 1) void gemm_tn4_kernel(const uint16_t* __rest
       float v[4][4];
 #pragma unroll
       for (int nt = 0; nt < 4; ++nt) load4(G + (long)n * ldg + k0 + wc * 64 + 4 * g + nt * 16, v[nt]);
+      // fixed order G + slice 0 + ... + slice S-1 whichever split is last (bitwise deterministic);
+      // the own slice is added from the registers (the same fp32 values it stored)
       for (int sp = 0; sp < S; ++sp) {
-        if (sp == split) continue;
+        if (sp == split) {
+#pragma unroll
+          for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) v[nt][i] += acc[mt][nt][i];
+          continue;
+        }
         const float* srow = out + (long)sp * split_stride + off;
 #pragma unroll
         for (int nt = 0; nt < 4; ++nt) {
@@ -540,11 +550,7 @@ __global__ __launch_bounds__(NTH, 1) void gemm_tn4_kernel(const uint16_t* __rest
         }
       }
 #pragma unroll
-      for (int nt = 0; nt < 4; ++nt) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) v[nt][i] += acc[mt][nt][i];
-        store4(G + (long)n * ldg + k0 + wc * 64 + 4 * g + nt * 16, v[nt]);
-      }
+      for (int nt = 0; nt < 4; ++nt) store4(G + (long)n * ldg + k0 + wc * 64 + 4 * g + nt * 16, v[nt]);
     }
   }
 }
@@ -602,6 +608,9 @@ int* tickets_for(int tiles) {
   if (g_tickets == nullptr) {  // once per process, outside any graph capture (the first call is eager)
     (void)hipMalloc((void**)&g_tickets, TICKETS * sizeof(int));
     (void)hipMemset(g_tickets, 0, TICKETS * sizeof(int));
+    // the zeroing must be complete before the first kernel on ANY stream reads the tickets (a
+    // non-blocking stream does not order behind the null-stream memset)
+    (void)hipDeviceSynchronize();
   }
   if (tiles > TICKETS) return nullptr;
   if (g_ticket_next + tiles > TICKETS) g_ticket_next = 0;

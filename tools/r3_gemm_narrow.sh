@@ -5,9 +5,10 @@
 set -o pipefail
 export TMPDIR=/tmp
 R=${GRAFT_REPO_ROOT:-$(pwd)}; cd $R; O=gpurun_out/$1; mkdir -p $O
-timeout -k 10 400 python -u -m pytest tests/test_kernels_gpu.py -x -q --timeout 120 --timeout-method thread -k "gemm or small_m" > $O/pytest.log 2>&1 || { tail -30 $O/pytest.log; exit 1; }
+timeout -k 10 400 python -u -m pytest tests/test_kernels_gpu.py -q --timeout 120 --timeout-method thread -k "gemm or small_m or tn_wgrad" > $O/pytest.log 2>&1; grep -E "passed|failed|FAILED" $O/pytest.log | tail -40
 tail -1 $O/pytest.log
-timeout -k 10 300 python -u tools/gemm_nt_bench.py --variant 0,0n,0w --only jumbo1,jumbo2,b_jumbo1,b_jumbo2,enc_wo,enc_ff2,b_wo,b_ff2,ft_wo,dec_wo --kinds fwd,dgrad --iters 10 --rounds 3 > $O/bench.txt 2>&1 || { tail $O/bench.txt; exit 1; }
+timeout -k 10 300 python -u -m pytest tests/test_dist_gpu.py tests/test_model_gpu.py -q --timeout 200 --timeout-method thread > $O/pytest_model.log 2>&1; grep -E "passed|failed|FAILED|Error" $O/pytest_model.log | tail -20
+timeout -k 10 300 python -u tools/gemm_nt_bench.py --variant 0 --only jumbo2,b_jumbo2 --kinds splitk --iters 10 --rounds 3 > $O/bench.txt 2>&1 || { tail $O/bench.txt; exit 1; }
 grep -v amdgpu.ids $O/bench.txt
 timeout -k 10 300 python -u tools/gemm_nt_bench.py --variant 0 --only jumbo1,b_jumbo1 --kinds fwd_gelu_d,dgrad_dmul --iters 10 --rounds 3 > $O/bench_epi.txt 2>&1 || { tail $O/bench_epi.txt; exit 1; }
 grep -v amdgpu.ids $O/bench_epi.txt
