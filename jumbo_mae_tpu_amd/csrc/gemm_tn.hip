@@ -658,6 +658,9 @@ int launch_tn(const uint16_t* A, long lda, const uint16_t* B, long ldb, int M, i
 }
 }  // namespace
 
+// rotating range of n zeroed counters for in-kernel last-arriver hand-offs (re-armed by their users)
+int* jm_tickets(int n) { return tickets_for(n); }
+
 void jm_gemm_tn_set_fused(int v) { g_tn_fused = v; }
 
 // G[N][K] (ldo) += A[M][N]^T . B[M][K]; partial: [S][N][K] fp32 workspace when S > 1 (else null).

@@ -372,11 +372,12 @@ def test_gemm_nt_splitk(ext, M, N, K, S, variant, narrow):
 
 @pytest.mark.parametrize("T0,view_y,with_scale", [(0, False, True), (3, False, True), (0, True, True),
                                                   (3, True, False)])
-@pytest.mark.parametrize("direct", [1, 0])
+@pytest.mark.parametrize("direct", [2, 1, 0])
 def test_layernorm_bwd_fused_residual(ext, T0, view_y, with_scale, direct):
     """LN backward with the consumer's residual backward fused in == layernorm_bwd followed by
     residual_bwd on the rows t >= T0 (y as a contiguous slab or a strided view into a buffer);
-    direct = parameter partials as float atomics from each block (1) or workspace + reduce (0)."""
+    direct: parameter partials folded in the kernel by the last block of each group (0), float
+    atomics from every block (1), workspace + reduce launch (2)."""
     ext.ln_set_direct(direct)
     torch.manual_seed(0)
     B, T, D = 6, 52, 1024
