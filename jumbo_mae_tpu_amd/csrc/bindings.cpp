@@ -87,7 +87,6 @@ int jm_gemm_nt_tiles(int M, int N);
 int jm_gemm_nt_colpart_rows(int M, int N);
 int jm_gemm_nt_tail_plan(int M, int N, int K, int epi, int* tail_r, long* ws_floats);
 int jm_gemm_tn_plan(int M, int N, int K, int* S_out);
-void jm_gemm_tn_set_fused(int v);
 int jm_gemm_tn(const uint16_t* A, long lda, const uint16_t* B, long ldb, int M, int N, int K, int sps, int S,
                float* G, long ldo, float* partial, hipStream_t st);
 struct TnSegs {
@@ -802,8 +801,8 @@ int64_t gemm_tn_wgrad(torch::Tensor dy, torch::Tensor x, torch::Tensor g) {
   if (S > 1) part = torch::empty({SP, (long)N * K}, g.options());
   const int done = jm_gemm_tn(bf(dy), dy.stride(0), bf(x), x.stride(0), M, N, K, sps, S, g.data_ptr<float>(), K,
                               S > 1 ? part.data_ptr<float>() : nullptr, stream());
-  check_rc(done < 0 ? done : 0, "gemm_tn_wgrad");
-  if (S > 1 && done == 0) check_rc(jm_splitk_reduce_add(part.data_ptr<float>(), g.data_ptr<float>(), (long)N * K, SP, stream()),
+  check_rc(done, "gemm_tn_wgrad");
+  if (S > 1) check_rc(jm_splitk_reduce_add(part.data_ptr<float>(), g.data_ptr<float>(), (long)N * K, SP, stream()),
                       "gemm_tn_wgrad reduce");
   return S;
 }
@@ -839,8 +838,8 @@ int64_t gemm_tn_wgrad_seg(std::vector<torch::Tensor> dys, std::vector<torch::Ten
   if (S > 1) part = torch::empty({SP, (long)N * K}, g.options());
   const int done = jm_gemm_tn_seg(segs, d0.stride(0), x0.stride(0), N, K, sps, S, g.data_ptr<float>(), K,
                                   S > 1 ? part.data_ptr<float>() : nullptr, stream());
-  check_rc(done < 0 ? done : 0, "gemm_tn_wgrad_seg");
-  if (S > 1 && done == 0) check_rc(jm_splitk_reduce_add(part.data_ptr<float>(), g.data_ptr<float>(), (long)N * K, SP, stream()),
+  check_rc(done, "gemm_tn_wgrad_seg");
+  if (S > 1) check_rc(jm_splitk_reduce_add(part.data_ptr<float>(), g.data_ptr<float>(), (long)N * K, SP, stream()),
                       "gemm_tn_wgrad_seg reduce");
   return S;
 }
@@ -930,7 +929,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("attn_set_max_seq", &jm_attn_set_max_seq);
   m.def("gemm_tn_wgrad", &gemm_tn_wgrad);
   m.def("gemm_tn_wgrad_seg", &gemm_tn_wgrad_seg);
-  m.def("gemm_tn_set_fused", &jm_gemm_tn_set_fused, "TN split reduction in the kernel (1, default) or a reduce launch (0)");
   m.def("gemm_set_variant", &jm_gemm_set_variant, py::arg("nt64"), py::arg("group") = 8,
         "nt64 = 1: every NT launch on the 64-deep main loop (tests); group: row tiles per column sweep");
   m.def("gemm_set_tail", &jm_gemm_set_tail);

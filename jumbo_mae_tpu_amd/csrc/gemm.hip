@@ -1091,13 +1091,20 @@ int g_narrow_max_m = 4096;  // M below this: 128 x 192 tiles (A/B switch: 0 = ne
 
 bool narrow(int M, int N) { return M < g_narrow_max_m && N % 8 == 0; }
 
+// split-K (EPI_PARTIAL, splits > 1) keeps the 256 x 256 kernels from M = 256 up: the jumbo MLP's
+// K = 12288 GEMMs ran 43 us there vs 47 us on narrow tiles (profiles/r3e_summary_vitl_b512_fused_reductions.txt)
+bool narrow_launch(int M, int N, int epi, int splits) {
+  if (!narrow(M, N)) return false;
+  return !(epi == EPI_PARTIAL && splits > 1 && M >= 256);
+}
+
 // narrow tiles for M < 4096; K in 128-deep units (split-K: per split) -> p4, else the 64-deep
 // kernel (nontemporal epilogue stores)
 template <int EPI>
 void launch_epi(const uint16_t* A, long lda, const uint16_t* B, long ldb, int M, int N, int K, const GemmEpi& ep,
                 int nwg, hipStream_t st) {
   if constexpr (EPI != EPI_TAIL) {
-    if (narrow(M, N) && ep.t_count == 0) return launch_narrow<EPI>(A, lda, B, ldb, M, N, K, ep, st);
+    if (narrow_launch(M, N, EPI, ep.splits) && ep.t_count == 0) return launch_narrow<EPI>(A, lda, B, ldb, M, N, K, ep, st);
   }
   if (!g_gemm_nt64 && K % 128 == 0 && (EPI != EPI_PARTIAL || K / 128 >= ep.splits))
     return launch_p4<EPI>(A, lda, B, ldb, M, N, K, ep, nwg, st);

@@ -254,7 +254,7 @@ __global__ __launch_bounds__(NTH, 1) void gemm_tn_kernel(const uint16_t* __restr
   step(K0{}, t + 1, f1, f0);
 
   // ---- epilogue: acc[mt][nt][i] = G[n0 + wr*128 + mt*16 + l16][k0 + wc*64 + nt*16 + 4g + i]
-  float* dst = ACC == 1 ? out : out + (long)split * split_stride;
+  float* dst = ACC ? out : out + (long)split * split_stride;
 #pragma unroll
   for (int mt = 0; mt < 8; ++mt) {
     const int n = n0 + wr * 128 + mt * 16 + l16;
@@ -262,7 +262,7 @@ __global__ __launch_bounds__(NTH, 1) void gemm_tn_kernel(const uint16_t* __restr
 #pragma unroll
     for (int nt = 0; nt < 4; ++nt) {
       float v[4] = {acc[mt][nt][0], acc[mt][nt][1], acc[mt][nt][2], acc[mt][nt][3]};
-      if (ACC == 1) {
+      if (ACC) {
         float o[4];
         load4(row + nt * 16, o);
 #pragma unroll
@@ -288,20 +288,11 @@ __global__ __launch_bounds__(NTH, 1) void gemm_tn_kernel(const uint16_t* __restr
 // address per block (+ immediates for the k offsets).  Waves 4-7 at static priority 1.
 constexpr int SLOT4 = 64 * 128;  // elements per slot
 
-// ACC = 2 (split reduction in the kernel): every split stores its fp32 partial tile, then takes
-// a ticket on the tile's counter; the split whose ticket is the last one adds the other S - 1
-// slices (in slice order) and G to its own accumulators and writes G -- no reduce launch, no
-// read-back of its own slice.  Hand-off (MI355X_MICROARCH.md "Valid forms"): every storing wave
-// waits vmcnt(0), workgroup barrier, one lane releases at agent scope, waits, takes the ticket;
-// the last one acquires at agent scope before the workgroup reads the slices, and re-arms the
-// counter (0) for the next launch.
 template <int ACC, bool SEG>
 __global__ __launch_bounds__(NTH, 1) void gemm_tn4_kernel(const uint16_t* __restrict__ A, long lda,
                                                           const uint16_t* __restrict__ B, long ldb, int M, int N,
                                                           int K, int steps_per_split, float* __restrict__ out,
-                                                          long ldo, long split_stride, TnSegs segs = {},
-                                                          float* __restrict__ G = nullptr, long ldg = 0,
-                                                          int* __restrict__ tickets = nullptr, int S = 1) {
+                                                          long ldo, long split_stride, TnSegs segs = {}) {
   JM_DGUARD(blockDim.x == NTH && steps_per_split >= 4 && steps_per_split % 4 == 0 && M > 0);
   extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
   const int tid = threadIdx.x;
@@ -485,7 +476,7 @@ __global__ __launch_bounds__(NTH, 1) void gemm_tn4_kernel(const uint16_t* __rest
   ktile(K0{}, t + 1, bq, bp);
 
   // ---- epilogue: acc[mt][nt][i] = G[n0 + wr*128 + mt*16 + l16][k0 + wc*64 + nt*16 + 4g + i]
-  float* dst = ACC == 1 ? out : out + (long)split * split_stride;
+  float* dst = ACC ? out : out + (long)split * split_stride;
 #pragma unroll
   for (int mt = 0; mt < 8; ++mt) {
     const int n = n0 + wr * 128 + mt * 16 + l16;
@@ -493,64 +484,13 @@ __global__ __launch_bounds__(NTH, 1) void gemm_tn4_kernel(const uint16_t* __rest
 #pragma unroll
     for (int nt = 0; nt < 4; ++nt) {
       float v[4] = {acc[mt][nt][0], acc[mt][nt][1], acc[mt][nt][2], acc[mt][nt][3]};
-      if (ACC == 1) {
+      if (ACC) {
         float o[4];
         load4(row + nt * 16, o);
 #pragma unroll
         for (int i = 0; i < 4; ++i) v[i] += o[i];
       }
       store4(row + nt * 16, v);
-    }
-  }
-  if constexpr (ACC == 2) {
-    // the flag lives in the (drained) dynamic LDS ring: a static __shared__ variable would move the
-    // ring's base, which the transposing-read asm addresses relative to an aligned origin
-    int& is_last = *reinterpret_cast<int*>(smem);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's slice stores are done
-    __syncthreads();
-    if (tid == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      const int ticket = __hip_atomic_fetch_add(tickets + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const int last = ticket == S - 1;
-      if (last) {
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __hip_atomic_store(tickets + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-      is_last = last;
-    }
-    __syncthreads();
-    if (!is_last) return;
-    // G += sum of all slices: own slice from the registers, the others (and G) loaded 16 B per lane
-#pragma unroll
-    for (int mt = 0; mt < 8; ++mt) {
-      const int n = n0 + wr * 128 + mt * 16 + l16;
-      const long off = (long)n * ldo + k0 + wc * 64 + 4 * g;
-      float v[4][4];
-#pragma unroll
-      for (int nt = 0; nt < 4; ++nt) load4(G + (long)n * ldg + k0 + wc * 64 + 4 * g + nt * 16, v[nt]);
-      // fixed order G + slice 0 + ... + slice S-1 whichever split is last (bitwise deterministic);
-      // the own slice is added from the registers (the same fp32 values it stored)
-      for (int sp = 0; sp < S; ++sp) {
-        if (sp == split) {
-#pragma unroll
-          for (int nt = 0; nt < 4; ++nt)
-#pragma unroll
-            for (int i = 0; i < 4; ++i) v[nt][i] += acc[mt][nt][i];
-          continue;
-        }
-        const float* srow = out + (long)sp * split_stride + off;
-#pragma unroll
-        for (int nt = 0; nt < 4; ++nt) {
-          float o[4];
-          load4(srow + nt * 16, o);
-#pragma unroll
-          for (int i = 0; i < 4; ++i) v[nt][i] += o[i];
-        }
-      }
-#pragma unroll
-      for (int nt = 0; nt < 4; ++nt) store4(G + (long)n * ldg + k0 + wc * 64 + 4 * g + nt * 16, v[nt]);
     }
   }
 }
@@ -598,33 +538,10 @@ void set_smem_once(KERN k, bool& done) {
 }
 
 // the 4-phase kernel (whole 128-row units, 64-row segments) or the r1 32-row-step kernel
-int g_tn_fused = 1;  // split reduction inside the 4-phase kernel (last-arriving split per tile)
-int* g_tickets = nullptr;  // per-tile tickets, zeroed once, re-armed by each tile's last split
-int g_ticket_next = 0;
-constexpr int TICKETS = 1 << 16;
-
-// a range of `tiles` zeroed tickets (rotating, so launches on different streams get disjoint ranges)
-int* tickets_for(int tiles) {
-  if (g_tickets == nullptr) {  // once per process, outside any graph capture (the first call is eager)
-    (void)hipMalloc((void**)&g_tickets, TICKETS * sizeof(int));
-    (void)hipMemset(g_tickets, 0, TICKETS * sizeof(int));
-    // the zeroing must be complete before the first kernel on ANY stream reads the tickets (a
-    // non-blocking stream does not order behind the null-stream memset)
-    (void)hipDeviceSynchronize();
-  }
-  if (tiles > TICKETS) return nullptr;
-  if (g_ticket_next + tiles > TICKETS) g_ticket_next = 0;
-  int* t = g_tickets + g_ticket_next;
-  g_ticket_next += tiles;
-  return t;
-}
-
-// returns 1 when the split reduction was done in the kernel (G final), 0 when the caller must
-// reduce the S partial slices, < 0 on error
+// returns 0 (the caller reduces the S partial slices into G when S > 1), < 0 on error
 template <bool SEG>
 int launch_tn(const uint16_t* A, long lda, const uint16_t* B, long ldb, int M, int N, int K, int sps, int S,
               float* G, long ldo, float* partial, const TnSegs& segs, bool p4, hipStream_t st) {
-  int* tickets = (p4 && S > 1 && g_tn_fused) ? tickets_for((N / TN_) * (K / TK_)) : nullptr;
   const int tiles = (N / TN_) * (K / TK_);
   const size_t sm = jm_gemm_tn_smem();
   if (S > 1 && partial == nullptr) return -3;
@@ -633,12 +550,6 @@ int launch_tn(const uint16_t* A, long lda, const uint16_t* B, long ldb, int M, i
       static bool a = false;
       set_smem_once(gemm_tn4_kernel<1, SEG>, a);
       gemm_tn4_kernel<1, SEG><<<tiles, NTH, sm, st>>>(A, lda, B, ldb, M, N, K, sps, G, ldo, 0, segs);
-    } else if (g_tn_fused && tickets != nullptr) {
-      static bool a = false;
-      set_smem_once(gemm_tn4_kernel<2, SEG>, a);
-      gemm_tn4_kernel<2, SEG><<<tiles * S, NTH, sm, st>>>(A, lda, B, ldb, M, N, K, sps, partial, K, (long)N * K,
-                                                          segs, G, ldo, tickets, S);
-      return 1;  // reduced in the kernel
     } else {
       static bool a = false;
       set_smem_once(gemm_tn4_kernel<0, SEG>, a);
@@ -658,13 +569,12 @@ int launch_tn(const uint16_t* A, long lda, const uint16_t* B, long ldb, int M, i
 }
 }  // namespace
 
-// rotating range of n zeroed counters for in-kernel last-arriver hand-offs (re-armed by their users)
-int* jm_tickets(int n) { return tickets_for(n); }
 
-void jm_gemm_tn_set_fused(int v) { g_tn_fused = v; }
 
-// G[N][K] (ldo) += A[M][N]^T . B[M][K]; partial: [S][N][K] fp32 workspace when S > 1 (else null).
-// Returns 1 when G is final (in-kernel split reduction), 0 when the S slices still need reducing.
+// G[N][K] (ldo) += A[M][N]^T . B[M][K]; partial: [S][N][K] fp32 workspace when S > 1 (else null);
+// the caller reduces the S slices into G (jm_splitk_reduce_add).  Measured and removed: float-atomic
+// split reduction (profiles/r2_tn_atomic.txt), split 0 into G (r1_ab_tn_acc0.txt), the last-arriving
+// split adding the other slices in the kernel (r3e_summary_vitl_b512_fused_reductions.txt).
 int jm_gemm_tn(const uint16_t* A, long lda, const uint16_t* B, long ldb, int M, int N, int K, int sps, int S,
                float* G, long ldo, float* partial, hipStream_t st) {
   if (N % TN_ || K % TK_ || M <= 0) return -1;

@@ -13,8 +13,6 @@
 #include "common.h"
 #include "jm_api.h"
 
-int* jm_tickets(int n);  // gemm_tn.hip: rotating range of zeroed per-launch counters
-
 namespace {
 
 template <int V, typename TO>
@@ -198,18 +196,15 @@ struct ParamOuts {
 // partial rows in ws: [dgamma | dbeta] (NP = 2) or [dgamma | dbeta | dscale | dbias] (NP = 4)
 // ER (early residual-gradient load): dres is loaded together with x / dy in the first pass (one
 // HBM round trip per row instead of two) while the parameter partials stay in registers.
-constexpr int LN_GROUP = 8;  // LN backward blocks whose partial rows one last-arriving block folds
-
 template <int V, typename TI, bool RES, bool ER = false>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(const TI* __restrict__ dy, const float* __restrict__ x,
                                                      long sB, long sT, int T, int rows, int D,
                                                      const float* __restrict__ mean, const float* __restrict__ rstd,
                                                      const float* __restrict__ gamma, LnBwdIO io, LnResIO rio,
-                                                     float* __restrict__ ws, int accum_params, ParamOuts outs,
-                                                     int* __restrict__ tickets) {
+                                                     float* __restrict__ ws, int accum_params, ParamOuts outs) {
   JM_DGUARD(blockDim.x == 256 && D % 4 == 0 && D <= V * 256);
   constexpr int NP = RES ? 4 : 2;
-  extern __shared__ __attribute__((aligned(16))) float red[];  // [NP*D] (+ 4 floats: group flag)
+  extern __shared__ __attribute__((aligned(16))) float red[];  // [NP*D]
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const bool partials = accum_params || RES;
   auto acc_add = [&](float (&acc)[NP][V][4], int k, int i, int j, float v) { acc[k][i][j] += v; };
@@ -332,37 +327,6 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const TI* __restrict__ dy, 
     float a[4];
     load4(red + i, a);
     store4(ws + (long)blockIdx.x * NP * D + i, a);
-  }
-  if (tickets == nullptr) return;  // ln_param_reduce_kernel sums the rows
-  // group fold: the last-arriving block of each LN_GROUP consecutive blocks adds the group's partial
-  // rows (in block order) and atomically adds the sums to the outputs -- the reduce launch and its
-  // full read of the workspace are gone.  Hand-off: MI355X_MICROARCH.md "Valid forms" (every
-  // storing wave vmcnt(0), barrier, one lane release + ticket; the last one acquires).
-  int* flag = reinterpret_cast<int*>(red + NP * D);
-  const int grp = blockIdx.x / LN_GROUP, gb0 = grp * LN_GROUP;
-  const int gn = min(LN_GROUP, (int)gridDim.x - gb0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const int t = __hip_atomic_fetch_add(tickets + grp, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const int last = t == gn - 1;
-    if (last) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __hip_atomic_store(tickets + grp, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    *flag = last;
-  }
-  __syncthreads();
-  if (!*flag) return;
-  // one float per lane: every row read and every atomic wave-instruction covers 256 contiguous B
-  for (int c = threadIdx.x; c < NP * D; c += 256) {
-    float a = 0.f;
-    for (int b = gb0; b < gb0 + gn; ++b) a += ws[(long)b * NP * D + c];
-    float* dst = outs.p[c / D];
-    if (dst != nullptr) atomicAdd(&dst[c - (c / D) * D], a);
   }
 }
 
@@ -583,10 +547,11 @@ constexpr int LN_WIDE_MAX_ROWS = 8192;
 int pick_vw(int D) { return D <= 2048 ? 2 : D <= 3072 ? 3 : D <= 4096 ? 4 : -1; }
 bool use_wide(int rows, int D) { return D > 1024 && rows <= LN_WIDE_MAX_ROWS && pick_vw(D) > 0; }
 
-// LN backward parameter partials: 0 (default) = per-block workspace rows folded in the kernel by
-// the last block of each group of 8 (float atomics from 1/8 of the blocks), 1 = float atomics
-// from every block straight into the outputs, 2 = workspace rows + ln_param_reduce_kernel (the r2
-// default; direct measured the same step time, profiles/r2_ln_param_reduce.txt)
+// LN backward parameter partials: 1 = float atomics from each block straight into the outputs,
+// 0 = per-block workspace rows + ln_param_reduce_kernel (default: the direct form measured the
+// same step time, ViT-L 94.05 vs 93.90 ms in one process -- 512 adders per address cost what the
+// reduce launch did; profiles/r2_ln_param_reduce.txt; folding the rows in the kernel by the last
+// block of each group of 8 made the backward 2.7 ms/step slower, r3e_summary_vitl_b512_fused_reductions.txt)
 int g_ln_direct = 0;
 
 // the residual-gradient input is loaded with x / dy (ER) where the registers allow it (V <= 4:
@@ -596,12 +561,11 @@ int g_ln_direct = 0;
 template <typename TI, bool RES>
 void launch_bwd(int V, dim3 grid, size_t smem, hipStream_t st, const TI* dy, const float* x, long sB, long sT,
                 int T, int rows, int D, const float* m, const float* r, const float* g, LnBwdIO dx, LnResIO rio,
-                float* ws, int acc, ParamOuts outs, int* tickets) {
+                float* ws, int acc, ParamOuts outs) {
 #define JM_LNB(VV)                                                                                          \
   case VV:                                                                                                  \
     ln_bwd_kernel<VV, TI, RES, (VV >= 2 && VV <= 4)><<<grid, 256, smem, st>>>(dy, x, sB, sT, T, rows, D, m, r, \
-                                                                              g, dx, rio, ws, acc, outs,      \
-                                                                              tickets);                       \
+                                                                              g, dx, rio, ws, acc, outs);     \
     break;
   switch (V) {
     JM_LNB(1) JM_LNB(2) JM_LNB(3) JM_LNB(4) JM_LNB(6) JM_LNB(8) JM_LNB(9) JM_LNB(12) JM_LNB(16)
@@ -716,31 +680,30 @@ int jm_layernorm_bwd(const void* dy, int dy_bf16, const float* x, long sB, long 
     }
     return 0;
   }
-  const size_t smem = partials ? NP * D * sizeof(float) + 16 : 0;
+  const size_t smem = partials ? NP * D * sizeof(float) : 0;
   const ParamOuts outs{{accum_params ? dgamma : nullptr, accum_params ? dbeta : nullptr,
                         res ? res->dscale : nullptr, res ? res->dbias : nullptr}};
-  // direct atomics, workspace + group fold in the kernel (default), or workspace + reduce launch
-  const bool direct = g_ln_direct == 1;
+  // direct atomics or workspace + reduce
+  const bool direct = g_ln_direct;
   float* wsk = direct ? nullptr : ws;
-  int* tickets = (partials && !direct && g_ln_direct == 0) ? jm_tickets((nb + LN_GROUP - 1) / LN_GROUP) : nullptr;
   LnResIO rio{nullptr, nullptr, 0, 0, nullptr, nullptr, 0};
   if (res) rio = LnResIO{res->y, res->dy, res->yB, res->yT, res->scale, res->mask, res->T0};
   if (dy_bf16) {
     if (res)
       launch_bwd<uint16_t, true>(V, grid, smem, st, (const uint16_t*)dy, x, sB, sT, T, rows, D, mean, rstd, gamma,
-                                 dx, rio, wsk, accum_params, outs, tickets);
+                                 dx, rio, wsk, accum_params, outs);
     else
       launch_bwd<uint16_t, false>(V, grid, smem, st, (const uint16_t*)dy, x, sB, sT, T, rows, D, mean, rstd, gamma,
-                                  dx, rio, wsk, accum_params, outs, tickets);
+                                  dx, rio, wsk, accum_params, outs);
   } else {
     if (res)
       launch_bwd<float, true>(V, grid, smem, st, (const float*)dy, x, sB, sT, T, rows, D, mean, rstd, gamma, dx, rio,
-                              wsk, accum_params, outs, tickets);
+                              wsk, accum_params, outs);
     else
       launch_bwd<float, false>(V, grid, smem, st, (const float*)dy, x, sB, sT, T, rows, D, mean, rstd, gamma, dx, rio,
-                               wsk, accum_params, outs, tickets);
+                               wsk, accum_params, outs);
   }
-  if (partials && !direct && tickets == nullptr)
+  if (partials && !direct)
     ln_param_reduce_kernel<<<param_reduce_grid(nb, D, NP), 256, 0, st>>>(ws, nb, D, NP, outs);
   return 0;
 }

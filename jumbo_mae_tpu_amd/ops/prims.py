@@ -123,16 +123,21 @@ def use_our_gemm(M: int, N: int, K: int, fused_gelu: bool = False, kind: str = "
 
 
 def splitk_plan(M: int, N: int, K: int) -> int:
-    """Split-K factor for a small-M GEMM on the narrow MFMA kernel (0 = not this path): the jumbo
-    MLP's K = 12288 GEMMs (W2 forward, W1 data gradient) have 64 narrow tiles at M = 512 -> 4
-    splits; the finetune jumbo MLP (M = 128) and the classifier head likewise.  Every split keeps
-    >= 512 of K; fp32 partial slices are summed by one reduce (+ bias, or + an fp32 addend)."""
+    """Split-K factor for a small-M GEMM whose narrow tiles cannot fill the chip (0 = not this path):
+    the jumbo MLP's K = 12288 GEMMs (W2 forward, W1 data gradient: 24 256 x 256 tiles at M = 512 ->
+    10 splits on the 4-phase kernel), the finetune jumbo MLP (M = 128: narrow tiles) and the
+    classifier head.  Every split keeps >= 512 of K; fp32 partial slices are summed by one reduce
+    (+ bias, or + an fp32 addend)."""
     if _GEMM_MODE == "blas" or M >= NARROW_MAX_M or K % 64 or N % 8:
         return 0
-    tiles = nt_tiles(M, N)
-    if tiles >= _NARROW_FUSED_MIN_TILES:
+    if nt_tiles(M, N) >= _NARROW_FUSED_MIN_TILES:
         return 0
-    s = min(256 // tiles, K // 512, 16)
+    if M >= 256:  # split launches keep the 256 x 256 tiles (jm_gemm narrow_launch): whole 128-deep units
+        if K % 128:
+            return 0
+        s = min(256 // (-(-M // 256) * -(-N // 256)), K // 512, 32)
+    else:
+        s = min(256 // nt_tiles(M, N), K // 512, 16)
     return s if s >= 2 else 0
 
 
