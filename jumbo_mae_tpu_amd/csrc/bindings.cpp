@@ -17,7 +17,6 @@ int jm_layernorm_bwd(const void* dy, int dy_bf16, const float* x, long sB, long 
                      const JmLnRes* res, hipStream_t st);
 int jm_layernorm_bwd_blocks(int rows, int D);
 void jm_ln_set_bwd_blocks(int v);
-void jm_ln_set_direct(int v);
 // debug build (-DJM_DEBUG): first failing soft-check line per kernel translation unit (0 = none;
 // reading clears it); always 0 in the release build
 int jm_debug_line_attention();
@@ -945,7 +944,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("gelu_only") = false, py::arg("gelu_deriv") = false);
   m.def("attn_set_tr", &jm_attn_set_tr);
   m.def("attn_set_remap", &jm_attn_set_remap, "attention grid: bit 0 XCD-aware (b, h) order, bit 1 forward Q prefetch");
-  m.def("ln_set_direct", &jm_ln_set_direct);
   m.def("attn_set_fwd_hpw", &jm_attn_set_fwd_hpw);
   m.def("attn_set_bwd_ppw", &jm_attn_set_bwd_ppw);
   m.def("attn_set_bwd3_hd64", &jm_attn_set_bwd3_hd64);

@@ -24,8 +24,14 @@ JM_DEVICE uint16_t f2bf(float f) {
   return *reinterpret_cast<uint16_t*>(&h);
 }
 
+// two floats -> one dword of two bf16 (a low): built as a 2-vector so that it lowers to ONE
+// v_cvt_pk_bf16_f32 (the shift-or form became two single-operand conversions + lshl + or)
 JM_DEVICE uint32_t pack_bf2(float a, float b) {
-  return (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16);
+  typedef __attribute__((ext_vector_type(2))) short s16x2_t;
+  s16x2_t s;
+  s[0] = (short)f2bf(a);
+  s[1] = (short)f2bf(b);
+  return __builtin_bit_cast(uint32_t, s);
 }
 
 template <typename T> JM_DEVICE float to_f(T v);
@@ -63,6 +69,42 @@ JM_DEVICE void gelu_and_grad_f(float x, float& g, float& d) {
   const float p = gelu_p_f(x);
   g = x * p;
   d = __builtin_fmaf(g * (1.f - p), __builtin_fmaf(0.21406444881780076f, x * x, 1.5957691216057308f), p);
+}
+
+// The same on element pairs as 2-vectors: mul / add / fma lower to v_pk_*_f32 (2 elements per
+// 4-cycle issue; for epilogue phases, not beside MFMAs -- MI355X_MICROARCH.md prices packed f32
+// there as an anti-lever), log2(e) folded into the polynomial (one v_exp_f32, no pre-multiply),
+// x^2 shared by p and the derivative.  Per element pair: 9 packed ops + 4 transcendentals.
+typedef __attribute__((ext_vector_type(2))) float f32x2_t;
+constexpr float GELU_C1 = -1.5957691216057308f * 1.4426950408889634f;   // -2 sqrt(2/pi) log2(e)
+constexpr float GELU_C2 = -0.07135481627260025f * 1.4426950408889634f;  // -2 sqrt(2/pi) 0.044715 log2(e)
+
+JM_DEVICE f32x2_t gelu_p2(f32x2_t x, f32x2_t x2) {
+  const f32x2_t m = x * (x2 * GELU_C2 + GELU_C1);  // -2u log2(e)
+  f32x2_t e = {__builtin_amdgcn_exp2f(m.x), __builtin_amdgcn_exp2f(m.y)};
+  e = e + 1.f;
+  return f32x2_t{__builtin_amdgcn_rcpf(e.x), __builtin_amdgcn_rcpf(e.y)};
+}
+
+// n (even) elements: g = gelu(x) and/or d = gelu'(x) (null pointers skipped at compile time)
+template <int NE, bool G, bool D>
+JM_DEVICE void gelu_n(const float* x, float* g, float* d) {
+#pragma unroll
+  for (int j = 0; j < NE; j += 2) {
+    const f32x2_t xv = {x[j], x[j + 1]};
+    const f32x2_t x2 = xv * xv;
+    const f32x2_t p = gelu_p2(xv, x2);
+    const f32x2_t gv = xv * p;
+    if (G) {
+      g[j] = gv.x;
+      g[j + 1] = gv.y;
+    }
+    if (D) {
+      const f32x2_t dv = (gv * (1.f - p)) * (x2 * 0.21406444881780076f + 1.5957691216057308f) + p;
+      d[j] = dv.x;
+      d[j + 1] = dv.y;
+    }
+  }
 }
 
 // DPP lane moves (VALU, no LDS round trip like __shfl_xor's ds_bpermute)

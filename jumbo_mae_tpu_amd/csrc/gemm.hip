@@ -234,38 +234,42 @@ JM_DEVICE void epilogue_lds(const f32x4_t (&acc)[8][NTW], const GemmEpi& ep, uin
     const uint4 v = *reinterpret_cast<const uint4*>(cs + r * RB + ((c ^ (r & 15)) << 3));
     if (m < M && col_ok) {
       if (EPI == EPI_DGELU || EPI == EPI_DMUL) {
-        float f[8], hp[8];
+        float f[8], hp[8], gd[8];
         const uint16_t* dg = reinterpret_cast<const uint16_t*>(&v);
         const uint16_t* ah = reinterpret_cast<const uint16_t*>(&av);
 #pragma unroll
         for (int j = 0; j < 8; ++j) hp[j] = bf2f(ah[j]);
+        if (EPI == EPI_DGELU) gelu_n<8, false, true>(hp, nullptr, gd);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          f[j] = bf2f(f2bf(bf2f(dg[j]) * (EPI == EPI_DMUL ? hp[j] : gelu_grad_f(hp[j]))));
+          f[j] = bf2f(f2bf(bf2f(dg[j]) * (EPI == EPI_DMUL ? hp[j] : gd[j])));
           csum[j] += f[j];
         }
         st16(ep.out + (long)m * ep.ldo + n0 + c * 8, pack8(f), NTS);
       } else if (EPI == EPI_GELU_D) {
-        float fg[8], fd[8];
+        float fh[8], fg[8], fd[8];
         const uint16_t* h = reinterpret_cast<const uint16_t*>(&v);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) gelu_and_grad_f(bf2f(h[j]), fg[j], fd[j]);
+        for (int j = 0; j < 8; ++j) fh[j] = bf2f(h[j]);
+        gelu_n<8, true, true>(fh, fg, fd);
         st16(ep.out + (long)m * ep.ldo + n0 + c * 8, pack8(fd), NTS);
         st16(ep.out2 + (long)m * ep.ldo + n0 + c * 8, pack8(fg), NTS);
       } else if (EPI == EPI_GELU_ONLY) {
-        float f[8];
+        float fh[8], f[8];
         const uint16_t* h = reinterpret_cast<const uint16_t*>(&v);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) f[j] = gelu_tanh_f(bf2f(h[j]));
+        for (int j = 0; j < 8; ++j) fh[j] = bf2f(h[j]);
+        gelu_n<8, true, false>(fh, f, nullptr);
         st16(ep.out + (long)m * ep.ldo + n0 + c * 8, pack8(f), NTS);
       } else {
         st16(ep.out + (long)m * ep.ldo + n0 + c * 8, v, NTS);
       }
       if (EPI == EPI_GELU) {
-        float f[8];
+        float fh[8], f[8];
         const uint16_t* h = reinterpret_cast<const uint16_t*>(&v);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) f[j] = gelu_tanh_f(bf2f(h[j]));
+        for (int j = 0; j < 8; ++j) fh[j] = bf2f(h[j]);
+        gelu_n<8, true, false>(fh, f, nullptr);
         st16(ep.out2 + (long)m * ep.ldo + n0 + c * 8, pack8(f), NTS);
       }
     }
@@ -823,31 +827,36 @@ JM_DEVICE void narrow_epilogue(const f32x4_t (&acc)[4][3], const GemmEpi& ep, ui
       const uint16_t* h = reinterpret_cast<const uint16_t*>(&v);
       if constexpr (PRE) {
         const uint16_t* ah = reinterpret_cast<const uint16_t*>(&auxv[i]);
-        float f[8];
+        float f[8], hp[8], gd[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) hp[j] = bf2f(ah[j]);
+        if constexpr (EPI == EPI_DGELU) gelu_n<8, false, true>(hp, nullptr, gd);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          const float hp = bf2f(ah[j]);
-          f[j] = bf2f(f2bf(bf2f(h[j]) * (EPI == EPI_DMUL ? hp : gelu_grad_f(hp))));
+          f[j] = bf2f(f2bf(bf2f(h[j]) * (EPI == EPI_DMUL ? hp[j] : gd[j])));
           csum[j] += f[j];
         }
         st16(o, pack8(f), false);
       } else if constexpr (EPI == EPI_GELU_D) {
-        float fg[8], fd[8];
+        float fh[8], fg[8], fd[8];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) gelu_and_grad_f(bf2f(h[j]), fg[j], fd[j]);
+        for (int j = 0; j < 8; ++j) fh[j] = bf2f(h[j]);
+        gelu_n<8, true, true>(fh, fg, fd);
         st16(o, pack8(fd), false);
         st16(ep.out2 + (long)m * ep.ldo + n, pack8(fg), false);
       } else if constexpr (EPI == EPI_GELU_ONLY) {
-        float f[8];
+        float fh[8], f[8];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) f[j] = gelu_tanh_f(bf2f(h[j]));
+        for (int j = 0; j < 8; ++j) fh[j] = bf2f(h[j]);
+        gelu_n<8, true, false>(fh, f, nullptr);
         st16(o, pack8(f), false);
       } else {
         st16(o, v, false);
         if constexpr (EPI == EPI_GELU) {
-          float f[8];
+          float fh[8], f[8];
 #pragma unroll
-          for (int j = 0; j < 8; ++j) f[j] = gelu_tanh_f(bf2f(h[j]));
+          for (int j = 0; j < 8; ++j) fh[j] = bf2f(h[j]);
+          gelu_n<8, true, false>(fh, f, nullptr);
           st16(ep.out2 + (long)m * ep.ldo + n, pack8(f), false);
         }
       }

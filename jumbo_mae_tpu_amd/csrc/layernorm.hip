@@ -293,14 +293,6 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const TI* __restrict__ dy, 
     }
   }
   if (!partials) return;
-  // ws == null: the block's sums go straight into the outputs with float atomics, one 256-B row
-  // segment per wave-instruction (no workspace round trip, no ln_param_reduce launch)
-  auto direct = [&]() {
-    for (int i = threadIdx.x; i < NP * D; i += 256) {
-      float* dst = outs.p[i / D];
-      if (dst != nullptr) atomicAdd(&dst[i - (i / D) * D], red[i]);
-    }
-  };
   // merge the 4 waves' partials through LDS in turn (float4, conflict-free, no atomics), then
   // one coalesced store of the block partial row into the workspace
   for (int w = 0; w < 4; ++w) {
@@ -322,7 +314,6 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const TI* __restrict__ dy, 
     }
     __syncthreads();
   }
-  if (ws == nullptr) return direct();
   for (int i = threadIdx.x * 4; i < NP * D; i += 256 * 4) {
     float a[4];
     load4(red + i, a);
@@ -547,12 +538,11 @@ constexpr int LN_WIDE_MAX_ROWS = 8192;
 int pick_vw(int D) { return D <= 2048 ? 2 : D <= 3072 ? 3 : D <= 4096 ? 4 : -1; }
 bool use_wide(int rows, int D) { return D > 1024 && rows <= LN_WIDE_MAX_ROWS && pick_vw(D) > 0; }
 
-// LN backward parameter partials: 1 = float atomics from each block straight into the outputs,
-// 0 = per-block workspace rows + ln_param_reduce_kernel (default: the direct form measured the
-// same step time, ViT-L 94.05 vs 93.90 ms in one process -- 512 adders per address cost what the
-// reduce launch did; profiles/r2_ln_param_reduce.txt; folding the rows in the kernel by the last
-// block of each group of 8 made the backward 2.7 ms/step slower, r3e_summary_vitl_b512_fused_reductions.txt)
-int g_ln_direct = 0;
+// LN backward parameter partials: per-block workspace rows + ln_param_reduce_kernel.  Measured
+// and removed: float atomics from each block straight into the outputs (the same step time, ViT-L
+// 94.05 vs 93.90 ms -- 512 adders per address cost what the reduce launch did;
+// profiles/r2_ln_param_reduce.txt), and folding the rows in the kernel by the last block of each
+// group of 8 (2.7 ms/step slower, r3e_summary_vitl_b512_fused_reductions.txt)
 
 // the residual-gradient input is loaded with x / dy (ER) where the registers allow it (V <= 4:
 // 97.96 -> 97.75 ms/step, profiles/r1_ab_ln_bwd_early_dres.txt).  Measured and removed: LDS-
@@ -634,8 +624,6 @@ int jm_residual_ln_fwd(const float* x, long sB, long sT, const uint16_t* y, cons
   return 0;
 }
 
-void jm_ln_set_direct(int v) { g_ln_direct = v; }
-
 // runtime switch: most row-loop blocks of the (non-wide) LN backward
 int g_ln_bwd_blocks = 512;  // = 2 resident blocks per CU (2 waves / SIMD): one round, half the partials of 1024 (-0.3 ms/step, profiles/r2_ln_bwd_blocks.txt)
 void jm_ln_set_bwd_blocks(int v) { g_ln_bwd_blocks = v < 64 ? 64 : v; }
@@ -683,9 +671,7 @@ int jm_layernorm_bwd(const void* dy, int dy_bf16, const float* x, long sB, long 
   const size_t smem = partials ? NP * D * sizeof(float) : 0;
   const ParamOuts outs{{accum_params ? dgamma : nullptr, accum_params ? dbeta : nullptr,
                         res ? res->dscale : nullptr, res ? res->dbias : nullptr}};
-  // direct atomics or workspace + reduce
-  const bool direct = g_ln_direct;
-  float* wsk = direct ? nullptr : ws;
+  float* wsk = ws;
   LnResIO rio{nullptr, nullptr, 0, 0, nullptr, nullptr, 0};
   if (res) rio = LnResIO{res->y, res->dy, res->yB, res->yT, res->scale, res->mask, res->T0};
   if (dy_bf16) {
@@ -703,7 +689,7 @@ int jm_layernorm_bwd(const void* dy, int dy_bf16, const float* x, long sB, long 
       launch_bwd<float, false>(V, grid, smem, st, (const float*)dy, x, sB, sT, T, rows, D, mean, rstd, gamma, dx, rio,
                                wsk, accum_params, outs);
   }
-  if (partials && !direct)
+  if (partials)
     ln_param_reduce_kernel<<<param_reduce_grid(nb, D, NP), 256, 0, st>>>(ws, nb, D, NP, outs);
   return 0;
 }

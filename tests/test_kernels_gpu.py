@@ -22,7 +22,6 @@ def _reset_gemm_variant(request):
         request.getfixturevalue("ext").attn_set_bwd_ppw(0)
         request.getfixturevalue("ext").gemm_set_tail(1)
         request.getfixturevalue("ext").gemm_set_narrow(4096)
-        request.getfixturevalue("ext").ln_set_direct(0)
 
 
 def rel(a, b):
@@ -367,12 +366,9 @@ def test_gemm_nt_splitk(ext, M, N, K, S, variant, narrow):
 
 @pytest.mark.parametrize("T0,view_y,with_scale", [(0, False, True), (3, False, True), (0, True, True),
                                                   (3, True, False)])
-@pytest.mark.parametrize("direct", [1, 0])
-def test_layernorm_bwd_fused_residual(ext, T0, view_y, with_scale, direct):
+def test_layernorm_bwd_fused_residual(ext, T0, view_y, with_scale):
     """LN backward with the consumer's residual backward fused in == layernorm_bwd followed by
-    residual_bwd on the rows t >= T0 (y as a contiguous slab or a strided view into a buffer);
-    direct = parameter partials as float atomics from each block (1) or workspace + reduce (0)."""
-    ext.ln_set_direct(direct)
+    residual_bwd on the rows t >= T0 (y as a contiguous slab or a strided view into a buffer)."""
     torch.manual_seed(0)
     B, T, D = 6, 52, 1024
     x = torch.randn(B, T, D, device="cuda") * 2

@@ -52,9 +52,6 @@ def apply(P, cfg: str):
         elif k == "ADAMW_VEC":
             from jumbo_mae_tpu_amd.ops import _ext
             _ext.load(True).opt_set_adamw_vec(int(v))
-        elif k == "LN_DIRECT":
-            from jumbo_mae_tpu_amd.ops import _ext
-            _ext.load(True).ln_set_direct(int(v))
         elif k == "ATTN_HPW":
             from jumbo_mae_tpu_amd.ops import _ext
             _ext.load(True).attn_set_fwd_hpw(int(v))
