@@ -300,15 +300,48 @@ __global__ __launch_bounds__(256) void splitk_reduce_add_kernel(const float* __r
     }
   }
 }
+
+// The same with S a template constant, one float4 per thread and every load of the thread -- the S
+// partial slices and g -- issued before the first add: the loop form kept two 16-B loads in flight
+// per thread and ran the weight-gradient reductions at ~4.8 TB/s although the slices were just
+// written (MALL-resident).
+template <int S>
+__global__ __launch_bounds__(256) void splitk_reduce_add_s_kernel(const float* __restrict__ part,
+                                                                  float* __restrict__ g, long n4) {
+  const long i = blockIdx.x * 256L + threadIdx.x;
+  if (i >= n4) return;
+  const long n = n4 * 4;
+  float v[S][4], o[4];
+#pragma unroll
+  for (int s = 0; s < S; ++s) load4(part + (long)s * n + i * 4, v[s]);
+  load4(g + i * 4, o);
+#pragma unroll
+  for (int s = 0; s < S; ++s)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) o[j] += v[s][j];
+  store4(g + i * 4, o);
+}
 }  // namespace
 
 int jm_splitk_reduce_add(const float* part, float* g, long n, int S, hipStream_t st) {
   if (n % 4) return -1;
-  long blocks = (n / 4 + 255) / 256;
+  const long n4 = n / 4;
+  if (S >= 1 && S <= 16 && n4 >= 256L * 256) {  // large slices: the all-loads-first kernel
+    const unsigned nb = (unsigned)((n4 + 255) / 256);
+    switch (S) {
+#define JM_SKR(SS) \
+  case SS: splitk_reduce_add_s_kernel<SS><<<nb, 256, 0, st>>>(part, g, n4); return 0;
+      JM_SKR(1) JM_SKR(2) JM_SKR(3) JM_SKR(4) JM_SKR(5) JM_SKR(6) JM_SKR(7) JM_SKR(8)
+      JM_SKR(9) JM_SKR(10) JM_SKR(11) JM_SKR(12) JM_SKR(13) JM_SKR(14) JM_SKR(15) JM_SKR(16)
+#undef JM_SKR
+      default: break;
+    }
+  }
+  long blocks = (n4 + 255) / 256;
   if (blocks > 4096) blocks = 4096;
   int ys = 1;  // slice the partials until the launch has ~512 workgroups of >= 8 rows each
   while (blocks * ys < 512 && S / (ys * 2) >= 8) ys *= 2;
-  splitk_reduce_add_kernel<<<dim3((unsigned)blocks, ys), 256, 0, st>>>(part, g, n / 4, S);
+  splitk_reduce_add_kernel<<<dim3((unsigned)blocks, ys), 256, 0, st>>>(part, g, n4, S);
   return 0;
 }
 
@@ -413,18 +446,33 @@ int jm_transpose_bf16_batch(const long long* desc, int n, int tiles, hipStream_t
 // ------------------------------------------------------------------ split-K finish
 // out[m][n] (bf16) = sum_s part[s][m][n] (+ bias[n]): the epilogue of a split-K NT GEMM
 namespace {
+// SC > 0: S == SC at compile time and every partial load of a thread is issued before the first
+// add (the runtime loop kept one or two loads in flight: ~5 TB/s on MALL-resident slices)
+template <int SC>
 __global__ __launch_bounds__(256) void splitk_reduce_bf16_kernel(const float* __restrict__ part, int S, long n8,
                                                                  int N, const float* __restrict__ bias,
                                                                  uint16_t* __restrict__ out) {
   const long total = n8 * 8;
   for (long i = blockIdx.x * 256L + threadIdx.x; i < n8; i += (long)gridDim.x * 256) {
     float acc[8];
-    load8(part + i * 8, acc);
-    for (int s = 1; s < S; ++s) {
-      float v[8];
-      load8(part + (long)s * total + i * 8, v);
+    if constexpr (SC > 0) {
+      float v[SC][8];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) acc[j] += v[j];
+      for (int s = 0; s < SC; ++s) load8(part + (long)s * total + i * 8, v[s]);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] = v[0][j];
+#pragma unroll
+      for (int s = 1; s < SC; ++s)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[j] += v[s][j];
+    } else {
+      load8(part + i * 8, acc);
+      for (int s = 1; s < S; ++s) {
+        float v[8];
+        load8(part + (long)s * total + i * 8, v);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[j] += v[j];
+      }
     }
     if (bias) {
       float b[8];
@@ -441,6 +489,7 @@ __global__ __launch_bounds__(256) void splitk_reduce_bf16_kernel(const float* __
 // GEMM whose result is summed into an fp32 residual-stream gradient (the shared jumbo MLP's input
 // gradient d hc = dx2_cls + W1 dpre) without a bf16 round trip and a separate add pass
 namespace {
+template <int SC>
 __global__ __launch_bounds__(256) void splitk_reduce_f32_kernel(const float* __restrict__ part, int S, long n4, int N,
                                                                 const float* __restrict__ bias,
                                                                 const float* __restrict__ add, long add_ld,
@@ -448,12 +497,24 @@ __global__ __launch_bounds__(256) void splitk_reduce_f32_kernel(const float* __r
   const long total = n4 * 4;
   for (long i = blockIdx.x * 256L + threadIdx.x; i < n4; i += (long)gridDim.x * 256) {
     float acc[4];
-    load4(part + i * 4, acc);
-    for (int s = 1; s < S; ++s) {
-      float v[4];
-      load4(part + (long)s * total + i * 4, v);
+    if constexpr (SC > 0) {
+      float v[SC][4];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) acc[j] += v[j];
+      for (int s = 0; s < SC; ++s) load4(part + (long)s * total + i * 4, v[s]);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[j] = v[0][j];
+#pragma unroll
+      for (int s = 1; s < SC; ++s)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[j] += v[s][j];
+    } else {
+      load4(part + i * 4, acc);
+      for (int s = 1; s < S; ++s) {
+        float v[4];
+        load4(part + (long)s * total + i * 4, v);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[j] += v[j];
+      }
     }
     const long m = (i * 4) / N, n = (i * 4) - m * N;
     if (bias) {
@@ -479,7 +540,14 @@ int jm_splitk_reduce_f32(const float* part, int S, int M, int N, const float* bi
   const long n = (long)M * N;
   long blocks = (n / 4 + 255) / 256;
   if (blocks > 8192) blocks = 8192;
-  splitk_reduce_f32_kernel<<<(int)blocks, 256, 0, st>>>(part, S, n / 4, N, bias, add, add_ld, out);
+#define JM_SKF(SS) \
+  case SS: splitk_reduce_f32_kernel<SS><<<(int)blocks, 256, 0, st>>>(part, S, n / 4, N, bias, add, add_ld, out); break;
+  switch (S) {
+    JM_SKF(2) JM_SKF(3) JM_SKF(4) JM_SKF(5) JM_SKF(6) JM_SKF(7) JM_SKF(8) JM_SKF(9) JM_SKF(10) JM_SKF(11)
+    JM_SKF(12) JM_SKF(13) JM_SKF(14) JM_SKF(15) JM_SKF(16)
+    default: splitk_reduce_f32_kernel<0><<<(int)blocks, 256, 0, st>>>(part, S, n / 4, N, bias, add, add_ld, out);
+  }
+#undef JM_SKF
   return 0;
 }
 
@@ -487,7 +555,14 @@ int jm_splitk_reduce_bf16(const float* part, int S, long n, int N, const float* 
   if (n % 8 || N % 8) return -1;
   long blocks = (n / 8 + 255) / 256;
   if (blocks > 8192) blocks = 8192;
-  splitk_reduce_bf16_kernel<<<(int)blocks, 256, 0, st>>>(part, S, n / 8, N, bias, out);
+#define JM_SKB(SS) \
+  case SS: splitk_reduce_bf16_kernel<SS><<<(int)blocks, 256, 0, st>>>(part, S, n / 8, N, bias, out); break;
+  switch (S) {
+    JM_SKB(2) JM_SKB(3) JM_SKB(4) JM_SKB(5) JM_SKB(6) JM_SKB(7) JM_SKB(8) JM_SKB(9) JM_SKB(10) JM_SKB(11)
+    JM_SKB(12) JM_SKB(13) JM_SKB(14) JM_SKB(15) JM_SKB(16)
+    default: splitk_reduce_bf16_kernel<0><<<(int)blocks, 256, 0, st>>>(part, S, n / 8, N, bias, out);
+  }
+#undef JM_SKB
   return 0;
 }
 
