@@ -558,9 +558,9 @@ JM_DEVICE int swo(int row, int col) {
   return row * (NCH * 8) + ((((col >> 3) ^ aswz(row)) & (NCH - 1)) << 3) + (col & 7);
 }
 
-template <int HD, int SP>
+template <int HD, int SP, int QC = 64>
 constexpr size_t bwd2_smem() {
-  return (size_t)(3 * SP * HD + SP * 64) * 2 + (2 * SP + 3 * HD) * sizeof(float);
+  return (size_t)(3 * SP * HD + SP * QC) * 2 + (2 * SP + 3 * HD) * sizeof(float);
 }
 
 
@@ -868,15 +868,20 @@ __global__ __launch_bounds__(256) void attn_bwd2_kernel(const uint16_t* __restri
 //    VALU of all four 16-query slices, then the 8 dV / dK MFMAs;
 //  * masks padded keys through the MFMA accumulator init (-1e30 for keys >= S) instead of a
 //    multiply per score.
-template <int HD, int SP>
-__global__ __launch_bounds__(256) void attn_bwd3_kernel(const uint16_t* __restrict__ qkv,
+// NWV waves per workgroup: 4 (the default), or 8 for hd 64 at long S, where the 4-wave form needs
+// more than 256 VGPRs (one wave per SIMD): 8 waves own half the key tiles each (half the dK / dV
+// accumulators) and sweep 128-query chunks (one 16-query dQ tile per wave), two waves per SIMD.
+template <int HD, int SP, int NWV = 4>
+__global__ __launch_bounds__(64 * NWV) void attn_bwd3_kernel(const uint16_t* __restrict__ qkv,
                                                         const uint16_t* __restrict__ o,
                                                         const uint16_t* __restrict__ dO,
                                                         const float* __restrict__ lse,
                                                         uint16_t* __restrict__ dqkv, int S, int H, float scale,
                                                         float* __restrict__ dbp, int remap) {
-  JM_DGUARD(S >= 1 && S <= SP && blockDim.x == 256);
-  constexpr int NW = 4, NTH = 256, QC = 64;
+  JM_DGUARD(S >= 1 && S <= SP && blockDim.x == 64 * NWV);
+  constexpr int NW = NWV, NTH = 64 * NWV, QC = 16 * NWV;
+  constexpr int QB = QC / 32;   // 32-query blocks per chunk
+  constexpr int DCH = QC / 8;   // 16-byte chunks per dS^T row
   constexpr int NT = SP / 16, KK = HD / 32, DT = HD / 16;
   constexpr int NKW = (NT + NW - 1) / NW;
   constexpr int NCH = HD / 8;
@@ -979,12 +984,12 @@ __global__ __launch_bounds__(256) void attn_bwd3_kernel(const uint16_t* __restri
   }
   int o_dsw[QC / 16];
 #pragma unroll
-  for (int j = 0; j < QC / 16; ++j) o_dsw[j] = swo<8>(l16, 16 * j + 4 * g);
+  for (int j = 0; j < QC / 16; ++j) o_dsw[j] = swo<DCH>(l16, 16 * j + 4 * g);
   const int krow = 8 * g + (l16 >> 2);
   int o_dsr[2], o_kt[DT][2];
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
-    o_dsr[u] = swo<8>(krow + 4 * u, wave * 16 + 4 * (l16 & 3));
+    o_dsr[u] = swo<DCH>(krow + 4 * u, wave * 16 + 4 * (l16 & 3));
 #pragma unroll
     for (int dt = 0; dt < DT; ++dt) o_kt[dt][u] = swo<NCH>(krow + 4 * u, dt * 16 + 4 * (l16 & 3));
   }
@@ -1004,9 +1009,10 @@ __global__ __launch_bounds__(256) void attn_bwd3_kernel(const uint16_t* __restri
 
   for (int qc = 0; qc * QC < SP; ++qc) {
     const int q0 = qc * QC;
-    const int nr = (SP - q0) >= QC ? 2 : 1;  // 32-query blocks in this chunk (SP % 32 == 0)
-#pragma unroll
-    for (int r = 0; r < 2; ++r) {
+    const int nr = (SP - q0) >= QC ? QB : (SP - q0) / 32;  // 32-query blocks in this chunk (SP % 32 == 0)
+    // (not unrolled at 8 waves: the 4-block chunk would keep every block's fragments live)
+#pragma unroll(NWV == 4 ? QB : 1)
+    for (int r = 0; r < QB; ++r) {
       if (r < nr) {
         // ---- key-tile independent fragments of this 32-query block
         const int qb = q0 + 32 * r;
@@ -1058,7 +1064,7 @@ __global__ __launch_bounds__(256) void attn_bwd3_kernel(const uint16_t* __restri
               uint2 pk;
               pk.x = pack_bf2(df[4 * hh], df[4 * hh + 1]);
               pk.y = pack_bf2(df[4 * hh + 2], df[4 * hh + 3]);
-              *reinterpret_cast<uint2*>(dsw + o_dsw[2 * r + hh]) = pk;
+              *reinterpret_cast<uint2*>(dsw + (NWV == 4 ? o_dsw[2 * r + hh] : swo<DCH>(l16, 16 * (2 * r + hh) + 4 * g))) = pk;
             }
             const bf16x8_t pb = pack8(pf);
             const bf16x8_t dsb = pack8(df);
@@ -1189,6 +1195,7 @@ int run_fwd(const uint16_t* qkv, uint16_t* out, float* lse_out, int B, int S, in
 int g_bwd_ppw = 0;
 // runtime switch: the batched backward (bwd3) also for head dim 64 at S > 64 (finetune S = 199);
 // 2: also at S <= 64 (the encoder, A/B)
+int g_bwd3_nw8 = 1;  // runtime switch: hd 64, S > 64 backward on the 8-wave bwd3
 int g_bwd3_hd64 = 1;  // finetune S=199 hd=64 backward 249 -> 177 us (profiles/r2_attn_ft_bwd.txt)
 // the backward that jm_attn_bwd runs is the batched bwd3 kernel (B dbias partial rows) -- the
 // single source of that choice for run_bwd2 and jm_attn_bwd_part_rows
@@ -1221,6 +1228,21 @@ int run_bwd2(const uint16_t* qkv, const uint16_t* o, const uint16_t* dO, const f
       (void)hipFuncSetAttribute((const void*)attn_bwd3_kernel<HD, SP>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)sm);
       attr3 = true;
+    }
+    if constexpr (HD == 64 && SP > 64) {
+      if (g_bwd3_nw8) {  // 8 waves: 2 / SIMD instead of 1 (the 4-wave form needs > 256 VGPRs here)
+        constexpr size_t sm8 = bwd2_smem<HD, SP, 128>();
+        static_assert(sm8 <= 160 * 1024, "8-wave backward LDS");
+        static bool attr8 = false;
+        if (!attr8) {
+          (void)hipFuncSetAttribute((const void*)attn_bwd3_kernel<HD, SP, 8>,
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm8);
+          attr8 = true;
+        }
+        attn_bwd3_kernel<HD, SP, 8><<<dim3(B * H), 512, sm8, st>>>(qkv, o, dO, lse_in, out, S, H, scale,
+                                                                   dbias_part, g_attn_remap);
+        return 0;
+      }
     }
     attn_bwd3_kernel<HD, SP><<<dim3(B * H), 256, sm, st>>>(qkv, o, dO, lse_in, out, S, H, scale, dbias_part,
                                                            g_attn_remap);
@@ -1651,6 +1673,7 @@ void jm_attn_set_remap(int v) { g_attn_remap = v; }
 void jm_attn_set_fwd_hpw(int v) { g_fwd_hpw = v < 0 ? 0 : v; }
 void jm_attn_set_bwd_ppw(int v) { g_bwd_ppw = v < 0 ? 0 : v; }
 void jm_attn_set_bwd3_hd64(int v) { g_bwd3_hd64 = v; }
+void jm_attn_set_bwd3_nw8(int v) { g_bwd3_nw8 = v; }
 
 // rows of the dbias_part workspace that jm_attn_bwd writes: the bwd2 kernel folds ``ppw`` batch
 // elements into one row, every other backward writes one row per batch element.  Must mirror the

@@ -58,6 +58,7 @@ void jm_attn_set_remap(int v);
 void jm_attn_set_fwd_hpw(int v);
 void jm_attn_set_bwd_ppw(int v);
 void jm_attn_set_bwd3_hd64(int v);
+void jm_attn_set_bwd3_nw8(int v);
 int jm_attn_bwd_part_rows(int B, int S, int hd);
 int jm_attn_bwd_long(const uint16_t* qkv, const uint16_t* o, const uint16_t* dO, const float* lse, uint16_t* dqkv,
                      float* delta, int B, int S, int H, int hd, hipStream_t st);
@@ -947,6 +948,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("attn_set_fwd_hpw", &jm_attn_set_fwd_hpw);
   m.def("attn_set_bwd_ppw", &jm_attn_set_bwd_ppw);
   m.def("attn_set_bwd3_hd64", &jm_attn_set_bwd3_hd64);
+  m.def("attn_set_bwd3_nw8", &jm_attn_set_bwd3_nw8);
   m.def("opt_sumsq", &opt_sumsq);
   m.def("opt_adamw", &opt_adamw);
   m.def("opt_set_adamw_vec", &jm_opt_set_adamw_vec);

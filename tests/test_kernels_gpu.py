@@ -20,6 +20,7 @@ def _reset_gemm_variant(request):
     if "ext" in request.fixturenames:
         request.getfixturevalue("ext").gemm_set_variant(0, 8)
         request.getfixturevalue("ext").attn_set_bwd_ppw(0)
+        request.getfixturevalue("ext").attn_set_bwd3_nw8(1)
         request.getfixturevalue("ext").gemm_set_tail(1)
         request.getfixturevalue("ext").gemm_set_narrow(4096)
 
@@ -115,13 +116,14 @@ def _attn_ref(qkv, H):
 
 
 @pytest.mark.parametrize("tr,hpw,ppw", [(3, 0, 0), (3, 1, 0), (2, 1, 0), (3, 3, 0), (3, 4, 0),
-                                        (3, 0, 1), (3, 0, 2), (2, 0, 3), (3, 0, 8)])
+                                        (3, 0, 1), (3, 0, 2), (2, 0, 3), (3, 0, 8), (3, 0, -1)])
 @pytest.mark.parametrize("B,S,H,hd", [(3, 52, 16, 64), (2, 199, 16, 32), (2, 17, 4, 32), (2, 100, 3, 64),
                                       (2, 199, 4, 64)])
 def test_attention(ext, B, S, H, hd, tr, hpw, ppw):
     ext.attn_set_tr(tr)
     ext.attn_set_fwd_hpw(hpw)
-    ext.attn_set_bwd_ppw(ppw)
+    ext.attn_set_bwd_ppw(max(ppw, 0))
+    ext.attn_set_bwd3_nw8(0 if ppw < 0 else 1)  # ppw -1: the 4-wave batched backward at hd 64
     torch.manual_seed(0)
     D = H * hd
     qkv = (torch.randn(B, S, 3 * D, device="cuda") * 1.5).bfloat16()

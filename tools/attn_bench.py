@@ -28,6 +28,7 @@ def main():
     ap.add_argument("--remap", default="", help="comma list of attn_set_remap values to A/B (interleaved)")
     ap.add_argument("--max-seq", type=int, default=0, help="attn_set_max_seq (longer S -> tile-streamed kernels)")
     ap.add_argument("--bwd3-hd64", type=int, default=-1, help="attn_set_bwd3_hd64 (batched backward at hd 64)")
+    ap.add_argument("--nw8", type=int, default=-1, help="attn_set_bwd3_nw8 (8-wave backward at hd 64, S > 64)")
     a = ap.parse_args()
     ext = _ext.load()
     remaps = [int(v) for v in a.remap.split(",")] if a.remap else [None]
@@ -41,6 +42,8 @@ def main():
         ext.attn_set_max_seq(a.max_seq)
     if a.bwd3_hd64 >= 0:
         ext.attn_set_bwd3_hd64(a.bwd3_hd64)
+    if a.nw8 >= 0:
+        ext.attn_set_bwd3_nw8(a.nw8)
     for name in a.shapes.split(","):
         B, S, H, hd = SHAPES[name]
         D = H * hd
