@@ -83,9 +83,10 @@ int jm_gemm_nt(const uint16_t* A, long lda, const uint16_t* B, long ldb, int M, 
 void jm_gemm_set_variant(int wn, int group);
 void jm_gemm_set_tail(int on);
 void jm_gemm_set_narrow(int max_m);
-int jm_gemm_nt_tiles(int M, int N);
-int jm_gemm_nt_colpart_rows(int M, int N);
-int jm_gemm_nt_tail_plan(int M, int N, int K, int epi, int* tail_r, long* ws_floats);
+int jm_gemm_nt_tiles(int M, int N, int K, int epi, long lda);
+int jm_gemm_nt_colpart_rows(int M, int N, int K, int epi, long lda);
+int jm_gemm_nt_tail_plan(int M, int N, int K, int epi, long lda, int* tail_r, long* ws_floats);
+void jm_gemm_set_rows(int rows);
 int jm_gemm_tn_plan(int M, int N, int K, int* S_out);
 int jm_gemm_tn(const uint16_t* A, long lda, const uint16_t* B, long ldb, int M, int N, int K, int sps, int S,
                float* G, long ldo, float* partial, hipStream_t st);
@@ -584,7 +585,7 @@ torch::Tensor patch_mse_bwd(torch::Tensor pred, torch::Tensor img, torch::Tensor
 int attach_tail(GemmEpi& ep, torch::Tensor& ws, int M, int N, int K, int epi, const torch::Tensor& like) {
   int r = 0;
   long n = 0;
-  const int S = jm_gemm_nt_tail_plan(M, N, K, epi, &r, &n);
+  const int S = jm_gemm_nt_tail_plan(M, N, K, epi, like.stride(0), &r, &n);
   if (S < 2) return 0;
   ws = torch::empty({n}, like.options().dtype(torch::kFloat32));
   ep.tail = ws.data_ptr<float>();
@@ -688,7 +689,7 @@ torch::Tensor gemm_nt_dgelu(torch::Tensor A, torch::Tensor B, torch::Tensor pre,
   torch::Tensor ws;
   const int epi = deriv ? 7 : 2;
   const int r = attach_tail(ep, ws, M, N, K, epi, A);
-  int nM = jm_gemm_nt_colpart_rows(M, N);
+  int nM = jm_gemm_nt_colpart_rows(M, N, K, epi, A.stride(0));
   if (dbias) {
     TORCH_CHECK(dbias->is_contiguous() && dbias->scalar_type() == torch::kFloat32 && dbias->numel() == N,
                 "gemm_nt_dgelu dbias");
@@ -933,7 +934,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "nt64 = 1: every NT launch on the 64-deep main loop (tests); group: row tiles per column sweep");
   m.def("gemm_set_tail", &jm_gemm_set_tail);
   m.def("gemm_set_narrow", &jm_gemm_set_narrow, "M below which NT GEMMs take the 128 x 192 narrow tiles (0 = never)");
-  m.def("gemm_nt_tiles", &jm_gemm_nt_tiles, "output tiles (workgroups before split-K) of an NT launch");
+  m.def("gemm_nt_tiles", &jm_gemm_nt_tiles, py::arg("M"), py::arg("N"), py::arg("K") = 1024, py::arg("epi") = 0,
+        py::arg("lda") = 0, "output tiles (workgroups before split-K) of an NT launch");
+  m.def("gemm_set_rows", &jm_gemm_set_rows,
+        "4-phase tile height: 0 = automatic (wave fill), 256 / 224 / 192 = forced (A/B, tests)");
   m.def("transpose_bf16_batch", &transpose_bf16_batch);
   m.def("ln_set_bwd_blocks", &jm_ln_set_bwd_blocks);
   m.def("gemm_nt_splitk", &gemm_nt_splitk, py::arg("A"), py::arg("B"), py::arg("bias") = py::none(),

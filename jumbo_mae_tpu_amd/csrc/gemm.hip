@@ -77,8 +77,8 @@ enum { EPI_STORE = 0, EPI_GELU = 1, EPI_DGELU = 2, EPI_PARTIAL = 3, EPI_GELU_ONL
 
 namespace {
 
-// acc[mt][nt][i] = C[mb + mt*16 + l16][nb + nt*16 + 4g + i]
-template <int EPI, int NTW>
+// acc[mt][nt][i] = C[mb + mt*16 + l16][nb + nt*16 + 4g + i]  (mt < MTW)
+template <int EPI, int NTW, int MTW = 8>
 JM_DEVICE void epilogue(const f32x4_t (&acc)[8][NTW], const GemmEpi& ep, int M, int N, int mb, int nb, int l16,
                         int g) {
 #pragma unroll
@@ -88,7 +88,7 @@ JM_DEVICE void epilogue(const f32x4_t (&acc)[8][NTW], const GemmEpi& ep, int M, 
     float bv[4] = {0.f, 0.f, 0.f, 0.f};
     if (ep.bias) load4(ep.bias + n, bv);
 #pragma unroll
-    for (int mt = 0; mt < 8; ++mt) {
+    for (int mt = 0; mt < MTW; ++mt) {
       const int m = mb + mt * 16 + l16;
       if (m >= M) continue;
       float v[4];
@@ -117,9 +117,10 @@ JM_DEVICE void epilogue(const f32x4_t (&acc)[8][NTW], const GemmEpi& ep, int M, 
   }
 }
 
-template <int BNT = BN>
+// TR = tile rows (256, or 224 / 192 for the short-row p4 launches, see tile_rows)
+template <int BNT = BN, int TR = BM>
 JM_DEVICE void tile_of(int M, int N, int GROUP_M, int& m0, int& n0, int splits = 1, int* split = nullptr) {
-  const int nM = (M + BM - 1) / BM, nN = (N + BNT - 1) / BNT;
+  const int nM = (M + TR - 1) / TR, nN = (N + BNT - 1) / BNT;
   const int nwg = nM * nN * splits;
   const int orig = blockIdx.x;
   const int xcd = orig & 7, q = nwg >> 3, r = nwg & 7;
@@ -131,7 +132,7 @@ JM_DEVICE void tile_of(int M, int N, int GROUP_M, int& m0, int& n0, int splits =
   const int per_group = GROUP_M * nN;
   const int first_m = (wg / per_group) * GROUP_M;
   const int gsz = min(nM - first_m, GROUP_M);
-  m0 = (first_m + (wg % per_group) % gsz) * BM;
+  m0 = (first_m + (wg % per_group) % gsz) * TR;
   n0 = ((wg % per_group) / gsz) * BNT;
 }
 
@@ -183,10 +184,11 @@ JM_DEVICE uint4 pack8(const float* f) {
   return v;
 }
 
-template <int EPI, int NTW, int NTH, int BNT = BN, bool NTS = false>
+template <int EPI, int NTW, int NTH, int BNT = BN, bool NTS = false, int TR = BM>
 JM_DEVICE void epilogue_lds(const f32x4_t (&acc)[8][NTW], const GemmEpi& ep, uint16_t* cs, int M, int N, int m0,
                             int n0, int wr, int wc, int l16, int g) {
   constexpr int RB = BNT;  // elements per LDS image row
+  constexpr int HR = TR / 2, MTW = HR / 16;  // rows and 16-row MFMA tiles per wave row
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
   constexpr int LPR = BNT / 8;        // lanes per row (16 B each)
   constexpr int RPP = NTH / LPR;      // rows per pass
@@ -198,7 +200,7 @@ JM_DEVICE void epilogue_lds(const f32x4_t (&acc)[8][NTW], const GemmEpi& ep, uin
   // are staged through LDS (their latency hides behind the staging) and each row pass then issues
   // the load PF passes ahead -- a register ring instead of one exposed load per pass
   constexpr bool PRE = EPI == EPI_DGELU || EPI == EPI_DMUL;
-  constexpr int NPASS = PRE ? BM / RPP : 1;
+  constexpr int NPASS = PRE ? TR / RPP : 1;
   constexpr int PF = NPASS < 8 ? NPASS : 8;
   uint4 auxv[PF];
   auto aux_load = [&](int i) {
@@ -217,8 +219,8 @@ JM_DEVICE void epilogue_lds(const f32x4_t (&acc)[8][NTW], const GemmEpi& ep, uin
     float bv[4] = {0.f, 0.f, 0.f, 0.f};
     if (ep.bias && n0 + nl < N) load4(ep.bias + n0 + nl, bv);
 #pragma unroll
-    for (int mt = 0; mt < 8; ++mt) {
-      const int r = wr * 128 + mt * 16 + l16;
+    for (int mt = 0; mt < MTW; ++mt) {
+      const int r = wr * HR + mt * 16 + l16;
       uint2 pk;
       pk.x = pack_bf2(acc[mt][nt][0] + bv[0], acc[mt][nt][1] + bv[1]);
       pk.y = pack_bf2(acc[mt][nt][2] + bv[2], acc[mt][nt][3] + bv[3]);
@@ -282,7 +284,7 @@ JM_DEVICE void epilogue_lds(const f32x4_t (&acc)[8][NTW], const GemmEpi& ep, uin
     }
   } else {
 #pragma unroll 4
-    for (int r = tid / LPR; r < BM; r += RPP) pass(r, auxv[0]);
+    for (int r = tid / LPR; r < TR; r += RPP) pass(r, auxv[0]);
   }
   if ((EPI == EPI_DGELU || EPI == EPI_DMUL) && ep.colpart != nullptr) {
     // column sums of this row tile: RPP threads share a column chunk -> reduce through LDS
@@ -296,7 +298,7 @@ JM_DEVICE void epilogue_lds(const f32x4_t (&acc)[8][NTW], const GemmEpi& ep, uin
       float acc = 0.f;
 #pragma unroll
       for (int q = 0; q < RPP; ++q) acc += red[(cc + q * LPR) * 8 + j];
-      if (n0 + col < N) ep.colpart[(long)(m0 / BM) * N + n0 + col] = acc;
+      if (n0 + col < N) ep.colpart[(long)(m0 / TR) * N + n0 + col] = acc;
     }
   }
 }
@@ -501,9 +503,15 @@ __global__ __launch_bounds__(512, 1) void gemm_nt64_kernel(const uint16_t* __res
 // and on the ds_read address (conflict-free ds_read_b128, the nt64 image).
 // Waves 4-7 (the younger half, SIMD partners of waves 0-3) run at priority 1 throughout (static
 // young-half priority, MI355X_MICROARCH.md "Two waves per SIMD" item 4; profiles/r2_gemm_p4.txt).
-// acc = A[m0:m0+256, k_begin:k_begin+K] . B[n0:n0+256, same]^T  (K % 128 == 0, K > 0); every LDS
+// acc = A[m0:m0+TR, k_begin:k_begin+K] . B[n0:n0+256, same]^T  (K % 128 == 0, K > 0); every LDS
 // slot is free on entry (caller's barrier) and the ring is drained on exit except for the reads
 // of the last K-tile's MFMAs (caller's epilogue barriers before reusing LDS).
+// Short-row tiles (MTL < 4: TR = 128 + 32 * MTL = 224 / 192 rows) keep the slot layout and the
+// counted-vmcnt schedule unchanged: each wave row owns 64 + 16 * MTL rows, the a1 slot's unused
+// rows are loaded from an out-of-range buffer offset (no memory traffic) and never read, and the
+// lower-half phases q3 / q4 run MTL instead of 4 row MFMA tiles.  They exist for wave fill
+// (tile_rows): e.g. M = 25088, N = 4096 is 6.1 waves of 256-row tiles but exactly 7 of 224.
+template <int MTL>
 __attribute__((always_inline)) JM_DEVICE void p4_mainloop(const uint16_t* __restrict__ A, long lda,
                                                           const uint16_t* __restrict__ B, long ldb, int M, int N,
                                                           int m0, int n0, int k_begin, int K,
@@ -515,6 +523,7 @@ __attribute__((always_inline)) JM_DEVICE void p4_mainloop(const uint16_t* __rest
   constexpr int NTW = 2 * NTQ;        // per wave (4)
   constexpr int P = 2;                // glds pieces per wave and slot
   constexpr int BK2 = 64, SLOT = 128 * BK2;  // elements per slot (16 KB)
+  constexpr int HR = 64 + 16 * MTL;   // tile rows per wave row
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
   const int l16 = lane & 15, g = lane >> 4;
@@ -529,9 +538,10 @@ __attribute__((always_inline)) JM_DEVICE void p4_mainloop(const uint16_t* __rest
     const int c = (lane & 7) ^ swz64(srow);
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-      const int arow = (srow >> 6) * 128 + h * 64 + (srow & 63);
+      const int arow = (srow >> 6) * HR + h * 64 + (srow & 63);
       const int bcol = (srow / QC) * (2 * QC) + h * QC + (srow % QC);
-      a_src[h][r] = (uint32_t)((arow * lda + c * 8) * 2);
+      const bool aok = h == 0 || (srow & 63) < 16 * MTL;  // host: A bytes < 2^31 (offset out of range)
+      a_src[h][r] = aok ? (uint32_t)((arow * lda + c * 8) * 2) : 0x80000000u;
       b_src[h][r] = (uint32_t)((bcol * ldb + c * 8) * 2);
     }
   }
@@ -551,9 +561,10 @@ __attribute__((always_inline)) JM_DEVICE void p4_mainloop(const uint16_t* __rest
   typedef bf16x8_t AF[4][2];    // [mt within the half][k32 step]
   typedef bf16x8_t BF[NTQ][2];  // [nt within the half][k32 step]
   auto read_a = [&](int t, auto half, AF& f) {
+    constexpr int NMT = decltype(half)::value ? MTL : 4;
     const uint16_t* base = smem + ((t & 1) * 4 + decltype(half)::value) * SLOT + a_row;
 #pragma unroll
-    for (int mt = 0; mt < 4; ++mt) {
+    for (int mt = 0; mt < NMT; ++mt) {
       f[mt][0] = lds8(base + mt * 16 * BK2 + ch0);
       f[mt][1] = lds8(base + mt * 16 * BK2 + ch1);
     }
@@ -572,10 +583,11 @@ __attribute__((always_inline)) JM_DEVICE void p4_mainloop(const uint16_t* __rest
     for (int j = 0; j < NTW; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
   auto mfma_q = [&](auto mh, auto nh, const AF& a, const BF& b) {
     constexpr int MH = decltype(mh)::value, NH = decltype(nh)::value;
+    constexpr int NMT = MH ? MTL : 4;
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
-      for (int mt = 0; mt < 4; ++mt)
+      for (int mt = 0; mt < NMT; ++mt)
 #pragma unroll
         for (int nt = 0; nt < NTQ; ++nt)
           acc[MH * 4 + mt][NH * NTQ + nt] = mfma16(b[nt][kk], a[mt][kk], acc[MH * 4 + mt][NH * NTQ + nt]);
@@ -588,8 +600,8 @@ __attribute__((always_inline)) JM_DEVICE void p4_mainloop(const uint16_t* __rest
     __builtin_amdgcn_sched_barrier(0);
   };
   // the phase's instruction order: its NR ds_reads spread evenly over its NM MFMAs
-  auto interleave = [&](auto nreads) {
-    constexpr int NM = 8 * NTQ;
+  auto interleave = [&](auto nreads, auto mh) {
+    constexpr int NM = (decltype(mh)::value ? MTL : 4) * 2 * NTQ;
     constexpr int NR = decltype(nreads)::value;
     constexpr int PER = NR >= NM ? 1 : NM / (NR > 0 ? NR : 1);
 #pragma unroll
@@ -609,6 +621,7 @@ __attribute__((always_inline)) JM_DEVICE void p4_mainloop(const uint16_t* __rest
   using IN = std::integral_constant<int, -1>;
   using RB = std::integral_constant<int, 2 * NTQ>;      // fragment reads of a B half
   using RQ4 = std::integral_constant<int, 8 + 2 * NTQ>;  // q4: a0 + b0 of the next tile
+  using RA1 = std::integral_constant<int, 2 * MTL>;      // q2: a1
 
   AF ax, ay;
   BF bp, bq;
@@ -623,18 +636,18 @@ __attribute__((always_inline)) JM_DEVICE void p4_mainloop(const uint16_t* __rest
     if constexpr (KIND == 2) issue(t + 2, I0{});
     read_b(t, I1{}, b1);
     mfma_q(I0{}, I0{}, ax, b0);
-    interleave(RB{});
+    interleave(RB{}, I0{});
     // q2 (0,1): read a1(t)
     sync(std::conditional_t<KIND == 0, I1, std::conditional_t<KIND == 1, I5, I6>>{});
     if constexpr (KIND == 2) issue(t + 2, I3{});
     read_a(t, I1{}, ay);
     mfma_q(I0{}, I1{}, ax, b1);
-    interleave(I8{});
+    interleave(RA1{}, I0{});
     // q3 (1,1): no reads
     sync(IN{});
     if constexpr (KIND == 2) issue(t + 2, I1{});
     mfma_q(I1{}, I1{}, ay, b1);
-    interleave(I0{});
+    interleave(I0{}, I1{});
     // q4 (1,0): read a0(t+1), b0(t+1) (into b1, free after q3)
     if constexpr (KIND > 0) {
       sync(std::conditional_t<KIND == 1, I0, I3>{});
@@ -642,7 +655,7 @@ __attribute__((always_inline)) JM_DEVICE void p4_mainloop(const uint16_t* __rest
       read_a(t + 1, I0{}, ax);
       read_b(t + 1, I0{}, b1);
       mfma_q(I1{}, I0{}, ay, b0);
-      interleave(RQ4{});
+      interleave(RQ4{}, I1{});
       } else {
       mfma_q(I1{}, I0{}, ay, b0);
       __builtin_amdgcn_sched_barrier(0);
@@ -677,10 +690,11 @@ __attribute__((always_inline)) JM_DEVICE void p4_mainloop(const uint16_t* __rest
 }
 
 // the 256 x 256 tile's epilogue from the p4 accumulators (EPI_PARTIAL: fp32 split slice)
-template <int EPI>
+template <int EPI, int MTL>
 __attribute__((always_inline)) JM_DEVICE void p4_epilogue(const f32x4_t (&acc)[8][4], const GemmEpi& ep, int M,
                                                           int N, int m0, int n0, int split, uint16_t* smem) {
   constexpr int NTW = 4, WN = 4;
+  constexpr int HR = 64 + 16 * MTL, MTW = 4 + MTL;
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
   const int l16 = lane & 15, g = lane >> 4;
@@ -688,8 +702,8 @@ __attribute__((always_inline)) JM_DEVICE void p4_epilogue(const f32x4_t (&acc)[8
   if (EPI == EPI_PARTIAL) {
     float* dst = ep.part + (long)split * M * N;
 #pragma unroll
-    for (int mt = 0; mt < 8; ++mt) {
-      const int m = m0 + wr * 128 + mt * 16 + l16;
+    for (int mt = 0; mt < MTW; ++mt) {
+      const int m = m0 + wr * HR + mt * 16 + l16;
       if (m >= M) continue;
 #pragma unroll
       for (int nt = 0; nt < NTW; ++nt) {
@@ -700,12 +714,12 @@ __attribute__((always_inline)) JM_DEVICE void p4_epilogue(const f32x4_t (&acc)[8
       }
     }
   } else if (N % 8 == 0)
-    epilogue_lds<EPI, NTW, 512, BN, true>(acc, ep, smem, M, N, m0, n0, wr, wc, l16, g);
+    epilogue_lds<EPI, NTW, 512, BN, true, 2 * HR>(acc, ep, smem, M, N, m0, n0, wr, wc, l16, g);
   else
-    epilogue<EPI, NTW>(acc, ep, M, N, m0 + wr * 128, n0 + wc * NTW * 16, l16, g);
+    epilogue<EPI, NTW, MTW>(acc, ep, M, N, m0 + wr * HR, n0 + wc * NTW * 16, l16, g);
 }
 
-template <int EPI>
+template <int EPI, int MTL = 4>
 __global__ __launch_bounds__(512, 1) void gemm_p4_kernel(const uint16_t* __restrict__ A, long lda,
                                                          const uint16_t* __restrict__ B, long ldb, int M, int N,
                                                          int K, GemmEpi ep, int GROUP_M) {
@@ -717,7 +731,8 @@ __global__ __launch_bounds__(512, 1) void gemm_p4_kernel(const uint16_t* __restr
     int tg;
     tile_of_range(M, N, GROUP_M, ep.t_begin, ep.t_count, 1, m0, n0, split, tg);
   } else {
-    tile_of(M, N, GROUP_M, m0, n0, EPI == EPI_PARTIAL ? ep.splits : 1, EPI == EPI_PARTIAL ? &split : nullptr);
+    tile_of<BN, 128 + 32 * MTL>(M, N, GROUP_M, m0, n0, EPI == EPI_PARTIAL ? ep.splits : 1,
+                                EPI == EPI_PARTIAL ? &split : nullptr);
   }
   int k_begin = 0;
   if (EPI == EPI_PARTIAL) {
@@ -727,8 +742,8 @@ __global__ __launch_bounds__(512, 1) void gemm_p4_kernel(const uint16_t* __restr
     K = (ku1 - ku0) * 128;
   }
   f32x4_t acc[8][4];
-  p4_mainloop(A, lda, B, ldb, M, N, m0, n0, k_begin, K, acc, smem);
-  p4_epilogue<EPI>(acc, ep, M, N, m0, n0, split, smem);
+  p4_mainloop<MTL>(A, lda, B, ldb, M, N, m0, n0, k_begin, K, acc, smem);
+  p4_epilogue<EPI, MTL>(acc, ep, M, N, m0, n0, split, smem);
 }
 
 // ------------------------------------------------------------------ narrow tiles (M < 4096)
@@ -1070,16 +1085,16 @@ void launch_nt64(const uint16_t* A, long lda, const uint16_t* B, long ldb, int M
   gemm_nt64_kernel<EPI, NTS><<<nwg, 512, GEMM_SMEM, st>>>(A, lda, B, ldb, M, N, K, ep, g_gemm_group);
 }
 
-template <int EPI>
+template <int EPI, int MTL>
 void launch_p4(const uint16_t* A, long lda, const uint16_t* B, long ldb, int M, int N, int K, const GemmEpi& ep,
                int nwg, hipStream_t st) {
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)gemm_p4_kernel<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    (void)hipFuncSetAttribute((const void*)gemm_p4_kernel<EPI, MTL>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)GEMM_SMEM);
     attr = true;
   }
-  gemm_p4_kernel<EPI><<<nwg, 512, GEMM_SMEM, st>>>(A, lda, B, ldb, M, N, K, ep, g_gemm_group);
+  gemm_p4_kernel<EPI, MTL><<<nwg, 512, GEMM_SMEM, st>>>(A, lda, B, ldb, M, N, K, ep, g_gemm_group);
 }
 
 template <int EPI>
@@ -1107,16 +1122,58 @@ bool narrow_launch(int M, int N, int epi, int splits) {
   return !(epi == EPI_PARTIAL && splits > 1 && M >= 256);
 }
 
-// narrow tiles for M < 4096; K in 128-deep units (split-K: per split) -> p4, else the 64-deep
-// kernel (nontemporal epilogue stores)
+bool p4_ok(int K, int epi, int splits) {
+  return !g_gemm_nt64 && K % 128 == 0 && (epi != EPI_PARTIAL || K / 128 >= splits);
+}
+
+int g_gemm_rows = 0;  // 0: tile_rows decides; 256 / 224 / 192 force the 4-phase tile height (A/B, tests)
+
+// Relative cost per tile row of the short-row 4-phase tiles vs 256 rows (the same B panel feeds
+// fewer MFMAs; measured per full wave, profiles/r3_gemm_tile_rows.txt)
+float rows_cost(int tr) { return tr == 256 ? 1.f : (tr == 224 ? 1.05f : 1.10f); }
+
+int tail_plan_256(int M, int N, int K, int epi, int* tail_r);
+
+// Tile height of a 4-phase launch: the candidate whose launch spans the fewest tile rows per CU,
+// waves x rows x rows_cost (a last wave that fills part of the chip costs a full wave; 256-row
+// launches may split a tail of at most a quarter wave instead, counted as 0.8 wave: the split
+// tail and its finish kernel lost to 224 / 192-row tiles on every measured shape).  Split-K,
+// tail-split and 64-deep launches and operands of >= 2 GB (the short tiles' unused a1 rows load
+// from offset 2^31, which must be out of range) keep 256.
+int tile_rows(int M, int N, int K, int epi, long lda) {
+  if (narrow(M, N) || !p4_ok(K, epi, 1) || epi == EPI_PARTIAL || epi == EPI_TAIL) return BM;
+  if ((long)M * lda * 2 >= (1L << 31) - (1L << 20)) return BM;
+  if (g_gemm_rows) return g_gemm_rows;
+  const int ncu = num_cus(), nN = (N + BN - 1) / BN;
+  int r = 0;
+  const int t256 = ((M + BM - 1) / BM) * nN;
+  float best_c = tail_plan_256(M, N, K, epi, &r) ? (t256 / ncu + 0.8f) * BM : (float)((t256 + ncu - 1) / ncu) * BM;
+  int best = BM;
+  for (int tr : {224, 192}) {
+    const int t = ((M + tr - 1) / tr) * nN;
+    const float c = (float)((t + ncu - 1) / ncu) * tr * rows_cost(tr);
+    if (c < best_c) best_c = c, best = tr;
+  }
+  return best;
+}
+
+// narrow tiles for M < 4096; K in 128-deep units (split-K: per split) -> p4 (256 / 224 / 192-row
+// tiles, tile_rows), else the 64-deep kernel (nontemporal epilogue stores)
 template <int EPI>
 void launch_epi(const uint16_t* A, long lda, const uint16_t* B, long ldb, int M, int N, int K, const GemmEpi& ep,
                 int nwg, hipStream_t st) {
   if constexpr (EPI != EPI_TAIL) {
     if (narrow_launch(M, N, EPI, ep.splits) && ep.t_count == 0) return launch_narrow<EPI>(A, lda, B, ldb, M, N, K, ep, st);
   }
-  if (!g_gemm_nt64 && K % 128 == 0 && (EPI != EPI_PARTIAL || K / 128 >= ep.splits))
-    return launch_p4<EPI>(A, lda, B, ldb, M, N, K, ep, nwg, st);
+  if (p4_ok(K, EPI, ep.splits)) {
+    const int tr = ep.t_count > 0 ? BM : tile_rows(M, N, K, EPI, lda);
+    if constexpr (EPI != EPI_PARTIAL && EPI != EPI_TAIL) {
+      const int nw = ((M + tr - 1) / tr) * ((N + BN - 1) / BN);
+      if (tr == 224) return launch_p4<EPI, 3>(A, lda, B, ldb, M, N, K, ep, nw, st);
+      if (tr == 192) return launch_p4<EPI, 2>(A, lda, B, ldb, M, N, K, ep, nw, st);
+    }
+    return launch_p4<EPI, 4>(A, lda, B, ldb, M, N, K, ep, nwg, st);
+  }
   return launch_nt64<EPI, true>(A, lda, B, ldb, M, N, K, ep, nwg, st);
 }
 
@@ -1148,22 +1205,29 @@ void jm_gemm_set_tail(int on) { g_gemm_tail = on; }
 
 void jm_gemm_set_narrow(int max_m) { g_narrow_max_m = max_m; }
 
-// output tiles of an NT launch (the narrow kernel's 128 x 192 or the 256 x 256 kernels)
-int jm_gemm_nt_tiles(int M, int N) {
+void jm_gemm_set_rows(int rows) { g_gemm_rows = (rows == 224 || rows == 192 || rows == 256) ? rows : 0; }
+
+// output tiles of an NT launch (the narrow kernel's 128 x 192 or the 4-phase 256 / 224 / 192 x 256)
+int jm_gemm_nt_tiles(int M, int N, int K, int epi, long lda) {
   if (narrow(M, N)) return ((M + NBM - 1) / NBM) * ((N + NBN - 1) / NBN);
-  return ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
+  const int tr = tile_rows(M, N, K, epi, lda);
+  return ((M + tr - 1) / tr) * ((N + BN - 1) / BN);
 }
 
 // rows of the EPI_DGELU / EPI_DMUL column-partial buffer (one per row tile, before tail rows)
-int jm_gemm_nt_colpart_rows(int M, int N) { return narrow(M, N) ? (M + NBM - 1) / NBM : (M + BM - 1) / BM; }
+int jm_gemm_nt_colpart_rows(int M, int N, int K, int epi, long lda) {
+  if (narrow(M, N)) return (M + NBM - 1) / NBM;
+  const int tr = tile_rows(M, N, K, epi, lda);
+  return (M + tr - 1) / tr;
+}
 
 // Tail split plan for an NT launch: the last wave of output tiles (tiles % CUs of them) fills only
 // part of the chip; when it is at most a quarter wave, those tiles run split-K S ways (compact fp32
 // partials, *ws_floats) and a finish kernel applies the epilogue.  Returns S (0 = no tail split);
 // *tail_r = number of tail tiles.
-int jm_gemm_nt_tail_plan(int M, int N, int K, int epi, int* tail_r, long* ws_floats) {
+namespace {
+int tail_plan_256(int M, int N, int K, int epi, int* tail_r) {
   *tail_r = 0;
-  *ws_floats = 0;
   if (!g_gemm_tail) return 0;
   if (!(epi == EPI_STORE || epi == EPI_GELU || epi == EPI_DGELU || epi == EPI_GELU_ONLY) || N % 8 || K % 128) return 0;
   if (narrow(M, N)) return 0;
@@ -1179,7 +1243,16 @@ int jm_gemm_nt_tail_plan(int M, int N, int K, int epi, int* tail_r, long* ws_flo
   if (S > 8) S = 8;
   if (S < 2) return 0;
   *tail_r = r;
-  *ws_floats = (long)S * r * BM * BN;
+  return S;
+}
+}  // namespace
+
+int jm_gemm_nt_tail_plan(int M, int N, int K, int epi, long lda, int* tail_r, long* ws_floats) {
+  *tail_r = 0;
+  *ws_floats = 0;
+  if (tile_rows(M, N, K, epi, lda) != BM) return 0;  // short-row tiles fill the last wave instead
+  const int S = tail_plan_256(M, N, K, epi, tail_r);
+  *ws_floats = (long)S * *tail_r * BM * BN;
   return S;
 }
 

@@ -23,6 +23,7 @@ def _reset_gemm_variant(request):
         request.getfixturevalue("ext").attn_set_bwd3_nw8(1)
         request.getfixturevalue("ext").gemm_set_tail(1)
         request.getfixturevalue("ext").gemm_set_narrow(4096)
+        request.getfixturevalue("ext").gemm_set_rows(0)
 
 
 def rel(a, b):
@@ -218,6 +219,57 @@ def test_gemm_nt(ext, M, N, K, gelu, nt64, narrow):
         g_ref = torch.nn.functional.gelu(outs[0].float(), approximate="tanh")
         assert rel(outs[1], g_ref) < 1e-2
     ext.gemm_set_variant(0, 8)
+
+
+@pytest.mark.parametrize("rows", [224, 192, 256])
+@pytest.mark.parametrize("M,N,K,lda", [(5000, 776, 256, 256), (4500, 260, 128, 192), (6272, 1024, 512, 512),
+                                       (4097, 512, 384, 448)])
+def test_gemm_nt_short_rows(ext, M, N, K, lda, rows):
+    """4-phase kernel at forced tile heights (224 / 192 rows: p4_mainloop MTL = 3 / 2) against fp32,
+    every epilogue (bias, GELU pair, gelu' / gelu, GELU only, dGELU and dGELU-multiply with the
+    column-partial bias gradient), ragged M, N % 8 != 0 (register epilogue) and strided A rows."""
+    ext.gemm_set_narrow(0)
+    ext.gemm_set_rows(rows)
+    ext.gemm_set_tail(0)
+    torch.manual_seed(0)
+    xa = (torch.rand(M, lda, device="cuda") * 2 - 1).bfloat16()
+    x = xa[:, :K]
+    w = ((torch.rand(N, K, device="cuda") * 2 - 1) * 0.1).bfloat16()
+    b = torch.randn(N, device="cuda") * 0.1
+    ref = x.float() @ w.float().t() + b
+    out = ext.gemm_nt(x, w, b)[0]
+    assert rel(out, ref) < 1e-2
+    h, g = ext.gemm_nt(x, w, b, True)
+    assert rel(h, ref) < 1e-2
+    assert rel(g, torch.nn.functional.gelu(h.float(), approximate="tanh")) < 1e-2
+    (go,) = ext.gemm_nt(x, w, b, True, True)
+    assert rel(go, g) < 1e-2
+    if N % 8:
+        return
+    d, g2 = ext.gemm_nt(x, w, b, True, False, True)
+    hr = h.float()
+    t = torch.tanh(0.7978845608028654 * (hr + 0.044715 * hr ** 3))
+    dref = 0.5 * (1 + t) + 0.5 * hr * (1 - t * t) * 0.7978845608028654 * (1 + 3 * 0.044715 * hr * hr)
+    assert rel(d, dref) < 1e-2 and rel(g2, g) < 1e-2
+    # data gradient through the GELU: [M, K'] x [N, K']^T * gelu'(pre)
+    dy = (torch.rand(M, K, device="cuda") * 2 - 1).bfloat16()
+    dg = (dy.float() @ w.float().t()).bfloat16().float()
+    for deriv, aux, fac in ((False, h, dref), (True, d, d.float())):
+        db = torch.full((N,), 0.25, device="cuda")
+        o = ext.gemm_nt_dgelu(dy, w, aux, db, deriv)
+        r = dg * fac
+        assert rel(o, r) < 1e-2, deriv
+        assert rel(db - 0.25, r.sum(0)) < 1e-2, deriv
+
+
+def test_gemm_tile_rows_choice(ext):
+    """Automatic tile height: the FF1 forward / FF2 data gradient of ViT-L pretraining (M = 25088,
+    N = 4096: 6.1 waves of 256-row tiles) takes 224-row tiles (exactly 7 waves) on 256 CUs; the
+    QKV forward (N = 3072, 4.9 waves) stays at 256."""
+    if torch.cuda.get_device_properties(0).multi_processor_count != 256:
+        pytest.skip("wave-fill expectations assume 256 CUs")
+    assert ext.gemm_nt_tiles(25088, 4096, 1024, 6, 1024) == 112 * 16
+    assert ext.gemm_nt_tiles(26624, 3072, 1024, 0, 1024) == 104 * 12
 
 
 @pytest.mark.parametrize("B,S,H,hd", [(2, 300, 4, 64), (1, 787, 3, 64), (2, 225, 2, 32), (1, 787, 2, 32)])

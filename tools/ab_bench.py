@@ -36,6 +36,9 @@ def apply(P, cfg: str):
         elif k == "GEMM_GROUP":  # row tiles per column sweep of the NT kernels
             from jumbo_mae_tpu_amd.ops import _ext
             _ext.load(True).gemm_set_variant(0, int(v))
+        elif k == "GEMM_ROWS":  # 4-phase tile height: 0 = automatic wave fill, 256 / 224 / 192 forced
+            from jumbo_mae_tpu_amd.ops import _ext
+            _ext.load(True).gemm_set_rows(int(v))
         elif k == "GEMM_TAIL":
             from jumbo_mae_tpu_amd.ops import _ext
             _ext.load(True).gemm_set_tail(int(v))

@@ -7,6 +7,7 @@ NT against the transposed weight W^T[K,N].  Interleaved timing in one process (A
 
 import argparse
 import os
+import re
 import sys
 
 import torch
@@ -73,7 +74,11 @@ def main():
     variants = a.variant.split(",")
 
     def setv(v):  # suffix t = tail split (last partial wave split-K + finish kernel), n = narrow
-        # 128 x 192 tiles at every M, w = never narrow (256 x 256 tiles at every M)
+        # 128 x 192 tiles at every M, w = never narrow (256 x 256 tiles at every M), rNNN = 4-phase
+        # tile height forced to NNN rows (256 / 224 / 192; default: automatic wave-fill choice)
+        m = re.search(r"r(\d+)", v)
+        ext.gemm_set_rows(int(m.group(1)) if m else 0)
+        v = re.sub(r"r\d+", "", v)
         ext.gemm_set_tail(1 if "t" in v else 0)
         ext.gemm_set_narrow(1 << 30 if "n" in v else 0 if "w" in v else 4096)
         ext.gemm_set_variant(int(v.rstrip("tnw")), a.group)
