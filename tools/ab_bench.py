@@ -88,7 +88,11 @@ def main():
     ap.add_argument("--rounds", type=int, default=4)
     ap.add_argument("--steps", type=int, default=6)
     ap.add_argument("--model", default="vit_large_patch16")
+    ap.add_argument("--task", default="pretrain", choices=["pretrain", "finetune"],
+                    help="finetune: the bench.py --task finetune step (ViT-B/16, config/ft.sh recipe, 128 images)")
     a = ap.parse_args()
+    if a.task == "finetune":
+        return run(a, finetune_step())
     from jumbo_mae_tpu_amd.config import decoder_config, vit_config
     from jumbo_mae_tpu_amd.models.mae import PretrainModel
     from jumbo_mae_tpu_amd.ops import prims as P
@@ -105,23 +109,68 @@ def main():
     gen = torch.Generator(device=dev).manual_seed(0)
     pool = [torch.randint(0, 256, (512, 3, 224, 224), dtype=torch.uint8, device=dev, generator=gen)
             for _ in range(2)]
+    it = 0
+
+    def step():
+        nonlocal it
+        tr.train_step([(pool[it % 2],)])
+        it += 1
+
+    run(a, (step, 512))
+
+
+def finetune_step():
+    """(step, images per step) of bench.py --task finetune at one rank."""
+    from jumbo_mae_tpu_amd.train import common as C
+    from jumbo_mae_tpu_amd.train.cli import finetune_parser
+    from jumbo_mae_tpu_amd.train.engine import Trainer
+    from jumbo_mae_tpu_amd.train.finetune import build_model
+    from jumbo_mae_tpu_amd.utils.rng import RngStreams
+    dev = torch.device("cuda")
+    B, N = 128, 1281167
+    flags = ["--mode", "finetune", "--layers", "12", "--dim", "768", "--heads", "12", "--labels", "1000",
+             "--posemb", "sincos2d", "--droppath", "0.1", "--mixup", "0.8", "--cutmix", "1.0",
+             "--label-smoothing", "0.1", "--optimizer", "adamw", "--learning-rate", "3e-3",
+             "--weight-decay", "0.05", "--lr-decay", "0.75", "--warmup-steps", str(N * 10 // 1024),
+             "--training-steps", str(N * 110 // 1024), "--train-batch-size", str(B)]
+    for k in ("init", "mixup", "dropout", "shuffle", "noise"):
+        flags += [f"--{k}-seed", "0"]
+    fargs = finetune_parser().parse_args(flags)
+    model = build_model(fargs, dev, torch.bfloat16, 0)
+    model.store.sync_shadow()
+    opt = C.make_optimizer(fargs, model.store, fargs.learning_rate, 1e-6)
+    tr = Trainer(model, opt, None, RngStreams({"mixup": 1, "dropout": 1, "noise": 1}, 0, dev))
+    gen = torch.Generator(device=dev).manual_seed(1234)
+    pool = [(torch.randint(0, 256, (B, 3, 224, 224), dtype=torch.uint8, device=dev, generator=gen),
+             torch.randint(0, 1000, (B,), device=dev, generator=gen)) for _ in range(2)]
+    it = 0
+
+    def step():
+        nonlocal it
+        tr.train_step([pool[it % 2]])
+        it += 1
+
+    return step, B
+
+
+def run(a, step_b):
+    from jumbo_mae_tpu_amd.ops import prims as P
+    step, B = step_b
     cfgs = [c.split(":", 1) for c in a.configs]
     times = {n: [] for n, _ in cfgs}
-    it = 0
     for r in range(a.rounds + 1):  # round 0 = warmup of every config
         for name, cfg in cfgs:
             apply(P, cfg)
             torch.cuda.synchronize()
             t0 = time.perf_counter()
             for _ in range(a.steps):
-                tr.train_step([(pool[it % 2],)])
-                it += 1
+                step()
             torch.cuda.synchronize()
             if r > 0:
                 times[name].append((time.perf_counter() - t0) * 1e3 / a.steps)
     for name, ts in times.items():
         print(f"{name:24s} median {statistics.median(ts):8.2f} ms  min {min(ts):8.2f} ms  "
-              f"({512 * 1e3 / statistics.median(ts):7.1f} img/s)  rounds {['%.1f' % t for t in ts]}", flush=True)
+              f"({B * 1e3 / statistics.median(ts):7.1f} img/s)  rounds {['%.1f' % t for t in ts]}", flush=True)
 
 
 if __name__ == "__main__":
