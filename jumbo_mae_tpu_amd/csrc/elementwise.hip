@@ -52,11 +52,11 @@ __global__ __launch_bounds__(256) void rowcol_kernel(const void* __restrict__ in
                                                      uint16_t* __restrict__ out, float* __restrict__ acc,
                                                      const float* __restrict__ scale, const float* __restrict__ mask,
                                                      int M, int N, int T, int rows_per_block, long sB, long sT,
-                                                     float* __restrict__ acc2, long yB, long yT) {
+                                                     float* __restrict__ acc2, long yB, long yT, int cw) {
   extern __shared__ __attribute__((aligned(16))) float red_s[];  // [2][<= 2048] block's columns
-  // 2-D grid: blockIdx.y picks a chunk of <= 2048 columns, blockIdx.x a slab of rows
-  const int c0 = blockIdx.y * 2048;
-  const int nc = (N - c0) < 2048 ? (N - c0) : 2048;
+  // 2-D grid: blockIdx.y picks a chunk of cw (<= 2048, % 8 == 0) columns, blockIdx.x a slab of rows
+  const int c0 = blockIdx.y * cw;
+  const int nc = (N - c0) < cw ? (N - c0) : cw;
   const ColPlan p = col_plan(nc);
   const int slot = threadIdx.x / p.tpr, c = threadIdx.x % p.tpr;
   const bool active = slot < p.rps;
@@ -194,10 +194,21 @@ void launch_rowcol(const void* in0, const uint16_t* in1, uint16_t* out, float* a
     yB = (long)T * N;
     yT = N;
   }
-  // 2-D grid: column chunks of 2048 x row slabs; each row-slot walks >= 16 rows, ~2048 blocks
-  // in total so the per-block column atomics stay cheap
-  const int ncol = (N + 2047) / 2048;
-  const int cgs = (N < 2048 ? N : 2048) / 8;
+  // 2-D grid: column chunks of cw <= 2048 x row slabs; each row-slot walks >= 16 rows, ~2048
+  // blocks in total so the per-block column atomics stay cheap.  Few rows (< 8192): chunks
+  // narrowed so ~256 blocks keep >= 32 rows each -- every block adds its column partials to the
+  // outputs with global atomics, and 128 row slabs per column (the 512 x 3072 jumbo residual
+  // backward) meant ~1M contended atomics and a 14 us call for 12 MB of data
+  int cw = N < 2048 ? N : 2048;
+  if (M < 32 * 256) {
+    const int nbr = M / 32 > 1 ? M / 32 : 1;
+    int nch = (256 + nbr - 1) / nbr;
+    if (nch > N / 64) nch = N / 64 > 1 ? N / 64 : 1;
+    const int w = ((N + nch - 1) / nch + 7) / 8 * 8;
+    if (w < cw) cw = w;
+  }
+  const int ncol = (N + cw - 1) / cw;
+  const int cgs = cw / 8;
   const int tpr = cgs < 256 ? cgs : 256;
   const int rps = 256 / tpr;
   int rows_per_block = rps * 16;
@@ -219,7 +230,7 @@ void launch_rowcol(const void* in0, const uint16_t* in1, uint16_t* out, float* a
   if (nb < 1) nb = 1;
   const size_t smem = (acc || acc2) ? 4096 * sizeof(float) : 0;
   rowcol_kernel<MODE><<<dim3(nb, ncol), 256, smem, st>>>(in0, in1, out, acc, scale, mask, M, N, T, rows_per_block,
-                                                          sB, sT, acc2, yB, yT);
+                                                          sB, sT, acc2, yB, yT, cw);
 }
 
 }  // namespace

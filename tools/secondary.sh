@@ -1,5 +1,5 @@
 #!/bin/bash
-# Secondary BASELINE configs (bench.py --task finetune / --model vit_base_patch16) + a rocprofv3
+# Secondary BASELINE configs (bench.py --task finetune / --model vit_base_patch16 / --task linear) + a rocprofv3
 # kernel-stats profile of each, on one MI355X:
 #   gpurun --timeout 900 -- bash tools/secondary.sh <outdir>
 set -o pipefail
@@ -14,4 +14,5 @@ run() {  # name, bench args
 }
 run finetune --task finetune
 run vitb_pretrain --model vit_base_patch16
+run linear --task linear
 echo "[secondary] done"
