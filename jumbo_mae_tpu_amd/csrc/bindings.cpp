@@ -88,6 +88,8 @@ int jm_gemm_nt_colpart_rows(int M, int N, int K, int epi, long lda);
 int jm_gemm_nt_tail_plan(int M, int N, int K, int epi, long lda, int* tail_r, long* ws_floats);
 void jm_gemm_set_rows(int rows);
 int jm_gemm_tn_plan(int M, int N, int K, int* S_out);
+int jm_gemm_tn_group_plan(const TnGroup& grp, int M, int* S_out);
+int jm_gemm_tn_group(TnGroup grp, int M, int sps, int S, hipStream_t st);
 int jm_gemm_tn(const uint16_t* A, long lda, const uint16_t* B, long ldb, int M, int N, int K, int sps, int S,
                float* G, long ldo, float* partial, hipStream_t st);
 struct TnSegs {
@@ -845,6 +847,53 @@ int64_t gemm_tn_wgrad_seg(std::vector<torch::Tensor> dys, std::vector<torch::Ten
   return S;
 }
 
+// g_p[N_p, K_p] += dys[p]^T . xs[p] for up to 4 problems over the same M rows in ONE grid (e.g. a
+// layer's FF1 + FF2 or QKV + Wo weight gradients): fewer M splits per problem than separate
+// launches -> fewer fp32 partial slices to write and reduce; returns the split count
+int64_t gemm_tn_wgrad_group(std::vector<torch::Tensor> dys, std::vector<torch::Tensor> xs,
+                            std::vector<torch::Tensor> gs) {
+  const int n = (int)dys.size();
+  TORCH_CHECK(n >= 1 && n <= 4 && (int)xs.size() == n && (int)gs.size() == n, "gemm_tn_wgrad_group: 1..4 problems");
+  const int M = dys[0].size(0);
+  TnGroup grp{};
+  grp.n = n;
+  long total = 0;
+  for (int p = 0; p < n; ++p) {
+    const auto &dy = dys[p], &x = xs[p], &g = gs[p];
+    CHECK_DT(dy, torch::kBFloat16);
+    CHECK_DT(x, torch::kBFloat16);
+    TORCH_CHECK(dy.dim() == 2 && x.dim() == 2 && dy.size(0) == M && x.size(0) == M,
+                "gemm_tn_wgrad_group: dy [M,N_p], x [M,K_p] with one M");
+    TORCH_CHECK(dy.stride(1) == 1 && x.stride(1) == 1, "gemm_tn_wgrad_group: rows must be contiguous");
+    const int N = dy.size(1), K = x.size(1);
+    TORCH_CHECK(N % 256 == 0 && K % 256 == 0, "gemm_tn_wgrad_group: N, K multiples of 256");
+    TORCH_CHECK(g.is_contiguous() && g.scalar_type() == torch::kFloat32 && g.numel() == (long)N * K && g.is_cuda(),
+                "gemm_tn_wgrad_group g");
+    grp.a[p] = bf(dy);
+    grp.b[p] = bf(x);
+    grp.lda[p] = dy.stride(0);
+    grp.ldb[p] = x.stride(0);
+    grp.N[p] = N;
+    grp.K[p] = K;
+    total += (long)N * K;
+  }
+  int S = 1;
+  const int sps = jm_gemm_tn_group_plan(grp, M, &S);
+  torch::Tensor part;
+  long off = 0;
+  if (S > 1) part = torch::empty({(long)S * total}, gs[0].options());
+  for (int p = 0; p < n; ++p) {
+    grp.out[p] = S > 1 ? part.data_ptr<float>() + off : gs[p].data_ptr<float>();
+    off += (long)S * grp.N[p] * grp.K[p];
+  }
+  check_rc(jm_gemm_tn_group(grp, M, sps, S, stream()), "gemm_tn_wgrad_group");
+  if (S > 1)
+    for (int p = 0; p < n; ++p)
+      check_rc(jm_splitk_reduce_add(grp.out[p], gs[p].data_ptr<float>(), (long)grp.N[p] * grp.K[p], S, stream()),
+               "gemm_tn_wgrad_group reduce");
+  return S;
+}
+
 // x1 = x + mask*scale*y ([B,T,D] fp32, fresh contiguous); h / mean / rstd = LN of rows t >= T0
 std::vector<torch::Tensor> residual_ln_fwd(torch::Tensor x, torch::Tensor y, c10::optional<torch::Tensor> scale,
                                            c10::optional<torch::Tensor> mask, torch::Tensor gamma,
@@ -930,6 +979,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("attn_set_max_seq", &jm_attn_set_max_seq);
   m.def("gemm_tn_wgrad", &gemm_tn_wgrad);
   m.def("gemm_tn_wgrad_seg", &gemm_tn_wgrad_seg);
+  m.def("gemm_tn_wgrad_group", &gemm_tn_wgrad_group, "grouped weight gradients over one M (<= 4 problems)");
   m.def("gemm_set_variant", &jm_gemm_set_variant, py::arg("nt64"), py::arg("group") = 8,
         "nt64 = 1: every NT launch on the 64-deep main loop (tests); group: row tiles per column sweep");
   m.def("gemm_set_tail", &jm_gemm_set_tail);

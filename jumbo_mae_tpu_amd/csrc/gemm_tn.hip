@@ -16,6 +16,7 @@
 #include <type_traits>
 
 #include "common.h"
+#include "jm_api.h"
 
 namespace {
 
@@ -288,11 +289,14 @@ __global__ __launch_bounds__(NTH, 1) void gemm_tn_kernel(const uint16_t* __restr
 // address per block (+ immediates for the k offsets).  Waves 4-7 at static priority 1.
 constexpr int SLOT4 = 64 * 128;  // elements per slot
 
-template <int ACC, bool SEG>
+// GRP: the grid covers the tiles of every problem of ``grp`` (same M); each workgroup picks its
+// problem's operands, shape and output from the tile index (workgroup-uniform)
+template <int ACC, bool SEG, bool GRP = false>
 __global__ __launch_bounds__(NTH, 1) void gemm_tn4_kernel(const uint16_t* __restrict__ A, long lda,
                                                           const uint16_t* __restrict__ B, long ldb, int M, int N,
                                                           int K, int steps_per_split, float* __restrict__ out,
-                                                          long ldo, long split_stride, TnSegs segs = {}) {
+                                                          long ldo, long split_stride, TnSegs segs = {},
+                                                          TnGroup grp = {}) {
   JM_DGUARD(blockDim.x == NTH && steps_per_split >= 4 && steps_per_split % 4 == 0 && M > 0);
   extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
   const int tid = threadIdx.x;
@@ -301,13 +305,29 @@ __global__ __launch_bounds__(NTH, 1) void gemm_tn4_kernel(const uint16_t* __rest
   const int wr = wave >> 2, wc = wave & 3;
   if (__builtin_amdgcn_readfirstlane(tid) >= 256) __builtin_amdgcn_s_setprio(1);
 
-  const int nK = K / TK_;
-  const int tiles = (N / TN_) * nK;
+  int nK = K / TK_;
+  const int tiles = GRP ? grp.tile0[grp.n] : (N / TN_) * nK;
   const int nwg = gridDim.x;
   const int orig = blockIdx.x;
   const int xcd = orig & 7, q = nwg >> 3, r = nwg & 7;
   const int wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
-  const int split = wg / tiles, tile = wg - split * tiles;
+  const int split = wg / tiles;
+  int tile = wg - split * tiles;
+  if constexpr (GRP) {
+    int p = 0;
+    while (p + 1 < grp.n && tile >= grp.tile0[p + 1]) ++p;
+    tile -= grp.tile0[p];
+    A = grp.a[p];
+    B = grp.b[p];
+    lda = grp.lda[p];
+    ldb = grp.ldb[p];
+    N = grp.N[p];
+    K = grp.K[p];
+    out = grp.out[p];
+    ldo = K;
+    split_stride = (long)N * K;
+    nK = K / TK_;
+  }
   const int n0 = (tile / nK) * TN_, k0 = (tile % nK) * TK_;
   const int m_begin = split * steps_per_split * BS;
   const int rows = min(M - m_begin, steps_per_split * BS);  // > 0 (host guarantees)
@@ -502,8 +522,8 @@ size_t jm_gemm_tn_smem() { return (size_t)NST * STAGE * sizeof(uint16_t); }
 // Split of the M range: returns steps (of 32 rows) per split; *S_out = number of splits.
 // Picks the split count that minimises an estimate of (waves of 256 CUs) x (steps per split +
 // epilogue) + the fp32 partial-tile traffic of the reduction (weight A/B: profiles/r2_tn_plan_scale.txt).
-int jm_gemm_tn_plan(int M, int N, int K, int* S_out) {
-  const int tiles = (N / TN_) * (K / TK_);
+namespace {
+int tn_plan(int M, int tiles, long NK, int* S_out) {
   const int steps = (M + BS - 1) / BS;
   const int unit = 4;  // steps per split: whole 128-row units of the 4-phase kernel
   double best = 1e30;
@@ -516,7 +536,7 @@ int jm_gemm_tn_plan(int M, int N, int K, int* S_out) {
     const long wgs = (long)tiles * s_eff;
     const long waves = (wgs + 255) / 256;
     const double t_steps = (double)waves * (sps + 12);                       // ~1 us per step
-    const double t_red = s_eff > 1 ? (double)s_eff * N * K * 8.0 / 5.0e12 * 1e6 : 0.0;  // us
+    const double t_red = s_eff > 1 ? (double)s_eff * NK * 8.0 / 5.0e12 * 1e6 : 0.0;  // us
     const double est = t_steps + t_red;
     if (est < best) {
       best = est;
@@ -526,6 +546,20 @@ int jm_gemm_tn_plan(int M, int N, int K, int* S_out) {
   }
   *S_out = best_S;
   return best_sps;
+}
+}  // namespace
+
+int jm_gemm_tn_plan(int M, int N, int K, int* S_out) { return tn_plan(M, (N / TN_) * (K / TK_), (long)N * K, S_out); }
+
+// split plan of a grouped launch: the problems' tiles and output elements together
+int jm_gemm_tn_group_plan(const TnGroup& grp, int M, int* S_out) {
+  long nk = 0;
+  int tiles = 0;
+  for (int p = 0; p < grp.n; ++p) {
+    nk += (long)grp.N[p] * grp.K[p];
+    tiles += (grp.N[p] / TN_) * (grp.K[p] / TK_);
+  }
+  return tn_plan(M, tiles, nk, S_out);
 }
 
 namespace {
@@ -590,6 +624,35 @@ int jm_gemm_tn_seg(const TnSegs& segs, long lda, long ldb, int N, int K, int sps
   const int M = segs.rows * segs.n;
   return launch_tn<true>(nullptr, lda, nullptr, ldb, M, N, K, sps, S, G, ldo, partial, segs,
                          sps % 4 == 0 && segs.rows % 64 == 0, st);
+}
+
+// Grouped launch of up to 4 TN problems over the same M rows (e.g. the FF1 and FF2 weight
+// gradients of a layer): one grid of sum(tiles) x S workgroups instead of two half-filled ones,
+// so each problem needs half the splits -- half the fp32 partial slices written and reduced.
+// S > 1: grp.out[p] = the [S][N_p K_p] partial workspace (the caller reduces into G_p); S == 1:
+// grp.out[p] = G_p, accumulated in place.
+int jm_gemm_tn_group(TnGroup grp, int M, int sps, int S, hipStream_t st) {
+  if (grp.n < 1 || grp.n > 4 || M <= 0 || sps % 4 || sps < 4 || S < 1) return -1;
+  grp.tile0[0] = 0;
+  for (int p = 0; p < grp.n; ++p) {
+    if (grp.N[p] % TN_ || grp.K[p] % TK_ || grp.out[p] == nullptr) return -1;
+    if ((long)M * grp.lda[p] * 2 >= (1L << 32) || (long)M * grp.ldb[p] * 2 >= (1L << 32)) return -2;
+    grp.tile0[p + 1] = grp.tile0[p] + (grp.N[p] / TN_) * (grp.K[p] / TK_);
+  }
+  const size_t sm = jm_gemm_tn_smem();
+  const int wgs = grp.tile0[grp.n] * S;
+  if (S == 1) {
+    static bool a = false;
+    set_smem_once(gemm_tn4_kernel<1, false, true>, a);
+    gemm_tn4_kernel<1, false, true><<<wgs, NTH, sm, st>>>(nullptr, 0, nullptr, 0, M, 0, 0, sps, nullptr, 0, 0,
+                                                          TnSegs{}, grp);
+  } else {
+    static bool a = false;
+    set_smem_once(gemm_tn4_kernel<0, false, true>, a);
+    gemm_tn4_kernel<0, false, true><<<wgs, NTH, sm, st>>>(nullptr, 0, nullptr, 0, M, 0, 0, sps, nullptr, 0, 0,
+                                                          TnSegs{}, grp);
+  }
+  return 0;
 }
 
 JM_DEBUG_EXPORT(gemm_tn)

@@ -16,6 +16,20 @@ struct JmLnRes {
   float* dbias;
 };
 
+// Grouped weight-gradient launch (gemm_tn.hip jm_gemm_tn_group): n <= 4 independent TN problems
+// G_p[N_p][K_p] (+)= A_p[M][N_p]^T . B_p[M][K_p] over the SAME M rows in one grid; tile0 = prefix
+// sums of the problems' 256 x 256 output tiles; out[p] = G_p (one split) or its [S][N_p K_p]
+// fp32 partial slices.
+struct TnGroup {
+  const uint16_t* a[4];
+  const uint16_t* b[4];
+  long lda[4], ldb[4];
+  int N[4], K[4];
+  float* out[4];
+  int tile0[5];
+  int n;
+};
+
 // Epilogue / output description of an NT GEMM launch (gemm.hip, bindings.cpp).
 struct GemmEpi {
   const float* bias;     // [N] fp32 or null

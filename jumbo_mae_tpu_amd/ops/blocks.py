@@ -155,45 +155,50 @@ class JumboBlockFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dx2):
-        (x, mu1, rs1, h1, qkv, o, lse, a, x1, muc, rsc, hcb, jpre, jg, jy,
-         hp, mup, rsp, fpre, fg, fy, m1, m2, m3) = ctx.saved_tensors
-        layer = ctx.layer
-        B, S, D = x.shape
-        C = layer.C
-        J = C * D
-        dt = h1.dtype
-        dx2 = dx2.contiguous()
-        dx1 = torch.empty_like(dx2)
-        a3 = a.view(B, S, D)
-        da = torch.empty_like(a)
-        da3 = da.view(B, S, D)
-        # ---- jumbo branch: d hc = dx2_cls + JumboMLP'(s3 * dp3 * dx2_cls); dx1_cls = LN3'(d hc)
-        dcls = dx2[:, :C].reshape(B, 1, J)
-        djy, bd = P.residual_bwd(dcls, jy, layer.scale3, m3, dt, layer.jumbo_mlp.w2.b)
-        # d hc = dcls + JumboMLP'(...) in fp32, the add fused into the jumbo dgrad's split-K reduce
-        dhc = _ff_bwd(layer.jumbo_mlp, djy, hcb, jpre, jg, bd, dx_add=dcls.reshape(B, J),
-                      deriv=ctx.gelu_deriv[0])
-        P.ln_bwd(dhc, x1[:, :C].reshape(B, 1, J), muc, rsc, layer.norm3.g, layer.norm3.b,
-                 out=dx1[:, :C].reshape(B, 1, J))
-        # attention-residual backward of the CLS rows (the patch rows ride on LN2' below, which
-        # also marks scale1 ready: it must come last)
-        P.residual_bwd(dx1[:, :C], a3[:, :C], layer.scale1, m1, dt, layer.attn.wo_b, out=da3[:, :C],
-                       mark_ready=False)
-        # ---- patch branch: dx1[:, C:] = dx2[:, C:] + LN2'(FF'(s2 * dp2 * dx2[:, C:]))
-        fused = ctx.link_out.take(dx2) if ctx.link_out is not None else None
-        if fused is not None:  # computed by the upper block's LN1 backward
-            dfy, bd = fused
-        else:
-            dfy, bd = P.residual_bwd(dx2[:, C:], fy, layer.scale2, m2, dt, layer.ff.w2.b)
-        dhp = _ff_bwd(layer.ff, dfy, hp, fpre, fg, bd, deriv=ctx.gelu_deriv[1])
-        # ... and the attention-residual backward of those rows in the same pass
-        _, _, bd = P.ln_bwd(dhp, x1[:, C:], mup, rsp, layer.norm2.g, layer.norm2.b, dres=dx2[:, C:],
-                            out=dx1[:, C:],
-                            res=P.ResSpec(a3[:, C:], layer.scale1, m1, layer.attn.wo_b, 0, da3[:, C:]))
-        # ---- attention branch: dx = dx1 + LN1'(Attn'(s1 * dp1 * dx1))
-        dh1 = _attn_bwd(layer.attn, da, h1, qkv, o, lse, B, S, bd)
-        dx = _ln1_bwd(ctx, dh1, x, mu1, rs1, layer, dx1)
+        with P.paired_wgrads():  # FF2 + FF1 and Wo + QKV weight gradients as grouped launches
+            dx = _jumbo_bwd(ctx, dx2)
         return dx, None, None, None, None, None, None, None, None
+
+
+def _jumbo_bwd(ctx, dx2):
+    (x, mu1, rs1, h1, qkv, o, lse, a, x1, muc, rsc, hcb, jpre, jg, jy,
+     hp, mup, rsp, fpre, fg, fy, m1, m2, m3) = ctx.saved_tensors
+    layer = ctx.layer
+    B, S, D = x.shape
+    C = layer.C
+    J = C * D
+    dt = h1.dtype
+    dx2 = dx2.contiguous()
+    dx1 = torch.empty_like(dx2)
+    a3 = a.view(B, S, D)
+    da = torch.empty_like(a)
+    da3 = da.view(B, S, D)
+    # ---- jumbo branch: d hc = dx2_cls + JumboMLP'(s3 * dp3 * dx2_cls); dx1_cls = LN3'(d hc)
+    dcls = dx2[:, :C].reshape(B, 1, J)
+    djy, bd = P.residual_bwd(dcls, jy, layer.scale3, m3, dt, layer.jumbo_mlp.w2.b)
+    # d hc = dcls + JumboMLP'(...) in fp32, the add fused into the jumbo dgrad's split-K reduce
+    dhc = _ff_bwd(layer.jumbo_mlp, djy, hcb, jpre, jg, bd, dx_add=dcls.reshape(B, J),
+                  deriv=ctx.gelu_deriv[0])
+    P.ln_bwd(dhc, x1[:, :C].reshape(B, 1, J), muc, rsc, layer.norm3.g, layer.norm3.b,
+             out=dx1[:, :C].reshape(B, 1, J))
+    # attention-residual backward of the CLS rows (the patch rows ride on LN2' below, which
+    # also marks scale1 ready: it must come last)
+    P.residual_bwd(dx1[:, :C], a3[:, :C], layer.scale1, m1, dt, layer.attn.wo_b, out=da3[:, :C],
+                   mark_ready=False)
+    # ---- patch branch: dx1[:, C:] = dx2[:, C:] + LN2'(FF'(s2 * dp2 * dx2[:, C:]))
+    fused = ctx.link_out.take(dx2) if ctx.link_out is not None else None
+    if fused is not None:  # computed by the upper block's LN1 backward
+        dfy, bd = fused
+    else:
+        dfy, bd = P.residual_bwd(dx2[:, C:], fy, layer.scale2, m2, dt, layer.ff.w2.b)
+    dhp = _ff_bwd(layer.ff, dfy, hp, fpre, fg, bd, deriv=ctx.gelu_deriv[1])
+    # ... and the attention-residual backward of those rows in the same pass
+    _, _, bd = P.ln_bwd(dhp, x1[:, C:], mup, rsp, layer.norm2.g, layer.norm2.b, dres=dx2[:, C:],
+                        out=dx1[:, C:],
+                        res=P.ResSpec(a3[:, C:], layer.scale1, m1, layer.attn.wo_b, 0, da3[:, C:]))
+    # ---- attention branch: dx = dx1 + LN1'(Attn'(s1 * dp1 * dx1))
+    dh1 = _attn_bwd(layer.attn, da, h1, qkv, o, lse, B, S, bd)
+    return _ln1_bwd(ctx, dh1, x, mu1, rs1, layer, dx1)
 
 
 def _ln1_fwd(x, layer, link_in, dt):
@@ -249,23 +254,28 @@ class ViTBlockFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dx2):
-        x, mu1, rs1, h1, qkv, o, lse, a, x1, mu2, rs2, h2, fpre, fg, fy, m1, m2 = ctx.saved_tensors
-        layer = ctx.layer
-        B, S, D = x.shape
-        dt = h1.dtype
-        dx2 = dx2.contiguous()
-        fused = ctx.link_out.take(dx2) if ctx.link_out is not None else None
-        if fused is not None:  # computed by the upper block's LN1 backward
-            dfy, bd = fused
-        else:
-            dfy, bd = P.residual_bwd(dx2, fy, layer.scale2, m2, dt, layer.ff.w2.b)
-        dh2 = _ff_bwd(layer.ff, dfy, h2, fpre, fg, bd, deriv=ctx.gelu_deriv[1])
-        # LN2' with the attention-residual backward of its dx fused in (never write autograd's dx2)
-        dx1, da, bd = P.ln_bwd(dh2, x1, mu2, rs2, layer.norm2.g, layer.norm2.b, dres=dx2,
-                               res=P.ResSpec(a, layer.scale1, m1, layer.attn.wo_b))
-        dh1 = _attn_bwd(layer.attn, da, h1, qkv, o, lse, B, S, bd)
-        dx = _ln1_bwd(ctx, dh1, x, mu1, rs1, layer, dx1)
+        with P.paired_wgrads():  # FF2 + FF1 and Wo + QKV weight gradients as grouped launches
+            dx = _vit_bwd(ctx, dx2)
         return dx, None, None, None, None, None, None, None
+
+
+def _vit_bwd(ctx, dx2):
+    x, mu1, rs1, h1, qkv, o, lse, a, x1, mu2, rs2, h2, fpre, fg, fy, m1, m2 = ctx.saved_tensors
+    layer = ctx.layer
+    B, S, D = x.shape
+    dt = h1.dtype
+    dx2 = dx2.contiguous()
+    fused = ctx.link_out.take(dx2) if ctx.link_out is not None else None
+    if fused is not None:  # computed by the upper block's LN1 backward
+        dfy, bd = fused
+    else:
+        dfy, bd = P.residual_bwd(dx2, fy, layer.scale2, m2, dt, layer.ff.w2.b)
+    dh2 = _ff_bwd(layer.ff, dfy, h2, fpre, fg, bd, deriv=ctx.gelu_deriv[1])
+    # LN2' with the attention-residual backward of its dx fused in (never write autograd's dx2)
+    dx1, da, bd = P.ln_bwd(dh2, x1, mu2, rs2, layer.norm2.g, layer.norm2.b, dres=dx2,
+                           res=P.ResSpec(a, layer.scale1, m1, layer.attn.wo_b))
+    dh1 = _attn_bwd(layer.attn, da, h1, qkv, o, lse, B, S, bd)
+    return _ln1_bwd(ctx, dh1, x, mu1, rs1, layer, dx1)
 
 
 def vit_block(layer, x, m1=None, m2=None, link_in: Link | None = None, link_out: Link | None = None):

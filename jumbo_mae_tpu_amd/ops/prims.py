@@ -11,6 +11,7 @@ owns into the flat fp32 gradient buffer and signals readiness to the data-parall
 
 from __future__ import annotations
 
+import contextlib
 import math
 import os
 
@@ -84,6 +85,60 @@ def wgrad(h: Handle, dy: torch.Tensor, x: torch.Tensor, rows: tuple[int, int] | 
             torch.addmm(g, dy.t(), x, out_dtype=torch.float32, out=g)
     else:
         g.addmm_(dy.t().float(), x.float())
+
+
+def _tn_ok(dy: torch.Tensor, x: torch.Tensor) -> bool:
+    """``wgrad`` runs this (dy, x) on the TN MFMA kernel (csrc/gemm_tn.hip)."""
+    return (_WGRAD_OURS and hip(dy) and dy.dtype == torch.bfloat16 and x.dtype == torch.bfloat16 and dy.dim() == 2
+            and dy.shape[1] % 256 == 0 and x.shape[1] % 256 == 0 and dy.shape[0] >= 4096
+            and dy.stride(1) == 1 and x.stride(1) == 1)
+
+
+# ------------------------------------------------------------- paired weight gradients
+# A weight gradient has only 16-64 256 x 256 output tiles (ViT-L: 1024 x 4096 -> 64), so the TN
+# kernel splits the token reduction over S fp32 partial slices (S = 4-16) to fill 256 CUs, and a
+# reduce pass sums them.  Inside a fused block's backward two consecutive weight gradients over the
+# same token rows -- FF2 then FF1, Wo then QKV -- are held and launched as ONE grouped grid
+# (gemm_tn_wgrad_group): twice the tiles, half the splits, half the partial bytes written and
+# re-read.  The first one's ``ready`` waits for the pair.  A/B switch: JMAE_PAIR_WGRAD=0.
+PAIR_WGRAD = os.environ.get("JMAE_PAIR_WGRAD", "1") == "1"
+_pair: dict = {"depth": 0, "held": None}
+
+
+@contextlib.contextmanager
+def paired_wgrads():
+    _pair["depth"] += 1
+    try:
+        yield
+    finally:
+        _pair["depth"] -= 1
+        if _pair["depth"] == 0:
+            _flush_pair()
+
+
+def _flush_pair() -> None:
+    held, _pair["held"] = _pair["held"], None
+    if held is not None:
+        hw, dy, x = held
+        wgrad(hw, dy, x)
+        hw.ready()
+
+
+def _wgrad_ready(hw: Handle, dy: torch.Tensor, x: torch.Tensor) -> None:
+    """grad[hw] += dy^T x, then tell the reducer -- or hold it for / launch it with its pair."""
+    if PAIR_WGRAD and _pair["depth"] > 0 and _tn_ok(dy, x):
+        held = _pair["held"]
+        if held is not None and held[1].shape[0] == dy.shape[0]:
+            _pair["held"] = None
+            _ext.load().gemm_tn_wgrad_group([held[1], dy], [held[2], x], [held[0].grad, hw.grad])
+            held[0].ready()
+            hw.ready()
+            return
+        _flush_pair()
+        _pair["held"] = (hw, dy, x)
+        return
+    wgrad(hw, dy, x)
+    hw.ready()
 
 
 def bias_grad(hb: Handle, dy: torch.Tensor) -> None:
@@ -357,11 +412,11 @@ def linear_bwd(dy: torch.Tensor, x2: torch.Tensor, hw: Handle, hb: Handle | None
                     bias_grad(hb, dy)
             dy.record_stream(side)
             x2.record_stream(side)
+            hw.ready()
         else:
-            wgrad(hw, dy, x2)
             if hb is not None and not bias_done:
                 bias_grad(hb, dy)
-        hw.ready()
+            _wgrad_ready(hw, dy, x2)
         if hb is not None:
             hb.ready()
     return dx

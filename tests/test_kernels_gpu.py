@@ -357,6 +357,23 @@ def test_gemm_tn_wgrad(ext, M, N, K):
         assert rel(g2, ref2) < 1e-4, n
 
 
+@pytest.mark.parametrize("M,shapes", [(4096, [(256, 1024), (1024, 256)]), (26624, [(1024, 1024), (3072, 1024)]),
+                                      (5000, [(512, 256), (256, 512), (768, 256)]), (25088, [(1024, 4096), (4096, 1024)])])
+def test_gemm_tn_wgrad_group(ext, M, shapes):
+    """Grouped TN weight gradients (one grid over several problems with the same M, ragged M
+    included) == separate fp64 references, accumulated into existing gradients; run twice."""
+    torch.manual_seed(0)
+    dys = [(torch.rand(M, n, device="cuda") * 2 - 1).bfloat16() for n, _ in shapes]
+    xs = [(torch.rand(M, k, device="cuda") * 2 - 1).bfloat16() for _, k in shapes]
+    gs = [torch.randn(n, k, device="cuda") for n, k in shapes]
+    refs = [g.double() + 2 * (d.double().t() @ x.double()) for g, d, x in zip(gs, dys, xs)]
+    S = ext.gemm_tn_wgrad_group(dys, xs, gs)
+    assert S >= 1
+    ext.gemm_tn_wgrad_group(dys, xs, gs)
+    for g, r in zip(gs, refs):
+        assert rel(g, r) < 1e-4
+
+
 @pytest.mark.parametrize("T0", [0, 3])
 @pytest.mark.parametrize("with_scale", [False, True])
 def test_residual_ln_fwd(ext, T0, with_scale):

@@ -156,3 +156,41 @@ def test_finetune_production_routing_matches_cpu():
     lg.backward()
     torch.cuda.synchronize()
     _compare_leaves(cpu, gpu, lc, lg)
+
+
+def test_paired_wgrads_match_separate():
+    """Fused-block backward with consecutive weight gradients (FF2 + FF1, Wo + QKV) launched as
+    grouped TN grids (ops/prims.py paired_wgrads) == every weight gradient on its own: same
+    gradients up to fp32 summation order, same DP ``ready`` notifications per parameter."""
+    from collections import Counter
+    from jumbo_mae_tpu_amd.config import DecoderConfig, ViTConfig
+    from jumbo_mae_tpu_amd.models.mae import PretrainModel
+    from jumbo_mae_tpu_amd.ops import prims as P
+    vc = ViTConfig(layers=2, dim=256, heads=4, labels=0, image_size=224, patch_size=16, posemb="sincos2d",
+                   layerscale=True)
+    dc = DecoderConfig(dec_layers=2, dec_dim=256, dec_heads=4, image_size=224, patch_size=16)
+    m = PretrainModel(vc, dc).to("cuda", torch.bfloat16, seed=0)
+    imgs = torch.randint(0, 256, (96, 3, 224, 224), dtype=torch.uint8, device="cuda")  # 4992 / 19104 rows
+    noise = torch.rand(196, device="cuda")
+    grads, readies = [], []
+    saved = P.PAIR_WGRAD
+    try:
+        for pair in (False, True):
+            P.PAIR_WGRAD = pair
+            seen = Counter()
+            m.store.hooks.append(lambda h: seen.update([h.start]))
+            m.store.zero_grad()
+            m(imgs, noise=noise)["loss"].backward()
+            torch.cuda.synchronize()
+            m.store.hooks.pop()
+            assert P._pair["held"] is None and P._pair["depth"] == 0
+            grads.append(m.store.grad.clone())
+            readies.append(seen)
+    finally:
+        P.PAIR_WGRAD = saved
+    assert readies[0] == readies[1] and sum(readies[0].values()) > 0
+    a, b = grads
+    assert ((a - b).norm() / a.norm()).item() < 1e-5
+    for s in m.store.segments:
+        x, y = a[s.offset:s.offset + s.numel], b[s.offset:s.offset + s.numel]
+        assert (x - y).abs().max().item() <= 1e-4 * max(x.abs().max().item(), 1e-6), s.key

@@ -39,6 +39,8 @@ def apply(P, cfg: str):
         elif k == "GEMM_ROWS":  # 4-phase tile height: 0 = automatic wave fill, 256 / 224 / 192 forced
             from jumbo_mae_tpu_amd.ops import _ext
             _ext.load(True).gemm_set_rows(int(v))
+        elif k == "JMAE_PAIR_WGRAD":  # 0: every weight gradient launched on its own
+            P.PAIR_WGRAD = v == "1"
         elif k == "GEMM_TAIL":
             from jumbo_mae_tpu_amd.ops import _ext
             _ext.load(True).gemm_set_tail(int(v))
