@@ -87,6 +87,7 @@ int jm_gemm_nt_tiles(int M, int N, int K, int epi, long lda);
 int jm_gemm_nt_colpart_rows(int M, int N, int K, int epi, long lda);
 int jm_gemm_nt_tail_plan(int M, int N, int K, int epi, long lda, int* tail_r, long* ws_floats);
 void jm_gemm_set_rows(int rows);
+void jm_gemm_set_narrow_splitk(int on);
 int jm_gemm_tn_plan(int M, int N, int K, int* S_out);
 int jm_gemm_tn_group_plan(const TnGroup& grp, int M, int* S_out);
 int jm_gemm_tn_group(TnGroup grp, int M, int sps, int S, hipStream_t st);
@@ -986,6 +987,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_set_narrow", &jm_gemm_set_narrow, "M below which NT GEMMs take the 128 x 192 narrow tiles (0 = never)");
   m.def("gemm_nt_tiles", &jm_gemm_nt_tiles, py::arg("M"), py::arg("N"), py::arg("K") = 1024, py::arg("epi") = 0,
         py::arg("lda") = 0, "output tiles (workgroups before split-K) of an NT launch");
+  m.def("gemm_set_narrow_splitk", &jm_gemm_set_narrow_splitk, "split-K from M = 256 on the narrow tiles (A/B)");
   m.def("gemm_set_rows", &jm_gemm_set_rows,
         "4-phase tile height: 0 = automatic (wave fill), 256 / 224 / 192 = forced (A/B, tests)");
   m.def("transpose_bf16_batch", &transpose_bf16_batch);

@@ -1117,9 +1117,11 @@ bool narrow(int M, int N) { return M < g_narrow_max_m && N % 8 == 0; }
 
 // split-K (EPI_PARTIAL, splits > 1) keeps the 256 x 256 kernels from M = 256 up: the jumbo MLP's
 // K = 12288 GEMMs ran 43 us there vs 47 us on narrow tiles (profiles/r3e_summary_vitl_b512_fused_reductions.txt)
+int g_narrow_splitk = 0;  // A/B: split-K launches from M = 256 on the narrow tiles too
+
 bool narrow_launch(int M, int N, int epi, int splits) {
   if (!narrow(M, N)) return false;
-  return !(epi == EPI_PARTIAL && splits > 1 && M >= 256);
+  return g_narrow_splitk || !(epi == EPI_PARTIAL && splits > 1 && M >= 256);
 }
 
 bool p4_ok(int K, int epi, int splits) {
@@ -1204,6 +1206,8 @@ void jm_gemm_set_variant(int nt64, int group) {
 void jm_gemm_set_tail(int on) { g_gemm_tail = on; }
 
 void jm_gemm_set_narrow(int max_m) { g_narrow_max_m = max_m; }
+
+void jm_gemm_set_narrow_splitk(int on) { g_narrow_splitk = on; }
 
 void jm_gemm_set_rows(int rows) { g_gemm_rows = (rows == 224 || rows == 192 || rows == 256) ? rows : 0; }
 

@@ -153,6 +153,7 @@ _DGRAD_OURS = os.environ.get("JMAE_DGRAD", "1") == "1"  # data-gradient GEMMs on
 
 
 NARROW_MAX_M = 4096  # csrc/gemm.hip g_narrow_max_m: below it the NT GEMMs take 128 x 192 tiles
+NARROW_SPLITK = False  # A/B: split-K from M = 256 on the narrow tiles (csrc/gemm.hip g_narrow_splitk)
 _NARROW_FUSED_MIN_TILES = 160  # a fused GELU epilogue needs the tiles alone to fill most CUs
 
 
@@ -187,7 +188,7 @@ def splitk_plan(M: int, N: int, K: int) -> int:
         return 0
     if nt_tiles(M, N) >= _NARROW_FUSED_MIN_TILES:
         return 0
-    if M >= 256:  # split launches keep the 256 x 256 tiles (jm_gemm narrow_launch): whole 128-deep units
+    if M >= 256 and not NARROW_SPLITK:  # split launches keep the 256 x 256 tiles (jm_gemm narrow_launch)
         if K % 128:
             return 0
         s = min(256 // (-(-M // 256) * -(-N // 256)), K // 512, 32)

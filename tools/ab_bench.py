@@ -41,6 +41,10 @@ def apply(P, cfg: str):
             _ext.load(True).gemm_set_rows(int(v))
         elif k == "JMAE_PAIR_WGRAD":  # 0: every weight gradient launched on its own
             P.PAIR_WGRAD = v == "1"
+        elif k == "NARROW_SPLITK":  # split-K GEMMs from M = 256 on the narrow 128 x 192 tiles
+            from jumbo_mae_tpu_amd.ops import _ext
+            _ext.load(True).gemm_set_narrow_splitk(int(v))
+            P.NARROW_SPLITK = v == "1"
         elif k == "GEMM_TAIL":
             from jumbo_mae_tpu_amd.ops import _ext
             _ext.load(True).gemm_set_tail(int(v))
