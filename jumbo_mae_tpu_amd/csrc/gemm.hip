@@ -1115,9 +1115,11 @@ int g_narrow_max_m = 4096;  // M below this: 128 x 192 tiles (A/B switch: 0 = ne
 
 bool narrow(int M, int N) { return M < g_narrow_max_m && N % 8 == 0; }
 
-// split-K (EPI_PARTIAL, splits > 1) keeps the 256 x 256 kernels from M = 256 up: the jumbo MLP's
-// K = 12288 GEMMs ran 43 us there vs 47 us on narrow tiles (profiles/r3e_summary_vitl_b512_fused_reductions.txt)
-int g_narrow_splitk = 0;  // A/B: split-K launches from M = 256 on the narrow tiles too
+// split-K (EPI_PARTIAL, splits > 1) from M = 256 on the narrow tiles too: the jumbo MLP's K = 12288
+// GEMMs take 4 splits of 128 x 192 tiles instead of 10 of 256 x 256 -- the GEMM alone is ~4 us
+// slower (r3e_summary_vitl_b512_fused_reductions.txt) but the fp32 partials shrink 2.5x
+// (profiles/r3_narrow_splitk.txt: ViT-L step -0.41 ms in-process).  0 = the 256 x 256 kernels.
+int g_narrow_splitk = 1;
 
 bool narrow_launch(int M, int N, int epi, int splits) {
   if (!narrow(M, N)) return false;

@@ -153,7 +153,7 @@ _DGRAD_OURS = os.environ.get("JMAE_DGRAD", "1") == "1"  # data-gradient GEMMs on
 
 
 NARROW_MAX_M = 4096  # csrc/gemm.hip g_narrow_max_m: below it the NT GEMMs take 128 x 192 tiles
-NARROW_SPLITK = False  # A/B: split-K from M = 256 on the narrow tiles (csrc/gemm.hip g_narrow_splitk)
+NARROW_SPLITK = True  # split-K from M = 256 on the narrow tiles too (csrc/gemm.hip g_narrow_splitk)
 _NARROW_FUSED_MIN_TILES = 160  # a fused GELU epilogue needs the tiles alone to fill most CUs
 
 
