@@ -93,12 +93,13 @@ int jm_gemm_tn_group_plan(const TnGroup& grp, int M, int* S_out);
 int jm_gemm_tn_group(TnGroup grp, int M, int sps, int S, hipStream_t st);
 int jm_gemm_tn(const uint16_t* A, long lda, const uint16_t* B, long ldb, int M, int N, int K, int sps, int S,
                float* G, long ldo, float* partial, hipStream_t st);
-struct TnSegs {
-  const uint16_t* a[32];
-  const uint16_t* b[32];
+struct TnSegs {  // gemm_tn.hip layout
+  const uint16_t* a[64];
+  const uint16_t* b[64];
   int rows;
   int n;
 };
+int jm_gemm_tn_group_seg(TnGroup grp, const TnSegs& segs, int sps, int S, hipStream_t st);
 int jm_gemm_tn_seg(const TnSegs& segs, long lda, long ldb, int N, int K, int sps, int S, float* G, long ldo,
                    float* partial, hipStream_t st);
 int jm_patchify_normalize(const uint8_t* img, float* out, int B, int H, int W, int p, hipStream_t st);
@@ -895,6 +896,62 @@ int64_t gemm_tn_wgrad_group(std::vector<torch::Tensor> dys, std::vector<torch::T
   return S;
 }
 
+// g_p[N_p, K_p] += sum_i dys[p][i]^T xs[p][i] for two problems whose reduction rows are the same
+// per-layer blocks (the shared jumbo MLP's W1 and W2 gradients over all layers), one grid
+int64_t gemm_tn_wgrad_seg_group(std::vector<std::vector<torch::Tensor>> dys, std::vector<std::vector<torch::Tensor>> xs,
+                                std::vector<torch::Tensor> gs) {
+  const int np = (int)dys.size();
+  TORCH_CHECK(np >= 1 && np <= 2 && (int)xs.size() == np && (int)gs.size() == np, "gemm_tn_wgrad_seg_group: 1-2 problems");
+  const int nb = (int)dys[0].size();
+  TORCH_CHECK(nb >= 1 && nb <= 32, "gemm_tn_wgrad_seg_group: 1..32 blocks");
+  const int rows = dys[0][0].size(0);
+  TnSegs segs{};
+  segs.rows = rows;
+  segs.n = nb;
+  TnGroup grp{};
+  grp.n = np;
+  long total = 0;
+  for (int p = 0; p < np; ++p) {
+    TORCH_CHECK((int)dys[p].size() == nb && (int)xs[p].size() == nb, "gemm_tn_wgrad_seg_group: block counts differ");
+    const auto &d0 = dys[p][0], &x0 = xs[p][0];
+    const int N = d0.size(1), K = x0.size(1);
+    for (int i = 0; i < nb; ++i) {
+      const auto &d = dys[p][i], &x = xs[p][i];
+      CHECK_DT(d, torch::kBFloat16);
+      CHECK_DT(x, torch::kBFloat16);
+      TORCH_CHECK(d.dim() == 2 && x.dim() == 2 && d.size(0) == rows && x.size(0) == rows && d.size(1) == N &&
+                      x.size(1) == K && d.stride(1) == 1 && x.stride(1) == 1 && d.stride(0) == d0.stride(0) &&
+                      x.stride(0) == x0.stride(0),
+                  "gemm_tn_wgrad_seg_group: block shapes / strides differ");
+      segs.a[32 * p + i] = bf(d);
+      segs.b[32 * p + i] = bf(x);
+    }
+    const auto& g = gs[p];
+    TORCH_CHECK(g.is_contiguous() && g.scalar_type() == torch::kFloat32 && g.numel() == (long)N * K,
+                "gemm_tn_wgrad_seg_group g");
+    grp.lda[p] = d0.stride(0);
+    grp.ldb[p] = x0.stride(0);
+    grp.N[p] = N;
+    grp.K[p] = K;
+    total += (long)N * K;
+  }
+  int S = 1;
+  const int sps = jm_gemm_tn_group_plan(grp, rows * nb, &S);
+  torch::Tensor part;
+  if (S > 1) part = torch::empty({(long)S * total}, gs[0].options());
+  long off = 0;
+  for (int p = 0; p < np; ++p) {
+    grp.out[p] = S > 1 ? part.data_ptr<float>() + off : gs[p].data_ptr<float>();
+    off += (long)S * grp.N[p] * grp.K[p];
+  }
+  check_rc(jm_gemm_tn_group_seg(grp, segs, sps, S, stream()), "gemm_tn_wgrad_seg_group");
+  if (S > 1)
+    for (int p = 0; p < np; ++p)
+      check_rc(jm_splitk_reduce_add(grp.out[p], gs[p].data_ptr<float>(), (long)grp.N[p] * grp.K[p], S, stream()),
+               "gemm_tn_wgrad_seg_group reduce");
+  return S;
+}
+
 // x1 = x + mask*scale*y ([B,T,D] fp32, fresh contiguous); h / mean / rstd = LN of rows t >= T0
 std::vector<torch::Tensor> residual_ln_fwd(torch::Tensor x, torch::Tensor y, c10::optional<torch::Tensor> scale,
                                            c10::optional<torch::Tensor> mask, torch::Tensor gamma,
@@ -980,6 +1037,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("attn_set_max_seq", &jm_attn_set_max_seq);
   m.def("gemm_tn_wgrad", &gemm_tn_wgrad);
   m.def("gemm_tn_wgrad_seg", &gemm_tn_wgrad_seg);
+  m.def("gemm_tn_wgrad_seg_group", &gemm_tn_wgrad_seg_group, "grouped segmented weight gradients (<= 2 problems)");
   m.def("gemm_tn_wgrad_group", &gemm_tn_wgrad_group, "grouped weight gradients over one M (<= 4 problems)");
   m.def("gemm_set_variant", &jm_gemm_set_variant, py::arg("nt64"), py::arg("group") = 8,
         "nt64 = 1: every NT launch on the 64-deep main loop (tests); group: row tiles per column sweep");

@@ -99,9 +99,10 @@ struct TFrags {
 // Segmented M (the batched shared-jumbo-MLP weight gradient): the reduction rows are the
 // concatenation of ``n`` separately allocated [rows, lda] / [rows, ldb] blocks (one per layer),
 // read in place instead of being copied into one tensor first.
+// A grouped segmented launch (jm_gemm_tn_group_seg) keeps problem p's blocks at entries 32 p + i.
 struct TnSegs {
-  const uint16_t* a[32];
-  const uint16_t* b[32];
+  const uint16_t* a[64];
+  const uint16_t* b[64];
   int rows;  // rows per block, multiple of the 32-row step
   int n;
 };
@@ -313,10 +314,12 @@ __global__ __launch_bounds__(NTH, 1) void gemm_tn4_kernel(const uint16_t* __rest
   const int wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
   const int split = wg / tiles;
   int tile = wg - split * tiles;
+  int soff = 0;  // GRP && SEG: this problem's entries in segs
   if constexpr (GRP) {
     int p = 0;
     while (p + 1 < grp.n && tile >= grp.tile0[p + 1]) ++p;
     tile -= grp.tile0[p];
+    soff = 32 * p;
     A = grp.a[p];
     B = grp.b[p];
     lda = grp.lda[p];
@@ -334,8 +337,8 @@ __global__ __launch_bounds__(NTH, 1) void gemm_tn4_kernel(const uint16_t* __rest
   int nk = (rows + 63) / 64;
   nk += nk & 1;  // even (pairs of K-tiles); rows past the split read zeros
 
-  const __amdgpu_buffer_rsrc_t ra = make_rsrc(SEG ? segs.a[0] : A + (long)m_begin * lda + n0, SEG ? 0 : (long)rows * lda * 2);
-  const __amdgpu_buffer_rsrc_t rb = make_rsrc(SEG ? segs.b[0] : B + (long)m_begin * ldb + k0, SEG ? 0 : (long)rows * ldb * 2);
+  const __amdgpu_buffer_rsrc_t ra = make_rsrc(SEG ? segs.a[soff] : A + (long)m_begin * lda + n0, SEG ? 0 : (long)rows * lda * 2);
+  const __amdgpu_buffer_rsrc_t rb = make_rsrc(SEG ? segs.b[soff] : B + (long)m_begin * ldb + k0, SEG ? 0 : (long)rows * ldb * 2);
   // glds pieces: 4 rows x 256 B; slot rows pr = (2 wave + rr) * 4 + (lane >> 4); LDS chunk lane & 15
   // holds logical chunk c = (lane & 15) ^ tswz(pr) -> column of the half's segment
   uint32_t a_src[2][2], b_src[2][2];  // [half][rr] byte offsets
@@ -358,11 +361,11 @@ __global__ __launch_bounds__(NTH, 1) void gemm_tn4_kernel(const uint16_t* __rest
       const int loc = row - sg * segs.rows;
       const int left = row < m_begin + rows ? min(segs.rows - loc, m_begin + rows - row) : 0;
       if constexpr (S < 2) {
-        const __amdgpu_buffer_rsrc_t sra = make_rsrc(segs.a[sg] + (long)loc * lda + n0, (long)left * lda * 2);
+        const __amdgpu_buffer_rsrc_t sra = make_rsrc(segs.a[soff + sg] + (long)loc * lda + n0, (long)left * lda * 2);
 #pragma unroll
         for (int rr = 0; rr < 2; ++rr) blds16(sra, a_src[S][rr], 0, l + rr * 4 * 128);
       } else {
-        const __amdgpu_buffer_rsrc_t srb = make_rsrc(segs.b[sg] + (long)loc * ldb + k0, (long)left * ldb * 2);
+        const __amdgpu_buffer_rsrc_t srb = make_rsrc(segs.b[soff + sg] + (long)loc * ldb + k0, (long)left * ldb * 2);
 #pragma unroll
         for (int rr = 0; rr < 2; ++rr) blds16(srb, b_src[S - 2][rr], 0, l + rr * 4 * 128);
       }
@@ -651,6 +654,35 @@ int jm_gemm_tn_group(TnGroup grp, int M, int sps, int S, hipStream_t st) {
     set_smem_once(gemm_tn4_kernel<0, false, true>, a);
     gemm_tn4_kernel<0, false, true><<<wgs, NTH, sm, st>>>(nullptr, 0, nullptr, 0, M, 0, 0, sps, nullptr, 0, 0,
                                                           TnSegs{}, grp);
+  }
+  return 0;
+}
+
+// Grouped + segmented (the batched jumbo-MLP weight gradients W1 and W2 of all layers in one
+// grid): problem p's per-layer blocks at segs.a / segs.b[32 p + i], one M split (S == 1, the
+// gradients accumulated in place) when the problems' tiles fill the chip, else partial slices.
+int jm_gemm_tn_group_seg(TnGroup grp, const TnSegs& segs, int sps, int S, hipStream_t st) {
+  const int M = segs.rows * segs.n;
+  if (grp.n < 1 || grp.n > 2 || segs.n < 1 || segs.n > 32 || segs.rows % 64 || sps % 4 || sps < 4 || S < 1)
+    return -1;
+  grp.tile0[0] = 0;
+  for (int p = 0; p < grp.n; ++p) {
+    if (grp.N[p] % TN_ || grp.K[p] % TK_ || grp.out[p] == nullptr) return -1;
+    if ((long)segs.rows * grp.lda[p] * 2 >= (1L << 32) || (long)segs.rows * grp.ldb[p] * 2 >= (1L << 32)) return -2;
+    grp.tile0[p + 1] = grp.tile0[p] + (grp.N[p] / TN_) * (grp.K[p] / TK_);
+  }
+  const size_t sm = jm_gemm_tn_smem();
+  const int wgs = grp.tile0[grp.n] * S;
+  if (S == 1) {
+    static bool a = false;
+    set_smem_once(gemm_tn4_kernel<1, true, true>, a);
+    gemm_tn4_kernel<1, true, true><<<wgs, NTH, sm, st>>>(nullptr, 0, nullptr, 0, M, 0, 0, sps, nullptr, 0, 0, segs,
+                                                         grp);
+  } else {
+    static bool a = false;
+    set_smem_once(gemm_tn4_kernel<0, true, true>, a);
+    gemm_tn4_kernel<0, true, true><<<wgs, NTH, sm, st>>>(nullptr, 0, nullptr, 0, M, 0, 0, sps, nullptr, 0, 0, segs,
+                                                         grp);
   }
   return 0;
 }

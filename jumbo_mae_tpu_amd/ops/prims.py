@@ -300,13 +300,40 @@ def _seg_ok(dys, xs) -> bool:
             and d0.stride(1) == 1 and x0.stride(1) == 1)
 
 
+GROUP_JUMBO_WGRAD = os.environ.get("JMAE_GROUP_JUMBO_WGRAD", "1") == "1"  # A/B switch
+
+
+def _flush_seg_group(todo: list) -> list:
+    """Batched weight gradients of two shared weights over the same per-layer row blocks (the
+    jumbo MLP's W1 and W2) as ONE grouped segmented grid, when neither needs chunked partial
+    readiness for the DP reducer: twice the tiles, so no M split and no partial slices to reduce
+    (gemm_tn_wgrad_seg_group).  Returns the entries left for the per-handle path."""
+    if not GROUP_JUMBO_WGRAD or len(todo) != 2:
+        return todo
+    (h1, p1), (h2, p2) = todo
+    if any(h.store.partial_hooks and len(h.segs) == 1 for h in (h1, h2)) or len(p1) != len(p2):
+        return todo
+    d1, x1 = [p[0] for p in p1], [p[1] for p in p1]
+    d2, x2 = [p[0] for p in p2], [p[1] for p in p2]
+    if not (_seg_ok(d1, x1) and _seg_ok(d2, x2) and d1[0].shape[0] == d2[0].shape[0]
+            and d1[0].shape[0] % 64 == 0 and h1.grad.is_contiguous() and h2.grad.is_contiguous()):
+        return todo
+    _ext.load().gemm_tn_wgrad_seg_group([d1, d2], [x1, x2], [h1.grad, h2.grad])
+    for h, pairs in todo:
+        for _ in pairs:
+            h.ready()
+    return []
+
+
 def flush_deferred_wgrads() -> None:
     _deferred["cb"] = False
     hs, _deferred["handles"] = _deferred["handles"], []
+    todo = []
     for h in hs:
         pairs, h.deferred = h.deferred, []
-        if not pairs:
-            continue
+        if pairs:
+            todo.append((h, pairs))
+    for h, pairs in _flush_seg_group(todo):
         dys = [p[0] for p in pairs]
         xs = [p[1] for p in pairs]
         N, K = dys[0].shape[1], xs[0].shape[1]

@@ -374,6 +374,21 @@ def test_gemm_tn_wgrad_group(ext, M, shapes):
         assert rel(g, r) < 1e-4
 
 
+@pytest.mark.parametrize("nb,rows", [(24, 512), (5, 128), (3, 64)])
+def test_gemm_tn_wgrad_seg_group(ext, nb, rows):
+    """Grouped + segmented TN weight gradients (the jumbo MLP's W1 / W2 over the per-layer row
+    blocks, read in place) == fp64 references, accumulated into existing gradients."""
+    torch.manual_seed(0)
+    shapes = [(1024, 256), (256, 1024)]
+    dys = [[(torch.rand(rows, n, device="cuda") * 2 - 1).bfloat16() for _ in range(nb)] for n, _ in shapes]
+    xs = [[(torch.rand(rows, k, device="cuda") * 2 - 1).bfloat16() for _ in range(nb)] for _, k in shapes]
+    gs = [torch.randn(n, k, device="cuda") for n, k in shapes]
+    refs = [g.double() + torch.cat(d).double().t() @ torch.cat(x).double() for g, d, x in zip(gs, dys, xs)]
+    ext.gemm_tn_wgrad_seg_group(dys, xs, gs)
+    for g, r in zip(gs, refs):
+        assert rel(g, r) < 1e-4
+
+
 @pytest.mark.parametrize("T0", [0, 3])
 @pytest.mark.parametrize("with_scale", [False, True])
 def test_residual_ln_fwd(ext, T0, with_scale):

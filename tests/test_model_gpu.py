@@ -160,7 +160,8 @@ def test_finetune_production_routing_matches_cpu():
 
 def test_paired_wgrads_match_separate():
     """Fused-block backward with consecutive weight gradients (FF2 + FF1, Wo + QKV) launched as
-    grouped TN grids (ops/prims.py paired_wgrads) == every weight gradient on its own: same
+    grouped TN grids (ops/prims.py paired_wgrads) and the batched jumbo W1 + W2 gradients as one
+    grouped segmented grid == every weight gradient on its own: same
     gradients up to fp32 summation order, same DP ``ready`` notifications per parameter."""
     from collections import Counter
     from jumbo_mae_tpu_amd.config import DecoderConfig, ViTConfig
@@ -170,13 +171,14 @@ def test_paired_wgrads_match_separate():
                    layerscale=True)
     dc = DecoderConfig(dec_layers=2, dec_dim=256, dec_heads=4, image_size=224, patch_size=16)
     m = PretrainModel(vc, dc).to("cuda", torch.bfloat16, seed=0)
-    imgs = torch.randint(0, 256, (96, 3, 224, 224), dtype=torch.uint8, device="cuda")  # 4992 / 19104 rows
+    # 6656 encoder / 25472 decoder rows (TN path); 128-row jumbo blocks (grouped segmented W1 + W2)
+    imgs = torch.randint(0, 256, (128, 3, 224, 224), dtype=torch.uint8, device="cuda")
     noise = torch.rand(196, device="cuda")
     grads, readies = [], []
-    saved = P.PAIR_WGRAD
+    saved = P.PAIR_WGRAD, P.GROUP_JUMBO_WGRAD
     try:
         for pair in (False, True):
-            P.PAIR_WGRAD = pair
+            P.PAIR_WGRAD = P.GROUP_JUMBO_WGRAD = pair
             seen = Counter()
             m.store.hooks.append(lambda h: seen.update([h.start]))
             m.store.zero_grad()
@@ -187,7 +189,7 @@ def test_paired_wgrads_match_separate():
             grads.append(m.store.grad.clone())
             readies.append(seen)
     finally:
-        P.PAIR_WGRAD = saved
+        P.PAIR_WGRAD, P.GROUP_JUMBO_WGRAD = saved
     assert readies[0] == readies[1] and sum(readies[0].values()) > 0
     a, b = grads
     assert ((a - b).norm() / a.norm()).item() < 1e-5
