@@ -84,7 +84,7 @@ class PretrainModel:
         y = self.decoder_proj(h).view(B, C + K, -1)
         dec_in = mae_ops.unshuffle_fused(y, self.mask_token, ids_restore, self.decoder.posemb_table(y.device), C)
         xd = self.decoder.blocks(dec_in, drop, det=det)
-        hd = self.decoder.dec_norm(xd[:, C:])  # [B*N, d] only patch rows are predicted
+        hd = self.decoder.dec_norm(xd, row0=C)  # [B*N, d] only patch rows are predicted
         pred = self.decoder_image_output(hd)  # [B*N, p*p*3]
         # target pixels come straight from the uint8 images (no fp32 patch tensor)
         per_patch = mae_ops.patch_mse(pred.view(B, N, -1), images_u8, cfg.patch_size, self.norm_pix_loss)

@@ -73,8 +73,8 @@ class LayerNorm:
         self.g = store.handle(store.add(path + ("scale",), (dim,), ones_, trainable=trainable))
         self.b = store.handle(store.add(path + ("bias",), (dim,), zeros_, trainable=trainable))
 
-    def __call__(self, x, out_dtype=None):
-        return Fn.layer_norm(x, self.g, self.b, out_dtype)
+    def __call__(self, x, out_dtype=None, row0: int = 0):
+        return Fn.layer_norm(x, self.g, self.b, out_dtype, row0)
 
 
 class FeedForward:

@@ -74,29 +74,38 @@ def gelu_bwd(h: torch.Tensor, da: torch.Tensor) -> torch.Tensor:
 
 # ------------------------------------------------------------------------------- layernorm
 class _LayerNorm(torch.autograd.Function):
-    """x: fp32 [B, T, D] (any strides, last dim contiguous) -> y [B*T, D] in ``out_dtype``."""
+    """x: fp32 [B, T, D] (any strides, last dim contiguous) -> y [B*(T-row0), D] in ``out_dtype``,
+    the LayerNorm of rows t >= row0.  With row0 > 0 the gradient of the whole x is returned
+    directly -- LN' written into rows >= row0 of a fresh tensor, zeros into the few rows below --
+    instead of autograd's slice backward (a full-size zero fill plus a copy of the rows)."""
 
     @staticmethod
-    def forward(ctx, x, gp, bp, hg: Handle, hb: Handle, out_dtype):
-        y, mean, rstd = P.ln_fwd(x, hg, hb, out_dtype)
+    def forward(ctx, x, gp, bp, hg: Handle, hb: Handle, out_dtype, row0=0):
+        y, mean, rstd = P.ln_fwd(x[:, row0:] if row0 else x, hg, hb, out_dtype)
         ctx.save_for_backward(x, mean, rstd)
-        ctx.hg, ctx.hb = hg, hb
+        ctx.hg, ctx.hb, ctx.row0 = hg, hb, row0
         return y
 
     @staticmethod
     def backward(ctx, dy):
         x, mean, rstd = ctx.saved_tensors
-        dx = P.ln_bwd(dy, x, mean, rstd, ctx.hg, ctx.hb)
-        return dx, None, None, None, None, None
+        r0 = ctx.row0
+        if not r0:
+            return P.ln_bwd(dy, x, mean, rstd, ctx.hg, ctx.hb), None, None, None, None, None, None
+        dx = torch.empty(x.shape, dtype=x.dtype, device=x.device)
+        dx[:, :r0].zero_()
+        P.ln_bwd(dy, x[:, r0:], mean, rstd, ctx.hg, ctx.hb, out=dx[:, r0:])
+        return dx, None, None, None, None, None, None
 
 
-def layer_norm(x: torch.Tensor, hg: Handle, hb: Handle, out_dtype=None) -> torch.Tensor:
+def layer_norm(x: torch.Tensor, hg: Handle, hb: Handle, out_dtype=None, row0: int = 0) -> torch.Tensor:
+    """LayerNorm of x (rows t >= ``row0`` of a [B, T, D] x only, when given)."""
     if x.dim() == 2:
         x = x.unsqueeze(0)
     out_dtype = out_dtype or hg.store.compute_dtype
     hg.note_use()
     hb.note_use()
-    return _LayerNorm.apply(x, hg.param, hb.param, hg, hb, out_dtype)
+    return _LayerNorm.apply(x, hg.param, hb.param, hg, hb, out_dtype, row0)
 
 
 # -------------------------------------------------------------------------------- residual
