@@ -41,7 +41,8 @@ int jm_gelu_fwd(const uint16_t* h, uint16_t* a, long n, hipStream_t st);
 int jm_gelu_bwd(const uint16_t* h, const uint16_t* da, uint16_t* dh, float* bias_grad, int M, int N, hipStream_t st,
                 int deriv = 0);
 int jm_colsum_bf16(const uint16_t* x, float* acc, int M, int N, hipStream_t st);
-int jm_splitk_reduce_add(const float* part, float* g, long n, int S, hipStream_t st);
+int jm_splitk_reduce_add(const float* part, float* g, long n, int S, hipStream_t st, int store = 0);
+int jm_zero_ranges(float* base, const long long* desc, int n, long long blocks, hipStream_t st);
 int jm_transpose_bf16(const uint16_t* src, uint16_t* dst, int R, int C, hipStream_t st);
 int jm_transpose_bf16_batch(const long long* desc, int n, int tiles, hipStream_t st);
 int jm_residual_fwd(const float* x, long sB, long sT, int B, int T, int D, const uint16_t* y, const float* scale,
@@ -90,18 +91,18 @@ void jm_gemm_set_rows(int rows);
 void jm_gemm_set_narrow_splitk(int on);
 int jm_gemm_tn_plan(int M, int N, int K, int* S_out);
 int jm_gemm_tn_group_plan(const TnGroup& grp, int M, int* S_out);
-int jm_gemm_tn_group(TnGroup grp, int M, int sps, int S, hipStream_t st);
+int jm_gemm_tn_group(TnGroup grp, int M, int sps, int S, hipStream_t st, int store);
 int jm_gemm_tn(const uint16_t* A, long lda, const uint16_t* B, long ldb, int M, int N, int K, int sps, int S,
-               float* G, long ldo, float* partial, hipStream_t st);
+               float* G, long ldo, float* partial, hipStream_t st, int store);
 struct TnSegs {  // gemm_tn.hip layout
   const uint16_t* a[64];
   const uint16_t* b[64];
   int rows;
   int n;
 };
-int jm_gemm_tn_group_seg(TnGroup grp, const TnSegs& segs, int sps, int S, hipStream_t st);
+int jm_gemm_tn_group_seg(TnGroup grp, const TnSegs& segs, int sps, int S, hipStream_t st, int store);
 int jm_gemm_tn_seg(const TnSegs& segs, long lda, long ldb, int N, int K, int sps, int S, float* G, long ldo,
-                   float* partial, hipStream_t st);
+                   float* partial, hipStream_t st, int store);
 int jm_patchify_normalize(const uint8_t* img, float* out, int B, int H, int W, int p, hipStream_t st);
 int jm_gather_patches(const uint8_t* img, const int* ids, long idsB, uint16_t* out, int B, int K, int H, int W, int p,
                       hipStream_t st);
@@ -792,7 +793,8 @@ void transpose_bf16_batch(torch::Tensor desc, int64_t tiles) {
 
 // weight gradient G[N, K] += dy[M, N]^T . x[M, K] on the TN MFMA kernel (split over M, fp32
 // partial tiles reduced into G); returns the number of M splits used
-int64_t gemm_tn_wgrad(torch::Tensor dy, torch::Tensor x, torch::Tensor g) {
+// store: g = dy^T . x (g's old contents ignored: its first contribution of the step)
+int64_t gemm_tn_wgrad(torch::Tensor dy, torch::Tensor x, torch::Tensor g, bool store) {
   CHECK_DT(dy, torch::kBFloat16);
   CHECK_DT(x, torch::kBFloat16);
   TORCH_CHECK(dy.dim() == 2 && x.dim() == 2 && dy.size(0) == x.size(0), "gemm_tn_wgrad: dy [M,N], x [M,K]");
@@ -805,16 +807,17 @@ int64_t gemm_tn_wgrad(torch::Tensor dy, torch::Tensor x, torch::Tensor g) {
   const int SP = S;  // fp32 partial slices, reduced into g
   if (S > 1) part = torch::empty({SP, (long)N * K}, g.options());
   const int done = jm_gemm_tn(bf(dy), dy.stride(0), bf(x), x.stride(0), M, N, K, sps, S, g.data_ptr<float>(), K,
-                              S > 1 ? part.data_ptr<float>() : nullptr, stream());
+                              S > 1 ? part.data_ptr<float>() : nullptr, stream(), store);
   check_rc(done, "gemm_tn_wgrad");
-  if (S > 1) check_rc(jm_splitk_reduce_add(part.data_ptr<float>(), g.data_ptr<float>(), (long)N * K, SP, stream()),
-                      "gemm_tn_wgrad reduce");
+  if (S > 1)
+    check_rc(jm_splitk_reduce_add(part.data_ptr<float>(), g.data_ptr<float>(), (long)N * K, SP, stream(), store),
+             "gemm_tn_wgrad reduce");
   return S;
 }
 
 // g[N, K] += sum_i dys[i]^T xs[i]: the reduction rows are the concatenation of the per-layer
 // blocks (all [rows, N] / [rows, K], same strides), read in place (no torch.cat copy)
-int64_t gemm_tn_wgrad_seg(std::vector<torch::Tensor> dys, std::vector<torch::Tensor> xs, torch::Tensor g) {
+int64_t gemm_tn_wgrad_seg(std::vector<torch::Tensor> dys, std::vector<torch::Tensor> xs, torch::Tensor g, bool store) {
   TORCH_CHECK(!dys.empty() && dys.size() == xs.size() && dys.size() <= 32, "gemm_tn_wgrad_seg: 1..32 blocks");
   const auto& d0 = dys[0];
   const auto& x0 = xs[0];
@@ -842,18 +845,35 @@ int64_t gemm_tn_wgrad_seg(std::vector<torch::Tensor> dys, std::vector<torch::Ten
   const int SP = S;
   if (S > 1) part = torch::empty({SP, (long)N * K}, g.options());
   const int done = jm_gemm_tn_seg(segs, d0.stride(0), x0.stride(0), N, K, sps, S, g.data_ptr<float>(), K,
-                                  S > 1 ? part.data_ptr<float>() : nullptr, stream());
+                                  S > 1 ? part.data_ptr<float>() : nullptr, stream(), store);
   check_rc(done, "gemm_tn_wgrad_seg");
-  if (S > 1) check_rc(jm_splitk_reduce_add(part.data_ptr<float>(), g.data_ptr<float>(), (long)N * K, SP, stream()),
-                      "gemm_tn_wgrad_seg reduce");
+  if (S > 1)
+    check_rc(jm_splitk_reduce_add(part.data_ptr<float>(), g.data_ptr<float>(), (long)N * K, SP, stream(), store),
+             "gemm_tn_wgrad_seg reduce");
   return S;
 }
 
 // g_p[N_p, K_p] += dys[p]^T . xs[p] for up to 4 problems over the same M rows in ONE grid (e.g. a
 // layer's FF1 + FF2 or QKV + Wo weight gradients): fewer M splits per problem than separate
 // launches -> fewer fp32 partial slices to write and reduce; returns the split count
+// One-split grouped launches store into every G or accumulate into every G (one kernel variant):
+// with mixed store flags the store problems' G are zeroed first and all accumulate.  Returns the
+// launch's store mode.
+int group_stores(const std::vector<bool>& stores, const std::vector<torch::Tensor>& gs, int S, int n) {
+  if (S > 1 || stores.empty()) return 0;
+  int ns = 0;
+  for (int p = 0; p < n; ++p) ns += p < (int)stores.size() && stores[p];
+  if (ns == n) return 1;
+  for (int p = 0; p < n; ++p)
+    if (p < (int)stores.size() && stores[p])
+      TORCH_CHECK(hipMemsetAsync(gs[p].data_ptr<float>(), 0, gs[p].numel() * 4, stream()) == hipSuccess,
+                  "group_stores: memset");
+  return 0;
+}
+
+// stores[p]: g_p = its product (first contribution of the step) instead of +=
 int64_t gemm_tn_wgrad_group(std::vector<torch::Tensor> dys, std::vector<torch::Tensor> xs,
-                            std::vector<torch::Tensor> gs) {
+                            std::vector<torch::Tensor> gs, std::vector<bool> stores) {
   const int n = (int)dys.size();
   TORCH_CHECK(n >= 1 && n <= 4 && (int)xs.size() == n && (int)gs.size() == n, "gemm_tn_wgrad_group: 1..4 problems");
   const int M = dys[0].size(0);
@@ -888,10 +908,12 @@ int64_t gemm_tn_wgrad_group(std::vector<torch::Tensor> dys, std::vector<torch::T
     grp.out[p] = S > 1 ? part.data_ptr<float>() + off : gs[p].data_ptr<float>();
     off += (long)S * grp.N[p] * grp.K[p];
   }
-  check_rc(jm_gemm_tn_group(grp, M, sps, S, stream()), "gemm_tn_wgrad_group");
+  const int all_store = group_stores(stores, gs, S, n);
+  check_rc(jm_gemm_tn_group(grp, M, sps, S, stream(), all_store), "gemm_tn_wgrad_group");
   if (S > 1)
     for (int p = 0; p < n; ++p)
-      check_rc(jm_splitk_reduce_add(grp.out[p], gs[p].data_ptr<float>(), (long)grp.N[p] * grp.K[p], S, stream()),
+      check_rc(jm_splitk_reduce_add(grp.out[p], gs[p].data_ptr<float>(), (long)grp.N[p] * grp.K[p], S, stream(),
+                                    p < (int)stores.size() && stores[p]),
                "gemm_tn_wgrad_group reduce");
   return S;
 }
@@ -899,7 +921,7 @@ int64_t gemm_tn_wgrad_group(std::vector<torch::Tensor> dys, std::vector<torch::T
 // g_p[N_p, K_p] += sum_i dys[p][i]^T xs[p][i] for two problems whose reduction rows are the same
 // per-layer blocks (the shared jumbo MLP's W1 and W2 gradients over all layers), one grid
 int64_t gemm_tn_wgrad_seg_group(std::vector<std::vector<torch::Tensor>> dys, std::vector<std::vector<torch::Tensor>> xs,
-                                std::vector<torch::Tensor> gs) {
+                                std::vector<torch::Tensor> gs, std::vector<bool> stores) {
   const int np = (int)dys.size();
   TORCH_CHECK(np >= 1 && np <= 2 && (int)xs.size() == np && (int)gs.size() == np, "gemm_tn_wgrad_seg_group: 1-2 problems");
   const int nb = (int)dys[0].size();
@@ -944,12 +966,25 @@ int64_t gemm_tn_wgrad_seg_group(std::vector<std::vector<torch::Tensor>> dys, std
     grp.out[p] = S > 1 ? part.data_ptr<float>() + off : gs[p].data_ptr<float>();
     off += (long)S * grp.N[p] * grp.K[p];
   }
-  check_rc(jm_gemm_tn_group_seg(grp, segs, sps, S, stream()), "gemm_tn_wgrad_seg_group");
+  const int all_store = group_stores(stores, gs, S, np);
+  check_rc(jm_gemm_tn_group_seg(grp, segs, sps, S, stream(), all_store), "gemm_tn_wgrad_seg_group");
   if (S > 1)
     for (int p = 0; p < np; ++p)
-      check_rc(jm_splitk_reduce_add(grp.out[p], gs[p].data_ptr<float>(), (long)grp.N[p] * grp.K[p], S, stream()),
+      check_rc(jm_splitk_reduce_add(grp.out[p], gs[p].data_ptr<float>(), (long)grp.N[p] * grp.K[p], S, stream(),
+                                    p < (int)stores.size() && stores[p]),
                "gemm_tn_wgrad_seg_group reduce");
   return S;
+}
+
+// zero the (offset, count) float ranges of ``base`` listed in desc (int64 [n, 2] on the device)
+void zero_ranges(torch::Tensor base, torch::Tensor desc, int64_t blocks) {
+  CHECK_CONTIG(base);
+  CHECK_DT(base, torch::kFloat32);
+  TORCH_CHECK(desc.is_cuda() && desc.scalar_type() == torch::kInt64 && desc.dim() == 2 && desc.size(1) == 2,
+              "zero_ranges: desc int64 [n, 2] on the device");
+  check_rc(jm_zero_ranges(base.data_ptr<float>(), reinterpret_cast<const long long*>(desc.data_ptr<int64_t>()),
+                          (int)desc.size(0), blocks, stream()),
+           "zero_ranges");
 }
 
 // x1 = x + mask*scale*y ([B,T,D] fp32, fresh contiguous); h / mean / rstd = LN of rows t >= T0
@@ -1035,10 +1070,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("dbias") = py::none());
   m.def("attn_max_seq", &jm_attn_max_seq);
   m.def("attn_set_max_seq", &jm_attn_set_max_seq);
-  m.def("gemm_tn_wgrad", &gemm_tn_wgrad);
-  m.def("gemm_tn_wgrad_seg", &gemm_tn_wgrad_seg);
-  m.def("gemm_tn_wgrad_seg_group", &gemm_tn_wgrad_seg_group, "grouped segmented weight gradients (<= 2 problems)");
-  m.def("gemm_tn_wgrad_group", &gemm_tn_wgrad_group, "grouped weight gradients over one M (<= 4 problems)");
+  m.def("gemm_tn_wgrad", &gemm_tn_wgrad, py::arg("dy"), py::arg("x"), py::arg("g"), py::arg("store") = false);
+  m.def("gemm_tn_wgrad_seg", &gemm_tn_wgrad_seg, py::arg("dys"), py::arg("xs"), py::arg("g"), py::arg("store") = false);
+  m.def("zero_ranges", &zero_ranges, "zero float ranges of a flat buffer (one launch)");
+  m.def("gemm_tn_wgrad_seg_group", &gemm_tn_wgrad_seg_group, py::arg("dys"), py::arg("xs"), py::arg("gs"),
+        py::arg("stores") = std::vector<bool>{}, "grouped segmented weight gradients (<= 2 problems)");
+  m.def("gemm_tn_wgrad_group", &gemm_tn_wgrad_group, py::arg("dys"), py::arg("xs"), py::arg("gs"),
+        py::arg("stores") = std::vector<bool>{}, "grouped weight gradients over one M (<= 4 problems)");
   m.def("gemm_set_variant", &jm_gemm_set_variant, py::arg("nt64"), py::arg("group") = 8,
         "nt64 = 1: every NT launch on the 64-deep main loop (tests); group: row tiles per column sweep");
   m.def("gemm_set_tail", &jm_gemm_set_tail);

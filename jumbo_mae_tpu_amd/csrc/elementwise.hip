@@ -316,16 +316,17 @@ __global__ __launch_bounds__(256) void splitk_reduce_add_kernel(const float* __r
 // partial slices and g -- issued before the first add: the loop form kept two 16-B loads in flight
 // per thread and ran the weight-gradient reductions at ~4.8 TB/s although the slices were just
 // written (MALL-resident).
-template <int S>
+// STORE: g = sum (g is not read: the first gradient contribution of a step, see jm_zero_ranges)
+template <int S, bool STORE = false>
 __global__ __launch_bounds__(256) void splitk_reduce_add_s_kernel(const float* __restrict__ part,
                                                                   float* __restrict__ g, long n4) {
   const long i = blockIdx.x * 256L + threadIdx.x;
   if (i >= n4) return;
   const long n = n4 * 4;
-  float v[S][4], o[4];
+  float v[S][4], o[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int s = 0; s < S; ++s) load4(part + (long)s * n + i * 4, v[s]);
-  load4(g + i * 4, o);
+  if (!STORE) load4(g + i * 4, o);
 #pragma unroll
   for (int s = 0; s < S; ++s)
 #pragma unroll
@@ -334,25 +335,56 @@ __global__ __launch_bounds__(256) void splitk_reduce_add_s_kernel(const float* _
 }
 }  // namespace
 
-int jm_splitk_reduce_add(const float* part, float* g, long n, int S, hipStream_t st) {
+// g[i] (+)= sum_s part[s][i]; store: g[i] = sum (g not read; smaller / longer-S shapes zero g first)
+int jm_splitk_reduce_add(const float* part, float* g, long n, int S, hipStream_t st, int store) {
   if (n % 4) return -1;
   const long n4 = n / 4;
   if (S >= 1 && S <= 16 && n4 >= 256L * 256) {  // large slices: the all-loads-first kernel
     const unsigned nb = (unsigned)((n4 + 255) / 256);
     switch (S) {
-#define JM_SKR(SS) \
-  case SS: splitk_reduce_add_s_kernel<SS><<<nb, 256, 0, st>>>(part, g, n4); return 0;
+#define JM_SKR(SS)                                                                     \
+  case SS:                                                                             \
+    if (store) splitk_reduce_add_s_kernel<SS, true><<<nb, 256, 0, st>>>(part, g, n4);  \
+    else splitk_reduce_add_s_kernel<SS><<<nb, 256, 0, st>>>(part, g, n4);              \
+    return 0;
       JM_SKR(1) JM_SKR(2) JM_SKR(3) JM_SKR(4) JM_SKR(5) JM_SKR(6) JM_SKR(7) JM_SKR(8)
       JM_SKR(9) JM_SKR(10) JM_SKR(11) JM_SKR(12) JM_SKR(13) JM_SKR(14) JM_SKR(15) JM_SKR(16)
 #undef JM_SKR
       default: break;
     }
   }
+  if (store) (void)hipMemsetAsync(g, 0, n * sizeof(float), st);
   long blocks = (n4 + 255) / 256;
   if (blocks > 4096) blocks = 4096;
   int ys = 1;  // slice the partials until the launch has ~512 workgroups of >= 8 rows each
   while (blocks * ys < 512 && S / (ys * 2) >= 8) ys *= 2;
   splitk_reduce_add_kernel<<<dim3((unsigned)blocks, ys), 256, 0, st>>>(part, g, n4, S);
+  return 0;
+}
+
+// ------------------------------------------------------------------ zero ranges
+// The per-step gradient reset of every flat-buffer range NOT written by a store-mode weight
+// gradient (ParamStore.zero_grad): desc int64 [n][2] = (offset, count) in floats, one launch;
+// block b zeroes 4096 floats of the range that owns it (first block of range r: desc-order prefix).
+namespace {
+__global__ __launch_bounds__(256) void zero_ranges_kernel(float* __restrict__ base, const long long* __restrict__ desc,
+                                                          int n) {
+  long long b = blockIdx.x;
+  int r = 0;
+  for (; r < n; ++r) {
+    const long long nb = (desc[2 * r + 1] + 4095) / 4096;
+    if (b < nb) break;
+    b -= nb;
+  }
+  if (r >= n) return;
+  const long long off = desc[2 * r], cnt = desc[2 * r + 1];
+  for (long long i = b * 4096 + threadIdx.x; i < (b + 1) * 4096 && i < cnt; i += 256) base[off + i] = 0.f;
+}
+}  // namespace
+
+int jm_zero_ranges(float* base, const long long* desc, int n, long long blocks, hipStream_t st) {
+  if (n <= 0 || blocks <= 0) return 0;
+  zero_ranges_kernel<<<(unsigned)blocks, 256, 0, st>>>(base, desc, n);
   return 0;
 }
 

@@ -576,12 +576,25 @@ void set_smem_once(KERN k, bool& done) {
 
 // the 4-phase kernel (whole 128-row units, 64-row segments) or the r1 32-row-step kernel
 // returns 0 (the caller reduces the S partial slices into G when S > 1), < 0 on error
+// store (S == 1): G = the product (the split-0 store kernel into G instead of the accumulating one)
 template <bool SEG>
 int launch_tn(const uint16_t* A, long lda, const uint16_t* B, long ldb, int M, int N, int K, int sps, int S,
-              float* G, long ldo, float* partial, const TnSegs& segs, bool p4, hipStream_t st) {
+              float* G, long ldo, float* partial, const TnSegs& segs, bool p4, hipStream_t st, bool store = false) {
   const int tiles = (N / TN_) * (K / TK_);
   const size_t sm = jm_gemm_tn_smem();
   if (S > 1 && partial == nullptr) return -3;
+  if (S == 1 && store) {
+    if (p4) {
+      static bool a = false;
+      set_smem_once(gemm_tn4_kernel<0, SEG>, a);
+      gemm_tn4_kernel<0, SEG><<<tiles, NTH, sm, st>>>(A, lda, B, ldb, M, N, K, sps, G, ldo, 0, segs);
+    } else {
+      static bool a = false;
+      set_smem_once(gemm_tn_kernel<0, SEG>, a);
+      gemm_tn_kernel<0, SEG><<<tiles, NTH, sm, st>>>(A, lda, B, ldb, M, N, K, sps, G, ldo, 0, segs);
+    }
+    return 0;
+  }
   if (p4) {
     if (S == 1) {
       static bool a = false;
@@ -613,20 +626,20 @@ int launch_tn(const uint16_t* A, long lda, const uint16_t* B, long ldb, int M, i
 // split reduction (profiles/r2_tn_atomic.txt), split 0 into G (r1_ab_tn_acc0.txt), the last-arriving
 // split adding the other slices in the kernel (r3e_summary_vitl_b512_fused_reductions.txt).
 int jm_gemm_tn(const uint16_t* A, long lda, const uint16_t* B, long ldb, int M, int N, int K, int sps, int S,
-               float* G, long ldo, float* partial, hipStream_t st) {
+               float* G, long ldo, float* partial, hipStream_t st, int store) {
   if (N % TN_ || K % TK_ || M <= 0) return -1;
   if ((long)M * lda * 2 >= (1L << 32) || (long)M * ldb * 2 >= (1L << 32)) return -2;
-  return launch_tn<false>(A, lda, B, ldb, M, N, K, sps, S, G, ldo, partial, TnSegs{}, sps % 4 == 0, st);
+  return launch_tn<false>(A, lda, B, ldb, M, N, K, sps, S, G, ldo, partial, TnSegs{}, sps % 4 == 0, st, store);
 }
 
 // Segmented-M variant of jm_gemm_tn: A / B rows come from segs (n blocks of segs.rows rows).
 int jm_gemm_tn_seg(const TnSegs& segs, long lda, long ldb, int N, int K, int sps, int S, float* G, long ldo,
-                   float* partial, hipStream_t st) {
+                   float* partial, hipStream_t st, int store) {
   if (N % TN_ || K % TK_ || segs.n < 1 || segs.n > 32 || segs.rows % BS) return -1;
   if ((long)segs.rows * lda * 2 >= (1L << 32) || (long)segs.rows * ldb * 2 >= (1L << 32)) return -2;
   const int M = segs.rows * segs.n;
   return launch_tn<true>(nullptr, lda, nullptr, ldb, M, N, K, sps, S, G, ldo, partial, segs,
-                         sps % 4 == 0 && segs.rows % 64 == 0, st);
+                         sps % 4 == 0 && segs.rows % 64 == 0, st, store);
 }
 
 // Grouped launch of up to 4 TN problems over the same M rows (e.g. the FF1 and FF2 weight
@@ -634,7 +647,7 @@ int jm_gemm_tn_seg(const TnSegs& segs, long lda, long ldb, int N, int K, int sps
 // so each problem needs half the splits -- half the fp32 partial slices written and reduced.
 // S > 1: grp.out[p] = the [S][N_p K_p] partial workspace (the caller reduces into G_p); S == 1:
 // grp.out[p] = G_p, accumulated in place.
-int jm_gemm_tn_group(TnGroup grp, int M, int sps, int S, hipStream_t st) {
+int jm_gemm_tn_group(TnGroup grp, int M, int sps, int S, hipStream_t st, int store) {
   if (grp.n < 1 || grp.n > 4 || M <= 0 || sps % 4 || sps < 4 || S < 1) return -1;
   grp.tile0[0] = 0;
   for (int p = 0; p < grp.n; ++p) {
@@ -644,7 +657,7 @@ int jm_gemm_tn_group(TnGroup grp, int M, int sps, int S, hipStream_t st) {
   }
   const size_t sm = jm_gemm_tn_smem();
   const int wgs = grp.tile0[grp.n] * S;
-  if (S == 1) {
+  if (S == 1 && !store) {
     static bool a = false;
     set_smem_once(gemm_tn4_kernel<1, false, true>, a);
     gemm_tn4_kernel<1, false, true><<<wgs, NTH, sm, st>>>(nullptr, 0, nullptr, 0, M, 0, 0, sps, nullptr, 0, 0,
@@ -661,7 +674,7 @@ int jm_gemm_tn_group(TnGroup grp, int M, int sps, int S, hipStream_t st) {
 // Grouped + segmented (the batched jumbo-MLP weight gradients W1 and W2 of all layers in one
 // grid): problem p's per-layer blocks at segs.a / segs.b[32 p + i], one M split (S == 1, the
 // gradients accumulated in place) when the problems' tiles fill the chip, else partial slices.
-int jm_gemm_tn_group_seg(TnGroup grp, const TnSegs& segs, int sps, int S, hipStream_t st) {
+int jm_gemm_tn_group_seg(TnGroup grp, const TnSegs& segs, int sps, int S, hipStream_t st, int store) {
   const int M = segs.rows * segs.n;
   if (grp.n < 1 || grp.n > 2 || segs.n < 1 || segs.n > 32 || segs.rows % 64 || sps % 4 || sps < 4 || S < 1)
     return -1;
@@ -673,7 +686,7 @@ int jm_gemm_tn_group_seg(TnGroup grp, const TnSegs& segs, int sps, int S, hipStr
   }
   const size_t sm = jm_gemm_tn_smem();
   const int wgs = grp.tile0[grp.n] * S;
-  if (S == 1) {
+  if (S == 1 && !store) {
     static bool a = false;
     set_smem_once(gemm_tn4_kernel<1, true, true>, a);
     gemm_tn4_kernel<1, true, true><<<wgs, NTH, sm, st>>>(nullptr, 0, nullptr, 0, M, 0, 0, sps, nullptr, 0, 0, segs,

@@ -64,6 +64,9 @@ def identity(a: np.ndarray) -> np.ndarray:
     return a
 
 
+# store-mode gradients (ParamStore.zero_grad; A/B switch JMAE_STORE_GRADS=0 zeroes the whole buffer)
+STORE_GRADS = os.environ.get("JMAE_STORE_GRADS", "1") == "1"
+
 # Handle.weight_t copies refreshed in one batched launch (A/B switch, JMAE_WT_BATCH=0 disables)
 BATCH_TRANSPOSES = os.environ.get("JMAE_WT_BATCH", "1") == "1"
 
@@ -85,6 +88,10 @@ class Handle:
         self._wt_version = -1
         self.defer_wgrad = False   # batch this weight's gradient GEMMs (weights shared by layers)
         self.deferred: list = []   # queued (dy, x) pairs of the current backward pass
+        # store-mode gradient (ParamStore.zero_grad): registered once its weight gradient ran on the
+        # store-capable TN path; _fresh = its grad was not zeroed this step and not written yet
+        self._store_reg = False
+        self._fresh = False
 
     def _view(self, flat: torch.Tensor) -> torch.Tensor:
         return flat[self.start:self.start + self.numel].view(self.shape)
@@ -142,6 +149,22 @@ class Handle:
     def ready(self) -> None:
         self.store.mark_ready(self)
 
+    def take_store(self) -> bool:
+        """Called by a weight-gradient kernel that can overwrite this gradient: True = store (the
+        first contribution since zero_grad skipped it), False = accumulate.  Registers the handle,
+        so the next zero_grad leaves its range to the store."""
+        if not self._store_reg:
+            self.store.register_store(self)
+            return False
+        fresh, self._fresh = self._fresh, False
+        return fresh
+
+    def settle(self) -> None:
+        """Before an accumulating write by a path that cannot store: zero a skipped gradient."""
+        if self._fresh:
+            self.grad.zero_()
+            self._fresh = False
+
     def note_use(self) -> None:
         """Record one differentiable forward use (the reducer expects one ``ready`` per use)."""
         if self.store.use_hooks and self.store.count_uses and self.segs[0].trainable and torch.is_grad_enabled():
@@ -170,6 +193,8 @@ class ParamStore:
         # batched refresh of the transposed weight copies (Handle.weight_t): device descriptor
         # table, cached per set of copies
         self._wt_batch: tuple | None = None
+        self._store_handles: list[Handle] = []  # zero_grad leaves these to their first (storing) write
+        self._zero_plan: tuple | None = None
 
     def refresh_transposes(self) -> bool:
         """Rewrite every existing transposed weight copy from the current bf16 shadow in ONE
@@ -261,7 +286,42 @@ class ParamStore:
 
     # ---------------------------------------------------------------- grads
     def zero_grad(self) -> None:
-        self.grad.zero_()
+        """Reset the gradients for a new step.  The Dense kernels whose weight gradient runs on the
+        TN MFMA kernel (registered by Handle.take_store) are NOT zeroed: their first contribution
+        stores instead of adding -- the split-K reduce then skips reading the gradient too -- and
+        everything else (biases, LayerNorm, embeddings: ~2 % of the bytes) is zeroed by one
+        multi-range launch.  A registered gradient nobody wrote is zeroed by flush_fresh."""
+        hs = self._store_handles
+        if not (STORE_GRADS and hs and self.grad.is_cuda):
+            self.grad.zero_()
+            return
+        key = tuple(h.start for h in hs)
+        if self._zero_plan is None or self._zero_plan[0] != key:
+            spans = sorted((h.start, h.start + h.numel) for h in hs)
+            ranges, pos = [], 0
+            for a, b in spans:
+                if a > pos:
+                    ranges.append((pos, a - pos))
+                pos = max(pos, b)
+            if pos < self.grad.numel():
+                ranges.append((pos, self.grad.numel() - pos))
+            blocks = sum(-(-c // 4096) for _, c in ranges)
+            desc = torch.tensor(ranges if ranges else [(0, 0)], dtype=torch.int64).to(self.grad.device)
+            self._zero_plan = (key, desc, blocks)
+        from ..ops import _ext  # noqa: PLC0415
+        _ext.load().zero_ranges(self.grad, self._zero_plan[1], self._zero_plan[2])
+        for h in hs:
+            h._fresh = True
+
+    def register_store(self, h: Handle) -> None:
+        if STORE_GRADS and not h._store_reg and self.grad is not None and self.grad.is_cuda:
+            h._store_reg = True
+            self._store_handles.append(h)
+
+    def flush_fresh(self) -> None:
+        """After the backward: zero any skipped gradient that received no contribution."""
+        for h in self._store_handles:
+            h.settle()
 
     def mark_ready(self, h: Handle) -> None:
         for fn in self.hooks:

@@ -66,8 +66,13 @@ def wgrad(h: Handle, dy: torch.Tensor, x: torch.Tensor, rows: tuple[int, int] | 
         K = x.shape[1]
         if (_WGRAD_OURS and hip(dy) and dy.dtype == torch.bfloat16 and x.dtype == torch.bfloat16
                 and N % 256 == 0 and K % 256 == 0 and M >= 4096 and dy.stride(1) == 1 and x.stride(1) == 1):
-            _ext.load().gemm_tn_wgrad(dy, x, g)
+            # whole-gradient writes may store (ParamStore.zero_grad skipped it); row slices settle
+            store = h.take_store() if rows is None else False
+            if rows is not None:
+                h.settle()
+            _ext.load().gemm_tn_wgrad(dy, x, g, store)
             return
+        h.settle()  # the paths below accumulate
         if (_WGRAD_OURS and hip(dy) and dy.dtype == torch.bfloat16 and x.dtype == torch.bfloat16
                 and M < NARROW_MAX_M and K % 8 == 0):
             # short reduction (the classifier head, small batches): G^T-free NT form on the narrow
@@ -130,7 +135,8 @@ def _wgrad_ready(hw: Handle, dy: torch.Tensor, x: torch.Tensor) -> None:
         held = _pair["held"]
         if held is not None and held[1].shape[0] == dy.shape[0]:
             _pair["held"] = None
-            _ext.load().gemm_tn_wgrad_group([held[1], dy], [held[2], x], [held[0].grad, hw.grad])
+            _ext.load().gemm_tn_wgrad_group([held[1], dy], [held[2], x], [held[0].grad, hw.grad],
+                                            [held[0].take_store(), hw.take_store()])
             held[0].ready()
             hw.ready()
             return
@@ -318,7 +324,7 @@ def _flush_seg_group(todo: list) -> list:
     if not (_seg_ok(d1, x1) and _seg_ok(d2, x2) and d1[0].shape[0] == d2[0].shape[0]
             and d1[0].shape[0] % 64 == 0 and h1.grad.is_contiguous() and h2.grad.is_contiguous()):
         return todo
-    _ext.load().gemm_tn_wgrad_seg_group([d1, d2], [x1, x2], [h1.grad, h2.grad])
+    _ext.load().gemm_tn_wgrad_seg_group([d1, d2], [x1, x2], [h1.grad, h2.grad], [h1.take_store(), h2.take_store()])
     for h, pairs in todo:
         for _ in pairs:
             h.ready()
@@ -344,9 +350,12 @@ def flush_deferred_wgrads() -> None:
         if not seg:
             dy = torch.cat(dys) if len(dys) > 1 else dys[0]
             x = torch.cat(xs) if len(xs) > 1 else xs[0]
+        store = h.take_store() if seg else False  # every chunk is its rows' only contribution
+        if len(chunks) > 1 and not seg:
+            h.settle()
         for r0, r1 in chunks:
             if seg:  # the batched GEMM reads the 24 per-layer blocks in place
-                _ext.load().gemm_tn_wgrad_seg([d[:, r0:r1] for d in dys], xs, h.grad[r0:r1])
+                _ext.load().gemm_tn_wgrad_seg([d[:, r0:r1] for d in dys], xs, h.grad[r0:r1], store)
             elif len(chunks) == 1:
                 wgrad(h, dy, x)
             else:

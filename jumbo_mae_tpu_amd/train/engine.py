@@ -82,6 +82,7 @@ class Trainer:
             m = {k: v.detach().float() for k, v in out.items()}
             metrics_acc = m if metrics_acc is None else {k: metrics_acc[k] + m[k] for k in m}
         join_wgrad_stream()  # weight-gradient GEMMs run on a side stream (ops/prims.py)
+        self.store.flush_fresh()  # a store-mode gradient nobody wrote this step is zeroed
         split = (self.overlap_optimizer and self.reducer is not None and self.reducer.enabled
                  and self.opt.can_split() and not self.skip_nonfinite)
         if split and not self._planned:

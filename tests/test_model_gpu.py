@@ -196,3 +196,37 @@ def test_paired_wgrads_match_separate():
     for s in m.store.segments:
         x, y = a[s.offset:s.offset + s.numel], b[s.offset:s.offset + s.numel]
         assert (x - y).abs().max().item() <= 1e-4 * max(x.abs().max().item(), 1e-6), s.key
+
+
+def test_store_mode_grads_match_zeroed():
+    """Store-mode gradients (ParamStore.zero_grad leaves the TN-path Dense kernels to their first,
+    storing write; the rest is zeroed by one multi-range launch) == zeroing the whole buffer, over
+    two steps (the first registers the handles) with gradient accumulation (2 micro-steps)."""
+    import jumbo_mae_tpu_amd.models.params as PM
+    from jumbo_mae_tpu_amd.config import DecoderConfig, ViTConfig
+    from jumbo_mae_tpu_amd.models.mae import PretrainModel
+    vc = ViTConfig(layers=2, dim=256, heads=4, labels=0, image_size=224, patch_size=16, posemb="sincos2d",
+                   layerscale=True)
+    dc = DecoderConfig(dec_layers=2, dec_dim=256, dec_heads=4, image_size=224, patch_size=16)
+    imgs = torch.randint(0, 256, (128, 3, 224, 224), dtype=torch.uint8, device="cuda")
+    noise = torch.rand(196, device="cuda")
+    out = []
+    saved = PM.STORE_GRADS
+    try:
+        for store in (False, True):
+            PM.STORE_GRADS = store
+            m = PretrainModel(vc, dc).to("cuda", torch.bfloat16, seed=0)
+            for _ in range(2):  # step 1 registers the store-mode handles, step 2 uses them
+                m.store.grad.fill_(1e3)  # stale values: whatever zero_grad skips must be overwritten
+                m.store.zero_grad()
+                for _ in range(2):  # two micro-steps: the second accumulates
+                    m(imgs, noise=noise)["loss"].backward()
+                m.store.flush_fresh()
+            torch.cuda.synchronize()
+            out.append((m.store.grad.clone(), len(m.store._store_handles)))
+    finally:
+        PM.STORE_GRADS = saved
+    (a, n0), (b, n1) = out
+    assert n0 == 0 and n1 > 0
+    assert torch.isfinite(b).all()
+    assert ((a - b).norm() / a.norm()).item() < 1e-5

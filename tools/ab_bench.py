@@ -47,6 +47,9 @@ def apply(P, cfg: str):
             P.NARROW_SPLITK = v == "1"
         elif k == "JMAE_GROUP_JUMBO_WGRAD":  # 0: the jumbo W1 / W2 batched weight gradients launched apart
             P.GROUP_JUMBO_WGRAD = v == "1"
+        elif k == "JMAE_STORE_GRADS":  # 0: zero the whole gradient buffer every step
+            import jumbo_mae_tpu_amd.models.params as PM
+            PM.STORE_GRADS = v == "1"
         elif k == "GEMM_TAIL":
             from jumbo_mae_tpu_amd.ops import _ext
             _ext.load(True).gemm_set_tail(int(v))
