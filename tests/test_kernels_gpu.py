@@ -374,6 +374,43 @@ def test_gemm_tn_wgrad_group(ext, M, shapes):
         assert rel(g, r) < 1e-4
 
 
+@pytest.mark.parametrize("M,N,K", [(4096, 256, 512), (26624, 1024, 256), (8192, 2048, 512)])
+def test_gemm_tn_wgrad_store(ext, M, N, K):
+    """Store mode of the TN weight gradient (first contribution of a step): G's previous contents
+    are ignored -- split-K reduce without reading G, one-split launches writing G -- plain, grouped
+    (mixed store flags) and segmented."""
+    torch.manual_seed(0)
+    dy = (torch.rand(M, N, device="cuda") * 2 - 1).bfloat16()
+    x = (torch.rand(M, K, device="cuda") * 2 - 1).bfloat16()
+    ref = dy.double().t() @ x.double()
+    g = torch.full((N, K), 1e4, device="cuda")
+    ext.gemm_tn_wgrad(dy, x, g, True)
+    assert rel(g, ref) < 1e-4
+    ext.gemm_tn_wgrad(dy, x, g)  # accumulate on top
+    assert rel(g, 2 * ref) < 1e-4
+    g1, g2 = torch.full((N, K), 1e4, device="cuda"), torch.ones(K, N, device="cuda")
+    ext.gemm_tn_wgrad_group([dy, x], [x, dy], [g1, g2], [True, False])
+    assert rel(g1, ref) < 1e-4 and rel(g2, 1 + ref.t()) < 1e-4
+    rows = M // 4
+    g3 = torch.full((N, K), -3.0, device="cuda")
+    ext.gemm_tn_wgrad_seg([dy[i * rows:(i + 1) * rows] for i in range(4)],
+                          [x[i * rows:(i + 1) * rows] for i in range(4)], g3, True)
+    assert rel(g3, ref) < 1e-4
+
+
+def test_zero_ranges(ext):
+    """Multi-range zeroing of a flat buffer (ParamStore.zero_grad): only the listed ranges change."""
+    buf = torch.arange(100000, device="cuda", dtype=torch.float32) + 1
+    ranges = [(0, 5), (17, 4096), (9000, 1), (20000, 50000), (99990, 10)]
+    desc = torch.tensor(ranges, dtype=torch.int64, device="cuda")
+    blocks = sum(-(-c // 4096) for _, c in ranges)
+    ext.zero_ranges(buf, desc, blocks)
+    ref = torch.arange(100000, device="cuda", dtype=torch.float32) + 1
+    for a, c in ranges:
+        ref[a:a + c] = 0
+    assert torch.equal(buf, ref)
+
+
 @pytest.mark.parametrize("nb,rows", [(24, 512), (5, 128), (3, 64)])
 def test_gemm_tn_wgrad_seg_group(ext, nb, rows):
     """Grouped + segmented TN weight gradients (the jumbo MLP's W1 / W2 over the per-layer row
