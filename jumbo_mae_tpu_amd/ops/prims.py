@@ -133,7 +133,7 @@ def _wgrad_ready(hw: Handle, dy: torch.Tensor, x: torch.Tensor) -> None:
     """grad[hw] += dy^T x, then tell the reducer -- or hold it for / launch it with its pair."""
     if PAIR_WGRAD and _pair["depth"] > 0 and _tn_ok(dy, x):
         held = _pair["held"]
-        if held is not None and held[1].shape[0] == dy.shape[0]:
+        if held is not None and held[1].shape[0] == dy.shape[0] and held[0] is not hw:
             _pair["held"] = None
             _ext.load().gemm_tn_wgrad_group([held[1], dy], [held[2], x], [held[0].grad, hw.grad],
                                             [held[0].take_store(), hw.take_store()])
