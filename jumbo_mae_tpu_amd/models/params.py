@@ -189,6 +189,9 @@ class ParamStore:
         self.partial_hooks: list[Callable[[Handle, int, int], None]] = []
         self._handles: list[Handle] = []
         self.count_uses = True  # off while an activation-checkpoint recompute re-runs a forward
+        # store-mode gradients (zero_grad skips the TN-kernel gradients, their first write stores);
+        # runtime/graph.py turns it off for captured steps
+        self.allow_store = True
         self.version = 0  # bumped whenever the shadow changes (optimizer step, sync, load)
         # batched refresh of the transposed weight copies (Handle.weight_t): device descriptor
         # table, cached per set of copies
@@ -292,8 +295,10 @@ class ParamStore:
         everything else (biases, LayerNorm, embeddings: ~2 % of the bytes) is zeroed by one
         multi-range launch.  A registered gradient nobody wrote is zeroed by flush_fresh."""
         hs = self._store_handles
-        if not (STORE_GRADS and hs and self.grad.is_cuda):
+        if not (STORE_GRADS and self.allow_store and hs and self.grad.is_cuda):
             self.grad.zero_()
+            for h in hs:
+                h._fresh = False
             return
         key = tuple(h.start for h in hs)
         if self._zero_plan is None or self._zero_plan[0] != key:
@@ -314,7 +319,7 @@ class ParamStore:
             h._fresh = True
 
     def register_store(self, h: Handle) -> None:
-        if STORE_GRADS and not h._store_reg and self.grad is not None and self.grad.is_cuda:
+        if STORE_GRADS and self.allow_store and not h._store_reg and self.grad is not None and self.grad.is_cuda:
             h._store_reg = True
             self._store_handles.append(h)
 

@@ -48,6 +48,11 @@ class GraphedTrainStep:
         if trainer.skip_nonfinite:
             raise ValueError("--skip-nonfinite needs a host sync per step; not capturable")
         self.tr = trainer
+        # Store-mode gradients are off in captured steps: a replay of them left tiles of the
+        # attention weight gradients unwritten at production routing (tests/test_graph_gpu.py::
+        # test_graphed_grads_match_eager_production_routing, tools/graph_grad_diag.py); with the
+        # plain zero-then-accumulate gradients the replay matches the eager step bit for bit.
+        trainer.store.allow_store = False
         self.static = [tuple(t.clone() for t in mb) for mb in example_micro_batches]
         snap = None
         if restore:

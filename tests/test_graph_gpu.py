@@ -107,3 +107,30 @@ def test_graph_restore_undoes_warmup():
     assert abs(a["loss"].item() - b["loss"].item()) < 1e-4 * max(1.0, abs(a["loss"].item()))
     torch.cuda.synchronize()
     assert torch.allclose(m1.store.master, m2.store.master, atol=1e-6, rtol=1e-5)
+
+
+def test_graphed_grads_match_eager_production_routing():
+    """B = 256 gives 256 x 19 = 4864 token rows, so the captured step runs the production
+    weight-gradient routing (TN MFMA kernel, paired launches, store-mode gradients with the
+    zero-range fill).  Compared on one step's gradients from identical weights: after several
+    AdamW steps two EAGER runs already differ in ~2e-4 of the weights (float-atomic order in a few
+    reductions, amplified where a gradient is near zero; tools/graph_diag.py), so the weights are
+    the wrong place to look for a stale captured buffer -- the raw gradients are not."""
+    from jumbo_mae_tpu_amd.runtime.graph import GraphedTrainStep
+
+    data = _batches(3, B=256)
+    m1, t1 = _finetune(0.0, 0.0)
+    m2, t2 = _finetune(0.0, 0.0)
+    gs = GraphedTrainStep(t2, [data[0]], warmup=3, restore=True)
+    assert torch.equal(m1.store.master, m2.store.master)
+    for i in (1, 2):
+        a = t1.train_step([data[i]])
+        b = gs([data[i]])
+        assert abs(a["loss"].item() - b["loss"].item()) < 1e-4 * max(1.0, abs(a["loss"].item()))
+        torch.cuda.synchronize()
+        for seg in m1.store.segments:
+            sl = slice(seg.offset, seg.offset + seg.numel)
+            g1, g2 = m1.store.grad[sl], m2.store.grad[sl]
+            scale = g1.abs().max().item()
+            err = (g1 - g2).abs().max().item()
+            assert err <= 2e-2 * scale + 1e-7, (i, seg.key, err, scale)
