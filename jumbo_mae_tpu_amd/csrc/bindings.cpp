@@ -65,6 +65,7 @@ int jm_attn_bwd_long(const uint16_t* qkv, const uint16_t* o, const uint16_t* dO,
                      float* delta, int B, int S, int H, int hd, hipStream_t st);
 void jm_opt_sumsq(const float* x, const int* chunks, int nchunks, float* out, hipStream_t st);
 void jm_opt_set_adamw_vec(int v);
+void jm_zero_f32(float* p, long n, hipStream_t st);
 void jm_opt_adamw(float* p, const float* g, float* mu, float* nu, uint16_t* shadow, const int* chunks, int nchunks,
                   const float* meta, const float* hyper, const float* gnorm_sq, hipStream_t st);
 void jm_opt_lamb_phase1(const float* p, const float* g, float* mu, float* nu, float* u, const int* chunks, int nchunks,
@@ -866,8 +867,7 @@ int group_stores(const std::vector<bool>& stores, const std::vector<torch::Tenso
   if (ns == n) return 1;
   for (int p = 0; p < n; ++p)
     if (p < (int)stores.size() && stores[p])
-      TORCH_CHECK(hipMemsetAsync(gs[p].data_ptr<float>(), 0, gs[p].numel() * 4, stream()) == hipSuccess,
-                  "group_stores: memset");
+      jm_zero_f32(gs[p].data_ptr<float>(), gs[p].numel(), stream());
   return 0;
 }
 

@@ -336,6 +336,21 @@ __global__ __launch_bounds__(256) void splitk_reduce_add_s_kernel(const float* _
 }  // namespace
 
 // g[i] (+)= sum_s part[s][i]; store: g[i] = sum (g not read; smaller / longer-S shapes zero g first)
+namespace {
+__global__ __launch_bounds__(256) void zero_f32_kernel(float* __restrict__ p, long n) {
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) p[i] = 0.f;
+}
+}  // namespace
+
+// g[0:n] = 0 by a kernel, not hipMemsetAsync: a memset captured into a HIP graph left store-mode
+// gradients as garbage on replay (tests/test_graph_gpu.py, tools/graph_grad_diag.py)
+void jm_zero_f32(float* p, long n, hipStream_t st) {
+  if (n <= 0) return;
+  long blocks = (n + 255) / 256;
+  if (blocks > 2048) blocks = 2048;
+  zero_f32_kernel<<<(unsigned)blocks, 256, 0, st>>>(p, n);
+}
+
 int jm_splitk_reduce_add(const float* part, float* g, long n, int S, hipStream_t st, int store) {
   if (n % 4) return -1;
   const long n4 = n / 4;
@@ -353,7 +368,7 @@ int jm_splitk_reduce_add(const float* part, float* g, long n, int S, hipStream_t
       default: break;
     }
   }
-  if (store) (void)hipMemsetAsync(g, 0, n * sizeof(float), st);
+  if (store) jm_zero_f32(g, n, st);
   long blocks = (n4 + 255) / 256;
   if (blocks > 4096) blocks = 4096;
   int ys = 1;  // slice the partials until the launch has ~512 workgroups of >= 8 rows each

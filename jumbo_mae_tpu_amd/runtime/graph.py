@@ -19,6 +19,8 @@ Scope: single-process steps (no DP reducer): RCCL collectives are not captured h
 
 from __future__ import annotations
 
+import os
+
 import torch
 
 
@@ -48,11 +50,12 @@ class GraphedTrainStep:
         if trainer.skip_nonfinite:
             raise ValueError("--skip-nonfinite needs a host sync per step; not capturable")
         self.tr = trainer
-        # Store-mode gradients are off in captured steps: a replay of them left tiles of the
-        # attention weight gradients unwritten at production routing (tests/test_graph_gpu.py::
-        # test_graphed_grads_match_eager_production_routing, tools/graph_grad_diag.py); with the
-        # plain zero-then-accumulate gradients the replay matches the eager step bit for bit.
-        trainer.store.allow_store = False
+        # Store-mode gradients in captured steps (JMAE_GRAPH_STORE=0: zero-then-accumulate).  A
+        # hipMemsetAsync captured into the graph left the small store-mode gradients as garbage on
+        # replay; those zero fills are kernels now (csrc/elementwise.hip jm_zero_f32) and the replay
+        # matches the eager step bit for bit (tests/test_graph_gpu.py::
+        # test_graphed_grads_match_eager_production_routing, tools/graph_grad_diag.py).
+        trainer.store.allow_store = os.environ.get("JMAE_GRAPH_STORE", "1") == "1"
         self.static = [tuple(t.clone() for t in mb) for mb in example_micro_batches]
         snap = None
         if restore:
