@@ -44,10 +44,13 @@ def main():
                                                                       "vit_small_patch16", "vit_tiny_patch16"])
     ap.add_argument("--batch-per-gpu", type=int, default=512)
     ap.add_argument("--grad-accum", type=int, default=1)
+    ap.add_argument("--grad-ckpt", action="store_true", help="activation checkpointing per layer (memory table)")
     ap.add_argument("--bucket-mb", type=float, default=64.0)
     ap.add_argument("--reduce-dtype", default="fp32", choices=["fp32", "bf16"],
                     help="gradient all-reduce dtype (fp32 master weights either way)")
     ap.add_argument("--no-overlap", action="store_true")
+    ap.add_argument("--shard-optimizer", action="store_true",
+                    help="ZeRO-1: reduce-scatter + sharded optimizer + all-gather (default: all-reduce)")
     ap.add_argument("--profile-steps", type=int, default=0, help="extra steps under torch.profiler (debug)")
     ap.add_argument("--task", default="pretrain", choices=["pretrain", "finetune", "linear"])
     ap.add_argument("--hip-graph", action="store_true",
@@ -79,8 +82,8 @@ def main():
     global_batch = B * world
 
     vc = vit_config(args.model, labels=0, posemb="sincos2d", image_mask_ratio=0.75, droppath=0.0, dropout=0.0,
-                    image_size=args.image_size)
-    dc = decoder_config(dec_droppath=0.0, image_size=args.image_size)
+                    image_size=args.image_size, grad_ckpt=args.grad_ckpt)
+    dc = decoder_config(dec_droppath=0.0, image_size=args.image_size, grad_ckpt=args.grad_ckpt)
     model = PretrainModel(vc, dc).to(dev, cdt, seed=0)
     store = model.store
     pdist.broadcast_(store.master)  # CC6: identical init on every rank
@@ -91,7 +94,8 @@ def main():
     opt = FlatOptimizer(store, "adamw", sched, b1=0.9, b2=0.95, eps=1e-8, weight_decay=0.05,
                         num_layers=vc.layers)
     rdt = torch.bfloat16 if args.reduce_dtype == "bf16" else torch.float32
-    reducer = (GradReducer(store, bucket_mb=args.bucket_mb, overlap=not args.no_overlap, reduce_dtype=rdt)
+    reducer = (GradReducer(store, bucket_mb=args.bucket_mb, overlap=not args.no_overlap, reduce_dtype=rdt,
+                           shard=args.shard_optimizer)
                if world > 1 or pdist.forced_group() else None)
     rngs = RngStreams({"noise": 0, "dropout": 0, "mixup": 0}, info.rank, dev)
     trainer = Trainer(model, opt, reducer, rngs, grad_accum=args.grad_accum)
@@ -162,6 +166,7 @@ def main():
 
     ms = elapsed / args.steps * 1000.0
     value = global_batch * args.steps / elapsed
+    peak_gb = round(torch.cuda.max_memory_allocated(dev) / 2**30, 2) if dev.type == "cuda" else None
     if info.is_main:
         out = {
             "metric": "pretrain images/sec (whole node) ViT-L/16 224 mask75% at 1/2/4/8 MI355X"
@@ -179,6 +184,8 @@ def main():
             # GPU time of the last step behind the DP reduction wait (exposed comm + overlapped
             # bucket updates); null on one GPU
             "exposed_comm_ms_last_step": None if comm_ms is None else round(comm_ms, 3),
+            # peak HBM held by PyTorch's allocator on this rank (torch.cuda.max_memory_allocated)
+            "peak_hbm_gb": peak_gb,
             "replica_weight_checksum_spread": spread, "weight_checksum": weight_checksum,
             "reducer": reducer.stats() if reducer is not None else None,
             "dtype": "fp32" if args.cpu else "bf16",
@@ -191,6 +198,7 @@ def main():
                 "parallelism": f"dp{world}",
                 "per_gpu_batch": B,
                 "grad_accum": args.grad_accum,
+                "grad_ckpt": args.grad_ckpt,
                 "hip_graph": bool(runner.graphed is not None),
                 "optimizer": "adamw(0.9,0.95) wd0.05 warmup-cosine",
                 "final_loss": round(final_loss, 5),
@@ -236,7 +244,8 @@ def bench_classifier(args):
     for k in ("init", "mixup", "dropout", "shuffle", "noise"):
         flags += [f"--{k}-seed", "0"]
     fargs = finetune_parser().parse_args(flags + ["--train-batch-size", str(gb), "--bucket-mb", str(args.bucket_mb),
-                                                "--reduce-dtype", args.reduce_dtype])
+                                                "--reduce-dtype", args.reduce_dtype]
+                                         + (["--shard-optimizer"] if args.shard_optimizer else []))
     model = build_model(fargs, dev, torch.bfloat16, info.rank)
     pdist.broadcast_(model.store.master)
     model.store.sync_shadow()
@@ -287,6 +296,8 @@ def bench_classifier(args):
             "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1000.0, 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "mfu_bf16_dense": round(util, 4), "dtype": "bf16",
+            "reducer": reducer.stats() if reducer is not None else None,
+            "peak_hbm_gb": round(torch.cuda.max_memory_allocated(dev) / 2**30, 2),
             "data": "synthetic uint8 224x224 images + random labels on GPU, random-init weights",
             "config": {"model": model_name, "global_batch": gb, "seq_len": model.cfg.num_cls_tokens
                        + model.cfg.seq_patches, "parallelism": f"dp{world}", "per_gpu_batch": B,

@@ -174,7 +174,7 @@ class ShardDataset(IterableDataset):
                     # counts records without decoding them).  Exact resume assumes no corrupt
                     # record BEFORE the resume point: the skip (samples consumed / r records) then
                     # lands one record early per corrupt record and repeats its successor's samples.
-                    index += r - skip if skip else r
+                    index += r  # as the decoded path: skip + (r - skip) positions
                     skip = 0
                     continue
                 first, skip = skip, 0

@@ -32,6 +32,10 @@ import numpy as np
 import torch
 
 ALIGN = 64
+# the flat total is padded to a multiple of this, so every data-parallel world size that divides
+# 1680 (1-8, 10, 12, 14, 15, 16, 20, 24, ...) can cut it into equal ALIGN-aligned shards
+# (ZeRO-1 optimizer sharding, parallel/ddp.py); costs at most 420 KB per fp32 buffer
+TOTAL_ALIGN = ALIGN * 1680
 
 
 @dataclass
@@ -143,6 +147,7 @@ class Handle:
     def accumulate_grad(self, g: torch.Tensor) -> None:
         if not self.segs[0].trainable:
             return
+        self.settle()  # a store-registered gradient skipped by zero_grad holds last step's values
         self.grad.add_(g.reshape(self.shape).to(torch.float32))
         self.store.mark_ready(self)
 
@@ -198,6 +203,7 @@ class ParamStore:
         self._wt_batch: tuple | None = None
         self._store_handles: list[Handle] = []  # zero_grad leaves these to their first (storing) write
         self._zero_plan: tuple | None = None
+        self._retired_plans: list[tuple] = []  # superseded plans stay alive (a graph may read them)
 
     def refresh_transposes(self) -> bool:
         """Rewrite every existing transposed weight copy from the current bf16 shadow in ONE
@@ -262,7 +268,7 @@ class ParamStore:
         return h
 
     def finalize(self, device, compute_dtype=torch.float32, generator: torch.Generator | None = None) -> None:
-        self.pad()
+        self.total = (self.total + TOTAL_ALIGN - 1) // TOTAL_ALIGN * TOTAL_ALIGN
         self.compute_dtype = compute_dtype
         self.master = torch.zeros(self.total, dtype=torch.float32, device=device)
         self.grad = torch.zeros(self.total, dtype=torch.float32, device=device)
@@ -302,6 +308,12 @@ class ParamStore:
             return
         key = tuple(h.start for h in hs)
         if self._zero_plan is None or self._zero_plan[0] != key:
+            # the plan's descriptor is an H2D copy: never built inside a HIP-graph capture (a
+            # captured step reuses the plan of its warmup steps; a changed handle set after
+            # capture would free the descriptor the graph reads -- runtime/graph.py pins it)
+            assert not torch.cuda.is_current_stream_capturing(), "zero_grad plan changed during capture"
+            if self._zero_plan is not None:
+                self._retired_plans.append(self._zero_plan)
             spans = sorted((h.start, h.start + h.numel) for h in hs)
             ranges, pos = [], 0
             for a, b in spans:

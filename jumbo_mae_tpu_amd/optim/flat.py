@@ -86,6 +86,9 @@ class FlatOptimizer:
         self._ranges = None      # (lo, hi) -> chunk-table rows (split updates, plan_ranges)
         self._rest = None        # chunk-table rows outside every planned range
         self._gn_ready = False   # gnorm_sq flag written for this step (split updates)
+        self._shard = None       # GradReducer in ZeRO-1 mode: update only this rank's pieces
+        self._owned_rows = None  # chunk-table rows of every owned piece
+        self._owned_mask = None  # torch path: bool mask of owned elements
 
     # ---------------------------------------------------------------- helpers
     def _elem_meta(self):
@@ -104,6 +107,8 @@ class FlatOptimizer:
     def _seg_norm_sq(self, x: torch.Tensor, seg_id: torch.Tensor, valid: torch.Tensor) -> torch.Tensor:
         out = torch.zeros(self.nseg, dtype=torch.float32, device=x.device)
         out.index_add_(0, seg_id[valid], (x[valid] * x[valid]))
+        if self._shard is not None:
+            self._shard.sum_(out)
         return out
 
     # ---------------------------------------------------------------- step
@@ -142,7 +147,44 @@ class FlatOptimizer:
     def can_split(self) -> bool:
         return self.kind in ("adamw", "sgd") and self.clip_grad <= 0
 
-    def plan_ranges(self, ranges: list[tuple[int, int]]) -> None:
+    def attach_shard(self, reducer) -> None:
+        """ZeRO-1: from now on every update touches only ``reducer``'s owned pieces (the rest of the
+        master arrives by the reducer's all-gather); norms and the clip norm are summed over ranks."""
+        if reducer is None or not getattr(reducer, "shard", False):
+            return
+        self._shard = reducer
+        pieces = reducer.owned_pieces()
+        self._owned_rows = self._rows_for(pieces)
+        own = torch.zeros(self.store.total, dtype=torch.bool, device=self.store.master.device)
+        for a, b in pieces:
+            own[a:b] = True
+        self._owned_mask = own
+
+    def _rows_for(self, pieces: list[tuple[int, int]]):
+        """Chunk-table rows covering exactly the segment elements inside ``pieces``."""
+        rows = []
+        for a, b in sorted(pieces):
+            for i, sg in enumerate(self.store.segments):
+                lo, hi = max(a, sg.offset), min(b, sg.offset + sg.numel)
+                for st in range(lo, hi, CHUNK):
+                    rows.append((st, min(CHUNK, hi - st), i))
+        if not rows:
+            return None
+        return torch.tensor(rows, dtype=torch.int64).to(torch.int32).to(self.store.master.device)
+
+    def gather_state(self) -> None:
+        """COLLECTIVE (every rank, same step): make the sharded moments whole on every rank before
+        ``state_dict`` (checkpoint).  No-op without sharding."""
+        if self._shard is not None:
+            self._shard.gather_state([self.mu, self.nu, self.trace])
+
+    def plan_ranges(self, ranges: list[tuple[int, int]], pieces: list[list[tuple[int, int]]] | None = None) -> None:
+        """Rows of each split-update range.  ``pieces`` (sharded): the exact element ranges of each
+        range that this rank updates; nothing outside them is ever updated."""
+        if pieces is not None:
+            self._ranges = {r: self._rows_for(pc) for r, pc in zip(ranges, pieces)}
+            self._rest = None
+            return
         starts = self.chunks[:, 0].long().cpu()
         covered = torch.zeros(len(starts), dtype=torch.bool)
         self._ranges = {}
@@ -168,7 +210,7 @@ class FlatOptimizer:
 
     def launch_rest(self) -> None:
         """Update everything no planned range covers; ends a split step."""
-        if self._rest is not None:
+        if self._rest is not None and self._shard is None:
             self._launch_rows(self._rest, None, None)
         self._gn_ready = False
 
@@ -199,7 +241,10 @@ class FlatOptimizer:
     def _clip_scale_torch(self, g: torch.Tensor) -> torch.Tensor:
         if self.clip_grad <= 0:
             return torch.ones((), device=g.device)
-        gn = torch.sqrt((g * g).sum())
+        sq = (g * g).sum().reshape(1)
+        if self._shard is not None:
+            self._shard.sum_(sq)
+        gn = torch.sqrt(sq[0])
         return torch.where(gn < self.clip_grad, torch.ones_like(gn), self.clip_grad / gn)
 
     @torch.no_grad()
@@ -223,7 +268,13 @@ class FlatOptimizer:
             return
         p, g = s.master, s.grad
         seg_id, valid, decay, llrd, trust_m, trainable = self._elem_meta()
-        g = g * self._clip_scale_torch(g)
+        own = self._owned_mask
+        if own is not None:  # ZeRO-1: norms over the owned elements, summed over the ranks
+            valid = valid & own
+        g = g * self._clip_scale_torch(torch.where(valid, g, torch.zeros_like(g)))  # segments only
+        if own is not None:  # moments / traces of non-owned pieces are left alone
+            g = torch.where(own, g, torch.zeros_like(g))
+            saved = [t.clone() for t in (self.mu, self.nu, self.trace) if t is not None]
         if self.kind in ("adamw", "lamb"):
             self.mu.mul_(self.b1).add_((1 - self.b1) * g)
             self.nu.mul_(self.b2).add_((1 - self.b2) * g * g)
@@ -251,6 +302,9 @@ class FlatOptimizer:
             upd = -lr * self.trace * llrd
         upd = torch.where(trainable & valid, upd, torch.zeros_like(upd))
         p.add_(upd)
+        if own is not None:
+            for t, old in zip([t for t in (self.mu, self.nu, self.trace) if t is not None], saved):
+                t.copy_(torch.where(own, t, old))
         s.sync_shadow()
 
     @torch.no_grad()
@@ -258,29 +312,41 @@ class FlatOptimizer:
         ext = _ext.load()
         s = self.store
         shadow = s.shadow if s.shadow is not s.master else None
+        rows = self.chunks
+        red = self._shard
+        if red is not None:  # ZeRO-1: this rank's pieces only; per-leaf / global norms summed over ranks
+            rows = self._owned_rows
+            if rows is None:
+                return
         if self.clip_grad > 0:
             self.gnorm_sq.zero_()
-            ext.opt_sumsq(s.grad, self.chunks, self.gnorm_sq)
+            ext.opt_sumsq(s.grad, rows, self.gnorm_sq)
+            if red is not None:
+                red.sum_(self.gnorm_sq)
         else:
             self.gnorm_sq.fill_(-1.0)
         if self.kind == "adamw":
-            ext.opt_adamw(s.master, s.grad, self.mu, self.nu, shadow, self.chunks, self.meta,
+            ext.opt_adamw(s.master, s.grad, self.mu, self.nu, shadow, rows, self.meta,
                           self.hyper, self.gnorm_sq)
         elif self.kind == "lamb":
             if self._tmp is None:
                 self._tmp = torch.empty_like(s.master)
             self.norms.zero_()
-            ext.opt_lamb_phase1(s.master, s.grad, self.mu, self.nu, self._tmp, self.chunks, self.meta,
+            ext.opt_lamb_phase1(s.master, s.grad, self.mu, self.nu, self._tmp, rows, self.meta,
                                 self.hyper, self.gnorm_sq, self.norms)
-            ext.opt_apply_trust(s.master, self._tmp, None, shadow, self.chunks, self.meta, self.hyper,
+            if red is not None:
+                red.sum_(self.norms)
+            ext.opt_apply_trust(s.master, self._tmp, None, shadow, rows, self.meta, self.hyper,
                                 self.norms, self.gnorm_sq, 0, 0.0, 1.0)
         elif self.kind == "lars":
             self.norms.zero_()
-            ext.opt_lars_norms(s.master, s.grad, self.chunks, self.hyper, self.gnorm_sq, self.norms)
-            ext.opt_apply_trust(s.master, s.grad, self.trace, shadow, self.chunks, self.meta, self.hyper,
+            ext.opt_lars_norms(s.master, s.grad, rows, self.hyper, self.gnorm_sq, self.norms)
+            if red is not None:
+                red.sum_(self.norms)
+            ext.opt_apply_trust(s.master, s.grad, self.trace, shadow, rows, self.meta, self.hyper,
                                 self.norms, self.gnorm_sq, 1, self.momentum, self.trust_coefficient)
         else:
-            ext.opt_sgd(s.master, s.grad, self.trace, shadow, self.chunks, self.meta, self.hyper,
+            ext.opt_sgd(s.master, s.grad, self.trace, shadow, rows, self.meta, self.hyper,
                         self.gnorm_sq, self.momentum)
 
     # ---------------------------------------------------------------- state io

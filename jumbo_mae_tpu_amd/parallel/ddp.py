@@ -31,6 +31,17 @@ MI355X design:
 * ``reduce_dtype=bf16`` converts each bucket (or partial slice) into ONE preallocated bf16
   staging buffer laid out like the flat gradient buffer -- no per-step allocation -- and copies
   the averaged slice back after the collective; partial launches work the same way.
+* ``shard=True`` (ZeRO-1 optimizer sharding): bucket boundaries are snapped to multiples of
+  world x 64 elements (a segment cut by a boundary belongs to both buckets and both wait for it),
+  so every bucket splits into ``world`` equal 64-aligned pieces and rank r owns piece r of every
+  bucket.  A complete bucket is REDUCE-SCATTERED (in place: rank r's piece of the flat gradient
+  receives the average), the optimizer updates only the owned pieces (1/world of the AdamW /
+  LAMB / LARS / SGD work; LAMB / LARS per-leaf norms and the global clip norm are summed over the
+  ranks by a tiny all-reduce), and each bucket's updated fp32 master is ALL-GATHERED in place
+  and re-cast to the bf16 shadow.  Link bytes per parameter: 4 + 4 (= the all-reduce's two
+  halves), 2 + 4 with ``reduce_dtype=bf16``.  Optimizer moments of non-owned pieces are never
+  touched; ``gather_state`` all-gathers them for a checkpoint.  Partial (chunked jumbo) launches
+  are off in this mode: the jumbo buckets are reduce-scattered whole.
 """
 
 from __future__ import annotations
@@ -42,7 +53,7 @@ import re
 import torch
 import torch.distributed as dist
 
-from ..models.params import Handle, ParamStore
+from ..models.params import ALIGN, Handle, ParamStore
 from . import dist as pdist
 
 
@@ -102,9 +113,25 @@ def plan_buckets(sizes: list[int], keys: list[tuple], limit: int) -> list[list[i
     return buckets
 
 
+def shard_ranges(buckets: list[tuple[int, int]], q: int) -> list[tuple[int, int]]:
+    """Bucket ranges with every boundary snapped DOWN to a multiple of ``q`` (the first start too,
+    the last end UP), in launch order (from the end of the buffer).  The ranges tile
+    [first start, last end); a bucket whose snapped boundary does not advance merges into the next."""
+    asc = sorted(buckets)
+    cuts = [asc[0][0] // q * q]
+    for _, hi in asc[:-1]:
+        c = hi // q * q
+        if c > cuts[-1]:
+            cuts.append(c)
+    end = -(-asc[-1][1] // q) * q
+    if end > cuts[-1]:
+        cuts.append(end)
+    return list(zip(cuts[:-1], cuts[1:]))[::-1]
+
+
 class GradReducer:
     def __init__(self, store: ParamStore, group=None, bucket_mb: float = 64.0, overlap: bool = True,
-                 reduce_dtype: torch.dtype = torch.float32, seg_filter=None):
+                 reduce_dtype: torch.dtype = torch.float32, seg_filter=None, shard: bool = False):
         self.store = store
         self.group = group
         self.world = dist.get_world_size(group) if (dist.is_available() and dist.is_initialized()) else 1
@@ -122,13 +149,25 @@ class GradReducer:
         buckets = plan_buckets([s.numel for s in segs], [unit_key(s.path) for s in segs], limit)
         self.segs = segs
         self.buckets = []
-        self.seg_bucket = [0] * len(segs)
-        for bi, idxs in enumerate(buckets):
+        for idxs in buckets:
             lo = min(segs[i].offset for i in idxs)
             hi = max(segs[i].offset + segs[i].numel for i in idxs)
             self.buckets.append((lo, hi, idxs))
+        self.shard = bool(shard) and self.enabled and bool(self.buckets)
+        self.rank = dist.get_rank(group) if self.enabled else 0
+        if self.shard:
+            q = self.world * ALIGN
+            if store.total % q:
+                raise ValueError(f"optimizer sharding over {self.world} ranks needs the flat total ({store.total}) "
+                                 f"to be a multiple of {q} (models/params.py TOTAL_ALIGN)")
+            self.buckets = [(lo, hi, [i for i, s in enumerate(segs) if s.offset < hi and s.offset + s.numel > lo])
+                            for lo, hi in shard_ranges([(lo, hi) for lo, hi, _ in self.buckets], q)]
+        self.seg_buckets: list[list[int]] = [[] for _ in segs]  # a snapped boundary may cut a segment
+        for bi, (_, _, idxs) in enumerate(self.buckets):
             for i in idxs:
-                self.seg_bucket[i] = bi
+                self.seg_buckets[i].append(bi)
+        self.gathers: list[tuple] = []  # (bucket, work) all-gathers of the updated master (shard)
+        self.gathered = [False] * len(self.buckets)
         self._stage = None  # bf16 staging buffer over [stage_lo, stage_hi) of the flat buffer
         self._stage_lo = min((lo for lo, _, _ in self.buckets), default=0)
         self._stage_hi = max((hi for _, hi, _ in self.buckets), default=0)
@@ -152,15 +191,25 @@ class GradReducer:
         self.launched = [False] * len(self.buckets)
         self.partial_done = [0] * len(self.buckets)
         self.works = []
+        self.gathers = []
+        self.gathered = [False] * len(self.buckets)
+
+    def piece(self, b: int) -> tuple[int, int]:
+        """This rank's piece [lo, hi) of bucket ``b`` (sharded mode; the whole bucket otherwise)."""
+        lo, hi, _ = self.buckets[b]
+        if not self.shard:
+            return lo, hi
+        n = (hi - lo) // self.world
+        return lo + self.rank * n, lo + (self.rank + 1) * n
 
     def _on_partial(self, h: Handle, lo: int, hi: int) -> None:
         """Elements [lo, hi) of single-segment handle ``h`` are final: reduce them now."""
-        if not (self.overlap and self.sync) or len(h.segs) != 1:
+        if not (self.overlap and self.sync) or len(h.segs) != 1 or self.shard:
             return
         i = self.seg_index.get(id(h.segs[0]))
         if i is None:
             return
-        b = self.seg_bucket[i]
+        b = self.seg_buckets[i][0]
         blo, bhi, idxs = self.buckets[b]
         if len(idxs) != 1 or self.launched[b]:
             return
@@ -188,10 +237,10 @@ class GradReducer:
                 continue
             self.pending_uses[i] -= 1
             if self.pending_uses[i] == 0:
-                b = self.seg_bucket[i]
-                self.bucket_left[b] -= 1
-                if self.bucket_left[b] == 0:
-                    self._launch(b)
+                for b in self.seg_buckets[i]:
+                    self.bucket_left[b] -= 1
+                    if self.bucket_left[b] == 0:
+                        self._launch(b)
 
     def _launch(self, b: int) -> None:
         if self.launched[b]:
@@ -214,9 +263,21 @@ class GradReducer:
         return self._stage
 
     def _reduce_range(self, b: int, lo: int, hi: int, partial: bool = False) -> None:
-        """Launch the all-reduce of flat-buffer elements [lo, hi) (bucket ``b``)."""
+        """Launch the all-reduce of flat-buffer elements [lo, hi) (bucket ``b``); sharded: the
+        in-place reduce-scatter whose result lands in this rank's piece."""
         view = self.store.grad[lo:hi]
         st = self.staging()
+        if self.shard:
+            plo, phi = self.piece(b)
+            src = view
+            if st is not None:
+                src = st[lo - self._stage_lo:hi - self._stage_lo]
+                src.copy_(view)
+            out = src[plo - lo:phi - lo]
+            w, to_div = self._collective(lambda op: dist.reduce_scatter_tensor(out, src, op=op, group=self.group,
+                                                                                async_op=True), out)
+            self.works.append((b, w, to_div, plo, phi, out if st is not None else None, False))
+            return
         if st is not None:
             sv = st[lo - self._stage_lo:hi - self._stage_lo]
             sv.copy_(view)
@@ -233,6 +294,11 @@ class GradReducer:
         issued from the weight-gradient stream (ops/prims.py) when that stream is enabled, after
         it has caught up with the main stream: RCCL then waits for the GEMM that wrote the
         bucket's last kernel gradient without stalling the backward chain on the main stream."""
+        return self._collective(lambda op: dist.all_reduce(t, op=op, group=self.group, async_op=True), t)
+
+    def _collective(self, issue, t: torch.Tensor):
+        """Issue an averaging collective (``issue(op)``) whose result is ``t``, on the
+        weight-gradient stream when there is one (see _allreduce) -> (work, tensor to divide)."""
         from ..ops.prims import wgrad_stream
         native_avg = dist.get_backend(self.group) == "nccl"
         op = dist.ReduceOp.AVG if native_avg else dist.ReduceOp.SUM
@@ -240,8 +306,64 @@ class GradReducer:
         if side is not None:
             side.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(side) if side is not None else contextlib.nullcontext():
-            w = dist.all_reduce(t, op=op, group=self.group, async_op=True)
+            w = issue(op)
         return w, (None if native_avg else t)
+
+    # ---------------------------------------------------------------- sharded optimizer (ZeRO-1)
+    def owned_pieces(self, buckets=None) -> list[tuple[int, int]]:
+        return [self.piece(b) for b in (range(len(self.buckets)) if buckets is None else buckets)]
+
+    def _gather_into(self, flat: torch.Tensor, b: int):
+        lo, hi, _ = self.buckets[b]
+        plo, phi = self.piece(b)
+        out = flat[lo:hi]
+        inp = flat[plo:phi]
+        side = None
+        if flat.is_cuda:
+            from ..ops.prims import wgrad_stream
+            side = wgrad_stream() or torch.cuda.current_stream()
+            if side is not torch.cuda.current_stream():
+                side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side) if side is not None else contextlib.nullcontext():
+            return dist.all_gather_into_tensor(out, inp, group=self.group, async_op=True)
+
+    def gather(self, b: int) -> None:
+        """All-gather bucket ``b``'s updated fp32 master (in place) after the owned piece's update."""
+        if not self.shard or self.gathered[b]:
+            return
+        self.gathered[b] = True
+        self.gathers.append((b, self._gather_into(self.store.master, b)))
+
+    def gather_all(self) -> None:
+        for b in range(len(self.buckets)):
+            self.gather(b)
+
+    def wait_gathers(self) -> None:
+        """Wait for the master all-gathers and re-cast the gathered ranges to the bf16 shadow."""
+        s = self.store
+        for b, w in self.gathers:
+            w.wait()
+            if s.shadow is not s.master:
+                lo, hi, _ = self.buckets[b]
+                with torch.no_grad():
+                    s.shadow[lo:hi].copy_(s.master[lo:hi])
+        self.gathers = []
+
+    def gather_state(self, tensors) -> None:
+        """COLLECTIVE: all-gather optimizer state buffers (flat, like the master) so every rank
+        holds every piece (checkpoint save)."""
+        if not self.shard:
+            return
+        for t in tensors:
+            if t is None:
+                continue
+            for b in range(len(self.buckets)):
+                self._gather_into(t, b).wait()
+
+    def sum_(self, t: torch.Tensor) -> None:
+        """In-place SUM all-reduce (sharded LAMB / LARS norms, global clip norm)."""
+        if self.shard:
+            dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
 
     def bucket_ranges(self) -> list[tuple[int, int]]:
         return [(lo, hi) for lo, hi, _ in self.buckets]
@@ -257,6 +379,12 @@ class GradReducer:
         g = int(os.environ.get("JMAE_OPT_GROUPS", "4"))
         g = nb if g <= 0 else max(1, min(g, nb))
         return [list(range(nb * i // g, nb * (i + 1) // g)) for i in range(g)]
+
+    def optimizer_pieces(self) -> list[list[tuple[int, int]]] | None:
+        """Sharded: the owned pieces of each optimizer group (None when not sharded)."""
+        if not self.shard:
+            return None
+        return [self.owned_pieces(grp) for grp in self.optimizer_groups()]
 
     def optimizer_ranges(self) -> list[tuple[int, int]]:
         return [(min(self.buckets[b][0] for b in grp), max(self.buckets[b][1] for b in grp))
@@ -292,13 +420,19 @@ class GradReducer:
             left[gid[b]] -= 1
             if on_bucket_done is not None and left[gid[b]] == 0:
                 on_bucket_done(*ranges[gid[b]])
+                for bb in groups[gid[b]]:  # sharded: the group's owned pieces are updated
+                    self.gather(bb)
         if on_bucket_done is not None:  # a group without any reduction of its own (none today)
             for i, grp in enumerate(groups):
                 if not any(gid[wk[0]] == i for wk in self.works):
                     on_bucket_done(*ranges[i])
+                    for bb in grp:
+                        self.gather(bb)
         self.works = []
 
     def stats(self) -> dict:
         sizes = [(hi - lo) * 4 / 2**20 for lo, hi, _ in self.buckets]
         return {"buckets": len(self.buckets), "bucket_mb_max": max(sizes) if sizes else 0.0,
-                "bucket_mb_min": min(sizes) if sizes else 0.0}
+                "bucket_mb_min": min(sizes) if sizes else 0.0,
+                "mode": "zero1-reduce-scatter" if self.shard else "all-reduce",
+                "reduce_dtype": "bf16" if self.reduce_dtype == torch.bfloat16 else "fp32"}

@@ -70,7 +70,15 @@ def _optim(p: argparse.ArgumentParser):
     p.add_argument("--name")
     p.add_argument("--ipaddr")
     p.add_argument("--hostname")
-    p.add_argument("--output-dir", default=".")
+    p.add_argument("--output-dir", default=".", type=_output_dir)
+
+
+def _output_dir(v: str) -> str:
+    """Checkpoint names are joined onto the output dir, which a ``pipe:`` command cannot take (its
+    read command would run with the checkpoint bytes on stdin and write nothing)."""
+    if v.startswith("pipe:"):
+        raise argparse.ArgumentTypeError("--output-dir cannot be a pipe: command; use a path or gs:// / s3:// URL")
+    return v
 
 
 def _extensions(p: argparse.ArgumentParser):
@@ -84,6 +92,9 @@ def _extensions(p: argparse.ArgumentParser):
     g.add_argument("--reduce-dtype", default="fp32", choices=["fp32", "bf16"],
                    help="gradient all-reduce dtype (bf16 halves the bytes on xGMI; master weights, "
                         "optimizer state and the local gradient stay fp32)")
+    g.add_argument("--shard-optimizer", action="store_true",
+                   help="ZeRO-1: reduce-scatter the gradient buckets, update 1/N of the parameters per rank, "
+                        "all-gather the updated weights (parallel/ddp.py)")
     g.add_argument("--stop-after-steps", type=int, default=0,
                    help="end this invocation after N steps, writing 'last' (time-sliced / preemptible "
                         "jobs: continue with --resume auto); 0 = run to --training-steps")

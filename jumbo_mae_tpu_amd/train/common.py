@@ -49,7 +49,8 @@ def make_optimizer(args, store, peak_lr: float, end_value: float) -> FlatOptimiz
 def make_reducer(args, store):
     if pdist.info().world_size > 1 or pdist.forced_group():
         dt = torch.bfloat16 if getattr(args, "reduce_dtype", "fp32") == "bf16" else torch.float32
-        return GradReducer(store, bucket_mb=args.bucket_mb, reduce_dtype=dt)
+        return GradReducer(store, bucket_mb=args.bucket_mb, reduce_dtype=dt,
+                           shard=getattr(args, "shard_optimizer", False))
     return None
 
 
@@ -116,6 +117,8 @@ def save_last(args, model, opt, step, rngs, extra_state=None, postfix="last", pe
     The sidecar holds the optimizer state, every rank's random state (``per_rank`` from
     ``rank_states``), the data position (train batches consumed per rank) and the best
     validation metric so far."""
+    if hasattr(opt, "gather_state"):
+        opt.gather_state()  # collective: sharded optimizer moments made whole on every rank
     if not pdist.info().is_main:
         return None
     tree = model.flax_params()

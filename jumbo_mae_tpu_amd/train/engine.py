@@ -35,6 +35,8 @@ class Trainer:
         self.overlap_optimizer = os.environ.get("JMAE_OVERLAP_OPT", "1") == "1"
         self._planned = False
         self._comm_events = None  # (start, end) around the last step's reduction wait
+        if reducer is not None and getattr(reducer, "shard", False):
+            optimizer.attach_shard(reducer)  # ZeRO-1: owned pieces only, master all-gathered
 
     @property
     def store(self):
@@ -86,7 +88,7 @@ class Trainer:
         split = (self.overlap_optimizer and self.reducer is not None and self.reducer.enabled
                  and self.opt.can_split() and not self.skip_nonfinite)
         if split and not self._planned:
-            self.opt.plan_ranges(self.reducer.optimizer_ranges())
+            self.opt.plan_ranges(self.reducer.optimizer_ranges(), self.reducer.optimizer_pieces())
             self._planned = True
         if self.reducer is not None:
             with trace_range("allreduce_wait"):
@@ -115,6 +117,10 @@ class Trainer:
                 self.opt.launch_rest()
             else:
                 self.opt.launch()
+        if self.reducer is not None and self.reducer.shard:
+            with trace_range("allgather_wait"):
+                self.reducer.gather_all()    # groups not gathered during finish (monolithic update)
+                self.reducer.wait_gathers()  # next forward reads the whole master / shadow
         return metrics
 
     def nonfinite_anywhere(self, loss: torch.Tensor) -> bool:

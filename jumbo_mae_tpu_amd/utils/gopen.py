@@ -72,6 +72,8 @@ def join(base: str, *parts: str) -> str:
     """``os.path.join`` for local paths, '/'-join for URLs (never turns ``gs://b`` into ``gs:/b``)."""
     if is_local(base):
         return os.path.join(base, *parts)
+    if scheme(base) == "pipe":
+        raise ValueError(f"cannot join a path onto a pipe: command: {base}")
     out = base
     for p in parts:
         out = out.rstrip("/") + "/" + p.lstrip("/")

@@ -150,3 +150,22 @@ def test_launcher_ckpt_dir_from_pipe_prefix(tmp_path):
     env["DATA_DIR"] = "gs://bkt/data"
     out = subprocess.run(["bash", str(script)], env=env, capture_output=True, text=True, check=True).stdout
     assert "CKPT=gs://bkt/data/CKPT " in out
+
+
+def test_pipe_output_dir_rejected():
+    """A pipe: command cannot take a joined checkpoint name: the drivers refuse it as --output-dir
+    and gopen.join refuses to build such a URL (the read command would swallow the bytes)."""
+    import argparse
+
+    import pytest
+
+    from jumbo_mae_tpu_amd.train.cli import pretrain_parser
+    from jumbo_mae_tpu_amd.utils import gopen
+
+    with pytest.raises(ValueError):
+        gopen.join("pipe:gsutil cat gs://b/ckpt", "run-last.msgpack")
+    p = pretrain_parser()
+    p.error = lambda msg: (_ for _ in ()).throw(argparse.ArgumentTypeError(msg))
+    with pytest.raises(argparse.ArgumentTypeError):
+        p.parse_args(["--output-dir", "pipe:cat"])
+    assert p.parse_args(["--output-dir", "gs://b/out"]).output_dir == "gs://b/out"

@@ -133,4 +133,8 @@ def test_graphed_grads_match_eager_production_routing():
             g1, g2 = m1.store.grad[sl], m2.store.grad[sl]
             scale = g1.abs().max().item()
             err = (g1 - g2).abs().max().item()
-            assert err <= 2e-2 * scale + 1e-7, (i, seg.key, err, scale)
+            # step 1 starts from identical weights: only float-atomic summation order may differ;
+            # step 2 also carries step 1's AdamW update of those (m / sqrt(v) amplifies near-zero
+            # gradient differences), so it gets a looser bound -- a stale tile is O(scale) either way
+            tol = 1e-5 if i == 1 else 1e-3
+            assert err <= tol * scale + 1e-9, (i, seg.key, err, scale)

@@ -79,3 +79,24 @@ def test_rccl_pretrain_bf16_reduce_and_accum():
 def test_rccl_finetune_matches_plain():
     _check_equal(["--task", "finetune", "--gpus", "1", "--steps", "2", "--warmup", "1", "--model",
                   "vit_tiny_patch16", "--batch-per-gpu", "32", "--bucket-mb", "0.5"])
+
+
+def test_forced_group_zero1_matches_plain_cpu():
+    _check_equal(PRETRAIN[:-4] + ["--batch-per-gpu", "4", "--image-size", "64", "--bucket-mb", "0.5", "--cpu",
+                                  "--shard-optimizer"])
+
+
+@pytest.mark.gpu
+def test_rccl_pretrain_zero1_matches_plain():
+    """ZeRO-1 on a 1-rank RCCL communicator: reduce_scatter_tensor / all_gather_into_tensor in
+    place on the flat buffers, the sharded AdamW rows and the shadow re-cast all execute; over one
+    rank they are identities, so the step must equal the plain one."""
+    plain, dp = _check_equal(PRETRAIN + ["--shard-optimizer"])
+    assert dp["reducer"]["mode"] == "zero1-reduce-scatter", dp
+
+
+@pytest.mark.gpu
+def test_rccl_linear_zero1_lars_matches_plain():
+    """LARS (per-leaf trust ratios: the sharded norms are all-reduced) on the linear-probe step."""
+    _check_equal(["--task", "linear", "--gpus", "1", "--steps", "2", "--warmup", "1", "--batch-per-gpu", "32",
+                  "--bucket-mb", "0.5", "--shard-optimizer"])

@@ -1,0 +1,100 @@
+"""ZeRO-1 optimizer sharding (parallel/ddp.py ``shard=True``) on CPU gloo ranks: reduce-scatter of
+the gradient buckets, update of this rank's pieces only, all-gather of the updated master.  The
+result must be the replicated all-reduce step's, for every optimizer (per-leaf LAMB / LARS trust
+ratios and the global clip norm are summed over the ranks), with the split (per-bucket) and the
+monolithic update, and the gathered optimizer moments must equal the replicated ones."""
+
+import os
+import tempfile
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from test_dist import _cfgs, _free_port, _init
+
+
+def _worker(rank, world, port, out, kind, clip, overlap, bf16):
+    _init(rank, world, port)
+    from jumbo_mae_tpu_amd.models.mae import PretrainModel
+    from jumbo_mae_tpu_amd.optim.flat import FlatOptimizer
+    from jumbo_mae_tpu_amd.optim.schedule import warmup_cosine_decay_schedule
+    from jumbo_mae_tpu_amd.parallel.ddp import GradReducer
+    from jumbo_mae_tpu_amd.train.engine import Trainer
+    vc, dc = _cfgs()
+    g = torch.Generator().manual_seed(0)
+    imgs = torch.randint(0, 256, (4 * world, 3, 32, 32), dtype=torch.uint8, generator=g)
+    res = {}
+    for shard in (False, True):
+        torch.manual_seed(100 + rank)  # same masking noise in both runs
+        m = PretrainModel(vc, dc).to("cpu", seed=0)
+        dist.broadcast(m.store.master, 0)
+        opt = FlatOptimizer(m.store, kind, warmup_cosine_decay_schedule(1e-6, 1e-2, 1, 10, 1e-5), b2=0.95,
+                            weight_decay=0.05, num_layers=vc.layers, clip_grad=clip)
+        red = GradReducer(m.store, bucket_mb=0.01, shard=shard,
+                          reduce_dtype=torch.bfloat16 if bf16 else torch.float32)
+        tr = Trainer(m, opt, red, None)
+        tr.overlap_optimizer = overlap
+        for _ in range(3):
+            tr.train_step([(imgs[rank * 4:(rank + 1) * 4],)])
+        opt.gather_state()
+        res[shard] = {"master": m.store.master.clone(), "mu": None if opt.mu is None else opt.mu.clone(),
+                      "trace": None if opt.trace is None else opt.trace.clone(), "stats": red.stats(),
+                      "nb": len(red.buckets), "pieces": red.owned_pieces()}
+    # every rank ends with the same master
+    ms = [torch.zeros_like(res[True]["master"]) for _ in range(world)]
+    dist.all_gather(ms, res[True]["master"])
+    if rank == 0:
+        torch.save({"rep": res[False], "zero": res[True], "same": all(torch.equal(ms[0], x) for x in ms)}, out)
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,kind,clip,overlap,bf16", [
+    (2, "adamw", 0.0, True, False),   # split update per bucket group + all-gather per group
+    (2, "adamw", 0.0, False, False),  # monolithic update, then all-gather
+    (2, "sgd", 0.0, True, False),
+    (2, "lamb", 0.0, True, False),    # per-leaf trust ratios: norms summed over the ranks
+    (2, "lars", 0.0, True, False),
+    (2, "adamw", 0.5, True, False),   # global clip norm summed over the ranks
+    (2, "adamw", 0.0, True, True),    # bf16 reduce-scatter
+    (4, "adamw", 0.0, True, False),
+    (4, "lamb", 0.3, True, False),
+])
+def test_zero1_matches_replicated(world, kind, clip, overlap, bf16):
+    port = _free_port()
+    with tempfile.TemporaryDirectory() as d:
+        out = os.path.join(d, "r.pt")
+        mp.spawn(_worker, args=(world, port, out, kind, clip, overlap, bf16), nprocs=world, join=True)
+        r = torch.load(out, weights_only=True)
+    rep, zero = r["rep"], r["zero"]
+    assert r["same"], "ranks disagree after the all-gather"
+    assert zero["stats"]["mode"] == "zero1-reduce-scatter" and rep["stats"]["mode"] == "all-reduce"
+    assert zero["nb"] > 3
+    # pieces: 64-aligned, one per bucket
+    assert all(a % 64 == 0 and b % 64 == 0 and b > a for a, b in zero["pieces"])
+    if world == 2 and not bf16 and kind in ("adamw", "sgd") and clip == 0:
+        # elementwise update, and two-rank sums are a single addition either way: bit for bit
+        assert torch.equal(zero["master"], rep["master"])
+        for k in ("mu", "trace"):
+            if rep[k] is not None:
+                assert torch.equal(zero[k], rep[k]), k
+    else:
+        # per-leaf / global norms summed as per-rank partials, gloo's 4-rank all-reduce and
+        # reduce-scatter adding in different orders, bf16 rounding per rank: equal to rounding
+        tol = 2e-3 if bf16 else 1e-5
+        d = (zero["master"] - rep["master"]).abs().max().item()
+        assert d <= tol * rep["master"].abs().max().item(), d
+        if rep["mu"] is not None:
+            d = (zero["mu"] - rep["mu"]).abs().max().item()
+            assert d <= 1e-3 * rep["mu"].abs().max().item() + 1e-9, d
+
+
+def test_shard_ranges_tile_and_align():
+    from jumbo_mae_tpu_amd.parallel.ddp import shard_ranges
+    rs = shard_ranges([(1000, 5000), (5000, 5003), (5003, 9000), (9000, 20000)], 512)
+    asc = sorted(rs)
+    assert asc[0][0] == 512 and asc[-1][1] == 20480
+    assert all(a % 512 == 0 and b % 512 == 0 and a < b for a, b in rs)
+    assert all(x[1] == y[0] for x, y in zip(asc[:-1], asc[1:]))  # contiguous tiling
+    assert rs == sorted(rs, reverse=True)  # launch order: from the end of the buffer
