@@ -24,7 +24,6 @@ from __future__ import annotations
 
 import argparse
 import json
-import os
 import sys
 import time
 
@@ -153,7 +152,7 @@ def main():
 
     if args.profile_steps > 0 and info.is_main:
         from torch.profiler import ProfilerActivity, profile
-        stacks = os.environ.get("JMAE_PROF_STACK", "")  # e.g. "aten::copy_,aten::cat": where they come from
+        stacks = ""
         with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], with_stack=bool(stacks)) as prof:
             for _ in range(args.profile_steps):
                 step()

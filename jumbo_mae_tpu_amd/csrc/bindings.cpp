@@ -83,6 +83,7 @@ int jm_splitk_reduce_f32(const float* part, int S, int M, int N, const float* bi
 int jm_gemm_nt(const uint16_t* A, long lda, const uint16_t* B, long ldb, int M, int N, int K, int epi,
                const GemmEpi& ep, hipStream_t st);
 void jm_gemm_set_variant(int wn, int group);
+void jm_gemm_set_epi_mode(int mode);
 void jm_gemm_set_tail(int on);
 void jm_gemm_set_narrow(int max_m);
 int jm_gemm_nt_tiles(int M, int N, int K, int epi, long lda);
@@ -109,6 +110,8 @@ int jm_gather_patches(const uint8_t* img, const int* ids, long idsB, uint16_t* o
                       hipStream_t st);
 int jm_embed_finish(const uint16_t* e, const float* pos, const int* ids, long idsB, const float* cls, float* out,
                     int B, int C, int K, int D, hipStream_t st);
+int jm_mask_ids(const float* noise, int R, int N, int keep, int64_t* shuffle, int64_t* restore, int* keep32,
+                int* restore32, float* mask, hipStream_t st);
 int jm_unshuffle_fwd(const uint16_t* y, const float* tok, const int* restore, long rsB, const float* pos, float* out,
                      int B, int C, int K, int N, int d, hipStream_t st);
 int jm_unshuffle_bwd_blocks(int B, int C, int N, int rows_per_block);
@@ -507,6 +510,28 @@ torch::Tensor unshuffle_fwd(torch::Tensor y, torch::Tensor tok, torch::Tensor id
                             out.data_ptr<float>(), B, C, K, N, d, stream()),
            "unshuffle_fwd");
   return out;
+}
+
+// random-masking ids from noise [N] or [R, N] fp32 -> (ids_shuffle i64, ids_restore i64, keep32 i32
+// [.., keep], restore32 i32, mask f32), each shaped like the noise (keep32: last dim keep)
+std::vector<torch::Tensor> mask_ids(torch::Tensor noise, int64_t keep) {
+  CHECK_CUDA(noise);
+  CHECK_CONTIG(noise);
+  CHECK_DT(noise, torch::kFloat32);
+  TORCH_CHECK(noise.dim() == 1 || noise.dim() == 2, "mask_ids: noise [N] or [R, N]");
+  const int N = noise.size(-1), R = noise.dim() == 1 ? 1 : noise.size(0);
+  TORCH_CHECK(N <= 1024 && keep >= 0 && keep <= N, "mask_ids: N <= 1024, 0 <= keep <= N");
+  auto i64 = noise.options().dtype(torch::kInt64), i32 = noise.options().dtype(torch::kInt32);
+  auto shuffle = torch::empty(noise.sizes(), i64), restore = torch::empty(noise.sizes(), i64);
+  auto restore32 = torch::empty(noise.sizes(), i32), mask = torch::empty(noise.sizes(), noise.options());
+  auto ks = noise.sizes().vec();
+  ks.back() = keep;
+  auto keep32 = torch::empty(ks, i32);
+  check_rc(jm_mask_ids(noise.data_ptr<float>(), R, N, (int)keep, shuffle.data_ptr<int64_t>(),
+                       restore.data_ptr<int64_t>(), keep32.data_ptr<int>(), restore32.data_ptr<int>(),
+                       mask.data_ptr<float>(), stream()),
+           "mask_ids");
+  return {shuffle, restore, keep32, restore32, mask};
 }
 
 // -> (dy bf16 [B, C+K, d], d mask_token fp32 [d])
@@ -1077,6 +1102,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("stores") = std::vector<bool>{}, "grouped segmented weight gradients (<= 2 problems)");
   m.def("gemm_tn_wgrad_group", &gemm_tn_wgrad_group, py::arg("dys"), py::arg("xs"), py::arg("gs"),
         py::arg("stores") = std::vector<bool>{}, "grouped weight gradients over one M (<= 4 problems)");
+  m.def("gemm_set_epi_mode", &jm_gemm_set_epi_mode, "experiment: NT epilogue mode (0 LDS-staged, 1 direct, 2 no stores)");
   m.def("gemm_set_variant", &jm_gemm_set_variant, py::arg("nt64"), py::arg("group") = 8,
         "nt64 = 1: every NT launch on the 64-deep main loop (tests); group: row tiles per column sweep");
   m.def("gemm_set_tail", &jm_gemm_set_tail);
@@ -1111,6 +1137,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("patchify_normalize", &patchify_normalize);
   m.def("gather_patches", &gather_patches);
   m.def("embed_finish", &embed_finish);
+  m.def("mask_ids", &mask_ids, "random-masking permutation ids + mask from noise (one workgroup per row)");
   m.def("unshuffle_fwd", &unshuffle_fwd);
   m.def("unshuffle_bwd", &unshuffle_bwd);
   m.def("patch_mse_fwd", &patch_mse_fwd);

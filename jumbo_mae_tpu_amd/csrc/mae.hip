@@ -428,4 +428,44 @@ int jm_mix_patches(const uint8_t* img, const int* perm, const float* prm, const 
   return 0;
 }
 
+// ------------------------------------------------------------------ random masking ids
+// random_masking's permutation algebra (utils_mae.py:88-102) for rows of uniform noise [R, N]
+// (R = 1: one permutation shared by the rank's batch; R = B: per-sample), one workgroup per row:
+// the rank of element i is the number of elements that sort before it (ties broken by index: a
+// stable argsort), so ids_shuffle[rank_i] = i, ids_restore[i] = rank_i and mask[i] = rank_i >= keep.
+// Written as int64 (the API's dtype) and int32 (the gather kernels' operand, keep32 = the first
+// ``keep`` of each row contiguous) -- replaces two radix sorts, their copies and the scatter of the
+// torch composition (a dozen small launches per step).
+namespace {
+__global__ __launch_bounds__(256) void mask_ids_kernel(const float* __restrict__ noise, int N, int keep,
+                                                       int64_t* __restrict__ shuffle, int64_t* __restrict__ restore,
+                                                       int* __restrict__ keep32, int* __restrict__ restore32,
+                                                       float* __restrict__ mask) {
+  __shared__ float v[1024];
+  const long r = blockIdx.x;
+  for (int i = threadIdx.x; i < N; i += 256) v[i] = noise[r * N + i];
+  __syncthreads();
+  for (int i = threadIdx.x; i < N; i += 256) {
+    const float x = v[i];
+    int rank = 0;
+    for (int j = 0; j < N; ++j) {
+      const float y = v[j];
+      rank += (y < x) || (y == x && j < i);
+    }
+    shuffle[r * N + rank] = i;
+    restore[r * N + i] = rank;
+    restore32[r * N + i] = rank;
+    if (rank < keep) keep32[r * keep + rank] = i;
+    mask[r * N + i] = rank >= keep ? 1.f : 0.f;
+  }
+}
+}  // namespace
+
+int jm_mask_ids(const float* noise, int R, int N, int keep, int64_t* shuffle, int64_t* restore, int* keep32,
+                int* restore32, float* mask, hipStream_t st) {
+  if (N > 1024 || keep > N || keep < 0 || R <= 0) return -1;
+  mask_ids_kernel<<<R, 256, 0, st>>>(noise, N, keep, shuffle, restore, keep32, restore32, mask);
+  return 0;
+}
+
 JM_DEBUG_EXPORT(mae)

@@ -24,7 +24,6 @@ from __future__ import annotations
 import contextlib
 
 import math
-import os
 from dataclasses import dataclass, field
 from typing import Callable, Iterable
 
@@ -68,11 +67,11 @@ def identity(a: np.ndarray) -> np.ndarray:
     return a
 
 
-# store-mode gradients (ParamStore.zero_grad; A/B switch JMAE_STORE_GRADS=0 zeroes the whole buffer)
-STORE_GRADS = os.environ.get("JMAE_STORE_GRADS", "1") == "1"
+# store-mode gradients (ParamStore.zero_grad; False zeroes the whole buffer: A/B and tests)
+STORE_GRADS = True
 
-# Handle.weight_t copies refreshed in one batched launch (A/B switch, JMAE_WT_BATCH=0 disables)
-BATCH_TRANSPOSES = os.environ.get("JMAE_WT_BATCH", "1") == "1"
+# Handle.weight_t copies refreshed in one batched launch (False: one launch per copy)
+BATCH_TRANSPOSES = True
 
 
 class Handle:

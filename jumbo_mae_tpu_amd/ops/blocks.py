@@ -18,16 +18,15 @@ ViTBlock = ViTLayer (modeling.py:150-167), the MAE decoder block.
 
 from __future__ import annotations
 
-import os
 
 import torch
 
 from . import prims as P
 
 
-LINKS = os.environ.get("JMAE_LINK_BLOCKS", "1") == "1"  # A/B switch (tools/ab_bench.py)
+LINKS = True  # A/B switch (tools/ab_bench.py)
 # forward hand-off of the upper block's LN1 (Link.ln1); A/B switch
-FWD_LINKS = os.environ.get("JMAE_FWD_LINKS", "1") == "1"
+FWD_LINKS = True
 
 
 class Link:

@@ -77,6 +77,9 @@ def masked_mse(pred: torch.Tensor, target: torch.Tensor, mask: torch.Tensor, nor
 
 # ------------------------------------------------------------------ fused mask-first glue (GPU)
 def _i32(ids: torch.Tensor) -> torch.Tensor:
+    pre = getattr(ids, "_i32", None)  # written by the masking kernel (utils/mae.py masking_ids)
+    if pre is not None:
+        return pre
     return ids.to(torch.int32).contiguous()
 
 

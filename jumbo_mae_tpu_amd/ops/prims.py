@@ -13,7 +13,6 @@ from __future__ import annotations
 
 import contextlib
 import math
-import os
 
 from typing import NamedTuple
 
@@ -50,7 +49,7 @@ def wgrad_split(M: int, N: int, K: int) -> int:
     return s
 
 
-_WGRAD_OURS = os.environ.get("JMAE_WGRAD", "1") == "1"
+_WGRAD_OURS = True
 
 
 def wgrad(h: Handle, dy: torch.Tensor, x: torch.Tensor, rows: tuple[int, int] | None = None) -> None:
@@ -105,8 +104,8 @@ def _tn_ok(dy: torch.Tensor, x: torch.Tensor) -> bool:
 # reduce pass sums them.  Inside a fused block's backward two consecutive weight gradients over the
 # same token rows -- FF2 then FF1, Wo then QKV -- are held and launched as ONE grouped grid
 # (gemm_tn_wgrad_group): twice the tiles, half the splits, half the partial bytes written and
-# re-read.  The first one's ``ready`` waits for the pair.  A/B switch: JMAE_PAIR_WGRAD=0.
-PAIR_WGRAD = os.environ.get("JMAE_PAIR_WGRAD", "1") == "1"
+# re-read.  The first one's ``ready`` waits for the pair.  A/B switch (module attribute): PAIR_WGRAD = False.
+PAIR_WGRAD = True
 _pair: dict = {"depth": 0, "held": None}
 
 
@@ -154,8 +153,8 @@ def bias_grad(hb: Handle, dy: torch.Tensor) -> None:
         hb.grad.add_(dy.sum(0, dtype=torch.float32))
 
 
-_GEMM_MODE = os.environ.get("JMAE_GEMM", "auto")  # auto | blas | ours (forward / dgrad routing)
-_DGRAD_OURS = os.environ.get("JMAE_DGRAD", "1") == "1"  # data-gradient GEMMs on the MFMA kernel
+_GEMM_MODE = "auto"  # auto | blas | ours (forward / dgrad routing)
+_DGRAD_OURS = True  # data-gradient GEMMs on the MFMA kernel
 
 
 NARROW_MAX_M = 4096  # csrc/gemm.hip g_narrow_max_m: below it the NT GEMMs take 128 x 192 tiles
@@ -239,7 +238,7 @@ def linear_gelu_fwd(x2: torch.Tensor, hw: Handle, hb: Handle | None, need_pre: b
 
 
 # save gelu'(h) instead of h for the backward when the fused MFMA forward runs (A/B switch)
-_GELU_DERIV = os.environ.get("JMAE_GELU_DERIV", "1") == "1"
+_GELU_DERIV = True
 
 
 def linear_gelu_fwd_saved(x2: torch.Tensor, hw: Handle, hb: Handle | None, need_pre: bool = True):
@@ -267,7 +266,7 @@ def linear_gelu_fwd_saved(x2: torch.Tensor, hw: Handle, hb: Handle | None, need_
 # 0.4-0.6x.  Round 2 (TN MFMA wgrads): no collapse in 6 processes, +0.3-0.8 %, and ~0.5 ms/step of
 # cross-queue hand-off gaps in the trace (profiles/r2_wgrad_side_stream.txt); kept off so the DP
 # reducer's collectives stay on the compute stream in multi-GPU runs.
-_side = {"stream": None, "enabled": os.environ.get("JMAE_WGRAD_STREAM", "0") == "1", "cb": False}
+_side = {"stream": None, "enabled": False, "cb": False}
 
 
 def _end_of_backward() -> None:
@@ -280,10 +279,10 @@ def _end_of_backward() -> None:
 # 512 rows (one per layer, ~400 TF/s on hipBLASLt).  Their (dy, x) pairs are queued and, at the
 # end of the backward pass, concatenated into ONE GEMM over 24 x 512 rows on the TN MFMA kernel.
 # The DP reducer is told the segment is ready only then (one ``ready`` per queued use).
-_deferred: dict = {"handles": [], "cb": False, "enabled": os.environ.get("JMAE_DEFER_WGRAD", "1") == "1",
+_deferred: dict = {"handles": [], "cb": False, "enabled": True,
                    "force": False,  # also on CPU / fp32 (tests of the deferred + partial-reduce path)
-                   "chunks": int(os.environ.get("JMAE_JUMBO_CHUNKS", "4")),
-                   "seg": os.environ.get("JMAE_SEG_WGRAD", "1") == "1"}  # in-place segmented GEMM
+                   "chunks": 4,
+                   "seg": True}  # in-place segmented GEMM
 
 
 def _row_chunks(n: int, want: int, align: int = 256) -> list[tuple[int, int]]:
@@ -306,7 +305,7 @@ def _seg_ok(dys, xs) -> bool:
             and d0.stride(1) == 1 and x0.stride(1) == 1)
 
 
-GROUP_JUMBO_WGRAD = os.environ.get("JMAE_GROUP_JUMBO_WGRAD", "1") == "1"  # A/B switch
+GROUP_JUMBO_WGRAD = True  # A/B switch
 
 
 def _flush_seg_group(todo: list) -> list:
@@ -520,7 +519,7 @@ def ln_fwd(x3: torch.Tensor, hg: Handle, hb: Handle, out_dtype, also_dtype=None)
     return (y, mean, rstd) if also_dtype is None else (y, mean, rstd, y.to(also_dtype))
 
 
-_FUSE_LN_RES = os.environ.get("JMAE_FUSE_LN_RES", "1") == "1"  # A/B switch (tools/ab_bench.py)
+_FUSE_LN_RES = True  # A/B switch (tools/ab_bench.py)
 
 
 class ResSpec(NamedTuple):

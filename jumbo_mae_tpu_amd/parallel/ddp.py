@@ -47,7 +47,6 @@ MI355X design:
 from __future__ import annotations
 
 import contextlib
-import os
 import re
 
 import torch
@@ -58,6 +57,9 @@ from . import dist as pdist
 
 
 _LAYER = re.compile(r"(dec_)?layer_\d+")
+
+# optimizer launches per step on the split (per-bucket-group) path (profiles/r2_dp_overhead_1rank.txt)
+OPT_GROUPS = 4
 
 
 def unit_key(path: tuple[str, ...]) -> tuple[str, ...]:
@@ -138,8 +140,7 @@ class GradReducer:
         from .dist import forced_group
 
         self.enabled = self.world > 1 or (forced_group() and dist.is_available() and dist.is_initialized())
-        # JMAE_REDUCER_OVERLAP=0: every bucket is launched from finish() (diagnostics / A/B)
-        self.overlap = overlap and self.enabled and os.environ.get("JMAE_REDUCER_OVERLAP", "1") == "1"
+        self.overlap = overlap and self.enabled
         self.sync = True
         self.reduce_dtype = reduce_dtype
         segs = [s for s in store.segments if s.trainable and (seg_filter is None or seg_filter(s))]
@@ -370,13 +371,13 @@ class GradReducer:
 
     def optimizer_groups(self) -> list[list[int]]:
         """Consecutive bucket indices whose optimizer update is issued as ONE launch once all of
-        them are reduced (``JMAE_OPT_GROUPS``, default 4; 0 = one launch per bucket).  Buckets are
+        them are reduced (``OPT_GROUPS`` = 4; 0 = one launch per bucket).  Buckets are
         contiguous flat ranges in launch order, so a group is one contiguous range.  Measured at one
         rank on RCCL: 30 per-bucket AdamW launches cost 0.4 ms/step more than one
         (profiles/r2_dp_overhead_1rank.txt); a few groups keep the update of the early buckets
         overlapped with the reduction of the last ones."""
         nb = len(self.buckets)
-        g = int(os.environ.get("JMAE_OPT_GROUPS", "4"))
+        g = OPT_GROUPS
         g = nb if g <= 0 else max(1, min(g, nb))
         return [list(range(nb * i // g, nb * (i + 1) // g)) for i in range(g)]
 

@@ -19,7 +19,6 @@ Scope: single-process steps (no DP reducer): RCCL collectives are not captured h
 
 from __future__ import annotations
 
-import os
 
 import torch
 
@@ -50,12 +49,12 @@ class GraphedTrainStep:
         if trainer.skip_nonfinite:
             raise ValueError("--skip-nonfinite needs a host sync per step; not capturable")
         self.tr = trainer
-        # Store-mode gradients in captured steps (JMAE_GRAPH_STORE=0: zero-then-accumulate).  A
+        # Store-mode gradients in captured steps (allow_store=False would zero-then-accumulate).  A
         # hipMemsetAsync captured into the graph left the small store-mode gradients as garbage on
         # replay; those zero fills are kernels now (csrc/elementwise.hip jm_zero_f32) and the replay
         # matches the eager step bit for bit (tests/test_graph_gpu.py::
         # test_graphed_grads_match_eager_production_routing, tools/graph_grad_diag.py).
-        trainer.store.allow_store = os.environ.get("JMAE_GRAPH_STORE", "1") == "1"
+        trainer.store.allow_store = True
         self.static = [tuple(t.clone() for t in mb) for mb in example_micro_batches]
         snap = None
         if restore:

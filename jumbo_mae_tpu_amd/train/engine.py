@@ -10,7 +10,6 @@ reference pmean's them every step, CC3, which is a blocking host round trip we a
 
 from __future__ import annotations
 
-import os
 
 import torch
 
@@ -32,7 +31,7 @@ class Trainer:
         self.rngs = rngs
         self.grad_accum = grad_accum
         # update each DP bucket right after its all-reduce (optimizer / reduction-tail overlap)
-        self.overlap_optimizer = os.environ.get("JMAE_OVERLAP_OPT", "1") == "1"
+        self.overlap_optimizer = True
         self._planned = False
         self._comm_events = None  # (start, end) around the last step's reduction wait
         if reducer is not None and getattr(reducer, "shard", False):

@@ -91,7 +91,20 @@ def index_sequence(x: torch.Tensor, ids: torch.Tensor) -> torch.Tensor:
 
 
 def masking_ids(noise: torch.Tensor, keep_len: int):
-    """From uniform noise (N,) or (B,N): ids_shuffle, ids_restore, ids_keep, mask."""
+    """From uniform noise (N,) or (B,N): ids_shuffle, ids_restore, ids_keep, mask.
+
+    On a GPU one HIP kernel computes all of it (csrc/mae.hip mask_ids: stable ranks, one
+    workgroup per row) and also hands the int32 copies the gather kernels read to ops/mae.py as
+    ``ids_keep._i32`` / ``ids_restore._i32``; the torch composition below is the CPU path and the
+    GPU test's oracle."""
+    if noise.is_cuda:
+        from ..ops import _ext  # noqa: PLC0415 (utils import without the extension)
+        if _ext.use_hip(noise):
+            shuffle, restore, keep32, restore32, mask = _ext.load().mask_ids(noise.float().contiguous(), keep_len)
+            ids_keep = shuffle[..., :keep_len]
+            ids_keep._i32 = keep32
+            restore._i32 = restore32
+            return shuffle, restore, ids_keep, mask
     ids_shuffle = torch.argsort(noise, dim=-1)
     ids_restore = torch.argsort(ids_shuffle, dim=-1)
     ids_keep = ids_shuffle[..., :keep_len]

@@ -210,3 +210,22 @@ def test_gemm_tn_wgrad_segmented(ext, n, rows, N, K, cols):
     ref = g.double() + torch.cat(dys)[:, r0:r1].double().t() @ torch.cat(xs).double()
     ext.gemm_tn_wgrad_seg([d[:, r0:r1] for d in dys], xs, g)
     assert rel(g, ref) < 1e-5
+
+
+@pytest.mark.parametrize("R,N,K", [(1, 196, 49), (64, 196, 49), (3, 1024, 256), (2, 17, 0)])
+def test_mask_ids_matches_torch(ext, R, N, K):
+    """csrc/mae.hip mask_ids (stable ranks) == the torch argsort composition of random_masking
+    (utils_mae.py:88-102), including duplicated noise values (ties broken by index)."""
+    g = torch.Generator(device="cuda").manual_seed(5)
+    noise = torch.rand((R, N), device="cuda", generator=g)
+    noise[:, 1::7] = noise[:, 0:1]  # ties
+    x = noise[0] if R == 1 else noise
+    sh, rs, keep32, rs32, mask = ext.mask_ids(x.contiguous(), K)
+    ref_sh = torch.argsort(x, dim=-1, stable=True)
+    ref_rs = torch.argsort(ref_sh, dim=-1, stable=True)
+    assert torch.equal(sh, ref_sh) and torch.equal(rs, ref_rs)
+    assert torch.equal(keep32.long(), ref_sh[..., :K]) and torch.equal(rs32.long(), ref_rs)
+    assert torch.equal(mask, (ref_rs >= K).float())
+    # the model entry point returns the same ids and the int32 copies the gather kernels read
+    s2, r2, k2, m2 = masking_ids(x, K)
+    assert torch.equal(s2, ref_sh) and torch.equal(k2._i32, keep32) and torch.equal(r2._i32, rs32)
