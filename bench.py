@@ -5,8 +5,11 @@ Metric/config from BASELINE.json: "pretrain images/sec (whole node) ViT-L/16 224
 1/2/4/8 MI355X" -- ViT-L/16 Jumbo encoder (24 x 1024, 16 heads, 3 CLS tokens, shared jumbo
 MLP), MAE decoder 8 x 512 (16 heads), mask ratio 0.75, AdamW(0.9, 0.95) + warmup-cosine with the
 reference preset (config/pretrain/pretrain-vit-l16-224-in1k-800ep.sh), bf16 compute / fp32
-master weights.  Global batch 4096 on 8 GPUs = 512 images per GPU; weak scaling keeps 512 per
-GPU at every N.  Data: synthetic uint8 224x224 images resident on the GPU, random-init weights
+master weights.  The reference preset's global batch of 4096 images per optimizer step is kept at
+every N (strong scaling): 512 images per GPU on 8 GPUs, 1024 on 4, 2048 on 2, and on one GPU
+2 x 2048 accumulated micro-batches -- the global batch fits in one MI355X's 288 GB (peak ~174 GB at
+a 2048 micro-batch).  ``--batch-per-gpu B`` fixes the per-GPU batch instead (weak scaling).
+Data: synthetic uint8 224x224 images resident on the GPU, random-init weights
 (no datasets/checkpoints offline).  Every timed step is a full train step: forward, backward,
 RCCL gradient all-reduce, optimizer update.
 
@@ -41,8 +44,15 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--model", default="vit_large_patch16", choices=["vit_large_patch16", "vit_base_patch16",
                                                                       "vit_small_patch16", "vit_tiny_patch16"])
-    ap.add_argument("--batch-per-gpu", type=int, default=512)
-    ap.add_argument("--grad-accum", type=int, default=1)
+    ap.add_argument("--global-batch", type=int, default=4096,
+                    help="images per optimizer step over the whole job (reference preset: 4096)")
+    ap.add_argument("--batch-per-gpu", type=int, default=0,
+                    help="images per GPU per step; 0 (default) = global-batch / N (strong scaling); a value "
+                         "fixes the per-GPU work at every N (weak scaling)")
+    ap.add_argument("--max-micro-batch", type=int, default=2048,
+                    help="largest micro-batch per GPU (HBM: ~174 GB at 2048 for ViT-L); a larger per-GPU batch "
+                         "runs as gradient accumulation")
+    ap.add_argument("--grad-accum", type=int, default=0, help="micro-steps per step (0: derived)")
     ap.add_argument("--grad-ckpt", action="store_true", help="activation checkpointing per layer (memory table)")
     ap.add_argument("--bucket-mb", type=float, default=64.0)
     ap.add_argument("--reduce-dtype", default="fp32", choices=["fp32", "bf16"],
@@ -77,7 +87,17 @@ def main():
     cdt = torch.float32 if args.cpu else torch.bfloat16
     if world != args.gpus and info.is_main:
         log(f"[bench] warning: --gpus {args.gpus} but WORLD_SIZE={world}; reporting WORLD_SIZE")
-    B = args.batch_per_gpu
+    # strong scaling by default: the reference's global batch 4096 at every N -- 2 x 2048 accumulated
+    # micro-batches on 1 GPU (the global batch fitting in one MI355X's HBM), 2048 / 1024 / 512 per GPU
+    # on 2 / 4 / 8 GPUs; --batch-per-gpu fixes the per-GPU batch instead (weak scaling)
+    strong = args.batch_per_gpu == 0
+    B = args.global_batch // world if strong else args.batch_per_gpu
+    if strong and B * world != args.global_batch:
+        raise SystemExit(f"global batch {args.global_batch} does not split over {world} ranks")
+    if args.grad_accum <= 0:
+        args.grad_accum = max(1, -(-B // args.max_micro_batch))
+    if B % args.grad_accum:
+        raise SystemExit(f"batch {B} per GPU does not split into {args.grad_accum} micro-batches")
     global_batch = B * world
 
     vc = vit_config(args.model, labels=0, posemb="sincos2d", image_mask_ratio=0.75, droppath=0.0, dropout=0.0,
@@ -177,7 +197,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(ms, 3),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if strong else "weak",
             "vs_baseline": None,
             "mfu_bf16_dense": round(mfu(value, pretrain_fwd_flops_per_image(vc, dc), world), 4),
             # GPU time of the last step behind the DP reduction wait (exposed comm + overlapped
@@ -197,6 +217,7 @@ def main():
                 "parallelism": f"dp{world}",
                 "per_gpu_batch": B,
                 "grad_accum": args.grad_accum,
+                "micro_batch": mb,
                 "grad_ckpt": args.grad_ckpt,
                 "hip_graph": bool(runner.graphed is not None),
                 "optimizer": "adamw(0.9,0.95) wd0.05 warmup-cosine",
@@ -222,7 +243,7 @@ def bench_classifier(args):
     world = info.world_size
     N = 1281167
     if args.task == "finetune":
-        B = args.batch_per_gpu if args.batch_per_gpu != 512 else 128
+        B = args.batch_per_gpu or 128
         gb = B * world
         flags = ["--mode", "finetune", "--layers", "12", "--dim", "768", "--heads", "12", "--labels", "1000",
                  "--posemb", "sincos2d", "--droppath", "0.1", "--mixup", "0.8", "--cutmix", "1.0",
@@ -231,7 +252,7 @@ def bench_classifier(args):
                  "--training-steps", str(N * 110 // 1024)]
         model_name, recipe = "vit_base_patch16 jumbo (3 CLS) finetune", "adamw llrd0.75 mixup0.8 cutmix1.0 ls0.1 dp0.1"
     else:
-        B = args.batch_per_gpu if args.batch_per_gpu != 512 else 2048
+        B = args.batch_per_gpu or 2048
         gb = B * world
         flags = ["--mode", "linear", "--layers", "24", "--dim", "1024", "--heads", "16", "--labels", "1000",
                  "--posemb", "sincos2d", "--droppath", "0.0", "--mixup", "0.0", "--cutmix", "0.0",

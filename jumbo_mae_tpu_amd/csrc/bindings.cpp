@@ -83,7 +83,6 @@ int jm_splitk_reduce_f32(const float* part, int S, int M, int N, const float* bi
 int jm_gemm_nt(const uint16_t* A, long lda, const uint16_t* B, long ldb, int M, int N, int K, int epi,
                const GemmEpi& ep, hipStream_t st);
 void jm_gemm_set_variant(int wn, int group);
-void jm_gemm_set_epi_mode(int mode);
 void jm_gemm_set_tail(int on);
 void jm_gemm_set_narrow(int max_m);
 int jm_gemm_nt_tiles(int M, int N, int K, int epi, long lda);
@@ -510,6 +509,14 @@ torch::Tensor unshuffle_fwd(torch::Tensor y, torch::Tensor tok, torch::Tensor id
                             out.data_ptr<float>(), B, C, K, N, d, stream()),
            "unshuffle_fwd");
   return out;
+}
+
+// t[:] = 0 by the kernel the store-mode gradients use in front of an accumulating reduce (graph tests)
+void zero_f32(torch::Tensor t) {
+  CHECK_CUDA(t);
+  CHECK_CONTIG(t);
+  CHECK_DT(t, torch::kFloat32);
+  jm_zero_f32(t.data_ptr<float>(), t.numel(), stream());
 }
 
 // random-masking ids from noise [N] or [R, N] fp32 -> (ids_shuffle i64, ids_restore i64, keep32 i32
@@ -1102,7 +1109,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("stores") = std::vector<bool>{}, "grouped segmented weight gradients (<= 2 problems)");
   m.def("gemm_tn_wgrad_group", &gemm_tn_wgrad_group, py::arg("dys"), py::arg("xs"), py::arg("gs"),
         py::arg("stores") = std::vector<bool>{}, "grouped weight gradients over one M (<= 4 problems)");
-  m.def("gemm_set_epi_mode", &jm_gemm_set_epi_mode, "experiment: NT epilogue mode (0 LDS-staged, 1 direct, 2 no stores)");
   m.def("gemm_set_variant", &jm_gemm_set_variant, py::arg("nt64"), py::arg("group") = 8,
         "nt64 = 1: every NT launch on the 64-deep main loop (tests); group: row tiles per column sweep");
   m.def("gemm_set_tail", &jm_gemm_set_tail);
@@ -1137,6 +1143,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("patchify_normalize", &patchify_normalize);
   m.def("gather_patches", &gather_patches);
   m.def("embed_finish", &embed_finish);
+  m.def("zero_f32", &zero_f32, "fp32 zero fill kernel (the store-mode gradients' pre-reduce fill)");
   m.def("mask_ids", &mask_ids, "random-masking permutation ids + mask from noise (one workgroup per row)");
   m.def("unshuffle_fwd", &unshuffle_fwd);
   m.def("unshuffle_bwd", &unshuffle_bwd);

@@ -719,89 +719,7 @@ __attribute__((always_inline)) JM_DEVICE void p4_epilogue(const f32x4_t (&acc)[8
     epilogue<EPI, NTW, MTW>(acc, ep, M, N, m0 + wr * HR, n0 + wc * NTW * 16, l16, g);
 }
 
-// Direct epilogue (no LDS image, no barrier): bias / activation on the fp32 accumulators, bf16
-// packing, then one v_permlane16_swap per dword pairs the two 16-column MFMA tiles (2p, 2p + 1) of a
-// lane quad so that lane group g holds 8 CONSECUTIVE columns of its row -- tile 2p + (g & 1),
-// columns (g >> 1) * 8 + [0, 8) -- and every store is 16 B per lane (16 rows x 64 B per
-// instruction).  EM = 2 (diagnostic): no stores at all, the accumulators kept live -- the cost of
-// the epilogue is the difference to EM = 0.
-template <int EPI, int MTL, int EM>
-__attribute__((always_inline)) JM_DEVICE void p4_epilogue_direct(const f32x4_t (&acc)[8][4], const GemmEpi& ep,
-                                                                 int M, int N, int m0, int n0) {
-  constexpr int HR = 64 + 16 * MTL, MTW = 4 + MTL;
-  if constexpr (EM == 2) {
-#pragma unroll
-    for (int mt = 0; mt < MTW; ++mt)
-#pragma unroll
-      for (int nt = 0; nt < 4; ++nt) asm volatile("" ::"v"(acc[mt][nt]));
-    return;
-  }
-  const int tid = threadIdx.x;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
-  const int l16 = lane & 15, g = lane >> 4;
-  const int wr = wave / 4, wc = wave % 4;
-#pragma unroll
-  for (int p = 0; p < 2; ++p) {
-    const int nb = n0 + wc * 64 + p * 32;       // first column of the tile pair
-    const int ncol = nb + (g & 1) * 16 + (g >> 1) * 8;  // this lane's 8 columns after the swap
-    float b0[4] = {0.f, 0.f, 0.f, 0.f}, b1[4] = {0.f, 0.f, 0.f, 0.f};
-    if (ep.bias) {
-      if (nb + 4 * g < N) load4(ep.bias + nb + 4 * g, b0);
-      if (nb + 16 + 4 * g < N) load4(ep.bias + nb + 16 + 4 * g, b1);
-    }
-#pragma unroll
-    for (int mt = 0; mt < MTW; ++mt) {
-      const int m = m0 + wr * HR + mt * 16 + l16;
-      float v[8];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        v[i] = acc[mt][2 * p][i] + b0[i];
-        v[4 + i] = acc[mt][2 * p + 1][i] + b1[i];
-      }
-      uint32_t o[4], o2[4];
-      if constexpr (EPI == EPI_GELU_D || EPI == EPI_GELU_ONLY) {
-        float h[8], gv[8], dv[8];
-#pragma unroll
-        for (int i = 0; i < 8; ++i) h[i] = bf2f(f2bf(v[i]));
-        if constexpr (EPI == EPI_GELU_D) {
-          gelu_n<8, true, true>(h, gv, dv);
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            o[i] = pack_bf2(dv[2 * i], dv[2 * i + 1]);
-            o2[i] = pack_bf2(gv[2 * i], gv[2 * i + 1]);
-          }
-        } else {
-          gelu_n<8, true, false>(h, gv, nullptr);
-#pragma unroll
-          for (int i = 0; i < 4; ++i) o[i] = pack_bf2(gv[2 * i], gv[2 * i + 1]);
-        }
-      } else {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) o[i] = pack_bf2(v[2 * i], v[2 * i + 1]);
-      }
-      // o[0..1] = tile 2p (cols 4g..4g+3), o[2..3] = tile 2p+1: swap lanes 16-31 / 48-63 of the first
-      // with lanes 0-15 / 32-47 of the second
-#pragma unroll
-      for (int d = 0; d < 2; ++d) {
-        auto r = __builtin_amdgcn_permlane16_swap(o[d], o[2 + d], false, false);
-        o[d] = r[0];
-        o[2 + d] = r[1];
-        if constexpr (EPI == EPI_GELU_D) {
-          auto r2 = __builtin_amdgcn_permlane16_swap(o2[d], o2[2 + d], false, false);
-          o2[d] = r2[0];
-          o2[2 + d] = r2[1];
-        }
-      }
-      if (m < M && ncol < N) {
-        st16(ep.out + (long)m * ep.ldo + ncol, make_uint4(o[0], o[1], o[2], o[3]), true);
-        if constexpr (EPI == EPI_GELU_D)
-          st16(ep.out2 + (long)m * ep.ldo + ncol, make_uint4(o2[0], o2[1], o2[2], o2[3]), true);
-      }
-    }
-  }
-}
-
-template <int EPI, int MTL = 4, int EM = 0>
+template <int EPI, int MTL = 4>
 __global__ __launch_bounds__(512, 1) void gemm_p4_kernel(const uint16_t* __restrict__ A, long lda,
                                                          const uint16_t* __restrict__ B, long ldb, int M, int N,
                                                          int K, GemmEpi ep, int GROUP_M) {
@@ -825,12 +743,7 @@ __global__ __launch_bounds__(512, 1) void gemm_p4_kernel(const uint16_t* __restr
   }
   f32x4_t acc[8][4];
   p4_mainloop<MTL>(A, lda, B, ldb, M, N, m0, n0, k_begin, K, acc, smem);
-  if constexpr (EM > 0) {
-    if (__builtin_amdgcn_readfirstlane(threadIdx.x) >= 256) __builtin_amdgcn_s_setprio(0);
-    p4_epilogue_direct<EPI, MTL, EM>(acc, ep, M, N, m0, n0);
-  } else {
-    p4_epilogue<EPI, MTL>(acc, ep, M, N, m0, n0, split, smem);
-  }
+  p4_epilogue<EPI, MTL>(acc, ep, M, N, m0, n0, split, smem);
 }
 
 // ------------------------------------------------------------------ narrow tiles (M < 4096)
@@ -1172,30 +1085,16 @@ void launch_nt64(const uint16_t* A, long lda, const uint16_t* B, long ldb, int M
   gemm_nt64_kernel<EPI, NTS><<<nwg, 512, GEMM_SMEM, st>>>(A, lda, B, ldb, M, N, K, ep, g_gemm_group);
 }
 
-int g_gemm_epi_mode = 0;  // experiment: 1 = direct (register) epilogue, 2 = no stores (diagnostic)
-
-template <int EPI, int MTL, int EM>
-void launch_p4_em(const uint16_t* A, long lda, const uint16_t* B, long ldb, int M, int N, int K, const GemmEpi& ep,
-                  int nwg, hipStream_t st) {
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute((const void*)gemm_p4_kernel<EPI, MTL, EM>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)GEMM_SMEM);
-    attr = true;
-  }
-  gemm_p4_kernel<EPI, MTL, EM><<<nwg, 512, GEMM_SMEM, st>>>(A, lda, B, ldb, M, N, K, ep, g_gemm_group);
-}
-
 template <int EPI, int MTL>
 void launch_p4(const uint16_t* A, long lda, const uint16_t* B, long ldb, int M, int N, int K, const GemmEpi& ep,
                int nwg, hipStream_t st) {
-  if constexpr (EPI == EPI_STORE || EPI == EPI_GELU_D || EPI == EPI_GELU_ONLY) {
-    if (ep.t_count == 0 && N % 8 == 0) {
-      if (g_gemm_epi_mode == 1) return launch_p4_em<EPI, MTL, 1>(A, lda, B, ldb, M, N, K, ep, nwg, st);
-      if (g_gemm_epi_mode == 2) return launch_p4_em<EPI, MTL, 2>(A, lda, B, ldb, M, N, K, ep, nwg, st);
-    }
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)gemm_p4_kernel<EPI, MTL>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)GEMM_SMEM);
+    attr = true;
   }
-  launch_p4_em<EPI, MTL, 0>(A, lda, B, ldb, M, N, K, ep, nwg, st);
+  gemm_p4_kernel<EPI, MTL><<<nwg, 512, GEMM_SMEM, st>>>(A, lda, B, ldb, M, N, K, ep, g_gemm_group);
 }
 
 template <int EPI>
@@ -1307,8 +1206,6 @@ void jm_gemm_set_variant(int nt64, int group) {
 }
 
 void jm_gemm_set_tail(int on) { g_gemm_tail = on; }
-
-void jm_gemm_set_epi_mode(int mode) { g_gemm_epi_mode = mode; }
 
 void jm_gemm_set_narrow(int max_m) { g_narrow_max_m = max_m; }
 

@@ -81,9 +81,6 @@ def main():
         m = re.search(r"r(\d+)", v)
         ext.gemm_set_rows(int(m.group(1)) if m else 0)
         v = re.sub(r"r\d+", "", v)
-        m = re.search(r"e(\d)", v)  # eN: NT epilogue mode (0 LDS-staged, 1 direct, 2 no stores)
-        ext.gemm_set_epi_mode(int(m.group(1)) if m else 0)
-        v = re.sub(r"e\d", "", v)
         ext.gemm_set_tail(1 if "t" in v else 0)
         ext.gemm_set_narrow(1 << 30 if "n" in v else 0 if "w" in v else 4096)
         ext.gemm_set_variant(int(v.rstrip("tnw")), a.group)
