@@ -59,10 +59,10 @@ JM_DEVICE f32x4_t mfma(bf16x8_t a, bf16x8_t b, f32x4_t c) {
 // XCDs, so heads h and h + 1 of one token row -- the two halves of a 128-B line at hd = 32 --
 // would be read (and written) through two different L2s.  With remap the grid is relabelled
 // bijectively so that consecutive (b, h) share an XCD (the GEMM tile remap); placement only
-// changes speed, never results.
-JM_DEVICE int xcd_bid(int remap) {
+// changes speed, never results (dec fwd 175 -> 163 us, bwd 361 -> 340 us with the forward's
+// batched staging below; profiles/r2_attn_remap.txt).
+JM_DEVICE int xcd_bid() {
   const int orig = blockIdx.x, nwg = gridDim.x;
-  if (!(remap & 1)) return orig;
   const int xcd = orig & 7, q = nwg >> 3, r = nwg & 7;
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
 }
@@ -77,7 +77,6 @@ JM_DEVICE int xcd_bid(int remap) {
 //  * the row sum comes out of the MFMA: an all-ones A operand next to V^T sums the same bf16 P
 //    the P.V product uses (7 extra MFMAs per query tile instead of one add per score);
 //  * query tiles past S (fully padded) are skipped.
-// remap bit 2 selects the previous per-score form (A/B switch).
 JM_DEVICE f32x4_t key_init(int kt, int g, int S) {
   f32x4_t a = {0.f, 0.f, 0.f, 0.f};
   if (kt * 16 + 16 > S) {
@@ -137,21 +136,22 @@ JM_DEVICE f32x4_t qk_init(int kt, int g, int S) {
 }
 
 // --------------------------------------------------------------------------------- forward
-template <int HD, int SP, bool TR, bool EX = false>
+// One (b, h) per workgroup.  LDS holds row-major K and V images (V^T operands come out of the
+// transposing ds_read_b64_tr_b16); the Q fragments of every query tile of a wave and all of a
+// thread's K / V chunks are loaded up front, one HBM round trip instead of one per chunk.
+template <int HD, int SP, bool EX = false>
 __global__ __launch_bounds__(256) void attn_fwd_kernel(const uint16_t* __restrict__ qkv, uint16_t* __restrict__ o,
-                                                       float* __restrict__ lse, int S, int H, float scale,
-                                                       int remap) {
+                                                       float* __restrict__ lse, int S, int H, float scale) {
   JM_DGUARD(S >= 1 && S <= SP && blockDim.x == 256);
-  constexpr int KS = HD + 8;  // K row stride (elements), 16-B aligned, breaks bank aliasing
-  constexpr int VS = SP + 8;  // V^T row stride
+  constexpr int KS = HD + 8;  // K / V row stride (elements), 16-B aligned, breaks bank aliasing
   constexpr int NT = SP / 16;
   constexpr int KK = HD / 32;
   constexpr int DT = HD / 16;
   extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
   uint16_t* Ks = smem;
-  uint16_t* Vt = smem + SP * KS;  // TR: row-major V [SP][KS]; else V^T [HD][VS]
+  uint16_t* Vs = smem + SP * KS;
 
-  const int bh = xcd_bid(remap);
+  const int bh = xcd_bid();
   const int b = bh / H, h = bh - (bh / H) * H;
   const long ts = 3L * H * HD;  // token stride in qkv
   const uint16_t* base = qkv + (long)b * S * ts;
@@ -161,25 +161,19 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const uint16_t* __restric
 
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int l16 = lane & 15, g = lane >> 4;
-  // the Q fragments of every query tile of this wave, loaded up front so their latency overlaps
-  // the K / V staging instead of stalling each tile (remap bit 1; A/B switch)
   constexpr int NQW = (SP / 16 + 3) / 4;
-  bf16x8_t qpre[NQW][HD / 32];
-  const bool qp = (remap & 2) != 0;
-  if (qp) {
+  bf16x8_t qpre[NQW][KK];
 #pragma unroll
-    for (int i = 0; i < NQW; ++i) {
-      const int q = (wave + 4 * i) * 16 + l16;
+  for (int i = 0; i < NQW; ++i) {
+    const int q = (wave + 4 * i) * 16 + l16;
 #pragma unroll
-      for (int kk = 0; kk < HD / 32; ++kk) {
-        s16x8_t z = {0, 0, 0, 0, 0, 0, 0, 0};
-        qpre[i][kk] = q < S ? ld8(Qg + (long)q * ts + 32 * kk + 8 * g) : __builtin_bit_cast(bf16x8_t, z);
-      }
+    for (int kk = 0; kk < KK; ++kk) {
+      s16x8_t z = {0, 0, 0, 0, 0, 0, 0, 0};
+      qpre[i][kk] = q < S ? ld8(Qg + (long)q * ts + 32 * kk + 8 * g) : __builtin_bit_cast(bf16x8_t, z);
     }
   }
   constexpr int CPR = HD / 8;
-  if (TR && (remap & 2)) {
-    // all of this thread's K / V chunks in flight at once (one HBM round trip, not one per chunk)
+  {
     constexpr int NIT = (SP * CPR + 255) / 256;
     uint4 kv[NIT], vv[NIT];
 #pragma unroll
@@ -196,158 +190,35 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const uint16_t* __restric
       const int i = it * 256 + threadIdx.x, r = i / CPR, c = (i % CPR) * 8;
       if (i < SP * CPR) {
         *reinterpret_cast<uint4*>(Ks + r * KS + c) = kv[it];
-        *reinterpret_cast<uint4*>(Vt + r * KS + c) = vv[it];
-      }
-    }
-  } else {
-    for (int i = threadIdx.x; i < SP * CPR; i += 256) {
-      const int r = i / CPR, c = (i % CPR) * 8;
-      uint4 kv = make_uint4(0, 0, 0, 0), vv = make_uint4(0, 0, 0, 0);
-      if (r < S) {
-        kv = *reinterpret_cast<const uint4*>(Kg + r * ts + c);
-        vv = *reinterpret_cast<const uint4*>(Vg + r * ts + c);
-      }
-      *reinterpret_cast<uint4*>(Ks + r * KS + c) = kv;
-      if (TR) {
-        *reinterpret_cast<uint4*>(Vt + r * KS + c) = vv;
-      } else {
-        const uint16_t* vh = reinterpret_cast<const uint16_t*>(&vv);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) Vt[(c + j) * VS + r] = vh[j];
+        *reinterpret_cast<uint4*>(Vs + r * KS + c) = vv[it];
       }
     }
   }
   __syncthreads();
 
   const float sl2 = scale * LOG2E;
-
-  if (!(remap & 4)) {
-    const int NTv = (S + 15) >> 4;
-#pragma unroll
-    for (int it = 0; it < NQW; ++it) {
-      const int qt = wave + 4 * it;
-      if (qt >= NTv) break;
-      const int q = qt * 16 + l16;
-      bf16x8_t qf[KK];
-#pragma unroll
-      for (int kk = 0; kk < KK; ++kk) {
-        if (qp) {
-          qf[kk] = qpre[it][kk];
-        } else if (q < S) {
-          qf[kk] = ld8(Qg + (long)q * ts + 32 * kk + 8 * g);
-        } else {
-          s16x8_t z = {0, 0, 0, 0, 0, 0, 0, 0};
-          qf[kk] = __builtin_bit_cast(bf16x8_t, z);
-        }
-      }
-      f32x4_t sc[NT];
-#pragma unroll
-      for (int kt = 0; kt < NT; ++kt) {
-        f32x4_t acc = qk_init<NT, EX>(kt, g, S);
-#pragma unroll
-        for (int kk = 0; kk < KK; ++kk) acc = mfma(ld8(Ks + (kt * 16 + l16) * KS + 32 * kk + 8 * g), qf[kk], acc);
-        sc[kt] = acc;
-      }
-      f32x4_t oacc[DT];
-      float ms, l;
-      softmax_pv(sc, sl2,
-                 [&](int s, int dt) {
-                   if (TR) {
-                     const uint16_t* vr = Vt + (32 * s + 4 * g + (l16 >> 2)) * KS + dt * 16 + 4 * (l16 & 3);
-                     return cat44(tr4(vr), tr4(vr + 16 * KS));
-                   }
-                   const uint16_t* vr = Vt + (dt * 16 + l16) * VS + 32 * s + 4 * g;
-                   return cat44(ld4(vr), ld4(vr + 16));
-                 },
-                 oacc, ms, l);
-      if (q < S) {
-        const float inv = 1.f / l;
-        uint16_t* orow = o + ((long)b * S + q) * H * HD + h * HD;
-#pragma unroll
-        for (int dt = 0; dt < DT; ++dt) {
-          float v[4] = {oacc[dt][0] * inv, oacc[dt][1] * inv, oacc[dt][2] * inv, oacc[dt][3] * inv};
-          store4(orow + dt * 16 + 4 * g, v);
-        }
-        if (g == 0) lse[((long)b * H + h) * S + q] = (ms + log2f(l)) * LN2;
-      }
-    }
-    return;
-  }
-
+  const int NTv = (S + 15) >> 4;
 #pragma unroll
   for (int it = 0; it < NQW; ++it) {
     const int qt = wave + 4 * it;
-    if (qt >= NT) break;
+    if (qt >= NTv) break;
     const int q = qt * 16 + l16;
-    bf16x8_t qf[KK];
-#pragma unroll
-    for (int kk = 0; kk < KK; ++kk) {
-      if (qp) {
-        qf[kk] = qpre[it][kk];
-      } else if (q < S) {
-        qf[kk] = ld8(Qg + (long)q * ts + 32 * kk + 8 * g);
-      } else {
-        s16x8_t z = {0, 0, 0, 0, 0, 0, 0, 0};
-        qf[kk] = __builtin_bit_cast(bf16x8_t, z);
-      }
-    }
     f32x4_t sc[NT];
 #pragma unroll
     for (int kt = 0; kt < NT; ++kt) {
-      f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
+      f32x4_t acc = qk_init<NT, EX>(kt, g, S);
 #pragma unroll
-      for (int kk = 0; kk < KK; ++kk) acc = mfma(ld8(Ks + (kt * 16 + l16) * KS + 32 * kk + 8 * g), qf[kk], acc);
+      for (int kk = 0; kk < KK; ++kk) acc = mfma(ld8(Ks + (kt * 16 + l16) * KS + 32 * kk + 8 * g), qpre[it][kk], acc);
       sc[kt] = acc;
     }
-    // sc[kt][i] = S^T[key = kt*16 + 4g + i][query = qt*16 + l16]
-    float m = -INFINITY;
-#pragma unroll
-    for (int kt = 0; kt < NT; ++kt) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int key = kt * 16 + 4 * g + i;
-        const float v = key < S ? sc[kt][i] * sl2 : -INFINITY;
-        sc[kt][i] = v;
-        m = fmaxf(m, v);
-      }
-    }
-    m = fmaxf(m, __shfl_xor(m, 16, WAVE));
-    m = fmaxf(m, __shfl_xor(m, 32, WAVE));
-    float l = 0.f;
-#pragma unroll
-    for (int kt = 0; kt < NT; ++kt) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const float p = __builtin_amdgcn_exp2f(sc[kt][i] - m);
-        sc[kt][i] = p;
-        l += p;
-      }
-    }
-    l += __shfl_xor(l, 16, WAVE);
-    l += __shfl_xor(l, 32, WAVE);
-
     f32x4_t oacc[DT];
-#pragma unroll
-    for (int dt = 0; dt < DT; ++dt) oacc[dt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int s = 0; s < NT / 2; ++s) {
-      float pf[8] = {sc[2 * s][0], sc[2 * s][1], sc[2 * s][2], sc[2 * s][3],
-                     sc[2 * s + 1][0], sc[2 * s + 1][1], sc[2 * s + 1][2], sc[2 * s + 1][3]};
-      const bf16x8_t pb = pack8(pf);
-#pragma unroll
-      for (int dt = 0; dt < DT; ++dt) {
-        bf16x8_t va;
-        if (TR) {
-          const uint16_t* vr = Vt + (32 * s + 4 * g + (l16 >> 2)) * KS + dt * 16 + 4 * (l16 & 3);
-          va = cat44(tr4(vr), tr4(vr + 16 * KS));
-        } else {
-          const uint16_t* vr = Vt + (dt * 16 + l16) * VS + 32 * s + 4 * g;
-          va = cat44(ld4(vr), ld4(vr + 16));
-        }
-        oacc[dt] = mfma(va, pb, oacc[dt]);
-      }
-    }
-    // oacc[dt][i] = O^T[d = dt*16 + 4g + i][query]
+    float ms, l;
+    softmax_pv(sc, sl2,
+               [&](int s, int dt) {
+                 const uint16_t* vr = Vs + (32 * s + 4 * g + (l16 >> 2)) * KS + dt * 16 + 4 * (l16 & 3);
+                 return cat44(tr4(vr), tr4(vr + 16 * KS));
+               },
+               oacc, ms, l);
     if (q < S) {
       const float inv = 1.f / l;
       uint16_t* orow = o + ((long)b * S + q) * H * HD + h * HD;
@@ -356,13 +227,13 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const uint16_t* __restric
         float v[4] = {oacc[dt][0] * inv, oacc[dt][1] * inv, oacc[dt][2] * inv, oacc[dt][3] * inv};
         store4(orow + dt * 16 + 4 * g, v);
       }
-      if (g == 0) lse[((long)b * H + h) * S + q] = (m + log2f(l)) * LN2;
+      if (g == 0) lse[((long)b * H + h) * S + q] = (ms + log2f(l)) * LN2;
     }
   }
 }
 
 // ------------------------------------------------------------------ forward, multi-head loop
-// Same math and LDS images as attn_fwd_kernel<HD, SP, true>, but one workgroup walks ``hpw``
+// Same math and LDS images as attn_fwd_kernel, but one workgroup walks ``hpw``
 // consecutive (b, h) pairs: the next pair's K / V rows are loaded into registers right after
 // the current pair's images are in LDS, so their HBM latency hides behind the current pair's
 // MFMA / softmax work (the one-pair kernel stalls on every load phase); Q fragments of the next
@@ -370,7 +241,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const uint16_t* __restric
 template <int HD, int SP, bool EX = false>
 __global__ __launch_bounds__(256) void attn_fwd_ml_kernel(const uint16_t* __restrict__ qkv, uint16_t* __restrict__ o,
                                                           float* __restrict__ lse, int S, int H, int BH, int hpw,
-                                                          float scale, int remap) {
+                                                          float scale) {
   JM_DGUARD(S >= 1 && S <= SP && hpw >= 1 && blockDim.x == 256);
   constexpr int KS = HD + 8;
   constexpr int NT = SP / 16;
@@ -426,7 +297,7 @@ __global__ __launch_bounds__(256) void attn_fwd_ml_kernel(const uint16_t* __rest
     }
   };
 
-  const int bh0 = xcd_bid(remap) * hpw;
+  const int bh0 = xcd_bid() * hpw;
   load(bh0);
   for (int j = 0; j < hpw; ++j) {
     const int bh = bh0 + j;
@@ -446,80 +317,21 @@ __global__ __launch_bounds__(256) void attn_fwd_ml_kernel(const uint16_t* __rest
       for (int kk = 0; kk < KK; ++kk) qf[kk] = qn[kk];
       if (qt + 4 < NT) load_q(Qg, qt + 4, qn);
       f32x4_t sc[NT];
-      if (!(remap & 4)) {
-#pragma unroll
-        for (int kt = 0; kt < NT; ++kt) {
-          f32x4_t acc = qk_init<NT, EX>(kt, g, S);
-#pragma unroll
-          for (int kk = 0; kk < KK; ++kk) acc = mfma(ld8(Ks + (kt * 16 + l16) * KS + 32 * kk + 8 * g), qf[kk], acc);
-          sc[kt] = acc;
-        }
-        f32x4_t oacc[DT];
-        float ms, l;
-        softmax_pv(sc, sl2,
-                   [&](int s, int dt) {
-                     const uint16_t* vr2 = Vt + (32 * s + 4 * g + (l16 >> 2)) * KS + dt * 16 + 4 * (l16 & 3);
-                     return cat44(tr4(vr2), tr4(vr2 + 16 * KS));
-                   },
-                   oacc, ms, l);
-        if (q < S) {
-          const float inv = 1.f / l;
-          uint16_t* orow = o + ((long)b * S + q) * H * HD + h * HD;
-#pragma unroll
-          for (int dt = 0; dt < DT; ++dt) {
-            float v[4] = {oacc[dt][0] * inv, oacc[dt][1] * inv, oacc[dt][2] * inv, oacc[dt][3] * inv};
-            store4(orow + dt * 16 + 4 * g, v);
-          }
-          if (g == 0) lse[((long)b * H + h) * S + q] = (ms + log2f(l)) * LN2;
-        }
-        continue;
-      }
 #pragma unroll
       for (int kt = 0; kt < NT; ++kt) {
-        f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
+        f32x4_t acc = qk_init<NT, EX>(kt, g, S);
 #pragma unroll
         for (int kk = 0; kk < KK; ++kk) acc = mfma(ld8(Ks + (kt * 16 + l16) * KS + 32 * kk + 8 * g), qf[kk], acc);
         sc[kt] = acc;
       }
-      float m = -INFINITY;
-#pragma unroll
-      for (int kt = 0; kt < NT; ++kt) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int key = kt * 16 + 4 * g + i;
-          const float v = key < S ? sc[kt][i] * sl2 : -INFINITY;
-          sc[kt][i] = v;
-          m = fmaxf(m, v);
-        }
-      }
-      m = fmaxf(m, __shfl_xor(m, 16, WAVE));
-      m = fmaxf(m, __shfl_xor(m, 32, WAVE));
-      float l = 0.f;
-#pragma unroll
-      for (int kt = 0; kt < NT; ++kt) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const float p = __builtin_amdgcn_exp2f(sc[kt][i] - m);
-          sc[kt][i] = p;
-          l += p;
-        }
-      }
-      l += __shfl_xor(l, 16, WAVE);
-      l += __shfl_xor(l, 32, WAVE);
       f32x4_t oacc[DT];
-#pragma unroll
-      for (int dt = 0; dt < DT; ++dt) oacc[dt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int s = 0; s < NT / 2; ++s) {
-        float pf[8] = {sc[2 * s][0], sc[2 * s][1], sc[2 * s][2], sc[2 * s][3],
-                       sc[2 * s + 1][0], sc[2 * s + 1][1], sc[2 * s + 1][2], sc[2 * s + 1][3]};
-        const bf16x8_t pb = pack8(pf);
-#pragma unroll
-        for (int dt = 0; dt < DT; ++dt) {
-          const uint16_t* vr2 = Vt + (32 * s + 4 * g + (l16 >> 2)) * KS + dt * 16 + 4 * (l16 & 3);
-          oacc[dt] = mfma(cat44(tr4(vr2), tr4(vr2 + 16 * KS)), pb, oacc[dt]);
-        }
-      }
+      float ms, l;
+      softmax_pv(sc, sl2,
+                 [&](int s, int dt) {
+                   const uint16_t* vr2 = Vt + (32 * s + 4 * g + (l16 >> 2)) * KS + dt * 16 + 4 * (l16 & 3);
+                   return cat44(tr4(vr2), tr4(vr2 + 16 * KS));
+                 },
+                 oacc, ms, l);
       if (q < S) {
         const float inv = 1.f / l;
         uint16_t* orow = o + ((long)b * S + q) * H * HD + h * HD;
@@ -528,7 +340,7 @@ __global__ __launch_bounds__(256) void attn_fwd_ml_kernel(const uint16_t* __rest
           float v[4] = {oacc[dt][0] * inv, oacc[dt][1] * inv, oacc[dt][2] * inv, oacc[dt][3] * inv};
           store4(orow + dt * 16 + 4 * g, v);
         }
-        if (g == 0) lse[((long)b * H + h) * S + q] = (m + log2f(l)) * LN2;
+        if (g == 0) lse[((long)b * H + h) * S + q] = (ms + log2f(l)) * LN2;
       }
     }
   }
@@ -570,7 +382,7 @@ __global__ __launch_bounds__(256) void attn_bwd2_kernel(const uint16_t* __restri
                                                         const uint16_t* __restrict__ dO,
                                                         const float* __restrict__ lse,
                                                         uint16_t* __restrict__ dqkv, int S, int H, float scale,
-                                                        float* __restrict__ dbp, int B, int ppw, int remap) {
+                                                        float* __restrict__ dbp, int B, int ppw) {
   JM_DGUARD(S >= 1 && S <= SP && blockDim.x == 256 && ppw >= 1);
   constexpr int NW = 4, NTH = 256, QC = 64;
   constexpr int NT = SP / 16, KK = HD / 32, DT = HD / 16;
@@ -588,7 +400,7 @@ __global__ __launch_bounds__(256) void attn_bwd2_kernel(const uint16_t* __restri
 
   // one workgroup walks ``ppw`` batch elements of ONE head (blockIdx = bg * H + h): the QKV bias
   // gradient partials stay in registers across them and are reduced across lanes once
-  const int bid = xcd_bid(remap);
+  const int bid = xcd_bid();
   const int h = bid % H, bg = bid / H;
   const long ts = 3L * H * HD;
   const long os = (long)H * HD;
@@ -877,7 +689,7 @@ __global__ __launch_bounds__(64 * NWV) void attn_bwd3_kernel(const uint16_t* __r
                                                         const uint16_t* __restrict__ dO,
                                                         const float* __restrict__ lse,
                                                         uint16_t* __restrict__ dqkv, int S, int H, float scale,
-                                                        float* __restrict__ dbp, int remap) {
+                                                        float* __restrict__ dbp) {
   JM_DGUARD(S >= 1 && S <= SP && blockDim.x == 64 * NWV);
   constexpr int NW = NWV, NTH = 64 * NWV, QC = 16 * NWV;
   constexpr int QB = QC / 32;   // 32-query blocks per chunk
@@ -894,7 +706,7 @@ __global__ __launch_bounds__(64 * NWV) void attn_bwd3_kernel(const uint16_t* __r
   float* delta_s = lse_s + SP;
   float* bsum = delta_s + SP;
 
-  const int bh = xcd_bid(remap);
+  const int bh = xcd_bid();
   const int b = bh / H, h = bh - (bh / H) * H;
   const long ts = 3L * H * HD;
   const long os = (long)H * HD;
@@ -1160,11 +972,6 @@ __global__ __launch_bounds__(64 * NWV) void attn_bwd3_kernel(const uint16_t* __r
 template <int HD, int SP>
 size_t fwd_smem() { return (size_t)(2 * SP * (HD + 8)) * 2; }
 
-int g_attn_remap = 3;  // runtime switch: bit 0 XCD-aware workgroup -> (b, h) order (xcd_bid), bit 1 forward
-                       // Q prefetch + batched K / V staging; dec fwd 175 -> 163 us, bwd 361 -> 340 us
-                       // (profiles/r2_attn_remap.txt)
-int g_use_tr = 3;  // runtime switch: 3 = batched backward (bwd3) for hd 32, 2 = compact backward (bwd2)
-
 // one (b, h) per workgroup (S > 64; the short encoder sequences take the multi-pair kernel)
 template <int HD, int SP>
 int run_fwd(const uint16_t* qkv, uint16_t* out, float* lse_out, int B, int S, int H, float scale, hipStream_t st) {
@@ -1174,93 +981,74 @@ int run_fwd(const uint16_t* qkv, uint16_t* out, float* lse_out, int B, int S, in
   if (S > SP - 32) {
     static bool attr_ex = false;
     if (sm > 64 * 1024 && !attr_ex) {
-      (void)hipFuncSetAttribute((const void*)attn_fwd_kernel<HD, SP, true, true>,
+      (void)hipFuncSetAttribute((const void*)attn_fwd_kernel<HD, SP, true>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
       attr_ex = true;
     }
-    attn_fwd_kernel<HD, SP, true, true><<<grid, 256, sm, st>>>(qkv, out, lse_out, S, H, scale, g_attn_remap);
+    attn_fwd_kernel<HD, SP, true><<<grid, 256, sm, st>>>(qkv, out, lse_out, S, H, scale);
   } else {
     static bool attr = false;
     if (sm > 64 * 1024 && !attr) {
-      (void)hipFuncSetAttribute((const void*)attn_fwd_kernel<HD, SP, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+      (void)hipFuncSetAttribute((const void*)attn_fwd_kernel<HD, SP>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)sm);
       attr = true;
     }
-    attn_fwd_kernel<HD, SP, true><<<grid, 256, sm, st>>>(qkv, out, lse_out, S, H, scale, g_attn_remap);
+    attn_fwd_kernel<HD, SP><<<grid, 256, sm, st>>>(qkv, out, lse_out, S, H, scale);
   }
   return 0;
 }
 
-// runtime switch: batch elements per bwd2 workgroup (one head each); 0 = auto (bwd_ppw)
-int g_bwd_ppw = 0;
-// runtime switch: the batched backward (bwd3) also for head dim 64 at S > 64 (finetune S = 199);
-// 2: also at S <= 64 (the encoder, A/B)
-int g_bwd3_nw8 = 1;  // runtime switch: hd 64, S > 64 backward on the 8-wave bwd3
-int g_bwd3_hd64 = 1;  // finetune S=199 hd=64 backward 249 -> 177 us (profiles/r2_attn_ft_bwd.txt)
-// the backward that jm_attn_bwd runs is the batched bwd3 kernel (B dbias partial rows) -- the
-// single source of that choice for run_bwd2 and jm_attn_bwd_part_rows
-bool uses_bwd3(int S, int hd) {
-  return g_use_tr == 3 && (hd == 32 || (hd == 64 && (S > 64 ? g_bwd3_hd64 : g_bwd3_hd64 == 2)));
-}
-
+// The backward kernel per shape -- the single source of that choice for run_bwd and
+// jm_attn_bwd_part_rows:
+//  * hd 32 (decoder): the batched bwd3, 4 waves (profiles/r1_attn_bwd3.txt);
+//  * hd 64, S > 64 (finetune S = 199): bwd3 with 8 waves, two per SIMD (the 4-wave form needs
+//    more than 256 VGPRs there): 249 -> 177 us (profiles/r2_attn_ft_bwd.txt);
+//  * hd 64, S <= 64 (the ViT-L encoder): the compact bwd2, BWD2_PPW batch elements per workgroup.
+bool uses_bwd3(int S, int hd) { return hd == 32 || (hd == 64 && S > 64); }
+// ViT-L encoder (S 52): 160 -> 140 us at 8 batch elements per bwd2 workgroup (profiles/r1_attn_bwd_ppw.txt)
+constexpr int BWD2_PPW = 8;
 
 template <int HD, int SP>
-int bwd_ppw() {
-  if (g_bwd_ppw > 0) return g_bwd_ppw;
-  return 8;  // ViT-L encoder (S 52): 160 -> 140 us, finetune (S 199): 273 -> 256 us (profiles/r1_attn_bwd_ppw.txt)
-}
-
-template <int HD, int SP>
-int run_bwd2(const uint16_t* qkv, const uint16_t* o, const uint16_t* dO, const float* lse_in, uint16_t* out,
-             float* dbias_part, int B, int S, int H, float scale, hipStream_t st) {
-  constexpr size_t sm = bwd2_smem<HD, SP>();
-  if (sm > 160 * 1024) return -3;
-  static bool attr_set = false;
-  if (sm > 64 * 1024 && !attr_set) {
-    (void)hipFuncSetAttribute((const void*)attn_bwd2_kernel<HD, SP>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)sm);
-    attr_set = true;
-  }
-  if constexpr (HD == 32 || HD == 64) {
-    if (!uses_bwd3(S, HD)) goto bwd2;
-    static bool attr3 = false;
-    if (sm > 64 * 1024 && !attr3) {
-      (void)hipFuncSetAttribute((const void*)attn_bwd3_kernel<HD, SP>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)sm);
-      attr3 = true;
+int run_bwd(const uint16_t* qkv, const uint16_t* o, const uint16_t* dO, const float* lse_in, uint16_t* out,
+            float* dbias_part, int B, int S, int H, float scale, hipStream_t st) {
+  if constexpr (HD == 64 && SP > 64) {
+    constexpr size_t sm8 = bwd2_smem<HD, SP, 128>();
+    static_assert(sm8 <= 160 * 1024, "8-wave backward LDS");
+    static bool attr8 = false;
+    if (!attr8) {
+      (void)hipFuncSetAttribute((const void*)attn_bwd3_kernel<HD, SP, 8>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)sm8);
+      attr8 = true;
     }
-    if constexpr (HD == 64 && SP > 64) {
-      if (g_bwd3_nw8) {  // 8 waves: 2 / SIMD instead of 1 (the 4-wave form needs > 256 VGPRs here)
-        constexpr size_t sm8 = bwd2_smem<HD, SP, 128>();
-        static_assert(sm8 <= 160 * 1024, "8-wave backward LDS");
-        static bool attr8 = false;
-        if (!attr8) {
-          (void)hipFuncSetAttribute((const void*)attn_bwd3_kernel<HD, SP, 8>,
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm8);
-          attr8 = true;
-        }
-        attn_bwd3_kernel<HD, SP, 8><<<dim3(B * H), 512, sm8, st>>>(qkv, o, dO, lse_in, out, S, H, scale,
-                                                                   dbias_part, g_attn_remap);
-        return 0;
+    attn_bwd3_kernel<HD, SP, 8><<<dim3(B * H), 512, sm8, st>>>(qkv, o, dO, lse_in, out, S, H, scale, dbias_part);
+  } else {
+    constexpr size_t sm = bwd2_smem<HD, SP>();
+    static_assert(sm <= 160 * 1024, "backward LDS");
+    static bool attr = false;
+    if constexpr (HD == 32) {
+      if (sm > 64 * 1024 && !attr) {
+        (void)hipFuncSetAttribute((const void*)attn_bwd3_kernel<HD, SP>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)sm);
+        attr = true;
       }
+      attn_bwd3_kernel<HD, SP><<<dim3(B * H), 256, sm, st>>>(qkv, o, dO, lse_in, out, S, H, scale, dbias_part);
+    } else {
+      if (sm > 64 * 1024 && !attr) {
+        (void)hipFuncSetAttribute((const void*)attn_bwd2_kernel<HD, SP>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)sm);
+        attr = true;
+      }
+      attn_bwd2_kernel<HD, SP><<<dim3(((B + BWD2_PPW - 1) / BWD2_PPW) * H), 256, sm, st>>>(
+          qkv, o, dO, lse_in, out, S, H, scale, dbias_part, B, BWD2_PPW);
     }
-    attn_bwd3_kernel<HD, SP><<<dim3(B * H), 256, sm, st>>>(qkv, o, dO, lse_in, out, S, H, scale, dbias_part,
-                                                           g_attn_remap);
-    return 0;
-  }
-bwd2:
-  {
-    const int ppw = bwd_ppw<HD, SP>();
-    attn_bwd2_kernel<HD, SP><<<dim3(((B + ppw - 1) / ppw) * H), 256, sm, st>>>(qkv, o, dO, lse_in, out, S, H, scale,
-                                                                              dbias_part, B, ppw, g_attn_remap);
   }
   return 0;
 }
 
-// runtime switch: (b, h) pairs per forward workgroup; 1 = one-pair kernel, 0 = auto: 4 for the
-// short encoder sequences (SP <= 64: 43 -> 39 us), 1 for the decoder, where the extra prefetch
-// registers cost an occupancy step (199 -> 215 us; profiles/r1_attn_fwd_ml.txt)
-int g_fwd_hpw = 0;
+// forward: the multi-pair kernel (4 (b, h) per workgroup) for the short encoder sequences
+// (SP <= 64: 43 -> 39 us), the one-pair kernel for the decoder, where the extra prefetch registers
+// cost an occupancy step (199 -> 215 us; profiles/r1_attn_fwd_ml.txt)
+constexpr int FWD_ML_PAIRS = 4;
 
 template <int HD, int SP>
 int run_fwd_ml(const uint16_t* qkv, uint16_t* out, float* lse_out, int B, int S, int H, float scale, hipStream_t st) {
@@ -1273,21 +1061,19 @@ int run_fwd_ml(const uint16_t* qkv, uint16_t* out, float* lse_out, int B, int S,
     attr_set[ex] = true;
   }
   const int BH = B * H;
-  const int hpw = g_fwd_hpw > 0 ? g_fwd_hpw : 4;
-  const int grid = (BH + hpw - 1) / hpw;
+  const int grid = (BH + FWD_ML_PAIRS - 1) / FWD_ML_PAIRS;
   if (ex)
-    attn_fwd_ml_kernel<HD, SP, true><<<grid, 256, sm, st>>>(qkv, out, lse_out, S, H, BH, hpw, scale, g_attn_remap);
+    attn_fwd_ml_kernel<HD, SP, true><<<grid, 256, sm, st>>>(qkv, out, lse_out, S, H, BH, FWD_ML_PAIRS, scale);
   else
-    attn_fwd_ml_kernel<HD, SP><<<grid, 256, sm, st>>>(qkv, out, lse_out, S, H, BH, hpw, scale, g_attn_remap);
+    attn_fwd_ml_kernel<HD, SP><<<grid, 256, sm, st>>>(qkv, out, lse_out, S, H, BH, FWD_ML_PAIRS, scale);
   return 0;
 }
 
 template <int HD, int SP>
 int run(bool fwd, const uint16_t* qkv, const uint16_t* o, const uint16_t* dO, const float* lse_in, uint16_t* out,
         float* lse_out, int B, int S, int H, float scale, hipStream_t st) {
-  if (fwd && (g_fwd_hpw > 1 || (g_fwd_hpw == 0 && SP <= 64)))
-    return run_fwd_ml<HD, SP>(qkv, out, lse_out, B, S, H, scale, st);
-  if (!fwd) return run_bwd2<HD, SP>(qkv, o, dO, lse_in, out, lse_out, B, S, H, scale, st);
+  if (!fwd) return run_bwd<HD, SP>(qkv, o, dO, lse_in, out, lse_out, B, S, H, scale, st);
+  if constexpr (SP <= 64) return run_fwd_ml<HD, SP>(qkv, out, lse_out, B, S, H, scale, st);
   return run_fwd<HD, SP>(qkv, out, lse_out, B, S, H, scale, st);
 }
 
@@ -1663,30 +1449,16 @@ int run_long_bwd(const uint16_t* qkv, const uint16_t* o, const uint16_t* dO, con
 
 }  // namespace
 
-// longest sequence on the whole-sequence-in-LDS kernels (runtime switch; the tile-streamed
-// kernels take longer ones)
-int g_attn_max_seq = 224;
-int jm_attn_max_seq() { return g_attn_max_seq; }
-void jm_attn_set_max_seq(int v) { g_attn_max_seq = v < 32 ? 32 : (v > 224 ? 224 : v); }
-void jm_attn_set_tr(int v) { g_use_tr = v >= 3 ? 3 : 2; }
-void jm_attn_set_remap(int v) { g_attn_remap = v; }
-void jm_attn_set_fwd_hpw(int v) { g_fwd_hpw = v < 0 ? 0 : v; }
-void jm_attn_set_bwd_ppw(int v) { g_bwd_ppw = v < 0 ? 0 : v; }
-void jm_attn_set_bwd3_hd64(int v) { g_bwd3_hd64 = v; }
-void jm_attn_set_bwd3_nw8(int v) { g_bwd3_nw8 = v; }
+// longest sequence on the whole-sequence-in-LDS kernels (every flagship shape); the
+// tile-streamed kernels take longer ones
+constexpr int ATTN_MAX_SEQ = 224;
+int jm_attn_max_seq() { return ATTN_MAX_SEQ; }
 
-// rows of the dbias_part workspace that jm_attn_bwd writes: the bwd2 kernel folds ``ppw`` batch
-// elements into one row, every other backward writes one row per batch element.  Must mirror the
-// kernel choice of run_bwd2 exactly (bwd3 writes B rows).
+// rows of the dbias_part workspace that jm_attn_bwd writes: the bwd2 kernel folds BWD2_PPW batch
+// elements into one row, every other backward writes one row per batch element.
 int jm_attn_bwd_part_rows(int B, int S, int hd) {
-  const bool bwd2 = g_use_tr >= 2 && !uses_bwd3(S, hd);
-  if (!bwd2 || S > 224 || (hd != 32 && hd != 64)) return B;
-  int ppw;
-  if (hd == 64)
-    ppw = S <= 32 ? bwd_ppw<64, 32>() : S <= 64 ? bwd_ppw<64, 64>() : S <= 128 ? bwd_ppw<64, 128>() : bwd_ppw<64, 224>();
-  else
-    ppw = S <= 32 ? bwd_ppw<32, 32>() : S <= 64 ? bwd_ppw<32, 64>() : S <= 128 ? bwd_ppw<32, 128>() : bwd_ppw<32, 224>();
-  return (B + ppw - 1) / ppw;
+  if (uses_bwd3(S, hd) || S > ATTN_MAX_SEQ || hd != 64) return B;
+  return (B + BWD2_PPW - 1) / BWD2_PPW;
 }
 
 int jm_attn_fwd(const uint16_t* qkv, uint16_t* o, float* lse, int B, int S, int H, int hd, hipStream_t st) {

@@ -16,7 +16,6 @@ int jm_layernorm_bwd(const void* dy, int dy_bf16, const float* x, long sB, long 
                      const float* dres, long rB, long rT, float* dgamma, float* dbeta, int accum_params, float* ws,
                      const JmLnRes* res, hipStream_t st);
 int jm_layernorm_bwd_blocks(int rows, int D);
-void jm_ln_set_bwd_blocks(int v);
 // debug build (-DJM_DEBUG): first failing soft-check line per kernel translation unit (0 = none;
 // reading clears it); always 0 in the release build
 int jm_debug_line_attention();
@@ -53,18 +52,10 @@ int jm_attn_fwd(const uint16_t* qkv, uint16_t* o, float* lse, int B, int S, int 
 int jm_attn_bwd(const uint16_t* qkv, const uint16_t* o, const uint16_t* dO, const float* lse, uint16_t* dqkv, int B,
                 int S, int H, int hd, float* dbias_part, hipStream_t st);
 int jm_attn_max_seq();
-void jm_attn_set_max_seq(int v);
-void jm_attn_set_tr(int v);
-void jm_attn_set_remap(int v);
-void jm_attn_set_fwd_hpw(int v);
-void jm_attn_set_bwd_ppw(int v);
-void jm_attn_set_bwd3_hd64(int v);
-void jm_attn_set_bwd3_nw8(int v);
 int jm_attn_bwd_part_rows(int B, int S, int hd);
 int jm_attn_bwd_long(const uint16_t* qkv, const uint16_t* o, const uint16_t* dO, const float* lse, uint16_t* dqkv,
                      float* delta, int B, int S, int H, int hd, hipStream_t st);
 void jm_opt_sumsq(const float* x, const int* chunks, int nchunks, float* out, hipStream_t st);
-void jm_opt_set_adamw_vec(int v);
 void jm_zero_f32(float* p, long n, hipStream_t st);
 void jm_opt_adamw(float* p, const float* g, float* mu, float* nu, uint16_t* shadow, const int* chunks, int nchunks,
                   const float* meta, const float* hyper, const float* gnorm_sq, hipStream_t st);
@@ -82,14 +73,10 @@ int jm_splitk_reduce_f32(const float* part, int S, int M, int N, const float* bi
                          float* out, hipStream_t st);
 int jm_gemm_nt(const uint16_t* A, long lda, const uint16_t* B, long ldb, int M, int N, int K, int epi,
                const GemmEpi& ep, hipStream_t st);
-void jm_gemm_set_variant(int wn, int group);
-void jm_gemm_set_tail(int on);
-void jm_gemm_set_narrow(int max_m);
 int jm_gemm_nt_tiles(int M, int N, int K, int epi, long lda);
 int jm_gemm_nt_colpart_rows(int M, int N, int K, int epi, long lda);
 int jm_gemm_nt_tail_plan(int M, int N, int K, int epi, long lda, int* tail_r, long* ws_floats);
-void jm_gemm_set_rows(int rows);
-void jm_gemm_set_narrow_splitk(int on);
+void jm_gemm_test_force(int path, int rows);
 int jm_gemm_tn_plan(int M, int N, int K, int* S_out);
 int jm_gemm_tn_group_plan(const TnGroup& grp, int M, int* S_out);
 int jm_gemm_tn_group(TnGroup grp, int M, int sps, int S, hipStream_t st, int store);
@@ -1101,7 +1088,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("attn_bwd", &attn_bwd, py::arg("dO"), py::arg("qkv"), py::arg("o"), py::arg("lse"), py::arg("heads"),
         py::arg("dbias") = py::none());
   m.def("attn_max_seq", &jm_attn_max_seq);
-  m.def("attn_set_max_seq", &jm_attn_set_max_seq);
   m.def("gemm_tn_wgrad", &gemm_tn_wgrad, py::arg("dy"), py::arg("x"), py::arg("g"), py::arg("store") = false);
   m.def("gemm_tn_wgrad_seg", &gemm_tn_wgrad_seg, py::arg("dys"), py::arg("xs"), py::arg("g"), py::arg("store") = false);
   m.def("zero_ranges", &zero_ranges, "zero float ranges of a flat buffer (one launch)");
@@ -1109,17 +1095,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("stores") = std::vector<bool>{}, "grouped segmented weight gradients (<= 2 problems)");
   m.def("gemm_tn_wgrad_group", &gemm_tn_wgrad_group, py::arg("dys"), py::arg("xs"), py::arg("gs"),
         py::arg("stores") = std::vector<bool>{}, "grouped weight gradients over one M (<= 4 problems)");
-  m.def("gemm_set_variant", &jm_gemm_set_variant, py::arg("nt64"), py::arg("group") = 8,
-        "nt64 = 1: every NT launch on the 64-deep main loop (tests); group: row tiles per column sweep");
-  m.def("gemm_set_tail", &jm_gemm_set_tail);
-  m.def("gemm_set_narrow", &jm_gemm_set_narrow, "M below which NT GEMMs take the 128 x 192 narrow tiles (0 = never)");
+  m.def("gemm_test_force", &jm_gemm_test_force, py::arg("path"), py::arg("rows") = 0,
+        "numerics tests only: NT GEMM kernel path 0 = by shape, 1 = 64-deep main loop everywhere, "
+        "2 = 4-phase kernels at every M without tail split (rows = forced tile height)");
   m.def("gemm_nt_tiles", &jm_gemm_nt_tiles, py::arg("M"), py::arg("N"), py::arg("K") = 1024, py::arg("epi") = 0,
         py::arg("lda") = 0, "output tiles (workgroups before split-K) of an NT launch");
-  m.def("gemm_set_narrow_splitk", &jm_gemm_set_narrow_splitk, "split-K from M = 256 on the narrow tiles (A/B)");
-  m.def("gemm_set_rows", &jm_gemm_set_rows,
-        "4-phase tile height: 0 = automatic (wave fill), 256 / 224 / 192 = forced (A/B, tests)");
   m.def("transpose_bf16_batch", &transpose_bf16_batch);
-  m.def("ln_set_bwd_blocks", &jm_ln_set_bwd_blocks);
   m.def("gemm_nt_splitk", &gemm_nt_splitk, py::arg("A"), py::arg("B"), py::arg("bias") = py::none(),
         py::arg("splits") = 8, py::arg("add") = py::none());
   m.def("gemm_nt_dgelu", &gemm_nt_dgelu, py::arg("A"), py::arg("B"), py::arg("pre"), py::arg("dbias") = py::none(),
@@ -1127,15 +1108,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_nt_f32", &gemm_nt_f32, py::arg("A"), py::arg("B"));
   m.def("gemm_nt", &gemm_nt, py::arg("A"), py::arg("B"), py::arg("bias") = py::none(), py::arg("gelu") = false,
         py::arg("gelu_only") = false, py::arg("gelu_deriv") = false);
-  m.def("attn_set_tr", &jm_attn_set_tr);
-  m.def("attn_set_remap", &jm_attn_set_remap, "attention grid: bit 0 XCD-aware (b, h) order, bit 1 forward Q prefetch");
-  m.def("attn_set_fwd_hpw", &jm_attn_set_fwd_hpw);
-  m.def("attn_set_bwd_ppw", &jm_attn_set_bwd_ppw);
-  m.def("attn_set_bwd3_hd64", &jm_attn_set_bwd3_hd64);
-  m.def("attn_set_bwd3_nw8", &jm_attn_set_bwd3_nw8);
   m.def("opt_sumsq", &opt_sumsq);
   m.def("opt_adamw", &opt_adamw);
-  m.def("opt_set_adamw_vec", &jm_opt_set_adamw_vec);
   m.def("opt_lamb_phase1", &opt_lamb_phase1);
   m.def("opt_lars_norms", &opt_lars_norms);
   m.def("opt_apply_trust", &opt_apply_trust);

@@ -1058,8 +1058,11 @@ __global__ __launch_bounds__(256) void tail_finish_kernel(GemmEpi ep, int M, int
 }
 
 
-int g_gemm_group = 8;  // row tiles per column sweep (profiles/r2_gemm_group.txt: 8 best)
-int g_gemm_nt64 = 0;   // test switch: every launch on the nt64 main loop (it otherwise runs K % 128 == 64)
+constexpr int GEMM_GROUP = 8;  // row tiles per column sweep (profiles/r2_gemm_group.txt: 8 best)
+// Kernel-path override for the numerics tests only (jm_gemm_test_force); production launches
+// choose by shape.  1: every launch on the 64-deep main loop (it otherwise runs at K % 128 == 64);
+// 2: the 4-phase kernels at every M, no tail split, g_test_rows = forced tile height (0 = tile_rows).
+int g_test_path = 0, g_test_rows = 0;
 int g_num_cus = 0;
 
 int num_cus() {
@@ -1082,7 +1085,7 @@ void launch_nt64(const uint16_t* A, long lda, const uint16_t* B, long ldb, int M
                               (int)GEMM_SMEM);
     attr = true;
   }
-  gemm_nt64_kernel<EPI, NTS><<<nwg, 512, GEMM_SMEM, st>>>(A, lda, B, ldb, M, N, K, ep, g_gemm_group);
+  gemm_nt64_kernel<EPI, NTS><<<nwg, 512, GEMM_SMEM, st>>>(A, lda, B, ldb, M, N, K, ep, GEMM_GROUP);
 }
 
 template <int EPI, int MTL>
@@ -1094,7 +1097,7 @@ void launch_p4(const uint16_t* A, long lda, const uint16_t* B, long ldb, int M, 
                               (int)GEMM_SMEM);
     attr = true;
   }
-  gemm_p4_kernel<EPI, MTL><<<nwg, 512, GEMM_SMEM, st>>>(A, lda, B, ldb, M, N, K, ep, g_gemm_group);
+  gemm_p4_kernel<EPI, MTL><<<nwg, 512, GEMM_SMEM, st>>>(A, lda, B, ldb, M, N, K, ep, GEMM_GROUP);
 }
 
 template <int EPI>
@@ -1108,29 +1111,21 @@ void launch_narrow(const uint16_t* A, long lda, const uint16_t* B, long ldb, int
     attr = true;
   }
   const int nwg = ((M + NBM - 1) / NBM) * ((N + NBN - 1) / NBN) * (EPI == EPI_PARTIAL ? ep.splits : 1);
-  gemm_narrow_kernel<EPI><<<nwg, 512, sm, st>>>(A, lda, B, ldb, M, N, K, ep, g_gemm_group);
+  gemm_narrow_kernel<EPI><<<nwg, 512, sm, st>>>(A, lda, B, ldb, M, N, K, ep, GEMM_GROUP);
 }
 
-int g_narrow_max_m = 4096;  // M below this: 128 x 192 tiles (A/B switch: 0 = never)
+constexpr int NARROW_MAX_M = 4096;  // M below this: 128 x 192 tiles
 
-bool narrow(int M, int N) { return M < g_narrow_max_m && N % 8 == 0; }
+bool narrow(int M, int N) { return g_test_path == 0 && M < NARROW_MAX_M && N % 8 == 0; }
 
-// split-K (EPI_PARTIAL, splits > 1) from M = 256 on the narrow tiles too: the jumbo MLP's K = 12288
-// GEMMs take 4 splits of 128 x 192 tiles instead of 10 of 256 x 256 -- the GEMM alone is ~4 us
-// slower (r3e_summary_vitl_b512_fused_reductions.txt) but the fp32 partials shrink 2.5x
-// (profiles/r3_narrow_splitk.txt: ViT-L step -0.41 ms in-process).  0 = the 256 x 256 kernels.
-int g_narrow_splitk = 1;
-
-bool narrow_launch(int M, int N, int epi, int splits) {
-  if (!narrow(M, N)) return false;
-  return g_narrow_splitk || !(epi == EPI_PARTIAL && splits > 1 && M >= 256);
-}
+// split-K (EPI_PARTIAL, splits > 1) takes the narrow tiles too: the jumbo MLP's K = 12288 GEMMs
+// run 4 splits of 128 x 192 tiles instead of 10 of 256 x 256 -- the GEMM alone is ~4 us slower
+// (r3e_summary_vitl_b512_fused_reductions.txt) but the fp32 partials shrink 2.5x
+// (profiles/r3_narrow_splitk.txt: ViT-L step -0.41 ms in-process).
 
 bool p4_ok(int K, int epi, int splits) {
-  return !g_gemm_nt64 && K % 128 == 0 && (epi != EPI_PARTIAL || K / 128 >= splits);
+  return g_test_path != 1 && K % 128 == 0 && (epi != EPI_PARTIAL || K / 128 >= splits);
 }
-
-int g_gemm_rows = 0;  // 0: tile_rows decides; 256 / 224 / 192 force the 4-phase tile height (A/B, tests)
 
 // Relative cost per tile row of the short-row 4-phase tiles vs 256 rows (the same B panel feeds
 // fewer MFMAs; measured per full wave, profiles/r3_gemm_tile_rows.txt)
@@ -1147,7 +1142,7 @@ int tail_plan_256(int M, int N, int K, int epi, int* tail_r);
 int tile_rows(int M, int N, int K, int epi, long lda) {
   if (narrow(M, N) || !p4_ok(K, epi, 1) || epi == EPI_PARTIAL || epi == EPI_TAIL) return BM;
   if ((long)M * lda * 2 >= (1L << 31) - (1L << 20)) return BM;
-  if (g_gemm_rows) return g_gemm_rows;
+  if (g_test_rows) return g_test_rows;
   const int ncu = num_cus(), nN = (N + BN - 1) / BN;
   int r = 0;
   const int t256 = ((M + BM - 1) / BM) * nN;
@@ -1167,7 +1162,7 @@ template <int EPI>
 void launch_epi(const uint16_t* A, long lda, const uint16_t* B, long ldb, int M, int N, int K, const GemmEpi& ep,
                 int nwg, hipStream_t st) {
   if constexpr (EPI != EPI_TAIL) {
-    if (narrow_launch(M, N, EPI, ep.splits) && ep.t_count == 0) return launch_narrow<EPI>(A, lda, B, ldb, M, N, K, ep, st);
+    if (narrow(M, N) && ep.t_count == 0) return launch_narrow<EPI>(A, lda, B, ldb, M, N, K, ep, st);
   }
   if (p4_ok(K, EPI, ep.splits)) {
     const int tr = ep.t_count > 0 ? BM : tile_rows(M, N, K, EPI, lda);
@@ -1181,8 +1176,6 @@ void launch_epi(const uint16_t* A, long lda, const uint16_t* B, long ldb, int M,
   return launch_nt64<EPI, true>(A, lda, B, ldb, M, N, K, ep, nwg, st);
 }
 
-int g_gemm_tail = 1;  // tail split of the last partial wave (K >= 1024): ViT-B FF2 fwd 127 -> 109 us (profiles/r2_gemm_tail_p4.txt)
-
 template <int EPI>
 void launch_tail(const uint16_t* A, long lda, const uint16_t* B, long ldb, int M, int N, int K, const GemmEpi& ep,
                  int tiles, hipStream_t st) {
@@ -1194,24 +1187,17 @@ void launch_tail(const uint16_t* A, long lda, const uint16_t* B, long ldb, int M
   GemmEpi et = ep;
   et.t_begin = tiles - r;
   launch_nt64<EPI_TAIL, false>(A, lda, B, ldb, M, N, K, et, r * ep.tail_S, st);
-  tail_finish_kernel<EPI><<<r * 8, 256, 0, st>>>(et, M, N, g_gemm_group);
+  tail_finish_kernel<EPI><<<r * 8, 256, 0, st>>>(et, M, N, GEMM_GROUP);
 }
 
 }  // namespace
 
-// nt64 = 1 forces the 64-deep main loop (tests); group = row tiles per column sweep
-void jm_gemm_set_variant(int nt64, int group) {
-  g_gemm_nt64 = nt64;
-  g_gemm_group = group;
+// numerics tests: path 0 = by shape, 1 = 64-deep main loop everywhere, 2 = 4-phase kernels at
+// every M without tail split (rows 256 / 224 / 192 forced, 0 = tile_rows)
+void jm_gemm_test_force(int path, int rows) {
+  g_test_path = (path == 1 || path == 2) ? path : 0;
+  g_test_rows = (g_test_path == 2 && (rows == 224 || rows == 192 || rows == 256)) ? rows : 0;
 }
-
-void jm_gemm_set_tail(int on) { g_gemm_tail = on; }
-
-void jm_gemm_set_narrow(int max_m) { g_narrow_max_m = max_m; }
-
-void jm_gemm_set_narrow_splitk(int on) { g_narrow_splitk = on; }
-
-void jm_gemm_set_rows(int rows) { g_gemm_rows = (rows == 224 || rows == 192 || rows == 256) ? rows : 0; }
 
 // output tiles of an NT launch (the narrow kernel's 128 x 192 or the 4-phase 256 / 224 / 192 x 256)
 int jm_gemm_nt_tiles(int M, int N, int K, int epi, long lda) {
@@ -1231,10 +1217,11 @@ int jm_gemm_nt_colpart_rows(int M, int N, int K, int epi, long lda) {
 // part of the chip; when it is at most a quarter wave, those tiles run split-K S ways (compact fp32
 // partials, *ws_floats) and a finish kernel applies the epilogue.  Returns S (0 = no tail split);
 // *tail_r = number of tail tiles.
+// ViT-B FF2 fwd 127 -> 109 us (profiles/r2_gemm_tail_p4.txt).
 namespace {
 int tail_plan_256(int M, int N, int K, int epi, int* tail_r) {
   *tail_r = 0;
-  if (!g_gemm_tail) return 0;
+  if (g_test_path != 0) return 0;
   if (!(epi == EPI_STORE || epi == EPI_GELU || epi == EPI_DGELU || epi == EPI_GELU_ONLY) || N % 8 || K % 128) return 0;
   if (narrow(M, N)) return 0;
   const int ncu = num_cus();

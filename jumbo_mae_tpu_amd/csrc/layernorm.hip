@@ -624,9 +624,9 @@ int jm_residual_ln_fwd(const float* x, long sB, long sT, const uint16_t* y, cons
   return 0;
 }
 
-// runtime switch: most row-loop blocks of the (non-wide) LN backward
-int g_ln_bwd_blocks = 512;  // = 2 resident blocks per CU (2 waves / SIMD): one round, half the partials of 1024 (-0.3 ms/step, profiles/r2_ln_bwd_blocks.txt)
-void jm_ln_set_bwd_blocks(int v) { g_ln_bwd_blocks = v < 64 ? 64 : v; }
+// most row-loop blocks of the (non-wide) LN backward: 512 = 2 resident blocks per CU (2 waves /
+// SIMD): one round, half the partials of 1024 (-0.3 ms/step, profiles/r2_ln_bwd_blocks.txt)
+constexpr int LN_BWD_BLOCKS = 512;
 
 int jm_layernorm_bwd_blocks(int rows, int D) {
   // wide rows: one workgroup per row (at most 1024 workgroups, grid-stride beyond)
@@ -634,7 +634,7 @@ int jm_layernorm_bwd_blocks(int rows, int D) {
   // grid-stride over rows, 4 waves per block; each block writes one [NP*D] partial (no atomics in
   // the hot kernel)
   int nb = (rows + 3) / 4;
-  return nb > g_ln_bwd_blocks ? g_ln_bwd_blocks : nb;
+  return nb > LN_BWD_BLOCKS ? LN_BWD_BLOCKS : nb;
 }
 
 int jm_layernorm_bwd(const void* dy, int dy_bf16, const float* x, long sB, long sT, int B, int T, int D,

@@ -53,7 +53,7 @@ __global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ p, const
                                                     float* __restrict__ mu, float* __restrict__ nu,
                                                     uint16_t* __restrict__ shadow, const Chunk* __restrict__ chunks,
                                                     const float* __restrict__ meta, const float* __restrict__ hyper,
-                                                    const float* __restrict__ gnorm_sq, int vec) {
+                                                    const float* __restrict__ gnorm_sq) {
   const Chunk c = chunks[blockIdx.x];
   const float* m = meta + 4 * c.seg;
   if (m[3] == 0.f) return;
@@ -73,7 +73,7 @@ __global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ p, const
   // 16 B per lane (chunk starts are multiples of 64 elements).  Same step time as the r1
   // 4-B-per-lane loop in a same-process A/B (profiles/r2_adamw_vector.txt: the pass is HBM-bound
   // either way; its 2.1-2.4 ms spread is box to box)
-  const int n4 = vec ? c.len >> 2 : 0;  // vec = 0: the r1 4-B-per-lane loop (A/B)
+  const int n4 = c.len >> 2;
   for (int i = threadIdx.x; i < n4; i += 256) {
     const long k = (long)c.start + 4L * i;
     float gv[4], mm[4], vv[4], pv[4], np[4];
@@ -210,19 +210,14 @@ __global__ __launch_bounds__(256) void sgd_kernel(float* __restrict__ p, const f
 
 }  // namespace
 
-int g_adamw_vec = 1;  // A/B switch: 16-B-per-lane AdamW loop (1) vs the r1 scalar loop (0)
-
 void jm_opt_sumsq(const float* x, const int* chunks, int nchunks, float* out, hipStream_t st) {
   sumsq_kernel<<<nchunks, 256, 0, st>>>(x, (const Chunk*)chunks, out);
 }
 
 void jm_opt_adamw(float* p, const float* g, float* mu, float* nu, uint16_t* shadow, const int* chunks, int nchunks,
                   const float* meta, const float* hyper, const float* gnorm_sq, hipStream_t st) {
-  adamw_kernel<<<nchunks, 256, 0, st>>>(p, g, mu, nu, shadow, (const Chunk*)chunks, meta, hyper, gnorm_sq,
-                                        g_adamw_vec);
+  adamw_kernel<<<nchunks, 256, 0, st>>>(p, g, mu, nu, shadow, (const Chunk*)chunks, meta, hyper, gnorm_sq);
 }
-
-void jm_opt_set_adamw_vec(int v) { g_adamw_vec = v; }
 
 void jm_opt_lamb_phase1(const float* p, const float* g, float* mu, float* nu, float* u, const int* chunks,
                         int nchunks, const float* meta, const float* hyper, const float* gnorm_sq, float* norms,

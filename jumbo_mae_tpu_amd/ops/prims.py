@@ -157,8 +157,7 @@ _GEMM_MODE = "auto"  # auto | blas | ours (forward / dgrad routing)
 _DGRAD_OURS = True  # data-gradient GEMMs on the MFMA kernel
 
 
-NARROW_MAX_M = 4096  # csrc/gemm.hip g_narrow_max_m: below it the NT GEMMs take 128 x 192 tiles
-NARROW_SPLITK = True  # split-K from M = 256 on the narrow tiles too (csrc/gemm.hip g_narrow_splitk)
+NARROW_MAX_M = 4096  # csrc/gemm.hip NARROW_MAX_M: below it the NT GEMMs (split-K too) take 128 x 192 tiles
 _NARROW_FUSED_MIN_TILES = 160  # a fused GELU epilogue needs the tiles alone to fill most CUs
 
 
@@ -193,12 +192,7 @@ def splitk_plan(M: int, N: int, K: int) -> int:
         return 0
     if nt_tiles(M, N) >= _NARROW_FUSED_MIN_TILES:
         return 0
-    if M >= 256 and not NARROW_SPLITK:  # split launches keep the 256 x 256 tiles (jm_gemm narrow_launch)
-        if K % 128:
-            return 0
-        s = min(256 // (-(-M // 256) * -(-N // 256)), K // 512, 32)
-    else:
-        s = min(256 // nt_tiles(M, N), K // 512, 16)
+    s = min(256 // nt_tiles(M, N), K // 512, 16)
     return s if s >= 2 else 0
 
 

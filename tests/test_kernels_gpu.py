@@ -18,12 +18,7 @@ def ext():
 def _reset_gemm_variant(request):
     yield
     if "ext" in request.fixturenames:
-        request.getfixturevalue("ext").gemm_set_variant(0, 8)
-        request.getfixturevalue("ext").attn_set_bwd_ppw(0)
-        request.getfixturevalue("ext").attn_set_bwd3_nw8(1)
-        request.getfixturevalue("ext").gemm_set_tail(1)
-        request.getfixturevalue("ext").gemm_set_narrow(4096)
-        request.getfixturevalue("ext").gemm_set_rows(0)
+        request.getfixturevalue("ext").gemm_test_force(0)
 
 
 def rel(a, b):
@@ -116,15 +111,13 @@ def _attn_ref(qkv, H):
     return o, lse
 
 
-@pytest.mark.parametrize("tr,hpw,ppw", [(3, 0, 0), (3, 1, 0), (2, 1, 0), (3, 3, 0), (3, 4, 0),
-                                        (3, 0, 1), (3, 0, 2), (2, 0, 3), (3, 0, 8), (3, 0, -1)])
-@pytest.mark.parametrize("B,S,H,hd", [(3, 52, 16, 64), (2, 199, 16, 32), (2, 17, 4, 32), (2, 100, 3, 64),
-                                      (2, 199, 4, 64)])
-def test_attention(ext, B, S, H, hd, tr, hpw, ppw):
-    ext.attn_set_tr(tr)
-    ext.attn_set_fwd_hpw(hpw)
-    ext.attn_set_bwd_ppw(max(ppw, 0))
-    ext.attn_set_bwd3_nw8(0 if ppw < 0 else 1)  # ppw -1: the 4-wave batched backward at hd 64
+# every kernel the shape dispatch reaches: forward multi-pair (S <= 64) / one-pair, padded and
+# exactly-filled key tiles; backward bwd3 4-wave (hd 32), bwd3 8-wave (hd 64, S > 64) and bwd2
+# with partial and full 8-element batch groups (hd 64, S <= 64)
+@pytest.mark.parametrize("B,S,H,hd", [(3, 52, 16, 64), (9, 52, 4, 64), (16, 64, 2, 64), (2, 199, 16, 32),
+                                      (2, 17, 4, 32), (5, 64, 3, 32), (2, 100, 3, 64), (2, 199, 4, 64),
+                                      (3, 224, 2, 64), (2, 128, 2, 32), (1, 33, 5, 64)])
+def test_attention(ext, B, S, H, hd):
     torch.manual_seed(0)
     D = H * hd
     qkv = (torch.randn(B, S, 3 * D, device="cuda") * 1.5).bfloat16()
@@ -146,9 +139,6 @@ def test_attention(ext, B, S, H, hd, tr, hpw, ppw):
     d = dqkv.view(B, S, 3, D)
     for i in range(3):
         assert rel(d[:, :, i], g[:, :, i]) < 2e-2, i
-    ext.attn_set_tr(3)
-    ext.attn_set_fwd_hpw(0)
-    ext.attn_set_bwd_ppw(0)
 
 
 @pytest.mark.parametrize("S,n", [(4, 4096), (512, 3072), (37, 1024)])
@@ -199,15 +189,15 @@ def test_optimizer_hip_matches_torch(kind, clip):
     assert rel(res[0], res[1]) < 1e-5
 
 
-@pytest.mark.parametrize("nt64,narrow", [(0, 4096), (1, 0), (0, 0)])
+@pytest.mark.parametrize("path", [0, 1, 2])
 @pytest.mark.parametrize("M,N,K,gelu", [(512, 256, 64, False), (300, 196, 128, True), (1000, 1536, 512, False),
                                         (257, 260, 192, True), (16100, 2048, 128, True), (40000, 520, 64, False)])
-def test_gemm_nt(ext, M, N, K, gelu, nt64, narrow):
-    """Hand-written MFMA GEMMs (csrc/gemm.hip) vs an fp32 reference, ragged M / N included: the
-    128 x 192 narrow kernel below M = 4096 (narrow = 4096), the 256 x 256 kernels otherwise (narrow
-    = 0: every M); nt64 = 1 forces the 64-deep main loop (it otherwise runs only at K % 128 == 64)."""
-    ext.gemm_set_variant(nt64)
-    ext.gemm_set_narrow(narrow)
+def test_gemm_nt(ext, M, N, K, gelu, path):
+    """Hand-written MFMA GEMMs (csrc/gemm.hip) vs an fp32 reference, ragged M / N included: by shape
+    (path 0: the 128 x 192 narrow kernel below M = 4096, the 256 x 256 kernels otherwise), the
+    64-deep main loop everywhere (path 1; by shape it runs only at K % 128 == 64) and the 4-phase
+    kernels at every M (path 2)."""
+    ext.gemm_test_force(path)
     torch.manual_seed(0)
     x = (torch.rand(M, K, device="cuda") * 2 - 1).bfloat16()
     w = ((torch.rand(N, K, device="cuda") * 2 - 1) * 0.1).bfloat16()
@@ -218,7 +208,6 @@ def test_gemm_nt(ext, M, N, K, gelu, nt64, narrow):
     if gelu:
         g_ref = torch.nn.functional.gelu(outs[0].float(), approximate="tanh")
         assert rel(outs[1], g_ref) < 1e-2
-    ext.gemm_set_variant(0, 8)
 
 
 @pytest.mark.parametrize("rows", [224, 192, 256])
@@ -228,9 +217,7 @@ def test_gemm_nt_short_rows(ext, M, N, K, lda, rows):
     """4-phase kernel at forced tile heights (224 / 192 rows: p4_mainloop MTL = 3 / 2) against fp32,
     every epilogue (bias, GELU pair, gelu' / gelu, GELU only, dGELU and dGELU-multiply with the
     column-partial bias gradient), ragged M, N % 8 != 0 (register epilogue) and strided A rows."""
-    ext.gemm_set_narrow(0)
-    ext.gemm_set_rows(rows)
-    ext.gemm_set_tail(0)
+    ext.gemm_test_force(2, rows)
     torch.manual_seed(0)
     xa = (torch.rand(M, lda, device="cuda") * 2 - 1).bfloat16()
     x = xa[:, :K]
@@ -299,12 +286,11 @@ def test_attention_long_sequence_path(ext, B, S, H, hd):
     assert torch.equal(dqkv, dqkv2)  # one writer per element: deterministic
 
 
-@pytest.mark.parametrize("variant,narrow", [(0, 4096), (0, 0), (1, 0)])
+@pytest.mark.parametrize("path", [0, 2, 1])
 @pytest.mark.parametrize("M,N,K", [(512, 256, 64), (1000, 1536, 512), (300, 512, 128), (5000, 776, 256)])
-def test_gemm_nt_dgelu(ext, M, N, K, variant, narrow):
+def test_gemm_nt_dgelu(ext, M, N, K, path):
     """FF2 data gradient through the GELU with the FF1 bias gradient (csrc/gemm.hip EPI_DGELU)."""
-    ext.gemm_set_variant(variant, 8)
-    ext.gemm_set_narrow(narrow)
+    ext.gemm_test_force(path)
     torch.manual_seed(0)
     dy = (torch.rand(M, K, device="cuda") * 2 - 1).bfloat16()
     w2t = ((torch.rand(N, K, device="cuda") * 2 - 1) * 0.1).bfloat16()
@@ -471,13 +457,12 @@ def test_residual_ln_fwd_partial_rows(ext, D):
     assert torch.allclose(mu, mur, atol=1e-6) and torch.allclose(rs, rsr, rtol=1e-5)
 
 
-@pytest.mark.parametrize("variant,narrow", [(0, 4096), (0, 0), (1, 0)])
+@pytest.mark.parametrize("path", [0, 2, 1])
 @pytest.mark.parametrize("M,N,K,S", [(512, 3072, 12288, 10), (300, 512, 4096, 3), (512, 256, 1024, 16),
                                      (128, 2304, 9216, 16), (128, 1000, 2304, 4)])
-def test_gemm_nt_splitk(ext, M, N, K, S, variant, narrow):
+def test_gemm_nt_splitk(ext, M, N, K, S, path):
     """Split-K MFMA GEMM (fp32 partial tiles + bf16 reduce with bias), ragged M."""
-    ext.gemm_set_variant(variant, 8)
-    ext.gemm_set_narrow(narrow)
+    ext.gemm_test_force(path)
     torch.manual_seed(0)
     x = (torch.rand(M, K, device="cuda") * 2 - 1).bfloat16()
     w = ((torch.rand(N, K, device="cuda") * 2 - 1) * 0.05).bfloat16()
@@ -538,7 +523,8 @@ def test_layernorm_bwd_fused_residual(ext, T0, view_y, with_scale):
 @pytest.mark.parametrize("kind", ["store", "gelu", "gelu_only", "dgelu"])
 @pytest.mark.parametrize("M,N,K", [(4352, 4096, 1024), (4200, 4096, 512), (25472, 768, 3072)])
 def test_gemm_nt_tail_split(ext, kind, M, N, K):
-    """Last partial wave of tiles computed split-K + finish kernel == the plain launch."""
+    """Last partial wave of tiles computed split-K + finish kernel == the plain launch (path 2 at
+    256-row tiles: no tail split)."""
     torch.manual_seed(5)
     A = (torch.rand(M, K, device="cuda") * 2 - 1).bfloat16()
     W = ((torch.rand(N, K, device="cuda") * 2 - 1) * 0.05).bfloat16()
@@ -546,13 +532,13 @@ def test_gemm_nt_tail_split(ext, kind, M, N, K):
     pre = (torch.randn(M, N, device="cuda") * 2).bfloat16()
     outs = []
     for tail in (0, 1):
-        ext.gemm_set_tail(tail)
+        ext.gemm_test_force(0 if tail else 2, 256)
         if kind == "dgelu":
             db = torch.zeros(N, device="cuda")
             outs.append((ext.gemm_nt_dgelu(A, W, pre, db), db))
         else:
             outs.append(tuple(ext.gemm_nt(A, W, b, kind != "store", kind == "gelu_only")))
-    ext.gemm_set_tail(1)
+    ext.gemm_test_force(0)
     ref = A.float() @ W.float().t()
     for o0, o1 in zip(outs[0], outs[1]):
         assert o0.shape == o1.shape
@@ -706,8 +692,8 @@ def test_small_m_routing_uses_mfma(ext):
     narrow GEMMs otherwise, a padded reduction for the 1000-class head's data gradient."""
     from jumbo_mae_tpu_amd.ops import prims as P
     assert P.use_our_gemm(512, 12288, 3072, fused_gelu=True) and P.splitk_plan(512, 12288, 3072) == 0
-    # K = 12288 jumbo GEMMs: 64 narrow tiles x 4 splits (10 x 24 tiles with NARROW_SPLITK off)
-    assert P.splitk_plan(512, 3072, 12288) == (4 if P.NARROW_SPLITK else 10)
+    # K = 12288 jumbo GEMMs: 64 narrow tiles x 4 splits
+    assert P.splitk_plan(512, 3072, 12288) == 4
     assert not P.use_our_gemm(128, 9216, 2304, fused_gelu=True) and P.splitk_plan(128, 9216, 2304) >= 2
     from jumbo_mae_tpu_amd.models.params import ParamStore, trunc_normal_t, zeros_
     st = ParamStore()

@@ -1,11 +1,11 @@
 """Interleaved A/B of runtime switches on the flagship step (one process, one device).
 
-    python tools/ab_bench.py --configs "blas:JMAE_GEMM=blas" "auto:" --rounds 4 --steps 6
+    python tools/ab_bench.py --configs "blas:GEMM=blas" "auto:" --rounds 4 --steps 6
 
 Each config is a list of ``KEY=VALUE`` switches applied to ``ops.prims`` module state between
 rounds (same model, same data, same device -> no cross-process / cross-device variance).
-Supported keys: JMAE_GEMM (auto|blas|ours), JMAE_DGRAD (0|1), JMAE_WGRAD (0|1), JMAE_WGRAD_STREAM (0|1),
-GEMM_VARIANT (12 default, 6 = plain stores, 4 = 32-deep ring, 5 = persistent).
+Supported keys: GEMM (auto|blas|ours), DGRAD (0|1), WGRAD (0|1), WGRAD_STREAM (0|1),
+and the Python-side constants below (kernel-level choices are fixed by shape in csrc/).
 Prints per-config median / min ms per step."""
 
 import argparse
@@ -22,72 +22,37 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 def apply(P, cfg: str):
     for kv in filter(None, cfg.split(",")):
         k, v = kv.split("=")
-        if k == "JMAE_GEMM":
+        if k == "GEMM":
             P._GEMM_MODE = v
-        elif k == "JMAE_DGRAD":
+        elif k == "DGRAD":
             P._DGRAD_OURS = v == "1"
-        elif k == "JMAE_WGRAD_STREAM":
+        elif k == "WGRAD_STREAM":
             P.set_wgrad_stream(v == "1")
-        elif k == "JMAE_WGRAD":
+        elif k == "WGRAD":
             P._WGRAD_OURS = v == "1"
-        elif k == "GEMM_NT64":  # 1: every NT launch on the 64-deep main loop
-            from jumbo_mae_tpu_amd.ops import _ext
-            _ext.load(True).gemm_set_variant(int(v), 8)
-        elif k == "GEMM_GROUP":  # row tiles per column sweep of the NT kernels
-            from jumbo_mae_tpu_amd.ops import _ext
-            _ext.load(True).gemm_set_variant(0, int(v))
-        elif k == "GEMM_ROWS":  # 4-phase tile height: 0 = automatic wave fill, 256 / 224 / 192 forced
-            from jumbo_mae_tpu_amd.ops import _ext
-            _ext.load(True).gemm_set_rows(int(v))
-        elif k == "JMAE_PAIR_WGRAD":  # 0: every weight gradient launched on its own
+        elif k == "PAIR_WGRAD":  # 0: every weight gradient launched on its own
             P.PAIR_WGRAD = v == "1"
-        elif k == "NARROW_SPLITK":  # split-K GEMMs from M = 256 on the narrow 128 x 192 tiles
-            from jumbo_mae_tpu_amd.ops import _ext
-            _ext.load(True).gemm_set_narrow_splitk(int(v))
-            P.NARROW_SPLITK = v == "1"
-        elif k == "JMAE_GROUP_JUMBO_WGRAD":  # 0: the jumbo W1 / W2 batched weight gradients launched apart
+        elif k == "GROUP_JUMBO_WGRAD":  # 0: the jumbo W1 / W2 batched weight gradients launched apart
             P.GROUP_JUMBO_WGRAD = v == "1"
-        elif k == "JMAE_STORE_GRADS":  # 0: zero the whole gradient buffer every step
+        elif k == "STORE_GRADS":  # 0: zero the whole gradient buffer every step
             import jumbo_mae_tpu_amd.models.params as PM
             PM.STORE_GRADS = v == "1"
-        elif k == "GEMM_TAIL":
-            from jumbo_mae_tpu_amd.ops import _ext
-            _ext.load(True).gemm_set_tail(int(v))
-        elif k == "JMAE_WT_BATCH":
+        elif k == "WT_BATCH":
             import jumbo_mae_tpu_amd.models.params as PM
             PM.BATCH_TRANSPOSES = v == "1"
-        elif k == "NARROW_MAX_M":  # NT GEMMs below this M on the 128 x 192 narrow kernel (0 = never)
-            from jumbo_mae_tpu_amd.ops import _ext
-            _ext.load(True).gemm_set_narrow(int(v))
-            P.NARROW_MAX_M = int(v)
-        elif k == "LN_BWD_BLOCKS":
-            from jumbo_mae_tpu_amd.ops import _ext
-            _ext.load(True).ln_set_bwd_blocks(int(v))
-        elif k == "ADAMW_VEC":
-            from jumbo_mae_tpu_amd.ops import _ext
-            _ext.load(True).opt_set_adamw_vec(int(v))
-        elif k == "ATTN_HPW":
-            from jumbo_mae_tpu_amd.ops import _ext
-            _ext.load(True).attn_set_fwd_hpw(int(v))
-        elif k == "ATTN_PPW":
-            from jumbo_mae_tpu_amd.ops import _ext
-            _ext.load(True).attn_set_bwd_ppw(int(v))
-        elif k == "ATTN_TR":
-            from jumbo_mae_tpu_amd.ops import _ext
-            _ext.load(True).attn_set_tr(int(v))
-        elif k == "JMAE_GELU_DERIV":
+        elif k == "GELU_DERIV":
             P._GELU_DERIV = v == "1"
-        elif k == "JMAE_FWD_LINKS":
+        elif k == "FWD_LINKS":
             from jumbo_mae_tpu_amd.ops import blocks
             blocks.FWD_LINKS = v == "1"
-        elif k == "JMAE_LINK_BLOCKS":
+        elif k == "LINK_BLOCKS":
             from jumbo_mae_tpu_amd.ops import blocks
             blocks.LINKS = v == "1"
-        elif k == "JMAE_FUSE_LN_RES":
+        elif k == "FUSE_LN_RES":
             P._FUSE_LN_RES = v == "1"
-        elif k == "JMAE_SEG_WGRAD":
+        elif k == "SEG_WGRAD":
             P._deferred["seg"] = v == "1"
-        elif k == "JMAE_DEFER_WGRAD":
+        elif k == "DEFER_WGRAD":
             P._deferred["enabled"] = v == "1"
         else:
             raise ValueError(k)

@@ -1,8 +1,7 @@
-"""AdamW multi-tensor kernel (csrc/optim.hip) alone, ViT-L-sized flat buffers, in-process A/B of
-the load/store variants (ext.opt_set_adamw_vec: 1 = float4 per lane (default), 0 = the r1
-4-B-per-lane loop).  profiles/r3_adamw_streaming.txt: the pass runs at ~5.0 TB/s.
+"""AdamW multi-tensor kernel (csrc/optim.hip) alone on ViT-L-sized flat buffers (16 B per lane;
+profiles/r3_adamw_streaming.txt: the pass runs at ~5.0 TB/s).
 
-    python tools/adamw_bench.py [--n 400000000] [--variants 1,0] [--rounds 5]"""
+    python tools/adamw_bench.py [--n 400000000] [--rounds 5]"""
 
 import argparse
 import os
@@ -17,7 +16,6 @@ from jumbo_mae_tpu_amd.ops import _ext  # noqa: E402
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--n", type=int, default=400_000_000)
-    ap.add_argument("--variants", default="1,0")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=10)
     a = ap.parse_args()
@@ -31,33 +29,19 @@ def main():
     meta = torch.tensor([1.0, 1.0, 0.0, 1.0], device="cuda")
     hyper = torch.tensor([1e-4, 0.1, 0.05, 1.0, 0.9, 0.95, 1e-8, 0.05], device="cuda")
     gn = torch.tensor([-1.0], device="cuda")
-    outs = {}
-    for v in a.variants.split(","):  # same update from the same state: results must agree
-        ext.opt_set_adamw_vec(int(v))
-        q, m_, v_ = p.clone(), mu.clone(), nu.clone()
-        ext.opt_adamw(q, g, m_, v_, shadow, chunks, meta, hyper, gn)
-        outs[v] = q
-    base = outs[a.variants.split(",")[0]]
-    for v, q in outs.items():
-        print(f"variant {v}: max |diff| vs first {(q - base).abs().max().item():.3e}")
-    del outs
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    t = {v: [] for v in a.variants.split(",")}
+    ts = []
     for _ in range(a.rounds):
-        for v in t:
-            ext.opt_set_adamw_vec(int(v))
+        ext.opt_adamw(p, g, mu, nu, shadow, chunks, meta, hyper, gn)
+        e0.record()
+        for _ in range(a.iters):
             ext.opt_adamw(p, g, mu, nu, shadow, chunks, meta, hyper, gn)
-            e0.record()
-            for _ in range(a.iters):
-                ext.opt_adamw(p, g, mu, nu, shadow, chunks, meta, hyper, gn)
-            e1.record()
-            torch.cuda.synchronize()
-            t[v].append(e0.elapsed_time(e1) * 1e3 / a.iters)
-    ext.opt_set_adamw_vec(1)
-    for v, ts in t.items():
-        tb = min(ts)
-        print(f"variant {v}: {tb:8.1f} us (rounds {', '.join(f'{x:.0f}' for x in ts)})  "
-              f"{30.0 * n / tb / 1e6:5.2f} TB/s at 30 B/param", flush=True)
+        e1.record()
+        torch.cuda.synchronize()
+        ts.append(e0.elapsed_time(e1) * 1e3 / a.iters)
+    tb = min(ts)
+    print(f"adamw: {tb:8.1f} us (rounds {', '.join(f'{x:.0f}' for x in ts)})  "
+          f"{30.0 * n / tb / 1e6:5.2f} TB/s at 30 B/param", flush=True)
 
 
 if __name__ == "__main__":

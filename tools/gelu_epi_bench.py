@@ -33,11 +33,10 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--rounds", type=int, default=3)
-    ap.add_argument("--variant", type=int, default=0, help="NT GEMM variant (ext.gemm_set_variant), 0 = default")
+    ap.add_argument("--path", type=int, default=0, help="NT GEMM kernel path (ext.gemm_test_force), 0 = by shape")
     a = ap.parse_args()
     ext = _ext.load()
-    if a.variant:
-        ext.gemm_set_variant(a.variant, 8)
+    ext.gemm_test_force(a.path)
     for name, (M, N, K) in SHAPES.items():
         x = (torch.randn(M, K, device="cuda") * 0.5).bfloat16()
         w1 = (torch.randn(N, K, device="cuda") * 0.03).bfloat16()

@@ -65,25 +65,16 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--only", default="")
     ap.add_argument("--kinds", default="fwd,fwd_gelu,dgrad")
-    ap.add_argument("--variant", default="0", help="kernel variant(s), comma separated: 0 = default routing, "
-                    "1 = 64-deep main loop everywhere; suffix t = tail split, n = narrow tiles at every M, w = never narrow; "
-                    "several = interleaved A/B")
-    ap.add_argument("--group", type=int, default=8, help="row tiles per column sweep")
-    ap.add_argument("--tail", type=int, default=0, help="tail split of the last partial wave (1 = on)")
+    ap.add_argument("--variant", default="0", help="kernel path(s) (ext.gemm_test_force), comma separated: 0 = by "
+                    "shape, 1 = 64-deep main loop everywhere, 2 = 4-phase kernels at every M without tail split, "
+                    "2rNNN = the same at forced tile height NNN (256 / 224 / 192); several = interleaved A/B")
     a = ap.parse_args()
     ext = _ext.load()
-    ext.gemm_set_tail(a.tail)
     variants = a.variant.split(",")
 
-    def setv(v):  # suffix t = tail split (last partial wave split-K + finish kernel), n = narrow
-        # 128 x 192 tiles at every M, w = never narrow (256 x 256 tiles at every M), rNNN = 4-phase
-        # tile height forced to NNN rows (256 / 224 / 192; default: automatic wave-fill choice)
+    def setv(v):
         m = re.search(r"r(\d+)", v)
-        ext.gemm_set_rows(int(m.group(1)) if m else 0)
-        v = re.sub(r"r\d+", "", v)
-        ext.gemm_set_tail(1 if "t" in v else 0)
-        ext.gemm_set_narrow(1 << 30 if "n" in v else 0 if "w" in v else 4096)
-        ext.gemm_set_variant(int(v.rstrip("tnw")), a.group)
+        ext.gemm_test_force(int(re.sub(r"r\d+", "", v)), int(m.group(1)) if m else 0)
 
     setv(variants[0])
     names = [n for n in FWD if not a.only or n in a.only.split(",")]
