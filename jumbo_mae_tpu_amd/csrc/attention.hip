@@ -140,7 +140,7 @@ JM_DEVICE f32x4_t qk_init(int kt, int g, int S) {
 // transposing ds_read_b64_tr_b16); the Q fragments of every query tile of a wave and all of a
 // thread's K / V chunks are loaded up front, one HBM round trip instead of one per chunk.
 template <int HD, int SP, bool EX = false>
-__global__ __launch_bounds__(256) void attn_fwd_kernel(const uint16_t* __restrict__ qkv, uint16_t* __restrict__ o,
+__global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const uint16_t* __restrict__ qkv, uint16_t* __restrict__ o,
                                                        float* __restrict__ lse, int S, int H, float scale) {
   JM_DGUARD(S >= 1 && S <= SP && blockDim.x == 256);
   constexpr int KS = HD + 8;  // K / V row stride (elements), 16-B aligned, breaks bank aliasing
@@ -239,7 +239,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const uint16_t* __restric
 // MFMA / softmax work (the one-pair kernel stalls on every load phase); Q fragments of the next
 // query tile are prefetched the same way.
 template <int HD, int SP, bool EX = false>
-__global__ __launch_bounds__(256) void attn_fwd_ml_kernel(const uint16_t* __restrict__ qkv, uint16_t* __restrict__ o,
+__global__ __launch_bounds__(256, 2) void attn_fwd_ml_kernel(const uint16_t* __restrict__ qkv, uint16_t* __restrict__ o,
                                                           float* __restrict__ lse, int S, int H, int BH, int hpw,
                                                           float scale) {
   JM_DGUARD(S >= 1 && S <= SP && hpw >= 1 && blockDim.x == 256);
@@ -377,7 +377,7 @@ constexpr size_t bwd2_smem() {
 
 
 template <int HD, int SP>
-__global__ __launch_bounds__(256) void attn_bwd2_kernel(const uint16_t* __restrict__ qkv,
+__global__ __launch_bounds__(256, 2) void attn_bwd2_kernel(const uint16_t* __restrict__ qkv,
                                                         const uint16_t* __restrict__ o,
                                                         const uint16_t* __restrict__ dO,
                                                         const float* __restrict__ lse,
@@ -684,7 +684,7 @@ __global__ __launch_bounds__(256) void attn_bwd2_kernel(const uint16_t* __restri
 // more than 256 VGPRs (one wave per SIMD): 8 waves own half the key tiles each (half the dK / dV
 // accumulators) and sweep 128-query chunks (one 16-query dQ tile per wave), two waves per SIMD.
 template <int HD, int SP, int NWV = 4>
-__global__ __launch_bounds__(64 * NWV) void attn_bwd3_kernel(const uint16_t* __restrict__ qkv,
+__global__ __launch_bounds__(64 * NWV, 2) void attn_bwd3_kernel(const uint16_t* __restrict__ qkv,
                                                         const uint16_t* __restrict__ o,
                                                         const uint16_t* __restrict__ dO,
                                                         const float* __restrict__ lse,
@@ -1139,7 +1139,7 @@ JM_DEVICE bf16x8_t tr_frag(const uint16_t* t, int s, int dt, int l16, int g) {
 }
 
 template <int HD>
-__global__ __launch_bounds__(256) void attn_fwd_long_kernel(const uint16_t* __restrict__ qkv,
+__global__ __launch_bounds__(256, 2) void attn_fwd_long_kernel(const uint16_t* __restrict__ qkv,
                                                             uint16_t* __restrict__ o, float* __restrict__ lse,
                                                             int S, int H, float scale) {
   constexpr int KS = HD + 8, KK = HD / 32, DT = HD / 16;
@@ -1234,7 +1234,7 @@ __global__ __launch_bounds__(256) void attn_fwd_long_kernel(const uint16_t* __re
 }
 
 template <int HD>
-__global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const uint16_t* __restrict__ qkv,
+__global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(const uint16_t* __restrict__ qkv,
                                                           const uint16_t* __restrict__ o,
                                                           const uint16_t* __restrict__ dO,
                                                           const float* __restrict__ lse,
@@ -1326,7 +1326,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const uint16_t* __rest
 }
 
 template <int HD>
-__global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(const uint16_t* __restrict__ qkv,
+__global__ __launch_bounds__(256, 2) void attn_bwd_dkv_kernel(const uint16_t* __restrict__ qkv,
                                                            const uint16_t* __restrict__ dO,
                                                            const float* __restrict__ lse,
                                                            const float* __restrict__ delta,
