@@ -51,6 +51,15 @@ JM_DEVICE s16x4_t tr4(const uint16_t* p) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4_t*)(p));
 }
 
+// 8 bf16 values (one 16-byte chunk) times f, rounded back to bf16
+JM_DEVICE uint4 scale_bf16x8(uint4 v, float f) {
+  uint32_t* w = reinterpret_cast<uint32_t*>(&v);
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+    w[j] = pack_bf2(__uint_as_float(w[j] << 16) * f, __uint_as_float(w[j] & 0xffff0000u) * f);
+  return v;
+}
+
 JM_DEVICE f32x4_t mfma(bf16x8_t a, bf16x8_t b, f32x4_t c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
@@ -372,7 +381,7 @@ JM_DEVICE int swo(int row, int col) {
 
 template <int HD, int SP, int QC = 64>
 constexpr size_t bwd2_smem() {
-  return (size_t)(3 * SP * HD + SP * QC) * 2 + (2 * SP + 3 * HD) * sizeof(float);
+  return (size_t)(3 * SP * HD + SP * QC) * 2 + (2 * SP + (QC / 16) * 3 * HD) * sizeof(float);
 }
 
 
@@ -435,8 +444,6 @@ __global__ __launch_bounds__(256, 2) void attn_bwd2_kernel(const uint16_t* __res
   for (int dt = 0; dt < DT; ++dt)
 #pragma unroll
     for (int i = 0; i < 4; ++i) qb[dt][i] = kb[dt][i] = vb[dt][i] = 0.f;
-  if (dbp != nullptr)
-    for (int i = threadIdx.x; i < 3 * HD; i += NTH) bsum[i] = 0.f;
 
   constexpr int NIT = (SP * NCH + NTH - 1) / NTH;
   uint4 qv[NIT], kv[NIT], dv[NIT], ov[NIT];
@@ -477,7 +484,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd2_kernel(const uint16_t* __res
       }
     }
     const int i = threadIdx.x;
-    lsen = (i < SP && i < S) ? lse[((long)b * H + h) * S + i] * LOG2E : INFINITY;
+    lsen = (i < SP && i < S) ? -lse[((long)b * H + h) * S + i] * LOG2E : -INFINITY;
   };
 
   // one batch element
@@ -493,10 +500,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd2_kernel(const uint16_t* __res
   for (int w = 0; w < NKW; ++w)
 #pragma unroll
     for (int kk = 0; kk < KK; ++kk) vf[w][kk] = vfn[w][kk];
-  if (threadIdx.x < SP) {
-    delta_s[threadIdx.x] = 0.f;
-    lse_s[threadIdx.x] = lsen;
-  }
+  if (threadIdx.x < SP) lse_s[threadIdx.x] = lsen;  // -lse (log2 domain): the S accumulator init
   __syncthreads();
   // LDS images from the registers; delta = O . dO
 #pragma unroll
@@ -505,21 +509,25 @@ __global__ __launch_bounds__(256, 2) void attn_bwd2_kernel(const uint16_t* __res
     const int r = i / NCH, c = (i % NCH) * 8;
     if (i < SP * NCH) {
       const int off = swo<NCH>(r, c);
-      *reinterpret_cast<uint4*>(Qs + off) = qv[it];
+      *reinterpret_cast<uint4*>(Qs + off) = scale_bf16x8(qv[it], sl2);  // P = exp2(S) (see attn_bwd3_kernel)
       *reinterpret_cast<uint4*>(Ks + off) = kv[it];
       *reinterpret_cast<uint4*>(dOs + off) = dv[it];
-      if (r < S) {
-        const uint32_t* ow = reinterpret_cast<const uint32_t*>(&ov[it]);
-        const uint32_t* dw = reinterpret_cast<const uint32_t*>(&dv[it]);
-        float dsum = 0.f;
+    }
+    // delta = O . dO: the NCH chunks of row r sit in NCH consecutive lanes (whole groups in or out
+    // of range) -> butterfly sum and one plain store: the same value on every run, no atomics
+    float dsum = 0.f;
+    if (i < SP * NCH && r < S) {
+      const uint32_t* ow = reinterpret_cast<const uint32_t*>(&ov[it]);
+      const uint32_t* dw = reinterpret_cast<const uint32_t*>(&dv[it]);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          dsum += __uint_as_float(ow[j] << 16) * __uint_as_float(dw[j] << 16);
-          dsum += __uint_as_float(ow[j] & 0xffff0000u) * __uint_as_float(dw[j] & 0xffff0000u);
-        }
-        atomicAdd(&delta_s[r], dsum);
+      for (int j = 0; j < 4; ++j) {
+        dsum += __uint_as_float(ow[j] << 16) * __uint_as_float(dw[j] << 16);
+        dsum += __uint_as_float(ow[j] & 0xffff0000u) * __uint_as_float(dw[j] & 0xffff0000u);
       }
     }
+#pragma unroll
+    for (int m = 1; m < NCH; m <<= 1) dsum += __shfl_xor(dsum, m, WAVE);
+    if (i < SP * NCH && c == 0) delta_s[r] = -dsum;  // -delta: the dP accumulator init; padded rows 0
   }
   __syncthreads();
 
@@ -537,54 +545,60 @@ __global__ __launch_bounds__(256, 2) void attn_bwd2_kernel(const uint16_t* __res
   }
 
   for (int qc = 0; qc * QC < SP; ++qc) {
+    // one key tile; ``kneg`` = -1e30 on padded keys (only in the tile that holds them)
+    auto tile = [&](int w, int kt, float kneg) {
+      uint16_t* dsw = dSt + kt * 16 * QC;
+#pragma unroll
+      for (int r = 0; r < QC / 32; ++r) {
+        const int qbase = qc * QC + 32 * r;
+        if (qbase < SP) {
+          float pf[8], df[8];
+#pragma unroll
+          for (int half = 0; half < 2; ++half) {
+            const int q0 = qbase + 16 * half;
+            const float4 l4 = *reinterpret_cast<const float4*>(lse_s + q0 + 4 * g);
+            const float4 d4 = *reinterpret_cast<const float4*>(delta_s + q0 + 4 * g);
+            f32x4_t sacc = {l4.x + kneg, l4.y + kneg, l4.z + kneg, l4.w + kneg};
+            f32x4_t dp = {d4.x, d4.y, d4.z, d4.w};
+#pragma unroll
+            for (int kk = 0; kk < KK; ++kk) {
+              sacc = mfma(ld8(Qs + q0 * HD + o_frag[kk]), kf[w][kk], sacc);
+              dp = mfma(ld8(dOs + q0 * HD + o_frag[kk]), vf[w][kk], dp);
+            }
+            // sacc[i] = S[q = q0 + 4g + i][key] (log2 domain, minus lse)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              const float p = __builtin_amdgcn_exp2f(sacc[i]);
+              pf[4 * half + i] = p;
+              df[4 * half + i] = p * dp[i];
+            }
+            uint2 pk;
+            pk.x = pack_bf2(df[4 * half], df[4 * half + 1]);
+            pk.y = pack_bf2(df[4 * half + 2], df[4 * half + 3]);
+            *reinterpret_cast<uint2*>(dsw + o_dsw[2 * r + half]) = pk;
+          }
+          const bf16x8_t pb = pack8(pf);
+          const bf16x8_t dsb = pack8(df);
+#pragma unroll
+          for (int dt = 0; dt < DT; ++dt) {
+            const uint16_t* dor = dOs + qbase * HD;
+            const uint16_t* qr = Qs + qbase * HD;
+            const bf16x8_t a_do = cat44(tr4(dor + o_tr[dt][0]), tr4(dor + o_tr[dt][1]));
+            const bf16x8_t a_q = cat44(tr4(qr + o_tr[dt][0]), tr4(qr + o_tr[dt][1]));
+            dvacc[w][dt] = mfma(a_do, pb, dvacc[w][dt]);
+            dkacc[w][dt] = mfma(a_q, dsb, dkacc[w][dt]);
+          }
+        }
+      }
+    };
 #pragma unroll
     for (int w = 0; w < NKW; ++w) {
       const int kt = wave + NW * w;
-      if (kt < NT) {
-        const float kmask = kt * 16 + l16 < S ? 1.f : 0.f;  // padded keys: P = 0
-        uint16_t* dsw = dSt + kt * 16 * QC;
-#pragma unroll
-        for (int r = 0; r < QC / 32; ++r) {
-          const int qbase = qc * QC + 32 * r;
-          if (qbase < SP) {
-            float pf[8], df[8];
-#pragma unroll
-            for (int half = 0; half < 2; ++half) {
-              const int q0 = qbase + 16 * half;
-              f32x4_t sacc = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-              for (int kk = 0; kk < KK; ++kk) {
-                sacc = mfma(ld8(Qs + q0 * HD + o_frag[kk]), kf[w][kk], sacc);
-                dp = mfma(ld8(dOs + q0 * HD + o_frag[kk]), vf[w][kk], dp);
-              }
-              // sacc[i] = S[q = q0 + 4g + i][key]
-              const float4 l4 = *reinterpret_cast<const float4*>(lse_s + q0 + 4 * g);
-              const float4 d4 = *reinterpret_cast<const float4*>(delta_s + q0 + 4 * g);
-              const float lv[4] = {l4.x, l4.y, l4.z, l4.w}, dv[4] = {d4.x, d4.y, d4.z, d4.w};
-#pragma unroll
-              for (int i = 0; i < 4; ++i) {
-                const float p = kmask * __builtin_amdgcn_exp2f(sacc[i] * sl2 - lv[i]);
-                pf[4 * half + i] = p;
-                df[4 * half + i] = p * (dp[i] - dv[i]);
-              }
-              uint2 pk;
-              pk.x = pack_bf2(df[4 * half], df[4 * half + 1]);
-              pk.y = pack_bf2(df[4 * half + 2], df[4 * half + 3]);
-              *reinterpret_cast<uint2*>(dsw + o_dsw[2 * r + half]) = pk;
-            }
-            const bf16x8_t pb = pack8(pf);
-            const bf16x8_t dsb = pack8(df);
-#pragma unroll
-            for (int dt = 0; dt < DT; ++dt) {
-              const uint16_t* dor = dOs + qbase * HD;
-              const uint16_t* qr = Qs + qbase * HD;
-              const bf16x8_t a_do = cat44(tr4(dor + o_tr[dt][0]), tr4(dor + o_tr[dt][1]));
-              const bf16x8_t a_q = cat44(tr4(qr + o_tr[dt][0]), tr4(qr + o_tr[dt][1]));
-              dvacc[w][dt] = mfma(a_do, pb, dvacc[w][dt]);
-              dkacc[w][dt] = mfma(a_q, dsb, dkacc[w][dt]);
-            }
-          }
-        }
+      if (kt * 16 + 16 <= S) {
+        tile(w, kt, 0.f);
+      } else if (kt < NT) {  // wave-uniform
+        asm volatile("" ::: "memory");  // keeps the two paths apart: no per-score selects
+        tile(w, kt, kt * 16 + l16 < S ? 0.f : -1e30f);
       }
     }
     __syncthreads();
@@ -629,8 +643,8 @@ __global__ __launch_bounds__(256, 2) void attn_bwd2_kernel(const uint16_t* __res
     if (kt < NT && key < S) {
 #pragma unroll
       for (int dt = 0; dt < DT; ++dt) {
-        float kv[4] = {dkacc[w][dt][0] * scale, dkacc[w][dt][1] * scale, dkacc[w][dt][2] * scale,
-                       dkacc[w][dt][3] * scale};
+        float kv[4] = {dkacc[w][dt][0] * LN2, dkacc[w][dt][1] * LN2, dkacc[w][dt][2] * LN2,
+                       dkacc[w][dt][3] * LN2};  // Q staged times scale * log2(e)
         float vv[4] = {dvacc[w][dt][0], dvacc[w][dt][1], dvacc[w][dt][2], dvacc[w][dt][3]};
         store4(dKg + (long)key * ts + dt * 16 + 4 * g, kv);
         store4(dVg + (long)key * ts + dt * 16 + 4 * g, vv);
@@ -656,16 +670,22 @@ __global__ __launch_bounds__(256, 2) void attn_bwd2_kernel(const uint16_t* __res
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const float sq = row16_sum(qb[dt][i]), sk = row16_sum(kb[dt][i]), sv = row16_sum(vb[dt][i]);
-        if (l16 == 0) {
+        if (l16 == 0) {  // one slot per wave, summed in wave order below: deterministic
+          float* bw = bsum + wave * 3 * HD;
           const int d = dt * 16 + 4 * g + i;
-          atomicAdd(&bsum[d], sq * scale);
-          atomicAdd(&bsum[HD + d], sk * scale);
-          atomicAdd(&bsum[2 * HD + d], sv);
+          bw[d] = sq * scale;
+          bw[HD + d] = sk * LN2;
+          bw[2 * HD + d] = sv;
         }
       }
     __syncthreads();
     float* dst = dbp + (long)bg * ts + h * HD;
-    for (int i = threadIdx.x; i < 3 * HD; i += NTH) dst[(i / HD) * H * HD + (i % HD)] = bsum[i];
+    for (int i = threadIdx.x; i < 3 * HD; i += NTH) {
+      float a = 0.f;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) a += bsum[w * 3 * HD + i];
+      dst[(i / HD) * H * HD + (i % HD)] = a;
+    }
   }
 }
 
@@ -678,8 +698,11 @@ __global__ __launch_bounds__(256, 2) void attn_bwd2_kernel(const uint16_t* __res
 //    tile (NKW = 4 key tiles per wave at S = 199);
 //  * per key tile issues the 8 independent S / dP MFMAs back to back, then the softmax-gradient
 //    VALU of all four 16-query slices, then the 8 dV / dK MFMAs;
-//  * masks padded keys through the MFMA accumulator init (-1e30 for keys >= S) instead of a
-//    multiply per score.
+//  * runs the softmax gradient on two VALU instructions per score besides the bf16 packs: Q is
+//    staged pre-multiplied by scale * log2(e) and the S accumulator starts at -lse (log2
+//    domain), so P = exp2(S) with no per-score fma; the dP accumulator starts at -delta, so
+//    dS = P * dP with no per-score subtraction (dK then scales by ln 2 instead of the softmax
+//    scale).  Padded keys (only in the last key tile) add -1e30 to that init.
 // NWV waves per workgroup: 4 (the default), or 8 for hd 64 at long S, where the 4-wave form needs
 // more than 256 VGPRs (one wave per SIMD): 8 waves own half the key tiles each (half the dK / dV
 // accumulators) and sweep 128-query chunks (one 16-query dQ tile per wave), two waves per SIMD.
@@ -724,11 +747,11 @@ __global__ __launch_bounds__(64 * NWV, 2) void attn_bwd3_kernel(const uint16_t* 
   const int l16 = lane & 15, g = lane >> 4;
 
   bf16x8_t vf[NKW][KK];
-  float kinit[NKW];
+  float kneg[NKW];  // -1e30 on padded keys
 #pragma unroll
   for (int w = 0; w < NKW; ++w) {
     const int key = (wave + NW * w) * 16 + l16;
-    kinit[w] = key < S ? 0.f : -1e30f;
+    kneg[w] = key < S ? 0.f : -1e30f;
 #pragma unroll
     for (int kk = 0; kk < KK; ++kk) {
       s16x8_t z = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -739,7 +762,8 @@ __global__ __launch_bounds__(64 * NWV, 2) void attn_bwd3_kernel(const uint16_t* 
   // every global load in one burst (V fragments above, lse, the staging rows): one exposed round
   // trip instead of two
   static_assert(SP <= NTH, "one lse per thread");
-  const float lsev = (int)threadIdx.x < S ? lse[((long)b * H + h) * S + threadIdx.x] * LOG2E : INFINITY;
+  // -lse in the log2 domain (the S accumulator init); padded queries -inf (P = 0)
+  const float nlse = (int)threadIdx.x < S ? -lse[((long)b * H + h) * S + threadIdx.x] * LOG2E : -INFINITY;
   constexpr int NIT = (SP * NCH + NTH - 1) / NTH;
   uint4 qv[NIT], kv[NIT], dv[NIT], ov[NIT];
 #pragma unroll
@@ -754,11 +778,9 @@ __global__ __launch_bounds__(64 * NWV, 2) void attn_bwd3_kernel(const uint16_t* 
       ov[it] = *reinterpret_cast<const uint4*>(Og + r * os + c);
     }
   }
-  for (int i = threadIdx.x; i < 3 * HD; i += NTH) bsum[i] = 0.f;
-  if ((int)threadIdx.x < SP) {
-    delta_s[threadIdx.x] = 0.f;
-    lse_s[threadIdx.x] = lsev;
-  }
+  for (int i = threadIdx.x; i < NW * 3 * HD; i += NTH) bsum[i] = 0.f;  // one slot per wave
+  const float sl2 = scale * LOG2E;
+  if ((int)threadIdx.x < SP) lse_s[threadIdx.x] = nlse;
   __syncthreads();
 #pragma unroll
   for (int it = 0; it < NIT; ++it) {
@@ -766,25 +788,28 @@ __global__ __launch_bounds__(64 * NWV, 2) void attn_bwd3_kernel(const uint16_t* 
     const int r = i / NCH, c = (i % NCH) * 8;
     if (i < SP * NCH) {
       const int off = swo<NCH>(r, c);
-      *reinterpret_cast<uint4*>(Qs + off) = qv[it];
+      *reinterpret_cast<uint4*>(Qs + off) = scale_bf16x8(qv[it], sl2);
       *reinterpret_cast<uint4*>(Ks + off) = kv[it];
       *reinterpret_cast<uint4*>(dOs + off) = dv[it];
-      if (r < S) {
-        const uint32_t* ow = reinterpret_cast<const uint32_t*>(&ov[it]);
-        const uint32_t* dw = reinterpret_cast<const uint32_t*>(&dv[it]);
-        float dsum = 0.f;
+    }
+    // delta = O . dO: the NCH chunks of row r sit in NCH consecutive lanes (whole groups in or out
+    // of range) -> butterfly sum and one plain store: the same value on every run, no atomics
+    float dsum = 0.f;
+    if (i < SP * NCH && r < S) {
+      const uint32_t* ow = reinterpret_cast<const uint32_t*>(&ov[it]);
+      const uint32_t* dw = reinterpret_cast<const uint32_t*>(&dv[it]);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          dsum += __uint_as_float(ow[j] << 16) * __uint_as_float(dw[j] << 16);
-          dsum += __uint_as_float(ow[j] & 0xffff0000u) * __uint_as_float(dw[j] & 0xffff0000u);
-        }
-        atomicAdd(&delta_s[r], dsum);
+      for (int j = 0; j < 4; ++j) {
+        dsum += __uint_as_float(ow[j] << 16) * __uint_as_float(dw[j] << 16);
+        dsum += __uint_as_float(ow[j] & 0xffff0000u) * __uint_as_float(dw[j] & 0xffff0000u);
       }
     }
+#pragma unroll
+    for (int m = 1; m < NCH; m <<= 1) dsum += __shfl_xor(dsum, m, WAVE);
+    if (i < SP * NCH && c == 0) delta_s[r] = -dsum;  // -delta: the dP accumulator init; padded rows 0
   }
   __syncthreads();
 
-  const float sl2 = scale * LOG2E;
   int o_frag[KK];
 #pragma unroll
   for (int kk = 0; kk < KK; ++kk) o_frag[kk] = swo<NCH>(l16, 32 * kk + 8 * g);
@@ -829,7 +854,7 @@ __global__ __launch_bounds__(64 * NWV, 2) void attn_bwd3_kernel(const uint16_t* 
         // ---- key-tile independent fragments of this 32-query block
         const int qb = q0 + 32 * r;
         bf16x8_t qf[2][KK], dof[2][KK], a_do[DT], a_q[DT];
-        float lv[2][4], dl[2][4];
+        f32x4_t lv[2], dl[2];  // accumulator inits: -lse (log2 domain) and -delta
 #pragma unroll
         for (int hh = 0; hh < 2; ++hh) {
 #pragma unroll
@@ -839,52 +864,59 @@ __global__ __launch_bounds__(64 * NWV, 2) void attn_bwd3_kernel(const uint16_t* 
           }
           const float4 l4 = *reinterpret_cast<const float4*>(lse_s + qb + 16 * hh + 4 * g);
           const float4 d4 = *reinterpret_cast<const float4*>(delta_s + qb + 16 * hh + 4 * g);
-          lv[hh][0] = l4.x; lv[hh][1] = l4.y; lv[hh][2] = l4.z; lv[hh][3] = l4.w;
-          dl[hh][0] = d4.x; dl[hh][1] = d4.y; dl[hh][2] = d4.z; dl[hh][3] = d4.w;
+          lv[hh] = f32x4_t{l4.x, l4.y, l4.z, l4.w};
+          dl[hh] = f32x4_t{d4.x, d4.y, d4.z, d4.w};
         }
 #pragma unroll
         for (int dt = 0; dt < DT; ++dt) {
           a_do[dt] = cat44(tr4(dOs + qb * HD + o_tr[dt][0]), tr4(dOs + qb * HD + o_tr[dt][1]));
           a_q[dt] = cat44(tr4(Qs + qb * HD + o_tr[dt][0]), tr4(Qs + qb * HD + o_tr[dt][1]));
         }
+        // one key tile: S / dP products from the accumulator inits, softmax gradient, dV / dK
+        auto tile = [&](int w, int kt, const f32x4_t (&ini)[2]) {
+          f32x4_t sacc[2], dp[2];
+#pragma unroll
+          for (int hh = 0; hh < 2; ++hh) {
+            sacc[hh] = ini[hh];
+            dp[hh] = dl[hh];
+#pragma unroll
+            for (int kk = 0; kk < KK; ++kk) {
+              sacc[hh] = mfma(qf[hh][kk], kf[w][kk], sacc[hh]);
+              dp[hh] = mfma(dof[hh][kk], vf[w][kk], dp[hh]);
+            }
+          }
+          float pf[8], df[8];
+          uint16_t* dsw = dSt + kt * 16 * QC;
+#pragma unroll
+          for (int hh = 0; hh < 2; ++hh) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              const float p = __builtin_amdgcn_exp2f(sacc[hh][i]);
+              pf[4 * hh + i] = p;
+              df[4 * hh + i] = p * dp[hh][i];
+            }
+            uint2 pk;
+            pk.x = pack_bf2(df[4 * hh], df[4 * hh + 1]);
+            pk.y = pack_bf2(df[4 * hh + 2], df[4 * hh + 3]);
+            *reinterpret_cast<uint2*>(dsw + (NWV == 4 ? o_dsw[2 * r + hh] : swo<DCH>(l16, 16 * (2 * r + hh) + 4 * g))) = pk;
+          }
+          const bf16x8_t pb = pack8(pf);
+          const bf16x8_t dsb = pack8(df);
+#pragma unroll
+          for (int dt = 0; dt < DT; ++dt) {
+            dvacc[w][dt] = mfma(a_do[dt], pb, dvacc[w][dt]);
+            dkacc[w][dt] = mfma(a_q[dt], dsb, dkacc[w][dt]);
+          }
+        };
 #pragma unroll
         for (int w = 0; w < NKW; ++w) {
           const int kt = wave + NW * w;
-          if (kt < NT) {
-            const f32x4_t ki = {kinit[w], kinit[w], kinit[w], kinit[w]};
-            f32x4_t sacc[2], dp[2];
-#pragma unroll
-            for (int hh = 0; hh < 2; ++hh) {
-              sacc[hh] = ki;
-              dp[hh] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-              for (int kk = 0; kk < KK; ++kk) {
-                sacc[hh] = mfma(qf[hh][kk], kf[w][kk], sacc[hh]);
-                dp[hh] = mfma(dof[hh][kk], vf[w][kk], dp[hh]);
-              }
-            }
-            float pf[8], df[8];
-            uint16_t* dsw = dSt + kt * 16 * QC;
-#pragma unroll
-            for (int hh = 0; hh < 2; ++hh) {
-#pragma unroll
-              for (int i = 0; i < 4; ++i) {
-                const float p = __builtin_amdgcn_exp2f(sacc[hh][i] * sl2 - lv[hh][i]);
-                pf[4 * hh + i] = p;
-                df[4 * hh + i] = p * (dp[hh][i] - dl[hh][i]);
-              }
-              uint2 pk;
-              pk.x = pack_bf2(df[4 * hh], df[4 * hh + 1]);
-              pk.y = pack_bf2(df[4 * hh + 2], df[4 * hh + 3]);
-              *reinterpret_cast<uint2*>(dsw + (NWV == 4 ? o_dsw[2 * r + hh] : swo<DCH>(l16, 16 * (2 * r + hh) + 4 * g))) = pk;
-            }
-            const bf16x8_t pb = pack8(pf);
-            const bf16x8_t dsb = pack8(df);
-#pragma unroll
-            for (int dt = 0; dt < DT; ++dt) {
-              dvacc[w][dt] = mfma(a_do[dt], pb, dvacc[w][dt]);
-              dkacc[w][dt] = mfma(a_q[dt], dsb, dkacc[w][dt]);
-            }
+          if (kt * 16 + 16 <= S) {
+            tile(w, kt, lv);
+          } else if (kt < NT) {  // the tile holding padded keys (wave-uniform branch)
+            asm volatile("" ::: "memory");  // keeps the two paths apart: no per-tile selects
+            const f32x4_t lm[2] = {lv[0] + kneg[w], lv[1] + kneg[w]};
+            tile(w, kt, lm);
           }
         }
       }
@@ -913,7 +945,7 @@ __global__ __launch_bounds__(64 * NWV, 2) void attn_bwd3_kernel(const uint16_t* 
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
               const float v = row16_sum(dq[dt][i]);
-              if (l16 == 0) atomicAdd(&bsum[dt * 16 + 4 * g + i], v * scale);
+              if (l16 == 0) bsum[wave * 3 * HD + dt * 16 + 4 * g + i] += v * scale;  // this wave's slot
             }
         }
         const int q = qt * 16 + l16;
@@ -935,8 +967,8 @@ __global__ __launch_bounds__(64 * NWV, 2) void attn_bwd3_kernel(const uint16_t* 
     if (kt < NT && key < S) {
 #pragma unroll
       for (int dt = 0; dt < DT; ++dt) {
-        float kv2[4] = {dkacc[w][dt][0] * scale, dkacc[w][dt][1] * scale, dkacc[w][dt][2] * scale,
-                        dkacc[w][dt][3] * scale};
+        float kv2[4] = {dkacc[w][dt][0] * LN2, dkacc[w][dt][1] * LN2, dkacc[w][dt][2] * LN2,
+                        dkacc[w][dt][3] * LN2};
         float vv[4] = {dvacc[w][dt][0], dvacc[w][dt][1], dvacc[w][dt][2], dvacc[w][dt][3]};
         store4(dKg + (long)key * ts + dt * 16 + 4 * g, kv2);
         store4(dVg + (long)key * ts + dt * 16 + 4 * g, vv);
@@ -957,14 +989,20 @@ __global__ __launch_bounds__(64 * NWV, 2) void attn_bwd3_kernel(const uint16_t* 
         sk = row16_sum(sk);
         sv = row16_sum(sv);
         if (l16 == 0) {
+          float* bw = bsum + wave * 3 * HD;
           const int d = dt * 16 + 4 * g + i;
-          atomicAdd(&bsum[HD + d], sk * scale);
-          atomicAdd(&bsum[2 * HD + d], sv);
+          bw[HD + d] = sk * LN2;
+          bw[2 * HD + d] = sv;
         }
       }
     __syncthreads();
     float* dst = dbp + (long)b * ts + h * HD;
-    for (int i = threadIdx.x; i < 3 * HD; i += NTH) dst[(i / HD) * H * HD + (i % HD)] = bsum[i];
+    for (int i = threadIdx.x; i < 3 * HD; i += NTH) {
+      float a = 0.f;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) a += bsum[w * 3 * HD + i];  // wave order: deterministic
+      dst[(i / HD) * H * HD + (i % HD)] = a;
+    }
   }
 }
 
