@@ -41,6 +41,7 @@ int jm_gelu_bwd(const uint16_t* h, const uint16_t* da, uint16_t* dh, float* bias
                 int deriv = 0);
 int jm_colsum_bf16(const uint16_t* x, float* acc, int M, int N, hipStream_t st);
 int jm_splitk_reduce_add(const float* part, float* g, long n, int S, hipStream_t st, int store = 0);
+int jm_colsum_add_f32(const float* x, long ld, int rows, long n, float* g, hipStream_t st);
 int jm_zero_ranges(float* base, const long long* desc, int n, long long blocks, hipStream_t st);
 int jm_transpose_bf16(const uint16_t* src, uint16_t* dst, int R, int C, hipStream_t st);
 int jm_transpose_bf16_batch(const long long* desc, int n, int tiles, hipStream_t st);
@@ -260,6 +261,19 @@ void splitk_reduce_add(torch::Tensor part, torch::Tensor g) {
   TORCH_CHECK(g.is_contiguous() && g.numel() * part.size(0) == part.numel(), "splitk_reduce_add shapes");
   check_rc(jm_splitk_reduce_add(part.data_ptr<float>(), g.data_ptr<float>(), g.numel(), part.size(0), stream()),
            "splitk_reduce_add");
+}
+
+// g += x.sum(0) for a 2-D fp32 view with unit column stride (any row stride), no torch reduce
+void colsum_add_f32(torch::Tensor x, torch::Tensor g) {
+  CHECK_CUDA(x);
+  CHECK_DT(x, torch::kFloat32);
+  CHECK_DT(g, torch::kFloat32);
+  TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1 && g.is_contiguous() && g.numel() == x.size(1),
+              "colsum_add_f32: x [rows, n] with unit column stride, g [n]");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(g.data_ptr()) % 16 == 0,
+              "colsum_add_f32: 16-byte aligned operands");
+  check_rc(jm_colsum_add_f32(x.data_ptr<float>(), x.stride(0), x.size(0), x.size(1), g.data_ptr<float>(), stream()),
+           "colsum_add_f32");
 }
 
 torch::Tensor residual_fwd(torch::Tensor x, torch::Tensor y, c10::optional<torch::Tensor> scale,
@@ -542,7 +556,7 @@ std::vector<torch::Tensor> unshuffle_bwd(torch::Tensor dout, torch::Tensor ids_r
   check_rc(jm_unshuffle_bwd(dout.data_ptr<float>(), ids_restore.data_ptr<int>(), sb, bfp(dy), part.data_ptr<float>(), B,
                             C, K, N, d, rpb, stream()),
            "unshuffle_bwd");
-  return {dy, part.sum(0)};
+  return {dy, part};  // [nb, d] fp32 partials: the caller adds their column sums (colsum_add_f32)
 }
 
 // finetune input: [B*N, 3p^2] bf16 normalized patches of the (Mixup / CutMix) blended batch
@@ -1091,6 +1105,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_tn_wgrad", &gemm_tn_wgrad, py::arg("dy"), py::arg("x"), py::arg("g"), py::arg("store") = false);
   m.def("gemm_tn_wgrad_seg", &gemm_tn_wgrad_seg, py::arg("dys"), py::arg("xs"), py::arg("g"), py::arg("store") = false);
   m.def("zero_ranges", &zero_ranges, "zero float ranges of a flat buffer (one launch)");
+  m.def("colsum_add_f32", &colsum_add_f32, "g += x.sum(0) for a row-strided fp32 [rows, n] view");
   m.def("gemm_tn_wgrad_seg_group", &gemm_tn_wgrad_seg_group, py::arg("dys"), py::arg("xs"), py::arg("gs"),
         py::arg("stores") = std::vector<bool>{}, "grouped segmented weight gradients (<= 2 problems)");
   m.def("gemm_tn_wgrad_group", &gemm_tn_wgrad_group, py::arg("dys"), py::arg("xs"), py::arg("gs"),

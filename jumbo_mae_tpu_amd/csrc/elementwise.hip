@@ -277,9 +277,10 @@ int jm_residual_bwd(const float* dout, long dB, long dT, const uint16_t* y, cons
 namespace {
 // g[i] += sum_s part[s][i].  grid.y > 1 splits the S partials into slices that are summed with
 // atomics: used when n is small and S large (per-sample bias partials, n = 3D, S = batch).
+// ``ld``: row stride of part in floats (n for the packed partial slices, a strided view otherwise).
 __global__ __launch_bounds__(256) void splitk_reduce_add_kernel(const float* __restrict__ part,
-                                                                float* __restrict__ g, long n4, int S) {
-  const long n = n4 * 4;
+                                                                float* __restrict__ g, long n4, int S, long ld) {
+  const long n = ld;
   const int per = (S + gridDim.y - 1) / gridDim.y;
   const int s0 = blockIdx.y * per;
   const int s1 = min(S, s0 + per);
@@ -373,7 +374,20 @@ int jm_splitk_reduce_add(const float* part, float* g, long n, int S, hipStream_t
   if (blocks > 4096) blocks = 4096;
   int ys = 1;  // slice the partials until the launch has ~512 workgroups of >= 8 rows each
   while (blocks * ys < 512 && S / (ys * 2) >= 8) ys *= 2;
-  splitk_reduce_add_kernel<<<dim3((unsigned)blocks, ys), 256, 0, st>>>(part, g, n4, S);
+  splitk_reduce_add_kernel<<<dim3((unsigned)blocks, ys), 256, 0, st>>>(part, g, n4, S, n);
+  return 0;
+}
+
+// g[i] += sum_r x[r * ld + i], i < n: column sums of a row-strided fp32 view (token-parameter
+// gradients: the CLS rows of dx, the mask-token partials) added straight into the flat gradient
+int jm_colsum_add_f32(const float* x, long ld, int rows, long n, float* g, hipStream_t st) {
+  if (n % 4 || ld % 4 || ld < n || rows < 1) return -1;
+  const long n4 = n / 4;
+  long blocks = (n4 + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  int ys = 1;
+  while (blocks * ys < 512 && rows / (ys * 2) >= 8) ys *= 2;
+  splitk_reduce_add_kernel<<<dim3((unsigned)blocks, ys), 256, 0, st>>>(x, g, n4, rows, ld);
   return 0;
 }
 

@@ -150,6 +150,22 @@ class Handle:
         self.grad.add_(g.reshape(self.shape).to(torch.float32))
         self.store.mark_ready(self)
 
+    def accumulate_grad_rows(self, x: torch.Tensor) -> None:
+        """grad += x.sum(0) for a 2-D fp32 [rows, numel] view (any row stride): on the GPU one HIP
+        column-sum kernel adding straight into the flat gradient -- no torch reduce (whose
+        cross-block accumulator is zeroed by a runtime memset, a graph node that replays wrong on
+        ROCm 7.x, profiles/r4_graph_memset.txt) and no separate add."""
+        if not self.segs[0].trainable:
+            return
+        self.settle()
+        from ..ops import _ext
+        if (_ext.use_hip(x) and x.dtype == torch.float32 and x.stride(-1) == 1 and x.shape[-1] % 4 == 0
+                and x.stride(0) % 4 == 0 and x.data_ptr() % 16 == 0):
+            _ext.load().colsum_add_f32(x, self.grad.view(-1))
+        else:
+            self.grad.add_(x.sum(0).reshape(self.shape).to(torch.float32))
+        self.store.mark_ready(self)
+
     def ready(self) -> None:
         self.store.mark_ready(self)
 

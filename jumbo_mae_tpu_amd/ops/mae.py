@@ -124,7 +124,7 @@ class _EmbedFinish(torch.autograd.Function):
         D = dx.shape[-1]
         dpatch = dx[:, C:]
         if ctx.h_cls.segs[0].trainable:
-            ctx.h_cls.accumulate_grad(dx[:, :C].sum(0))
+            ctx.h_cls.accumulate_grad_rows(dx[:, :C].reshape(B, C * D))
         h = ctx.h_wpe
         if h is not None and h.segs[0].trainable:
             if ids.dim() == 1:
@@ -161,9 +161,9 @@ class _Unshuffle(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dout):
         (ids32,) = ctx.saved_tensors
-        dy, dtok = _ext.load().unshuffle_bwd(dout.contiguous(), ids32, ctx.C, ctx.K)
+        dy, dtok_part = _ext.load().unshuffle_bwd(dout.contiguous(), ids32, ctx.C, ctx.K)
         if ctx.h_tok.segs[0].trainable:
-            ctx.h_tok.accumulate_grad(dtok)
+            ctx.h_tok.accumulate_grad_rows(dtok_part)
         return dy, None, None, None, None, None
 
 

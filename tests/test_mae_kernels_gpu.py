@@ -81,10 +81,26 @@ def test_unshuffle(ext, per_sample, d):
     ref = mae_ops.unshuffle(yr, tr, restore, pos, C)
     assert (out - ref).abs().max().item() < 1e-6
     dout = torch.randn_like(ref)
-    dy, dtok = ext.unshuffle_bwd(dout, restore.to(torch.int32).contiguous(), C, K)
+    dy, dtok_part = ext.unshuffle_bwd(dout, restore.to(torch.int32).contiguous(), C, K)
     ref.backward(dout)
     assert (dy.float() - yr.grad).abs().max().item() <= 2e-2 * yr.grad.abs().max().item()
-    assert rel(dtok, tr.grad) < 1e-5
+    assert rel(dtok_part.sum(0), tr.grad) < 1e-5
+    # the partials' column sums added in place by the strided HIP column sum (Handle.accumulate_grad_rows)
+    g = torch.full_like(tok, 0.25)
+    ext.colsum_add_f32(dtok_part, g)
+    assert rel(g - 0.25, tr.grad) < 1e-5
+
+
+@pytest.mark.parametrize("rows,ld,n", [(512, 3 * 1024 + 49 * 1024, 3 * 1024), (7, 100, 96), (2048, 4096, 4096)])
+def test_colsum_add_f32_strided(ext, rows, ld, n):
+    """g += x.sum(0) for a row-strided fp32 view (the CLS-row slice of dx)."""
+    torch.manual_seed(0)
+    buf = torch.randn(rows, ld, device="cuda")
+    x = buf[:, :n]
+    g = torch.randn(n, device="cuda")
+    ref = g.double() + x.double().sum(0)
+    ext.colsum_add_f32(x, g)
+    assert (g.double() - ref).abs().max().item() < 1e-4 * max(1.0, ref.abs().max().item())
 
 
 @pytest.mark.parametrize("norm_pix", [False, True])
