@@ -76,6 +76,18 @@ JM_DEVICE int xcd_bid() {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
 }
 
+// XOR swizzle of 16-byte chunks shared by every whole-sequence kernel's LDS images (the backward's
+// comment below has the details)
+JM_DEVICE int aswz(int row) {
+  return ((row >> 2) & 1) | ((((row >> 2) ^ (row >> 3)) & 1) << 1) | (((row >> 1) & 1) << 2);
+}
+
+// element offset of (row, col) in a swizzled image of NCH 16-byte chunks per row
+template <int NCH>
+JM_DEVICE int swo(int row, int col) {
+  return row * (NCH * 8) + ((((col >> 3) ^ aswz(row)) & (NCH - 1)) << 3) + (col & 7);
+}
+
 // ---------------------------------------------------------------- forward softmax (fast form)
 // The forward is VALU-bound (PMC: ~80 % of SIMD cycles in VALU at S = 199, hd = 32, ~10 VALU
 // instructions per score), so per score it now issues only an fma (scale and max subtraction in
@@ -149,16 +161,17 @@ JM_DEVICE f32x4_t qk_init(int kt, int g, int S) {
 // transposing ds_read_b64_tr_b16); the Q fragments of every query tile of a wave and all of a
 // thread's K / V chunks are loaded up front, one HBM round trip instead of one per chunk.
 template <int HD, int SP, bool EX = false>
-__global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const uint16_t* __restrict__ qkv, uint16_t* __restrict__ o,
+// waves per SIMD: the padded-row layout's occupancy, kept with the swizzled images
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HD == 64 && SP > 128 ? 4 : 2))) void attn_fwd_kernel(const uint16_t* __restrict__ qkv, uint16_t* __restrict__ o,
                                                        float* __restrict__ lse, int S, int H, float scale) {
   JM_DGUARD(S >= 1 && S <= SP && blockDim.x == 256);
-  constexpr int KS = HD + 8;  // K / V row stride (elements), 16-B aligned, breaks bank aliasing
   constexpr int NT = SP / 16;
   constexpr int KK = HD / 32;
   constexpr int DT = HD / 16;
+  constexpr int NCH = HD / 8;  // 16-byte chunks per row; K / V images XOR-swizzled (swo)
   extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
   uint16_t* Ks = smem;
-  uint16_t* Vs = smem + SP * KS;
+  uint16_t* Vs = smem + SP * HD;
 
   const int bh = xcd_bid();
   const int b = bh / H, h = bh - (bh / H) * H;
@@ -198,8 +211,8 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const uint16_t* __rest
     for (int it = 0; it < NIT; ++it) {
       const int i = it * 256 + threadIdx.x, r = i / CPR, c = (i % CPR) * 8;
       if (i < SP * CPR) {
-        *reinterpret_cast<uint4*>(Ks + r * KS + c) = kv[it];
-        *reinterpret_cast<uint4*>(Vs + r * KS + c) = vv[it];
+        *reinterpret_cast<uint4*>(Ks + swo<NCH>(r, c)) = kv[it];
+        *reinterpret_cast<uint4*>(Vs + swo<NCH>(r, c)) = vv[it];
       }
     }
   }
@@ -207,6 +220,9 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const uint16_t* __rest
 
   const float sl2 = scale * LOG2E;
   const int NTv = (S + 15) >> 4;
+  // per-lane swizzled offsets within 16- / 32-row blocks; the other column blocks XOR into the
+  // chunk bits and rows r and r + 16 share a swizzle (aswz reads row bits 1-3): two registers
+  const int of0 = swo<NCH>(l16, 8 * g), ot0 = swo<NCH>(4 * g + (l16 >> 2), 4 * (l16 & 3));
 #pragma unroll
   for (int it = 0; it < NQW; ++it) {
     const int qt = wave + 4 * it;
@@ -217,15 +233,15 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const uint16_t* __rest
     for (int kt = 0; kt < NT; ++kt) {
       f32x4_t acc = qk_init<NT, EX>(kt, g, S);
 #pragma unroll
-      for (int kk = 0; kk < KK; ++kk) acc = mfma(ld8(Ks + (kt * 16 + l16) * KS + 32 * kk + 8 * g), qpre[it][kk], acc);
+      for (int kk = 0; kk < KK; ++kk) acc = mfma(ld8(Ks + kt * 16 * HD + (of0 ^ (kk << 5))), qpre[it][kk], acc);
       sc[kt] = acc;
     }
     f32x4_t oacc[DT];
     float ms, l;
     softmax_pv(sc, sl2,
                [&](int s, int dt) {
-                 const uint16_t* vr = Vs + (32 * s + 4 * g + (l16 >> 2)) * KS + dt * 16 + 4 * (l16 & 3);
-                 return cat44(tr4(vr), tr4(vr + 16 * KS));
+                 const uint16_t* vr = Vs + 32 * s * HD + (ot0 ^ (dt << 4));
+                 return cat44(tr4(vr), tr4(vr + 16 * HD));
                },
                oacc, ms, l);
     if (q < S) {
@@ -248,11 +264,10 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const uint16_t* __rest
 // MFMA / softmax work (the one-pair kernel stalls on every load phase); Q fragments of the next
 // query tile are prefetched the same way.
 template <int HD, int SP, bool EX = false>
-__global__ __launch_bounds__(256, 2) void attn_fwd_ml_kernel(const uint16_t* __restrict__ qkv, uint16_t* __restrict__ o,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SP <= 64 ? 5 : 2))) void attn_fwd_ml_kernel(const uint16_t* __restrict__ qkv, uint16_t* __restrict__ o,
                                                           float* __restrict__ lse, int S, int H, int BH, int hpw,
                                                           float scale) {
   JM_DGUARD(S >= 1 && S <= SP && hpw >= 1 && blockDim.x == 256);
-  constexpr int KS = HD + 8;
   constexpr int NT = SP / 16;
   constexpr int KK = HD / 32;
   constexpr int DT = HD / 16;
@@ -260,7 +275,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_ml_kernel(const uint16_t* __r
   constexpr int LPT = (SP * CPR + 255) / 256;
   extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
   uint16_t* Ks = smem;
-  uint16_t* Vt = smem + SP * KS;
+  uint16_t* Vt = smem + SP * HD;
   const long ts = 3L * H * HD;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int l16 = lane & 15, g = lane >> 4;
@@ -288,8 +303,8 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_ml_kernel(const uint16_t* __r
       const int i = threadIdx.x + 256 * j;
       const int r = i / CPR, c = (i % CPR) * 8;
       if (i < SP * CPR) {
-        *reinterpret_cast<uint4*>(Ks + r * KS + c) = kr[j];
-        *reinterpret_cast<uint4*>(Vt + r * KS + c) = vr[j];
+        *reinterpret_cast<uint4*>(Ks + swo<CPR>(r, c)) = kr[j];
+        *reinterpret_cast<uint4*>(Vt + swo<CPR>(r, c)) = vr[j];
       }
     }
   };
@@ -306,6 +321,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_ml_kernel(const uint16_t* __r
     }
   };
 
+  const int of0 = swo<CPR>(l16, 8 * g), ot0 = swo<CPR>(4 * g + (l16 >> 2), 4 * (l16 & 3));  // see attn_fwd_kernel
   const int bh0 = xcd_bid() * hpw;
   load(bh0);
   for (int j = 0; j < hpw; ++j) {
@@ -330,15 +346,15 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_ml_kernel(const uint16_t* __r
       for (int kt = 0; kt < NT; ++kt) {
         f32x4_t acc = qk_init<NT, EX>(kt, g, S);
 #pragma unroll
-        for (int kk = 0; kk < KK; ++kk) acc = mfma(ld8(Ks + (kt * 16 + l16) * KS + 32 * kk + 8 * g), qf[kk], acc);
+        for (int kk = 0; kk < KK; ++kk) acc = mfma(ld8(Ks + kt * 16 * HD + (of0 ^ (kk << 5))), qf[kk], acc);
         sc[kt] = acc;
       }
       f32x4_t oacc[DT];
       float ms, l;
       softmax_pv(sc, sl2,
                  [&](int s, int dt) {
-                   const uint16_t* vr2 = Vt + (32 * s + 4 * g + (l16 >> 2)) * KS + dt * 16 + 4 * (l16 & 3);
-                   return cat44(tr4(vr2), tr4(vr2 + 16 * KS));
+                   const uint16_t* vr2 = Vt + 32 * s * HD + (ot0 ^ (dt << 4));
+                   return cat44(tr4(vr2), tr4(vr2 + 16 * HD));
                  },
                  oacc, ms, l);
       if (q < S) {
@@ -369,16 +385,6 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_ml_kernel(const uint16_t* __r
 //  * dS is stored TRANSPOSED ([key][64 queries], same swizzle): one ds_write_b64 of 4 consecutive
 //    queries per lane instead of four 2-byte stores, read back for dQ with the transposing read.
 // 4 waves, 64-query chunks, one 16-query dQ tile per wave per chunk.
-JM_DEVICE int aswz(int row) {
-  return ((row >> 2) & 1) | ((((row >> 2) ^ (row >> 3)) & 1) << 1) | (((row >> 1) & 1) << 2);
-}
-
-// element offset of (row, col) in a swizzled image of NCH 16-byte chunks per row
-template <int NCH>
-JM_DEVICE int swo(int row, int col) {
-  return row * (NCH * 8) + ((((col >> 3) ^ aswz(row)) & (NCH - 1)) << 3) + (col & 7);
-}
-
 template <int HD, int SP, int QC = 64>
 constexpr size_t bwd2_smem() {
   return (size_t)(3 * SP * HD + SP * QC) * 2 + (2 * SP + (QC / 16) * 3 * HD) * sizeof(float);
@@ -1006,9 +1012,9 @@ __global__ __launch_bounds__(64 * NWV, 2) void attn_bwd3_kernel(const uint16_t* 
   }
 }
 
-// forward images: row-major Q and V (V^T operands through ds_read_b64_tr_b16)
+// forward images: row-major K and V, XOR-swizzled (V^T operands through ds_read_b64_tr_b16)
 template <int HD, int SP>
-size_t fwd_smem() { return (size_t)(2 * SP * (HD + 8)) * 2; }
+size_t fwd_smem() { return (size_t)(2 * SP * HD) * 2; }
 
 // one (b, h) per workgroup (S > 64; the short encoder sequences take the multi-pair kernel)
 template <int HD, int SP>
