@@ -62,6 +62,9 @@ def main():
                     help="ZeRO-1: reduce-scatter + sharded optimizer + all-gather (default: all-reduce)")
     ap.add_argument("--profile-steps", type=int, default=0, help="extra steps under torch.profiler (debug)")
     ap.add_argument("--task", default="pretrain", choices=["pretrain", "finetune", "linear"])
+    ap.add_argument("--cls-global-batch", type=int, default=0,
+                    help="finetune / linear: images per step over the job; 0 = the reference preset "
+                         "(config/ft.sh 1024, LARS linear probe 16384), split over N GPUs (strong scaling)")
     ap.add_argument("--hip-graph", action="store_true",
                     help="replay the captured train step from a HIP graph (single process; runtime/graph.py)")
     ap.add_argument("--cpu", action="store_true",
@@ -242,9 +245,17 @@ def bench_classifier(args):
     dev = info.device
     world = info.world_size
     N = 1281167
+    strong = not args.batch_per_gpu
+    gb_ref = args.cls_global_batch or (1024 if args.task == "finetune" else 16384)
+    if strong and gb_ref % world:
+        raise SystemExit(f"global batch {gb_ref} is not divisible by {world} GPUs")
+    B = args.batch_per_gpu or gb_ref // world
+    gb = B * world
+    accum = -(-B // max(1, args.max_micro_batch))
+    while B % accum:
+        accum += 1
+    micro = B // accum
     if args.task == "finetune":
-        B = args.batch_per_gpu or 128
-        gb = B * world
         flags = ["--mode", "finetune", "--layers", "12", "--dim", "768", "--heads", "12", "--labels", "1000",
                  "--posemb", "sincos2d", "--droppath", "0.1", "--mixup", "0.8", "--cutmix", "1.0",
                  "--label-smoothing", "0.1", "--optimizer", "adamw", "--learning-rate", "3e-3",
@@ -252,8 +263,6 @@ def bench_classifier(args):
                  "--training-steps", str(N * 110 // 1024)]
         model_name, recipe = "vit_base_patch16 jumbo (3 CLS) finetune", "adamw llrd0.75 mixup0.8 cutmix1.0 ls0.1 dp0.1"
     else:
-        B = args.batch_per_gpu or 2048
-        gb = B * world
         flags = ["--mode", "linear", "--layers", "24", "--dim", "1024", "--heads", "16", "--labels", "1000",
                  "--posemb", "sincos2d", "--droppath", "0.0", "--mixup", "0.0", "--cutmix", "0.0",
                  "--label-smoothing", "0.0", "--optimizer", "lars", "--learning-rate", "0.1",
@@ -279,16 +288,16 @@ def bench_classifier(args):
     from jumbo_mae_tpu_amd.runtime.graph import StepRunner
     runner = StepRunner(trainer, hip_graph=args.hip_graph and world == 1)
     gen = torch.Generator(device=dev).manual_seed(1234 + info.rank)
-    pool = [(torch.randint(0, 256, (B, 3, 224, 224), dtype=torch.uint8, device=dev, generator=gen),
-             torch.randint(0, 1000, (B,), device=dev, generator=gen)) for _ in range(2)]
+    pool = [(torch.randint(0, 256, (micro, 3, 224, 224), dtype=torch.uint8, device=dev, generator=gen),
+             torch.randint(0, 1000, (micro,), device=dev, generator=gen)) for _ in range(2)]
     if info.is_main:
         log(f"[bench] task={args.task} params={model.store.num_params()/1e6:.1f}M "
-            f"trainable={model.store.num_params(True)/1e6:.2f}M world={world} batch/gpu={B}")
+            f"trainable={model.store.num_params(True)/1e6:.2f}M world={world} batch/gpu={B} = {accum} x {micro}")
     it = 0
 
     def step():
         nonlocal it
-        m = runner([pool[it % 2]])
+        m = runner([pool[(it + j) % 2] for j in range(accum)])
         it += 1
         return m
 
@@ -314,13 +323,14 @@ def bench_classifier(args):
             + " 224",
             "value": round(value, 2), "unit": "images/sec", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1000.0, 3),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "higher_is_better": True, "scaling": "strong" if strong else "weak", "vs_baseline": None,
             "mfu_bf16_dense": round(util, 4), "dtype": "bf16",
             "reducer": reducer.stats() if reducer is not None else None,
             "peak_hbm_gb": round(torch.cuda.max_memory_allocated(dev) / 2**30, 2),
             "data": "synthetic uint8 224x224 images + random labels on GPU, random-init weights",
             "config": {"model": model_name, "global_batch": gb, "seq_len": model.cfg.num_cls_tokens
                        + model.cfg.seq_patches, "parallelism": f"dp{world}", "per_gpu_batch": B,
+                       "micro_batch": micro, "grad_accum": accum,
                        "hip_graph": bool(runner.graphed is not None),
                        "recipe": recipe, "final_loss": round(float(m["loss"].item()), 5)},
         }), flush=True)

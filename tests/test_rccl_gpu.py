@@ -81,6 +81,15 @@ def test_rccl_finetune_matches_plain():
                   "vit_tiny_patch16", "--batch-per-gpu", "32", "--bucket-mb", "0.5"])
 
 
+@pytest.mark.gpu
+def test_rccl_finetune_accum_matches_plain():
+    """Classifier bench at a per-GPU batch above --max-micro-batch: accumulated micro-steps."""
+    plain, dp = _check_equal(["--task", "finetune", "--gpus", "1", "--steps", "2", "--warmup", "1", "--model",
+                              "vit_tiny_patch16", "--batch-per-gpu", "32", "--max-micro-batch", "16",
+                              "--bucket-mb", "0.5"])
+    assert dp["config"]["grad_accum"] == 2 and dp["config"]["micro_batch"] == 16, dp["config"]
+
+
 def test_forced_group_zero1_matches_plain_cpu():
     _check_equal(PRETRAIN[:-4] + ["--batch-per-gpu", "4", "--image-size", "64", "--bucket-mb", "0.5", "--cpu",
                                   "--shard-optimizer"])
