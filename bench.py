@@ -62,6 +62,8 @@ def main():
                     help="ZeRO-1: reduce-scatter + sharded optimizer + all-gather (default: all-reduce)")
     ap.add_argument("--profile-steps", type=int, default=0, help="extra steps under torch.profiler (debug)")
     ap.add_argument("--task", default="pretrain", choices=["pretrain", "finetune", "linear"])
+    ap.add_argument("--dropout", type=float, default=0.0,
+                    help="finetune: dropout rate of the attention / FF layers (config/ft.sh uses 0)")
     ap.add_argument("--cls-global-batch", type=int, default=0,
                     help="finetune / linear: images per step over the job; 0 = the reference preset "
                          "(config/ft.sh 1024, LARS linear probe 16384), split over N GPUs (strong scaling)")
@@ -257,11 +259,13 @@ def bench_classifier(args):
     micro = B // accum
     if args.task == "finetune":
         flags = ["--mode", "finetune", "--layers", "12", "--dim", "768", "--heads", "12", "--labels", "1000",
-                 "--posemb", "sincos2d", "--droppath", "0.1", "--mixup", "0.8", "--cutmix", "1.0",
+                 "--posemb", "sincos2d", "--droppath", "0.1", "--dropout", str(args.dropout),
+                 "--mixup", "0.8", "--cutmix", "1.0",
                  "--label-smoothing", "0.1", "--optimizer", "adamw", "--learning-rate", "3e-3",
                  "--weight-decay", "0.05", "--lr-decay", "0.75", "--warmup-steps", str(N * 10 // 1024),
                  "--training-steps", str(N * 110 // 1024)]
-        model_name, recipe = "vit_base_patch16 jumbo (3 CLS) finetune", "adamw llrd0.75 mixup0.8 cutmix1.0 ls0.1 dp0.1"
+        model_name = "vit_base_patch16 jumbo (3 CLS) finetune"
+        recipe = "adamw llrd0.75 mixup0.8 cutmix1.0 ls0.1 dp0.1" + (f" dropout{args.dropout}" if args.dropout else "")
     else:
         flags = ["--mode", "linear", "--layers", "24", "--dim", "1024", "--heads", "16", "--labels", "1000",
                  "--posemb", "sincos2d", "--droppath", "0.0", "--mixup", "0.0", "--cutmix", "0.0",

@@ -117,8 +117,31 @@ JM_DEVICE bf16x8_t bf16_ones() {
 // sc: raw S^T tiles (key on the lane group) of one query tile, NTv of them real; va(s, dt): the
 // V^T A operand of key pair s, d tile dt.  Returns O^T (unnormalised), ms = scaled row max (log2
 // domain) and l = row sum of the bf16 P.
-template <int NT, int DT, class VA>
-JM_DEVICE void softmax_pv(const f32x4_t (&sc)[NT], float sl2, VA&& va, f32x4_t (&oacc)[DT], float& ms, float& l) {
+// Attention-probability dropout (reference modeling.py:133): keep bit of P[b, h, q, k] from
+// common.h drop_keep at index ((b * H + h) * S + k) * SE + q, SE = S rounded up to even, so that
+// queries 2m, 2m + 1 of a key share one hash: the backward's lanes hold 4 consecutive queries of
+// one key (2 hashes per 4 scores), the forward's 4 keys of one query (4 hashes).  ops/dropout.py
+// keep_mask_rows mirrors it.  The row statistics (lse, row sum) are those of the undropped P; the
+// forward scales O by 1 / keep, the backward folds the mask into dP and P^T dO.
+struct AttnDrop {
+  const int64_t* seed;  // int64 [1] on the device; null: no dropout
+  uint32_t thr;         // round(keep * 65536)
+  float scale;          // 1 / keep
+};
+
+// keep bits of keys k0 .. k0 + 3 for one query: pair index jq + k * seh (jq = (b H + h) S seh +
+// q / 2, seh = SE / 2), half q & 1
+JM_DEVICE void keep4(uint64_t seed, uint32_t jq, uint32_t seh, int k0, int qodd, uint32_t thr, bool (&k)[4]) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) k[i] = drop_keep_half(drop_hash(jq + (uint32_t)(k0 + i) * seh, seed), qodd, thr);
+}
+
+// DROP: P.V uses the masked P (keys of pair s: 32 s + 4 g + i, 32 s + 16 + 4 g + i; keep4
+// arguments jq, seh, qodd); the row sum l stays the undropped one.
+template <int NT, int DT, bool DROP = false, class VA>
+JM_DEVICE void softmax_pv(const f32x4_t (&sc)[NT], float sl2, VA&& va, f32x4_t (&oacc)[DT], float& ms, float& l,
+                          uint64_t dseed = 0, uint32_t dthr = 0, uint32_t jq = 0, uint32_t seh = 0, int qodd = 0,
+                          int g = 0) {
   float m = -INFINITY;
 #pragma unroll
   for (int kt = 0; kt < NT; ++kt) {  // two v_max3 per tile
@@ -142,8 +165,23 @@ JM_DEVICE void softmax_pv(const f32x4_t (&sc)[NT], float sl2, VA&& va, f32x4_t (
     }
     const bf16x8_t pb = pack8(pf);
     lacc = mfma(ones, pb, lacc);
+    if constexpr (DROP) {
+      bool k0[4], k1[4];
+      keep4(dseed, jq, seh, 32 * s + 4 * g, qodd, dthr, k0);
+      keep4(dseed, jq, seh, 32 * s + 16 + 4 * g, qodd, dthr, k1);
+      float pd[8];
 #pragma unroll
-    for (int dt = 0; dt < DT; ++dt) oacc[dt] = mfma(va(s, dt), pb, oacc[dt]);
+      for (int i = 0; i < 4; ++i) {
+        pd[i] = k0[i] ? pf[i] : 0.f;
+        pd[4 + i] = k1[i] ? pf[4 + i] : 0.f;
+      }
+      const bf16x8_t pbd = pack8(pd);
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt) oacc[dt] = mfma(va(s, dt), pbd, oacc[dt]);
+    } else {
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt) oacc[dt] = mfma(va(s, dt), pb, oacc[dt]);
+    }
   }
   l = lacc[0];
 }
@@ -160,10 +198,11 @@ JM_DEVICE f32x4_t qk_init(int kt, int g, int S) {
 // One (b, h) per workgroup.  LDS holds row-major K and V images (V^T operands come out of the
 // transposing ds_read_b64_tr_b16); the Q fragments of every query tile of a wave and all of a
 // thread's K / V chunks are loaded up front, one HBM round trip instead of one per chunk.
-template <int HD, int SP, bool EX = false>
+template <int HD, int SP, bool EX = false, bool DROP = false>
 // waves per SIMD: the padded-row layout's occupancy, kept with the swizzled images
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HD == 64 && SP > 128 ? 4 : 2))) void attn_fwd_kernel(const uint16_t* __restrict__ qkv, uint16_t* __restrict__ o,
-                                                       float* __restrict__ lse, int S, int H, float scale) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HD == 64 && SP > 128 && !DROP ? 4 : 2))) void attn_fwd_kernel(const uint16_t* __restrict__ qkv, uint16_t* __restrict__ o,
+                                                       float* __restrict__ lse, int S, int H, float scale,
+                                                       AttnDrop drop) {
   JM_DGUARD(S >= 1 && S <= SP && blockDim.x == 256);
   constexpr int NT = SP / 16;
   constexpr int KK = HD / 32;
@@ -238,14 +277,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HD == 64 &&
     }
     f32x4_t oacc[DT];
     float ms, l;
-    softmax_pv(sc, sl2,
-               [&](int s, int dt) {
-                 const uint16_t* vr = Vs + 32 * s * HD + (ot0 ^ (dt << 4));
-                 return cat44(tr4(vr), tr4(vr + 16 * HD));
-               },
-               oacc, ms, l);
+    const uint32_t seh = (uint32_t)((S + 1) >> 1), jq = (uint32_t)(bh * S) * seh + (uint32_t)(q >> 1);
+    softmax_pv<NT, DT, DROP>(sc, sl2,
+                             [&](int s, int dt) {
+                               const uint16_t* vr = Vs + 32 * s * HD + (ot0 ^ (dt << 4));
+                               return cat44(tr4(vr), tr4(vr + 16 * HD));
+                             },
+                             oacc, ms, l, DROP ? (uint64_t)drop.seed[0] : 0, drop.thr, jq, seh, q & 1, g);
     if (q < S) {
-      const float inv = 1.f / l;
+      const float inv = (DROP ? drop.scale : 1.f) / l;
       uint16_t* orow = o + ((long)b * S + q) * H * HD + h * HD;
 #pragma unroll
       for (int dt = 0; dt < DT; ++dt) {
@@ -263,10 +303,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HD == 64 &&
 // the current pair's images are in LDS, so their HBM latency hides behind the current pair's
 // MFMA / softmax work (the one-pair kernel stalls on every load phase); Q fragments of the next
 // query tile are prefetched the same way.
-template <int HD, int SP, bool EX = false>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SP <= 64 ? 5 : 2))) void attn_fwd_ml_kernel(const uint16_t* __restrict__ qkv, uint16_t* __restrict__ o,
+template <int HD, int SP, bool EX = false, bool DROP = false>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SP <= 64 && !DROP ? 5 : 2))) void attn_fwd_ml_kernel(const uint16_t* __restrict__ qkv, uint16_t* __restrict__ o,
                                                           float* __restrict__ lse, int S, int H, int BH, int hpw,
-                                                          float scale) {
+                                                          float scale, AttnDrop drop) {
   JM_DGUARD(S >= 1 && S <= SP && hpw >= 1 && blockDim.x == 256);
   constexpr int NT = SP / 16;
   constexpr int KK = HD / 32;
@@ -351,14 +391,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SP <= 64 ? 
       }
       f32x4_t oacc[DT];
       float ms, l;
-      softmax_pv(sc, sl2,
-                 [&](int s, int dt) {
-                   const uint16_t* vr2 = Vt + 32 * s * HD + (ot0 ^ (dt << 4));
-                   return cat44(tr4(vr2), tr4(vr2 + 16 * HD));
-                 },
-                 oacc, ms, l);
+      const uint32_t seh = (uint32_t)((S + 1) >> 1), jq = (uint32_t)(bh * S) * seh + (uint32_t)(q >> 1);
+      softmax_pv<NT, DT, DROP>(sc, sl2,
+                               [&](int s, int dt) {
+                                 const uint16_t* vr2 = Vt + 32 * s * HD + (ot0 ^ (dt << 4));
+                                 return cat44(tr4(vr2), tr4(vr2 + 16 * HD));
+                               },
+                               oacc, ms, l, DROP ? (uint64_t)drop.seed[0] : 0, drop.thr, jq, seh, q & 1, g);
       if (q < S) {
-        const float inv = 1.f / l;
+        const float inv = (DROP ? drop.scale : 1.f) / l;
         uint16_t* orow = o + ((long)b * S + q) * H * HD + h * HD;
 #pragma unroll
         for (int dt = 0; dt < DT; ++dt) {
@@ -391,13 +432,13 @@ constexpr size_t bwd2_smem() {
 }
 
 
-template <int HD, int SP>
+template <int HD, int SP, bool DROP = false>
 __global__ __launch_bounds__(256, 2) void attn_bwd2_kernel(const uint16_t* __restrict__ qkv,
                                                         const uint16_t* __restrict__ o,
                                                         const uint16_t* __restrict__ dO,
                                                         const float* __restrict__ lse,
                                                         uint16_t* __restrict__ dqkv, int S, int H, float scale,
-                                                        float* __restrict__ dbp, int B, int ppw) {
+                                                        float* __restrict__ dbp, int B, int ppw, AttnDrop drop) {
   JM_DGUARD(S >= 1 && S <= SP && blockDim.x == 256 && ppw >= 1);
   constexpr int NW = 4, NTH = 256, QC = 64;
   constexpr int NT = SP / 16, KK = HD / 32, DT = HD / 16;
@@ -422,6 +463,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd2_kernel(const uint16_t* __res
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int l16 = lane & 15, g = lane >> 4;
   const float sl2 = scale * LOG2E;
+  const uint64_t dseed = DROP ? (uint64_t)drop.seed[0] : 0;
   // Every swizzled address below is (16-row-aligned base) + (per-lane constant): aswz depends on
   // row bits 1-3 only, and all bases are multiples of 16 rows.
   int o_frag[KK];  // fragment row l16, chunk 4kk + g
@@ -565,18 +607,32 @@ __global__ __launch_bounds__(256, 2) void attn_bwd2_kernel(const uint16_t* __res
             const float4 l4 = *reinterpret_cast<const float4*>(lse_s + q0 + 4 * g);
             const float4 d4 = *reinterpret_cast<const float4*>(delta_s + q0 + 4 * g);
             f32x4_t sacc = {l4.x + kneg, l4.y + kneg, l4.z + kneg, l4.w + kneg};
-            f32x4_t dp = {d4.x, d4.y, d4.z, d4.w};
+            f32x4_t dp = DROP ? f32x4_t{0.f, 0.f, 0.f, 0.f} : f32x4_t{d4.x, d4.y, d4.z, d4.w};
 #pragma unroll
             for (int kk = 0; kk < KK; ++kk) {
               sacc = mfma(ld8(Qs + q0 * HD + o_frag[kk]), kf[w][kk], sacc);
               dp = mfma(ld8(dOs + q0 * HD + o_frag[kk]), vf[w][kk], dp);
             }
             // sacc[i] = S[q = q0 + 4g + i][key] (log2 domain, minus lse)
+            const float nd[4] = {d4.x, d4.y, d4.z, d4.w};  // -delta
+            uint32_t dh[2] = {0u, 0u};  // one hash per query pair (q0 + 4g even)
+            if constexpr (DROP) {
+              const uint32_t seh = (uint32_t)((S + 1) >> 1);
+              const uint32_t jk = (uint32_t)((b * H + h) * S + kt * 16 + l16) * seh + (uint32_t)((q0 + 4 * g) >> 1);
+              dh[0] = drop_hash(jk, dseed);
+              dh[1] = drop_hash(jk + 1, dseed);
+            }
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
               const float p = __builtin_amdgcn_exp2f(sacc[i]);
-              pf[4 * half + i] = p;
-              df[4 * half + i] = p * dp[i];
+              if constexpr (DROP) {  // dS = P (M dP' / keep - delta); P^T dO uses M P (1 / keep at the end)
+                const bool kp = drop_keep_half(dh[i >> 1], i & 1, drop.thr);
+                pf[4 * half + i] = kp ? p : 0.f;
+                df[4 * half + i] = p * ((kp ? dp[i] * drop.scale : 0.f) + nd[i]);
+              } else {
+                pf[4 * half + i] = p;
+                df[4 * half + i] = p * dp[i];
+              }
             }
             uint2 pk;
             pk.x = pack_bf2(df[4 * half], df[4 * half + 1]);
@@ -651,7 +707,8 @@ __global__ __launch_bounds__(256, 2) void attn_bwd2_kernel(const uint16_t* __res
       for (int dt = 0; dt < DT; ++dt) {
         float kv[4] = {dkacc[w][dt][0] * LN2, dkacc[w][dt][1] * LN2, dkacc[w][dt][2] * LN2,
                        dkacc[w][dt][3] * LN2};  // Q staged times scale * log2(e)
-        float vv[4] = {dvacc[w][dt][0], dvacc[w][dt][1], dvacc[w][dt][2], dvacc[w][dt][3]};
+        const float vs = DROP ? drop.scale : 1.f;
+        float vv[4] = {dvacc[w][dt][0] * vs, dvacc[w][dt][1] * vs, dvacc[w][dt][2] * vs, dvacc[w][dt][3] * vs};
         store4(dKg + (long)key * ts + dt * 16 + 4 * g, kv);
         store4(dVg + (long)key * ts + dt * 16 + 4 * g, vv);
       }
@@ -681,7 +738,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd2_kernel(const uint16_t* __res
           const int d = dt * 16 + 4 * g + i;
           bw[d] = sq * scale;
           bw[HD + d] = sk * LN2;
-          bw[2 * HD + d] = sv;
+          bw[2 * HD + d] = DROP ? sv * drop.scale : sv;
         }
       }
     __syncthreads();
@@ -712,13 +769,13 @@ __global__ __launch_bounds__(256, 2) void attn_bwd2_kernel(const uint16_t* __res
 // NWV waves per workgroup: 4 (the default), or 8 for hd 64 at long S, where the 4-wave form needs
 // more than 256 VGPRs (one wave per SIMD): 8 waves own half the key tiles each (half the dK / dV
 // accumulators) and sweep 128-query chunks (one 16-query dQ tile per wave), two waves per SIMD.
-template <int HD, int SP, int NWV = 4>
+template <int HD, int SP, int NWV = 4, bool DROP = false>
 __global__ __launch_bounds__(64 * NWV, 2) void attn_bwd3_kernel(const uint16_t* __restrict__ qkv,
                                                         const uint16_t* __restrict__ o,
                                                         const uint16_t* __restrict__ dO,
                                                         const float* __restrict__ lse,
                                                         uint16_t* __restrict__ dqkv, int S, int H, float scale,
-                                                        float* __restrict__ dbp) {
+                                                        float* __restrict__ dbp, AttnDrop drop) {
   JM_DGUARD(S >= 1 && S <= SP && blockDim.x == 64 * NWV);
   constexpr int NW = NWV, NTH = 64 * NWV, QC = 16 * NWV;
   constexpr int QB = QC / 32;   // 32-query blocks per chunk
@@ -786,6 +843,7 @@ __global__ __launch_bounds__(64 * NWV, 2) void attn_bwd3_kernel(const uint16_t* 
   }
   for (int i = threadIdx.x; i < NW * 3 * HD; i += NTH) bsum[i] = 0.f;  // one slot per wave
   const float sl2 = scale * LOG2E;
+  const uint64_t dseed = DROP ? (uint64_t)drop.seed[0] : 0;
   if ((int)threadIdx.x < SP) lse_s[threadIdx.x] = nlse;
   __syncthreads();
 #pragma unroll
@@ -868,23 +926,41 @@ __global__ __launch_bounds__(64 * NWV, 2) void attn_bwd3_kernel(const uint16_t* 
             qf[hh][kk] = ld8(Qs + (qb + 16 * hh) * HD + o_frag[kk]);
             dof[hh][kk] = ld8(dOs + (qb + 16 * hh) * HD + o_frag[kk]);
           }
-          const float4 l4 = *reinterpret_cast<const float4*>(lse_s + qb + 16 * hh + 4 * g);
-          const float4 d4 = *reinterpret_cast<const float4*>(delta_s + qb + 16 * hh + 4 * g);
-          lv[hh] = f32x4_t{l4.x, l4.y, l4.z, l4.w};
-          dl[hh] = f32x4_t{d4.x, d4.y, d4.z, d4.w};
+          if constexpr (!(DROP && NWV == 8)) {
+            const float4 l4 = *reinterpret_cast<const float4*>(lse_s + qb + 16 * hh + 4 * g);
+            const float4 d4 = *reinterpret_cast<const float4*>(delta_s + qb + 16 * hh + 4 * g);
+            lv[hh] = f32x4_t{l4.x, l4.y, l4.z, l4.w};
+            dl[hh] = f32x4_t{d4.x, d4.y, d4.z, d4.w};
+          }
         }
+        // the transposed dO / Q operands of the dV / dK products: loaded once per block, or per
+        // key tile in the 8-wave dropout variant (whose mask work would otherwise spill)
+        constexpr bool TILE_AOP = DROP && NWV == 8;
+        auto load_aop = [&]() {
 #pragma unroll
-        for (int dt = 0; dt < DT; ++dt) {
-          a_do[dt] = cat44(tr4(dOs + qb * HD + o_tr[dt][0]), tr4(dOs + qb * HD + o_tr[dt][1]));
-          a_q[dt] = cat44(tr4(Qs + qb * HD + o_tr[dt][0]), tr4(Qs + qb * HD + o_tr[dt][1]));
-        }
+          for (int dt = 0; dt < DT; ++dt) {
+            a_do[dt] = cat44(tr4(dOs + qb * HD + o_tr[dt][0]), tr4(dOs + qb * HD + o_tr[dt][1]));
+            a_q[dt] = cat44(tr4(Qs + qb * HD + o_tr[dt][0]), tr4(Qs + qb * HD + o_tr[dt][1]));
+          }
+        };
+        if constexpr (!TILE_AOP) load_aop();
         // one key tile: S / dP products from the accumulator inits, softmax gradient, dV / dK
-        auto tile = [&](int w, int kt, const f32x4_t (&ini)[2]) {
-          f32x4_t sacc[2], dp[2];
+        // TILE_AOP: -lse / -delta re-read from LDS per tile too (kn: the padded-key init), so no
+        // per-block vectors stay live across the key tiles
+        auto tile = [&](int w, int kt, const f32x4_t (&ini)[2], float kn) {
+          f32x4_t sacc[2], dp[2], dlt[2];
 #pragma unroll
           for (int hh = 0; hh < 2; ++hh) {
-            sacc[hh] = ini[hh];
-            dp[hh] = dl[hh];
+            if constexpr (TILE_AOP) {
+              const float4 l4 = *reinterpret_cast<const float4*>(lse_s + qb + 16 * hh + 4 * g);
+              const float4 d4 = *reinterpret_cast<const float4*>(delta_s + qb + 16 * hh + 4 * g);
+              sacc[hh] = f32x4_t{l4.x + kn, l4.y + kn, l4.z + kn, l4.w + kn};
+              dlt[hh] = f32x4_t{d4.x, d4.y, d4.z, d4.w};
+            } else {
+              sacc[hh] = ini[hh];
+              dlt[hh] = dl[hh];
+            }
+            dp[hh] = DROP ? f32x4_t{0.f, 0.f, 0.f, 0.f} : dlt[hh];
 #pragma unroll
             for (int kk = 0; kk < KK; ++kk) {
               sacc[hh] = mfma(qf[hh][kk], kf[w][kk], sacc[hh]);
@@ -895,11 +971,24 @@ __global__ __launch_bounds__(64 * NWV, 2) void attn_bwd3_kernel(const uint16_t* 
           uint16_t* dsw = dSt + kt * 16 * QC;
 #pragma unroll
           for (int hh = 0; hh < 2; ++hh) {
+            uint32_t dh[2] = {0u, 0u};  // one hash per query pair (qb + 16 hh + 4 g even)
+            if constexpr (DROP) {
+              const uint32_t seh = (uint32_t)((S + 1) >> 1);
+              const uint32_t jk = (uint32_t)(bh * S + kt * 16 + l16) * seh + (uint32_t)((qb + 16 * hh + 4 * g) >> 1);
+              dh[0] = drop_hash(jk, dseed);
+              dh[1] = drop_hash(jk + 1, dseed);
+            }
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
               const float p = __builtin_amdgcn_exp2f(sacc[hh][i]);
-              pf[4 * hh + i] = p;
-              df[4 * hh + i] = p * dp[hh][i];
+              if constexpr (DROP) {  // dS = P (M dP' / keep - delta); P^T dO uses M P (1 / keep at the end)
+                const bool kp = drop_keep_half(dh[i >> 1], i & 1, drop.thr);
+                pf[4 * hh + i] = kp ? p : 0.f;
+                df[4 * hh + i] = p * ((kp ? dp[hh][i] * drop.scale : 0.f) + dlt[hh][i]);
+              } else {
+                pf[4 * hh + i] = p;
+                df[4 * hh + i] = p * dp[hh][i];
+              }
             }
             uint2 pk;
             pk.x = pack_bf2(df[4 * hh], df[4 * hh + 1]);
@@ -908,6 +997,7 @@ __global__ __launch_bounds__(64 * NWV, 2) void attn_bwd3_kernel(const uint16_t* 
           }
           const bf16x8_t pb = pack8(pf);
           const bf16x8_t dsb = pack8(df);
+          if constexpr (TILE_AOP) load_aop();
 #pragma unroll
           for (int dt = 0; dt < DT; ++dt) {
             dvacc[w][dt] = mfma(a_do[dt], pb, dvacc[w][dt]);
@@ -918,11 +1008,15 @@ __global__ __launch_bounds__(64 * NWV, 2) void attn_bwd3_kernel(const uint16_t* 
         for (int w = 0; w < NKW; ++w) {
           const int kt = wave + NW * w;
           if (kt * 16 + 16 <= S) {
-            tile(w, kt, lv);
+            tile(w, kt, lv, 0.f);
           } else if (kt < NT) {  // the tile holding padded keys (wave-uniform branch)
             asm volatile("" ::: "memory");  // keeps the two paths apart: no per-tile selects
-            const f32x4_t lm[2] = {lv[0] + kneg[w], lv[1] + kneg[w]};
-            tile(w, kt, lm);
+            if constexpr (TILE_AOP) {
+              tile(w, kt, lv, kneg[w]);
+            } else {
+              const f32x4_t lm[2] = {lv[0] + kneg[w], lv[1] + kneg[w]};
+              tile(w, kt, lm, 0.f);
+            }
           }
         }
       }
@@ -975,7 +1069,8 @@ __global__ __launch_bounds__(64 * NWV, 2) void attn_bwd3_kernel(const uint16_t* 
       for (int dt = 0; dt < DT; ++dt) {
         float kv2[4] = {dkacc[w][dt][0] * LN2, dkacc[w][dt][1] * LN2, dkacc[w][dt][2] * LN2,
                         dkacc[w][dt][3] * LN2};
-        float vv[4] = {dvacc[w][dt][0], dvacc[w][dt][1], dvacc[w][dt][2], dvacc[w][dt][3]};
+        const float vs = DROP ? drop.scale : 1.f;
+        float vv[4] = {dvacc[w][dt][0] * vs, dvacc[w][dt][1] * vs, dvacc[w][dt][2] * vs, dvacc[w][dt][3] * vs};
         store4(dKg + (long)key * ts + dt * 16 + 4 * g, kv2);
         store4(dVg + (long)key * ts + dt * 16 + 4 * g, vv);
       }
@@ -998,7 +1093,7 @@ __global__ __launch_bounds__(64 * NWV, 2) void attn_bwd3_kernel(const uint16_t* 
           float* bw = bsum + wave * 3 * HD;
           const int d = dt * 16 + 4 * g + i;
           bw[HD + d] = sk * LN2;
-          bw[2 * HD + d] = sv;
+          bw[2 * HD + d] = DROP ? sv * drop.scale : sv;
         }
       }
     __syncthreads();
@@ -1017,27 +1112,28 @@ template <int HD, int SP>
 size_t fwd_smem() { return (size_t)(2 * SP * HD) * 2; }
 
 // one (b, h) per workgroup (S > 64; the short encoder sequences take the multi-pair kernel)
-template <int HD, int SP>
-int run_fwd(const uint16_t* qkv, uint16_t* out, float* lse_out, int B, int S, int H, float scale, hipStream_t st) {
+template <int HD, int SP, bool DROP>
+int run_fwd(const uint16_t* qkv, uint16_t* out, float* lse_out, int B, int S, int H, float scale, AttnDrop dr,
+            hipStream_t st) {
   dim3 grid(B * H);
   const size_t sm = fwd_smem<HD, SP>();
   if (sm > 160 * 1024) return -3;
   if (S > SP - 32) {
     static bool attr_ex = false;
     if (sm > 64 * 1024 && !attr_ex) {
-      (void)hipFuncSetAttribute((const void*)attn_fwd_kernel<HD, SP, true>,
+      (void)hipFuncSetAttribute((const void*)attn_fwd_kernel<HD, SP, true, DROP>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
       attr_ex = true;
     }
-    attn_fwd_kernel<HD, SP, true><<<grid, 256, sm, st>>>(qkv, out, lse_out, S, H, scale);
+    attn_fwd_kernel<HD, SP, true, DROP><<<grid, 256, sm, st>>>(qkv, out, lse_out, S, H, scale, dr);
   } else {
     static bool attr = false;
     if (sm > 64 * 1024 && !attr) {
-      (void)hipFuncSetAttribute((const void*)attn_fwd_kernel<HD, SP>, hipFuncAttributeMaxDynamicSharedMemorySize,
+      (void)hipFuncSetAttribute((const void*)attn_fwd_kernel<HD, SP, false, DROP>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)sm);
       attr = true;
     }
-    attn_fwd_kernel<HD, SP><<<grid, 256, sm, st>>>(qkv, out, lse_out, S, H, scale);
+    attn_fwd_kernel<HD, SP, false, DROP><<<grid, 256, sm, st>>>(qkv, out, lse_out, S, H, scale, dr);
   }
   return 0;
 }
@@ -1052,38 +1148,38 @@ bool uses_bwd3(int S, int hd) { return hd == 32 || (hd == 64 && S > 64); }
 // ViT-L encoder (S 52): 160 -> 140 us at 8 batch elements per bwd2 workgroup (profiles/r1_attn_bwd_ppw.txt)
 constexpr int BWD2_PPW = 8;
 
-template <int HD, int SP>
+template <int HD, int SP, bool DROP>
 int run_bwd(const uint16_t* qkv, const uint16_t* o, const uint16_t* dO, const float* lse_in, uint16_t* out,
-            float* dbias_part, int B, int S, int H, float scale, hipStream_t st) {
+            float* dbias_part, int B, int S, int H, float scale, AttnDrop dr, hipStream_t st) {
   if constexpr (HD == 64 && SP > 64) {
     constexpr size_t sm8 = bwd2_smem<HD, SP, 128>();
     static_assert(sm8 <= 160 * 1024, "8-wave backward LDS");
     static bool attr8 = false;
     if (!attr8) {
-      (void)hipFuncSetAttribute((const void*)attn_bwd3_kernel<HD, SP, 8>, hipFuncAttributeMaxDynamicSharedMemorySize,
+      (void)hipFuncSetAttribute((const void*)attn_bwd3_kernel<HD, SP, 8, DROP>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)sm8);
       attr8 = true;
     }
-    attn_bwd3_kernel<HD, SP, 8><<<dim3(B * H), 512, sm8, st>>>(qkv, o, dO, lse_in, out, S, H, scale, dbias_part);
+    attn_bwd3_kernel<HD, SP, 8, DROP><<<dim3(B * H), 512, sm8, st>>>(qkv, o, dO, lse_in, out, S, H, scale, dbias_part, dr);
   } else {
     constexpr size_t sm = bwd2_smem<HD, SP>();
     static_assert(sm <= 160 * 1024, "backward LDS");
     static bool attr = false;
     if constexpr (HD == 32) {
       if (sm > 64 * 1024 && !attr) {
-        (void)hipFuncSetAttribute((const void*)attn_bwd3_kernel<HD, SP>, hipFuncAttributeMaxDynamicSharedMemorySize,
+        (void)hipFuncSetAttribute((const void*)attn_bwd3_kernel<HD, SP, 4, DROP>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   (int)sm);
         attr = true;
       }
-      attn_bwd3_kernel<HD, SP><<<dim3(B * H), 256, sm, st>>>(qkv, o, dO, lse_in, out, S, H, scale, dbias_part);
+      attn_bwd3_kernel<HD, SP, 4, DROP><<<dim3(B * H), 256, sm, st>>>(qkv, o, dO, lse_in, out, S, H, scale, dbias_part, dr);
     } else {
       if (sm > 64 * 1024 && !attr) {
-        (void)hipFuncSetAttribute((const void*)attn_bwd2_kernel<HD, SP>, hipFuncAttributeMaxDynamicSharedMemorySize,
+        (void)hipFuncSetAttribute((const void*)attn_bwd2_kernel<HD, SP, DROP>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   (int)sm);
         attr = true;
       }
-      attn_bwd2_kernel<HD, SP><<<dim3(((B + BWD2_PPW - 1) / BWD2_PPW) * H), 256, sm, st>>>(
-          qkv, o, dO, lse_in, out, S, H, scale, dbias_part, B, BWD2_PPW);
+      attn_bwd2_kernel<HD, SP, DROP><<<dim3(((B + BWD2_PPW - 1) / BWD2_PPW) * H), 256, sm, st>>>(
+          qkv, o, dO, lse_in, out, S, H, scale, dbias_part, B, BWD2_PPW, dr);
     }
   }
   return 0;
@@ -1094,12 +1190,13 @@ int run_bwd(const uint16_t* qkv, const uint16_t* o, const uint16_t* dO, const fl
 // cost an occupancy step (199 -> 215 us; profiles/r1_attn_fwd_ml.txt)
 constexpr int FWD_ML_PAIRS = 4;
 
-template <int HD, int SP>
-int run_fwd_ml(const uint16_t* qkv, uint16_t* out, float* lse_out, int B, int S, int H, float scale, hipStream_t st) {
+template <int HD, int SP, bool DROP>
+int run_fwd_ml(const uint16_t* qkv, uint16_t* out, float* lse_out, int B, int S, int H, float scale, AttnDrop dr,
+               hipStream_t st) {
   const size_t sm = fwd_smem<HD, SP>();
   static bool attr_set[2] = {false, false};
   const bool ex = S > SP - 32;
-  const void* fn = ex ? (const void*)attn_fwd_ml_kernel<HD, SP, true> : (const void*)attn_fwd_ml_kernel<HD, SP>;
+  const void* fn = ex ? (const void*)attn_fwd_ml_kernel<HD, SP, true, DROP> : (const void*)attn_fwd_ml_kernel<HD, SP, false, DROP>;
   if (sm > 64 * 1024 && !attr_set[ex]) {
     (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
     attr_set[ex] = true;
@@ -1107,27 +1204,32 @@ int run_fwd_ml(const uint16_t* qkv, uint16_t* out, float* lse_out, int B, int S,
   const int BH = B * H;
   const int grid = (BH + FWD_ML_PAIRS - 1) / FWD_ML_PAIRS;
   if (ex)
-    attn_fwd_ml_kernel<HD, SP, true><<<grid, 256, sm, st>>>(qkv, out, lse_out, S, H, BH, FWD_ML_PAIRS, scale);
+    attn_fwd_ml_kernel<HD, SP, true, DROP><<<grid, 256, sm, st>>>(qkv, out, lse_out, S, H, BH, FWD_ML_PAIRS, scale, dr);
   else
-    attn_fwd_ml_kernel<HD, SP><<<grid, 256, sm, st>>>(qkv, out, lse_out, S, H, BH, FWD_ML_PAIRS, scale);
+    attn_fwd_ml_kernel<HD, SP, false, DROP><<<grid, 256, sm, st>>>(qkv, out, lse_out, S, H, BH, FWD_ML_PAIRS, scale, dr);
   return 0;
 }
 
 template <int HD, int SP>
 int run(bool fwd, const uint16_t* qkv, const uint16_t* o, const uint16_t* dO, const float* lse_in, uint16_t* out,
-        float* lse_out, int B, int S, int H, float scale, hipStream_t st) {
-  if (!fwd) return run_bwd<HD, SP>(qkv, o, dO, lse_in, out, lse_out, B, S, H, scale, st);
-  if constexpr (SP <= 64) return run_fwd_ml<HD, SP>(qkv, out, lse_out, B, S, H, scale, st);
-  return run_fwd<HD, SP>(qkv, out, lse_out, B, S, H, scale, st);
+        float* lse_out, int B, int S, int H, float scale, AttnDrop dr, hipStream_t st) {
+  if (dr.seed != nullptr) {
+    if (!fwd) return run_bwd<HD, SP, true>(qkv, o, dO, lse_in, out, lse_out, B, S, H, scale, dr, st);
+    if constexpr (SP <= 64) return run_fwd_ml<HD, SP, true>(qkv, out, lse_out, B, S, H, scale, dr, st);
+    return run_fwd<HD, SP, true>(qkv, out, lse_out, B, S, H, scale, dr, st);
+  }
+  if (!fwd) return run_bwd<HD, SP, false>(qkv, o, dO, lse_in, out, lse_out, B, S, H, scale, dr, st);
+  if constexpr (SP <= 64) return run_fwd_ml<HD, SP, false>(qkv, out, lse_out, B, S, H, scale, dr, st);
+  return run_fwd<HD, SP, false>(qkv, out, lse_out, B, S, H, scale, dr, st);
 }
 
 template <int HD>
 int dispatch_sp(bool fwd, const uint16_t* qkv, const uint16_t* o, const uint16_t* dO, const float* lse_in,
-                uint16_t* out, float* lse_out, int B, int S, int H, float scale, hipStream_t st) {
-  if (S <= 32) return run<HD, 32>(fwd, qkv, o, dO, lse_in, out, lse_out, B, S, H, scale, st);
-  if (S <= 64) return run<HD, 64>(fwd, qkv, o, dO, lse_in, out, lse_out, B, S, H, scale, st);
-  if (S <= 128) return run<HD, 128>(fwd, qkv, o, dO, lse_in, out, lse_out, B, S, H, scale, st);
-  if (S <= 224) return run<HD, 224>(fwd, qkv, o, dO, lse_in, out, lse_out, B, S, H, scale, st);
+                uint16_t* out, float* lse_out, int B, int S, int H, float scale, AttnDrop dr, hipStream_t st) {
+  if (S <= 32) return run<HD, 32>(fwd, qkv, o, dO, lse_in, out, lse_out, B, S, H, scale, dr, st);
+  if (S <= 64) return run<HD, 64>(fwd, qkv, o, dO, lse_in, out, lse_out, B, S, H, scale, dr, st);
+  if (S <= 128) return run<HD, 128>(fwd, qkv, o, dO, lse_in, out, lse_out, B, S, H, scale, dr, st);
+  if (S <= 224) return run<HD, 224>(fwd, qkv, o, dO, lse_in, out, lse_out, B, S, H, scale, dr, st);
   return -2;
 }
 
@@ -1505,24 +1607,31 @@ int jm_attn_bwd_part_rows(int B, int S, int hd) {
   return (B + BWD2_PPW - 1) / BWD2_PPW;
 }
 
-int jm_attn_fwd(const uint16_t* qkv, uint16_t* o, float* lse, int B, int S, int H, int hd, hipStream_t st) {
+// dseed (int64 [1] on the device) non-null: dropout on the attention probabilities with keep
+// threshold dthr = round(keep * 65536) and dscale = 1 / keep (whole-sequence kernels, S <= 224)
+int jm_attn_fwd(const uint16_t* qkv, uint16_t* o, float* lse, int B, int S, int H, int hd, const int64_t* dseed,
+                uint32_t dthr, float dscale, hipStream_t st) {
   const float scale = 1.f / sqrtf((float)hd);
+  const AttnDrop dr{dseed, dthr, dscale};
   if (S > jm_attn_max_seq()) {
+    if (dseed != nullptr) return -5;
     if (hd == 32) return run_long_fwd<32>(qkv, o, lse, B, S, H, scale, st);
     if (hd == 64) return run_long_fwd<64>(qkv, o, lse, B, S, H, scale, st);
     return -1;
   }
-  if (hd == 32) return dispatch_sp<32>(true, qkv, nullptr, nullptr, nullptr, o, lse, B, S, H, scale, st);
-  if (hd == 64) return dispatch_sp<64>(true, qkv, nullptr, nullptr, nullptr, o, lse, B, S, H, scale, st);
+  if (hd == 32) return dispatch_sp<32>(true, qkv, nullptr, nullptr, nullptr, o, lse, B, S, H, scale, dr, st);
+  if (hd == 64) return dispatch_sp<64>(true, qkv, nullptr, nullptr, nullptr, o, lse, B, S, H, scale, dr, st);
   return -1;
 }
 
 // dbias_part: optional [B][3*H*hd] fp32 per-sample column sums of dqkv (see attn_bwd_kernel)
 int jm_attn_bwd(const uint16_t* qkv, const uint16_t* o, const uint16_t* dO, const float* lse, uint16_t* dqkv, int B,
-                int S, int H, int hd, float* dbias_part, hipStream_t st) {
+                int S, int H, int hd, float* dbias_part, const int64_t* dseed, uint32_t dthr, float dscale,
+                hipStream_t st) {
   const float scale = 1.f / sqrtf((float)hd);
-  if (hd == 32) return dispatch_sp<32>(false, qkv, o, dO, lse, dqkv, dbias_part, B, S, H, scale, st);
-  if (hd == 64) return dispatch_sp<64>(false, qkv, o, dO, lse, dqkv, dbias_part, B, S, H, scale, st);
+  const AttnDrop dr{dseed, dthr, dscale};
+  if (hd == 32) return dispatch_sp<32>(false, qkv, o, dO, lse, dqkv, dbias_part, B, S, H, scale, dr, st);
+  if (hd == 64) return dispatch_sp<64>(false, qkv, o, dO, lse, dqkv, dbias_part, B, S, H, scale, dr, st);
   return -1;
 }
 

@@ -22,6 +22,8 @@ int jm_debug_line_attention();
 int jm_debug_line_dropout();
 int jm_dropout_apply(const void* x, void* y, long n, int bf16, const int64_t* seed, uint32_t thr, float scale,
                      hipStream_t st);
+int jm_gelu_drop(const uint16_t* h, uint16_t* g, uint16_t* gp, long n, const int64_t* seed, uint32_t thr, float scale,
+                 hipStream_t st);
 int jm_softmax_dropout_fwd(const float* z, float* p, float* pd, long rows, int S, const int64_t* seed, uint32_t thr,
                            float scale, hipStream_t st);
 int jm_softmax_dropout_bwd(const float* dpd, const float* p, float* dz, long rows, int S, const int64_t* seed,
@@ -49,9 +51,11 @@ int jm_residual_fwd(const float* x, long sB, long sT, int B, int T, int D, const
                     const float* mask, float* out, long oB, long oT, hipStream_t st);
 int jm_residual_bwd(const float* dout, long dB, long dT, const uint16_t* y, const float* scale, const float* mask,
                     float* dscale, uint16_t* dy, int B, int T, int D, float* dbias, long yB, long yT, hipStream_t st);
-int jm_attn_fwd(const uint16_t* qkv, uint16_t* o, float* lse, int B, int S, int H, int hd, hipStream_t st);
+int jm_attn_fwd(const uint16_t* qkv, uint16_t* o, float* lse, int B, int S, int H, int hd, const int64_t* dseed,
+                uint32_t dthr, float dscale, hipStream_t st);
 int jm_attn_bwd(const uint16_t* qkv, const uint16_t* o, const uint16_t* dO, const float* lse, uint16_t* dqkv, int B,
-                int S, int H, int hd, float* dbias_part, hipStream_t st);
+                int S, int H, int hd, float* dbias_part, const int64_t* dseed, uint32_t dthr, float dscale,
+                hipStream_t st);
 int jm_attn_max_seq();
 int jm_attn_bwd_part_rows(int B, int S, int hd);
 int jm_attn_bwd_long(const uint16_t* qkv, const uint16_t* o, const uint16_t* dO, const float* lse, uint16_t* dqkv,
@@ -345,21 +349,48 @@ torch::Tensor residual_bwd(torch::Tensor dout, c10::optional<torch::Tensor> y, c
 }
 
 // ------------------------------------------------------------------------------ attention
-std::vector<torch::Tensor> attn_fwd(torch::Tensor qkv, int64_t heads) {
+// dropout: keep threshold on 16 hash bits (common.h drop_keep) and the 1/keep scale of a drop
+// rate in [0, 1)
+static std::pair<uint32_t, float> keep_params(double rate) {
+  TORCH_CHECK(rate >= 0.0 && rate < 1.0, "dropout rate must be in [0, 1)");
+  const double keep = 1.0 - rate;
+  return {(uint32_t)std::llround(keep * 65536.0), (float)(1.0 / keep)};
+}
+
+static void check_seed(const torch::Tensor& seed, const torch::Tensor& like) {
+  TORCH_CHECK(seed.scalar_type() == torch::kInt64 && seed.numel() == 1 && seed.device() == like.device(),
+              "dropout seed: int64 [1] on the data's device");
+}
+
+// seed (int64 [1] on the device) with rate > 0: dropout on the attention probabilities (mask:
+// common.h drop_keep at ((b H + h) S + q) SE + k, the backward regenerates it from the same seed)
+static std::tuple<const int64_t*, uint32_t, float> attn_drop(const c10::optional<torch::Tensor>& seed, double rate,
+                                                             const torch::Tensor& like, int S) {
+  if (!seed.has_value() || !seed->defined() || rate <= 0.0) return {nullptr, 0u, 1.f};
+  check_seed(*seed, like);
+  TORCH_CHECK(S <= jm_attn_max_seq(), "attention dropout: S <= ", jm_attn_max_seq(), " (whole-sequence kernels)");
+  const auto kp = keep_params(rate);
+  return {seed->data_ptr<int64_t>(), kp.first, kp.second};
+}
+
+std::vector<torch::Tensor> attn_fwd(torch::Tensor qkv, int64_t heads, c10::optional<torch::Tensor> seed, double rate) {
   CHECK_CONTIG(qkv);
   CHECK_DT(qkv, torch::kBFloat16);
   const int B = qkv.size(0), S = qkv.size(1), D3 = qkv.size(2);
   const int D = D3 / 3, hd = D / heads;
   auto o = torch::empty({B, S, D}, qkv.options());
   auto lse = torch::empty({B, (long)heads, S}, qkv.options().dtype(torch::kFloat32));
-  check_rc(jm_attn_fwd(bf(qkv), bfm(o), lse.data_ptr<float>(), B, S, heads, hd, stream()), "attn_fwd");
+  const auto dr = attn_drop(seed, rate, qkv, S);
+  check_rc(jm_attn_fwd(bf(qkv), bfm(o), lse.data_ptr<float>(), B, S, heads, hd, std::get<0>(dr), std::get<1>(dr),
+                       std::get<2>(dr), stream()),
+           "attn_fwd");
   return {o, lse};
 }
 
 // dbias (optional, fp32 [3D]) += column sums of dqkv (the QKV Dense bias gradient), taken from
 // the kernel's fp32 accumulators as per-sample partials and reduced here.
 torch::Tensor attn_bwd(torch::Tensor dO, torch::Tensor qkv, torch::Tensor o, torch::Tensor lse, int64_t heads,
-                       c10::optional<torch::Tensor> dbias) {
+                       c10::optional<torch::Tensor> dbias, c10::optional<torch::Tensor> seed, double rate) {
   CHECK_CONTIG(dO);
   CHECK_CONTIG(qkv);
   CHECK_CONTIG(o);
@@ -367,6 +398,7 @@ torch::Tensor attn_bwd(torch::Tensor dO, torch::Tensor qkv, torch::Tensor o, tor
   const int B = qkv.size(0), S = qkv.size(1), D3 = qkv.size(2);
   const int D = D3 / 3, hd = D / heads;
   auto dqkv = torch::empty_like(qkv);
+  const auto dr = attn_drop(seed, rate, qkv, S);
   if (S > jm_attn_max_seq()) {  // tile-streamed kernels; the caller reduces the bias gradient
     TORCH_CHECK(!dbias, "attn_bwd: no fused bias gradient for S > ", jm_attn_max_seq());
     auto delta = torch::empty({B, (long)heads, S}, qkv.options().dtype(torch::kFloat32));
@@ -383,7 +415,8 @@ torch::Tensor attn_bwd(torch::Tensor dO, torch::Tensor qkv, torch::Tensor o, tor
     part = torch::empty({rows, D3}, qkv.options().dtype(torch::kFloat32));
   }
   float* pp = dbias ? part.data_ptr<float>() : nullptr;
-  check_rc(jm_attn_bwd(bf(qkv), bf(o), bf(dO), lse.data_ptr<float>(), bfm(dqkv), B, S, heads, hd, pp, stream()),
+  check_rc(jm_attn_bwd(bf(qkv), bf(o), bf(dO), lse.data_ptr<float>(), bfm(dqkv), B, S, heads, hd, pp, std::get<0>(dr),
+                       std::get<1>(dr), std::get<2>(dr), stream()),
            "attn_bwd");
   if (dbias) check_rc(jm_splitk_reduce_add(pp, dbias->data_ptr<float>(), D3, rows, stream()), "attn_bwd dbias");
   return dqkv;
@@ -746,17 +779,6 @@ torch::Tensor gemm_nt_dgelu(torch::Tensor A, torch::Tensor B, torch::Tensor pre,
 }
 
 // ---------------------------------------------------------------- dropout (csrc/dropout.hip)
-// keep threshold on the top 24 hash bits and the 1/keep scale of a drop rate in [0, 1)
-static std::pair<uint32_t, float> keep_params(double rate) {
-  TORCH_CHECK(rate >= 0.0 && rate < 1.0, "dropout rate must be in [0, 1)");
-  const double keep = 1.0 - rate;
-  return {(uint32_t)std::llround(keep * 16777216.0), (float)(1.0 / keep)};
-}
-
-static void check_seed(const torch::Tensor& seed, const torch::Tensor& like) {
-  TORCH_CHECK(seed.scalar_type() == torch::kInt64 && seed.numel() == 1 && seed.device() == like.device(),
-              "dropout seed: int64 [1] on the data's device");
-}
 
 // y = x * keep(seed, i) / keep  (bf16 or fp32, contiguous, numel % 8 == 0); also its own backward
 torch::Tensor dropout_apply(torch::Tensor x, torch::Tensor seed, double rate) {
@@ -773,6 +795,41 @@ torch::Tensor dropout_apply(torch::Tensor x, torch::Tensor seed, double rate) {
 }
 
 // rows of fp32 logits [..., S] -> (softmax p (saved for the backward), dropped p * mask / keep)
+// x *= keep(seed, i) / keep in place (bf16 or fp32, contiguous, numel % 8 == 0): the fused
+// blocks' Dense-output dropout (forward on the branch output, backward on its gradient)
+void dropout_apply_(torch::Tensor x, torch::Tensor seed, double rate) {
+  CHECK_CUDA(x);
+  check_seed(seed, x);
+  TORCH_CHECK(x.is_contiguous() && x.numel() % 8 == 0, "dropout_apply_: contiguous, numel % 8 == 0");
+  TORCH_CHECK(x.scalar_type() == torch::kBFloat16 || x.scalar_type() == torch::kFloat32, "dropout: bf16 / fp32");
+  const auto kp = keep_params(rate);
+  check_rc(jm_dropout_apply(x.data_ptr(), x.data_ptr(), x.numel(), x.scalar_type() == torch::kBFloat16,
+                            seed.data_ptr<int64_t>(), kp.first, kp.second, stream()),
+           "dropout_apply_");
+}
+
+// FF hidden dropout: (g, gp) masked in place (pair = the fused epilogue's gelu(h), gelu'(h)), or
+// from the pre-activation h: returns (gelu(h) m, gelu'(h) m)
+std::vector<torch::Tensor> gelu_drop(torch::Tensor a, c10::optional<torch::Tensor> b, torch::Tensor seed, double rate) {
+  CHECK_CONTIG(a);
+  CHECK_DT(a, torch::kBFloat16);
+  check_seed(seed, a);
+  TORCH_CHECK(a.numel() % 8 == 0, "gelu_drop: numel % 8");
+  const auto kp = keep_params(rate);
+  if (b.has_value() && b->defined()) {
+    CHECK_CONTIG((*b));
+    TORCH_CHECK(b->sizes() == a.sizes() && b->scalar_type() == torch::kBFloat16, "gelu_drop: (g, gp) pair");
+    check_rc(jm_gelu_drop(nullptr, bfm(a), bfm(*b), a.numel(), seed.data_ptr<int64_t>(), kp.first, kp.second,
+                          stream()),
+             "gelu_drop");
+    return {a, *b};
+  }
+  auto g = torch::empty_like(a), gp = torch::empty_like(a);
+  check_rc(jm_gelu_drop(bf(a), bfm(g), bfm(gp), a.numel(), seed.data_ptr<int64_t>(), kp.first, kp.second, stream()),
+           "gelu_drop");
+  return {g, gp};
+}
+
 std::vector<torch::Tensor> softmax_dropout_fwd(torch::Tensor z, torch::Tensor seed, double rate) {
   CHECK_CONTIG(z);
   CHECK_DT(z, torch::kFloat32);
@@ -1084,6 +1141,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("res_T0") = 0, py::arg("res_out") = py::none());
   m.def("gelu_fwd", &gelu_fwd);
   m.def("dropout_apply", &dropout_apply);
+  m.def("dropout_apply_", &dropout_apply_);
+  m.def("gelu_drop", &gelu_drop, py::arg("a"), py::arg("b") = py::none(), py::arg("seed"), py::arg("rate"));
   m.def("softmax_dropout_fwd", &softmax_dropout_fwd);
   m.def("softmax_dropout_bwd", &softmax_dropout_bwd);
   m.def("gelu_bwd", &gelu_bwd, py::arg("h"), py::arg("da"), py::arg("bias_grad") = py::none(),
@@ -1098,9 +1157,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("out") = py::none());
   m.def("residual_bwd", &residual_bwd, py::arg("dout"), py::arg("y"), py::arg("scale"), py::arg("mask"),
         py::arg("dscale"), py::arg("ydtype"), py::arg("dbias") = py::none(), py::arg("out") = py::none());
-  m.def("attn_fwd", &attn_fwd);
+  m.def("attn_fwd", &attn_fwd, py::arg("qkv"), py::arg("heads"), py::arg("seed") = py::none(), py::arg("rate") = 0.0);
   m.def("attn_bwd", &attn_bwd, py::arg("dO"), py::arg("qkv"), py::arg("o"), py::arg("lse"), py::arg("heads"),
-        py::arg("dbias") = py::none());
+        py::arg("dbias") = py::none(), py::arg("seed") = py::none(), py::arg("rate") = 0.0);
   m.def("attn_max_seq", &jm_attn_max_seq);
   m.def("gemm_tn_wgrad", &gemm_tn_wgrad, py::arg("dy"), py::arg("x"), py::arg("g"), py::arg("store") = false);
   m.def("gemm_tn_wgrad_seg", &gemm_tn_wgrad_seg, py::arg("dys"), py::arg("xs"), py::arg("g"), py::arg("store") = false);

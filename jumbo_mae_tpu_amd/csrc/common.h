@@ -17,6 +17,24 @@ constexpr int WAVE = 64;
 
 JM_DEVICE float bf2f(uint16_t v) { return __uint_as_float(((uint32_t)v) << 16); }
 
+// Dropout keep decisions, shared by every dropout site (dropout.hip, the attention kernels, the
+// GELU and residual kernels) and mirrored bit for bit by ops/dropout.py keep_mask.  Element idx
+// takes bits [16 * (idx & 1), +16) of ONE 32-bit hash per pair j = idx >> 1 (lowbias32 finalizer
+// of j + seed; j taken mod 2^32) and is kept iff they are below thr = round(keep * 65536).
+JM_DEVICE uint32_t drop_hash(uint32_t j, uint64_t seed) {
+  uint32_t x = (j + (uint32_t)seed) ^ (uint32_t)(seed >> 32);
+  x ^= x >> 16;
+  x *= 0x7feb352du;
+  x ^= x >> 15;
+  x *= 0x846ca68bu;
+  x ^= x >> 16;
+  return x;
+}
+JM_DEVICE bool drop_keep_half(uint32_t h, int odd, uint32_t thr) { return (odd ? (h >> 16) : (h & 0xffffu)) < thr; }
+JM_DEVICE bool drop_keep(uint64_t seed, uint64_t idx, uint32_t thr) {
+  return drop_keep_half(drop_hash((uint32_t)(idx >> 1), seed), (int)(idx & 1), thr);
+}
+
 JM_DEVICE uint16_t f2bf(float f) {
   // round-to-nearest-even; hipcc lowers the builtin conversion to v_cvt_pk_bf16_f32 on gfx950,
   // which keeps NaNs NaN (MI355X_MICROARCH.md "Correctness boundaries").

@@ -85,11 +85,11 @@ class FeedForward:
         self.w2 = Dense(store, path + ("w2",), hidden, dim, trainable)
         self.dropout = dropout
 
-    def __call__(self, x, rng=None, det=True):
+    def __call__(self, x, rng=None, det=True, seeds=None):
         h = self.w1(x, gelu=True)
-        h = _dropout(h, self.dropout, rng, det)
+        h = _dropout(h, self.dropout, rng, det, seeds and seeds[0])
         y = self.w2(h)
-        return _dropout(y, self.dropout, rng, det)
+        return _dropout(y, self.dropout, rng, det, seeds and seeds[1])
 
 
 class Attention:
@@ -105,24 +105,40 @@ class Attention:
         self.wo_k = store.handle(_dense_kernel(store, path + ("wo", "kernel"), (heads, hd), (dim,), trainable))
         self.wo_b = store.handle(_bias(store, path + ("wo", "bias"), (dim,), trainable))
 
-    def __call__(self, x2d, B, S, rng=None, det=True):
+    def __call__(self, x2d, B, S, rng=None, det=True, seeds=None):
         qkv = Fn.linear(x2d, self.qkv_k, self.qkv_b).view(B, S, 3 * self.dim)
         if self.dropout > 0 and not det:
-            o = _attention_with_dropout(qkv, self.heads, self.dropout, rng)
+            o = _attention_with_dropout(qkv, self.heads, self.dropout, rng, seeds and seeds[0])
         else:
             o = Fn.attention(qkv, self.heads)
         y = Fn.linear(o.view(B * S, self.dim), self.wo_k, self.wo_b)
-        return _dropout(y, self.dropout, rng, det)
+        return _dropout(y, self.dropout, rng, det, seeds and seeds[1])
 
 
-def _dropout(x, rate, rng, det):
+def _dropout(x, rate, rng, det, seed=None):
     """Flax nn.Dropout (train mode): hash-mask HIP kernel, mask regenerated in backward (ops/dropout.py)."""
     if rate <= 0.0 or det:
         return x
-    return Dr.dropout(x, rate, rng)
+    return Dr.dropout(x, rate, rng, seed)
 
 
-def _attention_with_dropout(qkv, heads, rate, rng):
+def _layer_seeds(rate, rng, device, det, n):
+    """The dropout seeds of one layer from one draw (both paths use the same order: attention
+    probabilities, attention output, [jumbo MLP hidden, output,] FF hidden, FF output), or None."""
+    if rate <= 0.0 or det or rate >= 1.0:
+        return None
+    return Dr.draw_seeds(rng, device, n)
+
+
+def _drops(seeds, rate, jumbo):
+    if seeds is None:
+        return None
+    if jumbo:
+        return blocks.Drops(rate, seeds[0], seeds[1], seeds[4], seeds[5], seeds[2], seeds[3])
+    return blocks.Drops(rate, *seeds)
+
+
+def _attention_with_dropout(qkv, heads, rate, rng, seed=None):
     """Attention with dropout on the probabilities (all presets use dropout 0): the two batched
     products on the BLAS library in fp32, softmax + dropout (and its backward) as one fused HIP
     row kernel each way -- the whole-sequence attention kernels never materialise P."""
@@ -131,7 +147,7 @@ def _attention_with_dropout(qkv, heads, rate, rng):
     hd = D // heads
     q, k, v = qkv.view(B, S, 3, heads, hd).unbind(2)
     z = torch.einsum("bqhd,bkhd->bhqk", q.float() / math.sqrt(hd), k.float())
-    p = Dr.softmax_dropout(z, rate, rng)
+    p = Dr.softmax_dropout(z, rate, rng, seed)
     return torch.einsum("bhqk,bkhd->bqhd", p, v.float()).reshape(B, S, D).to(qkv.dtype)
 
 
@@ -212,25 +228,26 @@ class JumboLayer:
         B, S, D = x.shape
         C = self.C
         p = self.cfg.droppath
-        if use_fused_blocks() and (self.cfg.dropout <= 0.0 or det):
+        sd = _layer_seeds(self.cfg.dropout, rng, x.device, det, 6)
+        if use_fused_blocks() and self.cfg.dropout < 1.0:
             m1 = _mask(masks, 0, p, B, rng, x.device, det)
             m3 = _mask(masks, 1, p, B, rng, x.device, det)
             m2 = _mask(masks, 2, p, B, rng, x.device, det)
-            return blocks.jumbo_block(self, x, m1, m2, m3, link_in, link_out)
+            return blocks.jumbo_block(self, x, m1, m2, m3, link_in, link_out, _drops(sd, self.cfg.dropout, True))
         h = self.norm1(x)
-        a = self.attn(h, B, S, rng, det)
+        a = self.attn(h, B, S, rng, det, sd and sd[0:2])
         x = Fn.residual(x, a, self.scale1, _mask(masks, 0, p, B, rng, x.device, det))
 
         # NB: the jumbo residual is added to the *normalized* CLS token (modeling.py:197-199),
         # so the CLS stream is re-normalized by norm3 in every layer.
         cls = x[:, :C].reshape(B, 1, C * D)
         hc = self.norm3(cls, out_dtype=torch.float32)  # [B, J] fp32 residual base
-        yc = self.jumbo_mlp(hc.to(self.norm3.g.store.compute_dtype), rng, det)
+        yc = self.jumbo_mlp(hc.to(self.norm3.g.store.compute_dtype), rng, det, sd and sd[2:4])
         xc = Fn.residual(hc.view(B, 1, C * D), yc, self.scale3, _mask(masks, 1, p, B, rng, x.device, det))
 
         pt = x[:, C:]
         hp = self.norm2(pt)
-        yp = self.ff(hp, rng, det)
+        yp = self.ff(hp, rng, det, sd and sd[4:6])
         xp = Fn.residual(pt, yp, self.scale2, _mask(masks, 2, p, B, rng, x.device, det))
         return torch.cat([xc.view(B, C, D), xp], 1)
 
@@ -258,15 +275,16 @@ class ViTLayer:
     def __call__(self, x, rng=None, det=True, link_in=None, link_out=None, masks=None):
         B, S, D = x.shape
         p = self.droppath
-        if use_fused_blocks() and (self.attn.dropout <= 0.0 or det):
+        sd = _layer_seeds(self.attn.dropout, rng, x.device, det, 4)
+        if use_fused_blocks() and self.attn.dropout < 1.0:
             m1 = _mask(masks, 0, p, B, rng, x.device, det)
             m2 = _mask(masks, 1, p, B, rng, x.device, det)
-            return blocks.vit_block(self, x, m1, m2, link_in, link_out)
+            return blocks.vit_block(self, x, m1, m2, link_in, link_out, _drops(sd, self.attn.dropout, False))
         h = self.norm1(x)
-        a = self.attn(h, B, S, rng, det)
+        a = self.attn(h, B, S, rng, det, sd and sd[0:2])
         x = Fn.residual(x, a, self.scale1, _mask(masks, 0, p, B, rng, x.device, det))
         h = self.norm2(x)
-        f = self.ff(h, rng, det)
+        f = self.ff(h, rng, det, sd and sd[2:4])
         return Fn.residual(x, f, self.scale2, _mask(masks, 1, p, B, rng, x.device, det))
 
 

@@ -1,7 +1,8 @@
 """Dropout with a counter-based hash mask (reference src/modeling.py:133-148, flax nn.Dropout).
 
-The keep bit of element ``i`` is a pure function of ``(seed, i)`` (``csrc/dropout.hip``
-``keep_bit``; :func:`keep_mask` is its bit-exact torch mirror), so no mask is ever stored: the
+The keep bit of element ``i`` is a pure function of ``(seed, i)`` (``csrc/common.h``
+``drop_keep``: one 32-bit hash per pair of elements, 16-bit thresholds; :func:`keep_mask` is its
+bit-exact torch mirror), so no mask is ever stored: the
 backward regenerates it, and so does the recompute of an activation-checkpointed layer (which
 redraws the same seed from the restored generator).  The seed is an int64 [1] tensor drawn from
 the caller's ``torch.Generator`` on the data's device -- no host round trip, HIP-graph safe.
@@ -31,35 +32,59 @@ def _mul32(a: torch.Tensor, c: int) -> torch.Tensor:
     return ((((a * hi) & 0xFFFF) << 16) + a * lo) & _M32
 
 
-def _fmix32(h: torch.Tensor) -> torch.Tensor:
-    h = h ^ (h >> 16)
-    h = _mul32(h, 0x85EBCA6B)
-    h = h ^ (h >> 13)
-    h = _mul32(h, 0xC2B2AE35)
-    return h ^ (h >> 16)
+def _hash(j: torch.Tensor, seed: int) -> torch.Tensor:
+    """common.h drop_hash: lowbias32 finalizer of (j + seed_lo) ^ seed_hi, all mod 2^32."""
+    s_lo, s_hi = seed & _M32, (seed >> 32) & _M32
+    x = ((j + s_lo) & _M32) ^ s_hi
+    x = x ^ (x >> 16)
+    x = _mul32(x, 0x7FEB352D)
+    x = x ^ (x >> 15)
+    x = _mul32(x, 0x846CA68B)
+    return x ^ (x >> 16)
 
 
 def keep_threshold(rate: float) -> tuple[int, float]:
+    """(16-bit keep threshold, 1/keep scale) of a drop rate in [0, 1)."""
     if not 0.0 <= rate < 1.0:
         raise ValueError(f"dropout rate must be in [0, 1), got {rate}")
     keep = 1.0 - rate
-    return int(round(keep * 16777216.0)), 1.0 / keep
+    return int(round(keep * 65536.0)), 1.0 / keep
+
+
+def keep_of_index(seed: torch.Tensor, idx: torch.Tensor, rate: float) -> torch.Tensor:
+    """bool: keep bits of the given int64 element indices (bit-exact mirror of common.h drop_keep:
+    one hash per pair idx >> 1, its low / high 16 bits for even / odd idx)."""
+    thr, _ = keep_threshold(rate)
+    s = int(seed.reshape(-1)[0].item())
+    h = _hash((idx >> 1) & _M32, s)
+    v = torch.where((idx & 1) == 1, h >> 16, h & 0xFFFF)
+    return v < thr
 
 
 def keep_mask(seed: torch.Tensor, n: int, rate: float, device=None) -> torch.Tensor:
-    """bool [n]: the keep bits of elements 0..n-1 (bit-exact mirror of csrc/dropout.hip keep_bit)."""
-    thr, _ = keep_threshold(rate)
-    s = int(seed.reshape(-1)[0].item())
-    s_lo, s_hi = s & _M32, (s >> 32) & _M32
-    i = torch.arange(n, dtype=torch.int64, device=device)
-    h = _fmix32(((i >> 32) + s_lo) & _M32)
-    h = _fmix32((i & _M32) ^ h)
-    h = _fmix32((h + s_hi) & _M32)
-    return (h >> 8) < thr
+    """bool [n]: the keep bits of elements 0..n-1 (elementwise dropout sites)."""
+    return keep_of_index(seed, torch.arange(n, dtype=torch.int64, device=device), rate)
+
+
+def keep_mask_rows(seed: torch.Tensor, rows: int, S: int, rate: float, device=None) -> torch.Tensor:
+    """bool [rows, S]: attention-probability keep bits for rows r = (b H + h) S + q: element (r, c)
+    at index ((r - q) + c) * SE + q with SE = S rounded up to even -- transposed, so that queries
+    2m, 2m + 1 of a key share one hash (the fused attention kernels' convention)."""
+    se = S + (S & 1)
+    r = torch.arange(rows, dtype=torch.int64, device=device)[:, None]
+    q = r % S
+    c = torch.arange(S, dtype=torch.int64, device=device)
+    return keep_of_index(seed, (r - q + c) * se + q, rate)
 
 
 def draw_seed(rng: torch.Generator | None, device) -> torch.Tensor:
     return torch.randint(0, 2 ** 62, (1,), generator=rng, device=device, dtype=torch.int64)
+
+
+def draw_seeds(rng: torch.Generator | None, device, n: int) -> list[torch.Tensor]:
+    """n seeds from ONE draw (one kernel per layer instead of one per dropout site)."""
+    t = torch.randint(0, 2 ** 62, (n,), generator=rng, device=device, dtype=torch.int64)
+    return [t[i:i + 1] for i in range(n)]
 
 
 def _apply(x: torch.Tensor, seed: torch.Tensor, rate: float) -> torch.Tensor:
@@ -68,6 +93,37 @@ def _apply(x: torch.Tensor, seed: torch.Tensor, rate: float) -> torch.Tensor:
     _, scale = keep_threshold(rate)
     m = keep_mask(seed, x.numel(), rate, x.device).view(x.shape)
     return torch.where(m, x * scale, torch.zeros((), dtype=x.dtype))
+
+
+def apply_(x: torch.Tensor, seed: torch.Tensor, rate: float) -> torch.Tensor:
+    """In place: x *= keep(seed, i) / keep over x's flat elements (the fused blocks' Dense-output
+    dropout, forward on the branch output and backward on its gradient)."""
+    if x.is_cuda:
+        _ext.load(True).dropout_apply_(x, seed, rate)
+        return x
+    _, scale = keep_threshold(rate)
+    m = keep_mask(seed, x.numel(), rate, x.device).view(x.shape)
+    return x.mul_(m.to(x.dtype) * scale)
+
+
+def gelu_drop(a: torch.Tensor, gp: torch.Tensor | None, seed: torch.Tensor, rate: float):
+    """FF hidden dropout of the fused blocks -> (gelu(h) m, gelu'(h) m) with m = keep / keep_p:
+    ``gp`` given: ``a`` = gelu(h) and ``gp`` = gelu'(h) (the fused epilogue's pair), masked in
+    place; else ``a`` is the pre-activation h."""
+    if a.is_cuda:
+        g, d = _ext.load(True).gelu_drop(a, gp, seed, rate)
+        return g, d
+    _, scale = keep_threshold(rate)
+    m = keep_mask(seed, a.numel(), rate, a.device).view(a.shape).to(torch.float32) * scale
+    if gp is not None:
+        a.copy_((a.float() * m).to(a.dtype))
+        gp.copy_((gp.float() * m).to(gp.dtype))
+        return a, gp
+    x = a.float()
+    t = torch.tanh(0.7978845608028654 * (x + 0.044715 * x ** 3))
+    g = 0.5 * x * (1 + t)
+    d = 0.5 * (1 + t) + 0.5 * x * (1 - t * t) * 0.7978845608028654 * (1 + 3 * 0.044715 * x * x)
+    return (g * m).to(a.dtype), (d * m).to(a.dtype)
 
 
 class _Dropout(torch.autograd.Function):
@@ -83,15 +139,16 @@ class _Dropout(torch.autograd.Function):
         return _apply(dy, seed, ctx.rate), None, None
 
 
-def dropout(x: torch.Tensor, rate: float, rng: torch.Generator | None) -> torch.Tensor:
-    """Inverted dropout of ``x`` (train mode); rate 0 is the identity, rate 1 gives zeros."""
+def dropout(x: torch.Tensor, rate: float, rng: torch.Generator | None, seed: torch.Tensor | None = None) -> torch.Tensor:
+    """Inverted dropout of ``x`` (train mode); rate 0 is the identity, rate 1 gives zeros.
+    ``seed``: a pre-drawn seed (draw_seeds) instead of a draw from ``rng``."""
     if rate <= 0.0:
         return x
     if rate >= 1.0:
         return x * 0.0
     if x.is_cuda and x.numel() % 8:
         raise ValueError("dropout: the HIP kernel needs numel % 8 == 0")
-    return _Dropout.apply(x, draw_seed(rng, x.device), rate)
+    return _Dropout.apply(x, seed if seed is not None else draw_seed(rng, x.device), rate)
 
 
 class _SoftmaxDropout(torch.autograd.Function):
@@ -102,7 +159,7 @@ class _SoftmaxDropout(torch.autograd.Function):
         else:
             p = torch.softmax(z, -1)
             _, scale = keep_threshold(rate)
-            m = keep_mask(seed, z.numel(), rate, z.device).view(z.shape)
+            m = keep_mask_rows(seed, z.numel() // z.shape[-1], z.shape[-1], rate, z.device).view(z.shape)
             pd = torch.where(m, p * scale, torch.zeros((), dtype=p.dtype))
         ctx.save_for_backward(p, seed)
         ctx.rate = rate
@@ -115,16 +172,17 @@ class _SoftmaxDropout(torch.autograd.Function):
         if p.is_cuda:
             return _ext.load(True).softmax_dropout_bwd(dpd, p, seed, ctx.rate), None, None
         _, scale = keep_threshold(ctx.rate)
-        m = keep_mask(seed, p.numel(), ctx.rate, p.device).view(p.shape)
+        m = keep_mask_rows(seed, p.numel() // p.shape[-1], p.shape[-1], ctx.rate, p.device).view(p.shape)
         dp = torch.where(m, dpd * scale, torch.zeros((), dtype=dpd.dtype))
         return p * (dp - (p * dp).sum(-1, keepdim=True)), None, None
 
 
-def softmax_dropout(z: torch.Tensor, rate: float, rng: torch.Generator | None) -> torch.Tensor:
+def softmax_dropout(z: torch.Tensor, rate: float, rng: torch.Generator | None,
+                    seed: torch.Tensor | None = None) -> torch.Tensor:
     """dropout(softmax(z, -1)) for fp32 logits ``z`` [..., S] (train mode)."""
     z = z.float().contiguous()
     if rate <= 0.0:
         return torch.softmax(z, -1)
     if rate >= 1.0:
         return z * 0.0
-    return _SoftmaxDropout.apply(z, draw_seed(rng, z.device), rate)
+    return _SoftmaxDropout.apply(z, seed if seed is not None else draw_seed(rng, z.device), rate)

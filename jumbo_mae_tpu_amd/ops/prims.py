@@ -658,40 +658,61 @@ def _attn_hip(qkv: torch.Tensor, heads: int) -> bool:
     return hd in (32, 64)
 
 
-def attn_fwd(qkv: torch.Tensor, heads: int):
-    """qkv [B, S, 3*D] -> (o [B, S, D], lse [B, H, S])."""
+def _drop_mask(drop, B: int, heads: int, S: int, device):
+    """float [B, H, S, S] keep mask / keep of attention-probability dropout ``drop`` = (seed, rate):
+    the fused kernels' index convention (ops/dropout.py keep_mask_rows), for the composition path."""
+    from . import dropout as Dr
+    seed, rate = drop
+    _, scale = Dr.keep_threshold(rate)
+    m = Dr.keep_mask_rows(seed.cpu(), B * heads * S, S, rate).view(B, heads, S, S).to(device)
+    return m.float() * scale
+
+
+def attn_fwd(qkv: torch.Tensor, heads: int, drop=None):
+    """qkv [B, S, 3*D] -> (o [B, S, D], lse [B, H, S]).  ``drop`` = (seed int64 [1] tensor, rate):
+    dropout on the attention probabilities (reference modeling.py:137), fused into the kernels up
+    to S = attn_max_seq(); lse is that of the undropped softmax."""
     B, S, three_d = qkv.shape
     D = three_d // 3
     hd = D // heads
-    if _attn_hip(qkv, heads):
-        return _ext.load().attn_fwd(qkv, heads)
+    if _attn_hip(qkv, heads) and (drop is None or S <= _ext.load().attn_max_seq()):
+        if drop is None:
+            return _ext.load().attn_fwd(qkv, heads)
+        return _ext.load().attn_fwd(qkv, heads, drop[0], drop[1])
     q, k, v = qkv.float().view(B, S, 3, heads, hd).unbind(2)
     z = torch.einsum("bqhd,bkhd->bhqk", q / math.sqrt(hd), k)
     lse = torch.logsumexp(z, -1)
     p = torch.exp(z - lse[..., None])
+    if drop is not None:
+        p = p * _drop_mask(drop, B, heads, S, qkv.device)
     o = torch.einsum("bhqk,bkhd->bqhd", p, v).reshape(B, S, D).to(qkv.dtype)
     return o, lse
 
 
 def attn_bwd(do: torch.Tensor, qkv: torch.Tensor, o: torch.Tensor, lse: torch.Tensor, heads: int,
-             hbias: Handle | None = None):
+             hbias: Handle | None = None, drop=None):
     """-> (dqkv [B, S, 3D], bias_done).  When ``hbias`` (the QKV Dense bias) is given, its gradient
-    colsum(dqkv) is fused into the HIP kernel."""
+    colsum(dqkv) is fused into the HIP kernel.  ``drop``: the forward's (seed, rate)."""
     B, S, three_d = qkv.shape
     D = three_d // 3
     hd = D // heads
     do = do.contiguous().view(B, S, D)
-    if _attn_hip(qkv, heads):
+    if _attn_hip(qkv, heads) and (drop is None or S <= _ext.load().attn_max_seq()):
         ext = _ext.load()
         bg = hbias.grad if _trainable(hbias) and S <= ext.attn_max_seq() else None
-        return ext.attn_bwd(do, qkv, o, lse, heads, bg), bg is not None
+        if drop is None:
+            return ext.attn_bwd(do, qkv, o, lse, heads, bg), bg is not None
+        return ext.attn_bwd(do, qkv, o, lse, heads, bg, drop[0], drop[1]), bg is not None
     q, k, v = qkv.float().view(B, S, 3, heads, hd).unbind(2)
     dof = do.float().view(B, S, heads, hd)
     sc = 1.0 / math.sqrt(hd)
     z = torch.einsum("bqhd,bkhd->bhqk", q * sc, k)
     p = torch.exp(z - lse[..., None])
-    dv = torch.einsum("bhqk,bqhd->bkhd", p, dof)
+    mk = _drop_mask(drop, B, heads, S, qkv.device) if drop is not None else None
+    dv = torch.einsum("bhqk,bqhd->bkhd", p if mk is None else p * mk, dof)
     dp = torch.einsum("bqhd,bkhd->bhqk", dof, v)
+    if mk is not None:
+        dp = dp * mk
     delta = (dof * o.float().view(B, S, heads, hd)).sum(-1).permute(0, 2, 1)
     ds = p * (dp - delta[..., None])
     dq = torch.einsum("bhqk,bkhd->bqhd", ds, k) * sc

@@ -51,7 +51,7 @@ def test_softmax_dropout_grad_matches_autograd():
     g2 = torch.Generator()
     g2.set_state(state)
     seed = Dr.draw_seed(g2, "cpu")
-    m = Dr.keep_mask(seed, z.numel(), 0.2).view(z.shape)
+    m = Dr.keep_mask_rows(seed, z.numel() // z.shape[-1], z.shape[-1], 0.2).view(z.shape)
     zr = z.clone().float().requires_grad_(True)
     ref = torch.where(m, torch.softmax(zr, -1) / 0.8, torch.zeros(()))
     assert torch.allclose(out, ref, atol=1e-6)

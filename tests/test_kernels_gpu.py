@@ -145,6 +145,40 @@ def test_attention(ext, B, S, H, hd):
         assert torch.equal(ext.attn_bwd(do, qkv, o, lse, H, db2), dqkv) and torch.equal(db2, dbias)
 
 
+@pytest.mark.parametrize("B,S,H,hd", [(3, 52, 4, 64), (2, 199, 4, 32), (2, 199, 3, 64), (5, 17, 2, 32),
+                                      (9, 30, 2, 64), (2, 100, 2, 32)])
+def test_attention_dropout(ext, B, S, H, hd):
+    """Dropout on the attention probabilities inside the fused kernels (forward: masked P.V with
+    the undropped row statistics; backward: the mask regenerated from the seed) against an fp64
+    reference with the mirrored mask (ops/dropout.py keep_mask_rows)."""
+    from jumbo_mae_tpu_amd.ops import dropout as Dr
+    torch.manual_seed(0)
+    rate = 0.2
+    D = H * hd
+    qkv = (torch.randn(B, S, 3 * D, device="cuda") * 1.5).bfloat16()
+    seed = torch.tensor([0x5EED_1234_5678], dtype=torch.int64, device="cuda")
+    o, lse = ext.attn_fwd(qkv, H, seed, rate)
+    m = Dr.keep_mask_rows(seed.cpu(), B * H * S, S, rate).view(B, H, S, S).cuda().double() / (1 - rate)
+    qr = qkv.double().requires_grad_()
+    q, k, v = qr.view(B, S, 3, H, hd).unbind(2)
+    z = torch.einsum("bqhd,bkhd->bhqk", q / math.sqrt(hd), k)
+    lser = torch.logsumexp(z, -1)
+    orf = torch.einsum("bhqk,bkhd->bqhd", torch.softmax(z, -1) * m, v).reshape(B, S, D)
+    assert rel(o, orf) < 1e-2
+    assert (lse.double() - lser).abs().max().item() < 2e-2
+    do = torch.randn(B, S, D, device="cuda").bfloat16()
+    dbias = torch.zeros(3 * D, device="cuda")
+    dqkv = ext.attn_bwd(do, qkv, o, lse, H, dbias, seed, rate)
+    orf.backward(do.double())
+    g = qr.grad.view(B, S, 3, D)
+    d = dqkv.view(B, S, 3, D)
+    for i in range(3):
+        assert rel(d[:, :, i], g[:, :, i]) < 2e-2, i
+    assert rel(dbias, qr.grad.sum((0, 1))) < 2e-2
+    o0, _ = ext.attn_fwd(qkv, H)
+    assert rel(o0, orf) > 0.05  # the mask is live
+
+
 @pytest.mark.parametrize("S,n", [(4, 4096), (512, 3072), (37, 1024)])
 def test_splitk_reduce_add(ext, S, n):
     part = torch.randn(S, n, device="cuda")

@@ -114,6 +114,34 @@ def test_fused_blocks_match_per_op_with_droppath(monkeypatch):
     assert torch.allclose(res[0][1], res[1][1], atol=1e-6, rtol=1e-4)
 
 
+@pytest.mark.parametrize("rate", [0.1, 0.5])
+def test_fused_blocks_match_per_op_with_dropout(monkeypatch, rate):
+    """Dropout > 0 on the fused blocks (attention probabilities, attention / FF / jumbo-MLP outputs
+    and hidden layers; ops/blocks.py Drops) == the per-op graph with the same seeds: the layer draws
+    them in the per-op order and every site uses the shared hash-mask convention."""
+    from jumbo_mae_tpu_amd.utils.rng import RngStreams
+    vc = ViTConfig(layers=2, dim=32, heads=4, labels=0, image_size=32, patch_size=8, posemb="sincos2d",
+                   layerscale=True, droppath=0.2, dropout=rate)
+    dc = DecoderConfig(dec_layers=2, dec_dim=16, dec_heads=2, image_size=32, patch_size=8, dec_layerscale=True,
+                       dec_dropout=rate)
+    imgs = torch.randint(0, 256, (4, 3, 32, 32), dtype=torch.uint8)
+    noise = torch.rand(16)
+    res = []
+    for per_op in ("0", "1"):
+        monkeypatch.setenv("JMAE_PER_OP", per_op)
+        m = PretrainModel(vc, dc).to("cpu", seed=0)
+        with torch.no_grad():
+            m.store.master.add_(torch.linspace(-0.02, 0.02, m.store.total))
+        rng = RngStreams({"dropout": 5}, 0, "cpu").as_dict()
+        loss = m(imgs, rngs=rng, noise=noise)["loss"]
+        loss.backward()
+        res.append((loss.item(), m.store.grad.clone()))
+    assert abs(res[0][0] - res[1][0]) < 1e-5 * max(1.0, abs(res[1][0]))
+    assert torch.allclose(res[0][1], res[1][1], atol=1e-6, rtol=1e-4)
+    # and the dropout is live: a different rate gives a different loss
+    assert res[0][1].abs().sum() > 0
+
+
 def test_forward_links_fuse_upper_ln1(monkeypatch):
     """Forward Link hand-off: each lower block computes the upper block's LN1 in its last residual
     pass (ops/blocks.py Link.ln1) -- fewer standalone LayerNorms, identical loss and gradients."""
