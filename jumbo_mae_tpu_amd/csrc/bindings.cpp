@@ -37,7 +37,8 @@ int jm_debug_line_optim();
 void jm_debug_selftest(int v, hipStream_t st);
 int jm_residual_ln_fwd(const float* x, long sB, long sT, const uint16_t* y, const float* scale, const float* mask,
                        float* x1, long oB, long oT, uint16_t* h, float* mean, float* rstd, int B, int T, int T0,
-                       int D, const float* gamma, const float* beta, float eps, hipStream_t st, int R0 = 0);
+                       int D, const float* gamma, const float* beta, float eps, hipStream_t st, int R0 = 0,
+                       JmDrop drop = JmDrop{nullptr, 0u, 1.f, 0});
 int jm_gelu_fwd(const uint16_t* h, uint16_t* a, long n, hipStream_t st);
 int jm_gelu_bwd(const uint16_t* h, const uint16_t* da, uint16_t* dh, float* bias_grad, int M, int N, hipStream_t st,
                 int deriv = 0);
@@ -48,9 +49,10 @@ int jm_zero_ranges(float* base, const long long* desc, int n, long long blocks, 
 int jm_transpose_bf16(const uint16_t* src, uint16_t* dst, int R, int C, hipStream_t st);
 int jm_transpose_bf16_batch(const long long* desc, int n, int tiles, hipStream_t st);
 int jm_residual_fwd(const float* x, long sB, long sT, int B, int T, int D, const uint16_t* y, const float* scale,
-                    const float* mask, float* out, long oB, long oT, hipStream_t st);
+                    const float* mask, float* out, long oB, long oT, hipStream_t st, JmDrop drop);
 int jm_residual_bwd(const float* dout, long dB, long dT, const uint16_t* y, const float* scale, const float* mask,
-                    float* dscale, uint16_t* dy, int B, int T, int D, float* dbias, long yB, long yT, hipStream_t st);
+                    float* dscale, uint16_t* dy, int B, int T, int D, float* dbias, long yB, long yT, hipStream_t st,
+                    JmDrop drop);
 int jm_attn_fwd(const uint16_t* qkv, uint16_t* o, float* lse, int B, int S, int H, int hd, const int64_t* dseed,
                 uint32_t dthr, float dscale, hipStream_t st);
 int jm_attn_bwd(const uint16_t* qkv, const uint16_t* o, const uint16_t* dO, const float* lse, uint16_t* dqkv, int B,
@@ -133,6 +135,28 @@ float* fopt_m(c10::optional<torch::Tensor>& t) { return t.has_value() && t->defi
 
 void check_rc(int rc, const char* what) { TORCH_CHECK(rc == 0, what, ": unsupported shape (rc=", rc, ")"); }
 
+// dropout: keep threshold on 16 hash bits (common.h drop_keep) and the 1/keep scale of a drop
+// rate in [0, 1)
+static std::pair<uint32_t, float> keep_params(double rate) {
+  TORCH_CHECK(rate >= 0.0 && rate < 1.0, "dropout rate must be in [0, 1)");
+  const double keep = 1.0 - rate;
+  return {(uint32_t)std::llround(keep * 65536.0), (float)(1.0 / keep)};
+}
+
+static void check_seed(const torch::Tensor& seed, const torch::Tensor& like) {
+  TORCH_CHECK(seed.scalar_type() == torch::kInt64 && seed.numel() == 1 && seed.device() == like.device(),
+              "dropout seed: int64 [1] on the data's device");
+}
+
+// Dense-output dropout descriptor for the residual kernels: seed null / rate 0 = none; ioff = the
+// element offset of y's view within the branch tensor the mask indexes
+JmDrop make_drop(const c10::optional<torch::Tensor>& seed, double rate, const torch::Tensor& like, int64_t ioff) {
+  if (!seed.has_value() || !seed->defined() || rate <= 0.0) return JmDrop{nullptr, 0u, 1.f, 0};
+  check_seed(*seed, like);
+  const auto kp = keep_params(rate);
+  return JmDrop{seed->data_ptr<int64_t>(), kp.first, kp.second, (long)ioff};
+}
+
 // ------------------------------------------------------------------------------ layernorm
 // also_bf16 (fp32 output only): a bf16 copy of y written by the same pass, returned 4th
 std::vector<torch::Tensor> layernorm_fwd(torch::Tensor x, torch::Tensor gamma, torch::Tensor beta, double eps,
@@ -167,7 +191,8 @@ std::vector<torch::Tensor> layernorm_bwd(torch::Tensor dy, torch::Tensor x, torc
                                          c10::optional<torch::Tensor> res_y, c10::optional<torch::Tensor> res_scale,
                                          c10::optional<torch::Tensor> res_mask, c10::optional<torch::Tensor> res_dscale,
                                          c10::optional<torch::Tensor> res_dbias, int64_t res_T0,
-                                         c10::optional<torch::Tensor> res_out) {
+                                         c10::optional<torch::Tensor> res_out, c10::optional<torch::Tensor> res_seed,
+                                         double res_rate, int64_t res_ioff) {
   CHECK_CONTIG(dy);
   TORCH_CHECK(x.dim() == 3 && x.stride(2) == 1, "x must be [B,T,D]");
   const int B = x.size(0), T = x.size(1), D = x.size(2);
@@ -216,7 +241,7 @@ std::vector<torch::Tensor> layernorm_bwd(torch::Tensor dy, torch::Tensor x, torc
       dyr = torch::empty_like(y);
     }
     res = JmLnRes{bf(y), bfm(dyr), yB, yT, fopt(res_scale), fopt(res_mask), (int)res_T0, fopt_m(res_dscale),
-                  fopt_m(res_dbias)};
+                  fopt_m(res_dbias), make_drop(res_seed, res_rate, y, res_ioff)};
   }
   const int NP = has_res ? 4 : 2;
   auto ws = torch::empty({(accum || has_res) ? (long)jm_layernorm_bwd_blocks(B * T, D) * NP * D : 1}, x.options());
@@ -281,7 +306,8 @@ void colsum_add_f32(torch::Tensor x, torch::Tensor g) {
 }
 
 torch::Tensor residual_fwd(torch::Tensor x, torch::Tensor y, c10::optional<torch::Tensor> scale,
-                           c10::optional<torch::Tensor> mask, c10::optional<torch::Tensor> out_opt) {
+                           c10::optional<torch::Tensor> mask, c10::optional<torch::Tensor> out_opt,
+                           c10::optional<torch::Tensor> seed, double rate, int64_t ioff) {
   TORCH_CHECK(x.dim() == 3 && x.stride(2) == 1, "x must be [B,T,D]");
   CHECK_DT(x, torch::kFloat32);
   CHECK_CONTIG(y);
@@ -296,7 +322,8 @@ torch::Tensor residual_fwd(torch::Tensor x, torch::Tensor y, c10::optional<torch
     out = torch::empty({B, T, D}, x.options());
   }
   check_rc(jm_residual_fwd(x.data_ptr<float>(), x.stride(0), x.stride(1), B, T, D, bf(y), fopt(scale), fopt(mask),
-                           out.data_ptr<float>(), out.stride(0), out.stride(1), stream()),
+                           out.data_ptr<float>(), out.stride(0), out.stride(1), stream(),
+                           make_drop(seed, rate, y, ioff)),
            "residual_fwd");
   return out;
 }
@@ -305,7 +332,8 @@ torch::Tensor residual_fwd(torch::Tensor x, torch::Tensor y, c10::optional<torch
 // with y absent: its own strides)
 torch::Tensor residual_bwd(torch::Tensor dout, c10::optional<torch::Tensor> y, c10::optional<torch::Tensor> scale,
                            c10::optional<torch::Tensor> mask, c10::optional<torch::Tensor> dscale, py::object ydtype,
-                           c10::optional<torch::Tensor> dbias, c10::optional<torch::Tensor> out) {
+                           c10::optional<torch::Tensor> dbias, c10::optional<torch::Tensor> out,
+                           c10::optional<torch::Tensor> seed, double rate, int64_t ioff) {
   TORCH_CHECK(dout.dim() == 3 && dout.stride(2) == 1, "dout must be a [B,T,D] view");
   CHECK_DT(dout, torch::kFloat32);
   const int B = dout.size(0), T = dout.size(1), D = dout.size(2);
@@ -343,25 +371,12 @@ torch::Tensor residual_bwd(torch::Tensor dout, c10::optional<torch::Tensor> y, c
   }
   check_rc(jm_residual_bwd(dout.data_ptr<float>(), dout.stride(0), dout.stride(1), has_y ? bf(*y) : nullptr,
                            fopt(scale), fopt(mask), fopt_m(dscale), bfm(dy), B, T, D, fopt_m(dbias), yB, yT,
-                           stream()),
+                           stream(), make_drop(seed, rate, dout, ioff)),
            "residual_bwd");
   return dy;
 }
 
 // ------------------------------------------------------------------------------ attention
-// dropout: keep threshold on 16 hash bits (common.h drop_keep) and the 1/keep scale of a drop
-// rate in [0, 1)
-static std::pair<uint32_t, float> keep_params(double rate) {
-  TORCH_CHECK(rate >= 0.0 && rate < 1.0, "dropout rate must be in [0, 1)");
-  const double keep = 1.0 - rate;
-  return {(uint32_t)std::llround(keep * 65536.0), (float)(1.0 / keep)};
-}
-
-static void check_seed(const torch::Tensor& seed, const torch::Tensor& like) {
-  TORCH_CHECK(seed.scalar_type() == torch::kInt64 && seed.numel() == 1 && seed.device() == like.device(),
-              "dropout seed: int64 [1] on the data's device");
-}
-
 // seed (int64 [1] on the device) with rate > 0: dropout on the attention probabilities (mask:
 // common.h drop_keep at ((b H + h) S + q) SE + k, the backward regenerates it from the same seed)
 static std::tuple<const int64_t*, uint32_t, float> attn_drop(const c10::optional<torch::Tensor>& seed, double rate,
@@ -668,7 +683,7 @@ int attach_tail(GemmEpi& ep, torch::Tensor& ws, int M, int N, int K, int epi, co
 
 // gelu_deriv (with gelu): returns {gelu'(h), gelu(h)} instead of {h, gelu(h)} (EPI_GELU_D)
 std::vector<torch::Tensor> gemm_nt(torch::Tensor A, torch::Tensor B, c10::optional<torch::Tensor> bias, bool gelu,
-                                   bool gelu_only, bool gelu_deriv) {
+                                   bool gelu_only, bool gelu_deriv, c10::optional<torch::Tensor> seed, double rate) {
   CHECK_DT(A, torch::kBFloat16);
   CHECK_DT(B, torch::kBFloat16);
   TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && A.size(1) == B.size(1), "gemm_nt: A [M,K], B [N,K]");
@@ -687,6 +702,14 @@ std::vector<torch::Tensor> gemm_nt(torch::Tensor A, torch::Tensor B, c10::option
   }
   TORCH_CHECK(!gelu_deriv || (gelu && !gelu_only), "gemm_nt: gelu_deriv needs gelu and not gelu_only");
   const int epi = gelu_only ? 4 : (gelu_deriv ? 6 : (gelu ? 1 : 0));
+  if (seed.has_value() && seed->defined() && rate > 0.0) {  // FF hidden dropout in the GELU_D epilogue
+    TORCH_CHECK(epi == 6, "gemm_nt: dropout only with gelu_deriv");
+    check_seed(*seed, A);
+    const auto kp = keep_params(rate);
+    ep.dseed = seed->data_ptr<int64_t>();
+    ep.dthr = kp.first;
+    ep.dscale = kp.second;
+  }
   torch::Tensor ws;
   attach_tail(ep, ws, M, N, K, epi, A);
   check_rc(jm_gemm_nt(bf(A), A.stride(0), bf(B), B.stride(0), M, N, K, epi, ep, stream()), "gemm_nt");
@@ -1081,7 +1104,8 @@ void zero_ranges(torch::Tensor base, torch::Tensor desc, int64_t blocks) {
 std::vector<torch::Tensor> residual_ln_fwd(torch::Tensor x, torch::Tensor y, c10::optional<torch::Tensor> scale,
                                            c10::optional<torch::Tensor> mask, torch::Tensor gamma,
                                            torch::Tensor beta, double eps, int64_t T0, int64_t R0,
-                                           c10::optional<torch::Tensor> out) {
+                                           c10::optional<torch::Tensor> out, c10::optional<torch::Tensor> seed,
+                                           double rate) {
   CHECK_CUDA(x);
   TORCH_CHECK(x.dim() == 3 && x.stride(2) == 1, "x must be [B,T,D] with contiguous last dim");
   CHECK_DT(x, torch::kFloat32);
@@ -1108,7 +1132,7 @@ std::vector<torch::Tensor> residual_ln_fwd(torch::Tensor x, torch::Tensor y, c10
   check_rc(jm_residual_ln_fwd(x.data_ptr<float>(), x.stride(0), x.stride(1), bf(y), fopt(scale), fopt(mask),
                               x1.data_ptr<float>(), x1.stride(0), x1.stride(1), bfm(h), mean.data_ptr<float>(),
                               rstd.data_ptr<float>(), B, T, T0, D, gamma.data_ptr<float>(), beta.data_ptr<float>(),
-                              (float)eps, stream(), (int)R0),
+                              (float)eps, stream(), (int)R0, make_drop(seed, rate, y, 0)),
            "residual_ln_fwd");
   return {x1, h, mean, rstd};
 }
@@ -1138,7 +1162,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("gamma"), py::arg("dgamma"), py::arg("dbeta"), py::arg("accum"), py::arg("dres") = py::none(),
         py::arg("out") = py::none(), py::arg("res_y") = py::none(), py::arg("res_scale") = py::none(),
         py::arg("res_mask") = py::none(), py::arg("res_dscale") = py::none(), py::arg("res_dbias") = py::none(),
-        py::arg("res_T0") = 0, py::arg("res_out") = py::none());
+        py::arg("res_T0") = 0, py::arg("res_out") = py::none(), py::arg("res_seed") = py::none(),
+        py::arg("res_rate") = 0.0, py::arg("res_ioff") = 0);
   m.def("gelu_fwd", &gelu_fwd);
   m.def("dropout_apply", &dropout_apply);
   m.def("dropout_apply_", &dropout_apply_);
@@ -1151,12 +1176,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("splitk_reduce_add", &splitk_reduce_add);
   m.def("residual_ln_fwd", &residual_ln_fwd, py::arg("x"), py::arg("y"), py::arg("scale"), py::arg("mask"),
         py::arg("gamma"), py::arg("beta"), py::arg("eps"), py::arg("T0"), py::arg("R0") = 0,
-        py::arg("out") = py::none());
+        py::arg("out") = py::none(), py::arg("seed") = py::none(), py::arg("rate") = 0.0);
   m.def("transpose_bf16", &transpose_bf16);
   m.def("residual_fwd", &residual_fwd, py::arg("x"), py::arg("y"), py::arg("scale"), py::arg("mask"),
-        py::arg("out") = py::none());
+        py::arg("out") = py::none(), py::arg("seed") = py::none(), py::arg("rate") = 0.0, py::arg("ioff") = 0);
   m.def("residual_bwd", &residual_bwd, py::arg("dout"), py::arg("y"), py::arg("scale"), py::arg("mask"),
-        py::arg("dscale"), py::arg("ydtype"), py::arg("dbias") = py::none(), py::arg("out") = py::none());
+        py::arg("dscale"), py::arg("ydtype"), py::arg("dbias") = py::none(), py::arg("out") = py::none(),
+        py::arg("seed") = py::none(), py::arg("rate") = 0.0, py::arg("ioff") = 0);
   m.def("attn_fwd", &attn_fwd, py::arg("qkv"), py::arg("heads"), py::arg("seed") = py::none(), py::arg("rate") = 0.0);
   m.def("attn_bwd", &attn_bwd, py::arg("dO"), py::arg("qkv"), py::arg("o"), py::arg("lse"), py::arg("heads"),
         py::arg("dbias") = py::none(), py::arg("seed") = py::none(), py::arg("rate") = 0.0);
@@ -1181,7 +1207,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("deriv") = false);
   m.def("gemm_nt_f32", &gemm_nt_f32, py::arg("A"), py::arg("B"));
   m.def("gemm_nt", &gemm_nt, py::arg("A"), py::arg("B"), py::arg("bias") = py::none(), py::arg("gelu") = false,
-        py::arg("gelu_only") = false, py::arg("gelu_deriv") = false);
+        py::arg("gelu_only") = false, py::arg("gelu_deriv") = false, py::arg("seed") = py::none(),
+        py::arg("rate") = 0.0);
   m.def("opt_sumsq", &opt_sumsq);
   m.def("opt_adamw", &opt_adamw);
   m.def("opt_lamb_phase1", &opt_lamb_phase1);

@@ -5,6 +5,8 @@
 #include <hip/hip_bf16.h>
 #include <stdint.h>
 
+#include "jm_api.h"
+
 #define JM_DEVICE __device__ __forceinline__
 
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8_t;
@@ -33,6 +35,21 @@ JM_DEVICE uint32_t drop_hash(uint32_t j, uint64_t seed) {
 JM_DEVICE bool drop_keep_half(uint32_t h, int odd, uint32_t thr) { return (odd ? (h >> 16) : (h & 0xffffu)) < thr; }
 JM_DEVICE bool drop_keep(uint64_t seed, uint64_t idx, uint32_t thr) {
   return drop_keep_half(drop_hash((uint32_t)(idx >> 1), seed), (int)(idx & 1), thr);
+}
+
+// Dense-output dropout applied where the branch output is consumed (the residual kernels): the
+// element at y + o (o = y's own element offset) has mask index ioff + o in the branch tensor.
+using DropIO = JmDrop;  // seed null: no dropout; scale = 1 / keep
+// f[j] = keep(idx + j) / keep for W consecutive elements (idx even, W even)
+template <int W>
+JM_DEVICE void drop_factors(const DropIO& d, long idx, float* f) {
+  const uint64_t seed = (uint64_t)d.seed[0];
+#pragma unroll
+  for (int j = 0; j < W; j += 2) {
+    const uint32_t h = drop_hash((uint32_t)((idx + j) >> 1), seed);
+    f[j] = drop_keep_half(h, 0, d.thr) ? d.scale : 0.f;
+    f[j + 1] = drop_keep_half(h, 1, d.thr) ? d.scale : 0.f;
+  }
 }
 
 JM_DEVICE uint16_t f2bf(float f) {

@@ -52,7 +52,8 @@ __global__ __launch_bounds__(256) void rowcol_kernel(const void* __restrict__ in
                                                      uint16_t* __restrict__ out, float* __restrict__ acc,
                                                      const float* __restrict__ scale, const float* __restrict__ mask,
                                                      int M, int N, int T, int rows_per_block, long sB, long sT,
-                                                     float* __restrict__ acc2, long yB, long yT, int cw) {
+                                                     float* __restrict__ acc2, long yB, long yT, int cw,
+                                                     DropIO drop) {
   extern __shared__ __attribute__((aligned(16))) float red_s[];  // [2][<= 2048] block's columns
   // 2-D grid: blockIdx.y picks a chunk of cw (<= 2048, % 8 == 0) columns, blockIdx.x a slab of rows
   const int c0 = blockIdx.y * cw;
@@ -122,11 +123,12 @@ __global__ __launch_bounds__(256) void rowcol_kernel(const void* __restrict__ in
             }
             store8(out + off, b[u]);
           } else {
-            float o[8];
+            float o[8], f[8] = {1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f};
             const float m = mask ? mask[r / T] : 1.f;
+            if (drop.seed) drop_factors<8>(drop, drop.ioff + (r / T) * yB + (r % T) * yT + col, f);
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
-              const float md = m * a[u][j];
+              const float md = m * a[u][j] * f[j];  // f: the dropout of y
               o[j] = md * sc[j];
               if (scale) s[j] += md * b[u][j];
               s2[j] += bf2f(f2bf(o[j]));  // colsum of the bf16 values the GEMMs consume
@@ -156,7 +158,7 @@ __global__ __launch_bounds__(256) void residual_fwd_kernel(const float* __restri
                                                            const uint16_t* __restrict__ y,
                                                            const float* __restrict__ scale,
                                                            const float* __restrict__ mask, float* __restrict__ out,
-                                                           int rows, int D, long oB, long oT) {
+                                                           int rows, int D, long oB, long oT, DropIO drop) {
   const int cgs = D / 8;
   const long total = (long)rows * cgs;
   for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
@@ -166,6 +168,12 @@ __global__ __launch_bounds__(256) void residual_fwd_kernel(const float* __restri
     float xv[8], yv[8], sc[8];
     load8(x + b * sB + t * sT + col, xv);
     load8(y + (long)row * D + col, yv);
+    if (drop.seed) {
+      float f[8];
+      drop_factors<8>(drop, drop.ioff + (long)row * D + col, f);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) yv[j] *= f[j];
+    }
     const float m = mask ? mask[b] : 1.f;
     if (scale) {
       load8(scale + col, sc);
@@ -189,7 +197,7 @@ int grid_for(long work, int per_thread_items = 1) {
 template <int MODE>
 void launch_rowcol(const void* in0, const uint16_t* in1, uint16_t* out, float* acc, const float* scale,
                    const float* mask, int M, int N, int T, hipStream_t st, long sB = 0, long sT = 0,
-                   float* acc2 = nullptr, long yB = -1, long yT = -1) {
+                   float* acc2 = nullptr, long yB = -1, long yT = -1, JmDrop drop = JmDrop{nullptr, 0u, 1.f, 0}) {
   if (yB < 0) {  // y / out contiguous [M, N]
     yB = (long)T * N;
     yT = N;
@@ -230,7 +238,7 @@ void launch_rowcol(const void* in0, const uint16_t* in1, uint16_t* out, float* a
   if (nb < 1) nb = 1;
   const size_t smem = (acc || acc2) ? 4096 * sizeof(float) : 0;
   rowcol_kernel<MODE><<<dim3(nb, ncol), 256, smem, st>>>(in0, in1, out, acc, scale, mask, M, N, T, rows_per_block,
-                                                          sB, sT, acc2, yB, yT, cw);
+                                                          sB, sT, acc2, yB, yT, cw, drop);
 }
 
 }  // namespace
@@ -258,17 +266,18 @@ int jm_colsum_bf16(const uint16_t* x, float* acc, int M, int N, hipStream_t st) 
 }
 
 int jm_residual_fwd(const float* x, long sB, long sT, int B, int T, int D, const uint16_t* y, const float* scale,
-                    const float* mask, float* out, long oB, long oT, hipStream_t st) {
+                    const float* mask, float* out, long oB, long oT, hipStream_t st, JmDrop drop) {
   if (D % 8) return -1;
   const long work = (long)B * T * (D / 8);
-  residual_fwd_kernel<<<grid_for(work), 256, 0, st>>>(x, sB, sT, T, y, scale, mask, out, B * T, D, oB, oT);
+  residual_fwd_kernel<<<grid_for(work), 256, 0, st>>>(x, sB, sT, T, y, scale, mask, out, B * T, D, oB, oT, drop);
   return 0;
 }
 
 int jm_residual_bwd(const float* dout, long dB, long dT, const uint16_t* y, const float* scale, const float* mask,
-                    float* dscale, uint16_t* dy, int B, int T, int D, float* dbias, long yB, long yT, hipStream_t st) {
+                    float* dscale, uint16_t* dy, int B, int T, int D, float* dbias, long yB, long yT, hipStream_t st,
+                    JmDrop drop) {
   if (D % 8) return -1;
-  launch_rowcol<2>(dout, y, dy, dscale, scale, mask, B * T, D, T, st, dB, dT, dbias, yB, yT);
+  launch_rowcol<2>(dout, y, dy, dscale, scale, mask, B * T, D, T, st, dB, dT, dbias, yB, yT, drop);
   return 0;
 }
 

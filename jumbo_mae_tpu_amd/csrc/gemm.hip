@@ -77,6 +77,23 @@ enum { EPI_STORE = 0, EPI_GELU = 1, EPI_DGELU = 2, EPI_PARTIAL = 3, EPI_GELU_ONL
 
 namespace {
 
+// FF hidden dropout of the EPI_GELU_D outputs (GemmEpi::dseed): W consecutive elements from flat
+// index idx0 (even), both gelu(h) and gelu'(h) times the keep bit / keep
+template <int W>
+JM_DEVICE void gelu_d_drop(const GemmEpi& ep, long idx0, float* g, float* d) {
+  const uint64_t seed = (uint64_t)ep.dseed[0];
+#pragma unroll
+  for (int j = 0; j < W; j += 2) {
+    const uint32_t h = drop_hash((uint32_t)((idx0 + j) >> 1), seed);
+    const float k0 = drop_keep_half(h, 0, ep.dthr) ? ep.dscale : 0.f;
+    const float k1 = drop_keep_half(h, 1, ep.dthr) ? ep.dscale : 0.f;
+    g[j] *= k0;
+    d[j] *= k0;
+    g[j + 1] *= k1;
+    d[j + 1] *= k1;
+  }
+}
+
 // acc[mt][nt][i] = C[mb + mt*16 + l16][nb + nt*16 + 4g + i]  (mt < MTW)
 template <int EPI, int NTW, int MTW = 8>
 JM_DEVICE void epilogue(const f32x4_t (&acc)[8][NTW], const GemmEpi& ep, int M, int N, int mb, int nb, int l16,
@@ -102,6 +119,7 @@ JM_DEVICE void epilogue(const f32x4_t (&acc)[8][NTW], const GemmEpi& ep, int M, 
         float gv[4], dv[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) gelu_and_grad_f(bf2f(f2bf(v[i])), gv[i], dv[i]);
+        if (ep.dseed) gelu_d_drop<4>(ep, (long)m * ep.ldo + n, gv, dv);
         store4(ep.out + (long)m * ep.ldo + n, dv);
         store4(ep.out2 + (long)m * ep.ldo + n, gv);
         continue;
@@ -254,6 +272,7 @@ JM_DEVICE void epilogue_lds(const f32x4_t (&acc)[8][NTW], const GemmEpi& ep, uin
 #pragma unroll
         for (int j = 0; j < 8; ++j) fh[j] = bf2f(h[j]);
         gelu_n<8, true, true>(fh, fg, fd);
+        if (ep.dseed) gelu_d_drop<8>(ep, (long)m * ep.ldo + n0 + c * 8, fg, fd);
         st16(ep.out + (long)m * ep.ldo + n0 + c * 8, pack8(fd), NTS);
         st16(ep.out2 + (long)m * ep.ldo + n0 + c * 8, pack8(fg), NTS);
       } else if (EPI == EPI_GELU_ONLY) {
@@ -857,6 +876,7 @@ JM_DEVICE void narrow_epilogue(const f32x4_t (&acc)[4][3], const GemmEpi& ep, ui
 #pragma unroll
         for (int j = 0; j < 8; ++j) fh[j] = bf2f(h[j]);
         gelu_n<8, true, true>(fh, fg, fd);
+        if (ep.dseed) gelu_d_drop<8>(ep, (long)m * ep.ldo + n, fg, fd);
         st16(o, pack8(fd), false);
         st16(ep.out2 + (long)m * ep.ldo + n, pack8(fg), false);
       } else if constexpr (EPI == EPI_GELU_ONLY) {

@@ -2,6 +2,16 @@
 #pragma once
 #include <cstdint>
 
+// Dense-output dropout applied by the residual kernels that consume the branch output y (ops/blocks.py
+// Drops): the element at y + o (y's own element offset o) is kept with common.h drop_keep(seed, ioff + o),
+// kept values scaled by 1 / keep.  seed null: no dropout.
+struct JmDrop {
+  const int64_t* seed;
+  uint32_t thr;
+  float scale;
+  long ioff;
+};
+
 // Fused residual backward riding on the LayerNorm backward (layernorm.hip, LnResIO):
 // for rows t >= T0, dy(b, t) = bf16(mask[b] * scale * dx(b, t)) at y/dy + b * yB + (t - T0) * yT,
 // dscale += colsum(mask * dx * y), dbias += colsum(dy).  scale / mask / dscale / dbias may be null.
@@ -14,6 +24,7 @@ struct JmLnRes {
   int T0;
   float* dscale;
   float* dbias;
+  JmDrop drop;  // y's dropout (dy and dscale use the masked y)
 };
 
 // Grouped weight-gradient launch (gemm_tn.hip jm_gemm_tn_group): n <= 4 independent TN problems
@@ -47,4 +58,9 @@ struct GemmEpi {
   int tail_S;
   int t_begin;
   int t_count;
+  // EPI_GELU_D: FF hidden dropout (ops/blocks.py Drops) -- both outputs times keep(seed, m * ldo + n)
+  // / keep (common.h drop_keep); dseed null: none
+  const int64_t* dseed;
+  uint32_t dthr;
+  float dscale;
 };

@@ -88,6 +88,7 @@ struct ResLnIO {
   uint16_t* h;        // [B*(T-T0), D]
   float* mean;
   float* rstd;
+  DropIO drop;        // dropout of y (mask index: y's own element offset)
 };
 
 // R0 > 0: only rows t >= R0 are residual targets (y holds [B*(T-R0), D] rows); rows t < R0 of x1
@@ -118,6 +119,12 @@ __global__ __launch_bounds__(256) void res_ln_fwd_kernel(ResLnIO io, int T, int 
         float yv[4], sc[4] = {1.f, 1.f, 1.f, 1.f};
         load4(yr + col, yv);
         if (io.scale) load4(io.scale + col, sc);
+        if (io.drop.seed) {
+          float f[4];
+          drop_factors<4>(io.drop, io.drop.ioff + (yr - io.y) + col, f);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) yv[j] *= f[j];
+        }
 #pragma unroll
         for (int j = 0; j < 4; ++j) v[i][j] = xv[j] + m * sc[j] * yv[j];
         store4(x1r + col, v[i]);
@@ -186,6 +193,7 @@ struct LnResIO {
   const float* scale;
   const float* mask;
   int T0;
+  DropIO drop;
 };
 
 // parameter-gradient outputs (null entries skipped): dgamma, dbeta, dscale, dbias
@@ -279,10 +287,11 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const TI* __restrict__ dy, 
         for (int j = 0; j < 4; ++j) o[j] = rs * (g[i][j] - sg - xh[i][j] * sgx) + rv[j];
         store4(dxr + col, o);
         if (RES && rrow) {
-          float d[4];
+          float d[4], f[4] = {1.f, 1.f, 1.f, 1.f};
+          if (rio.drop.seed) drop_factors<4>(rio.drop, rio.drop.ioff + yoff + col, f);
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
-            const float md = m * o[j];
+            const float md = m * o[j] * f[j];  // f: the dropout of y (d(y_pre) and dscale see it)
             d[j] = md * sc[i][j];
             if (rio.scale) acc_add(acc, 2, i, j, md * yv[i][j]);
             acc_add(acc, 3 % NP, i, j, bf2f(f2bf(d[j])));  // colsum of the bf16 values the GEMMs consume
@@ -607,8 +616,9 @@ int jm_layernorm_fwd(const float* x, long sB, long sT, int B, int T, int D, cons
 
 int jm_residual_ln_fwd(const float* x, long sB, long sT, const uint16_t* y, const float* scale, const float* mask,
                        float* x1, long oB, long oT, uint16_t* h, float* mean, float* rstd, int B, int T, int T0,
-                       int D, const float* gamma, const float* beta, float eps, hipStream_t st, int R0) {
-  const ResLnIO io{x, sB, sT, y, scale, mask, x1, oB, oT, h, mean, rstd};
+                       int D, const float* gamma, const float* beta, float eps, hipStream_t st, int R0,
+                       JmDrop drop) {
+  const ResLnIO io{x, sB, sT, y, scale, mask, x1, oB, oT, h, mean, rstd, drop};
   if (R0 < 0 || R0 >= T) return -2;
   const int V = pick_v(D);
   if (V < 0 || (D % 4) != 0) return -1;
@@ -672,8 +682,8 @@ int jm_layernorm_bwd(const void* dy, int dy_bf16, const float* x, long sB, long 
   const ParamOuts outs{{accum_params ? dgamma : nullptr, accum_params ? dbeta : nullptr,
                         res ? res->dscale : nullptr, res ? res->dbias : nullptr}};
   float* wsk = ws;
-  LnResIO rio{nullptr, nullptr, 0, 0, nullptr, nullptr, 0};
-  if (res) rio = LnResIO{res->y, res->dy, res->yB, res->yT, res->scale, res->mask, res->T0};
+  LnResIO rio{nullptr, nullptr, 0, 0, nullptr, nullptr, 0, JmDrop{nullptr, 0u, 1.f, 0}};
+  if (res) rio = LnResIO{res->y, res->dy, res->yB, res->yT, res->scale, res->mask, res->T0, res->drop};
   if (dy_bf16) {
     if (res)
       launch_bwd<uint16_t, true>(V, grid, smem, st, (const uint16_t*)dy, x, sB, sT, T, rows, D, mean, rstd, gamma,

@@ -99,15 +99,15 @@ def _attn_fwd(attn, h1, B, S, dr: Drops | None = None):
     qkv = P.linear_fwd(h1, attn.qkv_k, attn.qkv_b)
     o, lse = P.attn_fwd(qkv.view(B, S, -1), attn.heads, drop=(dr.attn, dr.rate) if dr is not None else None)
     a = P.linear_fwd(o.view(B * S, -1), attn.wo_k, attn.wo_b)
-    if dr is not None:
-        Dr.apply_(a, dr.wo, dr.rate)
     return qkv, o, lse, a
 
 
+def _od(dr: Drops | None, name: str, base):
+    """The residual kernels' descriptor of a Dense output's dropout: (seed, rate, branch tensor)."""
+    return None if dr is None else (getattr(dr, name), dr.rate, base)
+
+
 def _attn_bwd(attn, da, h1, qkv, o, lse, B, S, wo_bias_done=False, dr: Drops | None = None):
-    if dr is not None:  # d(Wo output) = mask * d(dropped output); its bias gradient from the masked one
-        Dr.apply_(da, dr.wo, dr.rate)
-        wo_bias_done = False
     do = P.linear_bwd(da, o.view(B * S, -1), attn.wo_k, attn.wo_b, bias_done=wo_bias_done)
     dqkv, bd = P.attn_bwd(do, qkv.view(B, S, -1), o, lse, attn.heads, attn.qkv_b,
                           drop=(dr.attn, dr.rate) if dr is not None else None)
@@ -116,18 +116,18 @@ def _attn_bwd(attn, da, h1, qkv, o, lse, B, S, wo_bias_done=False, dr: Drops | N
 
 def _ff_fwd(ff, h, train=True, rate=0.0, sh=None, so=None):
     """(saved, gelu, y, deriv): ``saved`` is gelu'(pre) when ``deriv`` (fused MFMA forward), else pre.
-    With dropout seeds ``sh`` / ``so`` the hidden gelu(h) and gelu'(h) are masked together (saved
-    is then always the masked gelu') and the output y is masked in place."""
-    pre, g, deriv = P.linear_gelu_fwd_saved(h, ff.w1.k, ff.w1.b, need_pre=train)
-    if sh is not None:
+    With the dropout seed ``sh`` the hidden gelu(h) and gelu'(h) are masked together (in the GEMM
+    epilogue, or one pass after; saved is then always the masked gelu').  The output's dropout is
+    applied by the residual kernels that read y (``_od``)."""
+    pre, g, deriv, dropped = P.linear_gelu_fwd_saved(h, ff.w1.k, ff.w1.b, need_pre=train,
+                                                     drop=(sh, rate) if sh is not None else None)
+    if sh is not None and not dropped:
         if deriv:
             Dr.gelu_drop(g, pre, sh, rate)
         else:
             g, pre = Dr.gelu_drop(pre, None, sh, rate)
             deriv = True
-    y = P.linear_fwd(g, ff.w2.k, ff.w2.b)
-    if so is not None:
-        Dr.apply_(y, so, rate)
+    y = P.linear_fwd(g, ff.w2.k, ff.w2.b)  # its dropout (seed so) is applied where y is consumed
     return pre, g, y, deriv
 
 
@@ -161,7 +161,8 @@ class JumboBlockFn(torch.autograd.Function):
         h1, mu1, rs1 = _ln1_fwd(x, layer, link_in, dt)
         qkv, o, lse, a = _attn_fwd(layer.attn, h1, B, S, dr)
         # residual + LN2 of the patch rows in one pass
-        x1, hp, mup, rsp = P.residual_ln_fwd(x, a, layer.scale1, m1, layer.norm2.g, layer.norm2.b, C)
+        x1, hp, mup, rsp = P.residual_ln_fwd(x, a, layer.scale1, m1, layer.norm2.g, layer.norm2.b, C,
+                                             drop=_od(dr, "wo", a))
         # jumbo branch: LN3 on the concatenated CLS tokens, residual on the *normalized* value
         cls_in = x1[:, :C].reshape(B, 1, J)
         # fp32 hc for the residual and its compute-dtype copy for the jumbo MLP, one pass
@@ -172,21 +173,22 @@ class JumboBlockFn(torch.autograd.Function):
         pin = x1[:, C:]
         fpre, fg, fy, fd = _ff_fwd(layer.ff, hp, train, rate, dr and dr.fh, dr and dr.fo)
         x2 = torch.empty_like(x1)
-        P.residual_fwd(hc.view(B, 1, J), jy, layer.scale3, m3, out=x2[:, :C].reshape(B, 1, J))
+        P.residual_fwd(hc.view(B, 1, J), jy, layer.scale3, m3, out=x2[:, :C].reshape(B, 1, J), drop=_od(dr, "jo", jy))
         nl = link_out.ln1 if link_out is not None else None
         if nl is not None:  # patch-row residual + the upper block's LN1 over all rows, one pass
-            _, h1n, mun, rsn = P.residual_ln_fwd(x1, fy, layer.scale2, m2, nl[0], nl[1], 0, C, out=x2)
+            _, h1n, mun, rsn = P.residual_ln_fwd(x1, fy, layer.scale2, m2, nl[0], nl[1], 0, C, out=x2,
+                                                 drop=_od(dr, "fo", fy))
             link_out.put_h1(x2, h1n, mun, rsn)
         else:
-            P.residual_fwd(pin, fy, layer.scale2, m2, out=x2[:, C:])
+            P.residual_fwd(pin, fy, layer.scale2, m2, out=x2[:, C:], drop=_od(dr, "fo", fy))
         ctx.save_for_backward(x, mu1, rs1, h1, qkv, o, lse, a, x1, muc, rsc, hcb, jpre, jg, jy,
                               hp, mup, rsp, fpre, fg, fy, m1, m2, m3)
         ctx.layer = layer
         ctx.link_in, ctx.link_out = link_in, link_out
         ctx.gelu_deriv = (jd, fd)  # FF1 saved gelu'(h) instead of h (jumbo MLP, patch FF)
         ctx.dr = dr
-        if link_out is not None:  # with dropout the FF2 bias gradient waits for the masked dy
-            link_out.spec = P.ResSpec(fy, layer.scale2, m2, layer.ff.w2.b if dr is None else None, C)
+        if link_out is not None:
+            link_out.spec = P.ResSpec(fy, layer.scale2, m2, layer.ff.w2.b, C, drop=_od(dr, "fo", fy))
         return x2
 
     @staticmethod
@@ -212,9 +214,7 @@ def _jumbo_bwd(ctx, dx2):
     da3 = da.view(B, S, D)
     # ---- jumbo branch: d hc = dx2_cls + JumboMLP'(s3 * dp3 * dx2_cls); dx1_cls = LN3'(d hc)
     dcls = dx2[:, :C].reshape(B, 1, J)
-    djy, bd = P.residual_bwd(dcls, jy, layer.scale3, m3, dt, layer.jumbo_mlp.w2.b if dr is None else None)
-    if dr is not None:
-        Dr.apply_(djy, dr.jo, dr.rate)
+    djy, bd = P.residual_bwd(dcls, jy, layer.scale3, m3, dt, layer.jumbo_mlp.w2.b, drop=_od(dr, "jo", jy))
     # d hc = dcls + JumboMLP'(...) in fp32, the add fused into the jumbo dgrad's split-K reduce
     dhc = _ff_bwd(layer.jumbo_mlp, djy, hcb, jpre, jg, bd, dx_add=dcls.reshape(B, J),
                   deriv=ctx.gelu_deriv[0])
@@ -222,22 +222,20 @@ def _jumbo_bwd(ctx, dx2):
              out=dx1[:, :C].reshape(B, 1, J))
     # attention-residual backward of the CLS rows (the patch rows ride on LN2' below, which
     # also marks scale1 ready: it must come last)
-    P.residual_bwd(dx1[:, :C], a3[:, :C], layer.scale1, m1, dt, layer.attn.wo_b if dr is None else None,
-                   out=da3[:, :C], mark_ready=False)
+    P.residual_bwd(dx1[:, :C], a3[:, :C], layer.scale1, m1, dt, layer.attn.wo_b, out=da3[:, :C], mark_ready=False,
+                   drop=_od(dr, "wo", a))
     # ---- patch branch: dx1[:, C:] = dx2[:, C:] + LN2'(FF'(s2 * dp2 * dx2[:, C:]))
     fused = ctx.link_out.take(dx2) if ctx.link_out is not None else None
     if fused is not None:  # computed by the upper block's LN1 backward
         dfy, bd = fused
     else:
-        dfy, bd = P.residual_bwd(dx2[:, C:], fy, layer.scale2, m2, dt, layer.ff.w2.b if dr is None else None)
-    if dr is not None:
-        Dr.apply_(dfy, dr.fo, dr.rate)
+        dfy, bd = P.residual_bwd(dx2[:, C:], fy, layer.scale2, m2, dt, layer.ff.w2.b, drop=_od(dr, "fo", fy))
     dhp = _ff_bwd(layer.ff, dfy, hp, fpre, fg, bd, deriv=ctx.gelu_deriv[1])
     # ... and the attention-residual backward of those rows in the same pass
     _, _, bd = P.ln_bwd(dhp, x1[:, C:], mup, rsp, layer.norm2.g, layer.norm2.b, dres=dx2[:, C:],
                         out=dx1[:, C:],
-                        res=P.ResSpec(a3[:, C:], layer.scale1, m1, layer.attn.wo_b if dr is None else None, 0,
-                                      da3[:, C:]))
+                        res=P.ResSpec(a3[:, C:], layer.scale1, m1, layer.attn.wo_b, 0, da3[:, C:],
+                                      drop=_od(dr, "wo", a)))
     # ---- attention branch: dx = dx1 + LN1'(Attn'(s1 * dp1 * dx1))
     dh1 = _attn_bwd(layer.attn, da, h1, qkv, o, lse, B, S, bd, dr)
     return _ln1_bwd(ctx, dh1, x, mu1, rs1, layer, dx1)
@@ -279,22 +277,23 @@ class ViTBlockFn(torch.autograd.Function):
         dt = layer.norm1.g.store.compute_dtype
         h1, mu1, rs1 = _ln1_fwd(x, layer, link_in, dt)
         qkv, o, lse, a = _attn_fwd(layer.attn, h1, B, S, dr)
-        x1, h2, mu2, rs2 = P.residual_ln_fwd(x, a, layer.scale1, m1, layer.norm2.g, layer.norm2.b, 0)
+        x1, h2, mu2, rs2 = P.residual_ln_fwd(x, a, layer.scale1, m1, layer.norm2.g, layer.norm2.b, 0,
+                                             drop=_od(dr, "wo", a))
         fpre, fg, fy, fd = _ff_fwd(layer.ff, h2, train, dr.rate if dr is not None else 0.0, dr and dr.fh,
                                    dr and dr.fo)
         nl = link_out.ln1 if link_out is not None else None
         if nl is not None:  # last residual + the upper block's LN1, one pass
-            x2, h1n, mun, rsn = P.residual_ln_fwd(x1, fy, layer.scale2, m2, nl[0], nl[1], 0)
+            x2, h1n, mun, rsn = P.residual_ln_fwd(x1, fy, layer.scale2, m2, nl[0], nl[1], 0, drop=_od(dr, "fo", fy))
             link_out.put_h1(x2, h1n, mun, rsn)
         else:
-            x2 = P.residual_fwd(x1, fy, layer.scale2, m2)
+            x2 = P.residual_fwd(x1, fy, layer.scale2, m2, drop=_od(dr, "fo", fy))
         ctx.save_for_backward(x, mu1, rs1, h1, qkv, o, lse, a, x1, mu2, rs2, h2, fpre, fg, fy, m1, m2)
         ctx.layer = layer
         ctx.link_in, ctx.link_out = link_in, link_out
         ctx.gelu_deriv = (False, fd)
         ctx.dr = dr
         if link_out is not None:
-            link_out.spec = P.ResSpec(fy, layer.scale2, m2, layer.ff.w2.b if dr is None else None, 0)
+            link_out.spec = P.ResSpec(fy, layer.scale2, m2, layer.ff.w2.b, 0, drop=_od(dr, "fo", fy))
         return x2
 
     @staticmethod
@@ -315,13 +314,11 @@ def _vit_bwd(ctx, dx2):
     if fused is not None:  # computed by the upper block's LN1 backward
         dfy, bd = fused
     else:
-        dfy, bd = P.residual_bwd(dx2, fy, layer.scale2, m2, dt, layer.ff.w2.b if dr is None else None)
-    if dr is not None:
-        Dr.apply_(dfy, dr.fo, dr.rate)
+        dfy, bd = P.residual_bwd(dx2, fy, layer.scale2, m2, dt, layer.ff.w2.b, drop=_od(dr, "fo", fy))
     dh2 = _ff_bwd(layer.ff, dfy, h2, fpre, fg, bd, deriv=ctx.gelu_deriv[1])
     # LN2' with the attention-residual backward of its dx fused in (never write autograd's dx2)
     dx1, da, bd = P.ln_bwd(dh2, x1, mu2, rs2, layer.norm2.g, layer.norm2.b, dres=dx2,
-                           res=P.ResSpec(a, layer.scale1, m1, layer.attn.wo_b if dr is None else None))
+                           res=P.ResSpec(a, layer.scale1, m1, layer.attn.wo_b, drop=_od(dr, "wo", a)))
     dh1 = _attn_bwd(layer.attn, da, h1, qkv, o, lse, B, S, bd, dr)
     return _ln1_bwd(ctx, dh1, x, mu1, rs1, layer, dx1)
 

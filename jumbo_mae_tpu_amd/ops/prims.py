@@ -235,18 +235,23 @@ def linear_gelu_fwd(x2: torch.Tensor, hw: Handle, hb: Handle | None, need_pre: b
 _GELU_DERIV = True
 
 
-def linear_gelu_fwd_saved(x2: torch.Tensor, hw: Handle, hb: Handle | None, need_pre: bool = True):
-    """Like ``linear_gelu_fwd`` but returns (saved, gelu(h), deriv): on the fused MFMA path the
-    epilogue computes gelu(h) and gelu'(h) from one tanh and ``saved`` is gelu'(h) (deriv True),
+def linear_gelu_fwd_saved(x2: torch.Tensor, hw: Handle, hb: Handle | None, need_pre: bool = True, drop=None):
+    """Like ``linear_gelu_fwd`` but returns (saved, gelu(h), deriv, dropped): on the fused MFMA path
+    the epilogue computes gelu(h) and gelu'(h) from one tanh and ``saved`` is gelu'(h) (deriv True),
     so the backward's data-gradient epilogue multiplies instead of re-deriving it from h;
-    otherwise ``saved`` is h (deriv False)."""
+    otherwise ``saved`` is h (deriv False).  ``drop`` = (seed, rate): hidden dropout applied to both
+    outputs inside that epilogue (dropped True); the other paths leave it to the caller."""
     w = hw.weight()
     if (_GELU_DERIV and need_pre and hip(x2) and x2.dtype == torch.bfloat16
             and use_our_gemm(x2.shape[0], w.shape[0], x2.shape[1], True)):
-        gp, g = _ext.load().gemm_nt(x2, w, hb.master if hb is not None else None, True, False, True)
-        return gp, g, True
+        bias = hb.master if hb is not None else None
+        if drop is not None:
+            gp, g = _ext.load().gemm_nt(x2, w, bias, True, False, True, drop[0], drop[1])
+            return gp, g, True, True
+        gp, g = _ext.load().gemm_nt(x2, w, bias, True, False, True)
+        return gp, g, True, False
     pre, g = linear_gelu_fwd(x2, hw, hb, need_pre)
-    return pre, g, False
+    return pre, g, False, False
 
 
 # ------------------------------------------------------------------ weight-gradient stream
@@ -520,13 +525,33 @@ class ResSpec(NamedTuple):
     """Residual backward that consumes a LayerNorm backward's dx (fused into it by ``ln_bwd``):
     for rows t >= t0, dy = mask[b] * s * dx in bf16; s.grad += colsum(mask * dx * y);
     hbias.grad += colsum(dy).  ``y`` is the branch output of those rows ([B*(T-t0), D] contiguous
-    or a [B, T-t0, D] view); ``out`` an optional destination view with y's layout."""
+    or a [B, T-t0, D] view); ``out`` an optional destination view with y's layout; ``drop`` the
+    branch output's dropout (see ``_drop_args``)."""
     y: torch.Tensor
     hs: Handle | None
     mask: torch.Tensor | None
     hbias: Handle | None
     t0: int = 0
     out: torch.Tensor | None = None
+    drop: tuple | None = None
+
+
+def _drop_args(y: torch.Tensor, drop) -> tuple:
+    """Kernel arguments (seed, rate, ioff) of the Dense-output dropout ``drop`` = (seed, rate, base):
+    the mask indexes the branch tensor ``base`` (flat), ``y`` is a view of it."""
+    if drop is None:
+        return None, 0.0, 0
+    seed, rate, base = drop
+    return seed, rate, y.storage_offset() - base.storage_offset()
+
+
+def _drop_factor(y: torch.Tensor, drop) -> torch.Tensor:
+    """fp32 keep / keep_p factors in ``y``'s layout (CPU path of the residual kernels' dropout)."""
+    from . import dropout as Dr
+    seed, rate, base = drop
+    _, scale = Dr.keep_threshold(rate)
+    full = Dr.keep_mask(seed.cpu(), base.numel(), rate).to(y.device).float() * scale
+    return full.as_strided(y.shape, y.stride(), y.storage_offset() - base.storage_offset())
 
 
 def ln_bwd(dy: torch.Tensor, x3: torch.Tensor, mean, rstd, hg: Handle, hb: Handle, dres=None, out=None,
@@ -542,10 +567,11 @@ def ln_bwd(dy: torch.Tensor, x3: torch.Tensor, mean, rstd, hg: Handle, hb: Handl
     if hip(x3):
         if fused:
             hs, hbias = res.hs, res.hbias
+            dseed, drate, dioff = _drop_args(res.y, res.drop)
             dx, dyr = _ext.load().layernorm_bwd(
                 dy, x3, mean, rstd, hg.master, hg.grad, hb.grad, tr, dres, out, res.y,
                 hs.master if hs is not None else None, res.mask, hs.grad if _trainable(hs) else None,
-                hbias.grad if _trainable(hbias) else None, res.t0, res.out)
+                hbias.grad if _trainable(hbias) else None, res.t0, res.out, dseed, drate, dioff)
         else:
             dx = _ext.load().layernorm_bwd(dy, x3, mean, rstd, hg.master, hg.grad, hb.grad, tr, dres, out)[0]
     else:
@@ -572,17 +598,25 @@ def ln_bwd(dy: torch.Tensor, x3: torch.Tensor, mean, rstd, hg: Handle, hb: Handl
         if _trainable(res.hs):
             res.hs.ready()
         return dx, dyr, _trainable(res.hbias)
-    dyr, done = residual_bwd(dx[:, res.t0:], res.y, res.hs, res.mask, res.y.dtype, res.hbias, out=res.out)
+    dyr, done = residual_bwd(dx[:, res.t0:], res.y, res.hs, res.mask, res.y.dtype, res.hbias, out=res.out,
+                             drop=res.drop)
     return dx, dyr, done
 
 
 # ------------------------------------------------------------------------------ residual
-def residual_fwd(x3: torch.Tensor, y2: torch.Tensor, hs: Handle | None, mask, out=None) -> torch.Tensor:
-    """out[b,t] = x[b,t] + mask[b] * s * y[b*T+t]  (x, out: fp32 [B,T,D] views)."""
+def residual_fwd(x3: torch.Tensor, y2: torch.Tensor, hs: Handle | None, mask, out=None, drop=None) -> torch.Tensor:
+    """out[b,t] = x[b,t] + mask[b] * s * y[b*T+t]  (x, out: fp32 [B,T,D] views); ``drop``: the
+    dropout of y (seed, rate, base tensor), applied as y is read."""
     B, T, D = x3.shape
     if hip(x3):
-        return _ext.load().residual_fwd(x3, y2.reshape(B * T, D), hs.master if hs is not None else None, mask, out)
-    r = y2.float().reshape(B, T, D)
+        y2r = y2.reshape(B * T, D)
+        dseed, drate, dioff = _drop_args(y2r, drop)
+        return _ext.load().residual_fwd(x3, y2r, hs.master if hs is not None else None, mask, out, dseed, drate,
+                                        dioff)
+    r = y2.float()
+    if drop is not None:
+        r = r * _drop_factor(y2, drop)
+    r = r.reshape(B, T, D)
     if hs is not None:
         r = r * hs.master
     if mask is not None:
@@ -595,41 +629,48 @@ def residual_fwd(x3: torch.Tensor, y2: torch.Tensor, hs: Handle | None, mask, ou
 
 
 def residual_ln_fwd(x3: torch.Tensor, y2: torch.Tensor, hs: Handle | None, mask, hg: Handle, hb: Handle,
-                    t0: int = 0, r0: int = 0, out: torch.Tensor | None = None):
+                    t0: int = 0, r0: int = 0, out: torch.Tensor | None = None, drop=None):
     """x1 = x + mask*s*y (fresh [B,T,D] fp32, or ``out``) and the LayerNorm of its rows t >= t0 in
     one pass: returns (x1, h [B*(T-t0), D] bf16, mean, rstd).  The fused kernel saves the LN's re-read
     of x1.  ``r0 > 0``: only rows t >= r0 get the residual (``y2`` holds those rows); rows t < r0
     of ``out`` are already final and are only normalised."""
     B, T, D = x3.shape
     if hip(x3) and y2.dtype == torch.bfloat16:
+        if drop is not None:  # the kernel indexes y's own rows: y must be its branch tensor
+            assert y2.data_ptr() == drop[2].data_ptr() and y2.numel() == drop[2].numel()
         return tuple(_ext.load().residual_ln_fwd(x3, y2.reshape(B * (T - r0), D),
                                                  hs.master if hs is not None else None, mask, hg.master, hb.master,
-                                                 LN_EPS, t0, r0, out))
+                                                 LN_EPS, t0, r0, out, drop[0] if drop else None,
+                                                 drop[1] if drop else 0.0))
     if r0 == 0 and out is None:
-        x1 = residual_fwd(x3, y2, hs, mask)
+        x1 = residual_fwd(x3, y2, hs, mask, drop=drop)
     else:
         x1 = out if out is not None else torch.empty_like(x3)
-        residual_fwd(x3[:, r0:], y2, hs, mask, out=x1[:, r0:])
+        residual_fwd(x3[:, r0:], y2, hs, mask, out=x1[:, r0:], drop=drop)
     h, mean, rstd = ln_fwd(x1[:, t0:], hg, hb, hg.store.compute_dtype)
     return x1, h, mean, rstd
 
 
 def residual_bwd(dout3: torch.Tensor, y2: torch.Tensor | None, hs: Handle | None, mask, ydtype,
-                 hbias: Handle | None = None, out: torch.Tensor | None = None, mark_ready: bool = True):
+                 hbias: Handle | None = None, out: torch.Tensor | None = None, mark_ready: bool = True, drop=None):
     """dy = mask[b] * s * dout (in ``ydtype``); ds += sum mask*dout*y.  When ``hbias`` (the bias of
     the Dense that produced y) is given, its gradient colsum(dy) is fused into the same pass.
     ``y2``: [B*T, D] or a [B, T, D] view; ``out``: optional destination view with y2's layout.
     ``mark_ready=False`` leaves s's reducer readiness to a later contributor.  Returns (dy, bias_done)."""
     B, T, D = dout3.shape
     bg = hbias.grad if _trainable(hbias) else None
-    if hip(dout3) and ydtype == torch.bfloat16 and (hs is not None or mask is not None or bg is not None):
+    if hip(dout3) and ydtype == torch.bfloat16 and (hs is not None or mask is not None or bg is not None
+                                                    or drop is not None):
+        dseed, drate, dioff = _drop_args(y2 if y2 is not None else out, drop)
         dy = _ext.load().residual_bwd(dout3, y2, hs.master if hs is not None else None, mask,
-                                      hs.grad if _trainable(hs) else None, ydtype, bg, out)
+                                      hs.grad if _trainable(hs) else None, ydtype, bg, out, dseed, drate, dioff)
         done = bg is not None
     else:
         d = dout3.float()
         if mask is not None:
             d = d * mask.view(B, 1, 1)
+        if drop is not None:  # d(y_pre) = keep * d(y_dropped); the scale gradient sees the dropped y
+            d = d * _drop_factor(y2, drop).reshape(B, T, D)
         if hs is not None:
             if _trainable(hs):
                 hs.grad.add_((d * y2.float().reshape(B, T, D)).sum((0, 1)))
