@@ -283,42 +283,114 @@ int jm_residual_bwd(const float* dout, long dB, long dT, const uint16_t* y, cons
 
 // ---------------------------------------------------------------------------------------------
 // Split-K epilogue of the weight-gradient GEMMs: g[i] += sum_s part[s][i] (fp32), one pass.
+void jm_zero_f32(float* p, long n, hipStream_t st);
 namespace {
-// g[i] += sum_s part[s][i].  grid.y > 1 splits the S partials into slices that are summed with
-// atomics: used when n is small and S large (per-sample bias partials, n = 3D, S = batch).
+// g[i] += sum_s part[s][i], one thread per float4 column walking all S rows (n large).
 // ``ld``: row stride of part in floats (n for the packed partial slices, a strided view otherwise).
 __global__ __launch_bounds__(256) void splitk_reduce_add_kernel(const float* __restrict__ part,
                                                                 float* __restrict__ g, long n4, int S, long ld) {
   const long n = ld;
-  const int per = (S + gridDim.y - 1) / gridDim.y;
-  const int s0 = blockIdx.y * per;
-  const int s1 = min(S, s0 + per);
   for (long i = blockIdx.x * 256L + threadIdx.x; i < n4; i += (long)gridDim.x * 256) {
     float acc[4] = {0.f, 0.f, 0.f, 0.f};
-    int s = s0;
-    for (; s + 1 < s1; s += 2) {
+    int s = 0;
+    for (; s + 1 < S; s += 2) {
       float v[4], w[4];
       load4(part + (long)s * n + i * 4, v);
       load4(part + (long)(s + 1) * n + i * 4, w);
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[j] += v[j] + w[j];
     }
-    if (s < s1) {
+    if (s < S) {
       float v[4];
       load4(part + (long)s * n + i * 4, v);
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[j] += v[j];
     }
-    if (gridDim.y == 1) {
-      float o[4];
-      load4(g + i * 4, o);
+    float o[4];
+    load4(g + i * 4, o);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) o[j] += acc[j];
-      store4(g + i * 4, o);
-    } else {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) atomicAdd(g + i * 4 + j, acc[j]);
+    for (int j = 0; j < 4; ++j) o[j] += acc[j];
+    store4(g + i * 4, o);
+  }
+}
+
+// The same for few columns and many rows (per-sample bias partials: n = 3D, S = batch; token
+// partials): RL row lanes per column, each summing every RL-th row (4 loads in flight), then a
+// fixed-order LDS tree over the lanes -- the same bits on every run (the round-3 form split the
+// rows over grid.y slices summed with float atomics, whose order varies).
+// One workgroup per 256 / RL float4 columns; STORE: g = sum (g not read).
+template <int RL>
+__global__ __launch_bounds__(256) void colsum_rows_kernel(const float* __restrict__ part, float* __restrict__ g,
+                                                          long n4, int S, long ld, int store) {
+  constexpr int CW = 256 / RL;
+  __shared__ float4 red[256];
+  const int c = threadIdx.x % CW, rl = threadIdx.x / CW;
+  const long i = blockIdx.x * (long)CW + c;
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (i < n4) {
+    const float4* p = reinterpret_cast<const float4*>(part) + i;
+    const long l4 = ld / 4;
+    int s = rl;
+    for (; s + 3 * RL < S; s += 4 * RL) {
+      const float4 a = p[(long)s * l4], b = p[(long)(s + RL) * l4];
+      const float4 e = p[(long)(s + 2 * RL) * l4], f = p[(long)(s + 3 * RL) * l4];
+      acc.x += (a.x + b.x) + (e.x + f.x);
+      acc.y += (a.y + b.y) + (e.y + f.y);
+      acc.z += (a.z + b.z) + (e.z + f.z);
+      acc.w += (a.w + b.w) + (e.w + f.w);
     }
+    for (; s < S; s += RL) {
+      const float4 a = p[(long)s * l4];
+      acc.x += a.x;
+      acc.y += a.y;
+      acc.z += a.z;
+      acc.w += a.w;
+    }
+  }
+  red[threadIdx.x] = acc;
+  __syncthreads();
+#pragma unroll
+  for (int h = RL / 2; h >= 1; h >>= 1) {
+    if (rl < h) {
+      const float4 o = red[threadIdx.x + h * CW];
+      float4& r = red[threadIdx.x];
+      r.x += o.x;
+      r.y += o.y;
+      r.z += o.z;
+      r.w += o.w;
+    }
+    __syncthreads();
+  }
+  if (rl == 0 && i < n4) {
+    float4* gp = reinterpret_cast<float4*>(g) + i;
+    float4 o = store ? make_float4(0.f, 0.f, 0.f, 0.f) : *gp;
+    const float4 r = red[c];
+    o.x += r.x;
+    o.y += r.y;
+    o.z += r.z;
+    o.w += r.w;
+    *gp = o;
+  }
+}
+
+// column sums over S rows of stride ld into g (store: g = sum): the one-pass kernel when the
+// columns alone fill the chip, else colsum_rows_kernel with the row lanes sized to ~8 rows each
+void launch_colsum(const float* part, float* g, long n4, int S, long ld, int store, hipStream_t st) {
+  const long blocks = (n4 + 255) / 256;
+  if (blocks >= 512 || S < 16) {
+    if (store) jm_zero_f32(g, n4 * 4, st);
+    splitk_reduce_add_kernel<<<(unsigned)(blocks > 4096 ? 4096 : blocks), 256, 0, st>>>(part, g, n4, S, ld);
+    return;
+  }
+  int rl = 16;
+  while (rl < 256 && S > 8 * rl) rl *= 2;
+  const unsigned nb = (unsigned)((n4 * rl + 255) / 256);
+  switch (rl) {
+    case 16: colsum_rows_kernel<16><<<nb, 256, 0, st>>>(part, g, n4, S, ld, store); break;
+    case 32: colsum_rows_kernel<32><<<nb, 256, 0, st>>>(part, g, n4, S, ld, store); break;
+    case 64: colsum_rows_kernel<64><<<nb, 256, 0, st>>>(part, g, n4, S, ld, store); break;
+    case 128: colsum_rows_kernel<128><<<nb, 256, 0, st>>>(part, g, n4, S, ld, store); break;
+    default: colsum_rows_kernel<256><<<nb, 256, 0, st>>>(part, g, n4, S, ld, store); break;
   }
 }
 
@@ -378,12 +450,7 @@ int jm_splitk_reduce_add(const float* part, float* g, long n, int S, hipStream_t
       default: break;
     }
   }
-  if (store) jm_zero_f32(g, n, st);
-  long blocks = (n4 + 255) / 256;
-  if (blocks > 4096) blocks = 4096;
-  int ys = 1;  // slice the partials until the launch has ~512 workgroups of >= 8 rows each
-  while (blocks * ys < 512 && S / (ys * 2) >= 8) ys *= 2;
-  splitk_reduce_add_kernel<<<dim3((unsigned)blocks, ys), 256, 0, st>>>(part, g, n4, S, n);
+  launch_colsum(part, g, n4, S, n, store, st);
   return 0;
 }
 
@@ -391,12 +458,7 @@ int jm_splitk_reduce_add(const float* part, float* g, long n, int S, hipStream_t
 // gradients: the CLS rows of dx, the mask-token partials) added straight into the flat gradient
 int jm_colsum_add_f32(const float* x, long ld, int rows, long n, float* g, hipStream_t st) {
   if (n % 4 || ld % 4 || ld < n || rows < 1) return -1;
-  const long n4 = n / 4;
-  long blocks = (n4 + 255) / 256;
-  if (blocks > 4096) blocks = 4096;
-  int ys = 1;
-  while (blocks * ys < 512 && rows / (ys * 2) >= 8) ys *= 2;
-  splitk_reduce_add_kernel<<<dim3((unsigned)blocks, ys), 256, 0, st>>>(x, g, n4, rows, ld);
+  launch_colsum(x, g, n / 4, rows, ld, 0, st);
   return 0;
 }
 
