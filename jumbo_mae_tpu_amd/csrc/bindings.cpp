@@ -40,9 +40,10 @@ int jm_residual_ln_fwd(const float* x, long sB, long sT, const uint16_t* y, cons
                        int D, const float* gamma, const float* beta, float eps, hipStream_t st, int R0 = 0,
                        JmDrop drop = JmDrop{nullptr, 0u, 1.f, 0});
 int jm_gelu_fwd(const uint16_t* h, uint16_t* a, long n, hipStream_t st);
+long jm_rowcol_ws_floats(int M, int N, int nacc);
 int jm_gelu_bwd(const uint16_t* h, const uint16_t* da, uint16_t* dh, float* bias_grad, int M, int N, hipStream_t st,
-                int deriv = 0);
-int jm_colsum_bf16(const uint16_t* x, float* acc, int M, int N, hipStream_t st);
+                int deriv, float* ws);
+int jm_colsum_bf16(const uint16_t* x, float* acc, int M, int N, hipStream_t st, float* ws);
 int jm_splitk_reduce_add(const float* part, float* g, long n, int S, hipStream_t st, int store = 0);
 int jm_colsum_add_f32(const float* x, long ld, int rows, long n, float* g, hipStream_t st);
 int jm_zero_ranges(float* base, const long long* desc, int n, long long blocks, hipStream_t st);
@@ -52,7 +53,7 @@ int jm_residual_fwd(const float* x, long sB, long sT, int B, int T, int D, const
                     const float* mask, float* out, long oB, long oT, hipStream_t st, JmDrop drop);
 int jm_residual_bwd(const float* dout, long dB, long dT, const uint16_t* y, const float* scale, const float* mask,
                     float* dscale, uint16_t* dy, int B, int T, int D, float* dbias, long yB, long yT, hipStream_t st,
-                    JmDrop drop);
+                    JmDrop drop, float* ws);
 int jm_attn_fwd(const uint16_t* qkv, uint16_t* o, float* lse, int B, int S, int H, int hd, const int64_t* dseed,
                 uint32_t dthr, float dscale, hipStream_t st);
 int jm_attn_bwd(const uint16_t* qkv, const uint16_t* o, const uint16_t* dO, const float* lse, uint16_t* dqkv, int B,
@@ -62,14 +63,15 @@ int jm_attn_max_seq();
 int jm_attn_bwd_part_rows(int B, int S, int hd);
 int jm_attn_bwd_long(const uint16_t* qkv, const uint16_t* o, const uint16_t* dO, const float* lse, uint16_t* dqkv,
                      float* delta, int B, int S, int H, int hd, hipStream_t st);
-void jm_opt_sumsq(const float* x, const int* chunks, int nchunks, float* out, hipStream_t st);
+void jm_opt_sumsq(const float* x, const int* chunks, int nchunks, float* out, float* cpart, hipStream_t st);
 void jm_zero_f32(float* p, long n, hipStream_t st);
 void jm_opt_adamw(float* p, const float* g, float* mu, float* nu, uint16_t* shadow, const int* chunks, int nchunks,
                   const float* meta, const float* hyper, const float* gnorm_sq, hipStream_t st);
 void jm_opt_lamb_phase1(const float* p, const float* g, float* mu, float* nu, float* u, const int* chunks, int nchunks,
-                        const float* meta, const float* hyper, const float* gnorm_sq, float* norms, hipStream_t st);
+                        const float* meta, const float* hyper, const float* gnorm_sq, float* norms, float* cpart,
+                        hipStream_t st);
 void jm_opt_lars_norms(const float* p, const float* g, const int* chunks, int nchunks, const float* hyper,
-                       const float* gnorm_sq, float* norms, hipStream_t st);
+                       const float* gnorm_sq, float* norms, float* cpart, hipStream_t st);
 void jm_opt_apply_trust(float* p, const float* u_or_g, float* trace, uint16_t* shadow, const int* chunks, int nchunks,
                         const float* meta, const float* hyper, const float* norms, const float* gnorm_sq, int mode,
                         float momentum, float trust_coef, hipStream_t st);
@@ -265,6 +267,13 @@ torch::Tensor gelu_fwd(torch::Tensor h) {
 }
 
 // deriv: h holds the saved gelu'(pre-activation) (EPI_GELU_D forward) -> dh = da * h
+// partial-row workspace of the column-reducing elementwise kernels (their fixed-order bias /
+// scale gradient sums); a caching-allocator temporary on the current stream
+static torch::Tensor rowcol_ws(const torch::Tensor& like, int M, int N, int nacc) {
+  const long n = jm_rowcol_ws_floats(M, N, nacc);
+  return torch::empty({n > 0 ? n : 1}, like.options().dtype(torch::kFloat32));
+}
+
 torch::Tensor gelu_bwd(torch::Tensor h, torch::Tensor da, c10::optional<torch::Tensor> bias_grad, bool deriv) {
   CHECK_CONTIG(h);
   CHECK_CONTIG(da);
@@ -273,7 +282,11 @@ torch::Tensor gelu_bwd(torch::Tensor h, torch::Tensor da, c10::optional<torch::T
   const int N = h.size(-1);
   const int M = h.numel() / N;
   auto dh = torch::empty_like(h);
-  check_rc(jm_gelu_bwd(bf(h), bf(da), bfm(dh), fopt_m(bias_grad), M, N, stream(), deriv ? 1 : 0), "gelu_bwd");
+  float* bg = fopt_m(bias_grad);
+  torch::Tensor ws;
+  if (bg) ws = rowcol_ws(h, M, N, 1);
+  check_rc(jm_gelu_bwd(bf(h), bf(da), bfm(dh), bg, M, N, stream(), deriv ? 1 : 0, bg ? ws.data_ptr<float>() : nullptr),
+           "gelu_bwd");
   return dh;
 }
 
@@ -282,7 +295,8 @@ void colsum(torch::Tensor x, torch::Tensor acc) {
   CHECK_DT(x, torch::kBFloat16);
   const int N = x.size(-1);
   const int M = x.numel() / N;
-  check_rc(jm_colsum_bf16(bf(x), acc.data_ptr<float>(), M, N, stream()), "colsum");
+  auto ws = rowcol_ws(x, M, N, 1);
+  check_rc(jm_colsum_bf16(bf(x), acc.data_ptr<float>(), M, N, stream(), ws.data_ptr<float>()), "colsum");
 }
 
 void splitk_reduce_add(torch::Tensor part, torch::Tensor g) {
@@ -369,9 +383,12 @@ torch::Tensor residual_bwd(torch::Tensor dout, c10::optional<torch::Tensor> y, c
     TORCH_CHECK(yB == (long)T * D && yT == D, "residual_bwd: a strided y needs out");
     dy = torch::empty({(long)B * T, D}, dout.options().dtype(odt));
   }
+  torch::Tensor ws;
+  const bool sums = (dscale && dscale->defined()) || (dbias && dbias->defined());
+  if (sums) ws = rowcol_ws(dout, B * T, D, 2);
   check_rc(jm_residual_bwd(dout.data_ptr<float>(), dout.stride(0), dout.stride(1), has_y ? bf(*y) : nullptr,
                            fopt(scale), fopt(mask), fopt_m(dscale), bfm(dy), B, T, D, fopt_m(dbias), yB, yT,
-                           stream(), make_drop(seed, rate, dout, ioff)),
+                           stream(), make_drop(seed, rate, dout, ioff), sums ? ws.data_ptr<float>() : nullptr),
            "residual_bwd");
   return dy;
 }
@@ -444,8 +461,14 @@ uint16_t* shadow_ptr(c10::optional<torch::Tensor>& s) {
   return (s.has_value() && s->defined()) ? reinterpret_cast<uint16_t*>(s->data_ptr()) : nullptr;
 }
 
+// per-chunk partial sums of the norm kernels (summed per segment in chunk order: deterministic)
+torch::Tensor chunk_part(const torch::Tensor& like, const torch::Tensor& chunks, int nc) {
+  return torch::empty({(long)nch(chunks) * nc + 1}, like.options().dtype(torch::kFloat32));
+}
+
 void opt_sumsq(torch::Tensor x, torch::Tensor chunks, torch::Tensor out) {
-  jm_opt_sumsq(x.data_ptr<float>(), chp(chunks), nch(chunks), out.data_ptr<float>(), stream());
+  auto cp = chunk_part(x, chunks, 1);
+  jm_opt_sumsq(x.data_ptr<float>(), chp(chunks), nch(chunks), out.data_ptr<float>(), cp.data_ptr<float>(), stream());
 }
 
 void opt_adamw(torch::Tensor p, torch::Tensor g, torch::Tensor mu, torch::Tensor nu, c10::optional<torch::Tensor> shadow,
@@ -458,15 +481,17 @@ void opt_adamw(torch::Tensor p, torch::Tensor g, torch::Tensor mu, torch::Tensor
 void opt_lamb_phase1(torch::Tensor p, torch::Tensor g, torch::Tensor mu, torch::Tensor nu, torch::Tensor u,
                      torch::Tensor chunks, torch::Tensor meta, torch::Tensor hyper, torch::Tensor gnorm_sq,
                      torch::Tensor norms) {
+  auto cp = chunk_part(p, chunks, 2);
   jm_opt_lamb_phase1(p.data_ptr<float>(), g.data_ptr<float>(), mu.data_ptr<float>(), nu.data_ptr<float>(),
                      u.data_ptr<float>(), chp(chunks), nch(chunks), meta.data_ptr<float>(), hyper.data_ptr<float>(),
-                     gnorm_sq.data_ptr<float>(), norms.data_ptr<float>(), stream());
+                     gnorm_sq.data_ptr<float>(), norms.data_ptr<float>(), cp.data_ptr<float>(), stream());
 }
 
 void opt_lars_norms(torch::Tensor p, torch::Tensor g, torch::Tensor chunks, torch::Tensor hyper,
                     torch::Tensor gnorm_sq, torch::Tensor norms) {
+  auto cp = chunk_part(p, chunks, 2);
   jm_opt_lars_norms(p.data_ptr<float>(), g.data_ptr<float>(), chp(chunks), nch(chunks), hyper.data_ptr<float>(),
-                    gnorm_sq.data_ptr<float>(), norms.data_ptr<float>(), stream());
+                    gnorm_sq.data_ptr<float>(), norms.data_ptr<float>(), cp.data_ptr<float>(), stream());
 }
 
 void opt_apply_trust(torch::Tensor p, torch::Tensor u_or_g, c10::optional<torch::Tensor> trace,

@@ -9,7 +9,9 @@
 // All loads/stores are 16 B per lane (8 x bf16 or 2 x float4): hipcc does not vectorise bf16.
 // Column reductions use a 2-D decomposition: each thread owns 8 adjacent columns and walks a
 // slab of rows, keeps the 8 partial sums in registers, merges the block's row-slots through LDS
-// float atomics and issues one global atomicAdd per column per block into the fp32 grad buffer.
+// in slot order and stores one partial row per block; a row-lane column sum (colsum_rows_kernel)
+// adds the partial rows into the fp32 grad buffer in a fixed order (no float atomics: the same
+// bits on every run).
 #include "common.h"
 
 namespace {
@@ -53,20 +55,17 @@ __global__ __launch_bounds__(256) void rowcol_kernel(const void* __restrict__ in
                                                      const float* __restrict__ scale, const float* __restrict__ mask,
                                                      int M, int N, int T, int rows_per_block, long sB, long sT,
                                                      float* __restrict__ acc2, long yB, long yT, int cw,
-                                                     DropIO drop) {
-  extern __shared__ __attribute__((aligned(16))) float red_s[];  // [2][<= 2048] block's columns
+                                                     DropIO drop, float* __restrict__ ws) {
+  extern __shared__ __attribute__((aligned(16))) float red_s[];  // [2][rps][nc] slot partials
   // 2-D grid: blockIdx.y picks a chunk of cw (<= 2048, % 8 == 0) columns, blockIdx.x a slab of rows
   const int c0 = blockIdx.y * cw;
   const int nc = (N - c0) < cw ? (N - c0) : cw;
   const ColPlan p = col_plan(nc);
   const int slot = threadIdx.x / p.tpr, c = threadIdx.x % p.tpr;
   const bool active = slot < p.rps;
-  float* red = red_s - c0;  // index with absolute column
-  float* red2 = red_s + 2048 - c0;
-  if (acc || acc2) {
-    for (int i = threadIdx.x; i < 4096; i += 256) red_s[i] = 0.f;
-    __syncthreads();
-  }
+  // rps * nc <= 2048 (tpr = nc / 8 up to 256 threads): one plain store per (slot, column)
+  float* red = red_s + slot * nc - c0;  // index with absolute column
+  float* red2 = red_s + 2048 + slot * nc - c0;
   const int r_begin = blockIdx.x * rows_per_block;
   int r_end = r_begin + rows_per_block;
   if (r_end > M) r_end = M;
@@ -139,19 +138,30 @@ __global__ __launch_bounds__(256) void rowcol_kernel(const void* __restrict__ in
       }
       if (acc) {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) atomicAdd(&red[col + j], s[j]);
+        for (int j = 0; j < 8; ++j) red[col + j] = s[j];
       }
       if (MODE == 2 && acc2) {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) atomicAdd(&red2[col + j], s2[j]);
+        for (int j = 0; j < 8; ++j) red2[col + j] = s2[j];
       }
     }
   }
-  if (acc || acc2) __syncthreads();
-  if (acc)
-    for (int i = threadIdx.x; i < nc; i += 256) atomicAdd(&acc[c0 + i], red_s[i]);
-  if (MODE == 2 && acc2)
-    for (int i = threadIdx.x; i < nc; i += 256) atomicAdd(&acc2[c0 + i], red_s[2048 + i]);
+  if (!acc && !acc2) return;
+  __syncthreads();
+  // the block's partial row (slots summed in order) -> ws[blockIdx.x][c0 ..), acc2's after acc's
+  const long wrow = (long)blockIdx.x * N + c0;
+  for (int i = threadIdx.x; i < nc; i += 256) {
+    if (acc) {
+      float a = 0.f;
+      for (int k = 0; k < p.rps; ++k) a += red_s[k * nc + i];
+      ws[wrow + i] = a;
+    }
+    if (MODE == 2 && acc2) {
+      float a = 0.f;
+      for (int k = 0; k < p.rps; ++k) a += red_s[2048 + k * nc + i];
+      ws[(long)gridDim.x * N + wrow + i] = a;
+    }
+  }
 }
 
 __global__ __launch_bounds__(256) void residual_fwd_kernel(const float* __restrict__ x, long sB, long sT, int T,
@@ -194,19 +204,16 @@ int grid_for(long work, int per_thread_items = 1) {
   return (int)b;
 }
 
-template <int MODE>
-void launch_rowcol(const void* in0, const uint16_t* in1, uint16_t* out, float* acc, const float* scale,
-                   const float* mask, int M, int N, int T, hipStream_t st, long sB = 0, long sT = 0,
-                   float* acc2 = nullptr, long yB = -1, long yT = -1, JmDrop drop = JmDrop{nullptr, 0u, 1.f, 0}) {
-  if (yB < 0) {  // y / out contiguous [M, N]
-    yB = (long)T * N;
-    yT = N;
-  }
-  // 2-D grid: column chunks of cw <= 2048 x row slabs; each row-slot walks >= 16 rows, ~2048
-  // blocks in total so the per-block column atomics stay cheap.  Few rows (< 8192): chunks
-  // narrowed so ~256 blocks keep >= 32 rows each -- every block adds its column partials to the
-  // outputs with global atomics, and 128 row slabs per column (the 512 x 3072 jumbo residual
-  // backward) meant ~1M contended atomics and a 14 us call for 12 MB of data
+void launch_colsum(const float* part, float* g, long n4, int S, long ld, int store, hipStream_t st);
+
+// rowcol launch geometry: column chunks of cw <= 2048 x nb row slabs of rows_per_block rows
+struct RowcolGeom {
+  int cw, ncol, nb, rows_per_block;
+};
+
+RowcolGeom rowcol_geom(int M, int N) {
+  // each row-slot walks >= 16 rows, at most 1024 blocks in total (their partial rows are summed
+  // by a second pass).  Few rows (< 8192): chunks narrowed so ~256 blocks keep >= 32 rows each.
   int cw = N < 2048 ? N : 2048;
   if (M < 32 * 256) {
     const int nbr = M / 32 > 1 ? M / 32 : 1;
@@ -230,15 +237,30 @@ void launch_rowcol(const void* in0, const uint16_t* in1, uint16_t* out, float* a
     if (rows_per_block < rps) rows_per_block = rps;
     nb = (M + rows_per_block - 1) / rows_per_block;
   }
-  const int cap = 2048 / ncol > 1 ? 2048 / ncol : 1;
+  const int cap = 1024 / ncol > 1 ? 1024 / ncol : 1;
   if (nb > cap) {
     nb = cap;
     rows_per_block = (M + nb - 1) / nb;
   }
   if (nb < 1) nb = 1;
+  return RowcolGeom{cw, ncol, nb, rows_per_block};
+}
+
+// ws: the block partial rows, rowcol_ws_floats(M, N, 2 if acc2 else 1) floats
+template <int MODE>
+void launch_rowcol(const void* in0, const uint16_t* in1, uint16_t* out, float* acc, const float* scale,
+                   const float* mask, int M, int N, int T, hipStream_t st, float* ws, long sB = 0, long sT = 0,
+                   float* acc2 = nullptr, long yB = -1, long yT = -1, JmDrop drop = JmDrop{nullptr, 0u, 1.f, 0}) {
+  if (yB < 0) {  // y / out contiguous [M, N]
+    yB = (long)T * N;
+    yT = N;
+  }
+  const RowcolGeom g = rowcol_geom(M, N);
   const size_t smem = (acc || acc2) ? 4096 * sizeof(float) : 0;
-  rowcol_kernel<MODE><<<dim3(nb, ncol), 256, smem, st>>>(in0, in1, out, acc, scale, mask, M, N, T, rows_per_block,
-                                                          sB, sT, acc2, yB, yT, cw, drop);
+  rowcol_kernel<MODE><<<dim3(g.nb, g.ncol), 256, smem, st>>>(in0, in1, out, acc, scale, mask, M, N, T,
+                                                              g.rows_per_block, sB, sT, acc2, yB, yT, g.cw, drop, ws);
+  if (acc) launch_colsum(ws, acc, N / 4, g.nb, N, 0, st);
+  if (MODE == 2 && acc2) launch_colsum(ws + (long)g.nb * N, acc2, N / 4, g.nb, N, 0, st);
 }
 
 }  // namespace
@@ -249,19 +271,26 @@ int jm_gelu_fwd(const uint16_t* h, uint16_t* a, long n, hipStream_t st) {
   return 0;
 }
 
+// floats of the partial-row workspace of a column-reducing elementwise call (nacc: 1, or 2 for
+// residual_bwd with both dscale and dbias); 0 when N is not supported
+long jm_rowcol_ws_floats(int M, int N, int nacc) {
+  if (N % 8 || M < 1) return 0;
+  return (long)rowcol_geom(M, N).nb * N * nacc;
+}
+
 int jm_gelu_bwd(const uint16_t* h, const uint16_t* da, uint16_t* dh, float* bias_grad, int M, int N,
-                hipStream_t st, int deriv) {
-  if (N % 8) return -1;
+                hipStream_t st, int deriv, float* ws) {
+  if (N % 8 || (bias_grad && !ws)) return -1;
   if (deriv)
-    launch_rowcol<3>(h, da, dh, bias_grad, nullptr, nullptr, M, N, 1, st);
+    launch_rowcol<3>(h, da, dh, bias_grad, nullptr, nullptr, M, N, 1, st, ws);
   else
-    launch_rowcol<1>(h, da, dh, bias_grad, nullptr, nullptr, M, N, 1, st);
+    launch_rowcol<1>(h, da, dh, bias_grad, nullptr, nullptr, M, N, 1, st, ws);
   return 0;
 }
 
-int jm_colsum_bf16(const uint16_t* x, float* acc, int M, int N, hipStream_t st) {
-  if (N % 8) return -1;
-  launch_rowcol<0>(x, nullptr, nullptr, acc, nullptr, nullptr, M, N, 1, st);
+int jm_colsum_bf16(const uint16_t* x, float* acc, int M, int N, hipStream_t st, float* ws) {
+  if (N % 8 || !ws) return -1;
+  launch_rowcol<0>(x, nullptr, nullptr, acc, nullptr, nullptr, M, N, 1, st, ws);
   return 0;
 }
 
@@ -275,9 +304,10 @@ int jm_residual_fwd(const float* x, long sB, long sT, int B, int T, int D, const
 
 int jm_residual_bwd(const float* dout, long dB, long dT, const uint16_t* y, const float* scale, const float* mask,
                     float* dscale, uint16_t* dy, int B, int T, int D, float* dbias, long yB, long yT, hipStream_t st,
-                    JmDrop drop) {
+                    JmDrop drop, float* ws) {
   if (D % 8) return -1;
-  launch_rowcol<2>(dout, y, dy, dscale, scale, mask, B * T, D, T, st, dB, dT, dbias, yB, yT, drop);
+  if ((dscale || dbias) && !ws) return -1;
+  launch_rowcol<2>(dout, y, dy, dscale, scale, mask, B * T, D, T, st, ws, dB, dT, dbias, yB, yT, drop);
   return 0;
 }
 

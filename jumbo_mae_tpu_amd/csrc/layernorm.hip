@@ -330,60 +330,77 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const TI* __restrict__ dy, 
   }
 }
 
-// out_k[c] += sum_b ws[b][k*D + c] for the NP partial vectors (null outputs skipped); grid.y
-// splits the partial rows.
+// out_k[c] += sum_b ws[b][k*D + c] for the NP partial vectors (null outputs skipped).  RL row
+// lanes per float4 column, each summing every RL-th partial row (4 loads in flight), then a
+// fixed-order LDS tree over the lanes and ONE plain read-add-write per output column: the same
+// bits on every run.  (Rounds 1-3 split the rows over grid.y slices and added the slice sums with
+// float atomics, whose order varies from run to run.)
+template <int RL>
 __global__ __launch_bounds__(256) void ln_param_reduce_kernel(const float* __restrict__ ws, int nb, int D, int NP,
                                                               ParamOuts outs) {
-  // one float4 of columns per thread while loading (the whole 4-8 MB workspace in flight at once:
-  // the r1 one-float-per-thread form ran at ~1 TB/s, 8.7 us per call, 90 calls per ViT-L step);
-  // the sums are transposed through LDS so each atomic wave-instruction covers 256 contiguous
-  // bytes (a 16-B lane stride made the adds 4x the requests and the kernel slower than r1's)
-  __shared__ float red[1024];
-  const int i4 = blockIdx.x * 256 + threadIdx.x;
-  const long ld = (long)NP * D;
-  const int per = (nb + gridDim.y - 1) / gridDim.y;
-  const int b0 = blockIdx.y * per;
-  int b1 = b0 + per;
-  if (b1 > nb) b1 = nb;
-  float s[2][4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
-  if (i4 * 4 < NP * D) {
-    int b = b0;
-    for (; b + 1 < b1; b += 2) {
-      float a[4], c[4];
-      load4(ws + (long)b * ld + i4 * 4, a);
-      load4(ws + (long)(b + 1) * ld + i4 * 4, c);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        s[0][j] += a[j];
-        s[1][j] += c[j];
-      }
+  constexpr int CW = 256 / RL;
+  __shared__ float4 red[256];
+  const int c = threadIdx.x % CW, rl = threadIdx.x / CW;
+  const int i4 = blockIdx.x * CW + c;
+  const int n4 = NP * D / 4;
+  const long l4 = (long)NP * D / 4;
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (i4 < n4) {
+    const float4* p = reinterpret_cast<const float4*>(ws) + i4;
+    int b = rl;
+    for (; b + 3 * RL < nb; b += 4 * RL) {
+      const float4 a0 = p[b * l4], a1 = p[(b + RL) * l4], a2 = p[(b + 2 * RL) * l4], a3 = p[(b + 3 * RL) * l4];
+      acc.x += (a0.x + a1.x) + (a2.x + a3.x);
+      acc.y += (a0.y + a1.y) + (a2.y + a3.y);
+      acc.z += (a0.z + a1.z) + (a2.z + a3.z);
+      acc.w += (a0.w + a1.w) + (a2.w + a3.w);
     }
-    if (b < b1) {
-      float a[4];
-      load4(ws + (long)b * ld + i4 * 4, a);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) s[0][j] += a[j];
+    for (; b < nb; b += RL) {
+      const float4 a0 = p[b * l4];
+      acc.x += a0.x;
+      acc.y += a0.y;
+      acc.z += a0.z;
+      acc.w += a0.w;
     }
   }
-  float o[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) o[j] = s[0][j] + s[1][j];
-  store4(red + threadIdx.x * 4, o);
+  red[threadIdx.x] = acc;
   __syncthreads();
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int col = blockIdx.x * 1024 + j * 256 + threadIdx.x;
-    if (col >= NP * D) continue;
-    float* dst = outs.p[col / D];
-    if (dst != nullptr) atomicAdd(&dst[col % D], red[j * 256 + threadIdx.x]);
+  for (int h = RL / 2; h >= 1; h >>= 1) {
+    if (rl < h) {
+      const float4 o = red[threadIdx.x + h * CW];
+      float4& r = red[threadIdx.x];
+      r.x += o.x;
+      r.y += o.y;
+      r.z += o.z;
+      r.w += o.w;
+    }
+    __syncthreads();
+  }
+  if (rl == 0 && i4 < n4) {
+    const float4 r = red[c];
+    const float v[4] = {r.x, r.y, r.z, r.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {  // D % 4 == 0: the 4 columns share one output vector
+      const int col = i4 * 4 + j;
+      float* dst = outs.p[col / D];
+      if (dst != nullptr) dst[col % D] += v[j];
+    }
   }
 }
 
-// grid for ln_param_reduce_kernel over nb partial rows of NP * D floats: ~8 rows per thread
-dim3 param_reduce_grid(int nb, int D, int NP) {
-  int ys = (nb + 7) / 8;
-  if (ys < 1) ys = 1;
-  return dim3((NP * D / 4 + 255) / 256, ys);
+// ln_param_reduce_kernel over nb partial rows of NP * D floats: row lanes sized to ~8 rows each
+void launch_param_reduce(const float* ws, int nb, int D, int NP, ParamOuts outs, hipStream_t st) {
+  int rl = 16;
+  while (rl < 256 && nb > 8 * rl) rl *= 2;
+  const unsigned grid = (unsigned)((NP * D / 4) * rl + 255) / 256;
+  switch (rl) {
+    case 16: ln_param_reduce_kernel<16><<<grid, 256, 0, st>>>(ws, nb, D, NP, outs); break;
+    case 32: ln_param_reduce_kernel<32><<<grid, 256, 0, st>>>(ws, nb, D, NP, outs); break;
+    case 64: ln_param_reduce_kernel<64><<<grid, 256, 0, st>>>(ws, nb, D, NP, outs); break;
+    case 128: ln_param_reduce_kernel<128><<<grid, 256, 0, st>>>(ws, nb, D, NP, outs); break;
+    default: ln_param_reduce_kernel<256><<<grid, 256, 0, st>>>(ws, nb, D, NP, outs); break;
+  }
 }
 
 template <typename TO>
@@ -674,7 +691,7 @@ int jm_layernorm_bwd(const void* dy, int dy_bf16, const float* x, long sB, long 
 #undef JM_LNBW
     if (accum_params) {
       ParamOuts outs{{dgamma, dbeta, nullptr, nullptr}};
-      ln_param_reduce_kernel<<<param_reduce_grid(nb, D, 2), 256, 0, st>>>(ws, nb, D, 2, outs);
+      launch_param_reduce(ws, nb, D, 2, outs, st);
     }
     return 0;
   }
@@ -700,7 +717,7 @@ int jm_layernorm_bwd(const void* dy, int dy_bf16, const float* x, long sB, long 
                                wsk, accum_params, outs);
   }
   if (partials)
-    ln_param_reduce_kernel<<<param_reduce_grid(nb, D, NP), 256, 0, st>>>(ws, nb, D, NP, outs);
+    launch_param_reduce(ws, nb, D, NP, outs, st);
   return 0;
 }
 

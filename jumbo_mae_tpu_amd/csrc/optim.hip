@@ -36,8 +36,11 @@ JM_DEVICE float block_sum(float v, float* sh) {
   return r;
 }
 
+// Norm partials: every chunk block stores its sums in cpart[chunk][NC] and chunk_sums_kernel adds
+// them per segment in chunk order -- the same bits on every run (the round-1..3 kernels added the
+// block sums with float atomics, whose order varies).
 __global__ __launch_bounds__(256) void sumsq_kernel(const float* __restrict__ x, const Chunk* __restrict__ chunks,
-                                                    float* __restrict__ out) {
+                                                    float* __restrict__ cpart) {
   __shared__ float sh[8];
   const Chunk c = chunks[blockIdx.x];
   float s = 0.f;
@@ -46,7 +49,42 @@ __global__ __launch_bounds__(256) void sumsq_kernel(const float* __restrict__ x,
     s += v * v;
   }
   s = block_sum(s, sh);
-  if (threadIdx.x == 0) atomicAdd(out, s);
+  if (threadIdx.x == 0) cpart[blockIdx.x] = s;
+}
+
+// out[seg * NC + k] += sum over the run of chunks of seg (chunks sorted by segment) of
+// cpart[chunk * NC + k]; PER_SEG = false: one sum over all chunks into out[k].  One block per chunk:
+// the first chunk of each run reduces the run (thread-strided in order, then a fixed tree).
+template <int NC, bool PER_SEG>
+__global__ __launch_bounds__(256) void chunk_sums_kernel(const Chunk* __restrict__ chunks, int nchunks,
+                                                         const float* __restrict__ cpart, float* __restrict__ out) {
+  __shared__ float red[NC][256];
+  const int i0 = PER_SEG ? (int)blockIdx.x : 0;
+  const int seg = chunks[i0].seg;
+  if (PER_SEG && i0 > 0 && chunks[i0 - 1].seg == seg) return;  // not a run start (block-uniform)
+  float a[NC];
+#pragma unroll
+  for (int k = 0; k < NC; ++k) a[k] = 0.f;
+  for (int j = i0 + threadIdx.x; j < nchunks; j += 256) {
+    if (PER_SEG && chunks[j].seg != seg) break;  // runs are contiguous: nothing of seg beyond
+#pragma unroll
+    for (int k = 0; k < NC; ++k) a[k] += cpart[(long)j * NC + k];
+  }
+#pragma unroll
+  for (int k = 0; k < NC; ++k) red[k][threadIdx.x] = a[k];
+  __syncthreads();
+#pragma unroll
+  for (int h = 128; h >= 1; h >>= 1) {
+    if ((int)threadIdx.x < h) {
+#pragma unroll
+      for (int k = 0; k < NC; ++k) red[k][threadIdx.x] += red[k][threadIdx.x + h];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int k = 0; k < NC; ++k) out[(PER_SEG ? seg * NC : 0) + k] += red[k][0];
+  }
 }
 
 __global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ p, const float* __restrict__ g,
@@ -104,7 +142,7 @@ __global__ __launch_bounds__(256) void lamb_phase1_kernel(const float* __restric
                                                           float* __restrict__ u_out, const Chunk* __restrict__ chunks,
                                                           const float* __restrict__ meta,
                                                           const float* __restrict__ hyper,
-                                                          const float* __restrict__ gnorm_sq, float* __restrict__ norms) {
+                                                          const float* __restrict__ gnorm_sq, float* __restrict__ cpart) {
   __shared__ float sh[8];
   const Chunk c = chunks[blockIdx.x];
   const float* m = meta + 4 * c.seg;
@@ -128,15 +166,15 @@ __global__ __launch_bounds__(256) void lamb_phase1_kernel(const float* __restric
   sp = block_sum(sp, sh);
   su = block_sum(su, sh);
   if (threadIdx.x == 0) {
-    atomicAdd(&norms[2 * c.seg], sp);
-    atomicAdd(&norms[2 * c.seg + 1], su);
+    cpart[2 * blockIdx.x] = sp;
+    cpart[2 * blockIdx.x + 1] = su;
   }
 }
 
 __global__ __launch_bounds__(256) void lars_norms_kernel(const float* __restrict__ p, const float* __restrict__ g,
                                                          const Chunk* __restrict__ chunks,
                                                          const float* __restrict__ hyper,
-                                                         const float* __restrict__ gnorm_sq, float* __restrict__ norms) {
+                                                         const float* __restrict__ gnorm_sq, float* __restrict__ cpart) {
   __shared__ float sh[8];
   const Chunk c = chunks[blockIdx.x];
   const float f = clip_factor(hyper, gnorm_sq);
@@ -150,8 +188,8 @@ __global__ __launch_bounds__(256) void lars_norms_kernel(const float* __restrict
   sp = block_sum(sp, sh);
   su = block_sum(su, sh);
   if (threadIdx.x == 0) {
-    atomicAdd(&norms[2 * c.seg], sp);
-    atomicAdd(&norms[2 * c.seg + 1], su);
+    cpart[2 * blockIdx.x] = sp;
+    cpart[2 * blockIdx.x + 1] = su;
   }
 }
 
@@ -210,8 +248,11 @@ __global__ __launch_bounds__(256) void sgd_kernel(float* __restrict__ p, const f
 
 }  // namespace
 
-void jm_opt_sumsq(const float* x, const int* chunks, int nchunks, float* out, hipStream_t st) {
-  sumsq_kernel<<<nchunks, 256, 0, st>>>(x, (const Chunk*)chunks, out);
+// cpart: nchunks (sumsq) / 2 * nchunks (LAMB / LARS norms) floats of chunk partials
+void jm_opt_sumsq(const float* x, const int* chunks, int nchunks, float* out, float* cpart, hipStream_t st) {
+  if (nchunks < 1) return;
+  sumsq_kernel<<<nchunks, 256, 0, st>>>(x, (const Chunk*)chunks, cpart);
+  chunk_sums_kernel<1, false><<<1, 256, 0, st>>>((const Chunk*)chunks, nchunks, cpart, out);
 }
 
 void jm_opt_adamw(float* p, const float* g, float* mu, float* nu, uint16_t* shadow, const int* chunks, int nchunks,
@@ -221,13 +262,17 @@ void jm_opt_adamw(float* p, const float* g, float* mu, float* nu, uint16_t* shad
 
 void jm_opt_lamb_phase1(const float* p, const float* g, float* mu, float* nu, float* u, const int* chunks,
                         int nchunks, const float* meta, const float* hyper, const float* gnorm_sq, float* norms,
-                        hipStream_t st) {
-  lamb_phase1_kernel<<<nchunks, 256, 0, st>>>(p, g, mu, nu, u, (const Chunk*)chunks, meta, hyper, gnorm_sq, norms);
+                        float* cpart, hipStream_t st) {
+  if (nchunks < 1) return;
+  lamb_phase1_kernel<<<nchunks, 256, 0, st>>>(p, g, mu, nu, u, (const Chunk*)chunks, meta, hyper, gnorm_sq, cpart);
+  chunk_sums_kernel<2, true><<<nchunks, 256, 0, st>>>((const Chunk*)chunks, nchunks, cpart, norms);
 }
 
 void jm_opt_lars_norms(const float* p, const float* g, const int* chunks, int nchunks, const float* hyper,
-                       const float* gnorm_sq, float* norms, hipStream_t st) {
-  lars_norms_kernel<<<nchunks, 256, 0, st>>>(p, g, (const Chunk*)chunks, hyper, gnorm_sq, norms);
+                       const float* gnorm_sq, float* norms, float* cpart, hipStream_t st) {
+  if (nchunks < 1) return;
+  lars_norms_kernel<<<nchunks, 256, 0, st>>>(p, g, (const Chunk*)chunks, hyper, gnorm_sq, cpart);
+  chunk_sums_kernel<2, true><<<nchunks, 256, 0, st>>>((const Chunk*)chunks, nchunks, cpart, norms);
 }
 
 void jm_opt_apply_trust(float* p, const float* u_or_g, float* trace, uint16_t* shadow, const int* chunks, int nchunks,

@@ -48,10 +48,9 @@ def test_graphed_finetune_matches_eager():
         assert abs(a["loss"].item() - b["loss"].item()) < 1e-4 * max(1.0, abs(a["loss"].item()))
         assert abs(a["learning_rate"] - b["learning_rate"]) < 1e-12
     torch.cuda.synchronize()
-    # Float atomics in a few reductions (LayerNorm / bias parameter gradients, gradient norm) sum
-    # in arrival order, so two eager runs already differ in the last bits, and AdamW can turn a
-    # last-bit difference of a near-zero gradient into an lr-sized step: bound the outliers
-    # loosely, require the bulk to agree tightly (a stale captured buffer moves whole tensors).
+    # Written when a few reductions still used float atomics (two eager runs differed in the last
+    # bits, which AdamW can amplify on near-zero gradients): loose outlier bound, tight bulk.  The
+    # step is bitwise reproducible now -- tests/test_determinism_gpu.py checks equality.
     d = (m1.store.master - m2.store.master).abs()
     assert d.max().item() < 5e-3
     assert (d > 1e-5).float().mean().item() < 1e-4
@@ -112,10 +111,9 @@ def test_graph_restore_undoes_warmup():
 def test_graphed_grads_match_eager_production_routing():
     """B = 256 gives 256 x 19 = 4864 token rows, so the captured step runs the production
     weight-gradient routing (TN MFMA kernel, paired launches, store-mode gradients with the
-    zero-range fill).  Compared on one step's gradients from identical weights: after several
-    AdamW steps two EAGER runs already differ in ~2e-4 of the weights (float-atomic order in a few
-    reductions, amplified where a gradient is near zero; tools/graph_diag.py), so the weights are
-    the wrong place to look for a stale captured buffer -- the raw gradients are not."""
+    zero-range fill).  Compared on one step's gradients from identical weights (written when a few
+    reductions still summed with float atomics; bitwise equality of the whole step is
+    tests/test_determinism_gpu.py)."""
     from jumbo_mae_tpu_amd.runtime.graph import GraphedTrainStep
 
     data = _batches(3, B=256)
@@ -133,8 +131,6 @@ def test_graphed_grads_match_eager_production_routing():
             g1, g2 = m1.store.grad[sl], m2.store.grad[sl]
             scale = g1.abs().max().item()
             err = (g1 - g2).abs().max().item()
-            # step 1 starts from identical weights: only float-atomic summation order may differ;
-            # step 2 also carries step 1's AdamW update of those (m / sqrt(v) amplifies near-zero
-            # gradient differences), so it gets a looser bound -- a stale tile is O(scale) either way
+            # (bounds from the float-atomic era; a stale tile is O(scale) either way)
             tol = 1e-5 if i == 1 else 1e-3
             assert err <= tol * scale + 1e-9, (i, seg.key, err, scale)
