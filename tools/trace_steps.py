@@ -24,9 +24,9 @@ def category(n: str) -> str:
         return "mae glue (ours)"
     if "ln_" in n:
         return "layernorm"
-    if any(x in n for x in ("rowcol", "gelu", "residual", "splitk", "transpose_bf16", "zero_")):
+    if any(x in n for x in ("rowcol", "gelu", "residual", "splitk", "colsum", "transpose_bf16", "zero_")):
         return "fused elementwise (ours)"
-    if "adamw" in n or "opt" in n.lower() or "sumsq" in n or "lamb" in n or "lars" in n:
+    if "adamw" in n or "opt" in n.lower() or "sumsq" in n or "lamb" in n or "lars" in n or "chunk_sums" in n:
         return "optimizer"
     if "at::native" in n:
         return "torch native"
