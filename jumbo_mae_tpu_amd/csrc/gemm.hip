@@ -1134,14 +1134,7 @@ void launch_narrow(const uint16_t* A, long lda, const uint16_t* B, long ldb, int
   gemm_narrow_kernel<EPI><<<nwg, 512, sm, st>>>(A, lda, B, ldb, M, N, K, ep, GEMM_GROUP);
 }
 
-constexpr int NARROW_MAX_M = 4096;  // M below this: 128 x 192 tiles
-
-bool narrow(int M, int N) { return g_test_path == 0 && M < NARROW_MAX_M && N % 8 == 0; }
-
-// split-K (EPI_PARTIAL, splits > 1) takes the narrow tiles too: the jumbo MLP's K = 12288 GEMMs
-// run 4 splits of 128 x 192 tiles instead of 10 of 256 x 256 -- the GEMM alone is ~4 us slower
-// (r3e_summary_vitl_b512_fused_reductions.txt) but the fp32 partials shrink 2.5x
-// (profiles/r3_narrow_splitk.txt: ViT-L step -0.41 ms in-process).
+constexpr int NARROW_MAX_M = 4096;  // M below this: 128 x 192 tiles are a candidate
 
 bool p4_ok(int K, int epi, int splits) {
   return g_test_path != 1 && K % 128 == 0 && (epi != EPI_PARTIAL || K / 128 >= splits);
@@ -1150,6 +1143,32 @@ bool p4_ok(int K, int epi, int splits) {
 // Relative cost per tile row of the short-row 4-phase tiles vs 256 rows (the same B panel feeds
 // fewer MFMAs; measured per full wave, profiles/r3_gemm_tile_rows.txt)
 float rows_cost(int tr) { return tr == 256 ? 1.f : (tr == 224 ? 1.05f : 1.10f); }
+
+// Cost per output element of the 128 x 192 narrow tile relative to the 4-phase 256-row tile: its
+// smaller tile re-reads operands 1.5-1.7x as often per FLOP (MFMA busy 35 vs 43-57 %, r4_gemm_pmc)
+constexpr float NARROW_COST = 1.45f;
+
+// M < NARROW_MAX_M: the narrow tiles unless a 4-phase launch fills the chip's waves better --
+// waves x tile outputs x per-output cost.  The jumbo MLP at a 2048-row micro-batch: N = 12288
+// runs 1.9 waves of 224-row tiles (16-20 % faster than 4 waves of narrow tiles), N = 3072 one
+// full wave of narrow tiles (a 224-row launch would leave half the chip idle); at 512 rows every
+// jumbo GEMM stays narrow (profiles/r4z_jumbo_routing.txt).  Split-K (EPI_PARTIAL) keeps the
+// narrow tiles: the jumbo MLP's K = 12288 GEMMs run 4 splits of 128 x 192 tiles instead of 10 of
+// 256 x 256 -- the GEMM alone is ~4 us slower (r3e_summary_vitl_b512_fused_reductions.txt) but the
+// fp32 partials shrink 2.5x (profiles/r3_narrow_splitk.txt: ViT-L step -0.41 ms in-process).
+bool narrow(int M, int N, int K, int epi) {
+  if (g_test_path != 0 || M >= NARROW_MAX_M || N % 8) return false;
+  if (epi == EPI_PARTIAL || epi == EPI_TAIL || !p4_ok(K, epi, 1)) return true;
+  const int ncu = num_cus();
+  const long tn = (long)((M + NBM - 1) / NBM) * ((N + NBN - 1) / NBN);
+  const float c_narrow = (float)((tn + ncu - 1) / ncu) * NBM * NBN * NARROW_COST;
+  const int nN = (N + BN - 1) / BN;
+  for (int tr : {256, 224, 192}) {
+    const long t = (long)((M + tr - 1) / tr) * nN;
+    if ((float)((t + ncu - 1) / ncu) * tr * BN * rows_cost(tr) < c_narrow) return false;
+  }
+  return true;
+}
 
 int tail_plan_256(int M, int N, int K, int epi, int* tail_r);
 
@@ -1160,7 +1179,7 @@ int tail_plan_256(int M, int N, int K, int epi, int* tail_r);
 // tail-split and 64-deep launches and operands of >= 2 GB (the short tiles' unused a1 rows load
 // from offset 2^31, which must be out of range) keep 256.
 int tile_rows(int M, int N, int K, int epi, long lda) {
-  if (narrow(M, N) || !p4_ok(K, epi, 1) || epi == EPI_PARTIAL || epi == EPI_TAIL) return BM;
+  if (narrow(M, N, K, epi) || !p4_ok(K, epi, 1) || epi == EPI_PARTIAL || epi == EPI_TAIL) return BM;
   if ((long)M * lda * 2 >= (1L << 31) - (1L << 20)) return BM;
   if (g_test_rows) return g_test_rows;
   const int ncu = num_cus(), nN = (N + BN - 1) / BN;
@@ -1182,7 +1201,7 @@ template <int EPI>
 void launch_epi(const uint16_t* A, long lda, const uint16_t* B, long ldb, int M, int N, int K, const GemmEpi& ep,
                 int nwg, hipStream_t st) {
   if constexpr (EPI != EPI_TAIL) {
-    if (narrow(M, N) && ep.t_count == 0) return launch_narrow<EPI>(A, lda, B, ldb, M, N, K, ep, st);
+    if (narrow(M, N, K, EPI) && ep.t_count == 0) return launch_narrow<EPI>(A, lda, B, ldb, M, N, K, ep, st);
   }
   if (p4_ok(K, EPI, ep.splits)) {
     const int tr = ep.t_count > 0 ? BM : tile_rows(M, N, K, EPI, lda);
@@ -1221,14 +1240,14 @@ void jm_gemm_test_force(int path, int rows) {
 
 // output tiles of an NT launch (the narrow kernel's 128 x 192 or the 4-phase 256 / 224 / 192 x 256)
 int jm_gemm_nt_tiles(int M, int N, int K, int epi, long lda) {
-  if (narrow(M, N)) return ((M + NBM - 1) / NBM) * ((N + NBN - 1) / NBN);
+  if (narrow(M, N, K, epi)) return ((M + NBM - 1) / NBM) * ((N + NBN - 1) / NBN);
   const int tr = tile_rows(M, N, K, epi, lda);
   return ((M + tr - 1) / tr) * ((N + BN - 1) / BN);
 }
 
 // rows of the EPI_DGELU / EPI_DMUL column-partial buffer (one per row tile, before tail rows)
 int jm_gemm_nt_colpart_rows(int M, int N, int K, int epi, long lda) {
-  if (narrow(M, N)) return (M + NBM - 1) / NBM;
+  if (narrow(M, N, K, epi)) return (M + NBM - 1) / NBM;
   const int tr = tile_rows(M, N, K, epi, lda);
   return (M + tr - 1) / tr;
 }
@@ -1243,7 +1262,7 @@ int tail_plan_256(int M, int N, int K, int epi, int* tail_r) {
   *tail_r = 0;
   if (g_test_path != 0) return 0;
   if (!(epi == EPI_STORE || epi == EPI_GELU || epi == EPI_DGELU || epi == EPI_GELU_ONLY) || N % 8 || K % 128) return 0;
-  if (narrow(M, N)) return 0;
+  if (narrow(M, N, K, epi)) return 0;
   const int ncu = num_cus();
   const int tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
   if (tiles < ncu) return 0;

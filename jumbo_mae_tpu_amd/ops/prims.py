@@ -162,7 +162,9 @@ _NARROW_FUSED_MIN_TILES = 160  # a fused GELU epilogue needs the tiles alone to 
 
 
 def nt_tiles(M: int, N: int) -> int:
-    """Output tiles of an NT launch (mirror of jm_gemm_nt_tiles)."""
+    """Output tiles of an NT launch on the tiles its M selects (the split-K / fused-epilogue
+    decision below; jm_gemm_nt_tiles is exact: below NARROW_MAX_M the launch may take 4-phase
+    tiles where they fill the chip's waves better, e.g. the N = 12288 jumbo GEMMs at M = 2048)."""
     if M < NARROW_MAX_M:
         return -(-M // 128) * -(-N // 192)
     return -(-M // 256) * -(-N // 256)

@@ -23,6 +23,8 @@ FWD = {
     # ViT-B/16 encoder (D = 768, J = 2304)
     "b_qkv": (26624, 2304, 768), "b_wo": (26624, 768, 768), "b_ff1": (25088, 3072, 768),
     "b_ff2": (25088, 768, 3072), "b_jumbo1": (512, 9216, 2304), "b_jumbo2": (512, 2304, 9216),
+    # jumbo MLP at the headline's 2048-image micro-batch
+    "jumbo1_2k": (2048, 12288, 3072), "jumbo2_2k": (2048, 3072, 12288),
     # finetune jumbo MLP (128 images)
     "ft_jumbo1": (128, 9216, 2304), "ft_jumbo2": (128, 2304, 9216),
     # ViT-B/16 finetune (128 images x 199 tokens; the FF runs on the 196 patch rows = b_ff1/b_ff2)
@@ -82,9 +84,9 @@ def main():
     for kind in a.kinds.split(","):
         for name in names:
             M, N, K = FWD[name]
-            if kind.startswith("fwd_gelu") and name not in ("enc_ff1", "dec_ff1", "jumbo1", "b_ff1", "b_jumbo1", "ft_jumbo1"):
+            if kind.startswith("fwd_gelu") and name not in ("enc_ff1", "dec_ff1", "jumbo1", "jumbo1_2k", "b_ff1", "b_jumbo1", "ft_jumbo1"):
                 continue
-            if kind.startswith("dgrad_") and name not in ("enc_ff2", "dec_ff2", "b_ff2", "jumbo2", "b_jumbo2", "ft_jumbo2"):
+            if kind.startswith("dgrad_") and name not in ("enc_ff2", "dec_ff2", "b_ff2", "jumbo2", "jumbo2_2k", "b_jumbo2", "ft_jumbo2"):
                 continue
             if kind == "splitk" and name not in ("jumbo1", "jumbo2", "b_jumbo2", "ft_jumbo2"):
                 continue
