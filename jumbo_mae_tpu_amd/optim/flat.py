@@ -29,7 +29,10 @@ from ..models.params import ParamStore
 from ..ops import _ext
 from .schedule import WarmupCosine
 
-CHUNK = 65536  # elements per chunk of the multi-tensor table
+# elements per chunk of the multi-tensor table: one workgroup each; 8 Ki elements keep more
+# workgroups in flight than 64 Ki (AdamW alone: 551 -> 493 us at 86 M parameters, 2383 -> 2303 us
+# at 400 M, tools/adamw_bench.py --chunk, profiles/r4zb_adamw_chunk.txt)
+CHUNK = 8192
 
 
 def layer_index(path: tuple[str, ...], num_layers: int) -> int:

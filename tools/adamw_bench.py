@@ -18,14 +18,16 @@ def main():
     ap.add_argument("--n", type=int, default=400_000_000)
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--chunk", type=int, default=65536, help="elements per chunk-table row")
     a = ap.parse_args()
     ext = _ext.load()
-    n = a.n // 65536 * 65536
+    C = a.chunk
+    n = a.n // C * C
     p, g = torch.randn(n, device="cuda") * 0.02, torch.randn(n, device="cuda") * 1e-3
     mu, nu = torch.zeros(n, device="cuda"), torch.zeros(n, device="cuda")
     shadow = torch.empty(n, device="cuda", dtype=torch.bfloat16)
-    starts = torch.arange(0, n, 65536, dtype=torch.int32)
-    chunks = torch.stack([starts, torch.full_like(starts, 65536), torch.zeros_like(starts)], 1).contiguous().cuda()
+    starts = torch.arange(0, n, C, dtype=torch.int32)
+    chunks = torch.stack([starts, torch.full_like(starts, C), torch.zeros_like(starts)], 1).contiguous().cuda()
     meta = torch.tensor([1.0, 1.0, 0.0, 1.0], device="cuda")
     hyper = torch.tensor([1e-4, 0.1, 0.05, 1.0, 0.9, 0.95, 1e-8, 0.05], device="cuda")
     gn = torch.tensor([-1.0], device="cuda")
@@ -40,7 +42,7 @@ def main():
         torch.cuda.synchronize()
         ts.append(e0.elapsed_time(e1) * 1e3 / a.iters)
     tb = min(ts)
-    print(f"adamw: {tb:8.1f} us (rounds {', '.join(f'{x:.0f}' for x in ts)})  "
+    print(f"adamw n={n} chunk={C}: {tb:8.1f} us (rounds {', '.join(f'{x:.0f}' for x in ts)})  "
           f"{30.0 * n / tb / 1e6:5.2f} TB/s at 30 B/param", flush=True)
 
 
