@@ -413,7 +413,7 @@ void launch_colsum(const float* part, float* g, long n4, int S, long ld, int sto
     return;
   }
   int rl = 16;
-  while (rl < 256 && S > 8 * rl) rl *= 2;
+  while (rl < 256 && S > 32 * rl) rl *= 2;
   const unsigned nb = (unsigned)((n4 * rl + 255) / 256);
   switch (rl) {
     case 16: colsum_rows_kernel<16><<<nb, 256, 0, st>>>(part, g, n4, S, ld, store); break;
