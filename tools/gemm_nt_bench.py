@@ -27,6 +27,10 @@ FWD = {
     "jumbo1_2k": (2048, 12288, 3072), "jumbo2_2k": (2048, 3072, 12288),
     # finetune jumbo MLP (128 images)
     "ft_jumbo1": (128, 9216, 2304), "ft_jumbo2": (128, 2304, 9216),
+    # ViT-L at the headline's 2048-image micro-batch (52 / 49 encoder rows, 199 decoder rows per image)
+    "enc_qkv_2k": (106496, 3072, 1024), "enc_wo_2k": (106496, 1024, 1024), "enc_ff1_2k": (100352, 4096, 1024),
+    "enc_ff2_2k": (100352, 1024, 4096), "dec_qkv_2k": (407552, 1536, 512), "dec_wo_2k": (407552, 512, 512),
+    "dec_ff1_2k": (407552, 2048, 512), "dec_ff2_2k": (407552, 512, 2048),
     # ViT-B/16 finetune (128 images x 199 tokens; the FF runs on the 196 patch rows = b_ff1/b_ff2)
     "ft_qkv": (25472, 2304, 768), "ft_wo": (25472, 768, 768),
 }
@@ -84,9 +88,9 @@ def main():
     for kind in a.kinds.split(","):
         for name in names:
             M, N, K = FWD[name]
-            if kind.startswith("fwd_gelu") and name not in ("enc_ff1", "dec_ff1", "jumbo1", "jumbo1_2k", "b_ff1", "b_jumbo1", "ft_jumbo1"):
+            if kind.startswith("fwd_gelu") and name not in ("enc_ff1", "dec_ff1", "enc_ff1_2k", "dec_ff1_2k", "jumbo1", "jumbo1_2k", "b_ff1", "b_jumbo1", "ft_jumbo1"):
                 continue
-            if kind.startswith("dgrad_") and name not in ("enc_ff2", "dec_ff2", "b_ff2", "jumbo2", "jumbo2_2k", "b_jumbo2", "ft_jumbo2"):
+            if kind.startswith("dgrad_") and name not in ("enc_ff2", "dec_ff2", "enc_ff2_2k", "dec_ff2_2k", "b_ff2", "jumbo2", "jumbo2_2k", "b_jumbo2", "ft_jumbo2"):
                 continue
             if kind == "splitk" and name not in ("jumbo1", "jumbo2", "b_jumbo2", "ft_jumbo2"):
                 continue
