@@ -407,6 +407,12 @@ def linear_dgrad(dy: torch.Tensor, hw: Handle, add: torch.Tensor | None = None) 
     w = hw.weight()
     if _DGRAD_OURS and hip(dy) and dy.dtype == torch.bfloat16:
         s = splitk_plan(dy.shape[0], w.shape[1], w.shape[0])
+        if (not s and add is not None and dy.shape[0] < NARROW_MAX_M and w.shape[0] % 64 == 0
+                and w.shape[1] % 8 == 0 and _GEMM_MODE != "blas"):
+            # fp32 addend below the narrow-tile bound (the jumbo W1 data gradient at a 2048-row
+            # micro-batch): one fp32 "split" and the reduce's add instead of a bf16 output, an
+            # upcast copy and a torch add (same narrow kernel, 3 -> 2 launches, 125 -> 100 MB)
+            s = 1
         if s:
             if add is not None and add.stride(-1) == 1 and add.stride(0) % 4 == 0 and add.shape[1] % 4 == 0:
                 return _ext.load().gemm_nt_splitk(dy.contiguous(), hw.weight_t(), None, s, add)

@@ -619,6 +619,24 @@ def test_gemm_splitk_fused_fp32_add(ext):
     assert rel(ext.gemm_nt_splitk(A, B, None, 10), ref) < 1e-2
 
 
+def test_linear_dgrad_fp32_add_one_split(ext):
+    """Jumbo W1 data gradient at the headline's 2048-row micro-batch: no split-K plan, so the fp32
+    addend goes through ONE fp32 split + the reduce's add (ops/prims.py linear_dgrad) == fp32
+    reference, on the same narrow kernel as the bf16 path."""
+    from jumbo_mae_tpu_amd.ops import prims as P
+
+    torch.manual_seed(0)
+    M, N, K = 2048, 3072, 12288
+    assert P.splitk_plan(M, N, K) == 0
+    A = (torch.randn(M, K, device="cuda") * 0.05).bfloat16()
+    B = (torch.randn(N, K, device="cuda") * 0.05).bfloat16()
+    add = torch.randn(M, 3, N, device="cuda")[:, 1]
+    ref = A.float() @ B.float().t()
+    out = ext.gemm_nt_splitk(A, B, None, 1, add)
+    assert out.dtype == torch.float32 and out.shape == (M, N)
+    assert rel(out, ref + add) < 1e-5 + 1e-3 * ref.norm().item() / (ref + add).norm().item()
+
+
 @pytest.mark.parametrize("variant", [12, 24, 84])
 @pytest.mark.parametrize("M,N,K", [(1000, 512, 256), (600, 1000, 128)])
 def test_gemm_gelu_saved_derivative(ext, M, N, K, variant):
