@@ -204,7 +204,10 @@ struct ParamOuts {
 // partial rows in ws: [dgamma | dbeta] (NP = 2) or [dgamma | dbeta | dscale | dbias] (NP = 4)
 // ER (early residual-gradient load): dres is loaded together with x / dy in the first pass (one
 // HBM round trip per row instead of two) while the parameter partials stay in registers.
-template <int V, typename TI, bool RES, bool ER = false>
+// SC: the residual branch has a LayerScale (rio.scale); without one (every ViT-L / ViT-B preset)
+// the scale registers, the branch-output loads and the dscale partials are compiled out (ViT-L
+// encoder variant 200 -> 152 VGPRs: 3 waves per SIMD instead of 2).
+template <int V, typename TI, bool RES, bool ER = false, bool SC = true>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(const TI* __restrict__ dy, const float* __restrict__ x,
                                                      long sB, long sT, int T, int rows, int D,
                                                      const float* __restrict__ mean, const float* __restrict__ rstd,
@@ -228,7 +231,9 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const TI* __restrict__ dy, 
     }
     if (col < D) {
       load4(gamma + col, gg[i]);
-      if (RES && rio.scale) load4(rio.scale + col, sc[i]);
+      if constexpr (RES && SC) {
+        if (rio.scale) load4(rio.scale + col, sc[i]);
+      }
     }
   }
   for (int row = blockIdx.x * 4 + wave; row < rows; row += gridDim.x * 4) {
@@ -249,7 +254,9 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const TI* __restrict__ dy, 
         float xv[4], dv[4];
         load4(xr + col, xv);
         load4(dyr + col, dv);
-        if (RES && rrow && rio.scale) load4(rio.y + yoff + col, yv[i]);
+        if constexpr (RES && SC) {
+          if (rrow && rio.scale) load4(rio.y + yoff + col, yv[i]);
+        }
         if constexpr (ER) {
           if (rr) load4(rr + col, rvp[i]);
           else rvp[i][0] = rvp[i][1] = rvp[i][2] = rvp[i][3] = 0.f;
@@ -292,8 +299,10 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const TI* __restrict__ dy, 
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
             const float md = m * o[j] * f[j];  // f: the dropout of y (d(y_pre) and dscale see it)
-            d[j] = md * sc[i][j];
-            if (rio.scale) acc_add(acc, 2, i, j, md * yv[i][j]);
+            d[j] = SC ? md * sc[i][j] : md;
+            if constexpr (SC) {
+              if (rio.scale) acc_add(acc, 2, i, j, md * yv[i][j]);
+            }
             acc_add(acc, 3 % NP, i, j, bf2f(f2bf(d[j])));  // colsum of the bf16 values the GEMMs consume
           }
           store4(rio.dy + yoff + col, d);
@@ -574,14 +583,14 @@ bool use_wide(int rows, int D) { return D > 1024 && rows <= LN_WIDE_MAX_ROWS && 
 // 97.96 -> 97.75 ms/step, profiles/r1_ab_ln_bwd_early_dres.txt).  Measured and removed: LDS-
 // accumulated parameter partials (r1_ab_ln_bwd_lds_acc.txt), a next-row prefetch variant
 // (r2_ln_bwd_prefetch.txt).
-template <typename TI, bool RES>
+template <typename TI, bool RES, bool SC = true>
 void launch_bwd(int V, dim3 grid, size_t smem, hipStream_t st, const TI* dy, const float* x, long sB, long sT,
                 int T, int rows, int D, const float* m, const float* r, const float* g, LnBwdIO dx, LnResIO rio,
                 float* ws, int acc, ParamOuts outs) {
 #define JM_LNB(VV)                                                                                          \
   case VV:                                                                                                  \
-    ln_bwd_kernel<VV, TI, RES, (VV >= 2 && VV <= 4)><<<grid, 256, smem, st>>>(dy, x, sB, sT, T, rows, D, m, r, \
-                                                                              g, dx, rio, ws, acc, outs);     \
+    ln_bwd_kernel<VV, TI, RES, (VV >= 2 && VV <= 4), SC><<<grid, 256, smem, st>>>(dy, x, sB, sT, T, rows, D, m, \
+                                                                                  r, g, dx, rio, ws, acc, outs); \
     break;
   switch (V) {
     JM_LNB(1) JM_LNB(2) JM_LNB(3) JM_LNB(4) JM_LNB(6) JM_LNB(8) JM_LNB(9) JM_LNB(12) JM_LNB(16)
@@ -651,17 +660,21 @@ int jm_residual_ln_fwd(const float* x, long sB, long sT, const uint16_t* y, cons
   return 0;
 }
 
-// most row-loop blocks of the (non-wide) LN backward: 512 = 2 resident blocks per CU (2 waves /
-// SIMD): one round, half the partials of 1024 (-0.3 ms/step, profiles/r2_ln_bwd_blocks.txt)
-constexpr int LN_BWD_BLOCKS = 512;
+// most row-loop blocks of the (non-wide) LN backward: one resident round of the fused-residual
+// kernel without LayerScale -- 3 blocks per CU at V = 4 (147 VGPRs, D = 1024), 4 at V <= 2 (87,
+// D = 512), 2 beyond.  A second round only adds partial rows (r2: 1024 blocks at 2 per CU lost
+// 0.3 ms/step to 512, profiles/r2_ln_bwd_blocks.txt).
+constexpr int LN_BWD_CUS = 256;
+int ln_bwd_blocks_per_cu(int V) { return V <= 2 ? 4 : V <= 4 ? 3 : 2; }
 
 int jm_layernorm_bwd_blocks(int rows, int D) {
   // wide rows: one workgroup per row (at most 1024 workgroups, grid-stride beyond)
   if (use_wide(rows, D)) return rows > 1024 ? 1024 : rows;
   // grid-stride over rows, 4 waves per block; each block writes one [NP*D] partial (no atomics in
   // the hot kernel)
+  const int V = pick_v(D), cap = LN_BWD_CUS * ln_bwd_blocks_per_cu(V < 0 ? 16 : V);
   int nb = (rows + 3) / 4;
-  return nb > LN_BWD_BLOCKS ? LN_BWD_BLOCKS : nb;
+  return nb > cap ? cap : nb;
 }
 
 int jm_layernorm_bwd(const void* dy, int dy_bf16, const float* x, long sB, long sT, int B, int T, int D,
@@ -702,16 +715,22 @@ int jm_layernorm_bwd(const void* dy, int dy_bf16, const float* x, long sB, long 
   LnResIO rio{nullptr, nullptr, 0, 0, nullptr, nullptr, 0, JmDrop{nullptr, 0u, 1.f, 0}};
   if (res) rio = LnResIO{res->y, res->dy, res->yB, res->yT, res->scale, res->mask, res->T0, res->drop};
   if (dy_bf16) {
-    if (res)
+    if (res && res->scale)
       launch_bwd<uint16_t, true>(V, grid, smem, st, (const uint16_t*)dy, x, sB, sT, T, rows, D, mean, rstd, gamma,
                                  dx, rio, wsk, accum_params, outs);
+    else if (res)
+      launch_bwd<uint16_t, true, false>(V, grid, smem, st, (const uint16_t*)dy, x, sB, sT, T, rows, D, mean, rstd,
+                                        gamma, dx, rio, wsk, accum_params, outs);
     else
       launch_bwd<uint16_t, false>(V, grid, smem, st, (const uint16_t*)dy, x, sB, sT, T, rows, D, mean, rstd, gamma,
                                   dx, rio, wsk, accum_params, outs);
   } else {
-    if (res)
+    if (res && res->scale)
       launch_bwd<float, true>(V, grid, smem, st, (const float*)dy, x, sB, sT, T, rows, D, mean, rstd, gamma, dx, rio,
                               wsk, accum_params, outs);
+    else if (res)
+      launch_bwd<float, true, false>(V, grid, smem, st, (const float*)dy, x, sB, sT, T, rows, D, mean, rstd, gamma,
+                                     dx, rio, wsk, accum_params, outs);
     else
       launch_bwd<float, false>(V, grid, smem, st, (const float*)dy, x, sB, sT, T, rows, D, mean, rstd, gamma, dx, rio,
                                wsk, accum_params, outs);
