@@ -662,8 +662,8 @@ int jm_residual_ln_fwd(const float* x, long sB, long sT, const uint16_t* y, cons
 
 // most row-loop blocks of the (non-wide) LN backward: one resident round of the fused-residual
 // kernel without LayerScale -- 3 blocks per CU at V = 4 (147 VGPRs, D = 1024), 4 at V <= 2 (87,
-// D = 512), 2 beyond.  A second round only adds partial rows (r2: 1024 blocks at 2 per CU lost
-// 0.3 ms/step to 512, profiles/r2_ln_bwd_blocks.txt).
+// D = 512; 5 there measured 17.7 -> 18.5 ms/step, gpurun r4y2), 2 beyond.  A second round only
+// adds partial rows (r2: 1024 blocks at 2 per CU lost 0.3 ms/step to 512, r2_ln_bwd_blocks.txt).
 constexpr int LN_BWD_CUS = 256;
 int ln_bwd_blocks_per_cu(int V) { return V <= 2 ? 4 : V <= 4 ? 3 : 2; }
 

@@ -240,6 +240,59 @@ JM_DEVICE void patch_target(const uint8_t* __restrict__ img, long row, int N, in
   }
 }
 
+// p = 16 rows (768 = 64 lanes x 12): lane l owns the 12 CONSECUTIVE elements o = 12 l + j, i.e.
+// patch row ph = l / 4, pixels pw = 4 (l % 4) + j / 3, channel c = j % 3 -- so pred / dpred move as
+// three 8-byte accesses per lane instead of twelve 2-byte ones, the pred loads are issued before
+// the pixel staging (both HBM round trips overlap), and each channel's 4 pixels come out of the
+// staged patch in one 4-byte LDS read.
+JM_DEVICE void p16_load_pred(const uint16_t* __restrict__ pr, float* f) {
+#pragma unroll
+  for (int q = 0; q < 3; ++q) {
+    const uint2 v = *reinterpret_cast<const uint2*>(pr + 4 * q);
+    f[4 * q + 0] = __uint_as_float(v.x << 16);
+    f[4 * q + 1] = __uint_as_float(v.x & 0xffff0000u);
+    f[4 * q + 2] = __uint_as_float(v.y << 16);
+    f[4 * q + 3] = __uint_as_float(v.y & 0xffff0000u);
+  }
+}
+
+JM_DEVICE void p16_target(const uint8_t* __restrict__ img, long row, int N, int H, int W, bool norm_pix, uint8_t* lds,
+                          float* t) {
+  const int g = W / 16;
+  const int b = (int)(row / N), n = (int)(row - (long)b * N);
+  const int gy = n / g, gx = n - (n / g) * g;
+  const int lane = threadIdx.x & 63;
+  const uint8_t* src = img + ((long)b * 3 * H + gy * 16) * W + gx * 16;
+  if (lane < 48) {
+    const int c = lane >> 4, ph = lane & 15;
+    *reinterpret_cast<uint4*>(lds + lane * 16) = *reinterpret_cast<const uint4*>(src + ((long)c * H + ph) * W);
+  }
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the wave's LDS writes have landed
+  __builtin_amdgcn_wave_barrier();
+  const int ph = lane >> 2, pw0 = (lane & 3) * 4;
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    const uint32_t px = *reinterpret_cast<const uint32_t*>(lds + (c * 16 + ph) * 16 + pw0);
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      t[3 * k + c] = ((float)((px >> (8 * k)) & 0xffu) * (1.f / 255.f) - c_mean[c]) * c_istd[c];
+  }
+  if (norm_pix) {  // per-patch (t - mean) / sqrt(var + 1e-6), biased var (pretraining.py:114-117)
+    float s = 0.f;
+#pragma unroll
+    for (int j = 0; j < 12; ++j) s += t[j];
+    const float mean = wave_sum(s) * (1.f / 768.f);
+    float v = 0.f;
+#pragma unroll
+    for (int j = 0; j < 12; ++j) v += (t[j] - mean) * (t[j] - mean);
+    const float rs = rsqrtf(wave_sum(v) * (1.f / 768.f) + 1e-6f);
+#pragma unroll
+    for (int j = 0; j < 12; ++j) t[j] = (t[j] - mean) * rs;
+  }
+}
+
 // K14 forward: per-patch mean squared error of the prediction vs the normalized target, one wave
 // per (image, patch) row.  mse[row] = mean_pix (t - pred)^2 (utils_mae.py:51-64 before masking).
 template <int NJ, bool P16>
@@ -251,8 +304,19 @@ __global__ __launch_bounds__(256) void patch_mse_fwd_kernel(const uint16_t* __re
   const int P3 = 3 * p * p;
   __shared__ __attribute__((aligned(16))) uint8_t pix[4][64 * NJ];
   float t[NJ];
-  patch_target<NJ, P16>(img, row, N, H, W, p, P3, norm_pix != 0, pix[threadIdx.x >> 6], t);
   const int lane = threadIdx.x & 63;
+  if constexpr (P16) {  // ldp % 4 == 0 (host)
+    float f[12];
+    p16_load_pred(pred + row * ldp + 12 * lane, f);
+    p16_target(img, row, N, H, W, norm_pix != 0, pix[threadIdx.x >> 6], t);
+    float s = 0.f;
+#pragma unroll
+    for (int j = 0; j < 12; ++j) s += (t[j] - f[j]) * (t[j] - f[j]);
+    s = wave_sum(s);
+    if (lane == 0) mse[row] = s * (1.f / 768.f);
+    return;
+  }
+  patch_target<NJ, P16>(img, row, N, H, W, p, P3, norm_pix != 0, pix[threadIdx.x >> 6], t);
   float s = 0.f;
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {
@@ -278,12 +342,29 @@ __global__ __launch_bounds__(256) void patch_mse_bwd_kernel(const uint16_t* __re
   const int P3 = 3 * p * p;
   const int lane = threadIdx.x & 63;
   const float gsc = dmse[row];
+  __shared__ __attribute__((aligned(16))) uint8_t pix[4][64 * NJ];
+  float t[NJ];
+  if constexpr (P16) {  // ldp % 4 == 0 (host)
+    uint2* o = reinterpret_cast<uint2*>(dpred + row * 768 + 12 * lane);
+    if (gsc == 0.f) {
+#pragma unroll
+      for (int q = 0; q < 3; ++q) o[q] = make_uint2(0u, 0u);
+      return;
+    }
+    float f[12];
+    p16_load_pred(pred + row * ldp + 12 * lane, f);
+    p16_target(img, row, N, H, W, norm_pix != 0, pix[threadIdx.x >> 6], t);
+    const float k = 2.f * gsc * (1.f / 768.f);
+#pragma unroll
+    for (int q = 0; q < 3; ++q)
+      o[q] = make_uint2(pack_bf2(k * (f[4 * q] - t[4 * q]), k * (f[4 * q + 1] - t[4 * q + 1])),
+                        pack_bf2(k * (f[4 * q + 2] - t[4 * q + 2]), k * (f[4 * q + 3] - t[4 * q + 3])));
+    return;
+  }
   if (gsc == 0.f) {
     for (int o = lane; o < P3; o += 64) dpred[row * P3 + o] = 0;
     return;
   }
-  __shared__ __attribute__((aligned(16))) uint8_t pix[4][64 * NJ];
-  float t[NJ];
   patch_target<NJ, P16>(img, row, N, H, W, p, P3, norm_pix != 0, pix[threadIdx.x >> 6], t);
   const float k = 2.f * gsc / P3;
 #pragma unroll
@@ -343,7 +424,8 @@ int jm_patch_mse_fwd(const uint16_t* pred, long ldp, const uint8_t* img, float* 
   const int P3 = 3 * p * p;
   if (H % p || W % p || P3 > 64 * 16) return -1;
   const int nb = cdiv(rows, 4);
-  if (p == 16) patch_mse_fwd_kernel<12, true><<<nb, 256, 0, st>>>(pred, ldp, img, mse, rows, N, H, W, p, norm_pix);
+  if (p == 16 && ldp % 4 == 0 && (reinterpret_cast<uintptr_t>(pred) & 7) == 0)
+    patch_mse_fwd_kernel<12, true><<<nb, 256, 0, st>>>(pred, ldp, img, mse, rows, N, H, W, p, norm_pix);
   else if (P3 <= 64 * 4)
     patch_mse_fwd_kernel<4, false><<<nb, 256, 0, st>>>(pred, ldp, img, mse, rows, N, H, W, p, norm_pix);
   else if (P3 <= 64 * 12)
@@ -357,7 +439,7 @@ int jm_patch_mse_bwd(const uint16_t* pred, long ldp, const uint8_t* img, const f
   const int P3 = 3 * p * p;
   if (H % p || W % p || P3 > 64 * 16) return -1;
   const int nb = cdiv(rows, 4);
-  if (p == 16)
+  if (p == 16 && ldp % 4 == 0 && (reinterpret_cast<uintptr_t>(pred) & 7) == 0)
     patch_mse_bwd_kernel<12, true><<<nb, 256, 0, st>>>(pred, ldp, img, dmse, dpred, rows, N, H, W, p, norm_pix);
   else if (P3 <= 64 * 4)
     patch_mse_bwd_kernel<4, false><<<nb, 256, 0, st>>>(pred, ldp, img, dmse, dpred, rows, N, H, W, p, norm_pix);
