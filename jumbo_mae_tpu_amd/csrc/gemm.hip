@@ -1267,6 +1267,7 @@ int tail_plan_256(int M, int N, int K, int epi, int* tail_r) {
   const int tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
   if (tiles < ncu) return 0;
   const int r = tiles % ncu;
+  // (half a wave of tail tiles split 2 ways lost: ViT-L Wo 201 -> 224 us, step +5 ms, gpurun r4tl)
   if (r == 0 || r > ncu / 4) return 0;
   int S = ncu / r;
   // every split keeps >= 8 64-deep K steps (r1: splits of 1-2 steps lost to the partial round trip,
