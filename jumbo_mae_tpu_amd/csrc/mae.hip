@@ -65,6 +65,29 @@ JM_DEVICE float patch_pixel(const uint8_t* __restrict__ img, int b, int H, int W
   return (v * (1.f / 255.f) - c_mean[c]) * c_istd[c];
 }
 
+// p = 16 (768 outputs per patch, one 64-lane row group per patch): lane l produces the 12
+// consecutive outputs 12 l .. 12 l + 11 = patch row l / 4, pixels 4 (l % 4) .. + 3, channels 0-2,
+// from one 4-byte load per channel (W % 4 == 0 and a 4-byte aligned image: host checks) instead
+// of twelve byte loads; raw pixel bytes, channel c in byte k of px[c] = pixel 4 (l % 4) + k
+JM_DEVICE void p16_raw(const uint8_t* __restrict__ img, int b, int H, int W, int gy, int gx, int lane, uint32_t* px) {
+  const int ph = lane >> 2, pw0 = (lane & 3) * 4;
+#pragma unroll
+  for (int c = 0; c < 3; ++c)
+    px[c] = *reinterpret_cast<const uint32_t*>(img + (((long)b * 3 + c) * H + gy * 16 + ph) * W + gx * 16 + pw0);
+}
+
+JM_DEVICE float p16_norm(const uint32_t* px, int j) {  // output j = 3 k + c of the lane
+  const int k = j / 3, c = j - (j / 3) * 3;
+  return ((float)((px[c] >> (8 * k)) & 0xffu) * (1.f / 255.f) - c_mean[c]) * c_istd[c];
+}
+
+JM_DEVICE void p16_store12(uint16_t* o, const float* f) {
+  uint2* d = reinterpret_cast<uint2*>(o);
+#pragma unroll
+  for (int q = 0; q < 3; ++q)
+    d[q] = make_uint2(pack_bf2(f[4 * q], f[4 * q + 1]), pack_bf2(f[4 * q + 2], f[4 * q + 3]));
+}
+
 // K1+K3: kept patches of the normalized image as the bf16 patch-embed GEMM operand [B*K, 3p^2].
 // One thread writes 4 consecutive outputs (8-byte store).
 __global__ __launch_bounds__(256) void gather_patches_kernel(const uint8_t* __restrict__ img,
@@ -84,6 +107,26 @@ __global__ __launch_bounds__(256) void gather_patches_kernel(const uint8_t* __re
 #pragma unroll
   for (int j = 0; j < 4; ++j) f[j] = patch_pixel(img, b, H, W, p, gy, gx, o + j);
   store4(out + row * P3 + o, f);
+}
+
+// p = 16 form of gather_patches_kernel: 12 outputs per thread from 3 word loads (p16_raw)
+__global__ __launch_bounds__(256) void gather_patches16_kernel(const uint8_t* __restrict__ img,
+                                                               const int* __restrict__ ids, long idsB,
+                                                               uint16_t* __restrict__ out, int B, int K, int H, int W) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (long)B * K * 64) return;
+  const long row = i >> 6;
+  const int lane = (int)(i & 63);
+  const int b = (int)(row / K), k = (int)(row - (long)b * K);
+  const int g = W / 16;
+  const int n = ids[b * idsB + k];
+  JM_DASSERT(n >= 0 && n < (H / 16) * g);
+  uint32_t px[3];
+  p16_raw(img, b, H, W, n / g, n - (n / g) * g, lane, px);
+  float f[12];
+#pragma unroll
+  for (int j = 0; j < 12; ++j) f[j] = p16_norm(px, j);
+  p16_store12(out + row * 768 + 12 * lane, f);
 }
 
 // K2 epilogue + K4: x[b, t] = cls[t] (t < C); e[b*K + t - C] + pos[ids[t - C]] (t >= C), fp32.
@@ -383,6 +426,10 @@ int jm_gather_patches(const uint8_t* img, const int* ids, long idsB, uint16_t* o
   if ((3 * p * p) % 4 || H % p || W % p) return -1;
   const long n = (long)B * K * (3 * p * p / 4);
   if (n == 0) return 0;
+  if (p == 16 && W % 4 == 0 && (reinterpret_cast<uintptr_t>(img) & 3) == 0) {
+    gather_patches16_kernel<<<cdiv((long)B * K * 64, 256), 256, 0, st>>>(img, ids, idsB, out, B, K, H, W);
+    return 0;
+  }
   gather_patches_kernel<<<cdiv(n, 256), 256, 0, st>>>(img, ids, idsB, out, B, K, H, W, p);
   return 0;
 }
@@ -498,6 +545,45 @@ __global__ __launch_bounds__(256) void mix_patches_kernel(const uint8_t* __restr
   }
   store4(out + row * P3 + o0, f);
 }
+
+// p = 16 form of mix_patches_kernel: 12 outputs per thread from 3 word loads per source image
+__global__ __launch_bounds__(256) void mix_patches16_kernel(const uint8_t* __restrict__ img,
+                                                            const int* __restrict__ perm,
+                                                            const float* __restrict__ prm,
+                                                            const int* __restrict__ box,
+                                                            uint16_t* __restrict__ out, int B, int H, int W) {
+  const int g = W / 16, N = (H / 16) * g;
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (long)B * N * 64) return;
+  const int mode = prm ? (int)prm[0] : 0;
+  const float r = prm ? prm[1] : 1.f;
+  const long row = i >> 6;
+  const int lane = (int)(i & 63);
+  const int b = (int)(row / N), n = (int)(row - (long)b * N);
+  const int gy = n / g, gx = n - (n / g) * g;
+  uint32_t pa[3], pb[3];
+  p16_raw(img, b, H, W, gy, gx, lane, pa);
+  float f[12];
+  if (mode == 0) {
+#pragma unroll
+    for (int j = 0; j < 12; ++j) f[j] = p16_norm(pa, j);
+  } else {
+    p16_raw(img, perm[b], H, W, gy, gx, lane, pb);
+    if (mode == 1) {
+#pragma unroll
+      for (int j = 0; j < 12; ++j) f[j] = r * p16_norm(pa, j) + (1.f - r) * p16_norm(pb, j);
+    } else {  // cutmix: the permuted image inside the pixel box [y0, y1) x [x0, x1)
+      const int y = gy * 16 + (lane >> 2), x0 = gx * 16 + (lane & 3) * 4;
+      const bool yin = y >= box[0] && y < box[1];
+#pragma unroll
+      for (int j = 0; j < 12; ++j) {
+        const int x = x0 + j / 3;
+        f[j] = (yin && x >= box[2] && x < box[3]) ? p16_norm(pb, j) : p16_norm(pa, j);
+      }
+    }
+  }
+  p16_store12(out + row * 768 + 12 * lane, f);
+}
 }  // namespace
 
 int jm_mix_patches(const uint8_t* img, const int* perm, const float* prm, const int* box, uint16_t* out, int B, int H,
@@ -506,6 +592,11 @@ int jm_mix_patches(const uint8_t* img, const int* perm, const float* prm, const 
   if (prm != nullptr && (perm == nullptr || box == nullptr)) return -2;
   const long n = (long)B * (H / p) * (W / p) * (3 * p * p / 4);
   if (n == 0) return 0;
+  if (p == 16 && W % 4 == 0 && (reinterpret_cast<uintptr_t>(img) & 3) == 0) {
+    mix_patches16_kernel<<<cdiv((long)B * (H / 16) * (W / 16) * 64, 256), 256, 0, st>>>(img, perm, prm, box, out, B,
+                                                                                         H, W);
+    return 0;
+  }
   mix_patches_kernel<<<cdiv(n, 256), 256, 0, st>>>(img, perm, prm, box, out, B, H, W, p);
   return 0;
 }
