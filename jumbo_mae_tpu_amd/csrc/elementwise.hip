@@ -404,7 +404,7 @@ __global__ __launch_bounds__(256) void colsum_rows_kernel(const float* __restric
 }
 
 // column sums over S rows of stride ld into g (store: g = sum): the one-pass kernel when the
-// columns alone fill the chip, else colsum_rows_kernel with the row lanes sized to ~8 rows each
+// columns alone fill the chip, else colsum_rows_kernel with the row lanes sized to ~32 rows each
 void launch_colsum(const float* part, float* g, long n4, int S, long ld, int store, hipStream_t st) {
   const long blocks = (n4 + 255) / 256;
   if (blocks >= 512 || S < 16) {

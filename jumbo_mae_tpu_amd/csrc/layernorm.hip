@@ -398,7 +398,7 @@ __global__ __launch_bounds__(256) void ln_param_reduce_kernel(const float* __res
   }
 }
 
-// ln_param_reduce_kernel over nb partial rows of NP * D floats: row lanes sized to ~8 rows each
+// ln_param_reduce_kernel over nb partial rows of NP * D floats: row lanes sized to ~32 rows each
 void launch_param_reduce(const float* ws, int nb, int D, int NP, ParamOuts outs, hipStream_t st) {
   int rl = 16;
   while (rl < 256 && nb > 32 * rl) rl *= 2;
