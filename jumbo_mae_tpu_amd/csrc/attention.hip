@@ -1146,6 +1146,7 @@ int run_fwd(const uint16_t* qkv, uint16_t* out, float* lse_out, int B, int S, in
 //  * hd 64, S <= 64 (the ViT-L encoder): the compact bwd2, BWD2_PPW batch elements per workgroup.
 bool uses_bwd3(int S, int hd) { return hd == 32 || (hd == 64 && S > 64); }
 // ViT-L encoder (S 52): 160 -> 140 us at 8 batch elements per bwd2 workgroup (profiles/r1_attn_bwd_ppw.txt)
+// (16 at the 2048-image micro-batch: enc bwd 399.8 -> 403.0 us, tools/attn_bench.py enc2k, gpurun r4pp)
 constexpr int BWD2_PPW = 8;
 
 template <int HD, int SP, bool DROP>
@@ -1188,6 +1189,7 @@ int run_bwd(const uint16_t* qkv, const uint16_t* o, const uint16_t* dO, const fl
 // forward: the multi-pair kernel (4 (b, h) per workgroup) for the short encoder sequences
 // (SP <= 64: 43 -> 39 us), the one-pair kernel for the decoder, where the extra prefetch registers
 // cost an occupancy step (199 -> 215 us; profiles/r1_attn_fwd_ml.txt)
+// (8 pairs at the 2048-image micro-batch: enc fwd 186.6 -> 191.2 us, gpurun r4pp)
 constexpr int FWD_ML_PAIRS = 4;
 
 template <int HD, int SP, bool DROP>
