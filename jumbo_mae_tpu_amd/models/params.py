@@ -33,7 +33,8 @@ import torch
 ALIGN = 64
 # the flat total is padded to a multiple of this, so every data-parallel world size that divides
 # 1680 (1-8, 10, 12, 14, 15, 16, 20, 24, ...) can cut it into equal ALIGN-aligned shards
-# (ZeRO-1 optimizer sharding, parallel/ddp.py); costs at most 420 KB per fp32 buffer
+# (ZeRO-1 optimizer sharding, parallel/ddp.py); costs at most 420 KB per fp32 buffer.  Other
+# world sizes are folded in at finalize() when the process group exists.
 TOTAL_ALIGN = ALIGN * 1680
 
 
@@ -282,8 +283,18 @@ class ParamStore:
         self._handles.append(h)
         return h
 
+    def used_numel(self) -> int:
+        """Elements up to the end of the last segment (the flat total adds alignment padding)."""
+        return max((s.offset + s.numel for s in self.segments), default=0)
+
     def finalize(self, device, compute_dtype=torch.float32, generator: torch.Generator | None = None) -> None:
-        self.total = (self.total + TOTAL_ALIGN - 1) // TOTAL_ALIGN * TOTAL_ALIGN
+        q = TOTAL_ALIGN
+        # a data-parallel world that does not divide 1680 (32, 64 ranks) still gets equal 64-aligned
+        # ZeRO-1 shards: pad to lcm(TOTAL_ALIGN, world * ALIGN)
+        import torch.distributed as dist  # noqa: PLC0415
+        if dist.is_available() and dist.is_initialized():
+            q = math.lcm(q, dist.get_world_size() * ALIGN)
+        self.total = (self.total + q - 1) // q * q
         self.compute_dtype = compute_dtype
         self.master = torch.zeros(self.total, dtype=torch.float32, device=device)
         self.grad = torch.zeros(self.total, dtype=torch.float32, device=device)

@@ -365,6 +365,20 @@ class FlatOptimizer:
         assert d["kind"] == self.kind
         self.count = int(d["count"])
         for k in ("mu", "nu", "trace"):
-            if k in d and getattr(self, k) is not None:
-                getattr(self, k).copy_(d[k])
+            dst = getattr(self, k)
+            if k not in d or dst is None:
+                continue
+            src = d[k].reshape(-1)
+            # segment offsets do not depend on the flat total's padding (models/params.py
+            # TOTAL_ALIGN; earlier builds padded to 64): copy the common prefix, zero the rest.
+            # Everything past the last segment is padding, which is never read as a parameter.
+            n = min(src.numel(), dst.numel())
+            if src.numel() > n and bool(src[n:].any()):
+                raise ValueError(f"optimizer state '{k}' has {src.numel()} elements with non-zero entries "
+                                 f"past this store's {dst.numel()}")
+            if n < self.store.used_numel():
+                raise ValueError(f"optimizer state '{k}' has {src.numel()} elements; the parameters span "
+                                 f"{self.store.used_numel()}")
+            dst[:n].copy_(src[:n])
+            dst[n:].zero_()
         self.last_lr = self.schedule(max(self.count - 1, 0))

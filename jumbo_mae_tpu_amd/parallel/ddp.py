@@ -160,7 +160,8 @@ class GradReducer:
             q = self.world * ALIGN
             if store.total % q:
                 raise ValueError(f"optimizer sharding over {self.world} ranks needs the flat total ({store.total}) "
-                                 f"to be a multiple of {q} (models/params.py TOTAL_ALIGN)")
+                                 f"to be a multiple of {q}: build the model after init_process_group "
+                                 f"(models/params.py ParamStore.finalize pads for the world size)")
             self.buckets = [(lo, hi, [i for i, s in enumerate(segs) if s.offset < hi and s.offset + s.numel > lo])
                             for lo, hi in shard_ranges([(lo, hi) for lo, hi, _ in self.buckets], q)]
         self.seg_buckets: list[list[int]] = [[] for _ in segs]  # a snapped boundary may cut a segment

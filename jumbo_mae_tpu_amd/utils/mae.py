@@ -96,8 +96,9 @@ def masking_ids(noise: torch.Tensor, keep_len: int):
     On a GPU one HIP kernel computes all of it (csrc/mae.hip mask_ids: stable ranks, one
     workgroup per row) and also hands the int32 copies the gather kernels read to ops/mae.py as
     ``ids_keep._i32`` / ``ids_restore._i32``; the torch composition below is the CPU path and the
-    GPU test's oracle."""
-    if noise.is_cuda:
+    GPU test's oracle.  The kernel holds one row in a workgroup (N <= 1024 patches: 448 px at
+    p = 16 is 784); longer rows take the torch composition."""
+    if noise.is_cuda and noise.shape[-1] <= 1024:
         from ..ops import _ext  # noqa: PLC0415 (utils import without the extension)
         if _ext.use_hip(noise):
             shuffle, restore, keep32, restore32, mask = _ext.load().mask_ids(noise.float().contiguous(), keep_len)

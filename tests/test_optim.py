@@ -114,3 +114,30 @@ def test_optimizer_state_roundtrip():
     opt2.load_state_dict(sd)
     assert opt2.count == 1
     assert torch.equal(opt2.mu, opt.mu) and torch.equal(opt2.nu, opt.nu)
+
+
+def test_optimizer_state_from_older_padding():
+    """A sidecar written when the flat total was padded to 64 elements (round <= 3) resumes into
+    today's TOTAL_ALIGN-padded buffers: the common prefix is copied, the padding tail zeroed."""
+    m = _model()
+    opt = FlatOptimizer(m.store, "adamw", warmup_cosine_decay_schedule(1e-6, 1e-3, 2, 8, 1e-5))
+    m.store.grad.normal_()
+    m.store.grad[m.store.used_numel():] = 0
+    opt.step()
+    sd = opt.state_dict()
+    old_total = -(-m.store.used_numel() // 64) * 64
+    assert old_total < m.store.total
+    old = {k: (v[:old_total].clone() if isinstance(v, torch.Tensor) else v) for k, v in sd.items()}
+    opt2 = FlatOptimizer(m.store, "adamw", warmup_cosine_decay_schedule(1e-6, 1e-3, 2, 8, 1e-5))
+    opt2.mu.fill_(7.0)
+    opt2.load_state_dict(old)
+    assert torch.equal(opt2.mu, opt.mu) and torch.equal(opt2.nu, opt.nu)
+    # a larger saved buffer (a store padded for more ranks) loads too while its tail is zero
+    big = {k: (torch.cat([v, torch.zeros(128)]) if isinstance(v, torch.Tensor) else v) for k, v in sd.items()}
+    opt2.load_state_dict(big)
+    assert torch.equal(opt2.nu, opt.nu)
+    bad = dict(big, mu=torch.cat([sd["mu"], torch.ones(128)]))
+    with pytest.raises(ValueError):
+        opt2.load_state_dict(bad)
+    with pytest.raises(ValueError):
+        opt2.load_state_dict(dict(sd, mu=sd["mu"][:m.store.used_numel() - 1]))

@@ -8,7 +8,7 @@ set -e
 REV=${1:-HEAD}
 R=$(git rev-parse --show-toplevel); cd $R
 rm -rf _abbase && mkdir -p _abbase
-git archive "$REV" jumbo_mae_tpu_amd tools | tar -x -C _abbase
+git archive "$REV" jumbo_mae_tpu_amd tools bench.py | tar -x -C _abbase
 # the release extension only (the debug / asan variants are not needed for timing)
 (cd _abbase && python -m jumbo_mae_tpu_amd.csrc.build --variant release > /dev/null)
 ls -la _abbase/jumbo_mae_tpu_amd/_C*.so

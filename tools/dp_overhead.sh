@@ -11,6 +11,6 @@ run() { local n=$1; local a=$2; shift 2; (cd /tmp && timeout -k 10 240 env "$@" 
 run plain "" JMAE_FORCE_PG=0 python
 run dp64 "" JMAE_FORCE_PG=1 JMAE_RCCL_HIPRI=0 $TR
 run dp64_hipri "" JMAE_FORCE_PG=1 JMAE_RCCL_HIPRI=1 $TR
-run dp64_g1 "" JMAE_FORCE_PG=1 JMAE_OPT_GROUPS=1 JMAE_RCCL_HIPRI=0 $TR
-run dp64_g1_hipri "" JMAE_FORCE_PG=1 JMAE_OPT_GROUPS=1 JMAE_RCCL_HIPRI=1 $TR
+run dp64_nooverlap_hipri "--no-overlap" JMAE_FORCE_PG=1 JMAE_RCCL_HIPRI=1 $TR
+run dp64_zero1_hipri "--shard-optimizer" JMAE_FORCE_PG=1 JMAE_RCCL_HIPRI=1 $TR
 run dp16_hipri "--bucket-mb 16" JMAE_FORCE_PG=1 JMAE_RCCL_HIPRI=1 $TR
