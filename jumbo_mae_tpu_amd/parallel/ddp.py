@@ -40,8 +40,15 @@ MI355X design:
   ranks by a tiny all-reduce), and each bucket's updated fp32 master is ALL-GATHERED in place
   and re-cast to the bf16 shadow.  Link bytes per parameter: 4 + 4 (= the all-reduce's two
   halves), 2 + 4 with ``reduce_dtype=bf16``.  Optimizer moments of non-owned pieces are never
-  touched; ``gather_state`` all-gathers them for a checkpoint.  Partial (chunked jumbo) launches
-  are off in this mode: the jumbo buckets are reduce-scattered whole.
+  touched; ``gather_state`` all-gathers them for a checkpoint.
+* Chunked jumbo tail in ZeRO-1 mode: a reduce-scatter cannot start on a partial range of its bucket
+  (rank r owns piece r of the WHOLE bucket), so a bucket holding a segment larger than the bucket
+  size is cut into ``PARTIAL_SUB`` sub-buckets at the row-chunk boundaries of the batched jumbo
+  weight-gradient GEMM (quarters of the segment, snapped to world x 64), each with its own
+  owned pieces.  Readiness is tracked as covered element ranges per segment (whole segments from
+  the use counts, row chunks from ``mark_partial_ready``); a sub-bucket is reduce-scattered as soon
+  as every element of it is final, so only the last quarter's reduce-scatter waits for the end of
+  the backward -- the same exposure as the all-reduce mode's partial launches.
 """
 
 from __future__ import annotations
@@ -60,6 +67,45 @@ _LAYER = re.compile(r"(dec_)?layer_\d+")
 
 # optimizer launches per step on the split (per-bucket-group) path (profiles/r2_dp_overhead_1rank.txt)
 OPT_GROUPS = 4
+# sub-buckets of an oversized single segment in ZeRO-1 mode: the row chunks of the batched jumbo
+# weight-gradient GEMM (ops/prims.py _deferred["chunks"])
+PARTIAL_SUB = 4
+
+
+def split_oversized(buckets: list[tuple[int, int]], big: list[tuple[int, int]], q: int,
+                    parts: int = PARTIAL_SUB) -> list[tuple[int, int]]:
+    """Cut every bucket [lo, hi) that overlaps an oversized segment [off, off + n) of ``big`` at
+    that segment's ``parts`` equal-size boundaries snapped down to ``q`` -> ranges, same order."""
+    out = []
+    for lo, hi in buckets:
+        cuts = {lo, hi}
+        for off, n in big:
+            if off < hi and off + n > lo:
+                for j in range(1, parts):
+                    c = (off + n * j // parts) // q * q
+                    if lo < c < hi:
+                        cuts.add(c)
+        cs = sorted(cuts)
+        out.extend(list(zip(cs[:-1], cs[1:]))[::-1])  # launch order: from the end of the buffer
+    return out
+
+
+def _cover(ivs: list[tuple[int, int]], lo: int, hi: int) -> bool:
+    """[lo, hi) inside the union of the (merged, sorted) intervals ``ivs``."""
+    for a, b in ivs:
+        if a <= lo < b:
+            return hi <= b
+    return lo >= hi
+
+
+def _merge(ivs: list[tuple[int, int]], a: int, b: int) -> list[tuple[int, int]]:
+    out = []
+    for x, y in sorted(ivs + [(a, b)]):
+        if out and x <= out[-1][1]:
+            out[-1] = (out[-1][0], max(out[-1][1], y))
+        else:
+            out.append((x, y))
+    return out
 
 
 def unit_key(path: tuple[str, ...]) -> tuple[str, ...]:
@@ -162,8 +208,10 @@ class GradReducer:
                 raise ValueError(f"optimizer sharding over {self.world} ranks needs the flat total ({store.total}) "
                                  f"to be a multiple of {q}: build the model after init_process_group "
                                  f"(models/params.py ParamStore.finalize pads for the world size)")
+            ranges = shard_ranges([(lo, hi) for lo, hi, _ in self.buckets], q)
+            ranges = split_oversized(ranges, [(s.offset, s.numel) for s in segs if s.numel > limit], q)
             self.buckets = [(lo, hi, [i for i, s in enumerate(segs) if s.offset < hi and s.offset + s.numel > lo])
-                            for lo, hi in shard_ranges([(lo, hi) for lo, hi, _ in self.buckets], q)]
+                            for lo, hi in ranges]
         self.seg_buckets: list[list[int]] = [[] for _ in segs]  # a snapped boundary may cut a segment
         for bi, (_, _, idxs) in enumerate(self.buckets):
             for i in idxs:
@@ -174,6 +222,7 @@ class GradReducer:
         self._stage_lo = min((lo for lo, _, _ in self.buckets), default=0)
         self._stage_hi = max((hi for _, hi, _ in self.buckets), default=0)
         self.pending_uses = [0] * len(segs)
+        self.ready_iv: list[list[tuple[int, int]]] = [[] for _ in segs]  # shard: final element ranges
         self.bucket_left = [len(b[2]) for b in self.buckets]
         self.launched = [False] * len(self.buckets)
         self.works: list[tuple] = []  # (bucket, work, tensor to divide or None, lo, hi, staged, partial)
@@ -189,6 +238,7 @@ class GradReducer:
 
     def begin_step(self) -> None:
         self.pending_uses = [0] * len(self.segs)
+        self.ready_iv = [[] for _ in self.segs]
         self.bucket_left = [len(b[2]) for b in self.buckets]
         self.launched = [False] * len(self.buckets)
         self.partial_done = [0] * len(self.buckets)
@@ -204,12 +254,28 @@ class GradReducer:
         n = (hi - lo) // self.world
         return lo + self.rank * n, lo + (self.rank + 1) * n
 
+    def _shard_ready(self, i: int, lo: int, hi: int) -> None:
+        """ZeRO-1: elements [lo, hi) of segment ``i`` are final; reduce-scatter every bucket of that
+        segment whose elements are now all final (``split_oversized`` sub-buckets)."""
+        self.ready_iv[i] = _merge(self.ready_iv[i], lo, hi)
+        for b in self.seg_buckets[i]:
+            if self.launched[b]:
+                continue
+            blo, bhi, idxs = self.buckets[b]
+            if all(_cover(self.ready_iv[j], max(blo, self.segs[j].offset) - self.segs[j].offset,
+                          min(bhi, self.segs[j].offset + self.segs[j].numel) - self.segs[j].offset)
+                   for j in idxs):
+                self._launch(b)
+
     def _on_partial(self, h: Handle, lo: int, hi: int) -> None:
         """Elements [lo, hi) of single-segment handle ``h`` are final: reduce them now."""
-        if not (self.overlap and self.sync) or len(h.segs) != 1 or self.shard:
+        if not (self.overlap and self.sync) or len(h.segs) != 1:
             return
         i = self.seg_index.get(id(h.segs[0]))
         if i is None:
+            return
+        if self.shard:
+            self._shard_ready(i, lo, hi)
             return
         b = self.seg_buckets[i][0]
         blo, bhi, idxs = self.buckets[b]
@@ -238,7 +304,9 @@ class GradReducer:
             if i is None:
                 continue
             self.pending_uses[i] -= 1
-            if self.pending_uses[i] == 0:
+            if self.pending_uses[i] == 0 and self.shard:
+                self._shard_ready(i, 0, s.numel)
+            elif self.pending_uses[i] == 0:
                 for b in self.seg_buckets[i]:
                     self.bucket_left[b] -= 1
                     if self.bucket_left[b] == 0:

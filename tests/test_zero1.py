@@ -15,8 +15,10 @@ import torch.multiprocessing as mp
 from test_dist import _cfgs, _free_port, _init
 
 
-def _worker(rank, world, port, out, kind, clip, overlap, bf16):
+def _worker(rank, world, port, out, kind, clip, overlap, bf16, defer=False):
     _init(rank, world, port)
+    from jumbo_mae_tpu_amd.ops import prims
+    prims._deferred["force"] = defer  # batched jumbo wgrad in row chunks with partial readiness (GPU path)
     from jumbo_mae_tpu_amd.models.mae import PretrainModel
     from jumbo_mae_tpu_amd.optim.flat import FlatOptimizer
     from jumbo_mae_tpu_amd.optim.schedule import warmup_cosine_decay_schedule
@@ -36,12 +38,22 @@ def _worker(rank, world, port, out, kind, clip, overlap, bf16):
                           reduce_dtype=torch.bfloat16 if bf16 else torch.float32)
         tr = Trainer(m, opt, red, None)
         tr.overlap_optimizer = overlap
+        early = []
+        fin = red.finish
+
+        def finish(*a, _fin=fin, _red=red, **k):  # buckets launched during the backward
+            early.append([b for b, done in enumerate(_red.launched) if done])
+            return _fin(*a, **k)
+
+        red.finish = finish
         for _ in range(3):
             tr.train_step([(imgs[rank * 4:(rank + 1) * 4],)])
         opt.gather_state()
         res[shard] = {"master": m.store.master.clone(), "mu": None if opt.mu is None else opt.mu.clone(),
                       "trace": None if opt.trace is None else opt.trace.clone(), "stats": red.stats(),
-                      "nb": len(red.buckets), "pieces": red.owned_pieces()}
+                      "nb": len(red.buckets), "pieces": red.owned_pieces(), "early": early[-1],
+                      "jumbo": [b for b, (lo, hi, idxs) in enumerate(red.buckets)
+                                if any("jumbo_mlp" in red.segs[i].path and red.segs[i].numel > 1000 for i in idxs)]}
     # every rank ends with the same master
     ms = [torch.zeros_like(res[True]["master"]) for _ in range(world)]
     dist.all_gather(ms, res[True]["master"])
@@ -50,22 +62,24 @@ def _worker(rank, world, port, out, kind, clip, overlap, bf16):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,kind,clip,overlap,bf16", [
-    (2, "adamw", 0.0, True, False),   # split update per bucket group + all-gather per group
-    (2, "adamw", 0.0, False, False),  # monolithic update, then all-gather
-    (2, "sgd", 0.0, True, False),
-    (2, "lamb", 0.0, True, False),    # per-leaf trust ratios: norms summed over the ranks
-    (2, "lars", 0.0, True, False),
-    (2, "adamw", 0.5, True, False),   # global clip norm summed over the ranks
-    (2, "adamw", 0.0, True, True),    # bf16 reduce-scatter
-    (4, "adamw", 0.0, True, False),
-    (4, "lamb", 0.3, True, False),
+@pytest.mark.parametrize("world,kind,clip,overlap,bf16,defer", [
+    (2, "adamw", 0.0, True, False, False),   # split update per bucket group + all-gather per group
+    (2, "adamw", 0.0, False, False, False),  # monolithic update, then all-gather
+    (2, "sgd", 0.0, True, False, False),
+    (2, "lamb", 0.0, True, False, False),    # per-leaf trust ratios: norms summed over the ranks
+    (2, "lars", 0.0, True, False, False),
+    (2, "adamw", 0.5, True, False, False),   # global clip norm summed over the ranks
+    (2, "adamw", 0.0, True, True, False),    # bf16 reduce-scatter
+    (4, "adamw", 0.0, True, False, False),
+    (4, "lamb", 0.3, True, False, False),
+    (2, "adamw", 0.0, True, False, True),  # chunked jumbo weight gradients: sub-bucket reduce-scatters
+    (4, "lamb", 0.0, True, True, True),
 ])
-def test_zero1_matches_replicated(world, kind, clip, overlap, bf16):
+def test_zero1_matches_replicated(world, kind, clip, overlap, bf16, defer):
     port = _free_port()
     with tempfile.TemporaryDirectory() as d:
         out = os.path.join(d, "r.pt")
-        mp.spawn(_worker, args=(world, port, out, kind, clip, overlap, bf16), nprocs=world, join=True)
+        mp.spawn(_worker, args=(world, port, out, kind, clip, overlap, bf16, defer), nprocs=world, join=True)
         r = torch.load(out, weights_only=True)
     rep, zero = r["rep"], r["zero"]
     assert r["same"], "ranks disagree after the all-gather"
@@ -73,6 +87,12 @@ def test_zero1_matches_replicated(world, kind, clip, overlap, bf16):
     assert zero["nb"] > 3
     # pieces: 64-aligned, one per bucket
     assert all(a % 64 == 0 and b % 64 == 0 and b > a for a, b in zero["pieces"])
+    if defer:
+        # each oversized jumbo kernel is cut into quarter sub-buckets, and all but the last of them
+        # are reduce-scattered from their row chunks' partial readiness, before finish()
+        jb = zero["jumbo"]
+        assert len(jb) >= 8, jb
+        assert len([b for b in jb if b in zero["early"]]) >= len(jb) - 2, (jb, zero["early"])
     if world == 2 and not bf16 and kind in ("adamw", "sgd") and clip == 0:
         # elementwise update, and two-rank sums are a single addition either way: bit for bit
         assert torch.equal(zero["master"], rep["master"])
@@ -87,7 +107,7 @@ def test_zero1_matches_replicated(world, kind, clip, overlap, bf16):
         assert d <= tol * rep["master"].abs().max().item(), d
         if rep["mu"] is not None:
             d = (zero["mu"] - rep["mu"]).abs().max().item()
-            assert d <= 1e-3 * rep["mu"].abs().max().item() + 1e-9, d
+            assert d <= (4e-3 if bf16 else 1e-3) * rep["mu"].abs().max().item() + 1e-9, d
 
 
 def test_shard_ranges_tile_and_align():
