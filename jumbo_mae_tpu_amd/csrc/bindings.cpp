@@ -20,6 +20,10 @@ int jm_layernorm_bwd_blocks(int rows, int D);
 // reading clears it); always 0 in the release build
 int jm_debug_line_attention();
 int jm_debug_line_dropout();
+int jm_debug_line_augment();
+int jm_rrc_resize(const uint8_t* src, const int64_t* tab, int B, int S, uint8_t* tmp, int tmp_rows_max, uint8_t* out,
+                  hipStream_t st);
+int jm_rrc_kmax();
 int jm_dropout_apply(const void* x, void* y, long n, int bf16, const int64_t* seed, uint32_t thr, float scale,
                      hipStream_t st);
 int jm_gelu_drop(const uint16_t* h, uint16_t* g, uint16_t* gp, long n, const int64_t* seed, uint32_t thr, float scale,
@@ -706,7 +710,9 @@ int attach_tail(GemmEpi& ep, torch::Tensor& ws, int M, int N, int K, int epi, co
   return r;
 }
 
-// gelu_deriv (with gelu): returns {gelu'(h), gelu(h)} instead of {h, gelu(h)} (EPI_GELU_D)
+// gelu_deriv (with gelu): returns {gelu'(h) as uint8 codes (common.h gd_code), gelu(h)} instead of
+// {h, gelu(h)} (EPI_GELU_D); with dropout the codes are those of the kept gelu'(h) unscaled (0 where
+// dropped) and gemm_nt_dgelu applies 1 / keep when it decodes them
 std::vector<torch::Tensor> gemm_nt(torch::Tensor A, torch::Tensor B, c10::optional<torch::Tensor> bias, bool gelu,
                                    bool gelu_only, bool gelu_deriv, c10::optional<torch::Tensor> seed, double rate) {
   CHECK_DT(A, torch::kBFloat16);
@@ -714,9 +720,11 @@ std::vector<torch::Tensor> gemm_nt(torch::Tensor A, torch::Tensor B, c10::option
   TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && A.size(1) == B.size(1), "gemm_nt: A [M,K], B [N,K]");
   TORCH_CHECK(A.stride(1) == 1 && B.stride(1) == 1, "gemm_nt: K must be contiguous");
   const int M = A.size(0), N = B.size(0), K = A.size(1);
-  auto out = torch::empty({M, N}, A.options());
+  TORCH_CHECK(!gelu_deriv || N % 8 == 0, "gemm_nt: gelu_deriv needs N % 8 == 0");
+  auto out = torch::empty({M, N}, gelu_deriv ? A.options().dtype(torch::kUInt8) : A.options());
   torch::Tensor out2;
-  GemmEpi ep{nullptr, bfm(out), N, nullptr, nullptr, nullptr, nullptr, 1};
+  GemmEpi ep{nullptr, gelu_deriv ? nullptr : bfm(out), N, nullptr, nullptr, nullptr, nullptr, 1};
+  if (gelu_deriv) ep.dq = out.data_ptr<uint8_t>();
   if (bias) {
     TORCH_CHECK(bias->is_contiguous() && bias->scalar_type() == torch::kFloat32 && bias->numel() == N, "gemm_nt bias");
     ep.bias = bias->data_ptr<float>();
@@ -793,19 +801,25 @@ torch::Tensor gemm_nt_f32(torch::Tensor A, torch::Tensor B) {
 
 // dh[M, N] = (A[M, K] . B[N, K]^T) * gelu'(pre[M, N]) -- FF2 data gradient through the GELU,
 // B = W2^T; dbias (fp32 [N], optional) += column sums of dh (the FF1 bias gradient).
-// deriv: ``pre`` holds the saved gelu'(h) (EPI_GELU_D forward): the epilogue multiplies (EPI_DMUL)
+// deriv: ``pre`` holds the saved gelu'(h) as uint8 codes (EPI_GELU_D forward): the epilogue decodes
+// and multiplies (EPI_DMUL); ``rate`` > 0: the forward's FF hidden dropout rate (codes of the unscaled
+// kept derivative), 1 / keep applied with the decode
 torch::Tensor gemm_nt_dgelu(torch::Tensor A, torch::Tensor B, torch::Tensor pre, c10::optional<torch::Tensor> dbias,
-                            bool deriv) {
+                            bool deriv, double rate) {
   CHECK_DT(A, torch::kBFloat16);
   CHECK_DT(B, torch::kBFloat16);
-  CHECK_DT(pre, torch::kBFloat16);
+  CHECK_DT(pre, deriv ? torch::kUInt8 : torch::kBFloat16);
   TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && A.size(1) == B.size(1), "gemm_nt_dgelu: A [M,K], B [N,K]");
   TORCH_CHECK(A.stride(1) == 1 && B.stride(1) == 1, "gemm_nt_dgelu: K must be contiguous");
   const int M = A.size(0), N = B.size(0), K = A.size(1);
   TORCH_CHECK(pre.is_contiguous() && pre.size(0) == M && pre.size(1) == N, "gemm_nt_dgelu: pre [M,N]");
   auto out = torch::empty({M, N}, A.options());
   torch::Tensor part;
-  GemmEpi ep{nullptr, bfm(out), N, nullptr, bf(pre), nullptr, nullptr, 1};
+  GemmEpi ep{nullptr, bfm(out), N, nullptr, deriv ? nullptr : bf(pre), nullptr, nullptr, 1};
+  if (deriv) {
+    ep.dqa = pre.data_ptr<uint8_t>();
+    ep.dqs = (rate > 0.0 ? keep_params(rate).second : 1.f) / 195.f;  // common.h GD_Q
+  }
   torch::Tensor ws;
   const int epi = deriv ? 7 : 2;
   const int r = attach_tail(ep, ws, M, N, K, epi, A);
@@ -823,6 +837,27 @@ torch::Tensor gemm_nt_dgelu(torch::Tensor A, torch::Tensor B, torch::Tensor pre,
   check_rc(jm_gemm_nt(bf(A), A.stride(0), bf(B), B.stride(0), M, N, K, epi, ep, stream()), "gemm_nt_dgelu");
   if (dbias) check_rc(jm_splitk_reduce_add(part.data_ptr<float>(), dbias->data_ptr<float>(), N, nM, stream()),
                       "gemm_nt_dgelu dbias");
+  return out;
+}
+
+// ---------------------------------------------------------------- augment (csrc/augment.hip)
+// Pillow-exact RandomResizedCrop (bicubic) + flip of a batch of decoded crop windows on the device
+// (data/loader.py DeviceAugment): src = concatenated HWC uint8 windows, tab = [B, 13] int64
+// descriptors (csrc/augment.hip); tmp_bytes / tmp_rows_max from the host copy of the table.
+torch::Tensor rrc_resize(torch::Tensor src, torch::Tensor tab, int64_t size, int64_t tmp_bytes, int64_t tmp_rows_max) {
+  CHECK_CUDA(src);
+  CHECK_CUDA(tab);
+  CHECK_DT(src, torch::kUInt8);
+  CHECK_DT(tab, torch::kInt64);
+  TORCH_CHECK(src.dim() == 1 && src.is_contiguous(), "rrc_resize: src must be a flat uint8 buffer");
+  TORCH_CHECK(tab.dim() == 2 && tab.size(1) == 13 && tab.is_contiguous(), "rrc_resize: tab [B, 13] int64");
+  TORCH_CHECK(size > 0 && size <= 4096 && tmp_bytes > 0 && tmp_rows_max > 0, "rrc_resize: bad sizes");
+  const int B = tab.size(0);
+  auto out = torch::empty({B, 3, size, size}, src.options());
+  auto tmp = torch::empty({tmp_bytes}, src.options());
+  check_rc(jm_rrc_resize(src.data_ptr<uint8_t>(), tab.data_ptr<int64_t>(), B, (int)size, tmp.data_ptr<uint8_t>(),
+                         (int)tmp_rows_max, out.data_ptr<uint8_t>(), stream()),
+           "rrc_resize");
   return out;
 }
 
@@ -1166,6 +1201,7 @@ py::dict debug_lines() {
   py::dict d;
   const std::pair<const char*, int (*)()> tus[] = {
       {"attention", jm_debug_line_attention}, {"dropout", jm_debug_line_dropout},
+      {"augment", jm_debug_line_augment},
       {"elementwise", jm_debug_line_elementwise},
       {"gemm", jm_debug_line_gemm},           {"gemm_tn", jm_debug_line_gemm_tn},
       {"layernorm", jm_debug_line_layernorm}, {"mae", jm_debug_line_mae},
@@ -1192,6 +1228,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gelu_fwd", &gelu_fwd);
   m.def("dropout_apply", &dropout_apply);
   m.def("dropout_apply_", &dropout_apply_);
+  m.def("rrc_resize", &rrc_resize, py::arg("src"), py::arg("tab"), py::arg("size"), py::arg("tmp_bytes"),
+        py::arg("tmp_rows_max"));
+  m.def("rrc_kmax", &jm_rrc_kmax);
   m.def("gelu_drop", &gelu_drop, py::arg("a"), py::arg("b") = py::none(), py::arg("seed"), py::arg("rate"));
   m.def("softmax_dropout_fwd", &softmax_dropout_fwd);
   m.def("softmax_dropout_bwd", &softmax_dropout_bwd);
@@ -1229,7 +1268,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_nt_splitk", &gemm_nt_splitk, py::arg("A"), py::arg("B"), py::arg("bias") = py::none(),
         py::arg("splits") = 8, py::arg("add") = py::none());
   m.def("gemm_nt_dgelu", &gemm_nt_dgelu, py::arg("A"), py::arg("B"), py::arg("pre"), py::arg("dbias") = py::none(),
-        py::arg("deriv") = false);
+        py::arg("deriv") = false, py::arg("rate") = 0.0);
   m.def("gemm_nt_f32", &gemm_nt_f32, py::arg("A"), py::arg("B"));
   m.def("gemm_nt", &gemm_nt, py::arg("A"), py::arg("B"), py::arg("bias") = py::none(), py::arg("gelu") = false,
         py::arg("gelu_only") = false, py::arg("gelu_deriv") = false, py::arg("seed") = py::none(),

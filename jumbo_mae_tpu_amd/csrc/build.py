@@ -39,7 +39,8 @@ ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
 ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 HIPCC = os.path.join(ROCM, "bin", "hipcc")
 
-KERNELS = ["layernorm.hip", "elementwise.hip", "attention.hip", "optim.hip", "mae.hip", "gemm.hip", "gemm_tn.hip", "dropout.hip"]
+KERNELS = ["layernorm.hip", "elementwise.hip", "attention.hip", "optim.hip", "mae.hip", "gemm.hip", "gemm_tn.hip", "dropout.hip",
+           "augment.hip"]
 
 
 def _torch_paths():

@@ -9,6 +9,12 @@ Reference ``create_dataloaders`` (/root/reference/src/dataset.py:100-161) with h
 * valid: one pass, rank split, last batch padded with ``-1`` (uint8 images become 255, labels -1).
 * ``synthetic:N[:C]`` shard spec: N random images with C classes (plumbing tests / benchmarks;
   no dataset is reachable offline).
+* Device augment (``--device-augment``, on by default on a GPU when the train transform is the
+  pretraining one -- RandomResizedCrop + flip, nothing else): the workers decode, draw the crop /
+  flip parameters from the same per-sample RNG as the PIL path and ship only the crop window plus
+  a descriptor (``DeviceRRCParams``, packed per batch by ``collate_packed``); the resize and flip
+  run on the GPU (csrc/augment.hip), bit-exact to PIL's bicubic, when ``DevicePrefetcher`` lands
+  the batch.  A worker then spends its time on the JPEG decode only (profiles/r5_data_rate.txt).
 Per-rank split replaces the reference's per-host split (one process per GPU here).
 """
 
@@ -16,15 +22,103 @@ from __future__ import annotations
 
 import copy
 import itertools
+import math
 import random
 from functools import partial
+from typing import NamedTuple
 
 import numpy as np
 import torch
 from torch.utils.data import DataLoader, IterableDataset, get_worker_info
 
 from . import shards as S
-from .transforms import create_transforms
+from .transforms import RandomResizedCrop, create_transforms
+
+RRC_TAB = 13  # csrc/augment.hip descriptor width
+RRC_KMAX = 24  # csrc/augment.hip taps per output pixel
+
+
+class PackedImages(NamedTuple):
+    """A batch for the device augment: concatenated HWC uint8 crop windows + [B, 13] descriptors
+    (csrc/augment.hip), the scratch size of the horizontal pass and the output size."""
+    src: torch.Tensor
+    tab: torch.Tensor
+    tmp_bytes: int
+    rows_max: int
+    size: int
+
+
+def _span(n: int, a: int, c: int, out: int) -> tuple[int, int]:
+    """Input index range a superset of what Pillow's bicubic resample of [a, a + c) -> ``out`` reads."""
+    support = 2.0 * max(c / out, 1.0)
+    return max(0, math.floor(a - support) - 1), min(n, math.ceil(a + c + support) + 1)
+
+
+def _taps(c: int, out: int) -> int:
+    return math.ceil(2.0 * max(c / out, 1.0)) * 2 + 1  # Pillow's ksize
+
+
+class DeviceRRCParams:
+    """Worker side of the device augment, in place of RandomResizedCrop(scale 0.2-1, bicubic) +
+    RandomHorizontalFlip + PILToArray: the same RNG draws in the same order; returns the crop
+    window (HWC uint8) and its descriptor.  A crop too large for the kernel's tap budget is resized
+    here with PIL and shipped as an identity window."""
+
+    def __init__(self, size: int):
+        self.size = size
+        self.rrc = RandomResizedCrop(size, scale=(0.2, 1.0))
+
+    def __call__(self, img):
+        from PIL import Image
+        if img.mode != "RGB":
+            img = img.convert("RGB")
+        W, H = img.size
+        i, j, ch, cw = self.rrc.get_params(W, H)
+        flip = int(random.random() < 0.5)
+        S = self.size
+        if max(_taps(ch, S), _taps(cw, S)) > RRC_KMAX:
+            arr = np.asarray(img.resize((S, S), Image.BICUBIC, box=(j, i, j + cw, i + ch)))
+            H = W = S
+            i = j = 0
+            ch = cw = S
+        else:
+            arr = np.asarray(img)
+        y0, y1 = _span(H, i, ch, S)
+        x0, x1 = _span(W, j, cw, S)
+        win = np.ascontiguousarray(arr[y0:y1, x0:x1])
+        return win, np.array([0, y1 - y0, x1 - x0, y0, x0, H, W, i, j, ch, cw, flip, 0], dtype=np.int64)
+
+
+def collate_packed(batch, repeats: int = 1, size: int = 224):
+    """Device-augment collate: the repeat re-ordering of ``collate_and_shuffle``, then windows
+    concatenated into one flat buffer with offsets written into the descriptors."""
+    batch = sum([batch[i::repeats] for i in range(repeats)], [])
+    labels = None
+    if isinstance(batch[0][0], tuple):  # ((win, desc), label)
+        labels = torch.tensor([b[1] for b in batch])
+        batch = [b[0] for b in batch]
+    tab = np.stack([d for _, d in batch])
+    sizes = np.array([w.size for w, _ in batch], dtype=np.int64)
+    tab[:, 0] = np.concatenate([[0], np.cumsum(sizes)[:-1]])
+    rows = tab[:, 1]
+    tab[:, 12] = np.concatenate([[0], np.cumsum(rows * size * 3)[:-1]])
+    src = torch.from_numpy(np.concatenate([w.reshape(-1) for w, _ in batch]))
+    packed = PackedImages(src, torch.from_numpy(tab), int((rows * size * 3).sum()), int(rows.max()), size)
+    return packed if labels is None else (packed, labels)
+
+
+def unpack_on_device(p: PackedImages, device) -> torch.Tensor:
+    """uint8 [B, 3, S, S] from a packed batch: H2D of the windows, then the resize / flip kernels."""
+    from ..ops import _ext
+    src = p.src.to(device, non_blocking=True)
+    tab = p.tab.to(device, non_blocking=True)
+    return _ext.load(True).rrc_resize(src, tab, p.size, p.tmp_bytes, p.rows_max)
+
+
+def device_augment_ok(args) -> bool:
+    """The train transform is RandomResizedCrop + flip only (the pretraining presets)."""
+    return (getattr(args, "random_crop", "rrc") == "rrc" and getattr(args, "auto_augment", "none") in ("none", "", None)
+            and not getattr(args, "color_jitter", 0.0) and not getattr(args, "random_erasing", 0.0))
 
 
 def repeat_samples(samples, repeats: int = 1):
@@ -190,11 +284,16 @@ class ShardDataset(IterableDataset):
             epoch += 1
 
 
-def create_dataloaders(args, rank: int = 0, world: int = 1, start_batches: int = 0):
+def create_dataloaders(args, rank: int = 0, world: int = 1, start_batches: int = 0, device_augment: bool = False):
     """Returns (train_loader | None, valid_loader | None) like dataset.py:100-161.  ``start_batches``
-    (resume): train batches already consumed on this rank -- the stream continues after them."""
+    (resume): train batches already consumed on this rank -- the stream continues after them.
+    ``device_augment``: train batches are ``PackedImages`` for ``unpack_on_device`` (requires
+    ``device_augment_ok(args)``)."""
     train_t, valid_t = create_transforms(args.random_crop, args.image_size, args.auto_augment, args.color_jitter,
                                          args.random_erasing, args.test_crop_ratio)
+    if device_augment:
+        assert device_augment_ok(args), "device augment covers RandomResizedCrop + flip only"
+        train_t = DeviceRRCParams(args.image_size)
     train_dl = valid_dl = None
     pin = torch.cuda.is_available()
     if getattr(args, "train_dataset_shards", None):
@@ -203,8 +302,9 @@ def create_dataloaders(args, rank: int = 0, world: int = 1, start_batches: int =
                           args.shuffle_seed, rank, world, image_size=args.image_size,
                           skip_batches=start_batches, batch_size=bs)
         nw = args.train_loader_workers
-        train_dl = DataLoader(ds, batch_size=bs, num_workers=nw,
-                              collate_fn=partial(collate_and_shuffle, repeats=args.augment_repeats),
+        collate = (partial(collate_packed, repeats=args.augment_repeats, size=args.image_size) if device_augment
+                   else partial(collate_and_shuffle, repeats=args.augment_repeats))
+        train_dl = DataLoader(ds, batch_size=bs, num_workers=nw, collate_fn=collate,
                               drop_last=True, pin_memory=pin, prefetch_factor=4 if nw > 0 else None,
                               persistent_workers=nw > 0)
     if getattr(args, "valid_dataset_shards", None):

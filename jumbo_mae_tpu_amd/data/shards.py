@@ -264,7 +264,7 @@ def decode_pil(data: bytes):
 
     img = Image.open(io.BytesIO(data))
     img.load()
-    return img.convert("RGB")
+    return img if img.mode == "RGB" else img.convert("RGB")  # (convert would copy an RGB image)
 
 
 def decode_cls(data: bytes) -> int:

@@ -99,6 +99,9 @@ def _extensions(p: argparse.ArgumentParser):
                    help="end this invocation after N steps, writing 'last' (time-sliced / preemptible "
                         "jobs: continue with --resume auto); 0 = run to --training-steps")
     g.add_argument("--device", default=None, help="cuda|cpu (default: cuda if available)")
+    g.add_argument("--device-augment", default="auto", choices=["auto", "on", "off"],
+                   help="RandomResizedCrop + flip of the train batches on the GPU, bit-exact to PIL (auto: on a GPU "
+                        "when the train transform is exactly that -- the pretraining presets)")
     g.add_argument("--log-file-only", action="store_true", help="never use wandb even if installed")
     g.add_argument("--trace-ranges", action="store_true", help="roctx ranges per step phase (rocprofv3 --marker-trace)")
     g.add_argument("--hip-graph", action="store_true",

@@ -54,8 +54,22 @@ def make_reducer(args, store):
     return None
 
 
+def use_device_augment(args, device) -> bool:
+    """--device-augment: auto = on a GPU with the extension and the pretraining train transform."""
+    from ..data.loader import device_augment_ok
+    mode = getattr(args, "device_augment", "off")
+    if mode == "off" or device.type != "cuda" or not getattr(args, "train_dataset_shards", None):
+        return False
+    if not device_augment_ok(args):
+        if mode == "on":
+            raise SystemExit("--device-augment on: the train transform must be RandomResizedCrop + flip only")
+        return False
+    return True
+
+
 class DevicePrefetcher:
-    """Moves the next host batch to the device on a side stream while the current step runs."""
+    """Moves the next host batch to the device on a side stream while the current step runs; a
+    device-augment batch (data/loader.py ``PackedImages``) is resized / flipped there too."""
 
     def __init__(self, it, device):
         self.it = iter(it)
@@ -65,6 +79,9 @@ class DevicePrefetcher:
         self._preload()
 
     def _to(self, b):
+        from ..data.loader import PackedImages, unpack_on_device
+        if isinstance(b, PackedImages):
+            return unpack_on_device(b, self.device)
         if isinstance(b, (list, tuple)):
             return type(b)(self._to(x) for x in b)
         if isinstance(b, torch.Tensor):

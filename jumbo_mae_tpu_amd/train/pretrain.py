@@ -79,7 +79,8 @@ def main(args) -> dict:
     start = resumed.step
 
     # a resumed run continues the data stream after the batches the interrupted run consumed
-    train_loader, valid_loader = create_dataloaders(args, info.rank, info.world_size, resumed.batches)
+    train_loader, valid_loader = create_dataloaders(args, info.rank, info.world_size, resumed.batches,
+                                                    device_augment=C.use_device_augment(args, device))
     result = {}
     logger = Logger(args.output_dir, args.name, args.project, vars(args), enabled=info.is_main,
                     use_wandb=False if args.log_file_only else None)

@@ -279,3 +279,55 @@ def test_valid_dataset_uses_cache(tmp_path, monkeypatch):
     assert len(list(ds)) == 8
     assert len(list((tmp_path / "wc").iterdir())) == 2
     assert len(list(ds)) == 8  # second pass from the cache
+
+
+# ------------------------------------------------------------------ device augment (CPU side)
+def _dev_aug_args(spec, workers=0, batch=8):
+    from types import SimpleNamespace
+    return SimpleNamespace(random_crop="rrc", image_size=224, auto_augment="none", color_jitter=0.0,
+                           random_erasing=0.0, test_crop_ratio=0.875, train_dataset_shards=spec,
+                           valid_dataset_shards=None, mode="pretrain", train_batch_size=batch, grad_accum=1,
+                           augment_repeats=2, shuffle_seed=3, train_loader_workers=workers, valid_batch_size=batch,
+                           valid_loader_workers=0)
+
+
+def test_device_augment_packed_batches_equal_pil(tmp_path):
+    """The device-augment workers (decode + the same RNG draws, crop windows + descriptors) and
+    the NumPy mirror of csrc/augment.hip reproduce the PIL transform's batches bit for bit,
+    repeated augmentation included."""
+    from jumbo_mae_tpu_amd.data.jpeg_shards import write_shards
+    from jumbo_mae_tpu_amd.data.loader import PackedImages, create_dataloaders
+    from jumbo_mae_tpu_amd.data.resample_ref import unpack_packed
+    spec = write_shards(str(tmp_path), shards=2, per_shard=12, classes=5, seed=4)
+    cpu, _ = create_dataloaders(_dev_aug_args(spec))
+    dev, _ = create_dataloaders(_dev_aug_args(spec), device_augment=True)
+    for (a, b), _ in zip(zip(cpu, dev), range(3)):
+        assert isinstance(b, PackedImages) and b.tab.shape == (8, 13)
+        assert b.src.numel() < 8 * 500 * 500 * 3  # crop windows, not whole pictures
+        got = unpack_packed(b)
+        assert got.shape == tuple(a.shape) and np.array_equal(got, a.numpy())
+
+
+def test_device_augment_large_crop_fallback():
+    """A crop beyond the kernel's tap budget is resized by PIL in the worker and shipped as an
+    identity window: same result."""
+    import random
+
+    from PIL import Image
+
+    from jumbo_mae_tpu_amd.data.loader import DeviceRRCParams, collate_packed
+    from jumbo_mae_tpu_amd.data.resample_ref import unpack_packed
+    from jumbo_mae_tpu_amd.data.transforms import create_transforms
+    rs = np.random.default_rng(0)
+    imgs = [Image.fromarray(rs.integers(0, 256, (h, w, 3), dtype=np.uint8)) for h, w in
+            ((1500, 2100), (300, 260), (2600, 1900), (224, 224))]
+    cpu_t, _ = create_transforms("rrc", 224, "none", 0.0, 0.0, 0.875)
+    dev_t = DeviceRRCParams(224)
+    want, got = [], []
+    for k, im in enumerate(imgs):
+        random.seed(k)
+        want.append(cpu_t(im))
+        random.seed(k)
+        got.append(dev_t(im))
+    assert got[0][1][5] == 224  # fell back: identity window
+    assert np.array_equal(unpack_packed(collate_packed(got)), np.stack(want))
