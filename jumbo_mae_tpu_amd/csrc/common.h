@@ -142,6 +142,31 @@ JM_DEVICE void gelu_n(const float* x, float* g, float* d) {
   }
 }
 
+// gelu'(h) of the tanh GELU lies in [-0.1701, 1.1290].  The FF1 forward saves it for the FF2 data
+// gradient as an 8-bit code q = round(GD_Q gelu') + GD_Z -- step 1 / 195 = 0.0051, |error| <= 0.0026
+// (bf16 rounds values near 1 by up to 0.002), 0 and 1 exact (codes 34 and 229), codes 1..254 used --
+// half the bytes of a bf16 copy on both sides of the round trip (ops/prims.py GD_Q / GD_Z mirror).
+constexpr float GD_Q = 195.f;
+constexpr int GD_Z = 34;
+JM_DEVICE uint32_t gd_code(float d) {
+  return (uint32_t)fminf(fmaxf(__builtin_fmaf(d, GD_Q, (float)GD_Z + 0.5f), 0.f), 255.f);
+}
+// 8 derivatives -> 8 codes, 4 per 32-bit word, element 0 in the low byte
+JM_DEVICE uint2 gd_pack8(const float* d) {
+  uint2 v;
+  v.x = gd_code(d[0]) | (gd_code(d[1]) << 8) | (gd_code(d[2]) << 16) | (gd_code(d[3]) << 24);
+  v.y = gd_code(d[4]) | (gd_code(d[5]) << 8) | (gd_code(d[6]) << 16) | (gd_code(d[7]) << 24);
+  return v;
+}
+// codes -> (q - GD_Z) * s (v_cvt_f32_ubyte0..3 + one fma per element)
+JM_DEVICE void gd_unpack4(uint32_t w, float s, float* d) {
+  const float z = -(float)GD_Z * s;
+  d[0] = __builtin_fmaf((float)(w & 255u), s, z);
+  d[1] = __builtin_fmaf((float)((w >> 8) & 255u), s, z);
+  d[2] = __builtin_fmaf((float)((w >> 16) & 255u), s, z);
+  d[3] = __builtin_fmaf((float)(w >> 24), s, z);
+}
+
 // DPP lane moves (VALU, no LDS round trip like __shfl_xor's ds_bpermute)
 template <int CTRL>
 JM_DEVICE float dpp_mov(float v) {

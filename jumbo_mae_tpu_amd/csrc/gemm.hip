@@ -69,28 +69,29 @@ struct Frags {
 // EPI_GELU_ONLY: out = gelu(bf16(acc + bias)) alone -- inference (no backward needs the
 // pre-activation), half the epilogue bytes of EPI_GELU.
 // EPI_TAIL: split-K partial tile of a tail-split launch, stored compact in ep.tail (see GemmEpi).
-// EPI_GELU_D: out = gelu'(h), out2 = gelu(h) for h = bf16(acc + bias): the FF1 forward saves the GELU
-// derivative for the backward instead of h (one shared tanh here, no tanh in the backward epilogue).
-// EPI_DMUL: out = bf16(acc) * aux with aux = the saved gelu'(h), + column partials as EPI_DGELU.
+// EPI_GELU_D: dq = gelu'(h) as 8-bit codes (common.h gd_code), out2 = gelu(h) for h = bf16(acc + bias):
+// the FF1 forward saves the GELU derivative for the backward instead of h (one shared exp here, no
+// transcendental in the backward epilogue), in 1 byte per element instead of 2.
+// EPI_DMUL: out = bf16(acc) * gelu'(h) decoded from dqa, + column partials as EPI_DGELU.
 enum { EPI_STORE = 0, EPI_GELU = 1, EPI_DGELU = 2, EPI_PARTIAL = 3, EPI_GELU_ONLY = 4, EPI_TAIL = 5, EPI_GELU_D = 6,
        EPI_DMUL = 7 };
 
 namespace {
 
 // FF hidden dropout of the EPI_GELU_D outputs (GemmEpi::dseed): W consecutive elements from flat
-// index idx0 (even), both gelu(h) and gelu'(h) times the keep bit / keep
+// index idx0 (even); gelu(h) times the keep bit / keep, gelu'(h) times the keep bit (its 1 / keep is
+// applied when EPI_DMUL decodes the 8-bit code, GemmEpi::dqs, so the code range stays [-0.17, 1.13])
 template <int W>
 JM_DEVICE void gelu_d_drop(const GemmEpi& ep, long idx0, float* g, float* d) {
   const uint64_t seed = (uint64_t)ep.dseed[0];
 #pragma unroll
   for (int j = 0; j < W; j += 2) {
     const uint32_t h = drop_hash((uint32_t)((idx0 + j) >> 1), seed);
-    const float k0 = drop_keep_half(h, 0, ep.dthr) ? ep.dscale : 0.f;
-    const float k1 = drop_keep_half(h, 1, ep.dthr) ? ep.dscale : 0.f;
-    g[j] *= k0;
-    d[j] *= k0;
-    g[j + 1] *= k1;
-    d[j + 1] *= k1;
+    const bool k0 = drop_keep_half(h, 0, ep.dthr), k1 = drop_keep_half(h, 1, ep.dthr);
+    g[j] = k0 ? g[j] * ep.dscale : 0.f;
+    d[j] = k0 ? d[j] : 0.f;
+    g[j + 1] = k1 ? g[j + 1] * ep.dscale : 0.f;
+    d[j + 1] = k1 ? d[j + 1] : 0.f;
   }
 }
 
@@ -120,7 +121,8 @@ JM_DEVICE void epilogue(const f32x4_t (&acc)[8][NTW], const GemmEpi& ep, int M, 
 #pragma unroll
         for (int i = 0; i < 4; ++i) gelu_and_grad_f(bf2f(f2bf(v[i])), gv[i], dv[i]);
         if (ep.dseed) gelu_d_drop<4>(ep, (long)m * ep.ldo + n, gv, dv);
-        store4(ep.out + (long)m * ep.ldo + n, dv);
+        *reinterpret_cast<uint32_t*>(ep.dq + (long)m * ep.ldo + n) =
+            gd_code(dv[0]) | (gd_code(dv[1]) << 8) | (gd_code(dv[2]) << 16) | (gd_code(dv[3]) << 24);
         store4(ep.out2 + (long)m * ep.ldo + n, gv);
         continue;
       }
@@ -193,6 +195,12 @@ JM_DEVICE void st16(T* p, uint4 v, bool nts) {
   else *reinterpret_cast<uint4*>(p) = v;
 }
 
+JM_DEVICE void st8(uint8_t* p, uint2 v, bool nts) {
+  typedef __attribute__((ext_vector_type(2))) unsigned int u32x2_t;
+  if (nts) __builtin_nontemporal_store(u32x2_t{v.x, v.y}, reinterpret_cast<u32x2_t*>(p));
+  else *reinterpret_cast<uint2*>(p) = v;
+}
+
 JM_DEVICE uint4 pack8(const float* f) {
   uint4 v;
   v.x = pack_bf2(f[0], f[1]);
@@ -224,7 +232,15 @@ JM_DEVICE void epilogue_lds(const f32x4_t (&acc)[8][NTW], const GemmEpi& ep, uin
   auto aux_load = [&](int i) {
     const int m = m0 + tid / LPR + i * RPP;
     uint4 a = make_uint4(0, 0, 0, 0);
-    if (m < M && col_ok) a = *reinterpret_cast<const uint4*>(ep.aux + (long)m * ep.ldo + n0 + c * 8);
+    if (m < M && col_ok) {
+      if constexpr (EPI == EPI_DMUL) {  // 8 gelu' codes
+        const uint2 q = *reinterpret_cast<const uint2*>(ep.dqa + (long)m * ep.ldo + n0 + c * 8);
+        a.x = q.x;
+        a.y = q.y;
+      } else {
+        a = *reinterpret_cast<const uint4*>(ep.aux + (long)m * ep.ldo + n0 + c * 8);
+      }
+    }
     return a;
   };
   if constexpr (PRE) {
@@ -256,10 +272,15 @@ JM_DEVICE void epilogue_lds(const f32x4_t (&acc)[8][NTW], const GemmEpi& ep, uin
       if (EPI == EPI_DGELU || EPI == EPI_DMUL) {
         float f[8], hp[8], gd[8];
         const uint16_t* dg = reinterpret_cast<const uint16_t*>(&v);
-        const uint16_t* ah = reinterpret_cast<const uint16_t*>(&av);
+        if constexpr (EPI == EPI_DMUL) {
+          gd_unpack4(av.x, ep.dqs, hp);
+          gd_unpack4(av.y, ep.dqs, hp + 4);
+        } else {
+          const uint16_t* ah = reinterpret_cast<const uint16_t*>(&av);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) hp[j] = bf2f(ah[j]);
-        if (EPI == EPI_DGELU) gelu_n<8, false, true>(hp, nullptr, gd);
+          for (int j = 0; j < 8; ++j) hp[j] = bf2f(ah[j]);
+          gelu_n<8, false, true>(hp, nullptr, gd);
+        }
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           f[j] = bf2f(f2bf(bf2f(dg[j]) * (EPI == EPI_DMUL ? hp[j] : gd[j])));
@@ -273,7 +294,7 @@ JM_DEVICE void epilogue_lds(const f32x4_t (&acc)[8][NTW], const GemmEpi& ep, uin
         for (int j = 0; j < 8; ++j) fh[j] = bf2f(h[j]);
         gelu_n<8, true, true>(fh, fg, fd);
         if (ep.dseed) gelu_d_drop<8>(ep, (long)m * ep.ldo + n0 + c * 8, fg, fd);
-        st16(ep.out + (long)m * ep.ldo + n0 + c * 8, pack8(fd), NTS);
+        st8(ep.dq + (long)m * ep.ldo + n0 + c * 8, gd_pack8(fd), NTS);
         st16(ep.out2 + (long)m * ep.ldo + n0 + c * 8, pack8(fg), NTS);
       } else if (EPI == EPI_GELU_ONLY) {
         float fh[8], f[8];
@@ -847,7 +868,15 @@ JM_DEVICE void narrow_epilogue(const f32x4_t (&acc)[4][3], const GemmEpi& ep, ui
     for (int i = 0; i < 8; ++i) {
       const int m = m0 + rr + 16 * i;
       auxv[i] = make_uint4(0, 0, 0, 0);
-      if (col_ok && m < M) auxv[i] = *reinterpret_cast<const uint4*>(ep.aux + (long)m * ep.ldo + n);
+      if (col_ok && m < M) {
+        if constexpr (EPI == EPI_DMUL) {  // 8 gelu' codes
+          const uint2 q = *reinterpret_cast<const uint2*>(ep.dqa + (long)m * ep.ldo + n);
+          auxv[i].x = q.x;
+          auxv[i].y = q.y;
+        } else {
+          auxv[i] = *reinterpret_cast<const uint4*>(ep.aux + (long)m * ep.ldo + n);
+        }
+      }
     }
   }
   float csum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
@@ -860,11 +889,16 @@ JM_DEVICE void narrow_epilogue(const f32x4_t (&acc)[4][3], const GemmEpi& ep, ui
       uint16_t* o = ep.out + (long)m * ep.ldo + n;
       const uint16_t* h = reinterpret_cast<const uint16_t*>(&v);
       if constexpr (PRE) {
-        const uint16_t* ah = reinterpret_cast<const uint16_t*>(&auxv[i]);
         float f[8], hp[8], gd[8];
+        if constexpr (EPI == EPI_DMUL) {
+          gd_unpack4(auxv[i].x, ep.dqs, hp);
+          gd_unpack4(auxv[i].y, ep.dqs, hp + 4);
+        } else {
+          const uint16_t* ah = reinterpret_cast<const uint16_t*>(&auxv[i]);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) hp[j] = bf2f(ah[j]);
-        if constexpr (EPI == EPI_DGELU) gelu_n<8, false, true>(hp, nullptr, gd);
+          for (int j = 0; j < 8; ++j) hp[j] = bf2f(ah[j]);
+          gelu_n<8, false, true>(hp, nullptr, gd);
+        }
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           f[j] = bf2f(f2bf(bf2f(h[j]) * (EPI == EPI_DMUL ? hp[j] : gd[j])));
@@ -877,7 +911,7 @@ JM_DEVICE void narrow_epilogue(const f32x4_t (&acc)[4][3], const GemmEpi& ep, ui
         for (int j = 0; j < 8; ++j) fh[j] = bf2f(h[j]);
         gelu_n<8, true, true>(fh, fg, fd);
         if (ep.dseed) gelu_d_drop<8>(ep, (long)m * ep.ldo + n, fg, fd);
-        st16(o, pack8(fd), false);
+        st8(ep.dq + (long)m * ep.ldo + n, gd_pack8(fd), false);
         st16(ep.out2 + (long)m * ep.ldo + n, pack8(fg), false);
       } else if constexpr (EPI == EPI_GELU_ONLY) {
         float fh[8], f[8];

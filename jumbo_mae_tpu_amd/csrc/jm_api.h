@@ -44,7 +44,7 @@ struct TnGroup {
 // Epilogue / output description of an NT GEMM launch (gemm.hip, bindings.cpp).
 struct GemmEpi {
   const float* bias;     // [N] fp32 or null
-  uint16_t* out;         // bf16 [M, ldo]
+  uint16_t* out;         // bf16 [M, ldo] (EPI_GELU_D: unused, see dq)
   long ldo;
   uint16_t* out2;        // EPI_GELU: gelu(out) bf16 [M, ldo]
   const uint16_t* aux;   // EPI_DGELU: pre-activation h bf16 [M, ldo]
@@ -58,9 +58,14 @@ struct GemmEpi {
   int tail_S;
   int t_begin;
   int t_count;
-  // EPI_GELU_D: FF hidden dropout (ops/blocks.py Drops) -- both outputs times keep(seed, m * ldo + n)
-  // / keep (common.h drop_keep); dseed null: none
+  // EPI_GELU_D: FF hidden dropout (ops/blocks.py Drops) -- gelu(h) times keep(seed, m * ldo + n) / keep
+  // (common.h drop_keep), gelu'(h) times the keep bit alone (its 1 / keep travels as dqs); dseed null: none
   const int64_t* dseed;
   uint32_t dthr;
   float dscale;
+  // gelu'(h) as 8-bit codes (common.h gd_code): EPI_GELU_D writes dq [M, ldo] u8, EPI_DMUL reads dqa and
+  // decodes code q as (q - GD_Z) * dqs (dqs = keep scale / GD_Q)
+  uint8_t* dq;
+  const uint8_t* dqa;
+  float dqs;
 };

@@ -121,19 +121,17 @@ def _ff_fwd(ff, h, train=True, rate=0.0, sh=None, so=None):
     applied by the residual kernels that read y (``_od``)."""
     pre, g, deriv, dropped = P.linear_gelu_fwd_saved(h, ff.w1.k, ff.w1.b, need_pre=train,
                                                      drop=(sh, rate) if sh is not None else None)
-    if sh is not None and not dropped:
-        if deriv:
-            Dr.gelu_drop(g, pre, sh, rate)
-        else:
-            g, pre = Dr.gelu_drop(pre, None, sh, rate)
-            deriv = True
+    if sh is not None and not dropped:  # (the fused gelu' forward drops inside its epilogue)
+        g, pre = Dr.gelu_drop(pre, None, sh, rate)  # saved: the masked, scaled bf16 gelu'
+        deriv = True
     y = P.linear_fwd(g, ff.w2.k, ff.w2.b)  # its dropout (seed so) is applied where y is consumed
     return pre, g, y, deriv
 
 
-def _ff_bwd(ff, dy, h, pre, g, w2_bias_done=False, dx_add=None, deriv=False):
+def _ff_bwd(ff, dy, h, pre, g, w2_bias_done=False, dx_add=None, deriv=False, rate=0.0):
+    """``rate``: the hidden dropout rate the forward folded into uint8 gelu' codes (``pre``)."""
     hb1 = ff.w1.b if ff.w1.k.segs[0].trainable else None
-    dpre, bias_done = P.linear_gelu_bwd(dy, g, pre, ff.w2.k, ff.w2.b, hb1, w2_bias_done, deriv)
+    dpre, bias_done = P.linear_gelu_bwd(dy, g, pre, ff.w2.k, ff.w2.b, hb1, w2_bias_done, deriv, rate)
     return P.linear_bwd(dpre, h, ff.w1.k, ff.w1.b, bias_done=bias_done, dx_add=dx_add)
 
 
@@ -186,6 +184,7 @@ class JumboBlockFn(torch.autograd.Function):
         ctx.layer = layer
         ctx.link_in, ctx.link_out = link_in, link_out
         ctx.gelu_deriv = (jd, fd)  # FF1 saved gelu'(h) instead of h (jumbo MLP, patch FF)
+        ctx.gelu_rate = rate  # hidden dropout folded into uint8 gelu' codes (P.gd_decode)
         ctx.dr = dr
         if link_out is not None:
             link_out.spec = P.ResSpec(fy, layer.scale2, m2, layer.ff.w2.b, C, drop=_od(dr, "fo", fy))
@@ -217,7 +216,7 @@ def _jumbo_bwd(ctx, dx2):
     djy, bd = P.residual_bwd(dcls, jy, layer.scale3, m3, dt, layer.jumbo_mlp.w2.b, drop=_od(dr, "jo", jy))
     # d hc = dcls + JumboMLP'(...) in fp32, the add fused into the jumbo dgrad's split-K reduce
     dhc = _ff_bwd(layer.jumbo_mlp, djy, hcb, jpre, jg, bd, dx_add=dcls.reshape(B, J),
-                  deriv=ctx.gelu_deriv[0])
+                  deriv=ctx.gelu_deriv[0], rate=ctx.gelu_rate)
     P.ln_bwd(dhc, x1[:, :C].reshape(B, 1, J), muc, rsc, layer.norm3.g, layer.norm3.b,
              out=dx1[:, :C].reshape(B, 1, J))
     # attention-residual backward of the CLS rows (the patch rows ride on LN2' below, which
@@ -230,7 +229,7 @@ def _jumbo_bwd(ctx, dx2):
         dfy, bd = fused
     else:
         dfy, bd = P.residual_bwd(dx2[:, C:], fy, layer.scale2, m2, dt, layer.ff.w2.b, drop=_od(dr, "fo", fy))
-    dhp = _ff_bwd(layer.ff, dfy, hp, fpre, fg, bd, deriv=ctx.gelu_deriv[1])
+    dhp = _ff_bwd(layer.ff, dfy, hp, fpre, fg, bd, deriv=ctx.gelu_deriv[1], rate=ctx.gelu_rate)
     # ... and the attention-residual backward of those rows in the same pass
     _, _, bd = P.ln_bwd(dhp, x1[:, C:], mup, rsp, layer.norm2.g, layer.norm2.b, dres=dx2[:, C:],
                         out=dx1[:, C:],
@@ -291,6 +290,7 @@ class ViTBlockFn(torch.autograd.Function):
         ctx.layer = layer
         ctx.link_in, ctx.link_out = link_in, link_out
         ctx.gelu_deriv = (False, fd)
+        ctx.gelu_rate = dr.rate if dr is not None else 0.0
         ctx.dr = dr
         if link_out is not None:
             link_out.spec = P.ResSpec(fy, layer.scale2, m2, layer.ff.w2.b, 0, drop=_od(dr, "fo", fy))
@@ -315,7 +315,7 @@ def _vit_bwd(ctx, dx2):
         dfy, bd = fused
     else:
         dfy, bd = P.residual_bwd(dx2, fy, layer.scale2, m2, dt, layer.ff.w2.b, drop=_od(dr, "fo", fy))
-    dh2 = _ff_bwd(layer.ff, dfy, h2, fpre, fg, bd, deriv=ctx.gelu_deriv[1])
+    dh2 = _ff_bwd(layer.ff, dfy, h2, fpre, fg, bd, deriv=ctx.gelu_deriv[1], rate=ctx.gelu_rate)
     # LN2' with the attention-residual backward of its dx fused in (never write autograd's dx2)
     dx1, da, bd = P.ln_bwd(dh2, x1, mu2, rs2, layer.norm2.g, layer.norm2.b, dres=dx2,
                            res=P.ResSpec(a, layer.scale1, m1, layer.attn.wo_b, drop=_od(dr, "wo", a)))

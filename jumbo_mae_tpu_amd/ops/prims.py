@@ -237,14 +237,31 @@ def linear_gelu_fwd(x2: torch.Tensor, hw: Handle, hb: Handle | None, need_pre: b
 _GELU_DERIV = True
 
 
+# gelu'(h) saved as 8-bit codes by the fused FF1 forward (csrc/common.h gd_code): q = round(GD_Q d) + GD_Z
+GD_Q, GD_Z = 195.0, 34
+
+
+def gd_encode(d: torch.Tensor) -> torch.Tensor:
+    """Torch mirror of the epilogue's gelu' code (tests); the kernel's fma may differ at exact ties."""
+    return torch.clamp(torch.floor(d.float() * GD_Q + (GD_Z + 0.5)), 0, 255).to(torch.uint8)
+
+
+def gd_decode(q: torch.Tensor, rate: float = 0.0, dtype=torch.bfloat16) -> torch.Tensor:
+    """gelu'(h) from its codes; ``rate``: the forward's hidden dropout (codes of the unscaled kept value)."""
+    s = (1.0 / (1.0 - rate) if rate > 0 else 1.0) / GD_Q
+    return ((q.float() - GD_Z) * s).to(dtype)
+
+
 def linear_gelu_fwd_saved(x2: torch.Tensor, hw: Handle, hb: Handle | None, need_pre: bool = True, drop=None):
     """Like ``linear_gelu_fwd`` but returns (saved, gelu(h), deriv, dropped): on the fused MFMA path
-    the epilogue computes gelu(h) and gelu'(h) from one tanh and ``saved`` is gelu'(h) (deriv True),
-    so the backward's data-gradient epilogue multiplies instead of re-deriving it from h;
-    otherwise ``saved`` is h (deriv False).  ``drop`` = (seed, rate): hidden dropout applied to both
-    outputs inside that epilogue (dropped True); the other paths leave it to the caller."""
+    the epilogue computes gelu(h) and gelu'(h) from one exp and ``saved`` is gelu'(h) as uint8 codes
+    (deriv True, ``gd_decode``), so the backward's data-gradient epilogue multiplies instead of
+    re-deriving it from h and reads 1 byte per element; otherwise ``saved`` is h (deriv False).
+    ``drop`` = (seed, rate): hidden dropout applied inside that epilogue (dropped True; the codes
+    hold the unscaled kept derivative, 1 / keep is applied when the backward decodes them); the
+    other paths leave it to the caller."""
     w = hw.weight()
-    if (_GELU_DERIV and need_pre and hip(x2) and x2.dtype == torch.bfloat16
+    if (_GELU_DERIV and need_pre and hip(x2) and x2.dtype == torch.bfloat16 and w.shape[0] % 8 == 0
             and use_our_gemm(x2.shape[0], w.shape[0], x2.shape[1], True)):
         bias = hb.master if hb is not None else None
         if drop is not None:
@@ -466,21 +483,25 @@ def linear_bwd(dy: torch.Tensor, x2: torch.Tensor, hw: Handle, hb: Handle | None
 
 
 def linear_gelu_bwd(dy: torch.Tensor, g: torch.Tensor, pre: torch.Tensor, hw2: Handle, hb2: Handle | None,
-                    hb1: Handle | None, bias2_done: bool = False, deriv: bool = False):
+                    hb1: Handle | None, bias2_done: bool = False, deriv: bool = False, rate: float = 0.0):
     """Backward of ``y = Dense2(gelu(pre))`` down to d pre: returns (dpre, bias1_done).
 
     Fused path: one MFMA GEMM dy . W2 whose epilogue multiplies by gelu'(pre) and emits the
     column sums of dpre (= the gradient of Dense1's bias ``hb1``), so the GEMM output dg never
     makes an HBM round trip.  W2's own gradients (wgrad, bias) are queued as usual.  ``deriv``:
-    ``pre`` is the saved gelu'(h) (``linear_gelu_fwd_saved``), not h."""
+    ``pre`` is the saved gelu'(h) (``linear_gelu_fwd_saved``; uint8 codes), not h; ``rate``: the
+    forward's hidden dropout rate folded into those codes."""
     w2 = hw2.weight()
     M, N, K = dy.shape[0], w2.shape[1], w2.shape[0]
     if (_DGRAD_OURS and hip(dy) and dy.dtype == torch.bfloat16 and N % 8 == 0
+            and (not deriv or pre.dtype == torch.uint8)  # a bf16 gelu' (unfused forward) takes gelu_bwd
             and use_our_gemm(M, N, K, fused_gelu=True, kind="dgrad")):
         bg = hb1.grad if _trainable(hb1) else None
-        dpre = _ext.load().gemm_nt_dgelu(dy.contiguous(), hw2.weight_t(), pre.contiguous(), bg, deriv)
+        dpre = _ext.load().gemm_nt_dgelu(dy.contiguous(), hw2.weight_t(), pre.contiguous(), bg, deriv, rate)
         linear_bwd(dy, g, hw2, hb2, need_dx=False, bias_done=bias2_done)
         return dpre, bg is not None
+    if deriv and pre.dtype == torch.uint8:
+        pre = gd_decode(pre, rate, dy.dtype)
     dg = linear_bwd(dy, g, hw2, hb2, bias_done=bias2_done)
     return gelu_bwd(pre, dg, hb1, deriv)
 

@@ -271,20 +271,33 @@ def test_gemm_nt_short_rows(ext, M, N, K, lda, rows):
     assert rel(go, g) < 1e-2
     if N % 8:
         return
-    d, g2 = ext.gemm_nt(x, w, b, True, False, True)
+    dq, g2 = ext.gemm_nt(x, w, b, True, False, True)
     hr = h.float()
     t = torch.tanh(0.7978845608028654 * (hr + 0.044715 * hr ** 3))
     dref = 0.5 * (1 + t) + 0.5 * hr * (1 - t * t) * 0.7978845608028654 * (1 + 3 * 0.044715 * hr * hr)
-    assert rel(d, dref) < 1e-2 and rel(g2, g) < 1e-2
+    d = _gd_check(dq, dref)
+    assert rel(g2, g) < 1e-2
     # data gradient through the GELU: [M, K'] x [N, K']^T * gelu'(pre)
     dy = (torch.rand(M, K, device="cuda") * 2 - 1).bfloat16()
     dg = (dy.float() @ w.float().t()).bfloat16().float()
-    for deriv, aux, fac in ((False, h, dref), (True, d, d.float())):
+    for deriv, aux, fac in ((False, h, dref), (True, dq, d)):
         db = torch.full((N,), 0.25, device="cuda")
         o = ext.gemm_nt_dgelu(dy, w, aux, db, deriv)
         r = dg * fac
         assert rel(o, r) < 1e-2, deriv
         assert rel(db - 0.25, r.sum(0)) < 1e-2, deriv
+
+
+def _gd_check(dq, dref):
+    """uint8 gelu' codes of the fused FF1 forward (csrc/common.h gd_code) against the fp32 derivative
+    of the same bf16 pre-activation: the torch mirror's code up to one step (fma vs two roundings at
+    exact ties), the decoded value within half a step.  Returns the decoded fp32 gelu'."""
+    from jumbo_mae_tpu_amd.ops import prims as P
+    assert dq.dtype == torch.uint8 and dq.shape == dref.shape
+    assert (dq.int() - P.gd_encode(dref).int()).abs().max().item() <= 1
+    d = P.gd_decode(dq, dtype=torch.float32)
+    assert (d - dref).abs().max().item() <= 0.5 / P.GD_Q + 1e-4
+    return d
 
 
 def test_gemm_tile_rows_choice(ext):
@@ -652,7 +665,7 @@ def test_gemm_gelu_saved_derivative(ext, M, N, K, variant):
     hf = h.float()
     t = torch.tanh(0.7978845608028654 * (hf + 0.044715 * hf ** 3))
     dref = 0.5 * (1 + t) + 0.5 * hf * (1 - t * t) * 0.7978845608028654 * (1 + 3 * 0.044715 * hf * hf)
-    assert (gp.float() - dref).abs().max().item() < 1e-2
+    _gd_check(gp, dref)
     dy = (torch.randn(M, 384, device="cuda") * 0.5).bfloat16()
     w2t = (torch.randn(N, 384, device="cuda") * 0.05).bfloat16()
     db1, db2 = torch.zeros(N, device="cuda"), torch.zeros(N, device="cuda")
@@ -662,8 +675,41 @@ def test_gemm_gelu_saved_derivative(ext, M, N, K, variant):
     da = (torch.randn(M, N, device="cuda")).bfloat16()
     bg1, bg2 = torch.zeros(N, device="cuda"), torch.zeros(N, device="cuda")
     e1 = ext.gelu_bwd(h, da, bg1)
-    e2 = ext.gelu_bwd(gp, da, bg2, True)
+    from jumbo_mae_tpu_amd.ops import prims as P
+    e2 = ext.gelu_bwd(P.gd_decode(gp), da, bg2, True)
     assert rel(e2, e1) < 1e-2 and rel(bg2, bg1) < 1e-2
+
+
+@pytest.mark.parametrize("M,N,K", [(4352, 1024, 256), (512, 12288, 192)])
+def test_gemm_gelu_saved_derivative_dropout(ext, M, N, K):
+    """FF hidden dropout inside the GELU_D epilogue (4-phase and narrow kernels): gelu(h) is masked
+    and scaled by 1 / keep, the gelu' codes hold the unscaled derivative where kept and exact 0 where
+    dropped, and the DMUL data gradient decoding them with ``rate`` == dg * gelu'(h) * mask / keep."""
+    from jumbo_mae_tpu_amd.ops import dropout as Dr
+    from jumbo_mae_tpu_amd.ops import prims as P
+    torch.manual_seed(3)
+    rate = 0.1
+    x = (torch.randn(M, K, device="cuda") * 0.5).bfloat16()
+    w = (torch.randn(N, K, device="cuda") * 0.1).bfloat16()
+    b = torch.randn(N, device="cuda") * 0.1
+    seed = torch.tensor([0x5EED], dtype=torch.int64, device="cuda")
+    h, g = ext.gemm_nt(x, w, b, True)
+    gp, gd = ext.gemm_nt(x, w, b, True, False, True, seed, rate)
+    keep = Dr.keep_mask(seed.cpu(), M * N, rate).view(M, N).cuda()
+    scale = 1.0 / (1.0 - rate)
+    assert torch.equal(gd, torch.where(keep, (g.float() * scale).bfloat16(), torch.zeros_like(g)))
+    hf = h.float()
+    t = torch.tanh(0.7978845608028654 * (hf + 0.044715 * hf ** 3))
+    dref = 0.5 * (1 + t) + 0.5 * hf * (1 - t * t) * 0.7978845608028654 * (1 + 3 * 0.044715 * hf * hf)
+    assert bool((gp[~keep] == P.GD_Z).all())
+    _gd_check(torch.where(keep, gp, P.gd_encode(dref)), dref)
+    dy = (torch.randn(M, 384, device="cuda") * 0.5).bfloat16()
+    w2t = (torch.randn(N, 384, device="cuda") * 0.05).bfloat16()
+    db = torch.zeros(N, device="cuda")
+    out = ext.gemm_nt_dgelu(dy, w2t, gp, db, True, rate)
+    ref = (dy.float() @ w2t.float().t()).bfloat16().float() * P.gd_decode(gp, rate, torch.float32)
+    assert rel(out, ref) < 1e-2 and rel(db, ref.sum(0)) < 1e-2
+    assert bool((out[~keep] == 0).all())
 
 
 def test_transpose_bf16_batch(ext):
@@ -724,16 +770,19 @@ def test_gemm_narrow_epilogues(ext, M, N, K):
     hr = h.float()
     t = torch.tanh(0.7978845608028654 * (hr + 0.044715 * hr ** 3))
     d = 0.5 * (1 + t) + 0.5 * hr * (1 - t * t) * 0.7978845608028654 * (1 + 3 * 0.044715 * hr * hr)
-    assert rel(gd, d) < 1e-2 and rel(g2, gref) < 1e-2
+    _gd_check(gd, d)
+    assert rel(g2, gref) < 1e-2
     f = ext.gemm_nt_f32(x, w)
     assert f.dtype == torch.float32 and rel(f, base) < 1e-5
     pre = (torch.randn(M, N, device="cuda") * 2).bfloat16()
+    codes = torch.randint(0, 256, (M, N), device="cuda", dtype=torch.uint8)
+    from jumbo_mae_tpu_amd.ops import prims as P
     for deriv in (False, True):
         db = torch.full((N,), 0.5, device="cuda")
-        out = ext.gemm_nt_dgelu(x, w, pre, db, deriv)
+        out = ext.gemm_nt_dgelu(x, w, codes if deriv else pre, db, deriv)
         p = pre.float()
         if deriv:
-            mul = p
+            mul = P.gd_decode(codes, dtype=torch.float32)
         else:
             tt = torch.tanh(0.7978845608028654 * (p + 0.044715 * p ** 3))
             mul = 0.5 * (1 + tt) + 0.5 * p * (1 - tt * tt) * 0.7978845608028654 * (1 + 3 * 0.044715 * p * p)

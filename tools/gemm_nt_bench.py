@@ -115,10 +115,11 @@ def main():
                 blas = lambda: ext.gelu_bwd(pre, x @ wm, dbg)  # noqa: E731
             elif kind in ("dgrad_dmul", "dgrad_dmul_nob"):  # x saved gelu'(h) (training path), +- FF1 bias grad
                 wm = w.t().contiguous()
-                pre = (torch.rand(M, N, device="cuda") * 1.1).bfloat16()
+                pre = torch.randint(1, 255, (M, N), device="cuda", dtype=torch.uint8)  # gelu' codes
+                pre_bf = ((pre.float() - 34) / 195).bfloat16()
                 dbg = torch.zeros(N, device="cuda") if kind == "dgrad_dmul" else None
                 ours = lambda: (ext.gemm_nt_dgelu(x, w, pre, dbg, True),)  # noqa: E731
-                blas = lambda: (x @ wm) * pre  # noqa: E731
+                blas = lambda: (x @ wm) * pre_bf  # noqa: E731
             elif kind == "dgrad":
                 wm = w.t().contiguous()  # W as the model stores it: [N_fwd, K_fwd] = w^T
                 ours = lambda: ext.gemm_nt(x, w, None, False)  # noqa: E731
