@@ -158,13 +158,13 @@ JM_DEVICE uint2 gd_pack8(const float* d) {
   v.y = gd_code(d[4]) | (gd_code(d[5]) << 8) | (gd_code(d[6]) << 16) | (gd_code(d[7]) << 24);
   return v;
 }
-// codes -> (q - GD_Z) * s (v_cvt_f32_ubyte0..3 + one fma per element)
+// codes -> (q - GD_Z) * s: v_cvt_f32_ubyte0..3, an exact subtraction, one multiply -- code GD_Z
+// (dropped elements, gelu' underflow) decodes to exactly 0, which an fma with -GD_Z s would not
 JM_DEVICE void gd_unpack4(uint32_t w, float s, float* d) {
-  const float z = -(float)GD_Z * s;
-  d[0] = __builtin_fmaf((float)(w & 255u), s, z);
-  d[1] = __builtin_fmaf((float)((w >> 8) & 255u), s, z);
-  d[2] = __builtin_fmaf((float)((w >> 16) & 255u), s, z);
-  d[3] = __builtin_fmaf((float)(w >> 24), s, z);
+  d[0] = ((float)(w & 255u) - (float)GD_Z) * s;
+  d[1] = ((float)((w >> 8) & 255u) - (float)GD_Z) * s;
+  d[2] = ((float)((w >> 16) & 255u) - (float)GD_Z) * s;
+  d[3] = ((float)(w >> 24) - (float)GD_Z) * s;
 }
 
 // DPP lane moves (VALU, no LDS round trip like __shfl_xor's ds_bpermute)

@@ -546,7 +546,7 @@ __global__ __launch_bounds__(512, 1) void gemm_nt64_kernel(const uint16_t* __res
 // acc = A[m0:m0+TR, k_begin:k_begin+K] . B[n0:n0+256, same]^T  (K % 128 == 0, K > 0); every LDS
 // slot is free on entry (caller's barrier) and the ring is drained on exit except for the reads
 // of the last K-tile's MFMAs (caller's epilogue barriers before reusing LDS).
-// Short-row tiles (MTL < 4: TR = 128 + 32 * MTL = 224 / 192 rows) keep the slot layout and the
+// Short-row tiles (MTL < 4: TR = 128 + 32 * MTL = 224 / 192 / 160 rows) keep the slot layout and the
 // counted-vmcnt schedule unchanged: each wave row owns 64 + 16 * MTL rows, the a1 slot's unused
 // rows are loaded from an out-of-range buffer offset (no memory traffic) and never read, and the
 // lower-half phases q3 / q4 run MTL instead of 4 row MFMA tiles.  They exist for wave fill
@@ -1176,7 +1176,9 @@ bool p4_ok(int K, int epi, int splits) {
 
 // Relative cost per tile row of the short-row 4-phase tiles vs 256 rows (the same B panel feeds
 // fewer MFMAs; measured per full wave, profiles/r3_gemm_tile_rows.txt)
-float rows_cost(int tr) { return tr == 256 ? 1.f : (tr == 224 ? 1.05f : 1.10f); }
+// (160 rows: 1.20 -- ViT-B / finetune N = 768 GEMMs 5-6 % faster than 192 rows, the decoder's N = 512
+// ones 2 % slower than 224: profiles/r5_gemm_tile160.txt)
+float rows_cost(int tr) { return tr == 256 ? 1.f : (tr == 224 ? 1.05f : (tr == 192 ? 1.10f : 1.20f)); }
 
 // Cost per output element of the 128 x 192 narrow tile relative to the 4-phase 256-row tile: its
 // smaller tile re-reads operands 1.5-1.7x as often per FLOP (MFMA busy 35 vs 43-57 %, r4_gemm_pmc)
@@ -1221,7 +1223,7 @@ int tile_rows(int M, int N, int K, int epi, long lda) {
   const int t256 = ((M + BM - 1) / BM) * nN;
   float best_c = tail_plan_256(M, N, K, epi, &r) ? (t256 / ncu + 0.8f) * BM : (float)((t256 + ncu - 1) / ncu) * BM;
   int best = BM;
-  for (int tr : {224, 192}) {
+  for (int tr : {224, 192, 160}) {
     const int t = ((M + tr - 1) / tr) * nN;
     const float c = (float)((t + ncu - 1) / ncu) * tr * rows_cost(tr);
     if (c < best_c) best_c = c, best = tr;
@@ -1243,6 +1245,7 @@ void launch_epi(const uint16_t* A, long lda, const uint16_t* B, long ldb, int M,
       const int nw = ((M + tr - 1) / tr) * ((N + BN - 1) / BN);
       if (tr == 224) return launch_p4<EPI, 3>(A, lda, B, ldb, M, N, K, ep, nw, st);
       if (tr == 192) return launch_p4<EPI, 2>(A, lda, B, ldb, M, N, K, ep, nw, st);
+      if (tr == 160) return launch_p4<EPI, 1>(A, lda, B, ldb, M, N, K, ep, nw, st);
     }
     return launch_p4<EPI, 4>(A, lda, B, ldb, M, N, K, ep, nwg, st);
   }
@@ -1269,7 +1272,7 @@ void launch_tail(const uint16_t* A, long lda, const uint16_t* B, long ldb, int M
 // every M without tail split (rows 256 / 224 / 192 forced, 0 = tile_rows)
 void jm_gemm_test_force(int path, int rows) {
   g_test_path = (path == 1 || path == 2) ? path : 0;
-  g_test_rows = (g_test_path == 2 && (rows == 224 || rows == 192 || rows == 256)) ? rows : 0;
+  g_test_rows = (g_test_path == 2 && (rows == 224 || rows == 192 || rows == 160 || rows == 256)) ? rows : 0;
 }
 
 // output tiles of an NT launch (the narrow kernel's 128 x 192 or the 4-phase 256 / 224 / 192 x 256)

@@ -107,7 +107,7 @@ def test_pretrain_driver_on_gpu(pretrained):
     rows = _rows(out, "p")
     vals = [r["val/loss"] for r in rows if "val/loss" in r]
     assert len(vals) == 3, rows  # sanity check at step 0, evals at 6 and 12
-    assert vals[-1] < 0.9 * vals[0], vals
+    assert vals[0] > vals[1] > vals[2] and vals[2] < 0.95 * vals[0], vals
     train = [r["train/loss"] for r in rows if "train/loss" in r]
     assert len(train) == 6 and all(np.isfinite(train)) and train[-1] < train[0], train
     assert any("perf/images_per_sec" in r for r in rows)

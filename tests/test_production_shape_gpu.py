@@ -56,6 +56,11 @@ def test_vitl_2048_microbatch_equals_4x512_accumulation():
         a = g_big[seg.offset:seg.offset + seg.numel].double()
         b = g_acc[seg.offset:seg.offset + seg.numel].double()
         assert torch.isfinite(a).all() and torch.isfinite(b).all(), seg.key
+        if seg.key.endswith("attn/wk/bias"):
+            # analytically zero (adding b_k shifts every score of a query row by q . b_k; softmax is
+            # shift invariant): only rounding noise of ~1e-9 remains on both paths
+            assert a.abs().max() < 1e-6 and b.abs().max() < 1e-6, seg.key
+            continue
         na, nb = a.norm().item(), b.norm().item()
         if na == 0 and nb == 0:
             continue
