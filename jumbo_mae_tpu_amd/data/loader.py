@@ -244,6 +244,10 @@ class ShardDataset(IterableDataset):
     def __iter__(self):
         info = get_worker_info()
         wid, nw = (info.id, info.num_workers) if info is not None else (0, 1)
+        if self.train:
+            # a resumed loader's batch j is batch start + j of the interrupted stream, which worker
+            # (start + j) % nw produced: worker w takes over the role of worker (w + start) % nw
+            wid = (wid + self.skip_batches) % nw
         random.seed(self.seed * 1000 + self.rank * 97 + wid)
         np.random.seed((self.seed * 1000 + self.rank * 97 + wid) % (2 ** 32))
         if not self.train:

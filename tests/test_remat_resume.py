@@ -221,11 +221,12 @@ def test_loader_resume_continues_stream(workers):
     full, _ = create_dataloaders(args)
     it = iter(full)
     ref = [next(it) for _ in range(7)]
-    resumed, _ = create_dataloaders(args, start_batches=4)
-    it2 = iter(resumed)
-    for k in range(4, 7):
-        b = next(it2)
-        assert torch.equal(b[0], ref[k][0]) and torch.equal(b[1], ref[k][1]), k
+    for start in (4, 3, 5):  # odd starts: the resumed loader's worker 0 continues the stream of worker 1
+        resumed, _ = create_dataloaders(args, start_batches=start)
+        it2 = iter(resumed)
+        for k in range(start, 7):
+            b = next(it2)
+            assert torch.equal(b[0], ref[k][0]) and torch.equal(b[1], ref[k][1]), (start, k)
 
 
 @pytest.mark.parametrize("stop", [4, 3])
