@@ -783,6 +783,8 @@ __global__ __launch_bounds__(64 * NWV, 2) void attn_bwd3_kernel(const uint16_t* 
   constexpr int NT = SP / 16, KK = HD / 32, DT = HD / 16;
   constexpr int NKW = (NT + NW - 1) / NW;
   constexpr int NCH = HD / 8;
+  // smallest S dispatched to this SP (dispatch_sp buckets 32 / 64 / 128 / 224)
+  constexpr int SMIN = SP <= 32 ? 1 : (SP <= 64 ? 33 : (SP <= 128 ? 65 : 129));
   extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
   uint16_t* Qs = smem;
   uint16_t* dOs = Qs + SP * HD;
@@ -842,6 +844,10 @@ __global__ __launch_bounds__(64 * NWV, 2) void attn_bwd3_kernel(const uint16_t* 
     }
   }
   for (int i = threadIdx.x; i < NW * 3 * HD; i += NTH) bsum[i] = 0.f;  // one slot per wave
+  // dS^T rows of the key tiles past S: never written (those tiles are skipped), read by the dQ
+  // product against zero K rows -- zero, not whatever the LDS held
+  for (int i = ((S + 15) / 16) * 16 * QC + 8 * (int)threadIdx.x; i < SP * QC; i += 8 * NTH)
+    *reinterpret_cast<uint4*>(dSt + i) = make_uint4(0, 0, 0, 0);
   const float sl2 = scale * LOG2E;
   const uint64_t dseed = DROP ? (uint64_t)drop.seed[0] : 0;
   if ((int)threadIdx.x < SP) lse_s[threadIdx.x] = nlse;
@@ -1007,9 +1013,14 @@ __global__ __launch_bounds__(64 * NWV, 2) void attn_bwd3_kernel(const uint16_t* 
 #pragma unroll
         for (int w = 0; w < NKW; ++w) {
           const int kt = wave + NW * w;
-          if (kt * 16 + 16 <= S) {
+          if (NWV == 4 && NW * 16 * (w + 1) <= SMIN) {  // compile-time after the unroll (8 waves: spills)
+            // full for every S of this instantiation: no branch around it, so the scheduler
+            // interleaves these tiles' MFMA -> exp -> MFMA chains
             tile(w, kt, lv, 0.f);
-          } else if (kt < NT) {  // the tile holding padded keys (wave-uniform branch)
+          } else if (kt * 16 + 16 <= S) {
+            tile(w, kt, lv, 0.f);
+          } else if (kt * 16 < S) {  // the tile holding padded keys (wave-uniform branch); tiles
+                                     // past S are skipped (their dS^T rows stay zero)
             asm volatile("" ::: "memory");  // keeps the two paths apart: no per-tile selects
             if constexpr (TILE_AOP) {
               tile(w, kt, lv, kneg[w]);

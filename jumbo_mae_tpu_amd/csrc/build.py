@@ -106,7 +106,7 @@ def build_io(verbose: bool = True) -> Path:
 # 160 VGPR + 56 AGPR -> 109 VGPR, one occupancy step up; backward 296 -> 217).
 # -fno-honor-nans: fmaxf without the NaN-quieting v_max_f32 x, x on each MFMA result (the softmax
 # max is then one v_max3 per two scores).
-FILE_FLAGS = {"attention.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form", "-fno-honor-nans"]}
+FILE_FLAGS = {"attention.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form", "-fno-honor-nans", "-fno-slp-vectorize"]}
 
 
 def build(jobs: int = 8, verbose: bool = True, clean: bool = False, variant: str = "release") -> Path:
