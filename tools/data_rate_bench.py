@@ -7,11 +7,12 @@ training rate.  Shards are written with real JPEG files at ImageNet-like sizes
 (data/jpeg_shards.py) on first use.
 
     python tools/data_rate_bench.py [--workers 1,2,4,8] [--mode pretrain|finetune] [--batch 256]
-                                    [--batches 12] [--h2d]
+                                    [--h2d] [--device-augment]
 
-Prints one JSON line per worker count: images/s of the loader, per worker, and with ``--h2d`` the
-rate through the DevicePrefetcher (pinned batches copied to the GPU on a side stream) plus the
-host->device copy bandwidth."""
+Prints one JSON line per worker count: steady-state images/s of the loader (after draining what
+the workers prefetched), per worker, and with ``--h2d`` the rate through the DevicePrefetcher
+(pinned batches copied to the GPU on a side stream; with ``--device-augment`` also resized there)
+plus the host->device copy bandwidth."""
 
 from __future__ import annotations
 
@@ -48,7 +49,6 @@ def main():
     ap.add_argument("--workers", default="1,2,4,8")
     ap.add_argument("--mode", default="pretrain", choices=["pretrain", "finetune"])
     ap.add_argument("--batch", type=int, default=256)
-    ap.add_argument("--batches", type=int, default=12)
     ap.add_argument("--h2d", action="store_true", help="also through the DevicePrefetcher onto cuda:0")
     ap.add_argument("--device-augment", action="store_true",
                     help="workers decode + ship crop windows; resize / flip on the GPU (csrc/augment.hip)")
@@ -60,32 +60,37 @@ def main():
         print(f"[data] wrote {a.shards} x {a.per_shard} JPEGs in {time.time() - t0:.1f}s", file=sys.stderr)
     sizes = [os.path.getsize(os.path.join(a.dir, f"train-{i:06d}.tar")) for i in range(a.shards)]
     mean_kb = sum(sizes) / (a.shards * a.per_shard) / 1024
+    def steady(it, nw, batch):
+        """Steady-state images/s: first drain what the workers prefetched before the clock starts
+        (up to nw x prefetch_factor batches), then time 6x that many batches (a backlog refilled
+        while draining is then at most a sixth of the timed batches)."""
+        for _ in range(nw * 4 + 2):
+            last = next(it)
+        k = 6 * 4 * max(nw, 1)
+        if torch.cuda.is_available():
+            torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(k):
+            last = next(it)
+        if torch.cuda.is_available():
+            torch.cuda.synchronize()
+        return k * batch / (time.perf_counter() - t0), last
+
     for nw in [int(x) for x in a.workers.split(",")]:
         dl, _ = create_dataloaders(loader_args(spec, a.mode, a.batch, nw), device_augment=a.device_augment)
-        it = iter(dl)
-        for _ in range(2):  # worker start-up, first shards opened
-            next(it)
-        t0 = time.perf_counter()
-        for _ in range(a.batches):
-            b = next(it)
-        dt = time.perf_counter() - t0
-        rate = a.batches * a.batch / dt
+        rate, b = steady(iter(dl), nw, a.batch)
         out = {"mode": a.mode, "device_augment": a.device_augment, "workers": nw, "images_per_sec": round(rate, 1),
                "per_worker": round(rate / max(nw, 1), 1), "batch": a.batch, "jpeg_kb": round(mean_kb, 1),
                "cpus": os.cpu_count()}
         if a.device_augment:
             out["window_kb_per_image"] = round(b.src.numel() / a.batch / 1024, 1)
+        del dl
         if a.h2d and torch.cuda.is_available():
             from jumbo_mae_tpu_amd.train.common import DevicePrefetcher
             dev = torch.device("cuda:0")
-            pf = DevicePrefetcher(it, dev)
-            next(pf)
-            torch.cuda.synchronize()
-            t0 = time.perf_counter()
-            for _ in range(a.batches):
-                x = next(pf)
-            torch.cuda.synchronize()
-            out["prefetcher_images_per_sec"] = round(a.batches * a.batch / (time.perf_counter() - t0), 1)
+            dl, _ = create_dataloaders(loader_args(spec, a.mode, a.batch, nw), device_augment=a.device_augment)
+            rate, x = steady(DevicePrefetcher(dl, dev), nw, a.batch)
+            out["prefetcher_images_per_sec"] = round(rate, 1)
             out["device_shape"] = list((x[0] if isinstance(x, (list, tuple)) else x).shape)
             host = (x[0] if isinstance(x, (list, tuple)) else x).cpu().pin_memory()
             buf = torch.empty_like(host, device=dev)
@@ -95,8 +100,8 @@ def main():
                 buf.copy_(host, non_blocking=True)
             torch.cuda.synchronize()
             out["h2d_gb_per_sec"] = round(20 * host.numel() / (time.perf_counter() - t0) / 1e9, 2)
+            del dl
         print(json.dumps(out), flush=True)
-        del it, dl
 
 
 if __name__ == "__main__":
