@@ -10,7 +10,7 @@ O=$R/gpurun_out/$TAG
 mkdir -p $O
 cd $R
 echo "[gpucheck] tests"
-timeout -k 10 420 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/pytest_gpu.log 2>&1 \
+timeout -k 10 800 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/pytest_gpu.log 2>&1 \
   || { tail -30 $O/pytest_gpu.log; exit 1; }
 tail -3 $O/pytest_gpu.log
 echo "[gpucheck] smoke"
