@@ -113,11 +113,14 @@ def _attn_ref(qkv, H):
 
 # every kernel the shape dispatch reaches: forward multi-pair (S <= 64) / one-pair, padded and
 # exactly-filled key tiles; backward bwd3 4-wave (hd 32), bwd3 8-wave (hd 64, S > 64) and bwd2
-# with partial and full 8-element batch groups (hd 64, S <= 64)
+# with partial and full 8-element batch groups (hd 64, S <= 64); the 4-wave bwd3's shared last
+# key tile (one active tile in the last slot: S 193-208 at SP 224 -- the decoder's 197 -- and 65-80
+# at SP 128) with padded and exactly-filled keys, and the plain slot beside it (S 209)
 @pytest.mark.parametrize("B,S,H,hd", [(3, 52, 16, 64), (9, 52, 4, 64), (16, 64, 2, 64), (2, 199, 16, 32),
                                       (2, 17, 4, 32), (5, 64, 3, 32), (2, 100, 3, 64), (2, 199, 4, 64),
                                       (3, 224, 2, 64), (2, 128, 2, 32), (1, 33, 5, 64), (32, 19, 4, 64),
-                                      (11, 30, 2, 64)])
+                                      (11, 30, 2, 64), (2, 197, 16, 32), (2, 208, 2, 32), (2, 209, 2, 32),
+                                      (3, 72, 2, 32)])
 def test_attention(ext, B, S, H, hd):
     torch.manual_seed(0)
     D = H * hd
@@ -146,7 +149,7 @@ def test_attention(ext, B, S, H, hd):
 
 
 @pytest.mark.parametrize("B,S,H,hd", [(3, 52, 4, 64), (2, 199, 4, 32), (2, 199, 3, 64), (5, 17, 2, 32),
-                                      (9, 30, 2, 64), (2, 100, 2, 32)])
+                                      (9, 30, 2, 64), (2, 100, 2, 32), (3, 72, 2, 32)])
 def test_attention_dropout(ext, B, S, H, hd):
     """Dropout on the attention probabilities inside the fused kernels (forward: masked P.V with
     the undropped row statistics; backward: the mask regenerated from the seed) against an fp64
