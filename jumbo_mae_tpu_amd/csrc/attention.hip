@@ -813,17 +813,9 @@ __global__ __launch_bounds__(64 * NWV, 2) void attn_bwd3_kernel(const uint16_t* 
   uint16_t* dKg = dqkv + (long)b * S * ts + (H + h) * HD;
   uint16_t* dVg = dqkv + (long)b * S * ts + (2 * H + h) * HD;
 
-  // 4 waves: the wave index in an SGPR, so branches on it (key-tile ownership) are scalar branches
-  // instead of EXEC-mask regions (the 8-wave form keeps the VGPR index: the SGPR form spills there)
-  const int wave = NWV == 4 ? __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) : (int)(threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int l16 = lane & 15, g = lane >> 4;
 
-  // every global load in one burst, none behind a branch (V fragments, the staging rows, lse):
-  // rows at and past S read as zeros through the range-checked resources
-  const __amdgpu_buffer_rsrc_t rq = rsrc(Qg, (long)S * ts * 2), rk = rsrc(Kg, (long)S * ts * 2),
-                               rv = rsrc(Vg, (long)S * ts * 2), rdo = rsrc(dOg, (long)S * os * 2),
-                               ro = rsrc(Og, (long)S * os * 2), rl = rsrc(lse + ((long)b * H + h) * S, (long)S * 4);
   bf16x8_t vf[NKW][KK];
   float kneg[NKW];  // -1e30 on padded keys
 #pragma unroll
@@ -831,23 +823,31 @@ __global__ __launch_bounds__(64 * NWV, 2) void attn_bwd3_kernel(const uint16_t* 
     const int key = (wave + NW * w) * 16 + l16;
     kneg[w] = key < S ? 0.f : -1e30f;
 #pragma unroll
-    for (int kk = 0; kk < KK; ++kk) vf[w][kk] = __builtin_bit_cast(bf16x8_t, bld16(rv, (key * (int)ts + 32 * kk + 8 * g) * 2));
+    for (int kk = 0; kk < KK; ++kk) {
+      s16x8_t z = {0, 0, 0, 0, 0, 0, 0, 0};
+      vf[w][kk] = __builtin_bit_cast(bf16x8_t, z);
+      if (key < S) vf[w][kk] = ld8(Vg + (long)key * ts + 32 * kk + 8 * g);
+    }
   }
+  // every global load in one burst (V fragments above, lse, the staging rows): one exposed round
+  // trip instead of two
   static_assert(SP <= NTH, "one lse per thread");
+  // -lse in the log2 domain (the S accumulator init); padded queries -inf (P = 0)
+  const float nlse = (int)threadIdx.x < S ? -lse[((long)b * H + h) * S + threadIdx.x] * LOG2E : -INFINITY;
   constexpr int NIT = (SP * NCH + NTH - 1) / NTH;
   uint4 qv[NIT], kv[NIT], dv[NIT], ov[NIT];
 #pragma unroll
   for (int it = 0; it < NIT; ++it) {
     const int i = it * NTH + threadIdx.x;
-    const int r = i / NCH, c = (i % NCH) * 8;  // r >= SP >= S past the image: zeros
-    qv[it] = bld16(rq, (r * (int)ts + c) * 2);
-    kv[it] = bld16(rk, (r * (int)ts + c) * 2);
-    dv[it] = bld16(rdo, (r * (int)os + c) * 2);
-    ov[it] = bld16(ro, (r * (int)os + c) * 2);
+    const int r = i / NCH, c = (i % NCH) * 8;
+    qv[it] = kv[it] = dv[it] = ov[it] = make_uint4(0, 0, 0, 0);
+    if (i < SP * NCH && r < S) {
+      qv[it] = *reinterpret_cast<const uint4*>(Qg + r * ts + c);
+      kv[it] = *reinterpret_cast<const uint4*>(Kg + r * ts + c);
+      dv[it] = *reinterpret_cast<const uint4*>(dOg + r * os + c);
+      ov[it] = *reinterpret_cast<const uint4*>(Og + r * os + c);
+    }
   }
-  // -lse in the log2 domain (the S accumulator init); padded queries -inf (P = 0)
-  const float lraw = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rl, (int)threadIdx.x * 4, 0, 0));
-  const float nlse = (int)threadIdx.x < S ? -lraw * LOG2E : -INFINITY;
   for (int i = threadIdx.x; i < NW * 3 * HD; i += NTH) bsum[i] = 0.f;  // one slot per wave
   // dS^T rows of the key tiles past S: never written (those tiles are skipped), read by the dQ
   // product against zero K rows -- zero, not whatever the LDS held
@@ -1040,7 +1040,7 @@ __global__ __launch_bounds__(64 * NWV, 2) void attn_bwd3_kernel(const uint16_t* 
     __syncthreads();
     {
       const int qt = qc * (QC / 16) + wave;
-      if (qt < NT && qt * 16 < S) {  // query tiles of padding only: nothing to store
+      if (qt < NT) {
         f32x4_t dq[DT];
 #pragma unroll
         for (int dt = 0; dt < DT; ++dt) dq[dt] = f32x4_t{0.f, 0.f, 0.f, 0.f};

@@ -15,7 +15,7 @@ sys.path.insert(0, os.environ.get("JMAE_ROOT") or os.path.dirname(os.path.dirnam
 
 from jumbo_mae_tpu_amd.ops import _ext  # noqa: E402
 
-SHAPES = {"dec": (512, 199, 16, 32), "enc": (512, 52, 16, 64), "enc2k": (2048, 52, 16, 64), "ft": (128, 199, 16, 64), "ft12": (128, 199, 12, 64)}
+SHAPES = {"dec": (512, 199, 16, 32), "dec2k": (2048, 199, 16, 32), "enc": (512, 52, 16, 64), "enc2k": (2048, 52, 16, 64), "ft": (128, 199, 16, 64), "ft12": (128, 199, 12, 64)}
 
 
 def main():
