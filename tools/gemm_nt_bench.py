@@ -14,6 +14,7 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from jumbo_mae_tpu_amd.ops import _ext  # noqa: E402
+from jumbo_mae_tpu_amd.ops import prims as P  # noqa: E402
 
 FWD = {
     "enc_qkv": (26624, 3072, 1024), "enc_wo": (26624, 1024, 1024), "enc_ff1": (25088, 4096, 1024),
@@ -57,8 +58,8 @@ def reference(kind, x, w, b, pre):
         t = torch.tanh(0.7978845608028654 * (h + 0.044715 * h ** 3))
         d = 0.5 * (1 + t) + 0.5 * h * (1 - t * t) * 0.7978845608028654 * (1 + 3 * 0.044715 * h * h)
         return base.bfloat16().float() * d
-    if kind in ("dgrad_dmul", "dgrad_dmul_nob"):
-        return base.bfloat16().float() * pre.float()
+    if kind in ("dgrad_dmul", "dgrad_dmul_nob"):  # pre: the 8-bit gelu' codes (ops/prims.py gd_decode)
+        return base.bfloat16().float() * ((pre.float() - P.GD_Z) / P.GD_Q)
     r = base + b
     if kind in ("fwd_gelu_only", "fwd_gelu_d"):
         return torch.nn.functional.gelu(r.bfloat16().float(), approximate="tanh")
@@ -116,7 +117,7 @@ def main():
             elif kind in ("dgrad_dmul", "dgrad_dmul_nob"):  # x saved gelu'(h) (training path), +- FF1 bias grad
                 wm = w.t().contiguous()
                 pre = torch.randint(1, 255, (M, N), device="cuda", dtype=torch.uint8)  # gelu' codes
-                pre_bf = ((pre.float() - 34) / 195).bfloat16()
+                pre_bf = ((pre.float() - P.GD_Z) / P.GD_Q).bfloat16()
                 dbg = torch.zeros(N, device="cuda") if kind == "dgrad_dmul" else None
                 ours = lambda: (ext.gemm_nt_dgelu(x, w, pre, dbg, True),)  # noqa: E731
                 blas = lambda: (x @ wm) * pre_bf  # noqa: E731
