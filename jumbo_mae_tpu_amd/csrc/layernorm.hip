@@ -207,22 +207,42 @@ struct ParamOuts {
 // SC: the residual branch has a LayerScale (rio.scale); without one (every ViT-L / ViT-B preset)
 // the scale registers, the branch-output loads and the dscale partials are compiled out (ViT-L
 // encoder variant 200 -> 152 VGPRs: 3 waves per SIMD instead of 2).
-template <int V, typename TI, bool RES, bool ER = false, bool SC = true>
+// R rows per wave (1 or 2): at R = 2 each half-wave owns a row (the decoder's 512-wide rows: 16
+// elements per lane instead of 8, two rows' loads in flight per wave, half-wave sums), and the
+// halves' parameter partials are added across lanes before the block merge.
+template <int V, typename TI, bool RES, bool ER = false, bool SC = true, int R = 1>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(const TI* __restrict__ dy, const float* __restrict__ x,
                                                      long sB, long sT, int T, int rows, int D,
                                                      const float* __restrict__ mean, const float* __restrict__ rstd,
                                                      const float* __restrict__ gamma, LnBwdIO io, LnResIO rio,
                                                      float* __restrict__ ws, int accum_params, ParamOuts outs) {
   JM_DGUARD(blockDim.x == 256 && D % 4 == 0 && D <= V * 256);
+  static_assert(R == 1 || R == 2, "rows per wave");
   constexpr int NP = RES ? 4 : 2;
+  constexpr int LPR = 64 / R, VL = V * R;  // lanes per row, float4 chunks per lane
   extern __shared__ __attribute__((aligned(16))) float red[];  // [NP*D]
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int sub = lane / LPR, l = lane % LPR;
   const bool partials = accum_params || RES;
-  auto acc_add = [&](float (&acc)[NP][V][4], int k, int i, int j, float v) { acc[k][i][j] += v; };
-  float acc[NP][V][4], gg[V][4], sc[V][4];
+  auto acc_add = [&](float (&acc)[NP][VL][4], int k, int i, int j, float v) { acc[k][i][j] += v; };
+  // the row sum of this lane's row: the whole wave (R = 1) or its half (R = 2)
+  auto row_sum = [&](float v) {
+    if constexpr (R == 1) {
+      return wave_sum(v);
+    } else {
+      v = row16_sum(v);
+      const int iv = __builtin_bit_cast(int, v);
+      const float lo = __builtin_bit_cast(float, __builtin_amdgcn_readlane(iv, 0)) +
+                       __builtin_bit_cast(float, __builtin_amdgcn_readlane(iv, 16));
+      const float hi = __builtin_bit_cast(float, __builtin_amdgcn_readlane(iv, 32)) +
+                       __builtin_bit_cast(float, __builtin_amdgcn_readlane(iv, 48));
+      return sub ? hi : lo;
+    }
+  };
+  float acc[NP][VL][4], gg[VL][4], sc[VL][4];
 #pragma unroll
-  for (int i = 0; i < V; ++i) {
-    const int col = (i * 64 + lane) * 4;
+  for (int i = 0; i < VL; ++i) {
+    const int col = (i * LPR + l) * 4;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
 #pragma unroll
@@ -236,21 +256,23 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const TI* __restrict__ dy, 
       }
     }
   }
-  for (int row = blockIdx.x * 4 + wave; row < rows; row += gridDim.x * 4) {
+  for (int rw = blockIdx.x * 4 + wave; rw * R < rows; rw += gridDim.x * 4) {
+    const int row = rw * R + sub;
+    const bool valid = R == 1 || row < rows;  // R = 2: the second half of an odd tail has no row
     const int b = row / T, t = row - b * T;
     const float* xr = x + b * sB + t * sT;
     const TI* dyr = dy + (long)row * D;
-    const float mu = mean[row], rs = rstd[row];
+    const float mu = valid ? mean[row] : 0.f, rs = valid ? rstd[row] : 0.f;
     const bool rrow = RES && t >= rio.T0;
     const long yoff = RES ? b * rio.yB + (long)(t - rio.T0) * rio.yT : 0;
-    float xh[V][4], g[V][4], yv[V][4];
-    float rvp[ER ? V : 1][4];
+    float xh[VL][4], g[VL][4], yv[VL][4];
+    float rvp[ER ? VL : 1][4];
     const float* rr = io.dres ? io.dres + b * io.rB + t * io.rT : nullptr;
     float sg = 0.f, sgx = 0.f;
 #pragma unroll
-    for (int i = 0; i < V; ++i) {
-      const int col = (i * 64 + lane) * 4;
-      if (col < D) {
+    for (int i = 0; i < VL; ++i) {
+      const int col = (i * LPR + l) * 4;
+      if (valid && col < D) {
         float xv[4], dv[4];
         load4(xr + col, xv);
         load4(dyr + col, dv);
@@ -275,14 +297,14 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const TI* __restrict__ dy, 
         for (int j = 0; j < 4; ++j) xh[i][j] = g[i][j] = 0.f;
       }
     }
-    sg = wave_sum(sg) / D;
-    sgx = wave_sum(sgx) / D;
+    sg = row_sum(sg) / D;
+    sgx = row_sum(sgx) / D;
     float* dxr = io.dx + b * io.oB + t * io.oT;
-    const float m = (RES && rio.mask) ? rio.mask[b] : 1.f;
+    const float m = (RES && rio.mask) ? rio.mask[valid ? b : 0] : 1.f;
 #pragma unroll
-    for (int i = 0; i < V; ++i) {
-      const int col = (i * 64 + lane) * 4;
-      if (col < D) {
+    for (int i = 0; i < VL; ++i) {
+      const int col = (i * LPR + l) * 4;
+      if (valid && col < D) {
         float o[4], rv[4] = {0.f, 0.f, 0.f, 0.f};
         if constexpr (ER) {
 #pragma unroll
@@ -311,13 +333,21 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const TI* __restrict__ dy, 
     }
   }
   if (!partials) return;
+  if constexpr (R == 2) {  // both halves hold the same columns: add them (lane l gets lane l + 32's)
+#pragma unroll
+    for (int k = 0; k < NP; ++k)
+#pragma unroll
+      for (int i = 0; i < VL; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[k][i][j] += __shfl_xor(acc[k][i][j], 32, WAVE);
+  }
   // merge the 4 waves' partials through LDS in turn (float4, conflict-free, no atomics), then
   // one coalesced store of the block partial row into the workspace
   for (int w = 0; w < 4; ++w) {
-    if (wave == w) {
+    if (wave == w && sub == 0) {
 #pragma unroll
-      for (int i = 0; i < V; ++i) {
-        const int col = (i * 64 + lane) * 4;
+      for (int i = 0; i < VL; ++i) {
+        const int col = (i * LPR + l) * 4;
         if (col < D) {
 #pragma unroll
           for (int k = 0; k < NP; ++k) {
@@ -583,14 +613,16 @@ bool use_wide(int rows, int D) { return D > 1024 && rows <= LN_WIDE_MAX_ROWS && 
 // 97.96 -> 97.75 ms/step, profiles/r1_ab_ln_bwd_early_dres.txt).  Measured and removed: LDS-
 // accumulated parameter partials (r1_ab_ln_bwd_lds_acc.txt), a next-row prefetch variant
 // (r2_ln_bwd_prefetch.txt).
+// rows per wave of the row-loop backward: two half-wave rows at V = 2 (D <= 512, the decoder)
+#define LN_BWD_R(VV) ((VV) == 2 ? 2 : 1)
 template <typename TI, bool RES, bool SC = true>
 void launch_bwd(int V, dim3 grid, size_t smem, hipStream_t st, const TI* dy, const float* x, long sB, long sT,
                 int T, int rows, int D, const float* m, const float* r, const float* g, LnBwdIO dx, LnResIO rio,
                 float* ws, int acc, ParamOuts outs) {
 #define JM_LNB(VV)                                                                                          \
   case VV:                                                                                                  \
-    ln_bwd_kernel<VV, TI, RES, (VV >= 2 && VV <= 4), SC><<<grid, 256, smem, st>>>(dy, x, sB, sT, T, rows, D, m, \
-                                                                                  r, g, dx, rio, ws, acc, outs); \
+    ln_bwd_kernel<VV, TI, RES, (VV >= 2 && VV <= 4), SC, LN_BWD_R(VV)><<<grid, 256, smem, st>>>(             \
+        dy, x, sB, sT, T, rows, D, m, r, g, dx, rio, ws, acc, outs);                                         \
     break;
   switch (V) {
     JM_LNB(1) JM_LNB(2) JM_LNB(3) JM_LNB(4) JM_LNB(6) JM_LNB(8) JM_LNB(9) JM_LNB(12) JM_LNB(16)
@@ -661,11 +693,11 @@ int jm_residual_ln_fwd(const float* x, long sB, long sT, const uint16_t* y, cons
 }
 
 // most row-loop blocks of the (non-wide) LN backward: one resident round of the fused-residual
-// kernel without LayerScale -- 3 blocks per CU at V = 4 (147 VGPRs, D = 1024), 4 at V <= 2 (87,
-// D = 512; 5 there measured 17.7 -> 18.5 ms/step, gpurun r4y2), 2 beyond.  A second round only
-// adds partial rows (r2: 1024 blocks at 2 per CU lost 0.3 ms/step to 512, r2_ln_bwd_blocks.txt).
+// kernel without LayerScale -- 3 blocks per CU at V = 4 (147 VGPRs, D = 1024) and at V = 2 with
+// two rows per wave (148, D = 512), 4 at V = 1, 2 beyond.  A second round only adds partial rows
+// (r2: 1024 blocks at 2 per CU lost 0.3 ms/step to 512, r2_ln_bwd_blocks.txt).
 constexpr int LN_BWD_CUS = 256;
-int ln_bwd_blocks_per_cu(int V) { return V <= 2 ? 4 : V <= 4 ? 3 : 2; }
+int ln_bwd_blocks_per_cu(int V) { return V <= 1 ? 4 : V <= 4 ? 3 : 2; }
 
 int jm_layernorm_bwd_blocks(int rows, int D) {
   // wide rows: one workgroup per row (at most 1024 workgroups, grid-stride beyond)
@@ -673,7 +705,8 @@ int jm_layernorm_bwd_blocks(int rows, int D) {
   // grid-stride over rows, 4 waves per block; each block writes one [NP*D] partial (no atomics in
   // the hot kernel)
   const int V = pick_v(D), cap = LN_BWD_CUS * ln_bwd_blocks_per_cu(V < 0 ? 16 : V);
-  int nb = (rows + 3) / 4;
+  const int rpb = 4 * LN_BWD_R(V);  // rows per block and loop step
+  int nb = (rows + rpb - 1) / rpb;
   return nb > cap ? cap : nb;
 }
 

@@ -25,12 +25,12 @@ def rel(a, b):
     return ((a.float() - b.float()).norm() / (b.float().norm() + 1e-12)).item()
 
 
-@pytest.mark.parametrize("D", [32, 512, 768, 1024, 2304, 3072])
+@pytest.mark.parametrize("D", [32, 384, 512, 768, 1024, 2304, 3072])
 @pytest.mark.parametrize("out_dtype", [torch.bfloat16, torch.float32])
 def test_layernorm(ext, D, out_dtype):
     torch.manual_seed(0)
-    full = torch.randn(6, 9, D, device="cuda") * 3 + 1
-    x = full[:, 2:]  # strided [6,7,D] view
+    full = torch.randn(5, 9, D, device="cuda") * 3 + 1
+    x = full[:, 2:]  # strided [5,7,D] view: 35 rows (D <= 512 runs two rows per wave: an odd tail)
     g = torch.randn(D, device="cuda")
     b = torch.randn(D, device="cuda")
     y, mean, rstd = ext.layernorm_fwd(x, g, b, 1e-6, out_dtype)
@@ -528,11 +528,12 @@ def test_gemm_nt_splitk(ext, M, N, K, S, path):
 
 @pytest.mark.parametrize("T0,view_y,with_scale", [(0, False, True), (3, False, True), (0, True, True),
                                                   (3, True, False)])
-def test_layernorm_bwd_fused_residual(ext, T0, view_y, with_scale):
+@pytest.mark.parametrize("B,T,D", [(6, 52, 1024), (5, 51, 512)])
+def test_layernorm_bwd_fused_residual(ext, T0, view_y, with_scale, B, T, D):
     """LN backward with the consumer's residual backward fused in == layernorm_bwd followed by
-    residual_bwd on the rows t >= T0 (y as a contiguous slab or a strided view into a buffer)."""
+    residual_bwd on the rows t >= T0 (y as a contiguous slab or a strided view into a buffer);
+    D = 512 with an odd row count: the two-rows-per-wave decoder variant and its tail."""
     torch.manual_seed(0)
-    B, T, D = 6, 52, 1024
     x = torch.randn(B, T, D, device="cuda") * 2
     g, bt = torch.rand(D, device="cuda") + 0.5, torch.randn(D, device="cuda")
     _, mean, rstd = ext.layernorm_fwd(x, g, bt, 1e-6, torch.bfloat16)
