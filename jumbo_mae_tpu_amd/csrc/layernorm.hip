@@ -7,9 +7,10 @@
 // row in registers (D <= 256*V), so x is read exactly once.  Output rows are contiguous [B*T, D]
 // in bf16 (GEMM operand) or fp32.
 //
-// Backward: one wave per row for dx, while dgamma/dbeta are reduced per wave in registers over a
-// grid-stride row loop, then across the block's waves with LDS float atomics, then ONE global
-// atomicAdd per column per block straight into the flat fp32 gradient buffer.
+// Backward: one wave per row for dx (two half-wave rows at D <= 512), while dgamma/dbeta (and the
+// fused residual's dscale/dbias) are reduced per wave in registers over a grid-stride row loop,
+// then across the block's waves through LDS in a fixed order into one partial row per block, and
+// the partial rows are summed by ln_param_reduce_kernel (no float atomics: bit-reproducible).
 #include "common.h"
 #include "jm_api.h"
 
