@@ -19,7 +19,6 @@ import torch
 
 from ..config import DecoderConfig, ViTConfig
 from ..data.constants import IMAGENET_DEFAULT_MEAN, IMAGENET_DEFAULT_STD
-from ..ops import functional as Fn
 from ..ops import mae as mae_ops
 from ..utils.mae import masking_ids
 from .params import ParamStore, trunc_normal_

@@ -24,7 +24,7 @@ from __future__ import annotations
 import contextlib
 
 import math
-from dataclasses import dataclass, field
+from dataclasses import dataclass
 from typing import Callable, Iterable
 
 import numpy as np

@@ -30,7 +30,7 @@ from ..ops import dropout as Dr
 from ..ops import functional as Fn
 from ..ops import mae as mae_ops
 from ..utils.posemb import fixed_sincos2d_embeddings
-from .params import Handle, ParamStore, const_, ones_, trunc_normal_, trunc_normal_t, zeros_
+from .params import ParamStore, const_, ones_, trunc_normal_, trunc_normal_t, zeros_
 
 
 def use_fused_blocks() -> bool:

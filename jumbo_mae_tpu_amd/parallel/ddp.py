@@ -60,7 +60,6 @@ import torch
 import torch.distributed as dist
 
 from ..models.params import ALIGN, Handle, ParamStore
-from . import dist as pdist
 
 
 _LAYER = re.compile(r"(dec_)?layer_\d+")

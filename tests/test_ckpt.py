@@ -1,6 +1,5 @@
 """Flax msgpack wire format, converters, pretrained loading, resume sidecar."""
 
-import io
 import os
 
 import msgpack

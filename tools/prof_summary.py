@@ -1,4 +1,4 @@
-import csv, sys, re
+import csv, sys
 path = sys.argv[1]; steps = int(sys.argv[2]) if len(sys.argv) > 2 else 6
 rows = list(csv.DictReader(open(path)))
 tot = sum(float(r["TotalDurationNs"]) for r in rows)
