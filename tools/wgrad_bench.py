@@ -15,6 +15,10 @@ SHAPES = {
     "enc_ff2": (25088, 1024, 4096), "jumbo1": (512, 12288, 3072), "jumbo2": (512, 3072, 12288),
     "dec_qkv": (101888, 1536, 512), "dec_wo": (101888, 512, 512), "dec_ff1": (101888, 2048, 512),
     "dec_ff2": (101888, 512, 2048), "patch": (25088, 1024, 768), "pred": (100352, 768, 512),
+    # the headline's 2048-image micro-batch
+    "enc_qkv_2k": (106496, 3072, 1024), "enc_wo_2k": (106496, 1024, 1024), "enc_ff1_2k": (100352, 4096, 1024),
+    "enc_ff2_2k": (100352, 1024, 4096), "dec_qkv_2k": (407552, 1536, 512), "dec_wo_2k": (407552, 512, 512),
+    "dec_ff1_2k": (407552, 2048, 512), "dec_ff2_2k": (407552, 512, 2048),
 }
 
 
