@@ -60,6 +60,8 @@ def main():
     ap.add_argument("--no-overlap", action="store_true")
     ap.add_argument("--shard-optimizer", action="store_true",
                     help="ZeRO-1: reduce-scatter + sharded optimizer + all-gather (default: all-reduce)")
+    ap.add_argument("--zero1-gather", default="bf16", choices=["bf16", "fp32"],
+                    help="ZeRO-1 weight all-gather dtype (bf16 shadow, or the fp32 master re-cast)")
     ap.add_argument("--profile-steps", type=int, default=0, help="extra steps under torch.profiler (debug)")
     ap.add_argument("--task", default="pretrain", choices=["pretrain", "finetune", "linear"])
     ap.add_argument("--dropout", type=float, default=0.0,
@@ -119,7 +121,7 @@ def main():
                         num_layers=vc.layers)
     rdt = torch.bfloat16 if args.reduce_dtype == "bf16" else torch.float32
     reducer = (GradReducer(store, bucket_mb=args.bucket_mb, overlap=not args.no_overlap, reduce_dtype=rdt,
-                           shard=args.shard_optimizer)
+                           shard=args.shard_optimizer, gather_dtype=args.zero1_gather)
                if world > 1 or pdist.forced_group() else None)
     rngs = RngStreams({"noise": 0, "dropout": 0, "mixup": 0}, info.rank, dev)
     trainer = Trainer(model, opt, reducer, rngs, grad_accum=args.grad_accum)
@@ -169,6 +171,12 @@ def main():
     elapsed = pdist.all_reduce_max_scalar(elapsed, dev)
     final_loss = float(m["loss"].item())
     comm_ms = trainer.comm_ms()
+    # multi-GPU self-calibration, outside the timed region: one traced step (when each bucket's
+    # gradient became final, on the GPU clock) and one timed collective per distinct bucket size
+    # of the real plan -- the inputs of tools/dp_exposure_model.py (--sweep reads this JSON line)
+    calib = trace_and_calibrate(reducer, step, dev) if (reducer is not None and world > 1) else None
+    if reducer is not None and reducer.shard:
+        opt.gather_state()  # ZeRO-1: the sharded fp32 master (and moments) made whole for the checksum
     # data-parallel replicas must hold identical weights after the timed steps (outside the timed
     # region): spread of a weight checksum over the ranks, 0.0 when in sync
     spread = pdist.all_reduce_max_scalar(float(store.master.double().abs().sum()), dev) - \
@@ -212,6 +220,7 @@ def main():
             "peak_hbm_gb": peak_gb,
             "replica_weight_checksum_spread": spread, "weight_checksum": weight_checksum,
             "reducer": reducer.stats() if reducer is not None else None,
+            **(calib or {}),
             "dtype": "fp32" if args.cpu else "bf16",
             "data": f"synthetic uint8 {S}x{S} images on {'CPU' if args.cpu else 'GPU'}, random-init weights",
             "config": {
@@ -231,6 +240,34 @@ def main():
         }
         print(json.dumps(out), flush=True)
     pdist.cleanup()
+
+
+def trace_and_calibrate(reducer, step, dev) -> dict:
+    """One extra (untimed) step with the reducer's readiness trace on -> per-collective ready times
+    relative to the step start; then ``parallel.collbench.calibrate`` on the same process group."""
+    import time as _t
+
+    from jumbo_mae_tpu_amd.parallel.collbench import calibrate
+    cuda = dev.type == "cuda"
+    reducer.trace_events = []
+    if cuda:
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+    h0 = _t.perf_counter()
+    step()
+    if cuda:
+        e1.record()
+        torch.cuda.synchronize()
+    esz = 2 if reducer.reduce_dtype == torch.bfloat16 else 4
+    spans = []
+    for b, lo, hi, partial, ev in reducer.trace_events:
+        t = e0.elapsed_time(ev) if cuda else (ev - h0) * 1e3
+        spans.append({"bucket": b, "bytes": (hi - lo) * esz, "ready_ms": round(t, 3), "partial": bool(partial)})
+    reducer.trace_events = None
+    step_ms = e0.elapsed_time(e1) if cuda else (_t.perf_counter() - h0) * 1e3
+    return {"dp_traced_step_ms": round(step_ms, 3), "dp_ready_spans": spans,
+            "collective_sweep": calibrate(reducer, dev)}
 
 
 def bench_classifier(args):
@@ -278,7 +315,8 @@ def bench_classifier(args):
         flags += [f"--{k}-seed", "0"]
     fargs = finetune_parser().parse_args(flags + ["--train-batch-size", str(gb), "--bucket-mb", str(args.bucket_mb),
                                                 "--reduce-dtype", args.reduce_dtype]
-                                         + (["--shard-optimizer"] if args.shard_optimizer else []))
+                                         + (["--shard-optimizer", "--zero1-gather", args.zero1_gather]
+                                            if args.shard_optimizer else []))
     model = build_model(fargs, dev, torch.bfloat16, info.rank)
     pdist.broadcast_(model.store.master)
     model.store.sync_shadow()

@@ -14,7 +14,8 @@ int jm_layernorm_fwd(const float* x, long sB, long sT, int B, int T, int D, cons
 int jm_layernorm_bwd(const void* dy, int dy_bf16, const float* x, long sB, long sT, int B, int T, int D,
                      const float* mean, const float* rstd, const float* gamma, float* dx_ptr, long oB, long oT,
                      const float* dres, long rB, long rT, float* dgamma, float* dbeta, int accum_params, float* ws,
-                     const JmLnRes* res, hipStream_t st);
+                     const JmLnRes* res, hipStream_t st, const uint16_t* hx = nullptr,
+                     const float* beta = nullptr);
 int jm_layernorm_bwd_blocks(int rows, int D);
 // debug build (-DJM_DEBUG): first failing soft-check line per kernel translation unit (0 = none;
 // reading clears it); always 0 in the release build
@@ -198,7 +199,8 @@ std::vector<torch::Tensor> layernorm_bwd(torch::Tensor dy, torch::Tensor x, torc
                                          c10::optional<torch::Tensor> res_mask, c10::optional<torch::Tensor> res_dscale,
                                          c10::optional<torch::Tensor> res_dbias, int64_t res_T0,
                                          c10::optional<torch::Tensor> res_out, c10::optional<torch::Tensor> res_seed,
-                                         double res_rate, int64_t res_ioff) {
+                                         double res_rate, int64_t res_ioff, c10::optional<torch::Tensor> hx,
+                                         c10::optional<torch::Tensor> beta) {
   CHECK_CONTIG(dy);
   TORCH_CHECK(x.dim() == 3 && x.stride(2) == 1, "x must be [B,T,D]");
   const int B = x.size(0), T = x.size(1), D = x.size(2);
@@ -249,13 +251,24 @@ std::vector<torch::Tensor> layernorm_bwd(torch::Tensor dy, torch::Tensor x, torc
     res = JmLnRes{bf(y), bfm(dyr), yB, yT, fopt(res_scale), fopt(res_mask), (int)res_T0, fopt_m(res_dscale),
                   fopt_m(res_dbias), make_drop(res_seed, res_rate, y, res_ioff)};
   }
+  const uint16_t* hxp = nullptr;
+  const float* betap = nullptr;
+  if (hx.has_value() && hx->defined()) {  // the forward's bf16 LN output, rows like dy
+    CHECK_DT((*hx), torch::kBFloat16);
+    CHECK_CONTIG((*hx));
+    TORCH_CHECK(hx->numel() == (long)B * T * D, "hx shape");
+    TORCH_CHECK(beta.has_value() && beta->defined() && beta->numel() == D, "hx needs beta [D]");
+    CHECK_DT((*beta), torch::kFloat32);
+    hxp = bf(*hx);
+    betap = beta->data_ptr<float>();
+  }
   const int NP = has_res ? 4 : 2;
   auto ws = torch::empty({(accum || has_res) ? (long)jm_layernorm_bwd_blocks(B * T, D) * NP * D : 1}, x.options());
   check_rc(jm_layernorm_bwd(dy.data_ptr(), dyb, x.data_ptr<float>(), x.stride(0), x.stride(1), B, T, D,
                             mean.data_ptr<float>(), rstd.data_ptr<float>(), gamma.data_ptr<float>(),
                             dx.data_ptr<float>(), dx.stride(0), dx.stride(1), rp, rB, rT, dgamma.data_ptr<float>(),
                             dbeta.data_ptr<float>(), accum, ws.data_ptr<float>(), has_res ? &res : nullptr,
-                            stream()),
+                            stream(), hxp, betap),
            "layernorm_bwd");
   if (has_res) return {dx, dyr};
   return {dx};
@@ -1224,7 +1237,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("out") = py::none(), py::arg("res_y") = py::none(), py::arg("res_scale") = py::none(),
         py::arg("res_mask") = py::none(), py::arg("res_dscale") = py::none(), py::arg("res_dbias") = py::none(),
         py::arg("res_T0") = 0, py::arg("res_out") = py::none(), py::arg("res_seed") = py::none(),
-        py::arg("res_rate") = 0.0, py::arg("res_ioff") = 0);
+        py::arg("res_rate") = 0.0, py::arg("res_ioff") = 0, py::arg("hx") = py::none(), py::arg("beta") = py::none());
   m.def("gelu_fwd", &gelu_fwd);
   m.def("dropout_apply", &dropout_apply);
   m.def("dropout_apply_", &dropout_apply_);

@@ -175,12 +175,23 @@ __global__ __launch_bounds__(256) void res_ln_fwd_kernel(ResLnIO io, int T, int 
 
 // dx output and optional residual-gradient input, both [B, T, D] views with their own strides:
 // dx = LN'(dy) (+ dres), i.e. the residual-stream gradient add is fused into the LN backward.
+// hx / beta (optional): the forward's bf16 LN output h = bf16(gamma x-hat + beta), contiguous rows
+// like dy.  x-hat is then rebuilt as (h - beta) / gamma from 2 bytes per element instead of
+// re-reading the fp32 residual-stream input (4 bytes) and its (mean, rstd) -- for the columns
+// where that is accurate: |beta| <= |gamma| (x-hat error <= 2^-9 (|x-hat| + |beta / gamma|), i.e.
+// within 2x of bf16's own rounding of x-hat).  Lanes whose 4-column chunk has a column outside
+// that bound read x for that chunk as before.
 struct LnBwdIO {
   float* dx;
   long oB, oT;
   const float* dres;
   long rB, rT;
+  const uint16_t* hx;
+  const float* beta;
 };
+
+// a column where x-hat may be rebuilt from h: |beta| <= |gamma|, gamma not tiny
+JM_DEVICE bool ln_h_ok(float g, float b) { return fabsf(g) >= 1e-20f && fabsf(b) <= fabsf(g); }
 
 // Optional fused residual backward of the branch that FEEDS on dx (the next op of the backward
 // pass): rows t >= T0 of the LN's [B, T] grid are residual targets,
@@ -241,6 +252,10 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const TI* __restrict__ dy, 
     }
   };
   float acc[NP][VL][4], gg[VL][4], sc[VL][4];
+  // h path: beta and 1 / gamma per column in LDS (after the [NP*D] merge area), read per row
+  float* hbi = red + (partials ? NP * D : 0);  // [D] beta, then [D] 1 / gamma
+  const bool use_h = io.hx != nullptr;
+  uint32_t xchunk = 0;  // bit i: chunk i of this lane reads x (a column outside the h bound)
 #pragma unroll
   for (int i = 0; i < VL; ++i) {
     const int col = (i * LPR + l) * 4;
@@ -255,8 +270,24 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const TI* __restrict__ dy, 
       if constexpr (RES && SC) {
         if (rio.scale) load4(rio.scale + col, sc[i]);
       }
+      if (use_h) {
+        float bb[4], ig[4];
+        load4(io.beta + col, bb);
+        bool ok = true;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          ok = ok && ln_h_ok(gg[i][j], bb[j]);
+          ig[j] = 1.f / gg[i][j];
+        }
+        if (!ok) xchunk |= 1u << i;
+        if (wave == 0 && sub == 0) {
+          store4(hbi + col, bb);
+          store4(hbi + D + col, ig);
+        }
+      }
     }
   }
+  if (use_h) __syncthreads();
   for (int rw = blockIdx.x * 4 + wave; rw * R < rows; rw += gridDim.x * 4) {
     const int row = rw * R + sub;
     const bool valid = R == 1 || row < rows;  // R = 2: the second half of an odd tail has no row
@@ -270,12 +301,26 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const TI* __restrict__ dy, 
     float rvp[ER ? VL : 1][4];
     const float* rr = io.dres ? io.dres + b * io.rB + t * io.rT : nullptr;
     float sg = 0.f, sgx = 0.f;
+    const uint16_t* hr = use_h ? io.hx + (long)row * D : nullptr;
 #pragma unroll
     for (int i = 0; i < VL; ++i) {
       const int col = (i * LPR + l) * 4;
       if (valid && col < D) {
         float xv[4], dv[4];
-        load4(xr + col, xv);
+        if (use_h && !((xchunk >> i) & 1u)) {
+          float hv[4], bb[4], ig[4];
+          load4(hr + col, hv);
+          load4(hbi + col, bb);
+          load4(hbi + D + col, ig);
+          // x-hat = (h - beta) / gamma, fed through the same (x - mu) * rs below as x = x-hat
+          // with (mu, rs) = (0, 1): selects below
+#pragma unroll
+          for (int j = 0; j < 4; ++j) xv[j] = (hv[j] - bb[j]) * ig[j];
+        } else {
+          load4(xr + col, xv);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) xv[j] = (xv[j] - mu) * rs;
+        }
         load4(dyr + col, dv);
         if constexpr (RES && SC) {
           if (rrow && rio.scale) load4(rio.y + yoff + col, yv[i]);
@@ -286,7 +331,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const TI* __restrict__ dy, 
         }
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          xh[i][j] = (xv[j] - mu) * rs;
+          xh[i][j] = xv[j];
           g[i][j] = dv[j] * gg[i][j];
           sg += g[i][j];
           sgx += g[i][j] * xh[i][j];
@@ -714,8 +759,9 @@ int jm_layernorm_bwd_blocks(int rows, int D) {
 int jm_layernorm_bwd(const void* dy, int dy_bf16, const float* x, long sB, long sT, int B, int T, int D,
                      const float* mean, const float* rstd, const float* gamma, float* dx_ptr, long oB, long oT,
                      const float* dres, long rB, long rT, float* dgamma, float* dbeta, int accum_params, float* ws,
-                     const JmLnRes* res, hipStream_t st) {
-  const LnBwdIO dx{dx_ptr, oB, oT, dres, rB, rT};
+                     const JmLnRes* res, hipStream_t st, const uint16_t* hx, const float* beta) {
+  if (hx != nullptr && beta == nullptr) return -3;
+  const LnBwdIO dx{dx_ptr, oB, oT, dres, rB, rT, hx, beta};
   const int V = pick_v(D);
   if (V < 0 || (D % 4) != 0) return -1;
   const int rows = B * T;
@@ -742,7 +788,7 @@ int jm_layernorm_bwd(const void* dy, int dy_bf16, const float* x, long sB, long 
     }
     return 0;
   }
-  const size_t smem = partials ? NP * D * sizeof(float) : 0;
+  const size_t smem = ((partials ? NP * D : 0) + (hx ? 2 * D : 0)) * sizeof(float);
   const ParamOuts outs{{accum_params ? dgamma : nullptr, accum_params ? dbeta : nullptr,
                         res ? res->dscale : nullptr, res ? res->dbias : nullptr}};
   float* wsk = ws;

@@ -19,10 +19,10 @@ from ..utils.mae import extract_patches, index_sequence, patch_mse_loss
 from ..utils.posemb import fixed_sincos2d_embeddings
 
 
-def tree_to_torch(tree, requires_grad=True, dtype=torch.float64):
+def tree_to_torch(tree, requires_grad=True, dtype=torch.float64, device=None):
     if isinstance(tree, dict):
-        return {k: tree_to_torch(v, requires_grad, dtype) for k, v in tree.items()}
-    return torch.tensor(tree, dtype=dtype, requires_grad=requires_grad)
+        return {k: tree_to_torch(v, requires_grad, dtype, device) for k, v in tree.items()}
+    return torch.tensor(tree, dtype=dtype, device=device, requires_grad=requires_grad)
 
 
 def _ln(x, p, eps=1e-6):
@@ -75,8 +75,8 @@ def vit_layer(x, p, heads):
 
 def normalize_nhwc(images_u8, dtype=torch.float64):
     x = images_u8.permute(0, 2, 3, 1).to(dtype) / 255.0
-    m = torch.tensor(IMAGENET_DEFAULT_MEAN, dtype=dtype)
-    s = torch.tensor(IMAGENET_DEFAULT_STD, dtype=dtype)
+    m = torch.tensor(IMAGENET_DEFAULT_MEAN, dtype=dtype, device=images_u8.device)
+    s = torch.tensor(IMAGENET_DEFAULT_STD, dtype=dtype, device=images_u8.device)
     return (x - m) / s
 
 
@@ -87,14 +87,16 @@ def patch_embed(images_nhwc, p, posemb, patch, dim):
     if "wpe" in p:
         x = x + p["wpe"]
     else:
-        x = x + posemb.to(x.dtype)
+        x = x + posemb.to(x.device, x.dtype)
     return x.reshape(x.shape[0], -1, dim)
 
 
 def mae_loss(params, images_u8, noise, *, layers, dim, heads, dec_layers, dec_dim, dec_heads,
-             patch, mask_ratio, norm_pix_loss=False, posemb="sincos2d", C=3):
-    """Reference PretrainModule.__call__ with a given masking noise (shape (N,) or (B,N))."""
-    imgs = normalize_nhwc(images_u8)
+             patch, mask_ratio, norm_pix_loss=False, posemb="sincos2d", C=3, dtype=torch.float64):
+    """Reference PretrainModule.__call__ with a given masking noise (shape (N,) or (B,N)).  Runs on
+    the device of ``images_u8`` in ``dtype`` (fp64 on the CPU for the parity tests; fp32 on the GPU
+    as the reference of the ViT-L-width test)."""
+    imgs = normalize_nhwc(images_u8, dtype)
     B, H, W, _ = imgs.shape
     g = H // patch
     m = params["model"]
@@ -107,7 +109,7 @@ def mae_loss(params, images_u8, noise, *, layers, dim, heads, dec_layers, dec_di
     ids_shuffle = torch.argsort(noise, dim=-1)
     ids_restore = torch.argsort(ids_shuffle, dim=-1)
     kept = index_sequence(pt, ids_shuffle[..., :keep])
-    base = torch.ones(noise.shape, dtype=imgs.dtype)
+    base = torch.ones(noise.shape, dtype=imgs.dtype, device=imgs.device)
     base[..., :keep] = 0
     mask = base[ids_restore] if noise.dim() == 1 else torch.gather(base, -1, ids_restore)
     if mask.dim() == 1:
@@ -120,7 +122,7 @@ def mae_loss(params, images_u8, noise, *, layers, dim, heads, dec_layers, dec_di
     enc_cls, img = x[:, :C], x[:, C:]
     mt = params["image_mask_embedding"].expand(B, N - keep, dec_dim)
     img = index_sequence(torch.cat([img, mt], 1), ids_restore)
-    dpos = fixed_sincos2d_embeddings(g, g, dec_dim).to(img.dtype).reshape(1, N, dec_dim)
+    dpos = fixed_sincos2d_embeddings(g, g, dec_dim).to(img.device, img.dtype).reshape(1, N, dec_dim)
     x = torch.cat([enc_cls, img + dpos], 1)
     d = params["decoder_model"]
     for j in range(dec_layers):

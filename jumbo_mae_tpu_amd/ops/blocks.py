@@ -234,10 +234,10 @@ def _jumbo_bwd(ctx, dx2):
     _, _, bd = P.ln_bwd(dhp, x1[:, C:], mup, rsp, layer.norm2.g, layer.norm2.b, dres=dx2[:, C:],
                         out=dx1[:, C:],
                         res=P.ResSpec(a3[:, C:], layer.scale1, m1, layer.attn.wo_b, 0, da3[:, C:],
-                                      drop=_od(dr, "wo", a)))
+                                      drop=_od(dr, "wo", a)), h=hp)
     # ---- attention branch: dx = dx1 + LN1'(Attn'(s1 * dp1 * dx1))
     dh1 = _attn_bwd(layer.attn, da, h1, qkv, o, lse, B, S, bd, dr)
-    return _ln1_bwd(ctx, dh1, x, mu1, rs1, layer, dx1)
+    return _ln1_bwd(ctx, dh1, x, mu1, rs1, layer, dx1, h1)
 
 
 def _ln1_fwd(x, layer, link_in, dt):
@@ -248,13 +248,14 @@ def _ln1_fwd(x, layer, link_in, dt):
     return P.ln_fwd(x, layer.norm1.g, layer.norm1.b, dt)
 
 
-def _ln1_bwd(ctx, dh1, x, mu1, rs1, layer, dx1):
+def _ln1_bwd(ctx, dh1, x, mu1, rs1, layer, dx1, h1=None):
     """dx = dx1 + LN1'(dh1) into dx1; with a lower fused block linked, its patch-branch residual
-    backward rides on the same pass (Link)."""
+    backward rides on the same pass (Link).  ``h1``: LN1's bf16 output (x-hat rebuilt from it)."""
     li = ctx.link_in
     if li is None or li.spec is None:
-        return P.ln_bwd(dh1, x, mu1, rs1, layer.norm1.g, layer.norm1.b, dres=dx1, out=dx1)
-    dx, li.dy, li.done = P.ln_bwd(dh1, x, mu1, rs1, layer.norm1.g, layer.norm1.b, dres=dx1, out=dx1, res=li.spec)
+        return P.ln_bwd(dh1, x, mu1, rs1, layer.norm1.g, layer.norm1.b, dres=dx1, out=dx1, h=h1)
+    dx, li.dy, li.done = P.ln_bwd(dh1, x, mu1, rs1, layer.norm1.g, layer.norm1.b, dres=dx1, out=dx1, res=li.spec,
+                                  h=h1)
     li.dx_key = (dx.data_ptr(), tuple(dx.shape))
     li.spec = None
     return dx
@@ -318,9 +319,9 @@ def _vit_bwd(ctx, dx2):
     dh2 = _ff_bwd(layer.ff, dfy, h2, fpre, fg, bd, deriv=ctx.gelu_deriv[1], rate=ctx.gelu_rate)
     # LN2' with the attention-residual backward of its dx fused in (never write autograd's dx2)
     dx1, da, bd = P.ln_bwd(dh2, x1, mu2, rs2, layer.norm2.g, layer.norm2.b, dres=dx2,
-                           res=P.ResSpec(a, layer.scale1, m1, layer.attn.wo_b, drop=_od(dr, "wo", a)))
+                           res=P.ResSpec(a, layer.scale1, m1, layer.attn.wo_b, drop=_od(dr, "wo", a)), h=h2)
     dh1 = _attn_bwd(layer.attn, da, h1, qkv, o, lse, B, S, bd, dr)
-    return _ln1_bwd(ctx, dh1, x, mu1, rs1, layer, dx1)
+    return _ln1_bwd(ctx, dh1, x, mu1, rs1, layer, dx1, h1)
 
 
 def vit_block(layer, x, m1=None, m2=None, link_in: Link | None = None, link_out: Link | None = None,

@@ -13,6 +13,7 @@ from __future__ import annotations
 
 import contextlib
 import math
+import os
 
 from typing import NamedTuple
 
@@ -233,8 +234,10 @@ def linear_gelu_fwd(x2: torch.Tensor, hw: Handle, hb: Handle | None, need_pre: b
     return pre, gelu_fwd(pre)
 
 
-# save gelu'(h) instead of h for the backward when the fused MFMA forward runs (A/B switch)
-_GELU_DERIV = True
+# save gelu'(h) (8-bit codes) instead of h for the backward when the fused MFMA forward runs;
+# JMAE_GELU_CODES=0: save h and recompute gelu'(h) exactly in the backward epilogue (loss-curve A/B
+# of the two: profiles/r6b_gelu_code_loss_ab.txt)
+_GELU_DERIV = os.environ.get("JMAE_GELU_CODES", "1") != "0"
 
 
 # gelu'(h) saved as 8-bit codes by the fused FF1 forward (csrc/common.h gd_code): q = round(GD_Q d) + GD_Z
@@ -583,26 +586,37 @@ def _drop_factor(y: torch.Tensor, drop) -> torch.Tensor:
     return full.as_strided(y.shape, y.stride(), y.storage_offset() - base.storage_offset())
 
 
+# LN backward rebuilds x-hat from the forward's bf16 output h = bf16(gamma x-hat + beta) where
+# |beta| <= |gamma| (2 bytes per element instead of the fp32 input's 4; csrc/layernorm.hip LnBwdIO)
+_LN_BWD_FROM_H = True
+
+
 def ln_bwd(dy: torch.Tensor, x3: torch.Tensor, mean, rstd, hg: Handle, hb: Handle, dres=None, out=None,
-           res: ResSpec | None = None):
+           res: ResSpec | None = None, h: torch.Tensor | None = None):
     """dx = LN'(dy) (+ dres) written to ``out`` (a [B,T,D] view) or a new tensor; accumulates
     dgamma / dbeta.  With ``res`` the residual backward of dx's consumer rides on the same pass
-    and (dx, dy_res, bias_done) is returned (the separate pass would re-read dx from HBM)."""
+    and (dx, dy_res, bias_done) is returned (the separate pass would re-read dx from HBM).
+    ``h``: the forward's bf16 output of this LN (rows like ``dy``); the HIP kernel then reads it
+    instead of ``x3`` for the columns where that is exact to bf16 level."""
     B, T, D = x3.shape
     dy = dy.contiguous()
     tr = _trainable(hg)
     fused = res is not None and _FUSE_LN_RES and hip(x3) and res.y.dtype == torch.bfloat16
     dyr = None
     if hip(x3):
+        hx = h if (_LN_BWD_FROM_H and h is not None and h.dtype == torch.bfloat16 and h.is_contiguous()
+                   and h.numel() == dy.numel()) else None
+        beta = hb.master if hx is not None else None
         if fused:
             hs, hbias = res.hs, res.hbias
             dseed, drate, dioff = _drop_args(res.y, res.drop)
             dx, dyr = _ext.load().layernorm_bwd(
                 dy, x3, mean, rstd, hg.master, hg.grad, hb.grad, tr, dres, out, res.y,
                 hs.master if hs is not None else None, res.mask, hs.grad if _trainable(hs) else None,
-                hbias.grad if _trainable(hbias) else None, res.t0, res.out, dseed, drate, dioff)
+                hbias.grad if _trainable(hbias) else None, res.t0, res.out, dseed, drate, dioff, hx, beta)
         else:
-            dx = _ext.load().layernorm_bwd(dy, x3, mean, rstd, hg.master, hg.grad, hb.grad, tr, dres, out)[0]
+            dx = _ext.load().layernorm_bwd(dy, x3, mean, rstd, hg.master, hg.grad, hb.grad, tr, dres, out,
+                                           hx=hx, beta=beta)[0]
     else:
         xf = x3.reshape(B * T, D).float()
         xhat = (xf - mean[:, None]) * rstd[:, None]

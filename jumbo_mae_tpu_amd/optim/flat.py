@@ -308,6 +308,9 @@ class FlatOptimizer:
         if own is not None:
             for t, old in zip([t for t in (self.mu, self.nu, self.trace) if t is not None], saved):
                 t.copy_(torch.where(own, t, old))
+            if s.shadow is not s.master:  # owned pieces only: the rest arrives by the all-gather
+                s.shadow.copy_(torch.where(own, p, s.shadow.float()))
+                return
         s.sync_shadow()
 
     @torch.no_grad()

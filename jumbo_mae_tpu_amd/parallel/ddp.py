@@ -37,10 +37,18 @@ MI355X design:
   bucket.  A complete bucket is REDUCE-SCATTERED (in place: rank r's piece of the flat gradient
   receives the average), the optimizer updates only the owned pieces (1/world of the AdamW /
   LAMB / LARS / SGD work; LAMB / LARS per-leaf norms and the global clip norm are summed over the
-  ranks by a tiny all-reduce), and each bucket's updated fp32 master is ALL-GATHERED in place
-  and re-cast to the bf16 shadow.  Link bytes per parameter: 4 + 4 (= the all-reduce's two
-  halves), 2 + 4 with ``reduce_dtype=bf16``.  Optimizer moments of non-owned pieces are never
-  touched; ``gather_state`` all-gathers them for a checkpoint.
+  ranks by a tiny all-reduce), and each bucket's updated bf16 SHADOW (the compute copy the
+  optimizer kernel writes beside the owned fp32 master) is ALL-GATHERED in place: 2 bytes per
+  parameter on the link instead of the fp32 master's 4, no re-cast pass, bit-identical weights
+  (every rank's shadow piece is the cast of its owner's new master).  The fp32 master of a
+  non-owned piece is then stale on this rank -- only the owner updates it, as in ZeRO-1 -- and
+  ``gather_state`` all-gathers it (with the optimizer moments) for a checkpoint / export.  The few
+  parameters the kernels read in fp32 from the master (biases, LayerNorm / LayerScale, tokens:
+  every non-``kernel`` leaf, ~0.1 % of a ViT) are exchanged exactly each step by one small int32
+  all-reduce of their bits (``exchange_fp32``).
+  ``gather_dtype="fp32"`` gathers the master and re-casts (the round-5 path; also used whenever the
+  shadow IS the master, i.e. fp32 compute).  Link bytes per parameter: 4 + 2 (fp32 reduce-scatter
+  + bf16 gather), 2 + 2 with ``reduce_dtype=bf16``.
 * Chunked jumbo tail in ZeRO-1 mode: a reduce-scatter cannot start on a partial range of its bucket
   (rank r owns piece r of the WHOLE bucket), so a bucket holding a segment larger than the bucket
   size is cut into ``PARTIAL_SUB`` sub-buckets at the row-chunk boundaries of the batched jumbo
@@ -55,6 +63,7 @@ from __future__ import annotations
 
 import contextlib
 import re
+import time
 
 import torch
 import torch.distributed as dist
@@ -178,7 +187,8 @@ def shard_ranges(buckets: list[tuple[int, int]], q: int) -> list[tuple[int, int]
 
 class GradReducer:
     def __init__(self, store: ParamStore, group=None, bucket_mb: float = 64.0, overlap: bool = True,
-                 reduce_dtype: torch.dtype = torch.float32, seg_filter=None, shard: bool = False):
+                 reduce_dtype: torch.dtype = torch.float32, seg_filter=None, shard: bool = False,
+                 gather_dtype: str = "bf16"):
         self.store = store
         self.group = group
         self.world = dist.get_world_size(group) if (dist.is_available() and dist.is_initialized()) else 1
@@ -215,17 +225,25 @@ class GradReducer:
         for bi, (_, _, idxs) in enumerate(self.buckets):
             for i in idxs:
                 self.seg_buckets[i].append(bi)
-        self.gathers: list[tuple] = []  # (bucket, work) all-gathers of the updated master (shard)
+        # ZeRO-1 all-gathers the bf16 shadow (the master stays sharded between checkpoints)
+        self.gather_shadow = self.shard and gather_dtype == "bf16" and store.shadow is not store.master
+        self._fp32_idx = None
+        self.gathers: list[tuple] = []  # (bucket, work) all-gathers of the updated weights (shard)
         self.gathered = [False] * len(self.buckets)
         self._stage = None  # bf16 staging buffer over [stage_lo, stage_hi) of the flat buffer
         self._stage_lo = min((lo for lo, _, _ in self.buckets), default=0)
         self._stage_hi = max((hi for _, hi, _ in self.buckets), default=0)
+        if self.gather_shadow:
+            self._init_fp32_exchange()
         self.pending_uses = [0] * len(segs)
         self.ready_iv: list[list[tuple[int, int]]] = [[] for _ in segs]  # shard: final element ranges
         self.bucket_left = [len(b[2]) for b in self.buckets]
         self.launched = [False] * len(self.buckets)
         self.works: list[tuple] = []  # (bucket, work, tensor to divide or None, lo, hi, staged, partial)
         self.partial_done = [0] * len(self.buckets)  # elements of a bucket already launched
+        # readiness trace (bench.py calibration step): a list -> (bucket, lo, hi, partial, event)
+        # per collective launch, the event recorded on the compute stream when the range was final
+        self.trace_events: list | None = None
         if self.enabled:
             store.hooks.append(self._on_ready)
             store.use_hooks.append(self._on_use)
@@ -335,6 +353,11 @@ class GradReducer:
         """Launch the all-reduce of flat-buffer elements [lo, hi) (bucket ``b``); sharded: the
         in-place reduce-scatter whose result lands in this rank's piece."""
         view = self.store.grad[lo:hi]
+        if self.trace_events is not None:
+            ev = torch.cuda.Event(enable_timing=True) if view.is_cuda else None
+            if ev is not None:
+                ev.record()
+            self.trace_events.append((b, lo, hi, partial, ev if ev is not None else time.perf_counter()))
         st = self.staging()
         if self.shard:
             plo, phi = self.piece(b)
@@ -396,12 +419,47 @@ class GradReducer:
         with torch.cuda.stream(side) if side is not None else contextlib.nullcontext():
             return dist.all_gather_into_tensor(out, inp, group=self.group, async_op=True)
 
+    def _init_fp32_exchange(self) -> None:
+        """The parameters the kernels read in fp32 from the MASTER (biases, LayerNorm / LayerScale
+        parameters, CLS / mask tokens, learnable position embeddings: every leaf that is not a Dense
+        or conv ``kernel``) must be whole on every rank even when only the bf16 shadow is gathered.
+        Their elements (~0.1 % of a ViT) are exchanged each step by one int32 SUM all-reduce of
+        their bits, each rank contributing its owned elements and zeros: exact, bit for bit."""
+        idx, own = [], []
+        owned = torch.zeros(self.store.total, dtype=torch.bool)
+        for b in range(len(self.buckets)):
+            lo, hi = self.piece(b)
+            owned[lo:hi] = True
+        for sg in self.segs:
+            if sg.path[-1] == "kernel" and len(sg.shape) >= 2:
+                continue
+            r = torch.arange(sg.offset, sg.offset + sg.numel)
+            idx.append(r)
+            own.append(owned[r])
+        if not idx:
+            return
+        dev = self.store.master.device
+        self._fp32_idx = torch.cat(idx).to(dev)
+        self._fp32_own = torch.cat(own).to(dev)
+
+    def exchange_fp32(self) -> None:
+        """COLLECTIVE: the owners' updated fp32 values of the master-read parameters to every rank."""
+        if self._fp32_idx is None:
+            return
+        m = self.store.master
+        bits = m[self._fp32_idx].view(torch.int32)
+        bits = torch.where(self._fp32_own, bits, torch.zeros_like(bits))
+        dist.all_reduce(bits, op=dist.ReduceOp.SUM, group=self.group)
+        m[self._fp32_idx] = bits.view(torch.float32)
+
     def gather(self, b: int) -> None:
-        """All-gather bucket ``b``'s updated fp32 master (in place) after the owned piece's update."""
+        """All-gather bucket ``b``'s updated weights (in place) after the owned piece's update: the
+        bf16 shadow (``gather_shadow``) or the fp32 master."""
         if not self.shard or self.gathered[b]:
             return
         self.gathered[b] = True
-        self.gathers.append((b, self._gather_into(self.store.master, b)))
+        flat = self.store.shadow if self.gather_shadow else self.store.master
+        self.gathers.append((b, self._gather_into(flat, b)))
 
     def gather_all(self) -> None:
         for b in range(len(self.buckets)):
@@ -412,17 +470,23 @@ class GradReducer:
         s = self.store
         for b, w in self.gathers:
             w.wait()
-            if s.shadow is not s.master:
+            if s.shadow is not s.master and not self.gather_shadow:
                 lo, hi, _ = self.buckets[b]
                 with torch.no_grad():
                     s.shadow[lo:hi].copy_(s.master[lo:hi])
+        if self.gathers and self.gather_shadow:
+            with torch.no_grad():
+                self.exchange_fp32()
         self.gathers = []
 
-    def gather_state(self, tensors) -> None:
+    def gather_state(self, tensors=()) -> None:
         """COLLECTIVE: all-gather optimizer state buffers (flat, like the master) so every rank
-        holds every piece (checkpoint save)."""
+        holds every piece (checkpoint save) -- and the fp32 master itself when the steps gather
+        only the bf16 shadow."""
         if not self.shard:
             return
+        if self.gather_shadow:
+            tensors = [self.store.master] + list(tensors)
         for t in tensors:
             if t is None:
                 continue
@@ -504,4 +568,5 @@ class GradReducer:
         return {"buckets": len(self.buckets), "bucket_mb_max": max(sizes) if sizes else 0.0,
                 "bucket_mb_min": min(sizes) if sizes else 0.0,
                 "mode": "zero1-reduce-scatter" if self.shard else "all-reduce",
-                "reduce_dtype": "bf16" if self.reduce_dtype == torch.bfloat16 else "fp32"}
+                "reduce_dtype": "bf16" if self.reduce_dtype == torch.bfloat16 else "fp32",
+                **({"gather_dtype": "bf16" if self.gather_shadow else "fp32"} if self.shard else {})}

@@ -95,6 +95,9 @@ def _extensions(p: argparse.ArgumentParser):
     g.add_argument("--shard-optimizer", action="store_true",
                    help="ZeRO-1: reduce-scatter the gradient buckets, update 1/N of the parameters per rank, "
                         "all-gather the updated weights (parallel/ddp.py)")
+    g.add_argument("--zero1-gather", default="bf16", choices=["bf16", "fp32"],
+                   help="ZeRO-1 weight all-gather: the bf16 compute shadow (fp32 master stays sharded until a "
+                        "checkpoint) or the fp32 master (re-cast after the gather)")
     g.add_argument("--stop-after-steps", type=int, default=0,
                    help="end this invocation after N steps, writing 'last' (time-sliced / preemptible "
                         "jobs: continue with --resume auto); 0 = run to --training-steps")

@@ -49,7 +49,8 @@ def make_reducer(args, store):
     if pdist.info().world_size > 1 or pdist.forced_group():
         dt = torch.bfloat16 if getattr(args, "reduce_dtype", "fp32") == "bf16" else torch.float32
         return GradReducer(store, bucket_mb=args.bucket_mb, reduce_dtype=dt,
-                           shard=getattr(args, "shard_optimizer", False))
+                           shard=getattr(args, "shard_optimizer", False),
+                           gather_dtype=getattr(args, "zero1_gather", "bf16"))
     return None
 
 
@@ -62,6 +63,11 @@ def use_device_augment(args, device) -> bool:
     if not device_augment_ok(args):
         if mode == "on":
             raise SystemExit("--device-augment on: the train transform must be RandomResizedCrop + flip only")
+        return False
+    from ..ops import _ext
+    if not _ext.available():  # no built extension (JMAE_ALLOW_TORCH_FALLBACK runs): the PIL path
+        if mode == "on":
+            raise SystemExit("--device-augment on needs the built HIP extension (python -m jumbo_mae_tpu_amd.csrc.build)")
         return False
     return True
 

@@ -20,7 +20,8 @@ def _port():
         return s.getsockname()[1]
 
 
-@pytest.mark.parametrize("extra", [[], ["--reduce-dtype", "bf16", "--grad-accum", "2"], ["--no-overlap"]])
+@pytest.mark.parametrize("extra", [[], ["--reduce-dtype", "bf16", "--grad-accum", "2"], ["--no-overlap"],
+                                   ["--shard-optimizer"]])
 def test_bench_two_ranks_cpu(extra):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(_port()), os.path.join(ROOT, "bench.py"),
@@ -39,3 +40,16 @@ def test_bench_two_ranks_cpu(extra):
     assert out["config"]["final_loss"] == out["config"]["final_loss"]  # not NaN
     if "--grad-accum" in extra:
         assert out["config"]["grad_accum"] == 2
+    # self-calibration of the first multi-GPU run: one timed collective per distinct bucket size of
+    # the real plan (what tools/dp_exposure_model.py --sweep reads) and the traced step's bucket
+    # readiness times
+    sweep = out["collective_sweep"]
+    esz = 2 if "bf16" in extra else 4
+    plan = {sp["bytes"] for sp in out["dp_ready_spans"] if not sp["partial"]}
+    assert len(sweep) == len(plan)  # one row per distinct bucket size (rounded to world elements)
+    assert all(min(abs(r["bytes"] - b) for b in plan) < 2 * esz for r in sweep)
+    key = "reduce_scatter_busbw_GBs" if "--shard-optimizer" in extra else "allreduce_busbw_GBs"
+    assert sweep and all(r[key] > 0 and r["world"] == 2 and r["bytes"] % esz == 0 for r in sweep)
+    spans = out["dp_ready_spans"]
+    assert spans and all(0 <= sp["ready_ms"] <= out["dp_traced_step_ms"] for sp in spans)
+    assert out["reducer"]["mode"] == ("zero1-reduce-scatter" if "--shard-optimizer" in extra else "all-reduce")

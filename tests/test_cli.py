@@ -63,3 +63,28 @@ def test_defaults_match_reference():
     f = finetune_parser().parse_args([])
     assert (f.train_batch_size, f.valid_batch_size, f.posemb, f.criterion, f.label_smoothing) == \
         (2048, 256, "learnable", "ce", 0.1)
+
+
+def test_device_augment_auto_needs_the_extension(monkeypatch):
+    """--device-augment auto falls back to the PIL path when the HIP extension is not built (a
+    JMAE_ALLOW_TORCH_FALLBACK run); 'on' fails early with a clear message instead of inside the
+    prefetcher."""
+    from types import SimpleNamespace
+
+    import torch
+
+    from jumbo_mae_tpu_amd.ops import _ext
+    from jumbo_mae_tpu_amd.train import common as C
+
+    args = SimpleNamespace(device_augment="auto", train_dataset_shards="x-{0..1}.tar", random_crop="rrc",
+                           auto_augment="none", color_jitter=0.0, random_erasing=0.0)
+    cuda = torch.device("cuda")
+    monkeypatch.setattr(_ext, "available", lambda: False)
+    assert C.use_device_augment(args, cuda) is False
+    args.device_augment = "on"
+    with pytest.raises(SystemExit, match="extension"):
+        C.use_device_augment(args, cuda)
+    monkeypatch.setattr(_ext, "available", lambda: True)
+    assert C.use_device_augment(args, cuda) is True
+    args.device_augment = "auto"
+    assert C.use_device_augment(args, torch.device("cpu")) is False

@@ -575,6 +575,61 @@ def test_layernorm_bwd_fused_residual(ext, T0, view_y, with_scale, B, T, D):
     assert rel(dbi1, dbi2) < 1e-4  # colsums of bf16 values: rounding flips
 
 
+@pytest.mark.parametrize("gamma_kind", ["init", "trained", "zeros_tiny"])
+@pytest.mark.parametrize("fused", [False, True])
+@pytest.mark.parametrize("B,T,D", [(6, 52, 1024), (5, 51, 512), (4, 49, 768)])
+def test_layernorm_bwd_from_h(ext, gamma_kind, fused, B, T, D):
+    """LN backward that rebuilds x-hat from the forward's bf16 output h (hx / beta) against the
+    fp64 LayerNorm autograd: gamma = 1, beta = 0 (init); trained-like gamma / beta with |beta| > |gamma|
+    in a third of the columns (those chunks read x); gamma with exact zeros and 1e-6 entries
+    (read x there).  Same tolerance class as the x path: dx / dgamma / dbeta within 1e-2 relative
+    (bf16-level x-hat), and the x-path result within 1e-2 of it."""
+    torch.manual_seed(0)
+    x = torch.randn(B, T, D, device="cuda") * 2 + 0.5
+    if gamma_kind == "init":
+        g, bt = torch.ones(D, device="cuda"), torch.zeros(D, device="cuda")
+    elif gamma_kind == "trained":
+        g = torch.randn(D, device="cuda") * 0.5 + 1.0
+        bt = torch.randn(D, device="cuda") * 0.5
+        bt[::3] = 2.0 * g[::3].abs() + 0.1  # |beta| > |gamma|: x path for those chunks
+    else:
+        g = torch.rand(D, device="cuda") + 0.5
+        g[5] = 0.0
+        g[100:104] = 1e-6
+        g[-1] = -1e-6
+        bt = torch.randn(D, device="cuda") * 0.1
+    h, mean, rstd = ext.layernorm_fwd(x, g, bt, 1e-6, torch.bfloat16)
+    dy = torch.randn(B * T, D, device="cuda").bfloat16()
+    dres = torch.randn(B, T, D, device="cuda")
+    z = lambda: torch.zeros(D, device="cuda")  # noqa: E731
+    if fused:
+        y = torch.randn(B * T, D, device="cuda").bfloat16()
+        mask = torch.ones(B, device="cuda")
+        dg1, db1, dbi1 = z(), z(), z()
+        dx1, dyr1 = ext.layernorm_bwd(dy, x, mean, rstd, g, dg1, db1, True, dres, None, y, None, mask, None, dbi1, 0,
+                                      None, hx=h, beta=bt)
+        dg2, db2, dbi2 = z(), z(), z()
+        dx2, dyr2 = ext.layernorm_bwd(dy, x, mean, rstd, g, dg2, db2, True, dres, None, y, None, mask, None, dbi2, 0)
+        assert rel(dyr1, dyr2) < 1e-2 and rel(dbi1, dbi2) < 1e-2
+    else:
+        dg1, db1 = z(), z()
+        dx1 = ext.layernorm_bwd(dy, x, mean, rstd, g, dg1, db1, True, dres, hx=h, beta=bt)[0]
+        dg2, db2 = z(), z()
+        dx2 = ext.layernorm_bwd(dy, x, mean, rstd, g, dg2, db2, True, dres)[0]
+    xr = x.double().requires_grad_()
+    gr, br = g.double().requires_grad_(), bt.double().requires_grad_()
+    yr = torch.nn.functional.layer_norm(xr, (D,), gr, br, 1e-6)
+    yr.backward(dy.double().reshape(B, T, D))
+    dxr = xr.grad + dres.double()
+    for ours in (dx1, dx2):
+        assert rel(ours, dxr) < 1e-2
+    assert rel(dg1, gr.grad) < 1e-2 and rel(db1, br.grad) < 1e-5
+    assert rel(dx1, dx2) < 1e-2 and rel(dg1, dg2) < 1e-2
+    if gamma_kind == "zeros_tiny":  # columns with zero / tiny gamma took the exact path: dgamma there
+        cols = [5, 100, 101, 102, 103, D - 1]
+        assert torch.allclose(dg1[cols].double(), gr.grad[cols], rtol=1e-4, atol=1e-3)
+
+
 @pytest.mark.parametrize("kind", ["store", "gelu", "gelu_only", "dgelu"])
 @pytest.mark.parametrize("M,N,K", [(4352, 4096, 1024), (4200, 4096, 512), (25472, 768, 3072)])
 def test_gemm_nt_tail_split(ext, kind, M, N, K):

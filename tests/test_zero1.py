@@ -110,6 +110,55 @@ def test_zero1_matches_replicated(world, kind, clip, overlap, bf16, defer):
             assert d <= (4e-3 if bf16 else 1e-3) * rep["mu"].abs().max().item() + 1e-9, d
 
 
+def _gather_worker(rank, world, port, out):
+    _init(rank, world, port)
+    from jumbo_mae_tpu_amd.models.mae import PretrainModel
+    from jumbo_mae_tpu_amd.optim.flat import FlatOptimizer
+    from jumbo_mae_tpu_amd.optim.schedule import warmup_cosine_decay_schedule
+    from jumbo_mae_tpu_amd.parallel.ddp import GradReducer
+    from jumbo_mae_tpu_amd.train.engine import Trainer
+    vc, dc = _cfgs()
+    g = torch.Generator().manual_seed(0)
+    imgs = torch.randint(0, 256, (4 * world, 3, 32, 32), dtype=torch.uint8, generator=g)
+    res = {}
+    for gdt in ("fp32", "bf16"):
+        torch.manual_seed(100 + rank)
+        m = PretrainModel(vc, dc).to("cpu", torch.bfloat16, seed=0)  # bf16 compute: a separate shadow
+        dist.broadcast(m.store.master, 0)
+        m.store.sync_shadow()
+        opt = FlatOptimizer(m.store, "adamw", warmup_cosine_decay_schedule(1e-6, 1e-2, 1, 10, 1e-5), b2=0.95,
+                            weight_decay=0.05, num_layers=vc.layers)
+        red = GradReducer(m.store, bucket_mb=0.01, shard=True, gather_dtype=gdt)
+        assert red.gather_shadow == (gdt == "bf16")
+        tr = Trainer(m, opt, red, None)
+        for _ in range(3):
+            tr.train_step([(imgs[rank * 4:(rank + 1) * 4],)])
+        shadow = m.store.shadow.clone()  # before any master gather: what the next forward reads
+        stale = not torch.equal(m.store.master.to(torch.bfloat16), shadow)
+        opt.gather_state()  # checkpoint: the sharded master (bf16 mode) and moments made whole
+        res[gdt] = {"shadow": shadow, "master": m.store.master.clone(), "mu": opt.mu.clone(), "stale": stale,
+                    "stats": red.stats()}
+    if rank == 0:
+        torch.save(res, out)
+    dist.destroy_process_group()
+
+
+def test_zero1_bf16_shadow_gather_matches_fp32_gather():
+    """ZeRO-1 all-gathering the bf16 shadow (default) vs the fp32 master + re-cast: the same weights
+    bit for bit (shadow every step; master and moments after the checkpoint gather); with the bf16
+    gather the master of non-owned pieces is stale until that gather."""
+    port = _free_port()
+    with tempfile.TemporaryDirectory() as d:
+        out = os.path.join(d, "r.pt")
+        mp.spawn(_gather_worker, args=(2, port, out), nprocs=2, join=True)
+        r = torch.load(out, weights_only=True)
+    f, b = r["fp32"], r["bf16"]
+    assert f["stats"]["gather_dtype"] == "fp32" and b["stats"]["gather_dtype"] == "bf16"
+    assert torch.equal(b["shadow"], f["shadow"])
+    assert torch.equal(b["master"], f["master"]) and torch.equal(b["mu"], f["mu"])
+    assert b["stale"] and not f["stale"]
+
+
 def test_shard_ranges_tile_and_align():
     from jumbo_mae_tpu_amd.parallel.ddp import shard_ranges
     rs = shard_ranges([(1000, 5000), (5000, 5003), (5003, 9000), (9000, 20000)], 512)

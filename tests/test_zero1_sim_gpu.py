@@ -10,7 +10,8 @@ unsharded update: bit for bit for the elementwise optimizers, to rounding for th
 (LAMB, LARS, global-norm clipping: the chunk partials are summed in another grouping).  Nothing
 outside a rank's pieces may change.  Pieces come from the reducer's own bucket planner
 (``parallel/ddp.py`` plan_buckets + shard_ranges) at a small bucket size, so buckets cut
-segments.  Reference: /root/reference/src/pretraining.py:150 (pmean) + the optax update."""
+segments.  The bf16 shadow assembled from the owners' pieces -- what the default ZeRO-1 all-gather
+(``gather_dtype="bf16"``) puts on every rank -- must equal the replicated step's shadow bit for bit.  Reference: /root/reference/src/pretraining.py:150 (pmean) + the optax update."""
 
 import pytest
 import torch
@@ -136,6 +137,8 @@ def test_sharded_update_union_equals_replicated(world, kind, clip, split):
     assert len(totals) == (int(clip > 0) + int(kind in ("lamb", "lars")))
 
     got_master, got_state = master0.clone(), [v.clone() for v in state0]
+    # what the bf16-shadow all-gather assembles on every rank: each owner's shadow pieces
+    got_shadow = torch.zeros_like(s.shadow)
     for r in range(world):
         _, mr, sh, st, gr = run_rank(r, totals)
         own = torch.zeros(s.total, dtype=torch.bool, device="cuda")
@@ -149,6 +152,7 @@ def test_sharded_update_union_equals_replicated(world, kind, clip, split):
         # the kernel's bf16 shadow of the owned pieces is the cast of the new master
         assert torch.equal(sh[own], mr[own].to(torch.bfloat16))
         got_master[own] = mr[own]
+        got_shadow[own] = sh[own]
         for g, t in zip(got_state, st):
             g[own] = t[own]
     used = torch.zeros(s.total, dtype=torch.bool, device="cuda")
@@ -165,6 +169,8 @@ def test_sharded_update_union_equals_replicated(world, kind, clip, split):
         for g, w in zip(got_state, want_state):
             assert torch.equal(g[used], w[used])
         assert torch.equal(got_master[used].to(torch.bfloat16), want_shadow[used])
+        # ZeRO-1's bf16 gather == the fp32 gather + re-cast == the replicated step, bit for bit
+        assert torch.equal(got_shadow[used], want_shadow[used])
     else:
         delta = (want_master - master0)[used].abs().max().item()
         assert delta > 0

@@ -54,6 +54,8 @@ def apply(P, cfg: str):
             P._deferred["seg"] = v == "1"
         elif k == "DEFER_WGRAD":
             P._deferred["enabled"] = v == "1"
+        elif k == "LN_FROM_H":  # 0: the LN backward reads the fp32 input instead of the bf16 output
+            P._LN_BWD_FROM_H = v == "1"
         else:
             raise ValueError(k)
 
@@ -64,6 +66,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=4)
     ap.add_argument("--steps", type=int, default=6)
     ap.add_argument("--model", default="vit_large_patch16")
+    ap.add_argument("--batch", type=int, default=512, help="pretrain images per step (2048: the headline micro-batch)")
     ap.add_argument("--task", default="pretrain", choices=["pretrain", "finetune"],
                     help="finetune: the bench.py --task finetune step (ViT-B/16, config/ft.sh recipe, 128 images)")
     a = ap.parse_args()
@@ -83,7 +86,7 @@ def main():
                         num_layers=vc.layers)
     tr = Trainer(model, opt, None, RngStreams({"noise": 0, "dropout": 0, "mixup": 0}, 0, dev))
     gen = torch.Generator(device=dev).manual_seed(0)
-    pool = [torch.randint(0, 256, (512, 3, 224, 224), dtype=torch.uint8, device=dev, generator=gen)
+    pool = [torch.randint(0, 256, (a.batch, 3, 224, 224), dtype=torch.uint8, device=dev, generator=gen)
             for _ in range(2)]
     it = 0
 
@@ -92,7 +95,7 @@ def main():
         tr.train_step([(pool[it % 2],)])
         it += 1
 
-    run(a, (step, 512))
+    run(a, (step, a.batch))
 
 
 def finetune_step():

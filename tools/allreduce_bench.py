@@ -33,7 +33,6 @@ import argparse
 import json
 import os
 import sys
-import time
 
 import torch
 import torch.distributed as dist
@@ -46,53 +45,9 @@ VIT_L_GRAD_BYTES = 404_901_632 * 4
 VIT_L_JUMBO_TAIL_BYTES = 75_512_832 * 4
 
 
-def _sync(dev):
-    if dev.type == "cuda":
-        torch.cuda.synchronize(dev)
-
-
-def _time(fn, iters: int, warmup: int, dev) -> float:
-    for _ in range(warmup):
-        fn()
-    _sync(dev)
-    dist.barrier()
-    t0 = time.perf_counter()
-    for _ in range(iters):
-        fn()
-    _sync(dev)
-    dt = (time.perf_counter() - t0) / iters
-    t = torch.tensor([dt], dtype=torch.float64, device=dev if dev.type == "cuda" else "cpu")
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    return float(t.item())
-
-
 def sweep(sizes_mb, dtype: torch.dtype, iters: int, warmup: int, ops, dev) -> list[dict]:
-    n = dist.get_world_size()
-    esz = torch.tensor([], dtype=dtype).element_size()
-    rows = []
-    for mb in sizes_mb:
-        numel = max(n, int(mb * 2**20) // esz // n * n)
-        nbytes = numel * esz
-        buf = torch.ones(numel, dtype=dtype, device=dev)
-        res = {"size_mb": round(nbytes / 2**20, 3), "dtype": str(dtype).replace("torch.", ""), "world": n}
-        if "allreduce" in ops:
-            t = _time(lambda: dist.all_reduce(buf), iters, warmup, dev)
-            res["allreduce_ms"] = t * 1e3
-            res["allreduce_algbw_GBs"] = nbytes / t / 1e9
-            res["allreduce_busbw_GBs"] = nbytes / t / 1e9 * 2 * (n - 1) / n
-        if "reduce_scatter" in ops:
-            out = torch.empty(numel // n, dtype=dtype, device=dev)
-            t = _time(lambda: dist.reduce_scatter_tensor(out, buf), iters, warmup, dev)
-            res["reduce_scatter_ms"] = t * 1e3
-            res["reduce_scatter_busbw_GBs"] = nbytes / t / 1e9 * (n - 1) / n
-        if "all_gather" in ops:
-            part = torch.ones(numel // n, dtype=dtype, device=dev)
-            t = _time(lambda: dist.all_gather_into_tensor(buf, part), iters, warmup, dev)
-            res["all_gather_ms"] = t * 1e3
-            res["all_gather_busbw_GBs"] = nbytes / t / 1e9 * (n - 1) / n
-        rows.append(res)
-        del buf
-    return rows
+    from jumbo_mae_tpu_amd.parallel.collbench import sweep as _sweep
+    return _sweep([mb * 2**20 for mb in sizes_mb], dtype, iters, warmup, ops, dev)
 
 
 def model_exposed(rows: list[dict]) -> dict:

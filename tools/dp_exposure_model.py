@@ -18,8 +18,10 @@ backward-pass timeline and one RCCL stream:
   ``tools/allreduce_bench.py --json`` sweep of the node (interpolated per size);
 * optimizer: AdamW over the flat store (``--adamw-ms`` for the whole model on one GPU, 2.33 ms
   measured) per optimizer group right after that group's reduction -- on 1/N of the bytes with
-  ZeRO-1, whose updated fp32 master is then all-gathered on the same stream before the next
-  forward.
+  ZeRO-1, whose updated weights are then all-gathered on the same stream before the next
+  forward (the bf16 shadow, 2 bytes per parameter; ``zero1-fp32gather`` = the fp32 master).
+  Modes: all-reduce in fp32 / bf16 (``--reduce-dtype``), ZeRO-1 with an fp32 / bf16 reduce-scatter
+  and a bf16 gather, and the round-5 fp32-gather ZeRO-1.  The bf16 staging copies are not priced.
 
 Prints, per bucket size and mode, the number of collectives, the communication time, and the time
 the step waits after its backward (exposed communication + the optimizer tail).
@@ -38,10 +40,23 @@ import sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
+def load_sweep(path):
+    """``collective_sweep`` rows from a tools/allreduce_bench.py --json file, a bench.py JSON line
+    (the multi-GPU run's self-calibration: one row per bucket size of the real plan), or a driver
+    record holding that line under "parsed"."""
+    d = json.load(open(path))
+    for k in ("parsed", "result"):
+        if "collective_sweep" not in d and isinstance(d.get(k), dict):
+            d = d[k]
+    return d["collective_sweep"]
+
+
 def busbw_fn(args):
     if args.sweep:
-        rows = json.load(open(args.sweep))["collective_sweep"]
-        pts = sorted((r["size_mb"] * 2**20, r["allreduce_busbw_GBs"] * 1e9) for r in rows if "allreduce_busbw_GBs" in r)
+        rows = load_sweep(args.sweep)
+        key = next(k for k in ("allreduce_busbw_GBs", "reduce_scatter_busbw_GBs", "all_gather_busbw_GBs")
+                   if any(k in r for r in rows))
+        pts = sorted((r["size_mb"] * 2**20, r[key] * 1e9) for r in rows if key in r)
 
         def bw(b):
             if b <= pts[0][0]:
@@ -89,9 +104,13 @@ def final_times(red, vc, dc, backward_ms, parts):
     return out
 
 
-def simulate(red, segt, world, bw, alpha_ms, adamw_ms, backward_ms, shard, opt_groups=4):
+def simulate(red, segt, world, bw, alpha_ms, adamw_ms, backward_ms, shard, opt_groups=4, rbytes=4, gbytes=2):
+    """``rbytes``: bytes per element of the gradient reduction (4 fp32, 2 with --reduce-dtype bf16);
+    ``gbytes``: of the ZeRO-1 weight all-gather (2: the bf16 shadow, the default; 4: the fp32
+    master, the round-5 path)."""
     n = world
-    total = sum(hi - lo for lo, hi, _ in red.buckets) * 4
+    elems = sum(hi - lo for lo, hi, _ in red.buckets)
+    total = elems * rbytes
     ready = []
     for lo, hi, idxs in red.buckets:
         r = 0.0
@@ -111,9 +130,9 @@ def simulate(red, segt, world, bw, alpha_ms, adamw_ms, backward_ms, shard, opt_g
         if not shard and len(segs) == 1 and segt[idxs[0]][0] == "chunks":
             v = segt[idxs[0]][1]
             for c, tc in enumerate(v):
-                pieces.append((tc, (hi - lo) * 4 / len(v)))
+                pieces.append((tc, (hi - lo) * rbytes / len(v)))
         else:
-            pieces.append((r, (hi - lo) * 4))
+            pieces.append((r, (hi - lo) * rbytes))
     pieces.sort(key=lambda x: x[0])  # issued as they become ready (GradReducer._on_ready / _on_partial)
     fac = (n - 1) / n * (1 if shard else 2)
     t, comm, ends = 0.0, 0.0, []
@@ -133,8 +152,8 @@ def simulate(red, segt, world, bw, alpha_ms, adamw_ms, backward_ms, shard, opt_g
         if not g:
             continue
         comp = max(comp, g[-1]) + upd_ms
-        if shard:  # all-gather of the group's updated fp32 master on the same RCCL stream
-            gb = total / opt_groups
+        if shard:  # all-gather of the group's updated weights (bf16 shadow / fp32 master), same RCCL stream
+            gb = elems * gbytes / opt_groups
             d = alpha_ms + gb * (n - 1) / n / bw(gb) * 1e3
             gather_t = max(gather_t, comp) + d
             comm += d
@@ -175,8 +194,10 @@ def main(argv=None):
     store.total = -(-store.total // q) * q
     bw = busbw_fn(a)
     rows = []
+    variants = [("all-reduce", False, 4, 0), ("all-reduce-bf16", False, 2, 0), ("zero1", True, 4, 2),
+                ("zero1-bf16", True, 2, 2), ("zero1-fp32gather", True, 4, 4)]
     for mb in [float(x) for x in a.bucket_mb.split(",")]:
-        for shard in (False, True):
+        for mode, shard, rb, gbb in variants:
             red = ddp.GradReducer(store, bucket_mb=mb)
             if shard:  # the ZeRO-1 plan (ddp.GradReducer shard=True) without a process group
                 limit = int(mb * 2**20 / 4)
@@ -185,10 +206,11 @@ def main(argv=None):
                 red.buckets = [(lo, hi, [i for i, s in enumerate(red.segs) if s.offset < hi and s.offset + s.numel > lo])
                                for lo, hi in rngs]
             segt = final_times(red, vc, dc, a.backward_ms, ddp.PARTIAL_SUB)
-            r = simulate(red, segt, a.world, bw, a.alpha_us / 1e3, a.adamw_ms, a.backward_ms, shard)
-            r.update({"bucket_mb": mb, "mode": "zero1" if shard else "all-reduce", "buckets": len(red.buckets)})
+            r = simulate(red, segt, a.world, bw, a.alpha_us / 1e3, a.adamw_ms, a.backward_ms, shard,
+                         rbytes=rb, gbytes=gbb)
+            r.update({"bucket_mb": mb, "mode": mode, "buckets": len(red.buckets)})
             rows.append(r)
-            print(f"bucket {mb:6.1f} MB  {r['mode']:10s}  buckets {r['buckets']:3d}  collectives {r['collectives']:3d}  "
+            print(f"bucket {mb:6.1f} MB  {r['mode']:16s}  buckets {r['buckets']:3d}  collectives {r['collectives']:3d}  "
                   f"comm {r['comm_ms']:7.2f} ms  reductions end +{r['reduce_done_after_backward_ms']:.2f} ms  "
                   f"step waits +{r['wait_after_backward_ms']:.2f} ms after the backward")
     best = min(rows, key=lambda r: (r["wait_after_backward_ms"], r["collectives"]))

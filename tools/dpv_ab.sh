@@ -1,4 +1,5 @@
 #!/bin/bash
+# (The DPV variants were removed after this experiment, profiles/r6a_gemm_dma_placement.txt; kept as the recipe.)
 # DMA-issue placement A/B of the 4-phase GEMM main loops (JMAE_NT_DPV / JMAE_TN_DPV variants of
 # csrc/gemm.hip p4_mainloop and csrc/gemm_tn.hip gemm_tn4_kernel) against the baseline tree
 # _abbase/ (tools/ab_tree.sh), alternating processes on one box.  GEMM tests first.
