@@ -11,6 +11,8 @@
 // fused residual's dscale/dbias) are reduced per wave in registers over a grid-stride row loop,
 // then across the block's waves through LDS in a fixed order into one partial row per block, and
 // the partial rows are summed by ln_param_reduce_kernel (no float atomics: bit-reproducible).
+#include <type_traits>
+
 #include "common.h"
 #include "jm_api.h"
 
@@ -179,8 +181,8 @@ __global__ __launch_bounds__(256) void res_ln_fwd_kernel(ResLnIO io, int T, int 
 // like dy.  x-hat is then rebuilt as (h - beta) / gamma from 2 bytes per element instead of
 // re-reading the fp32 residual-stream input (4 bytes) and its (mean, rstd) -- for the columns
 // where that is accurate: |beta| <= |gamma| (x-hat error <= 2^-9 (|x-hat| + |beta / gamma|), i.e.
-// within 2x of bf16's own rounding of x-hat).  Lanes whose 4-column chunk has a column outside
-// that bound read x for that chunk as before.
+// within 2x of bf16's own rounding of x-hat).  With any column outside that bound the launch reads
+// x as before (every block sees the same gamma / beta, so every block takes the same path).
 struct LnBwdIO {
   float* dx;
   long oB, oT;
@@ -287,97 +289,114 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const TI* __restrict__ dy, 
       }
     }
   }
-  if (use_h) __syncthreads();
-  for (int rw = blockIdx.x * 4 + wave; rw * R < rows; rw += gridDim.x * 4) {
-    const int row = rw * R + sub;
-    const bool valid = R == 1 || row < rows;  // R = 2: the second half of an odd tail has no row
-    const int b = row / T, t = row - b * T;
-    const float* xr = x + b * sB + t * sT;
-    const TI* dyr = dy + (long)row * D;
-    const float mu = valid ? mean[row] : 0.f, rs = valid ? rstd[row] : 0.f;
-    const bool rrow = RES && t >= rio.T0;
-    const long yoff = RES ? b * rio.yB + (long)(t - rio.T0) * rio.yT : 0;
-    float xh[VL][4], g[VL][4], yv[VL][4];
-    float rvp[ER ? VL : 1][4];
-    const float* rr = io.dres ? io.dres + b * io.rB + t * io.rT : nullptr;
-    float sg = 0.f, sgx = 0.f;
-    const uint16_t* hr = use_h ? io.hx + (long)row * D : nullptr;
+  // one path per block: h when no column of the row needs x (every block sees the same gamma / beta,
+  // so every block takes the same path); a per-chunk choice serialised each chunk's loads
+  const bool hpath = use_h && !__syncthreads_or(xchunk != 0u);
+  // the row loop, compiled once per path (a runtime branch per chunk serialised the loads)
+  auto row_loop = [&](auto hp) {
+    constexpr bool HP = decltype(hp)::value;
+    for (int rw = blockIdx.x * 4 + wave; rw * R < rows; rw += gridDim.x * 4) {
+      const int row = rw * R + sub;
+      const bool valid = R == 1 || row < rows;  // R = 2: the second half of an odd tail has no row
+      const int b = row / T, t = row - b * T;
+      const float* xr = x + b * sB + t * sT;
+      const TI* dyr = dy + (long)row * D;
+      const float mu = valid ? mean[row] : 0.f, rs = valid ? rstd[row] : 0.f;
+      const bool rrow = RES && t >= rio.T0;
+      const long yoff = RES ? b * rio.yB + (long)(t - rio.T0) * rio.yT : 0;
+      float xh[VL][4], g[VL][4], yv[VL][4];
+      float rvp[ER ? VL : 1][4];
+      const float* rr = io.dres ? io.dres + b * io.rB + t * io.rT : nullptr;
+      float sg = 0.f, sgx = 0.f;
+      // the row's x (or h) first, in one run of loads; then dy / dres with the math below
+      if constexpr (HP) {
+        const uint16_t* hr = io.hx + (long)row * D;
 #pragma unroll
-    for (int i = 0; i < VL; ++i) {
-      const int col = (i * LPR + l) * 4;
-      if (valid && col < D) {
-        float xv[4], dv[4];
-        if (use_h && !((xchunk >> i) & 1u)) {
-          float hv[4], bb[4], ig[4];
-          load4(hr + col, hv);
-          load4(hbi + col, bb);
-          load4(hbi + D + col, ig);
-          // x-hat = (h - beta) / gamma, fed through the same (x - mu) * rs below as x = x-hat
-          // with (mu, rs) = (0, 1): selects below
-#pragma unroll
-          for (int j = 0; j < 4; ++j) xv[j] = (hv[j] - bb[j]) * ig[j];
-        } else {
-          load4(xr + col, xv);
-#pragma unroll
-          for (int j = 0; j < 4; ++j) xv[j] = (xv[j] - mu) * rs;
-        }
-        load4(dyr + col, dv);
-        if constexpr (RES && SC) {
-          if (rrow && rio.scale) load4(rio.y + yoff + col, yv[i]);
-        }
-        if constexpr (ER) {
-          if (rr) load4(rr + col, rvp[i]);
-          else rvp[i][0] = rvp[i][1] = rvp[i][2] = rvp[i][3] = 0.f;
-        }
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          xh[i][j] = xv[j];
-          g[i][j] = dv[j] * gg[i][j];
-          sg += g[i][j];
-          sgx += g[i][j] * xh[i][j];
-          acc_add(acc, 0, i, j, dv[j] * xh[i][j]);
-          acc_add(acc, 1, i, j, dv[j]);
+        for (int i = 0; i < VL; ++i) {
+          const int col = (i * LPR + l) * 4;
+          if (valid && col < D) load4(hr + col, xh[i]);
         }
       } else {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) xh[i][j] = g[i][j] = 0.f;
-      }
-    }
-    sg = row_sum(sg) / D;
-    sgx = row_sum(sgx) / D;
-    float* dxr = io.dx + b * io.oB + t * io.oT;
-    const float m = (RES && rio.mask) ? rio.mask[valid ? b : 0] : 1.f;
-#pragma unroll
-    for (int i = 0; i < VL; ++i) {
-      const int col = (i * LPR + l) * 4;
-      if (valid && col < D) {
-        float o[4], rv[4] = {0.f, 0.f, 0.f, 0.f};
-        if constexpr (ER) {
-#pragma unroll
-          for (int j = 0; j < 4; ++j) rv[j] = rvp[i][j];
-        } else if (rr) {
-          load4(rr + col, rv);
+        for (int i = 0; i < VL; ++i) {
+          const int col = (i * LPR + l) * 4;
+          if (valid && col < D) load4(xr + col, xh[i]);
         }
+      }
 #pragma unroll
-        for (int j = 0; j < 4; ++j) o[j] = rs * (g[i][j] - sg - xh[i][j] * sgx) + rv[j];
-        store4(dxr + col, o);
-        if (RES && rrow) {
-          float d[4], f[4] = {1.f, 1.f, 1.f, 1.f};
-          if (rio.drop.seed) drop_factors<4>(rio.drop, rio.drop.ioff + yoff + col, f);
+      for (int i = 0; i < VL; ++i) {
+        const int col = (i * LPR + l) * 4;
+        if (valid && col < D) {
+          float dv[4];
+          if constexpr (HP) {  // x-hat = (h - beta) / gamma
+            float bb[4], ig[4];
+            load4(hbi + col, bb);
+            load4(hbi + D + col, ig);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) xh[i][j] = (xh[i][j] - bb[j]) * ig[j];
+          } else {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) xh[i][j] = (xh[i][j] - mu) * rs;
+          }
+          load4(dyr + col, dv);
+          if constexpr (RES && SC) {
+            if (rrow && rio.scale) load4(rio.y + yoff + col, yv[i]);
+          }
+          if constexpr (ER) {
+            if (rr) load4(rr + col, rvp[i]);
+            else rvp[i][0] = rvp[i][1] = rvp[i][2] = rvp[i][3] = 0.f;
+          }
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
-            const float md = m * o[j] * f[j];  // f: the dropout of y (d(y_pre) and dscale see it)
-            d[j] = SC ? md * sc[i][j] : md;
-            if constexpr (SC) {
-              if (rio.scale) acc_add(acc, 2, i, j, md * yv[i][j]);
-            }
-            acc_add(acc, 3 % NP, i, j, bf2f(f2bf(d[j])));  // colsum of the bf16 values the GEMMs consume
+            g[i][j] = dv[j] * gg[i][j];
+            sg += g[i][j];
+            sgx += g[i][j] * xh[i][j];
+            acc_add(acc, 0, i, j, dv[j] * xh[i][j]);
+            acc_add(acc, 1, i, j, dv[j]);
           }
-          store4(rio.dy + yoff + col, d);
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) xh[i][j] = g[i][j] = 0.f;
+        }
+      }
+      sg = row_sum(sg) / D;
+      sgx = row_sum(sgx) / D;
+      float* dxr = io.dx + b * io.oB + t * io.oT;
+      const float m = (RES && rio.mask) ? rio.mask[valid ? b : 0] : 1.f;
+#pragma unroll
+      for (int i = 0; i < VL; ++i) {
+        const int col = (i * LPR + l) * 4;
+        if (valid && col < D) {
+          float o[4], rv[4] = {0.f, 0.f, 0.f, 0.f};
+          if constexpr (ER) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) rv[j] = rvp[i][j];
+          } else if (rr) {
+            load4(rr + col, rv);
+          }
+#pragma unroll
+          for (int j = 0; j < 4; ++j) o[j] = rs * (g[i][j] - sg - xh[i][j] * sgx) + rv[j];
+          store4(dxr + col, o);
+          if (RES && rrow) {
+            float d[4], f[4] = {1.f, 1.f, 1.f, 1.f};
+            if (rio.drop.seed) drop_factors<4>(rio.drop, rio.drop.ioff + yoff + col, f);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              const float md = m * o[j] * f[j];  // f: the dropout of y (d(y_pre) and dscale see it)
+              d[j] = SC ? md * sc[i][j] : md;
+              if constexpr (SC) {
+                if (rio.scale) acc_add(acc, 2, i, j, md * yv[i][j]);
+              }
+              acc_add(acc, 3 % NP, i, j, bf2f(f2bf(d[j])));  // colsum of the bf16 values the GEMMs consume
+            }
+            store4(rio.dy + yoff + col, d);
+          }
         }
       }
     }
-  }
+  };
+  if (hpath) row_loop(std::true_type{});
+  else row_loop(std::false_type{});
   if (!partials) return;
   if constexpr (R == 2) {  // both halves hold the same columns: add them (lane l gets lane l + 32's)
 #pragma unroll

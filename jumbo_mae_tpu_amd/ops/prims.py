@@ -586,9 +586,12 @@ def _drop_factor(y: torch.Tensor, drop) -> torch.Tensor:
     return full.as_strided(y.shape, y.stride(), y.storage_offset() - base.storage_offset())
 
 
-# LN backward rebuilds x-hat from the forward's bf16 output h = bf16(gamma x-hat + beta) where
-# |beta| <= |gamma| (2 bytes per element instead of the fp32 input's 4; csrc/layernorm.hip LnBwdIO)
-_LN_BWD_FROM_H = True
+# LN backward rebuilding x-hat from the forward's bf16 output h = bf16(gamma x-hat + beta) when every
+# column has |beta| <= |gamma| (2 bytes per element instead of the fp32 input's 4; csrc/layernorm.hip
+# LnBwdIO).  OFF: measured 8-9 % slower per LN backward and 0.4 % per step despite the 12.5 % fewer
+# bytes -- the pass is bound by its per-row latency chain, not HBM bytes
+# (profiles/r6d_ln_bwd_from_h.txt); kept as a tested switch (ab_bench LN_FROM_H=1).
+_LN_BWD_FROM_H = False
 
 
 def ln_bwd(dy: torch.Tensor, x3: torch.Tensor, mean, rstd, hg: Handle, hb: Handle, dres=None, out=None,
@@ -597,7 +600,7 @@ def ln_bwd(dy: torch.Tensor, x3: torch.Tensor, mean, rstd, hg: Handle, hb: Handl
     dgamma / dbeta.  With ``res`` the residual backward of dx's consumer rides on the same pass
     and (dx, dy_res, bias_done) is returned (the separate pass would re-read dx from HBM).
     ``h``: the forward's bf16 output of this LN (rows like ``dy``); the HIP kernel then reads it
-    instead of ``x3`` for the columns where that is exact to bf16 level."""
+    instead of ``x3`` when every column has |beta| <= |gamma| (x-hat exact to bf16 level)."""
     B, T, D = x3.shape
     dy = dy.contiguous()
     tr = _trainable(hg)

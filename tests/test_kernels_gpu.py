@@ -580,9 +580,9 @@ def test_layernorm_bwd_fused_residual(ext, T0, view_y, with_scale, B, T, D):
 @pytest.mark.parametrize("B,T,D", [(6, 52, 1024), (5, 51, 512), (4, 49, 768)])
 def test_layernorm_bwd_from_h(ext, gamma_kind, fused, B, T, D):
     """LN backward that rebuilds x-hat from the forward's bf16 output h (hx / beta) against the
-    fp64 LayerNorm autograd: gamma = 1, beta = 0 (init); trained-like gamma / beta with |beta| > |gamma|
-    in a third of the columns (those chunks read x); gamma with exact zeros and 1e-6 entries
-    (read x there).  Same tolerance class as the x path: dx / dgamma / dbeta within 1e-2 relative
+    fp64 LayerNorm autograd: gamma = 1, beta = 0 (init: the h path); trained-like gamma / beta with
+    |beta| > |gamma| in a third of the columns, and gamma with exact zeros and 1e-6 entries (the
+    launch falls back to reading x).  Same tolerance class as the x path: dx / dgamma / dbeta within 1e-2 relative
     (bf16-level x-hat), and the x-path result within 1e-2 of it."""
     torch.manual_seed(0)
     x = torch.randn(B, T, D, device="cuda") * 2 + 0.5
