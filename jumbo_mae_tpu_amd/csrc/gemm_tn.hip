@@ -83,6 +83,22 @@ JM_DEVICE bf16x8_t cat44(s16x4_t lo, s16x4_t hi) {
   return __builtin_bit_cast(bf16x8_t, s);
 }
 
+// both transposing reads of one fragment (rows +0 and +4: OFF and OFF + 1024) from (addr ^ X):
+// one v_xor per fragment instead of one per read
+template <int X, int OFF>
+JM_DEVICE bf16x8_t tr8x(uint32_t a) {
+  s16x4_t lo, hi;
+  if constexpr (X == 0) {
+    asm volatile("ds_read_b64_tr_b16 %0, %2 offset:%3\n\tds_read_b64_tr_b16 %1, %2 offset:%4"
+                 : "=&v"(lo), "=v"(hi) : "v"(a), "i"(OFF), "i"(OFF + 1024));
+  } else {
+    uint32_t tmp;
+    asm volatile("v_xor_b32 %2, %4, %3\n\tds_read_b64_tr_b16 %0, %2 offset:%5\n\tds_read_b64_tr_b16 %1, %2 offset:%6"
+                 : "=&v"(lo), "=&v"(hi), "=&v"(tmp) : "v"(a), "i"(X), "i"(OFF), "i"(OFF + 1024));
+  }
+  return cat44(lo, hi);
+}
+
 // chunk XOR (in 16-byte units, even so 32-byte pairs stay together): rows {0-3, 8-11} and
 // {4-7, 12-15} -- the two row sets of one transposing read -- land on 8 distinct 32-byte slots
 JM_DEVICE int tswz(int row) { return ((row & 3) | (((row >> 3) & 1) << 2)) << 1; }
@@ -287,7 +303,8 @@ __global__ __launch_bounds__(NTH, 1) void gemm_tn_kernel(const uint16_t* __restr
 // per lane): two ds_read_b64_tr_b16 each.  16-byte chunks XOR-swizzled by tswz(row) (bits 1-3):
 // the 8 rows of a transposing read's 32-lane half then cover 8 distinct 32-byte bank slots, and
 // the swizzle only permutes a fragment's 4 (A) / 2 (B) column blocks, so each lane keeps one
-// address per block (+ immediates for the k offsets).  Waves 4-7 at static priority 1.
+// address per block (+ immediates for the slot, the k offsets and the second 4 rows: no VALU in the
+// loop).  Waves 4-7 at static priority 1.
 constexpr int SLOT4 = 64 * 128;  // elements per slot
 
 // GRP: the grid covers the tiles of every problem of ``grp`` (same M); each workgroup picks its
@@ -381,27 +398,44 @@ __global__ __launch_bounds__(NTH, 1) void gemm_tn4_kernel(const uint16_t* __rest
   // 4p..4p+3 of the fragment's 16-column block; the block's swizzled chunk differs per lane only
   // through bits 1-2 of the chunk index (A: the 4 blocks mt, B: bit 1 = nt), i.e. address bits 5-6
   // Byte address of block 0 per operand and slot set; block j (A: mt, B: nt) is at
-  // addr ^ (j << 5) (the swizzle only permutes address bits 5-6), the slot within the set, the
-  // k step and the second 4 rows are immediates (<= 58 KB): 4 address VGPRs in all.
+  // addr ^ (j << 5) (the swizzle only permutes address bits 5-6); the slot within the set, the
+  // k step and the second 4 rows are immediates (<= 58 KB).
   const int qrow = 8 * g + (l16 >> 2), pp = l16 & 3;
   const int sw = tswz(qrow);  // == tswz(qrow + 4 + 32 kk): rows differ in bits 2 and 5 only
   const uint32_t lds0 = (uint32_t)(size_t)((const __attribute__((address_space(3))) uint16_t*)smem);
   const uint32_t a_lo = 2 * (qrow * 128 + (((wr * 8 + (pp >> 1)) ^ sw) << 3) + (pp & 1) * 4);
   const uint32_t b_lo = 2 * (qrow * 128 + (((wc * 4 + (pp >> 1)) ^ sw) << 3) + (pp & 1) * 4);
-  const uint32_t a_addr[2] = {lds0 + a_lo, lds0 + 4 * SLOT4 * 2 + a_lo};
-  const uint32_t b_addr[2] = {lds0 + b_lo, lds0 + 4 * SLOT4 * 2 + b_lo};
+  // one address VGPR per (slot set, column block): the blocks' swizzled addresses differ in bits
+  // 5-6 only (addr ^ (j << 5)), precomputed so the fragment reads need no v_xor (12 VGPRs instead
+  // of 4).  The loop's issue slots are the bound: per 16x16x32 MFMA gap (16 cycles, 8 of them the
+  // MFMA's own issue) it already carries 1.5 transposing reads, and the v_xor per read (round 5)
+  // pushed the gap past 16 cycles -- 5-8 % per weight-gradient GEMM (profiles/r6f_tn_xor_free.txt).
+  // (The segmented variant spills two address dwords around its loop for this; PRE = false would
+  // keep one address per set and one v_xor per fragment.)
+  constexpr bool PRE = true;
+  constexpr int NA = PRE ? 4 : 1, NB = PRE ? 2 : 1;
+  uint32_t a_addr[2][NA], b_addr[2][NB];
+#pragma unroll
+  for (int st = 0; st < 2; ++st) {
+#pragma unroll
+    for (int j = 0; j < NA; ++j) a_addr[st][j] = (lds0 + st * 4 * SLOT4 * 2 + a_lo) ^ (uint32_t)(j << 5);
+#pragma unroll
+    for (int j = 0; j < NB; ++j) b_addr[st][j] = (lds0 + st * 4 * SLOT4 * 2 + b_lo) ^ (uint32_t)(j << 5);
+  }
   typedef bf16x8_t AF[4][2];
   typedef bf16x8_t BF[2][2];
   // fragment i of a half: A (mt, kk) = (i % 4, i / 4), B (nt, kk) = (i % 2, i / 2); slot-in-set SL
   auto read_a1 = [&](int t, auto sl, AF& f, auto ic) {
     constexpr int SL = decltype(sl)::value, I = decltype(ic)::value;
     constexpr int OFF = SL * SLOT4 * 2 + (I / 4) * 32 * 256;
-    f[I % 4][I / 4] = cat44(tr4x<(I % 4) << 5, OFF>(a_addr[t & 1]), tr4x<(I % 4) << 5, OFF + 1024>(a_addr[t & 1]));
+    if constexpr (PRE) f[I % 4][I / 4] = tr8x<0, OFF>(a_addr[t & 1][I % 4]);
+    else f[I % 4][I / 4] = tr8x<(I % 4) << 5, OFF>(a_addr[t & 1][0]);
   };
   auto read_b1 = [&](int t, auto sl, BF& f, auto ic) {
     constexpr int SL = decltype(sl)::value, I = decltype(ic)::value;
     constexpr int OFF = SL * SLOT4 * 2 + (I / 2) * 32 * 256;
-    f[I % 2][I / 2] = cat44(tr4x<(I % 2) << 5, OFF>(b_addr[t & 1]), tr4x<(I % 2) << 5, OFF + 1024>(b_addr[t & 1]));
+    if constexpr (PRE) f[I % 2][I / 2] = tr8x<0, OFF>(b_addr[t & 1][I % 2]);
+    else f[I % 2][I / 2] = tr8x<(I % 2) << 5, OFF>(b_addr[t & 1][0]);
   };
   f32x4_t acc[8][4];
 #pragma unroll
