@@ -148,14 +148,19 @@ JM_DEVICE void gelu_n(const float* x, float* g, float* d) {
 // half the bytes of a bf16 copy on both sides of the round trip (ops/prims.py GD_Q / GD_Z mirror).
 constexpr float GD_Q = 195.f;
 constexpr int GD_Z = 34;
-JM_DEVICE uint32_t gd_code(float d) {
-  return (uint32_t)fminf(fmaxf(__builtin_fmaf(d, GD_Q, (float)GD_Z + 0.5f), 0.f), 255.f);
-}
+// v_cvt_pk_u8_f32 rounds to nearest even and saturates to [0, 255] (probed on gfx950:
+// tools/probes/cvt_pk_u8_probe.hip) and writes its byte into a word: one instruction per code
+// instead of the clamp / truncating convert / shift / or sequence -- the FF1 forward epilogue is
+// VALU-issue bound (profiles/r6h_gelu_code_cvt.txt).  Ties round to even (the torch mirror
+// gd_encode rounds them up: codes may differ by one at exact ties).
+JM_DEVICE uint32_t gd_code(float d) { return __builtin_amdgcn_cvt_pk_u8_f32(__builtin_fmaf(d, GD_Q, (float)GD_Z), 0, 0u); }
+template <int B>
+JM_DEVICE uint32_t gd_put(float d, uint32_t w) { return __builtin_amdgcn_cvt_pk_u8_f32(__builtin_fmaf(d, GD_Q, (float)GD_Z), B, w); }
 // 8 derivatives -> 8 codes, 4 per 32-bit word, element 0 in the low byte
 JM_DEVICE uint2 gd_pack8(const float* d) {
   uint2 v;
-  v.x = gd_code(d[0]) | (gd_code(d[1]) << 8) | (gd_code(d[2]) << 16) | (gd_code(d[3]) << 24);
-  v.y = gd_code(d[4]) | (gd_code(d[5]) << 8) | (gd_code(d[6]) << 16) | (gd_code(d[7]) << 24);
+  v.x = gd_put<3>(d[3], gd_put<2>(d[2], gd_put<1>(d[1], gd_put<0>(d[0], 0u))));
+  v.y = gd_put<3>(d[7], gd_put<2>(d[6], gd_put<1>(d[5], gd_put<0>(d[4], 0u))));
   return v;
 }
 // codes -> (q - GD_Z) * s: v_cvt_f32_ubyte0..3, an exact subtraction, one multiply -- code GD_Z

@@ -122,7 +122,7 @@ JM_DEVICE void epilogue(const f32x4_t (&acc)[8][NTW], const GemmEpi& ep, int M, 
         for (int i = 0; i < 4; ++i) gelu_and_grad_f(bf2f(f2bf(v[i])), gv[i], dv[i]);
         if (ep.dseed) gelu_d_drop<4>(ep, (long)m * ep.ldo + n, gv, dv);
         *reinterpret_cast<uint32_t*>(ep.dq + (long)m * ep.ldo + n) =
-            gd_code(dv[0]) | (gd_code(dv[1]) << 8) | (gd_code(dv[2]) << 16) | (gd_code(dv[3]) << 24);
+            gd_put<3>(dv[3], gd_put<2>(dv[2], gd_put<1>(dv[1], gd_put<0>(dv[0], 0u))));
         store4(ep.out2 + (long)m * ep.ldo + n, gv);
         continue;
       }
@@ -281,12 +281,22 @@ JM_DEVICE void epilogue_lds(const f32x4_t (&acc)[8][NTW], const GemmEpi& ep, uin
           for (int j = 0; j < 8; ++j) hp[j] = bf2f(ah[j]);
           gelu_n<8, false, true>(hp, nullptr, gd);
         }
+        // round the products to bf16 once (one v_cvt_pk_bf16_f32 per pair), then the column sums
+        // read the rounded values back from the packed words (shift / mask) -- the epilogue is
+        // VALU-issue bound, a second conversion per pair for the store cost issue slots
+        uint4 o;
+        uint32_t* ow = reinterpret_cast<uint32_t*>(&o);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          f[j] = bf2f(f2bf(bf2f(dg[j]) * (EPI == EPI_DMUL ? hp[j] : gd[j])));
+        for (int j = 0; j < 8; j += 2) {
+          const float a0 = bf2f(dg[j]) * (EPI == EPI_DMUL ? hp[j] : gd[j]);
+          const float a1 = bf2f(dg[j + 1]) * (EPI == EPI_DMUL ? hp[j + 1] : gd[j + 1]);
+          ow[j / 2] = pack_bf2(a0, a1);
+          f[j] = __uint_as_float(ow[j / 2] << 16);
+          f[j + 1] = __uint_as_float(ow[j / 2] & 0xffff0000u);
           csum[j] += f[j];
+          csum[j + 1] += f[j + 1];
         }
-        st16(ep.out + (long)m * ep.ldo + n0 + c * 8, pack8(f), NTS);
+        st16(ep.out + (long)m * ep.ldo + n0 + c * 8, o, NTS);
       } else if (EPI == EPI_GELU_D) {
         float fh[8], fg[8], fd[8];
         const uint16_t* h = reinterpret_cast<const uint16_t*>(&v);

@@ -245,8 +245,9 @@ GD_Q, GD_Z = 195.0, 34
 
 
 def gd_encode(d: torch.Tensor) -> torch.Tensor:
-    """Torch mirror of the epilogue's gelu' code (tests); the kernel's fma may differ at exact ties."""
-    return torch.clamp(torch.floor(d.float() * GD_Q + (GD_Z + 0.5)), 0, 255).to(torch.uint8)
+    """Torch mirror of the epilogue's gelu' code (tests): round to nearest even and saturate, as
+    v_cvt_pk_u8_f32; the kernel's fma (one rounding) may differ by one code at exact ties."""
+    return torch.clamp(torch.round(d.float() * GD_Q + GD_Z), 0, 255).to(torch.uint8)
 
 
 def gd_decode(q: torch.Tensor, rate: float = 0.0, dtype=torch.bfloat16) -> torch.Tensor:
