@@ -130,7 +130,8 @@ JM_DEVICE bf16x8_t bf16_ones() {
 // Attention-probability dropout (reference modeling.py:133): keep bit of P[b, h, q, k] from
 // common.h drop_keep at index ((b * H + h) * S + k) * SE + q, SE = S rounded up to even, so that
 // queries 2m, 2m + 1 of a key share one hash: the backward's lanes hold 4 consecutive queries of
-// one key (2 hashes per 4 scores), the forward's 4 keys of one query (4 hashes).  ops/dropout.py
+// one key (2 hashes per 4 scores), the forward's 4 keys of one query (2 hashes, the other 2 from
+// the partner query's lane).  ops/dropout.py
 // keep_mask_rows mirrors it.  The row statistics (lse, row sum) are those of the undropped P; the
 // forward scales O by 1 / keep, the backward folds the mask into dP and P^T dO.
 struct AttnDrop {
@@ -139,15 +140,9 @@ struct AttnDrop {
   float scale;          // 1 / keep
 };
 
-// keep bits of keys k0 .. k0 + 3 for one query: pair index jq + k * seh (jq = (b H + h) S seh +
-// q / 2, seh = SE / 2), half q & 1
-JM_DEVICE void keep4(uint64_t seed, uint32_t jq, uint32_t seh, int k0, int qodd, uint32_t thr, bool (&k)[4]) {
-#pragma unroll
-  for (int i = 0; i < 4; ++i) k[i] = drop_keep_half(drop_hash(jq + (uint32_t)(k0 + i) * seh, seed), qodd, thr);
-}
-
-// DROP: P.V uses the masked P (keys of pair s: 32 s + 4 g + i, 32 s + 16 + 4 g + i; keep4
-// arguments jq, seh, qodd); the row sum l stays the undropped one.
+// DROP: P.V uses the masked P (keys of pair s: 32 s + 4 g + i, 32 s + 16 + 4 g + i; hash index
+// jq + key * seh, half qodd); the row sum l stays the undropped one.  Every lane of the wave must be
+// active (the partner-lane DPP exchange).
 template <int NT, int DT, bool DROP = false, class VA>
 JM_DEVICE void softmax_pv(const f32x4_t (&sc)[NT], float sl2, VA&& va, f32x4_t (&oacc)[DT], float& ms, float& l,
                           uint64_t dseed = 0, uint32_t dthr = 0, uint32_t jq = 0, uint32_t seh = 0, int qodd = 0,
@@ -176,9 +171,25 @@ JM_DEVICE void softmax_pv(const f32x4_t (&sc)[NT], float sl2, VA&& va, f32x4_t (
     const bf16x8_t pb = pack8(pf);
     lacc = mfma(ones, pb, lacc);
     if constexpr (DROP) {
+      // queries q and q ^ 1 (lanes l16, l16 ^ 1 of one lane group) share each key's hash (the pair
+      // convention): a lane hashes two of its four keys per tile -- the pair half 2 qodd, 2 qodd + 1
+      // -- and takes the other two from its partner (DPP quad_perm [1,0,3,2], every lane active
+      // here): 4 hashes per 8 scores instead of 8
+      uint32_t hm[4], hp[4];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        hm[u] = drop_hash(jq + (uint32_t)(32 * s + 4 * g + 2 * qodd + u) * seh, dseed);
+        hm[2 + u] = drop_hash(jq + (uint32_t)(32 * s + 16 + 4 * g + 2 * qodd + u) * seh, dseed);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) hp[u] = dpp_mov_u32<0xB1>(hm[u]);
       bool k0[4], k1[4];
-      keep4(dseed, jq, seh, 32 * s + 4 * g, qodd, dthr, k0);
-      keep4(dseed, jq, seh, 32 * s + 16 + 4 * g, qodd, dthr, k1);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const bool own = (i >> 1) == qodd;
+        k0[i] = drop_keep_half(own ? hm[i & 1] : hp[i & 1], qodd, dthr);
+        k1[i] = drop_keep_half(own ? hm[2 + (i & 1)] : hp[2 + (i & 1)], qodd, dthr);
+      }
       float pd[8];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {

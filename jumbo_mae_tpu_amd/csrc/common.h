@@ -178,6 +178,11 @@ JM_DEVICE float dpp_mov(float v) {
   return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF, true));
 }
 
+template <int CTRL>
+JM_DEVICE uint32_t dpp_mov_u32(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xF, 0xF, true);
+}
+
 // sum over the 16 lanes of each DPP row; every lane of the row gets the result.
 // Requires the whole row active.
 JM_DEVICE float row16_sum(float v) {

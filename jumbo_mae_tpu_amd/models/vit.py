@@ -191,6 +191,32 @@ def droppath_masks(layers, batch: int, rng, device, det: bool):
     return out
 
 
+def dropout_seed_pool(layers, rng, device, det: bool, head=None):
+    """Every dropout seed of a layer stack from one draw (one kernel per step instead of one per
+    layer), sliced per layer in _layer_seeds order; None entries for layers without dropout.  The
+    activation-checkpoint recompute gets the same slices.  ``head`` = (x, rate): the stack's input
+    dropout takes the pool's first seed and is applied here (returned as the first element)."""
+    use = [(not det) and 0.0 < getattr(layer, "dropout_rate", 0.0) < 1.0 for layer in layers]
+    hd = head is not None and not det and 0.0 < head[1] < 1.0
+    total = sum(layer.n_seeds for layer, u in zip(layers, use) if u) + int(hd)
+    x = head[0] if head is not None else None
+    if head is not None and not hd:
+        x = _dropout(x, head[1], rng, det)  # rate 0 / det: identity; rate >= 1: zeros
+    if total == 0:
+        return x, [None] * len(layers)
+    pool = Dr.draw_seeds(rng, device, total)
+    if hd:
+        x = Dr.dropout(x, head[1], rng, pool[0])
+    out, i = [], int(hd)
+    for layer, u in zip(layers, use):
+        if u:
+            out.append(pool[i:i + layer.n_seeds])
+            i += layer.n_seeds
+        else:
+            out.append(None)
+    return x, out
+
+
 def _mask(masks, k, rate, batch, rng, device, det):
     """k-th pooled mask of a layer, or a fresh draw when the layer was called without a pool."""
     if masks is not None:
@@ -219,16 +245,21 @@ class JumboLayer:
             self.scale3 = store.handle(store.add(path + ("scale3",), (J,), const_(1e-4), trainable=trainable))
 
     n_droppath = 3  # masks per call, draw order: attention, jumbo, patch FF residual
+    n_seeds = 6  # dropout seeds per call (_layer_seeds order)
 
     @property
     def droppath_rate(self):
         return self.cfg.droppath
 
-    def __call__(self, x, rng=None, det=True, link_in=None, link_out=None, masks=None):
+    @property
+    def dropout_rate(self):
+        return self.cfg.dropout
+
+    def __call__(self, x, rng=None, det=True, link_in=None, link_out=None, masks=None, seeds=None):
         B, S, D = x.shape
         C = self.C
         p = self.cfg.droppath
-        sd = _layer_seeds(self.cfg.dropout, rng, x.device, det, 6)
+        sd = seeds if seeds is not None else _layer_seeds(self.cfg.dropout, rng, x.device, det, 6)
         if use_fused_blocks() and self.cfg.dropout < 1.0:
             m1 = _mask(masks, 0, p, B, rng, x.device, det)
             m3 = _mask(masks, 1, p, B, rng, x.device, det)
@@ -267,15 +298,20 @@ class ViTLayer:
             self.scale2 = store.handle(store.add(path + ("scale2",), (dim,), const_(1e-4), trainable=trainable))
 
     n_droppath = 2  # masks per call, draw order: attention, FF residual
+    n_seeds = 4  # dropout seeds per call (_layer_seeds order)
 
     @property
     def droppath_rate(self):
         return self.droppath
 
-    def __call__(self, x, rng=None, det=True, link_in=None, link_out=None, masks=None):
+    @property
+    def dropout_rate(self):
+        return self.attn.dropout
+
+    def __call__(self, x, rng=None, det=True, link_in=None, link_out=None, masks=None, seeds=None):
         B, S, D = x.shape
         p = self.droppath
-        sd = _layer_seeds(self.attn.dropout, rng, x.device, det, 4)
+        sd = seeds if seeds is not None else _layer_seeds(self.attn.dropout, rng, x.device, det, 4)
         if use_fused_blocks() and self.attn.dropout < 1.0:
             m1 = _mask(masks, 0, p, B, rng, x.device, det)
             m2 = _mask(masks, 1, p, B, rng, x.device, det)
@@ -357,17 +393,18 @@ class JumboViT:
         return self._posemb_cache[key]
 
     def blocks(self, x: torch.Tensor, rng=None, det=True) -> torch.Tensor:
-        x = _dropout(x, self.cfg.dropout, rng, det)
-        return _run_layers(self.layers, x, rng, det, self.cfg.grad_ckpt)
+        return _run_layers(self.layers, x, rng, det, self.cfg.grad_ckpt, in_dropout=self.cfg.dropout)
 
 
-def _run_layers(layers, x, rng, det, grad_ckpt):
+def _run_layers(layers, x, rng, det, grad_ckpt, in_dropout=0.0):
     """The layer loop; consecutive fused blocks are chained by ``blocks.Link`` hand-offs (not
-    under activation checkpointing, whose recompute would re-run forwards out of order)."""
+    under activation checkpointing, whose recompute would re-run forwards out of order).
+    ``in_dropout``: dropout of the stack's input (its seed drawn with the layers' seeds)."""
     masks = droppath_masks(layers, x.shape[0], rng, x.device, det)
+    x, seeds = dropout_seed_pool(layers, rng, x.device, det, head=(x, in_dropout))
     if grad_ckpt and torch.is_grad_enabled():
-        for layer, m in zip(layers, masks):
-            x = _checkpointed(layer, x, rng, det, m)
+        for layer, m, sd in zip(layers, masks, seeds):
+            x = _checkpointed(layer, x, rng, det, m, sd)
         return x
     link = None
     for i, layer in enumerate(layers):
@@ -377,12 +414,12 @@ def _run_layers(layers, x, rng, det, grad_ckpt):
             # the upper block's LN1 rides on this block's last residual pass (forward hand-off)
             ln1 = (up.norm1.g, up.norm1.b) if up is not None and blocks.FWD_LINKS else None
             nxt = blocks.Link(ln1)
-        x = layer(x, rng, det, link_in=link, link_out=nxt, masks=masks[i])
+        x = layer(x, rng, det, link_in=link, link_out=nxt, masks=masks[i], seeds=seeds[i])
         link = nxt
     return x
 
 
-def _checkpointed(layer, x, rng, det, masks=None):
+def _checkpointed(layer, x, rng, det, masks=None, seeds=None):
     """One layer under activation checkpointing (reference ``nn.remat``, modeling.py:232,280).
 
     The recompute in backward must see exactly the forward's random draws: droppath / dropout
@@ -399,13 +436,13 @@ def _checkpointed(layer, x, rng, det, masks=None):
     def run(inp):
         calls[0] += 1
         if calls[0] == 1:
-            return layer(inp, rng, det, masks=masks)
+            return layer(inp, rng, det, masks=masks, seeds=seeds)
         g = None
         if rng is not None:
             g = torch.Generator(device=rng.device)
             g.set_state(state)
         with store.uses_suppressed():
-            return layer(inp, g, det, masks=masks)
+            return layer(inp, g, det, masks=masks, seeds=seeds)
 
     return torch.utils.checkpoint.checkpoint(run, x, use_reentrant=False)
 

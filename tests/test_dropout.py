@@ -63,3 +63,32 @@ def test_rate_edges():
     x = torch.randn(8, 8)
     assert Dr.dropout(x, 0.0, None) is x
     assert torch.count_nonzero(Dr.dropout(x, 1.0, None)) == 0
+
+
+def test_dropout_seed_pool_one_draw_per_stack(monkeypatch):
+    """models/vit.py dropout_seed_pool: the whole stack's seeds (and the input dropout's) come from
+    ONE draw, sliced per layer in call order; layers without dropout get None."""
+    from types import SimpleNamespace
+
+    from jumbo_mae_tpu_amd.models import vit
+
+    calls = []
+    real = Dr.draw_seeds
+
+    def counting(rng, device, n):
+        calls.append(n)
+        return real(rng, device, n)
+
+    monkeypatch.setattr(Dr, "draw_seeds", counting)
+    layers = [SimpleNamespace(dropout_rate=0.1, n_seeds=6), SimpleNamespace(dropout_rate=0.0, n_seeds=6),
+              SimpleNamespace(dropout_rate=0.1, n_seeds=4)]
+    g = torch.Generator().manual_seed(0)
+    x = torch.randn(4, 8)
+    y, seeds = vit.dropout_seed_pool(layers, g, "cpu", False, head=(x, 0.25))
+    assert calls == [11]
+    assert [None if s is None else len(s) for s in seeds] == [6, None, 4]
+    assert len({int(t.item()) for s in seeds if s is not None for t in s}) == 10
+    assert ((y == 0) | torch.isclose(y, x / 0.75)).all()
+    calls.clear()
+    y2, seeds2 = vit.dropout_seed_pool(layers, g, "cpu", True, head=(x, 0.25))  # eval: nothing drawn
+    assert calls == [] and seeds2 == [None] * 3 and y2 is x
