@@ -876,7 +876,9 @@ __global__ __launch_bounds__(64 * NWV, 2) void attn_bwd3_kernel(const uint16_t* 
       const int off = swo<NCH>(r, c);
       *reinterpret_cast<uint4*>(Qs + off) = scale_bf16x8(qv[it], sl2);
       *reinterpret_cast<uint4*>(Ks + off) = kv[it];
-      *reinterpret_cast<uint4*>(dOs + off) = dv[it];
+      // dropout: dO staged times 1 / keep, so dP and P^T dO come out scaled (delta below is taken
+      // from the unscaled dO)
+      *reinterpret_cast<uint4*>(dOs + off) = DROP ? scale_bf16x8(dv[it], drop.scale) : dv[it];
     }
     // delta = O . dO: the NCH chunks of row r sit in NCH consecutive lanes (whole groups in or out
     // of range) -> butterfly sum and one plain store: the same value on every run, no atomics
@@ -982,7 +984,7 @@ __global__ __launch_bounds__(64 * NWV, 2) void attn_bwd3_kernel(const uint16_t* 
               sacc[hh] = ini[hh];
               dlt[hh] = dl[hh];
             }
-            dp[hh] = DROP ? f32x4_t{0.f, 0.f, 0.f, 0.f} : dlt[hh];
+            dp[hh] = dlt[hh];
 #pragma unroll
             for (int kk = 0; kk < KK; ++kk) {
               sacc[hh] = mfma(qf[hh][kk], kf[w][kk], sacc[hh]);
@@ -1003,10 +1005,11 @@ __global__ __launch_bounds__(64 * NWV, 2) void attn_bwd3_kernel(const uint16_t* 
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
               const float p = __builtin_amdgcn_exp2f(sacc[hh][i]);
-              if constexpr (DROP) {  // dS = P (M dP' / keep - delta); P^T dO uses M P (1 / keep at the end)
+              if constexpr (DROP) {  // dS = P (M dP' / keep - delta), dp = dP' / keep - delta (dO
+                                     // staged scaled, -delta init); P^T dO uses M P
                 const bool kp = drop_keep_half(dh[i >> 1], i & 1, drop.thr);
                 pf[4 * hh + i] = kp ? p : 0.f;
-                df[4 * hh + i] = p * ((kp ? dp[hh][i] * drop.scale : 0.f) + dlt[hh][i]);
+                df[4 * hh + i] = p * (kp ? dp[hh][i] : dlt[hh][i]);
               } else {
                 pf[4 * hh + i] = p;
                 df[4 * hh + i] = p * dp[hh][i];
@@ -1096,8 +1099,7 @@ __global__ __launch_bounds__(64 * NWV, 2) void attn_bwd3_kernel(const uint16_t* 
       for (int dt = 0; dt < DT; ++dt) {
         float kv2[4] = {dkacc[w][dt][0] * LN2, dkacc[w][dt][1] * LN2, dkacc[w][dt][2] * LN2,
                         dkacc[w][dt][3] * LN2};
-        const float vs = DROP ? drop.scale : 1.f;
-        float vv[4] = {dvacc[w][dt][0] * vs, dvacc[w][dt][1] * vs, dvacc[w][dt][2] * vs, dvacc[w][dt][3] * vs};
+        float vv[4] = {dvacc[w][dt][0], dvacc[w][dt][1], dvacc[w][dt][2], dvacc[w][dt][3]};  // dO staged scaled
         store4(dKg + (long)key * ts + dt * 16 + 4 * g, kv2);
         store4(dVg + (long)key * ts + dt * 16 + 4 * g, vv);
       }
@@ -1120,7 +1122,7 @@ __global__ __launch_bounds__(64 * NWV, 2) void attn_bwd3_kernel(const uint16_t* 
           float* bw = bsum + wave * 3 * HD;
           const int d = dt * 16 + 4 * g + i;
           bw[HD + d] = sk * LN2;
-          bw[2 * HD + d] = DROP ? sv * drop.scale : sv;
+          bw[2 * HD + d] = sv;
         }
       }
     __syncthreads();
