@@ -945,12 +945,12 @@ __global__ __launch_bounds__(64 * NWV, 2) void attn_bwd3_kernel(const uint16_t* 
         f32x4_t lv[2], dl[2];  // accumulator inits: -lse (log2 domain) and -delta
 #pragma unroll
         for (int hh = 0; hh < 2; ++hh) {
-#pragma unroll
-          for (int kk = 0; kk < KK; ++kk) {
-            qf[hh][kk] = ld8(Qs + (qb + 16 * hh) * HD + o_frag[kk]);
-            dof[hh][kk] = ld8(dOs + (qb + 16 * hh) * HD + o_frag[kk]);
-          }
           if constexpr (!(DROP && NWV == 8)) {
+#pragma unroll
+            for (int kk = 0; kk < KK; ++kk) {
+              qf[hh][kk] = ld8(Qs + (qb + 16 * hh) * HD + o_frag[kk]);
+              dof[hh][kk] = ld8(dOs + (qb + 16 * hh) * HD + o_frag[kk]);
+            }
             const float4 l4 = *reinterpret_cast<const float4*>(lse_s + qb + 16 * hh + 4 * g);
             const float4 d4 = *reinterpret_cast<const float4*>(delta_s + qb + 16 * hh + 4 * g);
             lv[hh] = f32x4_t{l4.x, l4.y, l4.z, l4.w};
@@ -985,6 +985,13 @@ __global__ __launch_bounds__(64 * NWV, 2) void attn_bwd3_kernel(const uint16_t* 
               dlt[hh] = dl[hh];
             }
             dp[hh] = dlt[hh];
+            if constexpr (TILE_AOP) {  // the Q / dO fragments too: nothing per block stays live
+#pragma unroll
+              for (int kk = 0; kk < KK; ++kk) {
+                qf[hh][kk] = ld8(Qs + (qb + 16 * hh) * HD + o_frag[kk]);
+                dof[hh][kk] = ld8(dOs + (qb + 16 * hh) * HD + o_frag[kk]);
+              }
+            }
 #pragma unroll
             for (int kk = 0; kk < KK; ++kk) {
               sacc[hh] = mfma(qf[hh][kk], kf[w][kk], sacc[hh]);

@@ -1,9 +1,9 @@
 #!/bin/bash
-# round 6 (n, same script as m): dropout backward with dO staged scaled and a -delta dP init -- dropout GPU tests, then finetune 128-image
+# round 6 (s, same script as m): 8-wave dropout backward with the Q / dO fragments loaded per key tile (no spills) -- dropout GPU tests, then finetune 128-image
 # step at dropout 0.1 / 0: tree vs _abbase (HEAD), alternating processes
 set -o pipefail
 export TMPDIR=/tmp
-R=${GRAFT_REPO_ROOT:-$(pwd)}; cd $R; O=gpurun_out/r6n; mkdir -p $O
+R=${GRAFT_REPO_ROOT:-$(pwd)}; cd $R; O=gpurun_out/r6s; mkdir -p $O
 timeout -k 10 400 python -u -m pytest tests/test_dropout_gpu.py tests/test_kernels_gpu.py -k "drop or attn" -x -q --timeout 120 --timeout-method thread > $O/pytest.log 2>&1 || { tail -30 $O/pytest.log; exit 1; }
 tail -3 $O/pytest.log
 A="--task finetune --batch-per-gpu 128 --steps 30 --warmup 5"
