@@ -1,6 +1,6 @@
 #!/bin/bash
 # round 6 (o): where the encoder attention backward's time goes -- attn_bwd2_kernel<64,64> at the 2048-image micro-batch;
-# _abc/d5 = no global loads, _abc/d6 = no compute loop (diagnostic trees built from HEAD by a scratch script)
+# _abc/d5 = no global loads, _abc/d6 = no compute loop (tools/r6_diag_trees.sh d5 / d6)
 set -o pipefail
 export TMPDIR=/tmp
 R=${GRAFT_REPO_ROOT:-$(pwd)}; cd $R; O=gpurun_out/r6o; mkdir -p $O

@@ -1,6 +1,6 @@
 #!/bin/bash
 # round 6 (t): is the LayerNorm backward byte-bound?  tools/ln_bench.py paths x (fp32 input) / h (bf16 LN output + affine
-# inverse) from the tree, and path h from _abc/d7 where the bf16 values are used as x-hat directly (no LDS loads, no
+# inverse) from the tree, and path h from _abc/d7 (tools/r6_diag_trees.sh d7) where the bf16 values are used as x-hat directly (no LDS loads, no
 # transform: timing only)
 set -o pipefail
 export TMPDIR=/tmp
