@@ -1,6 +1,6 @@
 #!/bin/bash
 # round 6 (j): decoder attention backward diagnostics (tree = HEAD build, _abc/d1 = bwd3 without its global
-# loads, _abc/d2 = bwd3 without its compute loop; built by a scratch script from HEAD) + device-augment bytes
+# loads, _abc/d2 = bwd3 without its compute loop; tools/r6_diag_trees.sh d1 / d2, then d3 / d4 for the second run) + device-augment bytes
 set -o pipefail
 export TMPDIR=/tmp
 R=${GRAFT_REPO_ROOT:-$(pwd)}; cd $R; O=gpurun_out/r6j2; mkdir -p $O
